@@ -1,0 +1,183 @@
+"""CPU oracle for the CG hot path -- TEST INFRASTRUCTURE ONLY.
+
+Only ``tests/``, ``__graft_entry__.smoke()`` and ``bench.py``'s cpu_baseline leg
+may import this package, and only as the checker (or as the timed CPU
+baseline).  The product (``conjugate_gradient_amd`` / ``libcgx.so`` /
+``cg_hip``) never imports it.
+
+ctypes bindings over ``oracle/liboracle.so`` (built from ``cg_oracle.c`` by
+``oracle/Makefile``), plus a pure-numpy restatement of ``conjgrad.m`` for small
+cases.  What each function restates, with reference file:line citations, is in
+``cg_oracle.h``.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = None
+
+
+class OracleStats(ctypes.Structure):
+    _fields_ = [
+        ("iterations", ctypes.c_int64),
+        ("converged", ctypes.c_int),
+        ("rr", ctypes.c_double),
+        ("t_init_s", ctypes.c_double),
+        ("t_loop_s", ctypes.c_double),
+    ]
+
+
+def build() -> None:
+    """Compile liboracle.so (and _ref/ when the reference is present)."""
+    subprocess.run(["make", "-s", "-C", _HERE], check=True)
+
+
+def lib() -> ctypes.CDLL:
+    global _LIB
+    if _LIB is None:
+        path = os.path.join(_HERE, "liboracle.so")
+        if not os.path.exists(path):
+            build()
+        L = ctypes.CDLL(path)
+        i64, f64, vp = ctypes.c_int64, ctypes.c_double, ctypes.c_void_p
+        L.oracle_mt_res53.argtypes = [ctypes.c_uint32, i64, vp]
+        L.oracle_spd_matlab.argtypes = [i64, ctypes.c_int, vp, vp]
+        L.oracle_spd_matlab.restype = ctypes.c_int
+        L.oracle_spd_hash.argtypes = [i64, i64, i64, ctypes.c_uint64, ctypes.c_int, vp, vp]
+        L.oracle_hash_u01.argtypes = [ctypes.c_uint64, ctypes.c_uint64, ctypes.c_uint64]
+        L.oracle_hash_u01.restype = f64
+        L.oracle_matvec_f32ref.argtypes = [i64, i64, vp, vp, vp]
+        L.oracle_dot_f32ref.argtypes = [i64, vp, vp]
+        L.oracle_dot_f32ref.restype = ctypes.c_float
+        L.oracle_matvec_f64.argtypes = [i64, i64, vp, vp, vp]
+        L.oracle_dot_f64.argtypes = [i64, vp, vp]
+        L.oracle_dot_f64.restype = f64
+        L.oracle_cg_f32ref.argtypes = [i64, vp, vp, vp, i64, f64, ctypes.c_int, ctypes.POINTER(OracleStats)]
+        L.oracle_cg_f32ref.restype = ctypes.c_int
+        L.oracle_cg_f64.argtypes = [i64, vp, vp, vp, i64, f64, ctypes.POINTER(OracleStats)]
+        L.oracle_cg_f64.restype = ctypes.c_int
+        L.oracle_set_threads.argtypes = [ctypes.c_int]
+        _LIB = L
+    return _LIB
+
+
+def _p(a: np.ndarray) -> int:
+    assert a.flags["C_CONTIGUOUS"]
+    return a.ctypes.data
+
+
+def set_threads(n: int) -> None:
+    lib().oracle_set_threads(int(n))
+
+
+def mt_res53(count: int, seed: int = 5489) -> np.ndarray:
+    out = np.empty(count, dtype=np.float64)
+    lib().oracle_mt_res53(seed, count, _p(out))
+    return out
+
+
+def spd_matlab(n: int, dtype=np.float32):
+    """generateSPDmatrix(n) under `rng default`, through its %.4f text format."""
+    dt = np.dtype(dtype)
+    A = np.empty((n, n), dtype=dt)
+    b = np.empty(n, dtype=dt)
+    rc = lib().oracle_spd_matlab(n, 1 if dt == np.float32 else 0, _p(A), _p(b))
+    if rc != 0:
+        raise MemoryError("oracle_spd_matlab")
+    return A, b
+
+
+def spd_hash(n: int, seed: int = 42, dtype=np.float64, row0: int = 0, nrows: int | None = None):
+    """Counter-hash SPD system rows [row0, row0+nrows)."""
+    nrows = n - row0 if nrows is None else nrows
+    dt = np.dtype(dtype)
+    A = np.empty((nrows, n), dtype=dt)
+    b = np.empty(nrows, dtype=dt)
+    lib().oracle_spd_hash(n, row0, nrows, seed, 1 if dt == np.float32 else 0, _p(A), _p(b))
+    return A, b
+
+
+def hash_u01(seed: int, i: int, j: int) -> float:
+    return lib().oracle_hash_u01(seed, i, j)
+
+
+def matvec_f32ref(A: np.ndarray, v: np.ndarray) -> np.ndarray:
+    A = np.ascontiguousarray(A, np.float32)
+    v = np.ascontiguousarray(v, np.float32)
+    out = np.empty(A.shape[0], np.float32)
+    lib().oracle_matvec_f32ref(A.shape[0], A.shape[1], _p(A), _p(v), _p(out))
+    return out
+
+
+def dot_f32ref(a: np.ndarray, b: np.ndarray) -> np.float32:
+    a = np.ascontiguousarray(a, np.float32)
+    b = np.ascontiguousarray(b, np.float32)
+    return np.float32(lib().oracle_dot_f32ref(a.size, _p(a), _p(b)))
+
+
+def matvec_f64(A: np.ndarray, v: np.ndarray) -> np.ndarray:
+    A = np.ascontiguousarray(A, np.float64)
+    v = np.ascontiguousarray(v, np.float64)
+    out = np.empty(A.shape[0], np.float64)
+    lib().oracle_matvec_f64(A.shape[0], A.shape[1], _p(A), _p(v), _p(out))
+    return out
+
+
+def cg_f32ref(A, b, x0, max_iter: int = -1, eps: float = 1e-6, nparts: int = 1):
+    """serialConjugate.c conjugrad restated; returns (x, OracleStats)."""
+    A = np.ascontiguousarray(A, np.float32)
+    b = np.ascontiguousarray(b, np.float32)
+    x = np.array(x0, dtype=np.float32, copy=True)
+    st = OracleStats()
+    rc = lib().oracle_cg_f32ref(b.size, _p(A), _p(b), _p(x), max_iter, eps, nparts, ctypes.byref(st))
+    if rc != 0:
+        raise RuntimeError(f"oracle_cg_f32ref rc={rc}")
+    return x, st
+
+
+def cg_f64(A, b, x0, max_iter: int = -1, eps: float = 1e-10):
+    """conjgrad.m restated in double; returns (x, OracleStats)."""
+    A = np.ascontiguousarray(A, np.float64)
+    b = np.ascontiguousarray(b, np.float64)
+    x = np.array(x0, dtype=np.float64, copy=True)
+    st = OracleStats()
+    rc = lib().oracle_cg_f64(b.size, _p(A), _p(b), _p(x), max_iter, eps, ctypes.byref(st))
+    if rc != 0:
+        raise RuntimeError(f"oracle_cg_f64 rc={rc}")
+    return x, st
+
+
+def conjgrad_numpy(A, b, x, tol: float = 1e-10, max_iter: int | None = None):
+    """conjgrad.m:1-18 line by line in numpy float64 (small cases only).
+    Returns (x, iterations)."""
+    A = np.asarray(A, np.float64)
+    b = np.asarray(b, np.float64)
+    x = np.array(x, np.float64, copy=True)
+    r = b - A @ x                       # conjgrad.m:2
+    p = r.copy()                        # :3
+    rsold = r @ r                       # :4
+    n = b.size if max_iter is None else max_iter
+    it = 0
+    for _ in range(n):                  # :6
+        Ap = A @ p                      # :7
+        alpha = rsold / (p @ Ap)        # :8
+        x = x + alpha * p               # :9
+        r = r - alpha * Ap              # :10
+        rsnew = r @ r                   # :11
+        it += 1
+        if np.sqrt(rsnew) < tol:        # :12-14
+            break
+        p = r + (rsnew / rsold) * p     # :15
+        rsold = rsnew                   # :16
+    return x, it
+
+
+def ref_binary() -> str | None:
+    """Path of the reference build oracle/_ref/serial_ref, if built."""
+    path = os.path.join(_HERE, "_ref", "serial_ref")
+    return path if os.path.exists(path) else None

@@ -1,0 +1,317 @@
+/*
+ * cg_oracle.c -- CPU restatement of the reference CG path (TEST INFRASTRUCTURE).
+ * See cg_oracle.h for what is restated and where it is pinned.
+ *
+ * Build: oracle/Makefile  (gcc -O2 -ffp-contract=off, no fast-math; the
+ * fp32-ref solve must round exactly like serialConjugate.c compiled by gcc on
+ * x86-64, i.e. every multiply and add rounded to float separately).
+ */
+#include "cg_oracle.h"
+
+#include <math.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+#ifdef _OPENMP
+#include <omp.h>
+#endif
+
+static int g_threads = 1;
+void oracle_set_threads(int nthreads) { g_threads = nthreads > 0 ? nthreads : 1; }
+
+static double now_s(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+/* ======================================================================= */
+/* MT19937 (Matsumoto & Nishimura 1998) as used by MATLAB's default stream  */
+/* ======================================================================= */
+typedef struct { uint32_t s[624]; int i; } mt_state;
+
+static void mt_seed(mt_state *m, uint32_t seed) {
+    m->s[0] = seed;
+    for (int k = 1; k < 624; ++k)
+        m->s[k] = 1812433253u * (m->s[k - 1] ^ (m->s[k - 1] >> 30)) + (uint32_t)k;
+    m->i = 624;
+}
+
+static void mt_twist(mt_state *m) {
+    for (int k = 0; k < 624; ++k) {
+        uint32_t y = (m->s[k] & 0x80000000u) | (m->s[(k + 1) % 624] & 0x7fffffffu);
+        uint32_t v = m->s[(k + 397) % 624] ^ (y >> 1);
+        if (y & 1u) v ^= 0x9908b0dfu;
+        m->s[k] = v;
+    }
+    m->i = 0;
+}
+
+static uint32_t mt_u32(mt_state *m) {
+    if (m->i >= 624) mt_twist(m);
+    uint32_t y = m->s[m->i++];
+    y ^= y >> 11;
+    y ^= (y << 7) & 0x9d2c5680u;
+    y ^= (y << 15) & 0xefc60000u;
+    y ^= y >> 18;
+    return y;
+}
+
+/* genrand_res53: 53-bit uniform on [0,1) from two draws (27 + 26 bits). */
+static double mt_res53(mt_state *m) {
+    uint32_t hi = mt_u32(m) >> 5, lo = mt_u32(m) >> 6;
+    return ((double)hi * 67108864.0 + (double)lo) * (1.0 / 9007199254740992.0);
+}
+
+void oracle_mt_res53(uint32_t seed, int64_t count, double *out) {
+    mt_state m;
+    mt_seed(&m, seed);
+    for (int64_t k = 0; k < count; ++k) out[k] = mt_res53(&m);
+}
+
+/* ======================================================================= */
+/* generateSPDmatrix.m restated (generateSPDmatrix.m:4-17, 28-43)          */
+/* ======================================================================= */
+/* One value through fprintf('%.4f\n') and back through the C reader. */
+static float text4_f(double v) {
+    char buf[64];
+    snprintf(buf, sizeof buf, "%.4f", v);
+    return strtof(buf, NULL);
+}
+static double text4_d(double v) {
+    char buf[64];
+    snprintf(buf, sizeof buf, "%.4f", v);
+    return strtod(buf, NULL);
+}
+
+int oracle_spd_matlab(int64_t n, int as_float, void *A, void *b) {
+    /* R = rand(n,n) fills column-major: R(i,j) is draw number j*n + i. */
+    double *R = (double *)malloc((size_t)n * (size_t)n * sizeof(double));
+    if (!R) return -1;
+    mt_state m;
+    mt_seed(&m, 5489u);
+    for (int64_t j = 0; j < n; ++j)
+        for (int64_t i = 0; i < n; ++i) R[(size_t)j * n + i] = mt_res53(&m);
+    /* A = 0.5*(R+R') + n*eye(n).  Symmetric, so the row-major reader sees
+     * the same values as MATLAB's column-major writer. */
+    for (int64_t i = 0; i < n; ++i) {
+        for (int64_t j = 0; j < n; ++j) {
+            double v = 0.5 * (R[(size_t)j * n + i] + R[(size_t)i * n + j]);
+            if (i == j) v = v + (double)n;
+            size_t at = (size_t)i * n + j;
+            if (as_float) ((float *)A)[at] = text4_f(v);
+            else ((double *)A)[at] = text4_d(v);
+        }
+    }
+    /* b = rand(n,1) continues the same stream. */
+    for (int64_t i = 0; i < n; ++i) {
+        double v = mt_res53(&m);
+        if (as_float) ((float *)b)[i] = text4_f(v);
+        else ((double *)b)[i] = text4_d(v);
+    }
+    free(R);
+    return 0;
+}
+
+/* ======================================================================= */
+/* counter-hash synthetic SPD system (SURVEY.md s8(d), N >= 16384)          */
+/* ======================================================================= */
+static uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+
+double oracle_hash_u01(uint64_t seed, uint64_t i, uint64_t j) {
+    uint64_t h = mix64(((i << 32) | (j & 0xffffffffull)) ^ mix64(seed));
+    return (double)(h >> 11) * (1.0 / 9007199254740992.0);
+}
+
+static double hash_b(uint64_t seed, uint64_t i) {
+    uint64_t h = mix64(i ^ mix64(seed + 1));
+    return (double)(h >> 11) * (1.0 / 9007199254740992.0);
+}
+
+void oracle_spd_hash(int64_t n, int64_t row0, int64_t nrows, uint64_t seed,
+                     int as_float, void *A_rows, void *b_rows) {
+    if (A_rows) {
+#pragma omp parallel for schedule(static) num_threads(g_threads)
+        for (int64_t r = 0; r < nrows; ++r) {
+            uint64_t i = (uint64_t)(row0 + r);
+            for (int64_t jj = 0; jj < n; ++jj) {
+                uint64_t j = (uint64_t)jj;
+                double v = 0.5 * (oracle_hash_u01(seed, i, j) + oracle_hash_u01(seed, j, i));
+                if (i == j) v = v + (double)n;
+                size_t at = (size_t)r * (size_t)n + (size_t)jj;
+                if (as_float) ((float *)A_rows)[at] = (float)v;
+                else ((double *)A_rows)[at] = v;
+            }
+        }
+    }
+    if (b_rows) {
+        for (int64_t r = 0; r < nrows; ++r) {
+            double v = hash_b(seed, (uint64_t)(row0 + r));
+            if (as_float) ((float *)b_rows)[r] = (float)v;
+            else ((double *)b_rows)[r] = v;
+        }
+    }
+}
+
+/* ======================================================================= */
+/* fp32 pieces in serialConjugate.c order                                   */
+/* ======================================================================= */
+/* matVec (serialConjugate.c:109-120): out[i] starts at 0 and takes
+ * += A[i][j]*v[j] for j ascending; product and sum each rounded to float. */
+void oracle_matvec_f32ref(int64_t rows, int64_t cols, const float *A,
+                          const float *v, float *out) {
+    for (int64_t i = 0; i < rows; ++i) {
+        const float *row = A + (size_t)i * (size_t)cols;
+        float acc = 0.0f;
+        for (int64_t j = 0; j < cols; ++j) {
+            float prod = row[j] * v[j];
+            acc = acc + prod;
+        }
+        out[i] = acc;
+    }
+}
+
+/* vecVec (serialConjugate.c:145-155). */
+float oracle_dot_f32ref(int64_t n, const float *a, const float *b) {
+    float s = 0.0f;
+    for (int64_t i = 0; i < n; ++i) {
+        float prod = a[i] * b[i];
+        s = s + prod;
+    }
+    return s;
+}
+
+/* Dot product as `nparts` row-block partials, each sequential, then summed in
+ * part order (point-to-point_cg.c allSum :344-357).  nparts == 1 is vecVec. */
+static float dot_parts_f32(int64_t n, const float *a, const float *b, int nparts) {
+    if (nparts <= 1) return oracle_dot_f32ref(n, a, b);
+    int64_t loc = n / nparts;
+    float total = 0.0f;
+    for (int q = 0; q < nparts; ++q) {
+        float part = oracle_dot_f32ref(loc, a + (size_t)q * loc, b + (size_t)q * loc);
+        total = (q == 0) ? part : total + part;
+    }
+    return total;
+}
+
+int oracle_cg_f32ref(int64_t n, const float *A, const float *b, float *x,
+                     int64_t max_iter, double eps, int nparts, oracle_stats *st) {
+    if (nparts < 1) nparts = 1;
+    if (n % nparts != 0) return -2;
+    if (max_iter < 0) max_iter = n;
+    float *Av = (float *)malloc((size_t)n * sizeof(float));
+    float *r = (float *)malloc((size_t)n * sizeof(float));
+    float *p = (float *)malloc((size_t)n * sizeof(float));
+    if (!Av || !r || !p) { free(Av); free(r); free(p); return -1; }
+
+    double t0 = now_s();
+    /* serialConjugate.c:209-212: r0 = p0 = b - A x0, rsold = r0.r0 */
+    oracle_matvec_f32ref(n, n, A, x, Av);
+    for (int64_t i = 0; i < n; ++i) r[i] = b[i] - Av[i];
+    for (int64_t i = 0; i < n; ++i) p[i] = b[i] - Av[i];
+    float rsold = dot_parts_f32(n, r, r, nparts);
+    double t1 = now_s();
+
+    int64_t iters = 0;
+    int converged = 0;
+    float rr = rsold;
+    for (int64_t k = 0; k < max_iter; ++k) {
+        oracle_matvec_f32ref(n, n, A, p, Av);                 /* :215      */
+        float pAp = dot_parts_f32(n, p, Av, nparts);          /* :219      */
+        float alpha = rsold / pAp;                            /* :220      */
+        for (int64_t i = 0; i < n; ++i) {                     /* :221,225  */
+            float t = p[i] * alpha;
+            x[i] = x[i] + t;
+        }
+        for (int64_t i = 0; i < n; ++i) {                     /* :226,230  */
+            float t = Av[i] * alpha;
+            r[i] = r[i] - t;
+        }
+        rr = dot_parts_f32(n, r, r, nparts);                  /* :234      */
+        iters = k + 1;
+        if (eps >= 0.0 && sqrt((double)rr) < eps) {           /* :235-238  */
+            converged = 1;
+            break;
+        }
+        float ratio = rr / rsold;                             /* :239      */
+        for (int64_t i = 0; i < n; ++i) {                     /* :239,243  */
+            float t = p[i] * ratio;
+            p[i] = r[i] + t;
+        }
+        rsold = rr;                                           /* :244      */
+    }
+    double t2 = now_s();
+    if (st) {
+        st->iterations = iters;
+        st->converged = converged;
+        st->rr = (double)rr;
+        st->t_init_s = t1 - t0;
+        st->t_loop_s = t2 - t1;
+    }
+    free(Av); free(r); free(p);
+    return 0;
+}
+
+/* ======================================================================= */
+/* fp64 (conjgrad.m)                                                        */
+/* ======================================================================= */
+void oracle_matvec_f64(int64_t rows, int64_t cols, const double *A,
+                       const double *v, double *out) {
+#pragma omp parallel for schedule(static) num_threads(g_threads)
+    for (int64_t i = 0; i < rows; ++i) {
+        const double *row = A + (size_t)i * (size_t)cols;
+        double acc = 0.0;
+        for (int64_t j = 0; j < cols; ++j) acc = acc + row[j] * v[j];
+        out[i] = acc;
+    }
+}
+
+double oracle_dot_f64(int64_t n, const double *a, const double *b) {
+    double s = 0.0;
+    for (int64_t i = 0; i < n; ++i) s = s + a[i] * b[i];
+    return s;
+}
+
+int oracle_cg_f64(int64_t n, const double *A, const double *b, double *x,
+                  int64_t max_iter, double eps, oracle_stats *st) {
+    if (max_iter < 0) max_iter = n;
+    double *Av = (double *)malloc((size_t)n * sizeof(double));
+    double *r = (double *)malloc((size_t)n * sizeof(double));
+    double *p = (double *)malloc((size_t)n * sizeof(double));
+    if (!Av || !r || !p) { free(Av); free(r); free(p); return -1; }
+    double t0 = now_s();
+    oracle_matvec_f64(n, n, A, x, Av);                 /* conjgrad.m:2  r=b-A*x */
+    for (int64_t i = 0; i < n; ++i) { r[i] = b[i] - Av[i]; p[i] = r[i]; } /* :3 */
+    double rsold = oracle_dot_f64(n, r, r);            /* :4 */
+    double t1 = now_s();
+    int64_t iters = 0;
+    int converged = 0;
+    double rr = rsold;
+    for (int64_t k = 0; k < max_iter; ++k) {           /* :6 for i=1:length(b) */
+        oracle_matvec_f64(n, n, A, p, Av);             /* :7 */
+        double alpha = rsold / oracle_dot_f64(n, p, Av); /* :8 */
+        for (int64_t i = 0; i < n; ++i) x[i] = x[i] + alpha * p[i];  /* :9  */
+        for (int64_t i = 0; i < n; ++i) r[i] = r[i] - alpha * Av[i]; /* :10 */
+        rr = oracle_dot_f64(n, r, r);                  /* :11 */
+        iters = k + 1;
+        if (eps >= 0.0 && sqrt(rr) < eps) { converged = 1; break; } /* :12-14 */
+        double beta = rr / rsold;
+        for (int64_t i = 0; i < n; ++i) p[i] = r[i] + beta * p[i]; /* :15 */
+        rsold = rr;                                    /* :16 */
+    }
+    double t2 = now_s();
+    if (st) {
+        st->iterations = iters;
+        st->converged = converged;
+        st->rr = rr;
+        st->t_init_s = t1 - t0;
+        st->t_loop_s = t2 - t1;
+    }
+    free(Av); free(r); free(p);
+    return 0;
+}
