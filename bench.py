@@ -1,0 +1,250 @@
+#!/usr/bin/env python3
+"""bench.py -- CG iterations/s and matVec HBM GB/s on MI355X (BASELINE.json metric).
+
+  python bench.py [--gpus N] [--steps K] [--warmup W] [--n 65536] [--no-cpu]
+  python -m torch.distributed.run --nnodes=1 --nproc-per-node N \
+      --master-addr 127.0.0.1 --master-port P bench.py --gpus N --steps K --warmup W
+
+A "step" is one CG iteration (serialConjugate.c:213-245 / parallel_cg.c:288-324):
+allgather p, A.p matVec with the fused p.Ap dot, allreduce, x/r update with the
+r.r dot, allreduce, p update.  The workload is configs[2] of BASELINE.json:
+N = 65536 dense SPD fp64 (generateSPDmatrix.m-style, generated on device),
+row-block partitioned over the N GPUs -- the 1-GPU point fits one GPU's HBM
+(34.4 GB), so the 1/2/4/8 series is strong scaling of one fixed system.
+Iterations run in fixed-count mode (no early stop) so every step does the full
+work; the true residual ||b - A x|| / ||b|| is checked after the timed region.
+
+Under torchrun each process drives one GPU (cgx_create_rank): RCCL carries the
+per-iteration exchange inside libcgx; torch.distributed (gloo, CPU) is only the
+control plane (RCCL id broadcast, barriers, max-over-ranks of the timings).
+Run without torchrun, the N=1 case uses a single-GPU context and no torch.
+
+Output: ONE JSON line on rank 0 (see the keys below).  `roofline.achieved`
+is ALGORITHMIC matVec bytes per launch (8*N_loc*N + 8*N + 8*N_loc, SURVEY.md
+s8(d)) / the average matVec kernel duration measured with HIP events on the
+stream the kernel runs on, over the timed region.  `roofline.traffic` is the
+HBM bytes per launch from rocprofv3 PMC counters (profiles/pmc_summary.json,
+FETCH_SIZE doubled per the gfx950 correction) when a summary for this
+workload exists, else null.  `cpu_baseline` times the oracle's fp32-ref
+restatement of serialConjugate.c (bit-identical to it, tests/test_oracle.py)
+on one host core, on a bounded sample: one iteration of the same system.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import platform
+import sys
+import time
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
+
+METRIC = "CG iterations/sec + matVec HBM GB/s, N×N dense SPD fp64, 1/2/4/8 MI355X"
+HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, Chip-level parameters)
+SEED = 42
+
+
+# ----------------------------------------------------------------------------
+# control plane (torch.distributed gloo) -- also exercised by tests/test_dist.py
+# ----------------------------------------------------------------------------
+def launched_by_torchrun() -> bool:
+    return "TORCHELASTIC_RUN_ID" in os.environ or "LOCAL_RANK" in os.environ
+
+
+def dist_env() -> tuple[int, int, int]:
+    return (int(os.environ.get("RANK", 0)), int(os.environ.get("LOCAL_RANK", 0)),
+            int(os.environ.get("WORLD_SIZE", 1)))
+
+
+def dist_init():
+    import torch.distributed as dist
+    if not dist.is_initialized():
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo")
+    return dist
+
+
+def bcast_bytes(dist, payload: bytes | None, src: int = 0) -> bytes:
+    obj = [payload]
+    dist.broadcast_object_list(obj, src=src)
+    return obj[0]
+
+
+def max_over_ranks(dist, value: float) -> float:
+    import torch
+    t = torch.tensor([value], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    return float(t.item())
+
+
+def sum_over_ranks(dist, value: float) -> float:
+    import torch
+    t = torch.tensor([value], dtype=torch.float64)
+    dist.all_reduce(t, op=dist.ReduceOp.SUM)
+    return float(t.item())
+
+
+# ----------------------------------------------------------------------------
+def matvec_bytes(n: int, nloc: int) -> int:
+    """Algorithmic bytes of one matVec launch on one GPU."""
+    return 8 * nloc * n + 8 * n + 8 * nloc
+
+
+def pmc_traffic(n: int, nranks: int) -> float | None:
+    path = os.path.join(ROOT, "profiles", "pmc_summary.json")
+    try:
+        with open(path) as f:
+            s = json.load(f)
+        key = f"n{n}_g{nranks}"
+        return float(s[key]["hbm_bytes_per_matvec"]) if key in s else None
+    except (OSError, ValueError, KeyError):
+        return None
+
+
+def cpu_baseline(n: int, threads_gen: int = 16) -> dict:
+    """Oracle fp32-ref restatement of serialConjugate.c, 1 host core, 1 iteration."""
+    import numpy as np
+
+    import oracle
+    oracle.set_threads(threads_gen)  # generation only; the timed solve is single-threaded
+    A, b = oracle.spd_hash(n, seed=SEED, dtype=np.float32)
+    _, st = oracle.cg_f32ref(A, b, np.zeros(n, np.float32), max_iter=1, eps=-1.0)
+    del A
+    cpu = platform.processor() or platform.machine()
+    try:
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                if line.startswith("model name"):
+                    cpu = line.split(":", 1)[1].strip()
+                    break
+    except OSError:
+        pass
+    return {
+        "value": 1.0 / st.t_loop_s,
+        "unit": "iterations/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": (f"1 CG iteration (matVec + 2 dots + 3 vector updates) of the same N={n} system in fp32, "
+                   f"oracle/cg_oracle.c restatement of serialConjugate.c (bit-identical to it), single thread; "
+                   f"initial residual matVec excluded; loop {st.t_loop_s:.2f} s, init {st.t_init_s:.2f} s; "
+                   f"host CPU: {cpu}, {os.cpu_count()} logical CPUs visible"),
+        "matvec_gbps_est": 4.0 * n * n / st.t_loop_s / 1e9,
+    }
+
+
+def main(argv=None) -> int:
+    ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=20)
+    ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--n", type=int, default=65536)
+    ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
+    ap.add_argument("--cpu-n", type=int, default=None, help="N for the CPU baseline (default: --n)")
+    args = ap.parse_args(argv)
+
+    rank, local_rank, world = dist_env()
+    use_dist = launched_by_torchrun()
+    dist = dist_init() if use_dist else None
+    if use_dist and world != args.gpus and rank == 0:
+        print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
+
+    import conjugate_gradient_amd as cg
+    n = args.n
+    if n % world:
+        raise SystemExit(f"{n} is not divisible by {world}")
+    flags = cg.CGX_F64 | cg.CGX_TIMING
+    if use_dist:
+        uid = bcast_bytes(dist, cg.get_unique_id() if rank == 0 else None)
+        solver = cg.Solver(n, rank=rank, nranks=world, unique_id=uid, device=local_rank, flags=flags)
+    else:
+        solver = cg.Solver(n, device=0, flags=flags)
+    nloc = solver.info.nrows
+
+    solver.generate_spd(SEED)
+    solver.begin()
+    if args.warmup:
+        solver.iterate(args.warmup, eps=-1.0)
+    solver.synchronize()
+    cg.lib().cgx_dev_synchronize()
+    solver.reset_timing()
+
+    if dist:
+        dist.barrier()
+    t0 = time.perf_counter()
+    done, _ = solver.iterate(args.steps, eps=-1.0)
+    solver.synchronize()
+    cg.lib().cgx_dev_synchronize()
+    t1 = time.perf_counter()
+    if dist:
+        dist.barrier()
+    assert done == args.steps
+    elapsed = t1 - t0
+    st = solver.stats()
+    mv_ms = st.matvec_ms / max(1, st.matvec_count)
+    if dist:
+        elapsed = max_over_ranks(dist, elapsed)
+        mv_ms_max = max_over_ranks(dist, mv_ms)
+    else:
+        mv_ms_max = mv_ms
+
+    # correctness after the timed region (not timed): true residual of x
+    rnorm, bnorm = solver.residual_norm()
+    solver.close()
+
+    if rank != 0:
+        if dist:
+            dist.barrier()
+        return 0
+
+    bytes_launch = matvec_bytes(n, nloc)
+    achieved = bytes_launch / (mv_ms * 1e-3) / 1e9
+    traffic = pmc_traffic(n, world)
+    iters_per_s = args.steps / elapsed
+    out = {
+        "metric": METRIC,
+        "value": iters_per_s,
+        "unit": "iterations/s",
+        "n_gpus": world,
+        "steps": args.steps,
+        "warmup": args.warmup,
+        "ms_per_step": elapsed / args.steps * 1e3,
+        "higher_is_better": True,
+        "scaling": "strong",
+        "vs_baseline": None,
+        "dtype": "f64",
+        "data": f"synthetic: generateSPDmatrix.m-style dense SPD (0.5(R+R')+nI, counter hash, seed {SEED}) "
+                f"generated on device; x0 = 0",
+        "config": {
+            "workload": f"configs[2]: N={n} dense SPD fp64 CG, row-block over {world} GPU(s), fixed-count iterations",
+            "n": n,
+            "rows_per_gpu": nloc,
+            "parallelism": f"rowblock{world}",
+            "exchange": "RCCL allgather(p) + 2x allreduce" if use_dist else "none (single GPU)",
+        },
+        "matvec_gbps": achieved,
+        "matvec_ms": mv_ms,
+        "matvec_ms_max_rank": mv_ms_max,
+        "roofline": {
+            "bound": "hbm",
+            "achieved": achieved,
+            "peak": HBM_PEAK_GBS,
+            "unit": "GB/s",
+            "frac": achieved / HBM_PEAK_GBS,
+            "traffic": traffic,
+            "kernel": "k_matvec_f64",
+            "algorithmic_bytes_per_launch": bytes_launch,
+        },
+        "check": {"relres": rnorm / bnorm},
+    }
+    if world == 1 and not args.no_cpu:
+        out["cpu_baseline"] = cpu_baseline(args.cpu_n or n)
+    print(json.dumps(out), flush=True)
+    if dist:
+        dist.barrier()
+    return 0
+
+
+if __name__ == "__main__":
+    sys.exit(main())

@@ -1,0 +1,407 @@
+"""conjugate_gradient_amd -- MI355X-native conjugate-gradient hot path.
+
+Python mirror of the reference's solver interface over the C ABI of
+``lib/libcgx.so`` (declared in ``include/cgx.h``).  The reference
+(mawunyega/conjugate_gradient) is a set of C programs; the functions a user
+of that code calls are reproduced here with the same names and argument
+meaning so the parity tests read like the reference's own call sites:
+
+=====================  ==============================================  =========================
+reference               where                                           here
+=====================  ==============================================  =========================
+``conjugrad(A,b,x)``    serialConjugate.c:180-259                       :func:`conjugrad`
+``conjugrad(..., P)``   parallel_cg.c:248-345 (row blocks, P ranks)     :func:`conjugrad` (shards)
+``matVec``              serialConjugate.c:109-120                       :func:`matVec`
+``vecVec``              serialConjugate.c:145-155                       :func:`vecVec`
+``residual``            serialConjugate.c:124-131                       :func:`residual`
+``scalarVec+vecAdd``    serialConjugate.c:221-243                       :func:`update_xr`,
+                                                                        :func:`update_p`
+``initialize``          serialConjugate.c:85-105                        :func:`read_text`
+=====================  ==============================================  =========================
+
+Everything runs on the GPU through libcgx.so; there is no CPU fallback.  If
+the library is missing or no GPU is visible the calls raise.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+__all__ = [
+    "CGX_F64", "CGX_F32_REF", "CGX_TIMING", "CgxError", "Stats", "Solver", "lib", "build",
+    "conjugrad", "matVec", "vecVec", "residual", "update_xr", "update_p", "read_text",
+    "count_text", "read_dims", "device_count", "get_unique_id", "DeviceArray",
+]
+
+CGX_F64 = 0x0
+CGX_F32_REF = 0x1
+CGX_TIMING = 0x100
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libcgx.so")
+CLI_PATH = os.path.join(_HERE, "bin", "cg_hip")
+_LIB = None
+
+
+class CgxError(RuntimeError):
+    def __init__(self, code: int, what: str):
+        L = lib()
+        msg = L.cgx_strerror(code).decode()
+        detail = L.cgx_last_error().decode()
+        super().__init__(f"{what}: {msg} ({detail})" if detail else f"{what}: {msg}")
+        self.code = code
+
+
+class Stats(ctypes.Structure):
+    _fields_ = [
+        ("iterations", ctypes.c_int64),
+        ("converged", ctypes.c_int),
+        ("rr", ctypes.c_double),
+        ("solve_ms", ctypes.c_double),
+        ("matvec_ms", ctypes.c_double),
+        ("matvec_count", ctypes.c_int64),
+        ("total_iterations", ctypes.c_int64),
+    ]
+
+
+class Info(ctypes.Structure):
+    _fields_ = [
+        ("n", ctypes.c_int64), ("lda", ctypes.c_int64), ("nranks", ctypes.c_int),
+        ("nshards", ctypes.c_int), ("rank0", ctypes.c_int), ("row0", ctypes.c_int64),
+        ("nrows", ctypes.c_int64), ("flags", ctypes.c_int), ("elem_bytes", ctypes.c_int),
+    ]
+
+
+class UniqueId(ctypes.Structure):
+    _fields_ = [("bytes", ctypes.c_char * 128)]
+
+
+def build() -> None:
+    """Compile libcgx.so and cg_hip for gfx950 (hipcc; works without a GPU)."""
+    subprocess.run(["make", "-s", "-C", os.path.join(_HERE, "csrc")], check=True)
+
+
+def lib() -> ctypes.CDLL:
+    """Load libcgx.so; raises if it has not been built (no fallback)."""
+    global _LIB
+    if _LIB is not None:
+        return _LIB
+    if not os.path.exists(LIB_PATH):
+        raise ImportError(f"{LIB_PATH} missing: run `make -C conjugate_gradient_amd/csrc` "
+                          "(or __graft_entry__.build()); there is no CPU fallback")
+    L = ctypes.CDLL(LIB_PATH)
+    i64, i32, f64, vp, sz = ctypes.c_int64, ctypes.c_int, ctypes.c_double, ctypes.c_void_p, ctypes.c_size_t
+    pctx = ctypes.POINTER(ctypes.c_void_p)
+    sigs = {
+        "cgx_strerror": ([i32], ctypes.c_char_p),
+        "cgx_last_error": ([], ctypes.c_char_p),
+        "cgx_version": ([], i32),
+        "cgx_device_count": ([ctypes.POINTER(i32)], i32),
+        "cgx_create": ([pctx, i64, i32, i32], i32),
+        "cgx_create_multi": ([pctx, i64, i32, ctypes.POINTER(i32), i32], i32),
+        "cgx_get_unique_id": ([ctypes.POINTER(UniqueId)], i32),
+        "cgx_create_rank": ([pctx, i64, i32, i32, ctypes.POINTER(UniqueId), i32, i32], i32),
+        "cgx_destroy": ([vp], i32),
+        "cgx_get_info": ([vp, ctypes.POINTER(Info)], i32),
+        "cgx_set_rows": ([vp, i64, i64, vp, i64, vp, vp], i32),
+        "cgx_set_system": ([vp, vp, vp, vp], i32),
+        "cgx_generate_spd": ([vp, ctypes.c_uint64], i32),
+        "cgx_get_x": ([vp, vp], i32),
+        "cgx_set_x": ([vp, vp], i32),
+        "cgx_solve": ([vp, vp, f64, i64, ctypes.POINTER(Stats)], i32),
+        "cgx_solve_begin": ([vp], i32),
+        "cgx_iterate": ([vp, i64, f64, ctypes.POINTER(i64), ctypes.POINTER(i32)], i32),
+        "cgx_get_stats": ([vp, ctypes.POINTER(Stats)], i32),
+        "cgx_reset_timing": ([vp], i32),
+        "cgx_synchronize": ([vp], i32),
+        "cgx_stream": ([vp], vp),
+        "cgx_residual_norm": ([vp, ctypes.POINTER(f64), ctypes.POINTER(f64)], i32),
+        "cgx_dev_malloc": ([ctypes.POINTER(vp), sz], i32),
+        "cgx_dev_free": ([vp], i32),
+        "cgx_memcpy_h2d": ([vp, vp, sz], i32),
+        "cgx_memcpy_d2h": ([vp, vp, sz], i32),
+        "cgx_dev_synchronize": ([], i32),
+        "cgx_matvec": ([i32, vp, i64, i64, i64, vp, vp, vp], i32),
+        "cgx_dot": ([i32, i64, vp, vp, vp, vp], i32),
+        "cgx_residual": ([i32, i64, vp, vp, vp, vp, vp, vp], i32),
+        "cgx_update_xr": ([i32, i64, vp, vp, vp, vp, vp, vp, vp, vp], i32),
+        "cgx_update_p": ([i32, i64, vp, vp, vp, vp, vp], i32),
+        "cgx_text_count": ([ctypes.c_char_p], i64),
+        "cgx_text_read": ([ctypes.c_char_p, i64, i32, vp, i32], i32),
+        "cgx_text_dims": ([ctypes.c_char_p, ctypes.POINTER(i64)], i32),
+    }
+    for name, (args, res) in sigs.items():
+        fn = getattr(L, name)
+        fn.argtypes = args
+        fn.restype = res
+    _LIB = L
+    return L
+
+
+def _check(rc: int, what: str) -> None:
+    if rc != 0:
+        raise CgxError(rc, what)
+
+
+def _ptr(a: np.ndarray) -> int:
+    if not a.flags["C_CONTIGUOUS"]:
+        raise ValueError("array must be C-contiguous")
+    return a.ctypes.data
+
+
+def _dtype(flags: int) -> np.dtype:
+    return np.dtype(np.float32) if flags & CGX_F32_REF else np.dtype(np.float64)
+
+
+def device_count() -> int:
+    n = ctypes.c_int(0)
+    _check(lib().cgx_device_count(ctypes.byref(n)), "cgx_device_count")
+    return n.value
+
+
+def get_unique_id() -> bytes:
+    """RCCL bootstrap id for cgx_create_rank (call on rank 0, broadcast)."""
+    u = UniqueId()
+    _check(lib().cgx_get_unique_id(ctypes.byref(u)), "cgx_get_unique_id")
+    return ctypes.string_at(ctypes.addressof(u), 128)  # may contain NULs
+
+
+# ----------------------------------------------------------------------------
+# text I/O (initialize(), serialConjugate.c:85-105)
+# ----------------------------------------------------------------------------
+def count_text(path: str) -> int:
+    c = lib().cgx_text_count(path.encode())
+    if c < 0:
+        raise FileNotFoundError(path)
+    return int(c)
+
+
+def read_text(path: str, count: int, dtype=np.float64, threads: int = 4) -> np.ndarray:
+    dt = np.dtype(dtype)
+    out = np.empty(count, dtype=dt)
+    rc = lib().cgx_text_read(path.encode(), count, 1 if dt == np.float32 else 0, _ptr(out), threads)
+    if rc == -1:
+        raise FileNotFoundError(path)
+    if rc == -2:
+        raise ValueError(f"{path}: fewer than {count} numbers")
+    if rc != 0:
+        raise ValueError(f"{path}: malformed number")
+    return out
+
+
+def read_dims(path: str) -> tuple[int, int, int, int]:
+    d = (ctypes.c_int64 * 4)()
+    rc = lib().cgx_text_dims(path.encode(), d)
+    if rc != 0:
+        raise ValueError(f"{path}: cannot read dimensions (rc={rc})")
+    return tuple(int(v) for v in d)
+
+
+# ----------------------------------------------------------------------------
+# device arrays (for the kernel-level entry points)
+# ----------------------------------------------------------------------------
+class DeviceArray:
+    """A device buffer owned by libcgx (hipMalloc), with host copy helpers."""
+
+    def __init__(self, count: int, dtype=np.float64):
+        self.dtype = np.dtype(dtype)
+        self.count = int(count)
+        p = ctypes.c_void_p()
+        _check(lib().cgx_dev_malloc(ctypes.byref(p), max(1, self.count) * self.dtype.itemsize), "cgx_dev_malloc")
+        self.ptr = p.value
+
+    @classmethod
+    def from_host(cls, a: np.ndarray, dtype=None) -> "DeviceArray":
+        a = np.ascontiguousarray(a, dtype=dtype or a.dtype)
+        d = cls(a.size, a.dtype)
+        if a.size:
+            _check(lib().cgx_memcpy_h2d(d.ptr, _ptr(a), a.nbytes), "cgx_memcpy_h2d")
+        return d
+
+    def to_host(self) -> np.ndarray:
+        out = np.empty(self.count, self.dtype)
+        if self.count:
+            _check(lib().cgx_dev_synchronize(), "cgx_dev_synchronize")
+            _check(lib().cgx_memcpy_d2h(_ptr(out), self.ptr, out.nbytes), "cgx_memcpy_d2h")
+        return out
+
+    def free(self) -> None:
+        if self.ptr:
+            lib().cgx_dev_free(self.ptr)
+            self.ptr = None
+
+    def __del__(self):
+        try:
+            self.free()
+        except Exception:
+            pass
+
+
+def _dt_flag(dtype) -> int:
+    return CGX_F32_REF if np.dtype(dtype) == np.float32 else CGX_F64
+
+
+def matVec(A: DeviceArray, v: DeviceArray, out: DeviceArray, rows: int, cols: int, lda: int | None = None) -> None:
+    """serialConjugate.c:109-120 / parallel_cg.c:172-184 (rows = local_row)."""
+    _check(lib().cgx_matvec(_dt_flag(A.dtype), A.ptr, lda or cols, rows, cols, v.ptr, out.ptr, None), "cgx_matvec")
+
+
+def vecVec(a: DeviceArray, b: DeviceArray, out: DeviceArray, n: int | None = None) -> None:
+    """serialConjugate.c:145-155: out[0] = a . b (device scalar)."""
+    _check(lib().cgx_dot(_dt_flag(a.dtype), n if n is not None else a.count, a.ptr, b.ptr, out.ptr, None), "cgx_dot")
+
+
+def residual(b, Ax, r, p, rr=None, n=None) -> None:
+    """serialConjugate.c:210-212: r = p = b - Ax; rr[0] = r . r."""
+    _check(lib().cgx_residual(_dt_flag(b.dtype), n if n is not None else b.count, b.ptr, Ax.ptr, r.ptr, p.ptr,
+                              rr.ptr if rr is not None else None, None), "cgx_residual")
+
+
+def update_xr(x, r, p, Ap, rsold, pAp, rr, n=None) -> None:
+    """serialConjugate.c:219-234: alpha = rsold/pAp; x += alpha p; r -= alpha Ap; rr = r.r."""
+    _check(lib().cgx_update_xr(_dt_flag(x.dtype), n if n is not None else x.count, x.ptr, r.ptr, p.ptr, Ap.ptr,
+                               rsold.ptr, pAp.ptr, rr.ptr, None), "cgx_update_xr")
+
+
+def update_p(p, r, rr, rsold, n=None) -> None:
+    """serialConjugate.c:239-243: p = r + (rr/rsold) p."""
+    _check(lib().cgx_update_p(_dt_flag(p.dtype), n if n is not None else p.count, p.ptr, r.ptr, rr.ptr, rsold.ptr,
+                              None), "cgx_update_p")
+
+
+# ----------------------------------------------------------------------------
+# the solver
+# ----------------------------------------------------------------------------
+class Solver:
+    """A CG context: one GPU, several row-block shards in this process, or one
+    rank of a one-process-per-GPU job (RCCL)."""
+
+    def __init__(self, n: int, *, flags: int = CGX_F64, device: int = 0, devices=None,
+                 rank: int | None = None, nranks: int | None = None, unique_id: bytes | None = None):
+        L = lib()
+        self.n = int(n)
+        self.flags = flags
+        self.dtype = _dtype(flags)
+        h = ctypes.c_void_p()
+        if rank is not None:
+            u = UniqueId()
+            if unique_id is None or len(unique_id) != 128:
+                raise ValueError("unique_id must be the 128 bytes from get_unique_id()")
+            ctypes.memmove(ctypes.addressof(u), unique_id, 128)
+            rc = L.cgx_create_rank(ctypes.byref(h), self.n, rank, nranks, ctypes.byref(u), device, flags)
+        elif devices is not None:
+            arr = (ctypes.c_int * len(devices))(*devices)
+            rc = L.cgx_create_multi(ctypes.byref(h), self.n, len(devices), arr, flags)
+        else:
+            rc = L.cgx_create(ctypes.byref(h), self.n, device, flags)
+        _check(rc, "cgx_create")
+        self._h = h.value
+
+    # lifetime
+    def close(self) -> None:
+        if getattr(self, "_h", None):
+            lib().cgx_destroy(self._h)
+            self._h = None
+
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *exc):
+        self.close()
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    @property
+    def info(self) -> Info:
+        i = Info()
+        _check(lib().cgx_get_info(self._h, ctypes.byref(i)), "cgx_get_info")
+        return i
+
+    # data
+    def set_system(self, A: np.ndarray, b: np.ndarray, x0: np.ndarray | None = None) -> None:
+        A = np.ascontiguousarray(A, self.dtype)
+        b = np.ascontiguousarray(b, self.dtype)
+        x0 = np.zeros(self.n, self.dtype) if x0 is None else np.ascontiguousarray(x0, self.dtype)
+        assert A.shape == (self.n, self.n) and b.shape == (self.n,) and x0.shape == (self.n,)
+        _check(lib().cgx_set_system(self._h, _ptr(A), _ptr(b), _ptr(x0)), "cgx_set_system")
+
+    def set_rows(self, row0: int, A_rows=None, b_rows=None, x_rows=None) -> None:
+        arrs = [None if a is None else np.ascontiguousarray(a, self.dtype) for a in (A_rows, b_rows, x_rows)]
+        nrows = next(a.shape[0] for a in arrs if a is not None)
+        lda = arrs[0].shape[1] if arrs[0] is not None else self.n
+        _check(lib().cgx_set_rows(self._h, row0, nrows, *(None if a is None else _ptr(a) for a in arrs[:1]), lda,
+                                  *(None if a is None else _ptr(a) for a in arrs[1:])), "cgx_set_rows")
+
+    def generate_spd(self, seed: int = 42) -> None:
+        _check(lib().cgx_generate_spd(self._h, seed), "cgx_generate_spd")
+
+    def get_x(self) -> np.ndarray:
+        x = np.empty(self.n, self.dtype)
+        _check(lib().cgx_get_x(self._h, _ptr(x)), "cgx_get_x")
+        return x
+
+    def set_x(self, x: np.ndarray) -> None:
+        x = np.ascontiguousarray(x, self.dtype)
+        _check(lib().cgx_set_x(self._h, _ptr(x)), "cgx_set_x")
+
+    # solve
+    def solve(self, x0: np.ndarray | None = None, eps: float = 1e-6, max_iter: int = -1) -> tuple[np.ndarray, Stats]:
+        st = Stats()
+        if x0 is not None:
+            x = np.array(x0, dtype=self.dtype, copy=True)
+            _check(lib().cgx_solve(self._h, _ptr(x), eps, max_iter, ctypes.byref(st)), "cgx_solve")
+        else:
+            _check(lib().cgx_solve(self._h, None, eps, max_iter, ctypes.byref(st)), "cgx_solve")
+            x = self.get_x()
+        return x, st
+
+    def begin(self) -> None:
+        _check(lib().cgx_solve_begin(self._h), "cgx_solve_begin")
+
+    def iterate(self, count: int, eps: float = -1.0) -> tuple[int, bool]:
+        done = ctypes.c_int64(0)
+        conv = ctypes.c_int(0)
+        _check(lib().cgx_iterate(self._h, count, eps, ctypes.byref(done), ctypes.byref(conv)), "cgx_iterate")
+        return done.value, bool(conv.value)
+
+    def stats(self) -> Stats:
+        st = Stats()
+        _check(lib().cgx_get_stats(self._h, ctypes.byref(st)), "cgx_get_stats")
+        return st
+
+    def residual_norm(self) -> tuple[float, float]:
+        """(||b - A x||, ||b||) for the current x (ends a solve in progress)."""
+        rn, bn = ctypes.c_double(), ctypes.c_double()
+        _check(lib().cgx_residual_norm(self._h, ctypes.byref(rn), ctypes.byref(bn)), "cgx_residual_norm")
+        return rn.value, bn.value
+
+    def reset_timing(self) -> None:
+        _check(lib().cgx_reset_timing(self._h), "cgx_reset_timing")
+
+    def synchronize(self) -> None:
+        _check(lib().cgx_synchronize(self._h), "cgx_synchronize")
+
+
+def conjugrad(A: np.ndarray, b: np.ndarray, x: np.ndarray, *, eps: float = 1e-6, max_iter: int = -1,
+              flags: int | None = None, shards=None) -> Stats:
+    """serialConjugate.c:180-259 ``conjugrad(A, b, x)``: solves in place (x is
+    x0 on entry, the solution on exit).  ``shards`` = list of device ids gives
+    parallel_cg.c's row-block split with P = len(shards) (parallel_cg.c:248).
+    The dtype of ``x`` picks the arithmetic unless ``flags`` is given:
+    float32 -> CGX_F32_REF (the reference's float results bit for bit),
+    float64 -> CGX_F64."""
+    if flags is None:
+        flags = CGX_F32_REF if x.dtype == np.float32 else CGX_F64
+    n = b.shape[0]
+    with Solver(n, flags=flags, devices=shards) as s:
+        s.set_system(A, b, x)
+        xs, st = s.solve(None, eps=eps, max_iter=max_iter)
+    x[...] = xs
+    return st

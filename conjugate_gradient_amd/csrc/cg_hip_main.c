@@ -1,0 +1,197 @@
+/*
+ * cg_hip -- drop-in for the reference's solver programs, host code in C over
+ * the libcgx C ABI (include/cgx.h).
+ *
+ *   serialConjugate.c  : cg_hip matrixA.txt vectorb.txt initialguess.txt
+ *   parallel_cg.c      : cg_hip --gpus P matrixA.txt vectorb.txt initialguess.txt
+ *
+ * Same positional arguments (serialConjugate.c:48-52, 65-67), same text
+ * formats, same stdout lines:
+ *   "Computing cg of matrix size : <N*N>"             serialConjugate.c:58
+ *   "average clock execution time in seconds: %f"     serialConjugate.c:250
+ *   with --gpus > 1 additionally, as parallel_cg.c:123-126 / :334-335:
+ *   "collective data distribution time in seconds: %f"
+ *   "cg method execution time in seconds: %f"
+ *   "clock execution time in seconds: %f"
+ * Same stopping rule: stop when sqrt(r.r) < EPSILON (1.0e-6,
+ * serialConjugate.c:28, :235), at most N iterations (:213).
+ *
+ * Differences (documented in DESIGN.md s2): N is read at run time (count of
+ * values in vectorb, or --dims dimensions.txt, or --n); errors exit non-zero
+ * (the reference exits 0, serialConjugate.c:51,56); arithmetic is fp64 unless
+ * --fp32-ref, which reproduces serialConjugate.c's float results bit for bit.
+ *
+ * Extra options: --eps E, --max-iter M, --print-x, --stats, --threads T (text
+ * parsing), --spd N [--seed S] (on-device synthetic system instead of files).
+ */
+#define _POSIX_C_SOURCE 200809L
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include "cgx.h"
+#include "cgx_textio.h"
+
+#define EPSILON_DEFAULT 1.0e-6 /* serialConjugate.c:28 */
+
+static double now_s(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+static void usage(const char *prog) {
+    fprintf(stderr,
+            "usage: %s [--gpus P] [--fp32-ref] [--eps E] [--max-iter M] [--dims FILE] [--n N]\n"
+            "          [--threads T] [--print-x] [--stats] matrixA vectorb initialguess\n"
+            "       %s --spd N [--seed S] [--gpus P] [--eps E] [--max-iter M] [--stats]\n",
+            prog, prog);
+}
+
+static int die_cgx(int rc, const char *what) {
+    fprintf(stderr, "%s failed: %s (%s)\n", what, cgx_strerror(rc), cgx_last_error());
+    return 1;
+}
+
+static int read_file(const char *path, int64_t count, int as_float, void *out, int threads) {
+    int rc = cgx_text_read(path, count, as_float, out, threads);
+    if (rc == -1) {
+        printf("Could not open file\n"); /* serialConjugate.c:103 */
+        fprintf(stderr, "%s: cannot open\n", path);
+    } else if (rc == -2) {
+        fprintf(stderr, "%s: fewer than %lld numbers\n", path, (long long)count);
+    } else if (rc != 0) {
+        fprintf(stderr, "%s: malformed number\n", path);
+    }
+    return rc;
+}
+
+int main(int argc, char **argv) {
+    const double t_prog0 = now_s();
+    int gpus = 1, fp32ref = 0, print_x = 0, stats = 0, threads = 8;
+    double eps = EPSILON_DEFAULT;
+    long long max_iter = -1, n_opt = -1, spd_n = -1;
+    unsigned long long seed = 42;
+    const char *dims_path = NULL;
+    const char *pos[3];
+    int npos = 0;
+
+    for (int i = 1; i < argc; ++i) {
+        const char *a = argv[i];
+        int has_val = (i + 1 < argc);
+        if (!strcmp(a, "--gpus") && has_val) gpus = atoi(argv[++i]);
+        else if (!strcmp(a, "--fp32-ref")) fp32ref = 1;
+        else if (!strcmp(a, "--eps") && has_val) eps = strtod(argv[++i], NULL);
+        else if (!strcmp(a, "--max-iter") && has_val) max_iter = strtoll(argv[++i], NULL, 10);
+        else if (!strcmp(a, "--dims") && has_val) dims_path = argv[++i];
+        else if (!strcmp(a, "--n") && has_val) n_opt = strtoll(argv[++i], NULL, 10);
+        else if (!strcmp(a, "--threads") && has_val) threads = atoi(argv[++i]);
+        else if (!strcmp(a, "--spd") && has_val) spd_n = strtoll(argv[++i], NULL, 10);
+        else if (!strcmp(a, "--seed") && has_val) seed = strtoull(argv[++i], NULL, 10);
+        else if (!strcmp(a, "--print-x")) print_x = 1;
+        else if (!strcmp(a, "--stats")) stats = 1;
+        else if (!strcmp(a, "-h") || !strcmp(a, "--help")) { usage(argv[0]); return 0; }
+        else if (a[0] == '-' && a[1] == '-') { usage(argv[0]); return 2; }
+        else if (npos < 3) pos[npos++] = a;
+        else npos = 4;
+    }
+    if (spd_n < 0 && npos != 3) {
+        printf("serialCongugate.c requires four (4) files \n"); /* serialConjugate.c:50 */
+        usage(argv[0]);
+        return 1;
+    }
+    if (gpus < 1) { fprintf(stderr, "--gpus must be >= 1\n"); return 2; }
+
+    /* ---- N ---------------------------------------------------------------- */
+    int64_t n = 0;
+    if (spd_n > 0) n = spd_n;
+    else if (n_opt > 0) n = n_opt;
+    else if (dims_path) {
+        int64_t d[4];
+        if (cgx_text_dims(dims_path, d) != 0) { fprintf(stderr, "%s: cannot read dimensions\n", dims_path); return 1; }
+        if (d[0] != d[1]) { printf("%lld and %lld must be same size\n", (long long)d[0], (long long)d[1]); return 1; }
+        if (d[2] != d[0] || d[3] != 1) { fprintf(stderr, "%s: b must be %lld x 1\n", dims_path, (long long)d[0]); return 1; }
+        n = d[0];
+    } else {
+        n = cgx_text_count(pos[1]);
+        if (n < 0) { printf("Could not open file\n"); fprintf(stderr, "%s: cannot open\n", pos[1]); return 1; }
+    }
+    if (n < 1) { fprintf(stderr, "empty system\n"); return 1; }
+    if (n % gpus != 0) { printf("%lld is not divisible by %d\n", (long long)n, gpus); return 1; } /* parallel_cg.c:88 */
+
+    printf("Computing cg of matrix size : %lld\n", (long long)n * (long long)n); /* serialConjugate.c:58 */
+    fflush(stdout);
+
+    const int flags = fp32ref ? CGX_F32_REF : CGX_F64;
+    const size_t es = fp32ref ? 4 : 8;
+    void *x = malloc((size_t)n * es);
+    void *A = NULL, *b = NULL;
+    if (!x) { fprintf(stderr, "can't allocate memory for vector\n"); return 1; }
+    if (spd_n > 0) {
+        memset(x, 0, (size_t)n * es);
+    } else {
+        /* initialize(A), initialize(b), initialize(x0): serialConjugate.c:65-67 */
+        A = malloc((size_t)n * (size_t)n * es);
+        b = malloc((size_t)n * es);
+        if (!A || !b) { fprintf(stderr, "can't allocate memory for vector\n"); return 1; }
+        if (read_file(pos[0], n * n, fp32ref, A, threads) || read_file(pos[1], n, fp32ref, b, threads) ||
+            read_file(pos[2], n, fp32ref, x, 1))
+            return 1;
+    }
+
+    cgx_ctx *ctx = NULL;
+    int rc;
+    if (gpus == 1) {
+        rc = cgx_create(&ctx, n, 0, flags);
+    } else {
+        int devs[32];
+        if (gpus > 32) { fprintf(stderr, "--gpus must be <= 32\n"); return 2; }
+        int ndev = 0;
+        cgx_device_count(&ndev);
+        for (int g = 0; g < gpus; ++g) devs[g] = ndev > 0 ? g % ndev : 0;
+        rc = cgx_create_multi(&ctx, n, gpus, devs, flags);
+    }
+    if (rc != CGX_OK) return die_cgx(rc, "cgx_create");
+
+    double t_dist0 = now_s(), t_dist1;
+    if (spd_n > 0) {
+        rc = cgx_generate_spd(ctx, seed);
+        t_dist1 = now_s();
+        if (rc != CGX_OK) return die_cgx(rc, "cgx_generate_spd");
+    } else {
+        /* MPI_Bcast(x0) + MPI_Scatter(A, b): parallel_cg.c:109-117 */
+        rc = cgx_set_system(ctx, A, b, x);
+        t_dist1 = now_s();
+        free(A);
+        free(b);
+        if (rc != CGX_OK) return die_cgx(rc, "cgx_set_system");
+    }
+
+    cgx_stats st;
+    rc = cgx_solve(ctx, NULL, eps, max_iter, &st);
+    if (rc != CGX_OK) return die_cgx(rc, "cgx_solve");
+    rc = cgx_get_x(ctx, x);
+    if (rc != CGX_OK) return die_cgx(rc, "cgx_get_x");
+
+    if (gpus > 1) {
+        printf("cg method execution time in seconds: %f\n", st.solve_ms / 1e3);
+        printf("collective data distribution time in seconds: %f\n", t_dist1 - t_dist0);
+        printf("clock execution time in seconds: %f\n", now_s() - t_prog0);
+    } else {
+        printf("average clock execution time in seconds: %f\n", st.solve_ms / 1e3);
+    }
+    if (stats)
+        printf("iterations: %lld converged: %d residual_norm: %.6e\n", (long long)st.iterations, st.converged,
+               st.rr >= 0 ? __builtin_sqrt(st.rr) : -1.0);
+    if (print_x) {
+        for (int64_t i = 0; i < n; ++i) {
+            if (fp32ref) printf("%.9g\n", (double)((float *)x)[i]);
+            else printf("%.17g\n", ((double *)x)[i]);
+        }
+    }
+    free(x);
+    cgx_destroy(ctx);
+    return 0;
+}

@@ -1,0 +1,931 @@
+// cgx_api.hip -- the C ABI of include/cgx.h: contexts, row-block shards,
+// per-iteration exchange, and the conjugrad driver loop.
+//
+// Reference mapping:
+//   conjugrad()              serialConjugate.c:180-259 / parallel_cg.c:248-345
+//       -> cgx_solve = cgx_solve_begin (:209-212) + cgx_iterate (:213-245)
+//   MPI_Bcast x0 / MPI_Scatter A,b   parallel_cg.c:109-117 -> cgx_set_rows
+//   MPI_Allgather(local_p -> p)      parallel_cg.c:290-291 -> exchange_allgather
+//   MPI_Allreduce(p.Ap), (r.r)       parallel_cg.c:287,294,313 -> exchange_scalar
+//
+// A context holds one or more shards.  A shard = one contiguous row block of
+// A (rows [row0, row0+nloc), every column, leading dimension lda = n rounded
+// up to 128 with zero padding), its slices of b, x, r, Ap, a full-length p
+// (padded, zero tail) whose own slice doubles as the local p, and a small
+// device scalar block.  Three exchange modes:
+//   SINGLE  one shard, no exchange.
+//   LOCAL   several shards in this process (distinct or repeated devices);
+//           allgather by device-to-device copies, scalars combined as
+//           partials summed in rank order (point-to-point_cg.c allSum order).
+//   RCCL    one shard per process (torchrun / mpirun style), RCCL allgather
+//           of p and allreduce of the scalars over xGMI on the shard stream.
+//
+// Scalar slots (8 bytes each; F32_REF stores a float at the slot start):
+//   RR(j)   = r_j.r_j (global)      PAP(k) = p_k.Ap_k (global)   ring of 4
+//   LRR(j), LPAP(k): this shard's partials when an exchange follows
+//   GATHER+q: the partial of shard q (ordered combine)
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <new>
+#include <string>
+#include <vector>
+
+#include "cgx.h"
+#include "cgx_kernels.h"
+
+using namespace cgx;
+
+namespace {
+
+thread_local char g_err[1024] = "";
+
+int fail(int code, const char *fmt, ...) {
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(g_err, sizeof g_err, fmt, ap);
+    va_end(ap);
+    return code;
+}
+
+#define HIPT(expr)                                                                              \
+    do {                                                                                        \
+        hipError_t e_ = (expr);                                                                 \
+        if (e_ != hipSuccess)                                                                   \
+            return fail(CGX_ERR_HIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, \
+                        __LINE__);                                                              \
+    } while (0)
+
+#define NCCLT(expr)                                                                               \
+    do {                                                                                          \
+        ncclResult_t e_ = (expr);                                                                 \
+        if (e_ != ncclSuccess)                                                                    \
+            return fail(CGX_ERR_RCCL, "%s: %s (%s:%d)", #expr, ncclGetErrorString(e_), __FILE__, \
+                        __LINE__);                                                                \
+    } while (0)
+
+#define TRY(expr)                          \
+    do {                                   \
+        int rc_ = (expr);                  \
+        if (rc_ != CGX_OK) return rc_;     \
+    } while (0)
+
+constexpr int kScalSlots = 136;  // 16 ring slots, up to 112 gathered partials, 4 aux
+constexpr int kMaxShards = 32;
+constexpr int S_RR = 0, S_PAP = 4, S_LRR = 8, S_LPAP = 12, S_GATHER = 16;
+constexpr int S_TR = 128, S_TB = 129, S_LTR = 130, S_LTB = 131;  // true-residual check
+inline int ring(int64_t j) { return (int)(j & 3); }
+
+enum Mode { M_SINGLE = 0, M_LOCAL = 1, M_RCCL = 2 };
+enum State { ST_IDLE = 0, ST_BEGUN = 1, ST_CONVERGED = 2 };
+
+constexpr int kEvPairs = 256;
+
+struct Shard {
+    int dev = 0;
+    int index = 0;  // global row-block index
+    int64_t row0 = 0, nloc = 0;
+    hipStream_t stream = nullptr;
+    ncclComm_t comm = nullptr;
+    char *A = nullptr, *b = nullptr, *x = nullptr, *r = nullptr, *Ap = nullptr, *pfull = nullptr,
+         *xfull = nullptr, *scal = nullptr;
+    RedWs ws{nullptr, nullptr};
+    double *h_pin = nullptr;
+    MatvecPlan plan;
+    hipEvent_t ev_sync = nullptr;  // cross-shard ordering (LOCAL mode)
+    std::vector<hipEvent_t> ev_t;  // timing pairs (CGX_TIMING)
+    int ev_used = 0;
+};
+
+}  // namespace
+
+struct cgx_ctx {
+    int64_t n = 0, lda = 0;
+    int nranks = 1;
+    int flags = 0;
+    int es = 8;
+    Mode mode = M_SINGLE;
+    std::vector<Shard> sh;
+    State state = ST_IDLE;
+    int64_t k = 0;  // iterations of the current solve
+    double last_rr = 0.0;
+    int converged = 0;
+    double solve_ms = 0.0, matvec_ms = 0.0;
+    int64_t matvec_count = 0, total_iters = 0;
+};
+
+namespace {
+
+inline bool f32ref(const cgx_ctx *c) { return (c->flags & CGX_F32_REF) != 0; }
+inline void *slot(const Shard &s, int i) { return s.scal + 8 * i; }
+
+int set_dev(const Shard &s) {
+    HIPT(hipSetDevice(s.dev));
+    return CGX_OK;
+}
+
+int alloc_shard(cgx_ctx *c, Shard &s) {
+    TRY(set_dev(s));
+    const size_t es = (size_t)c->es;
+    HIPT(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
+    HIPT(hipEventCreateWithFlags(&s.ev_sync, hipEventDisableTiming));
+    const size_t abytes = (size_t)s.nloc * (size_t)c->lda * es;
+    auto dmalloc = [&](char **p, size_t bytes) -> int {
+        if (bytes == 0) bytes = 16;
+        hipError_t e = hipMalloc(p, bytes);
+        if (e != hipSuccess)
+            return fail(CGX_ERR_NOMEM, "hipMalloc(%zu bytes) on device %d: %s", bytes, s.dev,
+                        hipGetErrorString(e));
+        return CGX_OK;
+    };
+    TRY(dmalloc(&s.A, abytes));
+    TRY(dmalloc(&s.b, s.nloc * es));
+    TRY(dmalloc(&s.x, s.nloc * es));
+    TRY(dmalloc(&s.r, s.nloc * es));
+    TRY(dmalloc(&s.Ap, s.nloc * es));
+    TRY(dmalloc(&s.pfull, c->lda * es));
+    TRY(dmalloc(&s.scal, kScalSlots * 8));
+    if (c->mode == M_RCCL && c->nranks > 1) TRY(dmalloc(&s.xfull, c->lda * es));
+    char *part = nullptr, *tick = nullptr;
+    TRY(dmalloc(&part, kMaxRedBlocks * sizeof(double)));
+    TRY(dmalloc(&tick, kTickets * sizeof(unsigned)));
+    s.ws.partials = reinterpret_cast<double *>(part);
+    s.ws.tickets = reinterpret_cast<unsigned *>(tick);
+    HIPT(hipMemsetAsync(s.A, 0, abytes, s.stream));  // zero padding columns
+    HIPT(hipMemsetAsync(s.b, 0, s.nloc * es, s.stream));
+    HIPT(hipMemsetAsync(s.x, 0, s.nloc * es, s.stream));
+    HIPT(hipMemsetAsync(s.r, 0, s.nloc * es, s.stream));
+    HIPT(hipMemsetAsync(s.Ap, 0, s.nloc * es, s.stream));
+    HIPT(hipMemsetAsync(s.pfull, 0, c->lda * es, s.stream));
+    HIPT(hipMemsetAsync(s.scal, 0, kScalSlots * 8, s.stream));
+    HIPT(hipMemsetAsync(s.ws.tickets, 0, kTickets * sizeof(unsigned), s.stream));
+    if (s.xfull) HIPT(hipMemsetAsync(s.xfull, 0, c->lda * es, s.stream));
+    HIPT(hipHostMalloc(reinterpret_cast<void **>(&s.h_pin), 64, hipHostMallocDefault));
+    if (c->flags & CGX_TIMING) {
+        s.ev_t.resize(2 * kEvPairs);
+        for (auto &e : s.ev_t) HIPT(hipEventCreate(&e));
+    }
+    if (!f32ref(c)) s.plan = plan_matvec_f64(s.dev, s.nloc);
+    HIPT(hipStreamSynchronize(s.stream));
+    return CGX_OK;
+}
+
+void free_shard(Shard &s) {
+    (void)hipSetDevice(s.dev);
+    if (s.stream) (void)hipStreamSynchronize(s.stream);
+    if (s.comm) ncclCommDestroy(s.comm);
+    for (char *p : {s.A, s.b, s.x, s.r, s.Ap, s.pfull, s.xfull, s.scal})
+        if (p) (void)hipFree(p);
+    if (s.ws.partials) (void)hipFree(s.ws.partials);
+    if (s.ws.tickets) (void)hipFree(s.ws.tickets);
+    if (s.h_pin) (void)hipHostFree(s.h_pin);
+    for (auto e : s.ev_t) (void)hipEventDestroy(e);
+    if (s.ev_sync) (void)hipEventDestroy(s.ev_sync);
+    if (s.stream) (void)hipStreamDestroy(s.stream);
+    s = Shard();
+}
+
+int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
+
+int check_n(int64_t n, int nranks) {
+    if (n < 1) return fail(CGX_ERR_ARG, "n must be >= 1 (got %lld)", (long long)n);
+    if (nranks < 1) return fail(CGX_ERR_ARG, "nranks must be >= 1");
+    if (n % nranks != 0)  // parallel_cg.c:86-90
+        return fail(CGX_ERR_SHAPE, "%lld is not divisible by %d", (long long)n, nranks);
+    if (n > (int64_t)0xffffffffLL) return fail(CGX_ERR_ARG, "n too large");
+    return CGX_OK;
+}
+
+cgx_ctx *new_ctx(int64_t n, int nranks, int flags) {
+    cgx_ctx *c = new (std::nothrow) cgx_ctx();
+    if (!c) return nullptr;
+    c->n = n;
+    c->lda = round_up(n, 128);
+    c->nranks = nranks;
+    c->flags = flags;
+    c->es = (flags & CGX_F32_REF) ? 4 : 8;
+    return c;
+}
+
+int finish_create(cgx_ctx *c, cgx_ctx **out) {
+    for (auto &s : c->sh) {
+        int rc = alloc_shard(c, s);
+        if (rc != CGX_OK) {
+            std::string keep = g_err;
+            for (auto &t : c->sh) free_shard(t);
+            delete c;
+            snprintf(g_err, sizeof g_err, "%s", keep.c_str());
+            return rc;
+        }
+    }
+    *out = c;
+    return CGX_OK;
+}
+
+// ---- timing -------------------------------------------------------------------
+int timing_resolve(cgx_ctx *c) {
+    if (!(c->flags & CGX_TIMING)) return CGX_OK;
+    Shard &s = c->sh[0];
+    TRY(set_dev(s));
+    for (int i = 0; i < s.ev_used; ++i) {
+        float ms = 0.f;
+        HIPT(hipEventSynchronize(s.ev_t[2 * i + 1]));
+        HIPT(hipEventElapsedTime(&ms, s.ev_t[2 * i], s.ev_t[2 * i + 1]));
+        c->matvec_ms += ms;
+        c->matvec_count += 1;
+    }
+    s.ev_used = 0;
+    return CGX_OK;
+}
+
+// ---- exchange ---------------------------------------------------------------------
+// Make every shard's stream wait for the work already queued on all shards.
+int local_barrier(cgx_ctx *c) {
+    for (auto &s : c->sh) {
+        TRY(set_dev(s));
+        HIPT(hipEventRecord(s.ev_sync, s.stream));
+    }
+    for (auto &d : c->sh) {
+        TRY(set_dev(d));
+        for (auto &s : c->sh)
+            if (&s != &d) HIPT(hipStreamWaitEvent(d.stream, s.ev_sync, 0));
+    }
+    return CGX_OK;
+}
+
+// Every shard's pfull gets every shard's slice of `src(shard)` (its own slice
+// of a full-length buffer when in_place, else a separate local buffer).
+int exchange_allgather(cgx_ctx *c, bool from_x) {
+    const size_t es = (size_t)c->es;
+    if (c->mode == M_SINGLE) {
+        if (from_x) {
+            Shard &s = c->sh[0];
+            TRY(set_dev(s));
+            HIPT(hipMemcpyAsync(s.pfull + s.row0 * es, s.x, s.nloc * es, hipMemcpyDeviceToDevice, s.stream));
+        }
+        return CGX_OK;
+    }
+    if (c->mode == M_RCCL) {
+        Shard &s = c->sh[0];
+        TRY(set_dev(s));
+        const ncclDataType_t t = f32ref(c) ? ncclFloat : ncclDouble;
+        const void *send = from_x ? (const void *)s.x : (const void *)(s.pfull + s.row0 * es);
+        NCCLT(ncclAllGather(send, s.pfull, (size_t)s.nloc, t, s.comm, s.stream));
+        return CGX_OK;
+    }
+    // LOCAL: device-to-device copies after all producers are done.
+    TRY(local_barrier(c));
+    for (auto &d : c->sh) {
+        TRY(set_dev(d));
+        for (auto &s : c->sh) {
+            char *dst = d.pfull + s.row0 * es;
+            const char *src = from_x ? s.x : s.pfull + s.row0 * es;
+            if (&s == &d && !from_x) continue;
+            HIPT(hipMemcpyPeerAsync(dst, d.dev, src, s.dev, s.nloc * es, d.stream));
+        }
+    }
+    return CGX_OK;
+}
+
+// Combine the per-shard partials in slot `lslot` into the global slot `gslot`.
+int exchange_scalar(cgx_ctx *c, int lslot, int gslot) {
+    if (c->mode == M_SINGLE) return CGX_OK;  // kernels wrote the global slot directly
+    const int S = (int)c->sh.size();
+    if (c->mode == M_RCCL) {
+        Shard &s = c->sh[0];
+        TRY(set_dev(s));
+        if (f32ref(c)) {
+            // point-to-point_cg.c allSum order: gather the partials, sum in rank order
+            NCCLT(ncclAllGather(slot(s, lslot), slot(s, S_GATHER), 1, ncclUint64, s.comm, s.stream));
+            HIPT(sum_ordered_f32(reinterpret_cast<const float *>(slot(s, S_GATHER)), c->nranks,
+                                 reinterpret_cast<float *>(slot(s, gslot)), s.stream));
+        } else {
+            NCCLT(ncclAllReduce(slot(s, lslot), slot(s, gslot), 1, ncclDouble, ncclSum, s.comm, s.stream));
+        }
+        return CGX_OK;
+    }
+    TRY(local_barrier(c));
+    for (auto &d : c->sh) {
+        TRY(set_dev(d));
+        for (auto &s : c->sh)
+            HIPT(hipMemcpyPeerAsync(slot(d, S_GATHER + s.index), d.dev, slot(s, lslot), s.dev, 8, d.stream));
+        if (f32ref(c))
+            HIPT(sum_ordered_f32(reinterpret_cast<const float *>(slot(d, S_GATHER)), S,
+                                 reinterpret_cast<float *>(slot(d, gslot)), d.stream));
+        else
+            HIPT(sum_ordered_f64(reinterpret_cast<const double *>(slot(d, S_GATHER)), S,
+                                 reinterpret_cast<double *>(slot(d, gslot)), d.stream));
+    }
+    return CGX_OK;
+}
+
+// Where a kernel writes its (partial) scalar: the global slot directly when
+// there is nothing to combine, else the shard-local slot.
+inline int out_slot(const cgx_ctx *c, int lslot, int gslot) { return c->mode == M_SINGLE ? gslot : lslot; }
+
+// ---- the iteration pieces ----------------------------------------------------------
+int launch_matvec(cgx_ctx *c, Shard &s, const char *vec, bool with_dot, int dot_slot) {
+    const bool timing = (c->flags & CGX_TIMING) && (&s == &c->sh[0]);
+    if (timing && s.ev_used >= kEvPairs) TRY(timing_resolve(c));
+    if (timing) HIPT(hipEventRecord(s.ev_t[2 * s.ev_used], s.stream));
+    if (f32ref(c)) {
+        HIPT(matvec_ref_f32(reinterpret_cast<const float *>(s.A), c->lda, s.nloc, c->n,
+                            reinterpret_cast<const float *>(vec), reinterpret_cast<float *>(s.Ap), s.stream));
+    } else {
+        HIPT(matvec_f64(s.plan, reinterpret_cast<const double *>(s.A), c->lda, s.nloc, c->lda,
+                        reinterpret_cast<const double *>(vec), reinterpret_cast<double *>(s.Ap),
+                        with_dot ? reinterpret_cast<const double *>(s.pfull + s.row0 * 8) : nullptr,
+                        with_dot ? reinterpret_cast<double *>(slot(s, dot_slot)) : nullptr, s.ws, s.stream));
+    }
+    if (timing) {
+        HIPT(hipEventRecord(s.ev_t[2 * s.ev_used + 1], s.stream));
+        s.ev_used++;
+    }
+    if (f32ref(c) && with_dot)  // vecVec(p, Ap) sequential (serialConjugate.c:219)
+        HIPT(dot_ref_f32(s.nloc, reinterpret_cast<const float *>(s.pfull + s.row0 * 4),
+                         reinterpret_cast<const float *>(s.Ap), reinterpret_cast<float *>(slot(s, dot_slot)),
+                         s.stream));
+    return CGX_OK;
+}
+
+int do_begin(cgx_ctx *c) {
+    // r0 = p0 = b - A x0; rr0 = r0.r0   (serialConjugate.c:209-212, parallel_cg.c:283-287)
+    TRY(exchange_allgather(c, /*from_x=*/true));  // full x0 into pfull
+    const int gs = S_RR + ring(0), ls = S_LRR + ring(0);
+    const int os = out_slot(c, ls, gs);
+    for (auto &s : c->sh) {
+        TRY(set_dev(s));
+        TRY(launch_matvec(c, s, s.pfull, false, 0));
+        if (f32ref(c)) {
+            float *pown = reinterpret_cast<float *>(s.pfull + s.row0 * 4);
+            HIPT(residual_ref_f32(s.nloc, reinterpret_cast<const float *>(s.b), reinterpret_cast<const float *>(s.Ap),
+                                  reinterpret_cast<float *>(s.r), pown, s.stream));
+            HIPT(dot_ref_f32(s.nloc, reinterpret_cast<const float *>(s.r), reinterpret_cast<const float *>(s.r),
+                             reinterpret_cast<float *>(slot(s, os)), s.stream));
+        } else {
+            double *pown = reinterpret_cast<double *>(s.pfull + s.row0 * 8);
+            HIPT(residual_f64(s.nloc, reinterpret_cast<const double *>(s.b), reinterpret_cast<const double *>(s.Ap),
+                              reinterpret_cast<double *>(s.r), pown, reinterpret_cast<double *>(slot(s, os)), s.ws,
+                              s.stream));
+        }
+    }
+    TRY(exchange_scalar(c, ls, gs));
+    c->k = 0;
+    c->converged = 0;
+    c->state = ST_BEGUN;
+    return CGX_OK;
+}
+
+int read_scalar(cgx_ctx *c, int gslot, double *out) {
+    Shard &s = c->sh[0];
+    TRY(set_dev(s));
+    HIPT(hipMemcpyAsync(s.h_pin, slot(s, gslot), 8, hipMemcpyDeviceToHost, s.stream));
+    HIPT(hipStreamSynchronize(s.stream));
+    if (f32ref(c)) {
+        float f;
+        std::memcpy(&f, s.h_pin, 4);
+        *out = (double)f;
+    } else {
+        *out = s.h_pin[0];
+    }
+    return CGX_OK;
+}
+
+// One loop iteration k (serialConjugate.c:215-244 / parallel_cg.c:290-323).
+// Returns 1 in *stop when sqrt(r.r) < eps ended the loop (before the p update,
+// as the reference breaks at :235-238).
+int do_iteration(cgx_ctx *c, double eps, int *stop) {
+    const int64_t k = c->k;
+    *stop = 0;
+    TRY(exchange_allgather(c, false));  // MPI_Allgather(local_p -> p)  parallel_cg.c:290
+    const int pg = S_PAP + ring(k), pl = S_LPAP + ring(k);
+    for (auto &s : c->sh) {
+        TRY(set_dev(s));
+        TRY(launch_matvec(c, s, s.pfull, true, out_slot(c, pl, pg)));  // :215 / :292-293
+    }
+    TRY(exchange_scalar(c, pl, pg));  // MPI_Allreduce(p.Ap)  parallel_cg.c:294
+    const int rg = S_RR + ring(k + 1), rl = S_LRR + ring(k + 1);
+    const int ro = out_slot(c, rl, rg);
+    for (auto &s : c->sh) {
+        TRY(set_dev(s));
+        if (f32ref(c)) {
+            HIPT(update_xr_ref_f32(s.nloc, reinterpret_cast<float *>(s.x), reinterpret_cast<float *>(s.r),
+                                   reinterpret_cast<const float *>(s.pfull + s.row0 * 4),
+                                   reinterpret_cast<const float *>(s.Ap),
+                                   reinterpret_cast<const float *>(slot(s, S_RR + ring(k))),
+                                   reinterpret_cast<const float *>(slot(s, pg)), s.stream));
+            HIPT(dot_ref_f32(s.nloc, reinterpret_cast<const float *>(s.r), reinterpret_cast<const float *>(s.r),
+                             reinterpret_cast<float *>(slot(s, ro)), s.stream));
+        } else {
+            HIPT(update_xr_f64(s.nloc, reinterpret_cast<double *>(s.x), reinterpret_cast<double *>(s.r),
+                               reinterpret_cast<const double *>(s.pfull + s.row0 * 8),
+                               reinterpret_cast<const double *>(s.Ap),
+                               reinterpret_cast<const double *>(slot(s, S_RR + ring(k))),
+                               reinterpret_cast<const double *>(slot(s, pg)), reinterpret_cast<double *>(slot(s, ro)),
+                               s.ws, s.stream));
+        }
+    }
+    TRY(exchange_scalar(c, rl, rg));  // MPI_Allreduce(r.r)  parallel_cg.c:313
+    c->k = k + 1;
+    c->total_iters += 1;
+    if (eps >= 0.0) {  // if (sqrt(beta) < EPSILON) break;  serialConjugate.c:235-238
+        double rr = 0.0;
+        TRY(read_scalar(c, rg, &rr));
+        c->last_rr = rr;
+        if (std::sqrt(rr) < eps) {
+            c->converged = 1;
+            c->state = ST_CONVERGED;
+            *stop = 1;
+            return CGX_OK;
+        }
+    }
+    for (auto &s : c->sh) {  // p = r + (beta/rsold) p    serialConjugate.c:239-243
+        TRY(set_dev(s));
+        if (f32ref(c))
+            HIPT(update_p_ref_f32(s.nloc, reinterpret_cast<float *>(s.pfull + s.row0 * 4),
+                                  reinterpret_cast<const float *>(s.r), reinterpret_cast<const float *>(slot(s, rg)),
+                                  reinterpret_cast<const float *>(slot(s, S_RR + ring(k))), s.stream));
+        else
+            HIPT(update_p_f64(s.nloc, reinterpret_cast<double *>(s.pfull + s.row0 * 8),
+                              reinterpret_cast<const double *>(s.r), reinterpret_cast<const double *>(slot(s, rg)),
+                              reinterpret_cast<const double *>(slot(s, S_RR + ring(k))), s.stream));
+    }
+    return CGX_OK;
+}
+
+int sync_all(cgx_ctx *c) {
+    for (auto &s : c->sh) {
+        TRY(set_dev(s));
+        HIPT(hipStreamSynchronize(s.stream));
+    }
+    return timing_resolve(c);
+}
+
+// Per-device workspace for the kernel-level entry points.
+std::mutex g_ws_mu;
+RedWs g_ws[64];
+int dev_ws(RedWs *out) {
+    int dev = 0;
+    HIPT(hipGetDevice(&dev));
+    if (dev < 0 || dev >= 64) return fail(CGX_ERR_ARG, "device id %d out of range", dev);
+    std::lock_guard<std::mutex> lk(g_ws_mu);
+    if (!g_ws[dev].partials) {
+        HIPT(hipMalloc(&g_ws[dev].partials, kMaxRedBlocks * sizeof(double)));
+        HIPT(hipMalloc(&g_ws[dev].tickets, kTickets * sizeof(unsigned)));
+        HIPT(hipMemset(g_ws[dev].tickets, 0, kTickets * sizeof(unsigned)));
+    }
+    *out = g_ws[dev];
+    return CGX_OK;
+}
+
+int check_dtype(int dtype) {
+    if (dtype != CGX_F64 && dtype != CGX_F32_REF) return fail(CGX_ERR_ARG, "dtype must be CGX_F64 or CGX_F32_REF");
+    return CGX_OK;
+}
+
+}  // namespace
+
+// =====================================================================================
+// C ABI
+// =====================================================================================
+extern "C" {
+
+const char *cgx_strerror(int code) {
+    switch (code) {
+        case CGX_OK: return "ok";
+        case CGX_ERR_ARG: return "invalid argument";
+        case CGX_ERR_HIP: return "HIP runtime error";
+        case CGX_ERR_RCCL: return "RCCL error";
+        case CGX_ERR_SHAPE: return "shape error";
+        case CGX_ERR_NOMEM: return "out of memory";
+        case CGX_ERR_STATE: return "call out of order";
+        case CGX_ERR_NODEV: return "no GPU device";
+        default: return "unknown error";
+    }
+}
+
+const char *cgx_last_error(void) { return g_err; }
+int cgx_version(void) { return CGX_VERSION; }
+
+int cgx_device_count(int *count) {
+    if (!count) return fail(CGX_ERR_ARG, "count is NULL");
+    int n = 0;
+    hipError_t e = hipGetDeviceCount(&n);
+    if (e != hipSuccess) n = 0;
+    *count = n;
+    return CGX_OK;
+}
+
+static int check_device(int device) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(CGX_ERR_NODEV, "no HIP device visible");
+    if (device < 0 || device >= n) return fail(CGX_ERR_ARG, "device %d out of range (%d visible)", device, n);
+    return CGX_OK;
+}
+
+int cgx_create(cgx_ctx **ctx, int64_t n, int device, int flags) {
+    if (!ctx) return fail(CGX_ERR_ARG, "ctx is NULL");
+    *ctx = nullptr;
+    TRY(check_n(n, 1));
+    TRY(check_device(device));
+    cgx_ctx *c = new_ctx(n, 1, flags);
+    if (!c) return fail(CGX_ERR_NOMEM, "host allocation failed");
+    c->mode = M_SINGLE;
+    c->sh.resize(1);
+    c->sh[0].dev = device;
+    c->sh[0].index = 0;
+    c->sh[0].row0 = 0;
+    c->sh[0].nloc = n;
+    return finish_create(c, ctx);
+}
+
+int cgx_create_multi(cgx_ctx **ctx, int64_t n, int nshards, const int *devices, int flags) {
+    if (!ctx || !devices) return fail(CGX_ERR_ARG, "ctx/devices is NULL");
+    *ctx = nullptr;
+    if (nshards < 1 || nshards > kMaxShards) return fail(CGX_ERR_ARG, "nshards must be in [1, %d]", kMaxShards);
+    TRY(check_n(n, nshards));
+    for (int i = 0; i < nshards; ++i) TRY(check_device(devices[i]));
+    cgx_ctx *c = new_ctx(n, nshards, flags);
+    if (!c) return fail(CGX_ERR_NOMEM, "host allocation failed");
+    c->mode = nshards == 1 ? M_SINGLE : M_LOCAL;
+    c->sh.resize(nshards);
+    const int64_t loc = n / nshards;
+    for (int i = 0; i < nshards; ++i) {
+        c->sh[i].dev = devices[i];
+        c->sh[i].index = i;
+        c->sh[i].row0 = (int64_t)i * loc;
+        c->sh[i].nloc = loc;
+    }
+    // Peer access between distinct devices (xGMI); repeated devices need none.
+    for (int i = 0; i < nshards; ++i)
+        for (int j = 0; j < nshards; ++j)
+            if (devices[i] != devices[j]) {
+                (void)hipSetDevice(devices[i]);
+                hipError_t e = hipDeviceEnablePeerAccess(devices[j], 0);
+                if (e == hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
+            }
+    return finish_create(c, ctx);
+}
+
+int cgx_get_unique_id(cgx_unique_id *id) {
+    if (!id) return fail(CGX_ERR_ARG, "id is NULL");
+    static_assert(sizeof(ncclUniqueId) == sizeof(cgx_unique_id), "unique id size");
+    ncclUniqueId u;
+    NCCLT(ncclGetUniqueId(&u));
+    std::memcpy(id, &u, sizeof u);
+    return CGX_OK;
+}
+
+int cgx_create_rank(cgx_ctx **ctx, int64_t n, int rank, int nranks, const cgx_unique_id *id, int device,
+                    int flags) {
+    if (!ctx || !id) return fail(CGX_ERR_ARG, "ctx/id is NULL");
+    *ctx = nullptr;
+    TRY(check_n(n, nranks));
+    if (rank < 0 || rank >= nranks) return fail(CGX_ERR_ARG, "rank %d not in [0, %d)", rank, nranks);
+    if (nranks > S_TR - S_GATHER) return fail(CGX_ERR_ARG, "at most %d ranks", S_TR - S_GATHER);
+    TRY(check_device(device));
+    cgx_ctx *c = new_ctx(n, nranks, flags);
+    if (!c) return fail(CGX_ERR_NOMEM, "host allocation failed");
+    c->mode = M_RCCL;
+    c->sh.resize(1);
+    Shard &s = c->sh[0];
+    s.dev = device;
+    s.index = rank;
+    s.nloc = n / nranks;
+    s.row0 = (int64_t)rank * s.nloc;
+    if (hipSetDevice(device) != hipSuccess) {
+        delete c;
+        return fail(CGX_ERR_HIP, "hipSetDevice(%d) failed", device);
+    }
+    ncclUniqueId u;
+    std::memcpy(&u, id, sizeof u);
+    ncclResult_t nr = ncclCommInitRank(&s.comm, nranks, u, rank);
+    if (nr != ncclSuccess) {
+        delete c;
+        return fail(CGX_ERR_RCCL, "ncclCommInitRank(rank %d of %d): %s", rank, nranks, ncclGetErrorString(nr));
+    }
+    return finish_create(c, ctx);
+}
+
+int cgx_destroy(cgx_ctx *ctx) {
+    if (!ctx) return CGX_OK;
+    for (auto &s : ctx->sh) free_shard(s);
+    delete ctx;
+    return CGX_OK;
+}
+
+int cgx_get_info(const cgx_ctx *c, cgx_info *info) {
+    if (!c || !info) return fail(CGX_ERR_ARG, "NULL argument");
+    info->n = c->n;
+    info->lda = c->lda;
+    info->nranks = c->nranks;
+    info->nshards = (int)c->sh.size();
+    info->rank0 = c->sh[0].index;
+    info->row0 = c->sh[0].row0;
+    info->nrows = 0;
+    for (auto &s : c->sh) info->nrows += s.nloc;
+    info->flags = c->flags;
+    info->elem_bytes = c->es;
+    return CGX_OK;
+}
+
+int cgx_set_rows(cgx_ctx *c, int64_t row0, int64_t nrows, const void *A_rows, int64_t lda_host,
+                 const void *b_rows, const void *x_rows) {
+    if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
+    if (row0 < 0 || nrows < 0 || row0 + nrows > c->n)
+        return fail(CGX_ERR_SHAPE, "rows [%lld, %lld) outside [0, %lld)", (long long)row0,
+                    (long long)(row0 + nrows), (long long)c->n);
+    if (A_rows && lda_host < c->n) return fail(CGX_ERR_ARG, "lda_host (%lld) < n", (long long)lda_host);
+    const size_t es = (size_t)c->es;
+    for (auto &s : c->sh) {
+        const int64_t lo = std::max(row0, s.row0), hi = std::min(row0 + nrows, s.row0 + s.nloc);
+        if (hi <= lo) continue;
+        TRY(set_dev(s));
+        if (A_rows)
+            HIPT(hipMemcpy2DAsync(s.A + (size_t)(lo - s.row0) * c->lda * es, (size_t)c->lda * es,
+                                  static_cast<const char *>(A_rows) + (size_t)(lo - row0) * lda_host * es,
+                                  (size_t)lda_host * es, (size_t)c->n * es, (size_t)(hi - lo), hipMemcpyHostToDevice,
+                                  s.stream));
+        if (b_rows)
+            HIPT(hipMemcpyAsync(s.b + (lo - s.row0) * es, static_cast<const char *>(b_rows) + (lo - row0) * es,
+                                (hi - lo) * es, hipMemcpyHostToDevice, s.stream));
+        if (x_rows)
+            HIPT(hipMemcpyAsync(s.x + (lo - s.row0) * es, static_cast<const char *>(x_rows) + (lo - row0) * es,
+                                (hi - lo) * es, hipMemcpyHostToDevice, s.stream));
+        HIPT(hipStreamSynchronize(s.stream));
+    }
+    c->state = ST_IDLE;
+    return CGX_OK;
+}
+
+int cgx_set_system(cgx_ctx *c, const void *A, const void *b, const void *x0) {
+    if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
+    return cgx_set_rows(c, 0, c->n, A, c->n, b, x0);
+}
+
+int cgx_generate_spd(cgx_ctx *c, uint64_t seed) {
+    if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
+    for (auto &s : c->sh) {
+        TRY(set_dev(s));
+        if (f32ref(c))
+            HIPT(gen_spd_f32(c->n, c->lda, s.row0, s.nloc, seed, reinterpret_cast<float *>(s.A),
+                             reinterpret_cast<float *>(s.b), s.stream));
+        else
+            HIPT(gen_spd_f64(c->n, c->lda, s.row0, s.nloc, seed, reinterpret_cast<double *>(s.A),
+                             reinterpret_cast<double *>(s.b), s.stream));
+        HIPT(hipMemsetAsync(s.x, 0, s.nloc * c->es, s.stream));
+    }
+    TRY(sync_all(c));
+    c->state = ST_IDLE;
+    return CGX_OK;
+}
+
+int cgx_set_x(cgx_ctx *c, const void *x) {
+    if (!c || !x) return fail(CGX_ERR_ARG, "NULL argument");
+    return cgx_set_rows(c, 0, c->n, nullptr, c->n, nullptr, x);
+}
+
+int cgx_get_x(cgx_ctx *c, void *x) {
+    if (!c || !x) return fail(CGX_ERR_ARG, "NULL argument");
+    const size_t es = (size_t)c->es;
+    if (c->mode == M_RCCL && c->nranks > 1) {
+        Shard &s = c->sh[0];
+        TRY(set_dev(s));
+        NCCLT(ncclAllGather(s.x, s.xfull, (size_t)s.nloc, f32ref(c) ? ncclFloat : ncclDouble, s.comm, s.stream));
+        HIPT(hipMemcpyAsync(x, s.xfull, (size_t)c->n * es, hipMemcpyDeviceToHost, s.stream));
+        HIPT(hipStreamSynchronize(s.stream));
+        return CGX_OK;
+    }
+    for (auto &s : c->sh) {
+        TRY(set_dev(s));
+        HIPT(hipMemcpyAsync(static_cast<char *>(x) + s.row0 * es, s.x, s.nloc * es, hipMemcpyDeviceToHost, s.stream));
+    }
+    return sync_all(c);
+}
+
+int cgx_solve_begin(cgx_ctx *c) {
+    if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
+    return do_begin(c);
+}
+
+int cgx_iterate(cgx_ctx *c, int64_t count, double eps, int64_t *done, int *converged) {
+    if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
+    if (c->state == ST_IDLE) return fail(CGX_ERR_STATE, "cgx_iterate before cgx_solve_begin");
+    int64_t did = 0;
+    for (; did < count && c->state == ST_BEGUN; ++did) {
+        int stop = 0;
+        TRY(do_iteration(c, eps, &stop));
+        if (stop) {
+            ++did;
+            break;
+        }
+    }
+    if (done) *done = did;
+    if (converged) *converged = c->converged;
+    return CGX_OK;
+}
+
+int cgx_solve(cgx_ctx *c, void *x_inout, double eps, int64_t max_iter, cgx_stats *st) {
+    if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
+    if (x_inout) TRY(cgx_set_x(c, x_inout));
+    TRY(sync_all(c));
+    const auto t0 = std::chrono::steady_clock::now();
+    TRY(do_begin(c));
+    const int64_t cap = max_iter < 0 ? c->n : max_iter;  // for(k=0; k<ROWS; ++k)
+    int64_t done = 0;
+    int conv = 0;
+    TRY(cgx_iterate(c, cap, eps, &done, &conv));
+    TRY(sync_all(c));
+    const auto t1 = std::chrono::steady_clock::now();
+    c->solve_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+    if (eps < 0.0 && c->k > 0) {
+        double rr = 0.0;
+        TRY(read_scalar(c, S_RR + ring(c->k), &rr));
+        c->last_rr = rr;
+    }
+    if (x_inout) TRY(cgx_get_x(c, x_inout));
+    if (st) TRY(cgx_get_stats(c, st));
+    return CGX_OK;
+}
+
+int cgx_get_stats(cgx_ctx *c, cgx_stats *st) {
+    if (!c || !st) return fail(CGX_ERR_ARG, "NULL argument");
+    TRY(sync_all(c));
+    st->iterations = c->k;
+    st->converged = c->converged;
+    st->rr = c->last_rr;
+    st->solve_ms = c->solve_ms;
+    st->matvec_ms = c->matvec_ms;
+    st->matvec_count = c->matvec_count;
+    st->total_iterations = c->total_iters;
+    return CGX_OK;
+}
+
+int cgx_reset_timing(cgx_ctx *c) {
+    if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
+    TRY(sync_all(c));
+    c->matvec_ms = 0.0;
+    c->matvec_count = 0;
+    return CGX_OK;
+}
+
+int cgx_synchronize(cgx_ctx *c) {
+    if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
+    return sync_all(c);
+}
+
+void *cgx_stream(cgx_ctx *c) { return c ? (void *)c->sh[0].stream : nullptr; }
+
+int cgx_residual_norm(cgx_ctx *c, double *rnorm, double *bnorm) {
+    if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
+    // ||b - A x|| with the current x: allgather x, matVec, residual, two dots.
+    TRY(exchange_allgather(c, /*from_x=*/true));
+    const int tro = out_slot(c, S_LTR, S_TR), tbo = out_slot(c, S_LTB, S_TB);
+    for (auto &s : c->sh) {
+        TRY(set_dev(s));
+        TRY(launch_matvec(c, s, s.pfull, false, 0));
+        if (f32ref(c)) {
+            HIPT(residual_ref_f32(s.nloc, reinterpret_cast<const float *>(s.b), reinterpret_cast<const float *>(s.Ap),
+                                  reinterpret_cast<float *>(s.r), nullptr, s.stream));
+            HIPT(dot_ref_f32(s.nloc, reinterpret_cast<const float *>(s.r), reinterpret_cast<const float *>(s.r),
+                             reinterpret_cast<float *>(slot(s, tro)), s.stream));
+            HIPT(dot_ref_f32(s.nloc, reinterpret_cast<const float *>(s.b), reinterpret_cast<const float *>(s.b),
+                             reinterpret_cast<float *>(slot(s, tbo)), s.stream));
+        } else {
+            HIPT(residual_f64(s.nloc, reinterpret_cast<const double *>(s.b), reinterpret_cast<const double *>(s.Ap),
+                              reinterpret_cast<double *>(s.r), nullptr, reinterpret_cast<double *>(slot(s, tro)), s.ws,
+                              s.stream));
+            HIPT(dot_f64(s.nloc, reinterpret_cast<const double *>(s.b), reinterpret_cast<const double *>(s.b),
+                         reinterpret_cast<double *>(slot(s, tbo)), s.ws, s.stream));
+        }
+    }
+    TRY(exchange_scalar(c, S_LTR, S_TR));
+    TRY(exchange_scalar(c, S_LTB, S_TB));
+    double rr = 0.0, bb = 0.0;
+    TRY(read_scalar(c, S_TR, &rr));
+    TRY(read_scalar(c, S_TB, &bb));
+    if (rnorm) *rnorm = std::sqrt(rr);
+    if (bnorm) *bnorm = std::sqrt(bb);
+    c->state = ST_IDLE;  // r and p were overwritten
+    return CGX_OK;
+}
+
+// ---- kernel-level entry points ---------------------------------------------------------
+int cgx_dev_malloc(void **ptr, size_t bytes) {
+    if (!ptr) return fail(CGX_ERR_ARG, "ptr is NULL");
+    hipError_t e = hipMalloc(ptr, bytes ? bytes : 16);
+    if (e != hipSuccess) return fail(CGX_ERR_NOMEM, "hipMalloc(%zu): %s", bytes, hipGetErrorString(e));
+    return CGX_OK;
+}
+int cgx_dev_free(void *ptr) {
+    if (ptr) HIPT(hipFree(ptr));
+    return CGX_OK;
+}
+int cgx_memcpy_h2d(void *dst, const void *src, size_t bytes) {
+    HIPT(hipMemcpy(dst, src, bytes, hipMemcpyHostToDevice));
+    return CGX_OK;
+}
+int cgx_memcpy_d2h(void *dst, const void *src, size_t bytes) {
+    HIPT(hipMemcpy(dst, src, bytes, hipMemcpyDeviceToHost));
+    return CGX_OK;
+}
+int cgx_dev_synchronize(void) {
+    HIPT(hipDeviceSynchronize());
+    return CGX_OK;
+}
+
+int cgx_matvec(int dtype, const void *A, int64_t lda, int64_t rows, int64_t cols, const void *v, void *out,
+               void *stream) {
+    TRY(check_dtype(dtype));
+    if (rows < 0 || cols < 0 || lda < cols) return fail(CGX_ERR_SHAPE, "bad matVec shape");
+    if (!A || !v || !out) return fail(CGX_ERR_ARG, "NULL pointer");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (dtype == CGX_F32_REF) {
+        HIPT(matvec_ref_f32(static_cast<const float *>(A), lda, rows, cols, static_cast<const float *>(v),
+                            static_cast<float *>(out), s));
+        return CGX_OK;
+    }
+    int dev = 0;
+    HIPT(hipGetDevice(&dev));
+    RedWs ws;
+    TRY(dev_ws(&ws));
+    MatvecPlan pl = plan_matvec_f64(dev, rows);
+    HIPT(matvec_f64(pl, static_cast<const double *>(A), lda, rows, cols, static_cast<const double *>(v),
+                    static_cast<double *>(out), nullptr, nullptr, ws, s));
+    return CGX_OK;
+}
+
+int cgx_dot(int dtype, int64_t n, const void *a, const void *b, void *out_dev, void *stream) {
+    TRY(check_dtype(dtype));
+    if (!a || !b || !out_dev || n < 0) return fail(CGX_ERR_ARG, "bad argument");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (dtype == CGX_F32_REF) {
+        HIPT(dot_ref_f32(n, static_cast<const float *>(a), static_cast<const float *>(b), static_cast<float *>(out_dev), s));
+        return CGX_OK;
+    }
+    RedWs ws;
+    TRY(dev_ws(&ws));
+    HIPT(dot_f64(n, static_cast<const double *>(a), static_cast<const double *>(b), static_cast<double *>(out_dev), ws, s));
+    return CGX_OK;
+}
+
+int cgx_residual(int dtype, int64_t n, const void *b, const void *Ax, void *r, void *p, void *rr_dev,
+                 void *stream) {
+    TRY(check_dtype(dtype));
+    if (!b || !Ax || !r || !p || n < 0) return fail(CGX_ERR_ARG, "bad argument");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (dtype == CGX_F32_REF) {
+        HIPT(residual_ref_f32(n, static_cast<const float *>(b), static_cast<const float *>(Ax), static_cast<float *>(r),
+                              static_cast<float *>(p), s));
+        if (rr_dev)
+            HIPT(dot_ref_f32(n, static_cast<const float *>(r), static_cast<const float *>(r), static_cast<float *>(rr_dev), s));
+        return CGX_OK;
+    }
+    RedWs ws;
+    TRY(dev_ws(&ws));
+    HIPT(residual_f64(n, static_cast<const double *>(b), static_cast<const double *>(Ax), static_cast<double *>(r),
+                      static_cast<double *>(p), static_cast<double *>(rr_dev), ws, s));
+    return CGX_OK;
+}
+
+int cgx_update_xr(int dtype, int64_t n, void *x, void *r, const void *p, const void *Ap, const void *rsold_dev,
+                  const void *pAp_dev, void *rr_dev, void *stream) {
+    TRY(check_dtype(dtype));
+    if (!x || !r || !p || !Ap || !rsold_dev || !pAp_dev || !rr_dev || n < 0) return fail(CGX_ERR_ARG, "bad argument");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (dtype == CGX_F32_REF) {
+        HIPT(update_xr_ref_f32(n, static_cast<float *>(x), static_cast<float *>(r), static_cast<const float *>(p),
+                               static_cast<const float *>(Ap), static_cast<const float *>(rsold_dev),
+                               static_cast<const float *>(pAp_dev), s));
+        HIPT(dot_ref_f32(n, static_cast<const float *>(r), static_cast<const float *>(r), static_cast<float *>(rr_dev), s));
+        return CGX_OK;
+    }
+    RedWs ws;
+    TRY(dev_ws(&ws));
+    HIPT(update_xr_f64(n, static_cast<double *>(x), static_cast<double *>(r), static_cast<const double *>(p),
+                       static_cast<const double *>(Ap), static_cast<const double *>(rsold_dev),
+                       static_cast<const double *>(pAp_dev), static_cast<double *>(rr_dev), ws, s));
+    return CGX_OK;
+}
+
+int cgx_update_p(int dtype, int64_t n, void *p, const void *r, const void *rr_dev, const void *rsold_dev,
+                 void *stream) {
+    TRY(check_dtype(dtype));
+    if (!p || !r || !rr_dev || !rsold_dev || n < 0) return fail(CGX_ERR_ARG, "bad argument");
+    hipStream_t s = static_cast<hipStream_t>(stream);
+    if (dtype == CGX_F32_REF)
+        HIPT(update_p_ref_f32(n, static_cast<float *>(p), static_cast<const float *>(r), static_cast<const float *>(rr_dev),
+                              static_cast<const float *>(rsold_dev), s));
+    else
+        HIPT(update_p_f64(n, static_cast<double *>(p), static_cast<const double *>(r), static_cast<const double *>(rr_dev),
+                          static_cast<const double *>(rsold_dev), s));
+    return CGX_OK;
+}
+
+}  // extern "C"

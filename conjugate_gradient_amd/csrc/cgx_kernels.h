@@ -1,0 +1,65 @@
+// cgx_kernels.h -- host-side launchers for the CDNA4 (gfx950) CG kernels.
+// Internal to libcgx.so; the public boundary is include/cgx.h.
+#pragma once
+#include <hip/hip_runtime.h>
+#include <cstdint>
+
+namespace cgx {
+
+// Scratch needed by the last-block reductions (one set per stream in use).
+struct RedWs {
+    double *partials;      // >= kMaxRedBlocks doubles
+    unsigned *tickets;     // kTickets counters, zero at rest
+};
+constexpr int kMaxRedBlocks = 8192;
+constexpr int kTickets = 8;
+enum Ticket { T_MATVEC = 0, T_RESID = 1, T_XR = 2, T_DOT = 3 };
+
+// Geometry of the fp64 row-streaming matVec, chosen once per (device, rows).
+struct MatvecPlan {
+    int R = 4;        // rows per wave
+    int U = 4;        // 128-column chunks in flight per row
+    int nt = 1;       // non-temporal loads of A
+    int blocks = 0;   // grid (256-thread blocks), grid-stride over row groups
+};
+MatvecPlan plan_matvec_f64(int device, int64_t rows);
+
+// ---- fp64 -------------------------------------------------------------------
+// out[i] = sum_j A[i*lda+j] v[j]; if pown != nullptr also *dot_out = pown . out
+// (last-block reduction, fixed order).
+hipError_t matvec_f64(const MatvecPlan &pl, const double *A, int64_t lda, int64_t rows,
+                      int64_t cols, const double *v, double *out, const double *pown,
+                      double *dot_out, const RedWs &ws, hipStream_t s);
+// r = b - Ax; p = r (if p); *rr_out = r.r (if rr_out)
+hipError_t residual_f64(int64_t n, const double *b, const double *Ax, double *r, double *p,
+                        double *rr_out, const RedWs &ws, hipStream_t s);
+// alpha = *rsold / *pAp; x += alpha p; r -= alpha Ap; *rr_out = r.r
+hipError_t update_xr_f64(int64_t n, double *x, double *r, const double *p, const double *Ap,
+                         const double *rsold, const double *pAp, double *rr_out,
+                         const RedWs &ws, hipStream_t s);
+// p = r + (*rr / *rsold) p
+hipError_t update_p_f64(int64_t n, double *p, const double *r, const double *rr,
+                        const double *rsold, hipStream_t s);
+hipError_t dot_f64(int64_t n, const double *a, const double *b, double *out,
+                   const RedWs &ws, hipStream_t s);
+// Rows [row0, row0+nrows) of the counter-hash SPD system; pad columns zeroed.
+hipError_t gen_spd_f64(int64_t n, int64_t lda, int64_t row0, int64_t nrows, uint64_t seed,
+                       double *A, double *b, hipStream_t s);
+// out = sum_{q<cnt} (8-byte slot q of in), in q order (one thread): rank-ordered combine.
+hipError_t sum_ordered_f64(const double *in, int cnt, double *out, hipStream_t s);
+
+// ---- fp32, serialConjugate.c operation order ---------------------------------
+hipError_t matvec_ref_f32(const float *A, int64_t lda, int64_t rows, int64_t cols,
+                          const float *v, float *out, hipStream_t s);
+hipError_t dot_ref_f32(int64_t n, const float *a, const float *b, float *out, hipStream_t s);
+hipError_t residual_ref_f32(int64_t n, const float *b, const float *Ax, float *r, float *p,
+                            hipStream_t s);
+hipError_t update_xr_ref_f32(int64_t n, float *x, float *r, const float *p, const float *Ap,
+                             const float *rsold, const float *pAp, hipStream_t s);
+hipError_t update_p_ref_f32(int64_t n, float *p, const float *r, const float *rr,
+                            const float *rsold, hipStream_t s);
+hipError_t gen_spd_f32(int64_t n, int64_t lda, int64_t row0, int64_t nrows, uint64_t seed,
+                       float *A, float *b, hipStream_t s);
+hipError_t sum_ordered_f32(const float *in, int cnt, float *out, hipStream_t s);
+
+}  // namespace cgx

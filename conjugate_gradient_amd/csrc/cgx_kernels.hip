@@ -1,0 +1,555 @@
+// cgx_kernels.hip -- hand-written CDNA4 (gfx950) kernels for the CG hot path.
+//
+// The reference's BLAS-1/2 loops (serialConjugate.c:109-177, parallel_cg.c:
+// 172-245) become:
+//   k_matvec_f64      matVec (+ the p.Ap vecVec fused into its epilogue)
+//   k_residual_f64    residual x2 + r.r      (serialConjugate.c:209-212)
+//   k_update_xr_f64   scalarVec+vecAdd (x), scalarVec+vecSub (r), r.r
+//                     (serialConjugate.c:219-234)
+//   k_update_p_f64    scalarVec+vecAdd (p)   (serialConjugate.c:239-243)
+// and, for CGX_F32_REF, kernels that keep the reference's exact fp32
+// operation order (sequential per-row and per-dot accumulation, every
+// multiply and add rounded separately: `#pragma clang fp contract(off)`).
+//
+// Design: the matVec is HBM-bound (0.25 flop/B in fp64), so it
+// streams A once with 16-B-per-lane coalesced loads (a wave covers one
+// 1-KiB, 128-column chunk of a row per instruction), R rows per wave share
+// each p chunk held in registers (p re-reads hit L1/L2: p is <= 1 MiB), U
+// chunks per row are in flight per lane, and the grid is sized to the
+// resident-wave capacity and grid-strides over row groups.  No MFMA: a GEMV
+// has no reuse of A.  Reductions are deterministic: per-block partials in
+// fixed slots, summed in index order by the last block to arrive (agent-scope
+// release/acquire, cdna_hip_programming.md Guideline 16).
+#include "cgx_kernels.h"
+
+#include <algorithm>
+#include <cstdlib>
+#include <mutex>
+
+namespace cgx {
+namespace {
+
+typedef double d2 __attribute__((ext_vector_type(2)));
+
+constexpr int kNT = 256;  // threads per block for the fp64 kernels
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Sum `v` over all threads of the grid.  Each block stores its total in
+// partials[blockIdx.x]; the last block to arrive sums the partials in index
+// order and writes *out.  Deterministic for a fixed grid.
+__device__ __forceinline__ void grid_sum_last_block(double v, double *partials, unsigned *ticket,
+                                                    double *out) {
+    __shared__ double red[kNT / 64];
+    __shared__ int is_last;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    v = wave_sum(v);
+    if (lane == 0) red[wid] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = red[0];
+#pragma unroll
+        for (int w = 1; w < kNT / 64; ++w) t += red[w];
+        partials[blockIdx.x] = t;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        unsigned prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        is_last = (prev == gridDim.x - 1);
+    }
+    __syncthreads();
+    if (!is_last) return;
+    if (threadIdx.x == 0) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
+    __syncthreads();
+    double s = 0.0;
+    for (unsigned i = threadIdx.x; i < gridDim.x; i += kNT) s += partials[i];
+    s = wave_sum(s);
+    if (lane == 0) red[wid] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = red[0];
+#pragma unroll
+        for (int w = 1; w < kNT / 64; ++w) t += red[w];
+        *out = t;
+        __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+template <bool NT>
+__device__ __forceinline__ d2 load_a(const d2 *p) {
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+
+// ---------------------------------------------------------------------------
+// matVec (serialConjugate.c:109-120 / parallel_cg.c:172-184), fp64.
+// Wave w owns row groups g = w, w + waves, ...; a group is R consecutive rows.
+// Per step a lane holds U 16-B chunks of p and R*U 16-B chunks of A.
+// ---------------------------------------------------------------------------
+template <int R, int U, bool NT>
+__global__ __launch_bounds__(kNT) void k_matvec_f64(
+    const double *__restrict__ A, int64_t lda, int64_t rows, int64_t cols, int64_t vec_cols,
+    const double *__restrict__ v, double *__restrict__ out, const double *__restrict__ pown,
+    double *dot_out, double *partials, unsigned *ticket) {
+    const int lane = threadIdx.x & 63;
+    const int wid = threadIdx.x >> 6;
+    const int64_t ngroups = (rows + R - 1) / R;
+    const int64_t wstride = (int64_t)gridDim.x * (kNT / 64);
+    const int64_t nchunk = vec_cols >> 7;  // 16-B-aligned 128-column chunks
+    const int64_t ctail = nchunk << 7;
+    const d2 *v2 = reinterpret_cast<const d2 *>(v) + lane;
+    double dacc = 0.0;
+
+    for (int64_t g = (int64_t)blockIdx.x * (kNT / 64) + wid; g < ngroups; g += wstride) {
+        const int64_t r0 = g * R;
+        int64_t ridx[R];
+        const d2 *arow[R];
+        d2 acc[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            ridx[r] = (r0 + r < rows) ? (r0 + r) : (rows - 1);
+            arow[r] = reinterpret_cast<const d2 *>(A + ridx[r] * lda) + lane;
+            acc[r] = (d2)(0.0);
+        }
+        int64_t c = 0;
+        for (; c + U <= nchunk; c += U) {
+            d2 pv[U];
+            d2 av[R][U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) pv[u] = v2[(c + u) * 64];
+#pragma unroll
+            for (int r = 0; r < R; ++r)
+#pragma unroll
+                for (int u = 0; u < U; ++u) av[r][u] = load_a<NT>(arow[r] + (c + u) * 64);
+#pragma unroll
+            for (int u = 0; u < U; ++u)
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    acc[r].x = __builtin_fma(av[r][u].x, pv[u].x, acc[r].x);
+                    acc[r].y = __builtin_fma(av[r][u].y, pv[u].y, acc[r].y);
+                }
+        }
+        for (; c < nchunk; ++c) {
+            const d2 pv = v2[c * 64];
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const d2 a = load_a<NT>(arow[r] + c * 64);
+                acc[r].x = __builtin_fma(a.x, pv.x, acc[r].x);
+                acc[r].y = __builtin_fma(a.y, pv.y, acc[r].y);
+            }
+        }
+        for (int64_t j = ctail + lane; j < cols; j += 64) {
+            const double vj = v[j];
+#pragma unroll
+            for (int r = 0; r < R; ++r) acc[r].x = __builtin_fma(A[ridx[r] * lda + j], vj, acc[r].x);
+        }
+        double mine = 0.0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const double s = wave_sum(acc[r].x + acc[r].y);
+            if (lane == r) mine = s;
+        }
+        if (lane < R && r0 + lane < rows) {
+            out[r0 + lane] = mine;
+            if (pown) dacc += pown[r0 + lane] * mine;
+        }
+    }
+    if (pown) grid_sum_last_block(dacc, partials, ticket, dot_out);
+}
+
+// residual x2 + vecVec (serialConjugate.c:210-212)
+__global__ __launch_bounds__(kNT) void k_residual_f64(int64_t n, const double *__restrict__ b,
+                                                      const double *__restrict__ Ax,
+                                                      double *__restrict__ r, double *__restrict__ p,
+                                                      double *rr_out, double *partials,
+                                                      unsigned *ticket) {
+    double acc = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kNT) {
+        const double ri = b[i] - Ax[i];
+        r[i] = ri;
+        if (p) p[i] = ri;
+        acc += ri * ri;
+    }
+    if (rr_out) grid_sum_last_block(acc, partials, ticket, rr_out);
+}
+
+// x += alpha p; r -= alpha Ap; r.r  (serialConjugate.c:219-234, conjgrad.m:8-11)
+__global__ __launch_bounds__(kNT) void k_update_xr_f64(int64_t n, double *__restrict__ x,
+                                                       double *__restrict__ r,
+                                                       const double *__restrict__ p,
+                                                       const double *__restrict__ Ap,
+                                                       const double *rsold, const double *pAp,
+                                                       double *rr_out, double *partials,
+                                                       unsigned *ticket) {
+    const double alpha = *rsold / *pAp;
+    double acc = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kNT) {
+        x[i] = x[i] + alpha * p[i];
+        const double ri = r[i] - alpha * Ap[i];
+        r[i] = ri;
+        acc += ri * ri;
+    }
+    grid_sum_last_block(acc, partials, ticket, rr_out);
+}
+
+// p = r + beta p  (serialConjugate.c:239-243, conjgrad.m:15)
+__global__ __launch_bounds__(kNT) void k_update_p_f64(int64_t n, double *__restrict__ p,
+                                                      const double *__restrict__ r,
+                                                      const double *rr, const double *rsold) {
+    const double beta = *rr / *rsold;
+    for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kNT)
+        p[i] = r[i] + beta * p[i];
+}
+
+__global__ __launch_bounds__(kNT) void k_dot_f64(int64_t n, const double *__restrict__ a,
+                                                 const double *__restrict__ b, double *out,
+                                                 double *partials, unsigned *ticket) {
+    double acc = 0.0;
+    for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kNT)
+        acc += a[i] * b[i];
+    grid_sum_last_block(acc, partials, ticket, out);
+}
+
+// ---------------------------------------------------------------------------
+// counter-hash SPD generator (generateSPDmatrix.m:4-17 distribution)
+// ---------------------------------------------------------------------------
+__host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ double u01(uint64_t salt, uint64_t i, uint64_t j) {
+    const uint64_t h = mix64(((i << 32) | (j & 0xffffffffull)) ^ salt);
+    return (double)(h >> 11) * 0x1.0p-53;
+}
+
+template <typename T>
+__global__ __launch_bounds__(kNT) void k_gen_spd(int64_t n, int64_t lda, int64_t row0, int64_t nrows,
+                                                 uint64_t salt, uint64_t salt_b, T *A, T *b) {
+#pragma clang fp contract(off)
+    for (int64_t rr = blockIdx.x; rr < nrows; rr += gridDim.x) {
+        const uint64_t i = (uint64_t)(row0 + rr);
+        T *row = A + rr * lda;
+        for (int64_t jj = threadIdx.x; jj < lda; jj += kNT) {
+            double val = 0.0;
+            if (jj < n) {
+                const uint64_t j = (uint64_t)jj;
+                val = 0.5 * (u01(salt, i, j) + u01(salt, j, i));
+                if (i == j) val = val + (double)n;
+            }
+            row[jj] = (T)val;
+        }
+        if (threadIdx.x == 0) {
+            const uint64_t h = mix64(i ^ salt_b);
+            b[rr] = (T)((double)(h >> 11) * 0x1.0p-53);
+        }
+    }
+}
+
+// Scalars combined in rank order: ((in0 + in1) + in2) + ...  Inputs sit in
+// 8-byte slots (a float at the slot start for F32_REF): element q at in[q*stride].
+template <typename T>
+__global__ void k_sum_ordered(const T *in, int cnt, int stride, T *out) {
+#pragma clang fp contract(off)
+    T s = in[0];
+    for (int q = 1; q < cnt; ++q) s = s + in[q * stride];
+    *out = s;
+}
+
+// ---------------------------------------------------------------------------
+// fp32 kernels in serialConjugate.c's exact operation order (CGX_F32_REF)
+// ---------------------------------------------------------------------------
+// matVec: one lane per row, columns in ascending order, out = ((0 + a0 v0) + a1 v1) + ...
+// A 64x64 tile is staged through LDS so the global reads stay coalesced.
+__global__ __launch_bounds__(64) void k_matvec_ref_f32(const float *__restrict__ A, int64_t lda,
+                                                       int64_t rows, int64_t cols,
+                                                       const float *__restrict__ v,
+                                                       float *__restrict__ out) {
+#pragma clang fp contract(off)
+    __shared__ float tile[64][65];
+    __shared__ float pv[64];
+    const int t = threadIdx.x;
+    const int64_t row0 = (int64_t)blockIdx.x * 64;
+    float acc = 0.0f;
+    for (int64_t c0 = 0; c0 < cols; c0 += 64) {
+        const int w = (cols - c0 < 64) ? (int)(cols - c0) : 64;
+        for (int i = 0; i < 64; ++i) {
+            const int64_t rr = row0 + i;
+            tile[i][t] = (rr < rows && t < w) ? A[rr * lda + c0 + t] : 0.0f;
+        }
+        pv[t] = (t < w) ? v[c0 + t] : 0.0f;
+        __syncthreads();
+        if (w == 64) {
+#pragma unroll 16
+            for (int j = 0; j < 64; ++j) {
+                const float prod = tile[t][j] * pv[j];
+                acc = acc + prod;
+            }
+        } else {
+            for (int j = 0; j < w; ++j) {
+                const float prod = tile[t][j] * pv[j];
+                acc = acc + prod;
+            }
+        }
+        __syncthreads();
+    }
+    if (row0 + t < rows) out[row0 + t] = acc;
+}
+
+// vecVec: one wave; products in parallel, the sum strictly sequential in
+// index order (s = s + a_i b_i), broadcast lane by lane with v_readlane.
+__global__ __launch_bounds__(64) void k_dot_ref_f32(int64_t n, const float *__restrict__ a,
+                                                    const float *__restrict__ b, float *out) {
+#pragma clang fp contract(off)
+    const int lane = threadIdx.x;
+    float s = 0.0f;
+    for (int64_t c0 = 0; c0 < n; c0 += 64) {
+        const float prod = (c0 + lane < n) ? a[c0 + lane] * b[c0 + lane] : 0.0f;
+        const int pb = __float_as_int(prod);
+        if (n - c0 >= 64) {
+#pragma unroll
+            for (int j = 0; j < 64; ++j) s = s + __int_as_float(__builtin_amdgcn_readlane(pb, j));
+        } else {
+            const int w = (int)(n - c0);
+            for (int j = 0; j < w; ++j) s = s + __int_as_float(__builtin_amdgcn_readlane(pb, j));
+        }
+    }
+    if (lane == 0) *out = s;
+}
+
+// residual(r) and residual(p): r = b - Ax; p = b - Ax  (serialConjugate.c:210-211)
+__global__ __launch_bounds__(kNT) void k_residual_ref_f32(int64_t n, const float *__restrict__ b,
+                                                          const float *__restrict__ Ax,
+                                                          float *__restrict__ r, float *__restrict__ p) {
+#pragma clang fp contract(off)
+    for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kNT) {
+        r[i] = b[i] - Ax[i];
+        if (p) p[i] = b[i] - Ax[i];
+    }
+}
+
+// alpha = rsold / pAp (:220); x = x + p*alpha (:221,225); r = r - Ap*alpha (:226,230)
+__global__ __launch_bounds__(kNT) void k_update_xr_ref_f32(int64_t n, float *__restrict__ x,
+                                                           float *__restrict__ r,
+                                                           const float *__restrict__ p,
+                                                           const float *__restrict__ Ap,
+                                                           const float *rsold, const float *pAp) {
+#pragma clang fp contract(off)
+    const float alpha = *rsold / *pAp;
+    for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kNT) {
+        const float tx = p[i] * alpha;
+        x[i] = x[i] + tx;
+        const float tr = Ap[i] * alpha;
+        r[i] = r[i] - tr;
+    }
+}
+
+// p = r + p*(beta/rsold)  (:239,243)
+__global__ __launch_bounds__(kNT) void k_update_p_ref_f32(int64_t n, float *__restrict__ p,
+                                                          const float *__restrict__ r,
+                                                          const float *rr, const float *rsold) {
+#pragma clang fp contract(off)
+    const float ratio = *rr / *rsold;
+    for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kNT) {
+        const float t = p[i] * ratio;
+        p[i] = r[i] + t;
+    }
+}
+
+// ---------------------------------------------------------------------------
+// host helpers
+// ---------------------------------------------------------------------------
+struct DevInfo {
+    int cus = 0;
+};
+std::mutex g_mu;
+DevInfo g_dev[64];
+
+int cu_count(int device) {
+    std::lock_guard<std::mutex> lk(g_mu);
+    if (device < 0 || device >= 64) return 256;
+    if (g_dev[device].cus == 0) {
+        int v = 0;
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || v <= 0)
+            v = 256;
+        g_dev[device].cus = v;
+    }
+    return g_dev[device].cus;
+}
+
+int env_int(const char *name, int dflt) {
+    const char *s = std::getenv(name);
+    return (s && *s) ? std::atoi(s) : dflt;
+}
+
+unsigned grid_1d(int64_t n, int per_block, unsigned cap) {
+    int64_t g = (n + per_block - 1) / per_block;
+    if (g < 1) g = 1;
+    if (g > (int64_t)cap) g = cap;
+    return (unsigned)g;
+}
+
+// Grid of the vector kernels: <= kMaxRedBlocks (the partial slots), ~4 blocks/CU.
+unsigned grid_vec(int64_t n) { return grid_1d(n, kNT, 1024); }
+
+using MvFn = void (*)(const double *, int64_t, int64_t, int64_t, int64_t, const double *, double *,
+                      const double *, double *, double *, unsigned *);
+
+template <int R, int U>
+MvFn pick_nt(int nt) {
+    return nt ? k_matvec_f64<R, U, true> : k_matvec_f64<R, U, false>;
+}
+template <int R>
+MvFn pick_u(int U, int nt) {
+    switch (U) {
+        case 2: return pick_nt<R, 2>(nt);
+        case 8: return pick_nt<R, 8>(nt);
+        default: return pick_nt<R, 4>(nt);
+    }
+}
+MvFn pick_mv(int R, int U, int nt) {
+    switch (R) {
+        case 1: return pick_u<1>(U, nt);
+        case 2: return pick_u<2>(U, nt);
+        case 8: return pick_u<8>(U, nt);
+        default: return pick_u<4>(U, nt);
+    }
+}
+
+}  // namespace
+
+MatvecPlan plan_matvec_f64(int device, int64_t rows) {
+    MatvecPlan pl;
+    const int cus = cu_count(device);
+    // Rows per wave: enough row groups to give every CU >= 8 waves.
+    const int64_t want_waves = (int64_t)cus * 8;
+    if (rows >= 4 * want_waves) pl.R = 4;
+    else if (rows >= 2 * want_waves) pl.R = 2;
+    else pl.R = 1;
+    pl.U = (pl.R == 1) ? 8 : 4;
+    pl.nt = 1;
+    pl.R = env_int("CGX_MV_R", pl.R);
+    pl.U = env_int("CGX_MV_U", pl.U);
+    pl.nt = env_int("CGX_MV_NT", pl.nt);
+    if (pl.R != 1 && pl.R != 2 && pl.R != 4 && pl.R != 8) pl.R = 4;
+    if (pl.U != 2 && pl.U != 4 && pl.U != 8) pl.U = 4;
+    int per_cu = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(pick_mv(pl.R, pl.U, pl.nt)),
+                                                     kNT, 0) != hipSuccess || per_cu <= 0)
+        per_cu = 2;
+    per_cu = env_int("CGX_MV_BLOCKS_PER_CU", per_cu);
+    const int64_t groups = (rows + pl.R - 1) / pl.R;
+    const int64_t need = (groups + (kNT / 64) - 1) / (kNT / 64);
+    int64_t cap = (int64_t)per_cu * cus;
+    if (cap > kMaxRedBlocks) cap = kMaxRedBlocks;
+    pl.blocks = (int)std::max<int64_t>(1, std::min(need, cap));
+    return pl;
+}
+
+hipError_t matvec_f64(const MatvecPlan &pl, const double *A, int64_t lda, int64_t rows, int64_t cols,
+                      const double *v, double *out, const double *pown, double *dot_out,
+                      const RedWs &ws, hipStream_t s) {
+    if (rows <= 0) return hipSuccess;
+    // The vector path needs 16-B-aligned rows and p; otherwise every column
+    // goes through the scalar tail loop.
+    const bool aligned = ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(v)) & 15) == 0 &&
+                         (lda & 1) == 0;
+    const int64_t vec_cols = aligned ? (cols & ~int64_t(127)) : 0;
+    MvFn fn = pick_mv(pl.R, pl.U, pl.nt);
+    hipLaunchKernelGGL(fn, dim3(pl.blocks), dim3(kNT), 0, s, A, lda, rows, cols, vec_cols, v, out, pown, dot_out,
+                       ws.partials, ws.tickets + T_MATVEC);
+    return hipGetLastError();
+}
+
+hipError_t residual_f64(int64_t n, const double *b, const double *Ax, double *r, double *p,
+                        double *rr_out, const RedWs &ws, hipStream_t s) {
+    hipLaunchKernelGGL(k_residual_f64, dim3(grid_vec(n)), dim3(kNT), 0, s, n, b, Ax, r, p, rr_out,
+                       ws.partials, ws.tickets + T_RESID);
+    return hipGetLastError();
+}
+
+hipError_t update_xr_f64(int64_t n, double *x, double *r, const double *p, const double *Ap,
+                         const double *rsold, const double *pAp, double *rr_out, const RedWs &ws,
+                         hipStream_t s) {
+    hipLaunchKernelGGL(k_update_xr_f64, dim3(grid_vec(n)), dim3(kNT), 0, s, n, x, r, p, Ap, rsold, pAp,
+                       rr_out, ws.partials, ws.tickets + T_XR);
+    return hipGetLastError();
+}
+
+hipError_t update_p_f64(int64_t n, double *p, const double *r, const double *rr, const double *rsold,
+                        hipStream_t s) {
+    hipLaunchKernelGGL(k_update_p_f64, dim3(grid_vec(n)), dim3(kNT), 0, s, n, p, r, rr, rsold);
+    return hipGetLastError();
+}
+
+hipError_t dot_f64(int64_t n, const double *a, const double *b, double *out, const RedWs &ws,
+                   hipStream_t s) {
+    hipLaunchKernelGGL(k_dot_f64, dim3(grid_vec(n)), dim3(kNT), 0, s, n, a, b, out, ws.partials,
+                       ws.tickets + T_DOT);
+    return hipGetLastError();
+}
+
+hipError_t gen_spd_f64(int64_t n, int64_t lda, int64_t row0, int64_t nrows, uint64_t seed, double *A,
+                       double *b, hipStream_t s) {
+    if (nrows <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gen_spd<double>, dim3(grid_1d(nrows, 1, 65536)), dim3(kNT), 0, s, n, lda, row0,
+                       nrows, mix64(seed), mix64(seed + 1), A, b);
+    return hipGetLastError();
+}
+
+hipError_t gen_spd_f32(int64_t n, int64_t lda, int64_t row0, int64_t nrows, uint64_t seed, float *A,
+                       float *b, hipStream_t s) {
+    if (nrows <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gen_spd<float>, dim3(grid_1d(nrows, 1, 65536)), dim3(kNT), 0, s, n, lda, row0,
+                       nrows, mix64(seed), mix64(seed + 1), A, b);
+    return hipGetLastError();
+}
+
+hipError_t sum_ordered_f64(const double *in, int cnt, double *out, hipStream_t s) {
+    hipLaunchKernelGGL(k_sum_ordered<double>, dim3(1), dim3(1), 0, s, in, cnt, 1, out);
+    return hipGetLastError();
+}
+
+hipError_t sum_ordered_f32(const float *in, int cnt, float *out, hipStream_t s) {
+    hipLaunchKernelGGL(k_sum_ordered<float>, dim3(1), dim3(1), 0, s, in, cnt, 2, out);
+    return hipGetLastError();
+}
+
+hipError_t matvec_ref_f32(const float *A, int64_t lda, int64_t rows, int64_t cols, const float *v,
+                          float *out, hipStream_t s) {
+    if (rows <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_matvec_ref_f32, dim3((unsigned)((rows + 63) / 64)), dim3(64), 0, s, A, lda, rows,
+                       cols, v, out);
+    return hipGetLastError();
+}
+
+hipError_t dot_ref_f32(int64_t n, const float *a, const float *b, float *out, hipStream_t s) {
+    hipLaunchKernelGGL(k_dot_ref_f32, dim3(1), dim3(64), 0, s, n, a, b, out);
+    return hipGetLastError();
+}
+
+hipError_t residual_ref_f32(int64_t n, const float *b, const float *Ax, float *r, float *p,
+                            hipStream_t s) {
+    hipLaunchKernelGGL(k_residual_ref_f32, dim3(grid_vec(n)), dim3(kNT), 0, s, n, b, Ax, r, p);
+    return hipGetLastError();
+}
+
+hipError_t update_xr_ref_f32(int64_t n, float *x, float *r, const float *p, const float *Ap,
+                             const float *rsold, const float *pAp, hipStream_t s) {
+    hipLaunchKernelGGL(k_update_xr_ref_f32, dim3(grid_vec(n)), dim3(kNT), 0, s, n, x, r, p, Ap, rsold, pAp);
+    return hipGetLastError();
+}
+
+hipError_t update_p_ref_f32(int64_t n, float *p, const float *r, const float *rr, const float *rsold,
+                            hipStream_t s) {
+    hipLaunchKernelGGL(k_update_p_ref_f32, dim3(grid_vec(n)), dim3(kNT), 0, s, n, p, r, rr, rsold);
+    return hipGetLastError();
+}
+
+}  // namespace cgx

@@ -1,0 +1,180 @@
+/*
+ * cgx.h -- C ABI of the MI355X-native conjugate-gradient hot path (libcgx.so).
+ *
+ * This is the drop-in boundary for the reference's CG loop
+ * (mawunyega/conjugate_gradient).  The reference has no library API of its
+ * own: its solvers are self-contained C programs whose functions are
+ *
+ *   void  matVec(float *out, float *A, float *x [, int local_row]);
+ *         serialConjugate.c:109-120, parallel_cg.c:172-184
+ *   float vecVec(float *v1, float *v2 [, int local_row]);
+ *         serialConjugate.c:145-155, parallel_cg.c:211-221
+ *   void  residual(float *out, float *b, float *Ax [, int]);      :124-131
+ *   void  scalarVec / vecAdd / vecSub(...)                          :135-177
+ *   void  conjugrad(float *A, float *b, float *x
+ *                   [, int local_row, int rank, int P]);
+ *         serialConjugate.c:180-259, parallel_cg.c:248-345
+ *   MPI_Bcast / MPI_Scatter distribution        parallel_cg.c:109-117
+ *   MPI_Allgather(p) + 2x MPI_Allreduce(SUM)     parallel_cg.c:287-313
+ *
+ * and this header maps each of them to an entry point (see INTEGRATION.md for
+ * the function-by-function table and the ctypes / C bindings a maintainer
+ * adds).  Conventions:
+ *   - plain C types only: pointers, sizes, int status codes; nothing aborts;
+ *   - host arrays are caller-owned; device buffers, streams, events and RCCL
+ *     communicators are owned by the context;
+ *   - a context is not thread-safe; one host thread drives it;
+ *   - x is in/out exactly like conjugrad's vectorX (x0 in, solution out).
+ *
+ * Numerics (flags):
+ *   CGX_F64      (default) double data and arithmetic; the fp64 reading of
+ *                conjgrad.m.  Dots are deterministic fixed-order reductions.
+ *   CGX_F32_REF  float data, serialConjugate.c's operation order: sequential
+ *                fp32 accumulation per row and per dot, no FMA contraction.
+ *                Produces the reference's x bit for bit (single shard).
+ *
+ * Multi-GPU: the matrix is split into contiguous row blocks (parallel_cg.c:83,
+ * 97-99; n % nranks == 0 as parallel_cg.c:86-90 requires).  Per iteration
+ * the p vector is allgathered and the two scalars p.Ap and r.r are
+ * allreduced (RCCL over xGMI in rank mode; intra-process device copies for
+ * the multi-shard mode).  x stays distributed and is gathered on demand.
+ */
+#ifndef CGX_H
+#define CGX_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define CGX_VERSION 100 /* 0.1.0 */
+
+/* ---- status codes (0 = OK, negative = error) --------------------------- */
+#define CGX_OK            0
+#define CGX_ERR_ARG      -1  /* bad argument / unsupported combination        */
+#define CGX_ERR_HIP      -2  /* a HIP runtime call failed                      */
+#define CGX_ERR_RCCL     -3  /* an RCCL call failed                            */
+#define CGX_ERR_SHAPE    -4  /* n not divisible by ranks, rows out of range   */
+#define CGX_ERR_NOMEM    -5  /* device or pinned allocation failed            */
+#define CGX_ERR_STATE    -6  /* call out of order (iterate before begin, ...) */
+#define CGX_ERR_NODEV    -7  /* no usable GPU                                  */
+
+/* ---- flags ---------------------------------------------------------------- */
+#define CGX_F64          0x0   /* double data (default)                        */
+#define CGX_F32_REF      0x1   /* float data, bit-exact serialConjugate.c order */
+#define CGX_TIMING       0x100 /* time every matVec launch with HIP events      */
+
+typedef struct cgx_ctx cgx_ctx;
+
+/* Opaque RCCL bootstrap id (ncclUniqueId is 128 bytes). */
+typedef struct { char bytes[128]; } cgx_unique_id;
+
+typedef struct {
+    int64_t n;            /* global system size                               */
+    int64_t lda;          /* device leading dimension (n rounded up to 128)   */
+    int     nranks;       /* row blocks in the whole job                      */
+    int     nshards;      /* row blocks driven by this process                */
+    int     rank0;        /* global index of this process's first row block   */
+    int64_t row0;         /* first global row owned by this process           */
+    int64_t nrows;        /* rows owned by this process                       */
+    int     flags;
+    int     elem_bytes;   /* 8 (CGX_F64) or 4 (CGX_F32_REF)                   */
+} cgx_info;
+
+typedef struct {
+    int64_t iterations;    /* loop iterations of the last solve (k+1 at break) */
+    int     converged;     /* 1 if sqrt(r.r) < eps ended the loop              */
+    double  rr;            /* last r.r (global)                                */
+    double  solve_ms;      /* host wall time of the last cgx_solve             */
+    double  matvec_ms;     /* sum of timed matVec kernel durations (CGX_TIMING)*/
+    int64_t matvec_count;  /* matVec launches timed                            */
+    int64_t total_iterations; /* iterations since the context was created     */
+} cgx_stats;
+
+/* ---- errors / info ------------------------------------------------------- */
+const char *cgx_strerror(int code);
+/* Detail message of the last failure on this thread ("" if none). */
+const char *cgx_last_error(void);
+int cgx_version(void);
+int cgx_device_count(int *count);
+
+/* ---- context lifetime ------------------------------------------------------ */
+/* One GPU (device `device`).  Replaces serialConjugate.c's single process. */
+int cgx_create(cgx_ctx **ctx, int64_t n, int device, int flags);
+
+/* One process driving `nshards` row blocks on devices[0..nshards-1] (a device
+ * may repeat: several row blocks on one GPU).  Exchange by device copies. */
+int cgx_create_multi(cgx_ctx **ctx, int64_t n, int nshards, const int *devices, int flags);
+
+/* One process per GPU (parallel_cg.c's one MPI rank per process): this
+ * process owns row block `rank` of `nranks`; `id` comes from
+ * cgx_get_unique_id() on rank 0 and is broadcast by the caller.  Exchange by
+ * RCCL (allgather p, allreduce p.Ap and r.r) on the context's stream. */
+int cgx_get_unique_id(cgx_unique_id *id);
+int cgx_create_rank(cgx_ctx **ctx, int64_t n, int rank, int nranks,
+                    const cgx_unique_id *id, int device, int flags);
+
+int cgx_destroy(cgx_ctx *ctx);
+int cgx_get_info(const cgx_ctx *ctx, cgx_info *info);
+
+/* ---- data in / out (host arrays; element type per flags) ----------------- */
+/* Rows [row0, row0+nrows) of A (row-major, host leading dimension lda_host),
+ * of b and of x0.  Any pointer may be NULL.  Rows this process does not own
+ * are ignored, so every rank may pass the full system (MPI_Scatter /
+ * MPI_Bcast, parallel_cg.c:111-115) or only its own block.  */
+int cgx_set_rows(cgx_ctx *ctx, int64_t row0, int64_t nrows, const void *A_rows,
+                 int64_t lda_host, const void *b_rows, const void *x_rows);
+/* Whole system: A is n x n row-major, b and x0 have n entries. */
+int cgx_set_system(cgx_ctx *ctx, const void *A, const void *b, const void *x0);
+/* On-device synthetic SPD system (generateSPDmatrix.m style, counter hash):
+ *   A_ij = 0.5*(u(i,j)+u(j,i)) + n*[i==j],  b_i = u_b(i),  x0 = 0,
+ * u = splitmix64-finalised counter hash -> 53-bit uniform in [0,1). */
+int cgx_generate_spd(cgx_ctx *ctx, uint64_t seed);
+/* x (n entries, replicated result like parallel_cg.c's local_vectorX). */
+int cgx_get_x(cgx_ctx *ctx, void *x);
+int cgx_set_x(cgx_ctx *ctx, const void *x);
+
+/* ---- the solve (conjugrad) -------------------------------------------------- */
+/* x_inout may be NULL (use / leave the device-resident x).  eps < 0: never
+ * stop early; max_iter < 0: n (the reference's `k < ROWS`). */
+int cgx_solve(cgx_ctx *ctx, void *x_inout, double eps, int64_t max_iter, cgx_stats *st);
+/* The same solve in pieces: r0 = p0 = b - A x, then `count` iterations. */
+int cgx_solve_begin(cgx_ctx *ctx);
+int cgx_iterate(cgx_ctx *ctx, int64_t count, double eps, int64_t *done, int *converged);
+int cgx_get_stats(cgx_ctx *ctx, cgx_stats *st);
+int cgx_reset_timing(cgx_ctx *ctx);
+int cgx_synchronize(cgx_ctx *ctx);
+/* The context's HIP stream of its first shard (hipStream_t as void*). */
+void *cgx_stream(cgx_ctx *ctx);
+/* True residual of the current x: *rnorm = ||b - A x||_2, *bnorm = ||b||_2
+ * (either may be NULL).  Overwrites r and p: ends a solve in progress. */
+int cgx_residual_norm(cgx_ctx *ctx, double *rnorm, double *bnorm);
+
+/* ---- kernel-level entry points (device pointers; unit parity) -------------- */
+/* dtype: CGX_F64 or CGX_F32_REF.  stream: hipStream_t or NULL. */
+int cgx_dev_malloc(void **ptr, size_t bytes);
+int cgx_dev_free(void *ptr);
+int cgx_memcpy_h2d(void *dst, const void *src, size_t bytes);
+int cgx_memcpy_d2h(void *dst, const void *src, size_t bytes);
+int cgx_dev_synchronize(void);
+/* matVec: out[i] = sum_j A[i*lda + j] * v[j], i < rows, j < cols. */
+int cgx_matvec(int dtype, const void *A, int64_t lda, int64_t rows, int64_t cols,
+               const void *v, void *out, void *stream);
+/* vecVec: *out_dev = a . b */
+int cgx_dot(int dtype, int64_t n, const void *a, const void *b, void *out_dev, void *stream);
+/* residual x2 + vecVec: r = b - Ax; p = b - Ax; *rr_dev = r.r (rr_dev may be NULL) */
+int cgx_residual(int dtype, int64_t n, const void *b, const void *Ax, void *r, void *p,
+                 void *rr_dev, void *stream);
+/* alpha = *rsold_dev / *pAp_dev; x += alpha p; r -= alpha Ap; *rr_dev = r.r */
+int cgx_update_xr(int dtype, int64_t n, void *x, void *r, const void *p, const void *Ap,
+                  const void *rsold_dev, const void *pAp_dev, void *rr_dev, void *stream);
+/* p = r + (*rr_dev / *rsold_dev) p */
+int cgx_update_p(int dtype, int64_t n, void *p, const void *r, const void *rr_dev,
+                 const void *rsold_dev, void *stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* CGX_H */

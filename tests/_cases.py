@@ -1,0 +1,58 @@
+"""Inputs of the golden cases (tests/golden/golden.json).
+
+kat* come from the reference's own text fixtures (copied data under
+tests/golden/ref_fixtures/); spd<n> are generateSPDmatrix(n) inputs regenerated
+by the oracle's MATLAB-compatible generator.  Reading the fixtures with a
+plain tokenizer here keeps the expected inputs independent of the product's
+text reader (which is tested against these same files)."""
+from __future__ import annotations
+
+import functools
+import os
+import re
+
+import numpy as np
+
+import oracle
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+GOLDEN = os.path.join(HERE, "golden")
+FIX = os.path.join(GOLDEN, "ref_fixtures")
+_NUM = re.compile(rb"[-+]?(?:\d+\.?\d*|\.\d+)(?:[eE][-+]?\d+)?")
+
+
+def numbers(name: str, count: int, dtype=np.float32) -> np.ndarray:
+    with open(os.path.join(FIX, name), "rb") as f:
+        toks = _NUM.findall(f.read())[:count]
+    assert len(toks) == count, name
+    return np.array([float(t) for t in toks], dtype=dtype)
+
+
+@functools.lru_cache(maxsize=4)
+def _spd(n: int, dt: str):
+    return oracle.spd_matlab(n, np.dtype(dt))
+
+
+def case(name: str, dtype=np.float32):
+    """(A, b, x0) of a golden case in `dtype` (values as the reference reads them)."""
+    dt = np.dtype(dtype)
+    if name == "kat2":
+        return numbers("matrixA.txt", 4, dt).reshape(2, 2), numbers("vectorb.txt", 2, dt), numbers("initialguess.txt", 2, dt)
+    if name == "kat2_x0":
+        return numbers("matrixA.txt", 4, dt).reshape(2, 2), numbers("vectorb.txt", 2, dt), numbers("initialguess1.txt", 2, dt)
+    if name == "kat4":
+        return numbers("matrixA1.txt", 16, dt).reshape(4, 4), numbers("vectorb1.txt", 4, dt), numbers("X0.txt", 4, dt)
+    if name.startswith("spd"):
+        n = int(name[3:])
+        A, b = _spd(n, dt.str)
+        return A, b, np.zeros(n, dt)
+    raise KeyError(name)
+
+
+def golden_x(golden: dict, name: str) -> np.ndarray:
+    return np.load(os.path.join(GOLDEN, golden["cases"][name]["x_file"]), allow_pickle=False)
+
+
+KATS = ["kat2", "kat2_x0", "kat4"]
+SPD_SMALL = ["spd512", "spd1024", "spd2048"]
+SPD_ALL = ["spd512", "spd1024", "spd2048", "spd4096", "spd8192"]

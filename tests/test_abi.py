@@ -1,0 +1,137 @@
+"""The C-ABI boundary (include/*.h -> lib/libcgx.so) and the host-side pieces
+that need no GPU: symbol exports, error reporting, the text reader, the CLI's
+argument / file handling."""
+import os
+import re
+import subprocess
+
+import numpy as np
+import pytest
+
+import conjugate_gradient_amd as cg
+from _cases import FIX, numbers
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+HEADERS = [os.path.join(ROOT, "include", h) for h in ("cgx.h", "cgx_textio.h")]
+
+
+def declared_functions(path):
+    src = open(path).read()
+    src = re.sub(r"/\*.*?\*/", "", src, flags=re.S)
+    return sorted(set(re.findall(r"^\s*(?:const\s+)?[A-Za-z_][\w\s\*]*?\b(cgx_\w+)\s*\(", src, flags=re.M)))
+
+
+def test_every_declared_symbol_exported(built):
+    out = subprocess.run(["nm", "-D", "--defined-only", cg.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    exported = set(re.findall(r"\sT\s(cgx_\w+)$", out, flags=re.M))
+    declared = [f for h in HEADERS for f in declared_functions(h)]
+    assert len(declared) >= 35
+    missing = [f for f in declared if f not in exported]
+    assert not missing, missing
+    L = cg.lib()
+    for f in declared:
+        assert hasattr(L, f)
+
+
+def test_library_links_hip_and_rccl(built):
+    out = subprocess.run(["readelf", "-d", cg.LIB_PATH], capture_output=True, text=True, check=True).stdout
+    assert "libamdhip64.so" in out and "librccl.so" in out
+
+
+def test_gfx950_code_object(built):
+    # the HIP kernels are compiled for gfx950 (offload bundle inside the .so)
+    data = open(cg.LIB_PATH, "rb").read()
+    assert b"gfx950" in data
+    assert b"k_matvec_f64" in data and b"k_matvec_ref_f32" in data
+
+
+def test_errors_and_version(built):
+    L = cg.lib()
+    assert L.cgx_version() == 100
+    assert L.cgx_strerror(0) == b"ok"
+    for code in (-1, -2, -3, -4, -5, -6, -7):
+        assert L.cgx_strerror(code) not in (b"ok", b"unknown error")
+    assert L.cgx_strerror(-99) == b"unknown error"
+
+
+def test_no_gpu_fails_loudly(built):
+    if cg.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    with pytest.raises(cg.CgxError) as ei:
+        cg.Solver(4)
+    assert ei.value.code == -7 and "no HIP device" in str(ei.value)
+
+
+def test_bad_shape_rejected_before_device(built):
+    # n % P != 0 (parallel_cg.c:86-90) is a shape error whatever the devices
+    with pytest.raises(cg.CgxError) as ei:
+        cg.Solver(10, devices=[0, 0, 0])
+    assert ei.value.code == -4 and "not divisible" in str(ei.value)
+
+
+def test_text_reader_reference_fixtures(built):
+    A = cg.read_text(os.path.join(FIX, "matrixA1.txt"), 16, np.float32)
+    assert np.array_equal(A, numbers("matrixA1.txt", 16))
+    assert cg.count_text(os.path.join(FIX, "vectorb.txt")) == 2
+    assert cg.read_dims(os.path.join(FIX, "dimensions.txt")) == (2, 2, 2, 1)
+    # initialguess1.txt ends in a stray UTF-8 BOM: the two values still read
+    x = cg.read_text(os.path.join(FIX, "initialguess1.txt"), 2, np.float64)
+    assert np.array_equal(x, [1.0, 0.0])
+    assert cg.count_text(os.path.join(FIX, "initialguess1.txt")) == 2
+
+
+def test_text_reader_errors(built, tmp_path):
+    with pytest.raises(FileNotFoundError):
+        cg.read_text(str(tmp_path / "missing.txt"), 2)
+    p = tmp_path / "short.txt"
+    p.write_text("1.0\n2.0\n")
+    with pytest.raises(ValueError, match="fewer"):
+        cg.read_text(str(p), 3)
+    p.write_text("1.0\nabc\n")
+    with pytest.raises(ValueError, match="malformed"):
+        cg.read_text(str(p), 2)
+
+
+def test_text_reader_parallel_equals_serial(built, tmp_path):
+    rng = np.random.default_rng(1)
+    vals = rng.random(50000) * 1e3 - 500
+    p = tmp_path / "big.txt"
+    p.write_text("\n".join(f"{v:.4f}" for v in vals) + "\n")
+    one = cg.read_text(str(p), vals.size, np.float32, threads=1)
+    many = cg.read_text(str(p), vals.size, np.float32, threads=7)
+    assert np.array_equal(one, many)
+    # strtof of the "%.4f" text, as fscanf("%f") does (serialConjugate.c:96)
+    assert np.array_equal(one, np.array([np.float32(f"{v:.4f}") for v in vals]))
+    d = cg.read_text(str(p), vals.size, np.float64, threads=5)
+    assert np.array_equal(d, np.array([float(f"{v:.4f}") for v in vals]))
+
+
+def run_cli(*args):
+    return subprocess.run([cg.CLI_PATH, *args], capture_output=True, text=True, timeout=120)
+
+
+def test_cli_argument_count(built):
+    r = run_cli()
+    assert r.returncode == 1
+    assert "serialCongugate.c requires four (4) files" in r.stdout  # serialConjugate.c:50
+
+
+def test_cli_missing_file(built, tmp_path):
+    r = run_cli(str(tmp_path / "nope.txt"), os.path.join(FIX, "vectorb.txt"), os.path.join(FIX, "initialguess.txt"))
+    assert r.returncode == 1
+    assert "Computing cg of matrix size : 4" in r.stdout
+    assert "Could not open file" in r.stdout  # serialConjugate.c:103
+
+
+def test_cli_not_divisible(built):
+    f = [os.path.join(FIX, n) for n in ("matrixA1.txt", "vectorb1.txt", "X0.txt")]
+    r = run_cli("--gpus", "3", *f)
+    assert r.returncode == 1 and "4 is not divisible by 3" in r.stdout  # parallel_cg.c:88
+
+
+def test_cli_dims_file(built, tmp_path):
+    d = tmp_path / "dims.txt"
+    d.write_text("3\n2\n3\n1\n")
+    f = [os.path.join(FIX, n) for n in ("matrixA.txt", "vectorb.txt", "initialguess.txt")]
+    r = run_cli("--dims", str(d), *f)
+    assert r.returncode == 1 and "3 and 2 must be same size" in r.stdout  # serialConjugate.c:55

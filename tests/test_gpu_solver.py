@@ -1,0 +1,199 @@
+"""Solver-level parity on the GPU (conjugrad through the C ABI).
+
+Pins:
+  1. CGX_F32_REF x == serialConjugate.c x bit for bit, same loop count
+     (golden vectors from the unmodified reference, tests/golden/);
+  2. CGX_F64 x vs the fp64 oracle: ||dx||/||x|| <= 1e-10, ||b-Ax||/||b|| <= 1e-10,
+     loop count == conjgrad.m's (tol 1e-10);
+  3. CGX_F64 x vs the reference's fp32 x: ||dx||/||x|| <= 1e-5;
+  4. KATs: 2x2 -> [2/3, 1/3], 4x4 -> [-1, 1, -1, 1] to 1e-12.
+Multi-shard runs (several row blocks on this GPU, the parallel_cg.c split)
+must give the oracle's row-block results: bit-exact in F32_REF against the
+point-to-point_cg.c dot order, 1e-10 in F64."""
+import numpy as np
+import pytest
+
+import conjugate_gradient_amd as cg
+import oracle
+from _cases import KATS, SPD_ALL, SPD_SMALL, case, golden_x
+
+pytestmark = pytest.mark.gpu
+TOL = 1e-10
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu(built):
+    assert cg.device_count() >= 1, "no GPU visible: the HIP path must run"
+
+
+def rel(a, b):
+    return np.linalg.norm(np.asarray(a, np.float64) - b) / np.linalg.norm(b)
+
+
+@pytest.mark.parametrize("name", KATS + SPD_ALL)
+def test_f32ref_bit_exact_vs_reference(golden, name):
+    A, b, x0 = case(name)
+    x = x0.copy()
+    st = cg.conjugrad(A, b, x, eps=1e-6)
+    ref = golden_x(golden, name)
+    assert st.iterations == golden["cases"][name]["ref_iterations"]
+    assert st.converged == 1
+    assert np.array_equal(x.view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.parametrize("name", KATS + SPD_ALL)
+def test_f64_parity(golden, name):
+    A, b, x0 = case(name, np.float64)
+    x = x0.copy()
+    st = cg.conjugrad(A, b, x, eps=1e-10)
+    xo, so = oracle.cg_f64(A, b, x0, eps=1e-10)
+    assert st.iterations == so.iterations == golden["cases"][name]["conjgrad_m_f64_iterations"]
+    assert rel(x, xo) <= TOL
+    assert np.linalg.norm(b - A @ x) <= TOL * np.linalg.norm(b)
+    assert rel(golden_x(golden, name), x) <= 1e-5
+
+
+def test_known_answers():
+    A, b, x0 = case("kat2", np.float64)
+    x = x0.copy()
+    cg.conjugrad(A, b, x, eps=1e-10)
+    assert np.allclose(x, [2 / 3, 1 / 3], rtol=0, atol=1e-12)
+    A, b, x0 = case("kat4", np.float64)
+    x = x0.copy()
+    cg.conjugrad(A, b, x, eps=1e-10)
+    assert np.allclose(x, [-1, 1, -1, 1], rtol=0, atol=1e-12)
+
+
+@pytest.mark.parametrize("P", [2, 4])
+@pytest.mark.parametrize("name", ["kat4", "spd512", "spd2048"])
+def test_row_block_shards_f32ref(name, P):
+    """P row blocks on this GPU == oracle with P-part dots (point-to-point_cg.c order)."""
+    A, b, x0 = case(name)
+    if b.size % P:
+        pytest.skip("n not divisible")
+    x = x0.copy()
+    st = cg.conjugrad(A, b, x, eps=1e-6, shards=[0] * P)
+    xo, so = oracle.cg_f32ref(A, b, x0, eps=1e-6, nparts=P)
+    assert st.iterations == so.iterations
+    assert np.array_equal(x.view(np.uint32), xo.view(np.uint32))
+
+
+@pytest.mark.parametrize("P", [2, 4, 8])
+@pytest.mark.parametrize("name", ["kat4", "spd1024", "spd4096"])
+def test_row_block_shards_f64(golden, name, P):
+    A, b, x0 = case(name, np.float64)
+    if b.size % P:
+        pytest.skip("n not divisible")
+    x = x0.copy()
+    st = cg.conjugrad(A, b, x, eps=1e-10, shards=[0] * P)
+    xo, so = oracle.cg_f64(A, b, x0, eps=1e-10)
+    assert st.iterations == so.iterations
+    assert rel(x, xo) <= TOL
+
+
+def test_rccl_rank_mode_world1():
+    """The one-process-per-GPU path (RCCL allgather/allreduce) at world size 1."""
+    A, b, x0 = case("spd1024", np.float64)
+    uid = cg.get_unique_id()
+    with cg.Solver(b.size, rank=0, nranks=1, unique_id=uid, device=0) as s:
+        s.set_system(A, b, x0)
+        x, st = s.solve(None, eps=1e-10)
+    xo, so = oracle.cg_f64(A, b, x0, eps=1e-10)
+    assert st.iterations == so.iterations and rel(x, xo) <= TOL
+    with cg.Solver(b.size, rank=0, nranks=1, unique_id=cg.get_unique_id(), flags=cg.CGX_F32_REF) as s:
+        A32, b32, x032 = case("spd1024")
+        s.set_system(A32, b32, x032)
+        x32, st32 = s.solve(None, eps=1e-6)
+    ref, _ = oracle.cg_f32ref(A32, b32, x032)
+    assert np.array_equal(x32, ref)
+
+
+def test_set_rows_partial_and_generator_rows():
+    """cgx_set_rows with each shard's own block only (MPI_Scatter)."""
+    A, b, x0 = case("spd2048", np.float64)
+    P = 4
+    with cg.Solver(b.size, devices=[0] * P) as s:
+        loc = b.size // P
+        for q in range(P):
+            sl = slice(q * loc, (q + 1) * loc)
+            s.set_rows(q * loc, A[sl], b[sl], x0[sl])
+        x, st = s.solve(None, eps=1e-10)
+    xo, _ = oracle.cg_f64(A, b, x0, eps=1e-10)
+    assert rel(x, xo) <= TOL
+
+
+@pytest.mark.parametrize("n,shards", [(1000, None), (2048, [0, 0]), (4096, [0] * 4)])
+def test_device_generator_matches_oracle(n, shards):
+    """cgx_generate_spd == oracle_spd_hash: identical A, b give identical solves."""
+    with cg.Solver(n, devices=shards) as s:
+        s.generate_spd(seed=42)
+        x, st = s.solve(None, eps=1e-10)
+        rn, bn = s.residual_norm()
+    A, b = oracle.spd_hash(n, seed=42)
+    xo, so = oracle.cg_f64(A, b, np.zeros(n), eps=1e-10)
+    assert st.iterations == so.iterations
+    assert rel(x, xo) <= 1e-12
+    assert abs(bn - np.linalg.norm(b)) <= 1e-14 * np.linalg.norm(b)
+    assert rn <= TOL * bn
+    with cg.Solver(n, flags=cg.CGX_F32_REF, devices=shards) as s:
+        s.generate_spd(seed=42)
+        x32, st32 = s.solve(None, eps=1e-6)
+    A32, b32 = oracle.spd_hash(n, seed=42, dtype=np.float32)
+    xo32, _ = oracle.cg_f32ref(A32, b32, np.zeros(n, np.float32), nparts=len(shards) if shards else 1)
+    assert np.array_equal(x32, xo32)
+
+
+def test_n16384_against_cpu_oracle():
+    """configs[1]: N=16384 dense SPD fp64 on one GPU vs the CPU fp64 oracle."""
+    n = 16384
+    with cg.Solver(n) as s:
+        s.generate_spd(seed=42)
+        x, st = s.solve(None, eps=1e-10)
+        rn, bn = s.residual_norm()
+    oracle.set_threads(16)
+    A, b = oracle.spd_hash(n, seed=42)
+    xo, so = oracle.cg_f64(A, b, np.zeros(n), eps=1e-10)
+    del A
+    assert st.iterations == so.iterations
+    assert rel(x, xo) <= TOL
+    assert rn <= TOL * bn
+
+
+def test_solve_in_pieces_and_fixed_count():
+    """cgx_solve_begin + cgx_iterate == cgx_solve; eps < 0 runs exactly max_iter."""
+    A, b, x0 = case("spd1024", np.float64)
+    with cg.Solver(b.size) as s:
+        s.set_system(A, b, x0)
+        x_full, st = s.solve(None, eps=1e-10)
+        s.set_x(x0)
+        s.begin()
+        total = 0
+        while True:
+            done, conv = s.iterate(2, eps=1e-10)
+            total += done
+            if conv or done == 0:
+                break
+        assert total == st.iterations
+        assert np.array_equal(s.get_x(), x_full)
+        s.set_x(x0)
+        _, st2 = s.solve(None, eps=-1.0, max_iter=9)
+        assert st2.iterations == 9 and st2.converged == 0
+
+
+def test_timing_events_count():
+    n = 4096
+    with cg.Solver(n, flags=cg.CGX_F64 | cg.CGX_TIMING) as s:
+        s.generate_spd(1)
+        s.solve(None, eps=-1.0, max_iter=5)
+        st = s.stats()
+    assert st.matvec_count == 6  # initial residual + 5 iterations
+    assert st.matvec_ms > 0
+
+
+def test_errors_are_reported():
+    with cg.Solver(8) as s:
+        with pytest.raises(cg.CgxError) as ei:
+            s.iterate(1)
+        assert ei.value.code == -6
+    with pytest.raises(cg.CgxError):
+        cg.Solver(8, device=99)
