@@ -161,6 +161,7 @@ def main(argv=None) -> int:
     else:
         solver = cg.Solver(n, device=0, flags=flags)
     nloc = solver.info.nrows
+    plan = solver.matvec_plan()
 
     solver.generate_spd(SEED)
     solver.begin()
@@ -234,6 +235,7 @@ def main(argv=None) -> int:
             "frac": achieved / HBM_PEAK_GBS,
             "traffic": traffic,
             "kernel": "k_matvec_f64",
+            "plan": plan,
             "algorithmic_bytes_per_launch": bytes_launch,
         },
         "check": {"relres": rnorm / bnorm},

@@ -119,6 +119,9 @@ def lib() -> ctypes.CDLL:
         "cgx_synchronize": ([vp], i32),
         "cgx_stream": ([vp], vp),
         "cgx_residual_norm": ([vp, ctypes.POINTER(f64), ctypes.POINTER(f64)], i32),
+        "cgx_set_matvec_plan": ([vp, i32, i32, i32, i32], i32),
+        "cgx_get_matvec_plan": ([vp, ctypes.POINTER(i32), ctypes.POINTER(i32), ctypes.POINTER(i32),
+                                 ctypes.POINTER(i32)], i32),
         "cgx_dev_malloc": ([ctypes.POINTER(vp), sz], i32),
         "cgx_dev_free": ([vp], i32),
         "cgx_memcpy_h2d": ([vp, vp, sz], i32),
@@ -381,6 +384,16 @@ class Solver:
         rn, bn = ctypes.c_double(), ctypes.c_double()
         _check(lib().cgx_residual_norm(self._h, ctypes.byref(rn), ctypes.byref(bn)), "cgx_residual_norm")
         return rn.value, bn.value
+
+    def set_matvec_plan(self, rows_per_wave: int, chunks_in_flight: int, nontemporal: int = 1,
+                        blocks_per_cu: int = 0) -> None:
+        _check(lib().cgx_set_matvec_plan(self._h, rows_per_wave, chunks_in_flight, nontemporal, blocks_per_cu),
+               "cgx_set_matvec_plan")
+
+    def matvec_plan(self) -> dict:
+        v = [ctypes.c_int() for _ in range(4)]
+        _check(lib().cgx_get_matvec_plan(self._h, *(ctypes.byref(x) for x in v)), "cgx_get_matvec_plan")
+        return dict(zip(("R", "U", "nt", "blocks"), (x.value for x in v)))
 
     def reset_timing(self) -> None:
         _check(lib().cgx_reset_timing(self._h), "cgx_reset_timing")

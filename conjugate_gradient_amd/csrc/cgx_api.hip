@@ -782,6 +782,30 @@ int cgx_synchronize(cgx_ctx *c) {
 
 void *cgx_stream(cgx_ctx *c) { return c ? (void *)c->sh[0].stream : nullptr; }
 
+int cgx_set_matvec_plan(cgx_ctx *c, int rows_per_wave, int chunks_in_flight, int nontemporal, int blocks_per_cu) {
+    if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
+    if (f32ref(c)) return fail(CGX_ERR_ARG, "the fp32-ref matVec has no tunable plan");
+    const int R = rows_per_wave, U = chunks_in_flight;
+    if (R != 1 && R != 2 && R != 4 && R != 8) return fail(CGX_ERR_ARG, "rows_per_wave must be 1, 2, 4 or 8");
+    if (U != 2 && U != 4 && U != 8) return fail(CGX_ERR_ARG, "chunks_in_flight must be 2, 4 or 8");
+    for (auto &s : c->sh) {
+        TRY(set_dev(s));
+        MatvecPlan pl = plan_matvec_f64(s.dev, s.nloc, R, U, nontemporal ? 1 : 0, blocks_per_cu);
+        s.plan = pl;
+    }
+    return CGX_OK;
+}
+
+int cgx_get_matvec_plan(cgx_ctx *c, int *rows_per_wave, int *chunks_in_flight, int *nontemporal, int *blocks) {
+    if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
+    const MatvecPlan &pl = c->sh[0].plan;
+    if (rows_per_wave) *rows_per_wave = pl.R;
+    if (chunks_in_flight) *chunks_in_flight = pl.U;
+    if (nontemporal) *nontemporal = pl.nt;
+    if (blocks) *blocks = pl.blocks;
+    return CGX_OK;
+}
+
 int cgx_residual_norm(cgx_ctx *c, double *rnorm, double *bnorm) {
     if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
     // ||b - A x|| with the current x: allgather x, matVec, residual, two dots.

@@ -22,7 +22,9 @@ struct MatvecPlan {
     int nt = 1;       // non-temporal loads of A
     int blocks = 0;   // grid (256-thread blocks), grid-stride over row groups
 };
-MatvecPlan plan_matvec_f64(int device, int64_t rows);
+// R/U/nt/blocks_per_cu <= 0 pick the defaults (env CGX_MV_* may override).
+MatvecPlan plan_matvec_f64(int device, int64_t rows, int R = 0, int U = 0, int nt = -1,
+                           int blocks_per_cu = 0);
 
 // ---- fp64 -------------------------------------------------------------------
 // out[i] = sum_j A[i*lda+j] v[j]; if pown != nullptr also *dot_out = pown . out

@@ -424,19 +424,26 @@ MvFn pick_mv(int R, int U, int nt) {
 
 }  // namespace
 
-MatvecPlan plan_matvec_f64(int device, int64_t rows) {
+MatvecPlan plan_matvec_f64(int device, int64_t rows, int R, int U, int nt, int blocks_per_cu) {
     MatvecPlan pl;
     const int cus = cu_count(device);
-    // Rows per wave: enough row groups to give every CU >= 8 waves.
-    const int64_t want_waves = (int64_t)cus * 8;
-    if (rows >= 4 * want_waves) pl.R = 4;
+    // Rows per wave: the most rows that still leave >= 4 row groups (waves)
+    // per CU.  Measured on MI355X (profiles/r01_sweep_*): with nt loads R=8,
+    // U=8 is best or within 1% of best from 8192 to 65536 rows (7.0-7.06 TB/s);
+    // default-policy loads are 11% slower (6.2-6.3 TB/s).
+    const int64_t want_waves = (int64_t)cus * 4;
+    if (rows >= 8 * want_waves) pl.R = 8;
+    else if (rows >= 4 * want_waves) pl.R = 4;
     else if (rows >= 2 * want_waves) pl.R = 2;
     else pl.R = 1;
-    pl.U = (pl.R == 1) ? 8 : 4;
+    pl.U = 8;
     pl.nt = 1;
     pl.R = env_int("CGX_MV_R", pl.R);
     pl.U = env_int("CGX_MV_U", pl.U);
     pl.nt = env_int("CGX_MV_NT", pl.nt);
+    if (R > 0) pl.R = R;
+    if (U > 0) pl.U = U;
+    if (nt >= 0) pl.nt = nt;
     if (pl.R != 1 && pl.R != 2 && pl.R != 4 && pl.R != 8) pl.R = 4;
     if (pl.U != 2 && pl.U != 4 && pl.U != 8) pl.U = 4;
     int per_cu = 0;
@@ -444,6 +451,7 @@ MatvecPlan plan_matvec_f64(int device, int64_t rows) {
                                                      kNT, 0) != hipSuccess || per_cu <= 0)
         per_cu = 2;
     per_cu = env_int("CGX_MV_BLOCKS_PER_CU", per_cu);
+    if (blocks_per_cu > 0) per_cu = blocks_per_cu;
     const int64_t groups = (rows + pl.R - 1) / pl.R;
     const int64_t need = (groups + (kNT / 64) - 1) / (kNT / 64);
     int64_t cap = (int64_t)per_cu * cus;

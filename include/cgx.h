@@ -148,6 +148,14 @@ int cgx_reset_timing(cgx_ctx *ctx);
 int cgx_synchronize(cgx_ctx *ctx);
 /* The context's HIP stream of its first shard (hipStream_t as void*). */
 void *cgx_stream(cgx_ctx *ctx);
+/* Tuning of the fp64 matVec (k_matvec_f64): rows per wave (1,2,4,8), 128-column
+ * chunks in flight per row (2,4,8), non-temporal A loads (0/1), resident
+ * blocks per CU for the grid (<= 0: occupancy query).  Results do not depend
+ * on the plan's R/U/nt; the p.Ap partial order depends on the grid size. */
+int cgx_set_matvec_plan(cgx_ctx *ctx, int rows_per_wave, int chunks_in_flight, int nontemporal,
+                        int blocks_per_cu);
+int cgx_get_matvec_plan(cgx_ctx *ctx, int *rows_per_wave, int *chunks_in_flight, int *nontemporal,
+                        int *blocks);
 /* True residual of the current x: *rnorm = ||b - A x||_2, *bnorm = ||b||_2
  * (either may be NULL).  Overwrites r and p: ends a solve in progress. */
 int cgx_residual_norm(cgx_ctx *ctx, double *rnorm, double *bnorm);

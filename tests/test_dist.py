@@ -1,0 +1,64 @@
+"""bench.py's multi-process control plane on CPU (gloo, world size 2):
+rendezvous on 127.0.0.1, broadcast of the 128-byte RCCL id (which contains
+NULs), max-over-ranks of the timings, and the row-block arithmetic each rank
+derives (parallel_cg.c:83 local_row = ROWS / procsnum)."""
+import os
+import socket
+
+import pytest
+import torch.multiprocessing as mp
+
+import bench
+
+
+def _free_port():
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    return port
+
+
+def _worker(rank, world, port, q):
+    os.environ.update({"RANK": str(rank), "LOCAL_RANK": str(rank), "WORLD_SIZE": str(world),
+                       "MASTER_ADDR": "127.0.0.1", "MASTER_PORT": str(port)})
+    try:
+        assert bench.launched_by_torchrun()
+        r, lr, w = bench.dist_env()
+        dist = bench.dist_init()
+        payload = bytes(range(128)) if r == 0 else None  # byte 0 is NUL
+        got = bench.bcast_bytes(dist, payload)
+        mx = bench.max_over_ranks(dist, float(r + 1) * 1.5)
+        sm = bench.sum_over_ranks(dist, 1.0)
+        n = 65536
+        nloc = n // w
+        q.put((r, got == bytes(range(128)), mx, sm, bench.matvec_bytes(n, nloc)))
+        dist.barrier()
+        dist.destroy_process_group()
+    except Exception as e:  # pragma: no cover - reported to the parent
+        q.put((rank, repr(e)))
+
+
+@pytest.mark.timeout(120)
+def test_gloo_world2_control_plane():
+    world = 2
+    port = _free_port()
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    procs = [ctx.Process(target=_worker, args=(r, world, port, q)) for r in range(world)]
+    for p in procs:
+        p.start()
+    res = sorted(q.get(timeout=100) for _ in range(world))
+    for p in procs:
+        p.join(timeout=30)
+    for r in res:
+        assert len(r) == 5, r
+        rank, ok, mx, sm, mvb = r
+        assert ok and mx == 3.0 and sm == 2.0
+        assert mvb == 8 * 32768 * 65536 + 8 * 65536 + 8 * 32768
+
+
+def test_matvec_bytes_formula():
+    # 34.36 GB on 1 GPU, 4.295 GB per GPU on 8 at N = 65536
+    assert abs(bench.matvec_bytes(65536, 65536) / 1e9 - 34.36) < 0.01
+    assert abs(bench.matvec_bytes(65536, 8192) / 1e9 - 4.295) < 0.001
