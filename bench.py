@@ -27,7 +27,7 @@ HBM bytes per launch from rocprofv3 PMC counters (profiles/pmc_summary.json,
 FETCH_SIZE doubled per the gfx950 correction) when a summary for this
 workload exists, else null.  `cpu_baseline` times the oracle's fp32-ref
 restatement of serialConjugate.c (bit-identical to it, tests/test_oracle.py)
-on one host core, on a bounded sample: one iteration of the same system.
+on one host core, on a bounded sample: 5 iterations of the same system (~10 s).
 """
 from __future__ import annotations
 
@@ -103,14 +103,14 @@ def pmc_traffic(n: int, nranks: int) -> float | None:
         return None
 
 
-def cpu_baseline(n: int, threads_gen: int = 16) -> dict:
-    """Oracle fp32-ref restatement of serialConjugate.c, 1 host core, 1 iteration."""
+def cpu_baseline(n: int, iters: int = 5, threads_gen: int = 16) -> dict:
+    """Oracle fp32-ref restatement of serialConjugate.c, 1 host core, `iters` iterations."""
     import numpy as np
 
     import oracle
     oracle.set_threads(threads_gen)  # generation only; the timed solve is single-threaded
     A, b = oracle.spd_hash(n, seed=SEED, dtype=np.float32)
-    _, st = oracle.cg_f32ref(A, b, np.zeros(n, np.float32), max_iter=1, eps=-1.0)
+    _, st = oracle.cg_f32ref(A, b, np.zeros(n, np.float32), max_iter=iters, eps=-1.0)
     del A
     cpu = platform.processor() or platform.machine()
     try:
@@ -122,15 +122,15 @@ def cpu_baseline(n: int, threads_gen: int = 16) -> dict:
     except OSError:
         pass
     return {
-        "value": 1.0 / st.t_loop_s,
+        "value": iters / st.t_loop_s,
         "unit": "iterations/s",
         "cores": 1,
         "kind": "port",
-        "sample": (f"1 CG iteration (matVec + 2 dots + 3 vector updates) of the same N={n} system in fp32, "
+        "sample": (f"{iters} CG iterations (matVec + 2 dots + 3 vector updates each) of the same N={n} system in fp32, "
                    f"oracle/cg_oracle.c restatement of serialConjugate.c (bit-identical to it), single thread; "
                    f"initial residual matVec excluded; loop {st.t_loop_s:.2f} s, init {st.t_init_s:.2f} s; "
                    f"host CPU: {cpu}, {os.cpu_count()} logical CPUs visible"),
-        "matvec_gbps_est": 4.0 * n * n / st.t_loop_s / 1e9,
+        "matvec_gbps_est": iters * 4.0 * n * n / st.t_loop_s / 1e9,
     }
 
 
