@@ -43,6 +43,7 @@ sys.path.insert(0, ROOT)
 
 METRIC = "CG iterations/sec + matVec HBM GB/s, N×N dense SPD fp64, 1/2/4/8 MI355X"
 HBM_PEAK_GBS = 8000.0  # MI355X HBM3E peak (MI355X_MICROARCH.md, Chip-level parameters)
+H2D_PEAK_GBS = 63.0    # PCIe Gen5 x16 host link per GPU (same table, spec)
 SEED = 42
 
 
@@ -139,7 +140,10 @@ def main(argv=None) -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--n", type=int, default=65536)
+    ap.add_argument("--workload", choices=["dense", "stream"], default="dense",
+                    help="dense: configs[2], A resident in HBM (default); "
+                         "stream: configs[3], A kept in pinned host memory and streamed every matVec")
+    ap.add_argument("--n", type=int, default=None, help="system size (default 65536 dense, 131072 stream)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-n", type=int, default=None, help="N for the CPU baseline (default: --n)")
     args = ap.parse_args(argv)
@@ -151,10 +155,11 @@ def main(argv=None) -> int:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
 
     import conjugate_gradient_amd as cg
-    n = args.n
+    stream = args.workload == "stream"
+    n = args.n or (131072 if stream else 65536)
     if n % world:
         raise SystemExit(f"{n} is not divisible by {world}")
-    flags = cg.CGX_F64 | cg.CGX_TIMING
+    flags = cg.CGX_F64 | cg.CGX_TIMING | (cg.CGX_HOST_STREAM if stream else 0)
     if use_dist:
         uid = bcast_bytes(dist, cg.get_unique_id() if rank == 0 else None)
         solver = cg.Solver(n, rank=rank, nranks=world, unique_id=uid, device=local_rank, flags=flags)
@@ -201,7 +206,8 @@ def main(argv=None) -> int:
 
     bytes_launch = matvec_bytes(n, nloc)
     achieved = bytes_launch / (mv_ms * 1e-3) / 1e9
-    traffic = pmc_traffic(n, world)
+    traffic = None if stream else pmc_traffic(n, world)
+    peak = H2D_PEAK_GBS if stream else HBM_PEAK_GBS
     iters_per_s = args.steps / elapsed
     out = {
         "metric": METRIC,
@@ -218,7 +224,9 @@ def main(argv=None) -> int:
         "data": f"synthetic: generateSPDmatrix.m-style dense SPD (0.5(R+R')+nI, counter hash, seed {SEED}) "
                 f"generated on device; x0 = 0",
         "config": {
-            "workload": f"configs[2]: N={n} dense SPD fp64 CG, row-block over {world} GPU(s), fixed-count iterations",
+            "workload": (f"configs[3]: N={n} dense SPD fp64 CG, A streamed from pinned host memory every matVec, "
+                         f"row-block over {world} GPU(s), fixed-count iterations") if stream else
+                        f"configs[2]: N={n} dense SPD fp64 CG, row-block over {world} GPU(s), fixed-count iterations",
             "n": n,
             "rows_per_gpu": nloc,
             "parallelism": f"rowblock{world}",
@@ -228,11 +236,11 @@ def main(argv=None) -> int:
         "matvec_ms": mv_ms,
         "matvec_ms_max_rank": mv_ms_max,
         "roofline": {
-            "bound": "hbm",
+            "bound": "h2d" if stream else "hbm",
             "achieved": achieved,
-            "peak": HBM_PEAK_GBS,
+            "peak": peak,
             "unit": "GB/s",
-            "frac": achieved / HBM_PEAK_GBS,
+            "frac": achieved / peak,
             "traffic": traffic,
             "kernel": "k_matvec_f64",
             "plan": plan,
@@ -240,7 +248,7 @@ def main(argv=None) -> int:
         },
         "check": {"relres": rnorm / bnorm},
     }
-    if world == 1 and not args.no_cpu:
+    if world == 1 and not args.no_cpu and not stream:
         out["cpu_baseline"] = cpu_baseline(args.cpu_n or n)
     print(json.dumps(out), flush=True)
     if dist:

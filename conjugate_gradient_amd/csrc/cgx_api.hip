@@ -31,11 +31,13 @@
 #include <cmath>
 #include <cstdarg>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <new>
 #include <string>
 #include <vector>
+#include <algorithm>
 
 #include "cgx.h"
 #include "cgx_kernels.h"
@@ -86,6 +88,8 @@ enum Mode { M_SINGLE = 0, M_LOCAL = 1, M_RCCL = 2 };
 enum State { ST_IDLE = 0, ST_BEGUN = 1, ST_CONVERGED = 2 };
 
 constexpr int kEvPairs = 256;
+constexpr int kStreamBufs = 3;
+constexpr int kMaxCopyStreams = 4;
 
 struct Shard {
     int dev = 0;
@@ -101,6 +105,19 @@ struct Shard {
     hipEvent_t ev_sync = nullptr;  // cross-shard ordering (LOCAL mode)
     std::vector<hipEvent_t> ev_t;  // timing pairs (CGX_TIMING)
     int ev_used = 0;
+    // CGX_HOST_STREAM: A stays in pinned host memory; row tiles are copied
+    // into kStreamBufs device buffers on `ncopy` copy streams while the
+    // compute stream multiplies the previous tiles.
+    char *A_host = nullptr;
+    int64_t tile_rows = 0;
+    char *tile[kStreamBufs] = {};
+    int ncopy = 0;
+    hipStream_t copy[kMaxCopyStreams] = {};
+    hipEvent_t ev_loaded[kStreamBufs][kMaxCopyStreams] = {};
+    hipEvent_t ev_free[kStreamBufs] = {};
+    bool buf_used[kStreamBufs] = {};
+    int next_buf = 0;
+    MatvecPlan tile_plan;
 };
 
 }  // namespace
@@ -144,7 +161,29 @@ int alloc_shard(cgx_ctx *c, Shard &s) {
                         hipGetErrorString(e));
         return CGX_OK;
     };
-    TRY(dmalloc(&s.A, abytes));
+    if (c->flags & CGX_HOST_STREAM) {
+        // A in pinned host memory, kStreamBufs device tiles of ~CGX_STREAM_TILE_MB.
+        hipError_t e = hipHostMalloc(reinterpret_cast<void **>(&s.A_host), abytes ? abytes : 16, hipHostMallocDefault);
+        if (e != hipSuccess)
+            return fail(CGX_ERR_NOMEM, "hipHostMalloc(%zu bytes) for streamed A: %s", abytes, hipGetErrorString(e));
+        const int64_t row_bytes = c->lda * (int64_t)es;
+        const char *tmb = std::getenv("CGX_STREAM_TILE_MB");
+        const int64_t tile_bytes = (int64_t)((tmb && *tmb) ? std::atoll(tmb) : 256) << 20;
+        s.tile_rows = std::max<int64_t>(1, std::min<int64_t>(s.nloc, tile_bytes / row_bytes));
+        const char *nc = std::getenv("CGX_STREAM_COPIES");
+        s.ncopy = std::max(1, std::min(kMaxCopyStreams, (nc && *nc) ? std::atoi(nc) : 2));
+        for (int b = 0; b < kStreamBufs; ++b) {
+            TRY(dmalloc(&s.tile[b], (size_t)s.tile_rows * row_bytes));
+            HIPT(hipMemsetAsync(s.tile[b], 0, (size_t)s.tile_rows * row_bytes, s.stream));
+            HIPT(hipEventCreateWithFlags(&s.ev_free[b], hipEventDisableTiming));
+            for (int q = 0; q < s.ncopy; ++q) HIPT(hipEventCreateWithFlags(&s.ev_loaded[b][q], hipEventDisableTiming));
+        }
+        for (int q = 0; q < s.ncopy; ++q) HIPT(hipStreamCreateWithFlags(&s.copy[q], hipStreamNonBlocking));
+        if (!f32ref(c)) s.tile_plan = plan_matvec_f64(s.dev, s.tile_rows);
+    } else {
+        TRY(dmalloc(&s.A, abytes));
+        HIPT(hipMemsetAsync(s.A, 0, abytes, s.stream));  // zero padding columns
+    }
     TRY(dmalloc(&s.b, s.nloc * es));
     TRY(dmalloc(&s.x, s.nloc * es));
     TRY(dmalloc(&s.r, s.nloc * es));
@@ -157,7 +196,6 @@ int alloc_shard(cgx_ctx *c, Shard &s) {
     TRY(dmalloc(&tick, kTickets * sizeof(unsigned)));
     s.ws.partials = reinterpret_cast<double *>(part);
     s.ws.tickets = reinterpret_cast<unsigned *>(tick);
-    HIPT(hipMemsetAsync(s.A, 0, abytes, s.stream));  // zero padding columns
     HIPT(hipMemsetAsync(s.b, 0, s.nloc * es, s.stream));
     HIPT(hipMemsetAsync(s.x, 0, s.nloc * es, s.stream));
     HIPT(hipMemsetAsync(s.r, 0, s.nloc * es, s.stream));
@@ -187,6 +225,18 @@ void free_shard(Shard &s) {
     if (s.h_pin) (void)hipHostFree(s.h_pin);
     for (auto e : s.ev_t) (void)hipEventDestroy(e);
     if (s.ev_sync) (void)hipEventDestroy(s.ev_sync);
+    for (int q = 0; q < kMaxCopyStreams; ++q)
+        if (s.copy[q]) {
+            (void)hipStreamSynchronize(s.copy[q]);
+            (void)hipStreamDestroy(s.copy[q]);
+        }
+    for (int b = 0; b < kStreamBufs; ++b) {
+        if (s.tile[b]) (void)hipFree(s.tile[b]);
+        if (s.ev_free[b]) (void)hipEventDestroy(s.ev_free[b]);
+        for (int q = 0; q < kMaxCopyStreams; ++q)
+            if (s.ev_loaded[b][q]) (void)hipEventDestroy(s.ev_loaded[b][q]);
+    }
+    if (s.A_host) (void)hipHostFree(s.A_host);
     if (s.stream) (void)hipStreamDestroy(s.stream);
     s = Shard();
 }
@@ -330,27 +380,69 @@ int exchange_scalar(cgx_ctx *c, int lslot, int gslot) {
 inline int out_slot(const cgx_ctx *c, int lslot, int gslot) { return c->mode == M_SINGLE ? gslot : lslot; }
 
 // ---- the iteration pieces ----------------------------------------------------------
+// One tile of the matVec: rows [r0, r0+rows) of this shard, A rows at `Arows`.
+int matvec_rows(cgx_ctx *c, Shard &s, const MatvecPlan &pl, const char *Arows, int64_t r0, int64_t rows,
+                const char *vec, bool fuse_dot, int dot_slot) {
+    if (f32ref(c)) {
+        HIPT(matvec_ref_f32(reinterpret_cast<const float *>(Arows), c->lda, rows, c->n,
+                            reinterpret_cast<const float *>(vec), reinterpret_cast<float *>(s.Ap) + r0, s.stream));
+    } else {
+        HIPT(matvec_f64(pl, reinterpret_cast<const double *>(Arows), c->lda, rows, c->lda,
+                        reinterpret_cast<const double *>(vec), reinterpret_cast<double *>(s.Ap) + r0,
+                        fuse_dot ? reinterpret_cast<const double *>(s.pfull + s.row0 * 8) + r0 : nullptr,
+                        fuse_dot ? reinterpret_cast<double *>(slot(s, dot_slot)) : nullptr, s.ws, s.stream));
+    }
+    return CGX_OK;
+}
+
+// CGX_HOST_STREAM matVec: tile t goes to buffer (next_buf++ % kStreamBufs);
+// its copy waits until the kernel that last read that buffer is done (A is
+// read-only, so copies of the next iteration's first tiles overlap this
+// iteration's vector work); its kernel waits for the copy.
+int matvec_streamed(cgx_ctx *c, Shard &s, const char *vec) {
+    const int64_t row_bytes = c->lda * (int64_t)c->es;
+    for (int64_t r0 = 0; r0 < s.nloc; r0 += s.tile_rows) {
+        const int64_t rows = std::min(s.tile_rows, s.nloc - r0);
+        const int b = s.next_buf;
+        s.next_buf = (s.next_buf + 1) % kStreamBufs;
+        const int64_t bytes = rows * row_bytes;
+        const char *src = s.A_host + (size_t)r0 * row_bytes;
+        const int64_t part = (bytes / s.ncopy + 4095) & ~int64_t(4095);
+        for (int q = 0; q < s.ncopy; ++q) {
+            const int64_t lo = std::min<int64_t>(bytes, q * part), hi = std::min<int64_t>(bytes, lo + part);
+            if (s.buf_used[b]) HIPT(hipStreamWaitEvent(s.copy[q], s.ev_free[b], 0));
+            if (hi > lo) HIPT(hipMemcpyAsync(s.tile[b] + lo, src + lo, hi - lo, hipMemcpyHostToDevice, s.copy[q]));
+            HIPT(hipEventRecord(s.ev_loaded[b][q], s.copy[q]));
+            HIPT(hipStreamWaitEvent(s.stream, s.ev_loaded[b][q], 0));
+        }
+        TRY(matvec_rows(c, s, s.tile_plan, s.tile[b], r0, rows, vec, false, 0));
+        HIPT(hipEventRecord(s.ev_free[b], s.stream));
+        s.buf_used[b] = true;
+    }
+    return CGX_OK;
+}
+
 int launch_matvec(cgx_ctx *c, Shard &s, const char *vec, bool with_dot, int dot_slot) {
     const bool timing = (c->flags & CGX_TIMING) && (&s == &c->sh[0]);
     if (timing && s.ev_used >= kEvPairs) TRY(timing_resolve(c));
     if (timing) HIPT(hipEventRecord(s.ev_t[2 * s.ev_used], s.stream));
-    if (f32ref(c)) {
-        HIPT(matvec_ref_f32(reinterpret_cast<const float *>(s.A), c->lda, s.nloc, c->n,
-                            reinterpret_cast<const float *>(vec), reinterpret_cast<float *>(s.Ap), s.stream));
-    } else {
-        HIPT(matvec_f64(s.plan, reinterpret_cast<const double *>(s.A), c->lda, s.nloc, c->lda,
-                        reinterpret_cast<const double *>(vec), reinterpret_cast<double *>(s.Ap),
-                        with_dot ? reinterpret_cast<const double *>(s.pfull + s.row0 * 8) : nullptr,
-                        with_dot ? reinterpret_cast<double *>(slot(s, dot_slot)) : nullptr, s.ws, s.stream));
-    }
+    const bool streamed = (c->flags & CGX_HOST_STREAM) != 0;
+    if (streamed) TRY(matvec_streamed(c, s, vec));
+    else TRY(matvec_rows(c, s, s.plan, s.A, 0, s.nloc, vec, with_dot && !f32ref(c), dot_slot));
     if (timing) {
         HIPT(hipEventRecord(s.ev_t[2 * s.ev_used + 1], s.stream));
         s.ev_used++;
     }
-    if (f32ref(c) && with_dot)  // vecVec(p, Ap) sequential (serialConjugate.c:219)
-        HIPT(dot_ref_f32(s.nloc, reinterpret_cast<const float *>(s.pfull + s.row0 * 4),
-                         reinterpret_cast<const float *>(s.Ap), reinterpret_cast<float *>(slot(s, dot_slot)),
+    if (with_dot && (f32ref(c) || streamed)) {
+        if (f32ref(c))  // vecVec(p, Ap) sequential (serialConjugate.c:219)
+            HIPT(dot_ref_f32(s.nloc, reinterpret_cast<const float *>(s.pfull + s.row0 * 4),
+                             reinterpret_cast<const float *>(s.Ap), reinterpret_cast<float *>(slot(s, dot_slot)),
+                             s.stream));
+        else
+            HIPT(dot_f64(s.nloc, reinterpret_cast<const double *>(s.pfull + s.row0 * 8),
+                         reinterpret_cast<const double *>(s.Ap), reinterpret_cast<double *>(slot(s, dot_slot)), s.ws,
                          s.stream));
+    }
     return CGX_OK;
 }
 
@@ -463,6 +555,7 @@ int sync_all(cgx_ctx *c) {
     for (auto &s : c->sh) {
         TRY(set_dev(s));
         HIPT(hipStreamSynchronize(s.stream));
+        for (int q = 0; q < s.ncopy; ++q) HIPT(hipStreamSynchronize(s.copy[q]));
     }
     return timing_resolve(c);
 }
@@ -647,7 +740,13 @@ int cgx_set_rows(cgx_ctx *c, int64_t row0, int64_t nrows, const void *A_rows, in
         const int64_t lo = std::max(row0, s.row0), hi = std::min(row0 + nrows, s.row0 + s.nloc);
         if (hi <= lo) continue;
         TRY(set_dev(s));
-        if (A_rows)
+        if (A_rows && s.A_host) {
+            for (int64_t i = lo; i < hi; ++i) {
+                char *dst = s.A_host + (size_t)(i - s.row0) * c->lda * es;
+                std::memcpy(dst, static_cast<const char *>(A_rows) + (size_t)(i - row0) * lda_host * es, (size_t)c->n * es);
+                if (c->lda > c->n) std::memset(dst + (size_t)c->n * es, 0, (size_t)(c->lda - c->n) * es);
+            }
+        } else if (A_rows)
             HIPT(hipMemcpy2DAsync(s.A + (size_t)(lo - s.row0) * c->lda * es, (size_t)c->lda * es,
                                   static_cast<const char *>(A_rows) + (size_t)(lo - row0) * lda_host * es,
                                   (size_t)lda_host * es, (size_t)c->n * es, (size_t)(hi - lo), hipMemcpyHostToDevice,
@@ -673,12 +772,29 @@ int cgx_generate_spd(cgx_ctx *c, uint64_t seed) {
     if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
     for (auto &s : c->sh) {
         TRY(set_dev(s));
-        if (f32ref(c))
+        if (s.A_host) {
+            // Generate each tile on the device and move it to the host copy of A;
+            // b is generated for the whole block first (rows are independent).
+            const int64_t row_bytes = c->lda * (int64_t)c->es;
+            for (int64_t r0 = 0; r0 < s.nloc; r0 += s.tile_rows) {
+                const int64_t rows = std::min(s.tile_rows, s.nloc - r0);
+                if (f32ref(c))
+                    HIPT(gen_spd_f32(c->n, c->lda, s.row0 + r0, rows, seed, reinterpret_cast<float *>(s.tile[0]),
+                                     reinterpret_cast<float *>(s.b) + r0, s.stream));
+                else
+                    HIPT(gen_spd_f64(c->n, c->lda, s.row0 + r0, rows, seed, reinterpret_cast<double *>(s.tile[0]),
+                                     reinterpret_cast<double *>(s.b) + r0, s.stream));
+                HIPT(hipMemcpyAsync(s.A_host + (size_t)r0 * row_bytes, s.tile[0], (size_t)rows * row_bytes,
+                                    hipMemcpyDeviceToHost, s.stream));
+            }
+            HIPT(hipStreamSynchronize(s.stream));
+        } else if (f32ref(c)) {
             HIPT(gen_spd_f32(c->n, c->lda, s.row0, s.nloc, seed, reinterpret_cast<float *>(s.A),
                              reinterpret_cast<float *>(s.b), s.stream));
-        else
+        } else {
             HIPT(gen_spd_f64(c->n, c->lda, s.row0, s.nloc, seed, reinterpret_cast<double *>(s.A),
                              reinterpret_cast<double *>(s.b), s.stream));
+        }
         HIPT(hipMemsetAsync(s.x, 0, s.nloc * c->es, s.stream));
     }
     TRY(sync_all(c));

@@ -65,6 +65,10 @@ extern "C" {
 #define CGX_F64          0x0   /* double data (default)                        */
 #define CGX_F32_REF      0x1   /* float data, bit-exact serialConjugate.c order */
 #define CGX_TIMING       0x100 /* time every matVec launch with HIP events      */
+#define CGX_HOST_STREAM  0x200 /* keep A in pinned host memory and stream row
+                                  tiles through the GPU every matVec (out-of-HBM
+                                  systems; tile size CGX_STREAM_TILE_MB, default
+                                  256, copy streams CGX_STREAM_COPIES, default 2) */
 
 typedef struct cgx_ctx cgx_ctx;
 

@@ -197,3 +197,32 @@ def test_errors_are_reported():
         assert ei.value.code == -6
     with pytest.raises(cg.CgxError):
         cg.Solver(8, device=99)
+
+
+@pytest.mark.parametrize("shards", [None, [0, 0]])
+def test_host_streamed_matvec(monkeypatch, shards):
+    """CGX_HOST_STREAM (configs[3] design): A in pinned host memory, row tiles
+    streamed through 3 device buffers.  Row sums are the resident kernel's
+    (same per-lane order), so the solve matches the resident one to rounding
+    of the separate p.Ap reduction, and F32_REF stays bit-exact."""
+    monkeypatch.setenv("CGX_STREAM_TILE_MB", "1")  # 1 MiB tiles: many tiles per matVec
+    n = 2048
+    A, b = oracle.spd_hash(n, seed=5)
+    flags = cg.CGX_F64 | cg.CGX_HOST_STREAM | cg.CGX_TIMING
+    with cg.Solver(n, flags=flags, devices=shards) as s:
+        s.set_system(A, b)
+        x, st = s.solve(None, eps=1e-10)
+        assert s.stats().matvec_count == st.iterations + 1
+    with cg.Solver(n, flags=cg.CGX_F64 | cg.CGX_HOST_STREAM, devices=shards) as s:
+        s.generate_spd(seed=5)  # generated tile by tile on the device, kept on the host
+        xg, stg = s.solve(None, eps=1e-10)
+    xo, so = oracle.cg_f64(A, b, np.zeros(n), eps=1e-10)
+    assert st.iterations == stg.iterations == so.iterations
+    assert rel(x, xo) <= TOL and rel(xg, xo) <= TOL
+    A32, b32, x032 = case("spd1024")
+    with cg.Solver(1024, flags=cg.CGX_F32_REF | cg.CGX_HOST_STREAM, devices=shards) as s:
+        s.set_system(A32, b32, x032)
+        x32, st32 = s.solve(None, eps=1e-6)
+    ref, sr = oracle.cg_f32ref(A32, b32, x032, nparts=len(shards) if shards else 1)
+    assert st32.iterations == sr.iterations
+    assert np.array_equal(x32, ref)
