@@ -140,9 +140,11 @@ def main(argv=None) -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=["dense", "stream"], default="dense",
+    ap.add_argument("--workload", choices=["dense", "stream", "poisson"], default="dense",
                     help="dense: configs[2], A resident in HBM (default); "
-                         "stream: configs[3], A kept in pinned host memory and streamed every matVec")
+                         "stream: configs[3], A kept in pinned host memory and streamed every matVec; "
+                         "poisson: configs[4], matrix-free 5-point Poisson on an m x m grid (b=1, x0=0)")
+    ap.add_argument("--m", type=int, default=8192, help="Poisson grid width (n = m*m)")
     ap.add_argument("--n", type=int, default=None, help="system size (default 65536 dense, 131072 stream)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-n", type=int, default=None, help="N for the CPU baseline (default: --n)")
@@ -156,19 +158,24 @@ def main(argv=None) -> int:
 
     import conjugate_gradient_amd as cg
     stream = args.workload == "stream"
-    n = args.n or (131072 if stream else 65536)
-    if n % world:
-        raise SystemExit(f"{n} is not divisible by {world}")
+    poisson = args.workload == "poisson"
+    m = args.m if poisson else None
+    n = m * m if poisson else (args.n or (131072 if stream else 65536))
+    if (m if poisson else n) % world:
+        raise SystemExit(f"{m if poisson else n} is not divisible by {world}")
     flags = cg.CGX_F64 | cg.CGX_TIMING | (cg.CGX_HOST_STREAM if stream else 0)
     if use_dist:
         uid = bcast_bytes(dist, cg.get_unique_id() if rank == 0 else None)
-        solver = cg.Solver(n, rank=rank, nranks=world, unique_id=uid, device=local_rank, flags=flags)
+        solver = cg.Solver(n, rank=rank, nranks=world, unique_id=uid, device=local_rank, flags=flags, poisson_m=m)
     else:
-        solver = cg.Solver(n, device=0, flags=flags)
+        solver = cg.Solver(n, device=0, flags=flags, poisson_m=m)
     nloc = solver.info.nrows
-    plan = solver.matvec_plan()
+    plan = None if poisson else solver.matvec_plan()
 
-    solver.generate_spd(SEED)
+    if poisson:
+        solver.fill(1.0, 0.0)
+    else:
+        solver.generate_spd(SEED)
     solver.begin()
     if args.warmup:
         solver.iterate(args.warmup, eps=-1.0)
@@ -204,9 +211,10 @@ def main(argv=None) -> int:
             dist.barrier()
         return 0
 
-    bytes_launch = matvec_bytes(n, nloc)
+    # stencil: read the slab once (+2 halo rows), write Ap; dense: SURVEY.md s8(d)
+    bytes_launch = (16 * nloc + 16 * m) if poisson else matvec_bytes(n, nloc)
     achieved = bytes_launch / (mv_ms * 1e-3) / 1e9
-    traffic = None if stream else pmc_traffic(n, world)
+    traffic = None if (stream or poisson) else pmc_traffic(n, world)
     peak = H2D_PEAK_GBS if stream else HBM_PEAK_GBS
     iters_per_s = args.steps / elapsed
     out = {
@@ -221,11 +229,14 @@ def main(argv=None) -> int:
         "scaling": "strong",
         "vs_baseline": None,
         "dtype": "f64",
-        "data": f"synthetic: generateSPDmatrix.m-style dense SPD (0.5(R+R')+nI, counter hash, seed {SEED}) "
-                f"generated on device; x0 = 0",
+        "data": ("synthetic: 5-point Laplacian, b = 1, x0 = 0" if poisson else
+                 f"synthetic: generateSPDmatrix.m-style dense SPD (0.5(R+R')+nI, counter hash, seed {SEED}) "
+                 f"generated on device; x0 = 0"),
         "config": {
             "workload": (f"configs[3]: N={n} dense SPD fp64 CG, A streamed from pinned host memory every matVec, "
                          f"row-block over {world} GPU(s), fixed-count iterations") if stream else
+                        (f"configs[4]: matrix-free 5-point Poisson CG, m={m} (N={n}), b=1, x0=0, slabs over {world} "
+                         f"GPU(s), halo exchange, fixed-count iterations") if poisson else
                         f"configs[2]: N={n} dense SPD fp64 CG, row-block over {world} GPU(s), fixed-count iterations",
             "n": n,
             "rows_per_gpu": nloc,
@@ -242,13 +253,14 @@ def main(argv=None) -> int:
             "unit": "GB/s",
             "frac": achieved / peak,
             "traffic": traffic,
-            "kernel": "k_matvec_f64",
+            "kernel": "k_stencil5_f64" if poisson else "k_matvec_f64",
             "plan": plan,
             "algorithmic_bytes_per_launch": bytes_launch,
         },
         "check": {"relres": rnorm / bnorm},
+        "iteration_gbps": (88.0 * n / (elapsed / args.steps) / 1e9) if poisson else None,
     }
-    if world == 1 and not args.no_cpu and not stream:
+    if world == 1 and not args.no_cpu and not stream and not poisson:
         out["cpu_baseline"] = cpu_baseline(args.cpu_n or n)
     print(json.dumps(out), flush=True)
     if dist:

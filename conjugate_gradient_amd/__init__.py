@@ -105,6 +105,10 @@ def lib() -> ctypes.CDLL:
         "cgx_create_multi": ([pctx, i64, i32, ctypes.POINTER(i32), i32], i32),
         "cgx_get_unique_id": ([ctypes.POINTER(UniqueId)], i32),
         "cgx_create_rank": ([pctx, i64, i32, i32, ctypes.POINTER(UniqueId), i32, i32], i32),
+        "cgx_create_poisson": ([pctx, i64, i32, i32], i32),
+        "cgx_create_poisson_multi": ([pctx, i64, i32, ctypes.POINTER(i32), i32], i32),
+        "cgx_create_poisson_rank": ([pctx, i64, i32, i32, ctypes.POINTER(UniqueId), i32, i32], i32),
+        "cgx_fill": ([vp, f64, f64], i32),
         "cgx_destroy": ([vp], i32),
         "cgx_get_info": ([vp, ctypes.POINTER(Info)], i32),
         "cgx_set_rows": ([vp, i64, i64, vp, i64, vp, vp], i32),
@@ -284,13 +288,29 @@ class Solver:
     rank of a one-process-per-GPU job (RCCL)."""
 
     def __init__(self, n: int, *, flags: int = CGX_F64, device: int = 0, devices=None,
-                 rank: int | None = None, nranks: int | None = None, unique_id: bytes | None = None):
+                 rank: int | None = None, nranks: int | None = None, unique_id: bytes | None = None,
+                 poisson_m: int | None = None):
+        """Dense n x n system, or (poisson_m=m) the matrix-free 5-point Poisson
+        operator on an m x m grid (n must then be m*m or None)."""
         L = lib()
+        self.poisson_m = poisson_m
+        if poisson_m is not None:
+            n = poisson_m * poisson_m
         self.n = int(n)
         self.flags = flags
         self.dtype = _dtype(flags)
         h = ctypes.c_void_p()
-        if rank is not None:
+        if poisson_m is not None:
+            if rank is not None:
+                u = UniqueId()
+                ctypes.memmove(ctypes.addressof(u), unique_id, 128)
+                rc = L.cgx_create_poisson_rank(ctypes.byref(h), poisson_m, rank, nranks, ctypes.byref(u), device, flags)
+            elif devices is not None:
+                arr = (ctypes.c_int * len(devices))(*devices)
+                rc = L.cgx_create_poisson_multi(ctypes.byref(h), poisson_m, len(devices), arr, flags)
+            else:
+                rc = L.cgx_create_poisson(ctypes.byref(h), poisson_m, device, flags)
+        elif rank is not None:
             u = UniqueId()
             if unique_id is None or len(unique_id) != 128:
                 raise ValueError("unique_id must be the 128 bytes from get_unique_id()")
@@ -342,6 +362,9 @@ class Solver:
         lda = arrs[0].shape[1] if arrs[0] is not None else self.n
         _check(lib().cgx_set_rows(self._h, row0, nrows, *(None if a is None else _ptr(a) for a in arrs[:1]), lda,
                                   *(None if a is None else _ptr(a) for a in arrs[1:])), "cgx_set_rows")
+
+    def fill(self, b_value: float, x_value: float = 0.0) -> None:
+        _check(lib().cgx_fill(self._h, b_value, x_value), "cgx_fill")
 
     def generate_spd(self, seed: int = 42) -> None:
         _check(lib().cgx_generate_spd(self._h, seed), "cgx_generate_spd")

@@ -85,6 +85,7 @@ constexpr int S_TR = 128, S_TB = 129, S_LTR = 130, S_LTB = 131;  // true-residua
 inline int ring(int64_t j) { return (int)(j & 3); }
 
 enum Mode { M_SINGLE = 0, M_LOCAL = 1, M_RCCL = 2 };
+enum Op { OP_DENSE = 0, OP_POISSON = 1 };
 enum State { ST_IDLE = 0, ST_BEGUN = 1, ST_CONVERGED = 2 };
 
 constexpr int kEvPairs = 256;
@@ -99,6 +100,7 @@ struct Shard {
     ncclComm_t comm = nullptr;
     char *A = nullptr, *b = nullptr, *x = nullptr, *r = nullptr, *Ap = nullptr, *pfull = nullptr,
          *xfull = nullptr, *scal = nullptr;
+    char *pown = nullptr;  // this shard's p: pfull + row0 (dense) or the slab interior (Poisson)
     RedWs ws{nullptr, nullptr};
     double *h_pin = nullptr;
     MatvecPlan plan;
@@ -124,6 +126,8 @@ struct Shard {
 
 struct cgx_ctx {
     int64_t n = 0, lda = 0;
+    int op = 0;        // OP_DENSE or OP_POISSON
+    int64_t m = 0;     // Poisson grid width (n = m*m)
     int nranks = 1;
     int flags = 0;
     int es = 8;
@@ -161,7 +165,9 @@ int alloc_shard(cgx_ctx *c, Shard &s) {
                         hipGetErrorString(e));
         return CGX_OK;
     };
-    if (c->flags & CGX_HOST_STREAM) {
+    if (c->op == OP_POISSON) {
+        // matrix-free: no A
+    } else if (c->flags & CGX_HOST_STREAM) {
         // A in pinned host memory, kStreamBufs device tiles of ~CGX_STREAM_TILE_MB.
         hipError_t e = hipHostMalloc(reinterpret_cast<void **>(&s.A_host), abytes ? abytes : 16, hipHostMallocDefault);
         if (e != hipSuccess)
@@ -188,9 +194,13 @@ int alloc_shard(cgx_ctx *c, Shard &s) {
     TRY(dmalloc(&s.x, s.nloc * es));
     TRY(dmalloc(&s.r, s.nloc * es));
     TRY(dmalloc(&s.Ap, s.nloc * es));
-    TRY(dmalloc(&s.pfull, c->lda * es));
+    // full-length p (dense) or the slab with one halo row above and below (Poisson)
+    const int64_t plen = (c->op == OP_POISSON) ? s.nloc + 2 * c->m : c->lda;
+    const int64_t xlen = (c->op == OP_POISSON) ? c->n : c->lda;
+    TRY(dmalloc(&s.pfull, plen * es));
+    s.pown = (c->op == OP_POISSON) ? s.pfull + c->m * es : s.pfull + s.row0 * es;
     TRY(dmalloc(&s.scal, kScalSlots * 8));
-    if (c->mode == M_RCCL && c->nranks > 1) TRY(dmalloc(&s.xfull, c->lda * es));
+    if (c->mode == M_RCCL && c->nranks > 1) TRY(dmalloc(&s.xfull, xlen * es));
     char *part = nullptr, *tick = nullptr;
     TRY(dmalloc(&part, kMaxRedBlocks * sizeof(double)));
     TRY(dmalloc(&tick, kTickets * sizeof(unsigned)));
@@ -200,16 +210,16 @@ int alloc_shard(cgx_ctx *c, Shard &s) {
     HIPT(hipMemsetAsync(s.x, 0, s.nloc * es, s.stream));
     HIPT(hipMemsetAsync(s.r, 0, s.nloc * es, s.stream));
     HIPT(hipMemsetAsync(s.Ap, 0, s.nloc * es, s.stream));
-    HIPT(hipMemsetAsync(s.pfull, 0, c->lda * es, s.stream));
+    HIPT(hipMemsetAsync(s.pfull, 0, plen * es, s.stream));
     HIPT(hipMemsetAsync(s.scal, 0, kScalSlots * 8, s.stream));
     HIPT(hipMemsetAsync(s.ws.tickets, 0, kTickets * sizeof(unsigned), s.stream));
-    if (s.xfull) HIPT(hipMemsetAsync(s.xfull, 0, c->lda * es, s.stream));
+    if (s.xfull) HIPT(hipMemsetAsync(s.xfull, 0, xlen * es, s.stream));
     HIPT(hipHostMalloc(reinterpret_cast<void **>(&s.h_pin), 64, hipHostMallocDefault));
     if (c->flags & CGX_TIMING) {
         s.ev_t.resize(2 * kEvPairs);
         for (auto &e : s.ev_t) HIPT(hipEventCreate(&e));
     }
-    if (!f32ref(c)) s.plan = plan_matvec_f64(s.dev, s.nloc);
+    if (!f32ref(c) && c->op == OP_DENSE) s.plan = plan_matvec_f64(s.dev, s.nloc);
     HIPT(hipStreamSynchronize(s.stream));
     return CGX_OK;
 }
@@ -309,15 +319,62 @@ int local_barrier(cgx_ctx *c) {
     return CGX_OK;
 }
 
+// Poisson: refresh the two halo rows of every slab from its neighbours
+// (ncclSend/Recv of one grid row each way in rank mode, device copies in
+// LOCAL mode); from_x first copies x into the slab interior (for A x0).
+int exchange_halo(cgx_ctx *c, bool from_x) {
+    const size_t es = (size_t)c->es, row = (size_t)c->m * es;
+    if (from_x)
+        for (auto &s : c->sh) {
+            TRY(set_dev(s));
+            HIPT(hipMemcpyAsync(s.pown, s.x, s.nloc * es, hipMemcpyDeviceToDevice, s.stream));
+        }
+    if (c->mode == M_SINGLE) return CGX_OK;
+    const int64_t mloc = c->sh[0].nloc / c->m;
+    if (c->mode == M_RCCL) {
+        Shard &s = c->sh[0];
+        if (c->nranks == 1) return CGX_OK;
+        TRY(set_dev(s));
+        const int g = s.index;
+        NCCLT(ncclGroupStart());
+        if (g > 0) {
+            NCCLT(ncclSend(s.pown, (size_t)c->m, ncclDouble, g - 1, s.comm, s.stream));
+            NCCLT(ncclRecv(s.pfull, (size_t)c->m, ncclDouble, g - 1, s.comm, s.stream));
+        }
+        if (g < c->nranks - 1) {
+            NCCLT(ncclSend(s.pown + (size_t)(mloc - 1) * row, (size_t)c->m, ncclDouble, g + 1, s.comm, s.stream));
+            NCCLT(ncclRecv(s.pown + (size_t)mloc * row, (size_t)c->m, ncclDouble, g + 1, s.comm, s.stream));
+        }
+        NCCLT(ncclGroupEnd());
+        return CGX_OK;
+    }
+    TRY(local_barrier(c));
+    const int S = (int)c->sh.size();
+    for (int q = 0; q < S; ++q) {
+        Shard &d = c->sh[q];
+        TRY(set_dev(d));
+        if (q > 0) {
+            const Shard &u = c->sh[q - 1];
+            HIPT(hipMemcpyPeerAsync(d.pfull, d.dev, u.pown + (size_t)(mloc - 1) * row, u.dev, row, d.stream));
+        }
+        if (q < S - 1) {
+            const Shard &w = c->sh[q + 1];
+            HIPT(hipMemcpyPeerAsync(d.pown + (size_t)mloc * row, d.dev, w.pown, w.dev, row, d.stream));
+        }
+    }
+    return CGX_OK;
+}
+
 // Every shard's pfull gets every shard's slice of `src(shard)` (its own slice
 // of a full-length buffer when in_place, else a separate local buffer).
 int exchange_allgather(cgx_ctx *c, bool from_x) {
+    if (c->op == OP_POISSON) return exchange_halo(c, from_x);
     const size_t es = (size_t)c->es;
     if (c->mode == M_SINGLE) {
         if (from_x) {
             Shard &s = c->sh[0];
             TRY(set_dev(s));
-            HIPT(hipMemcpyAsync(s.pfull + s.row0 * es, s.x, s.nloc * es, hipMemcpyDeviceToDevice, s.stream));
+            HIPT(hipMemcpyAsync(s.pown, s.x, s.nloc * es, hipMemcpyDeviceToDevice, s.stream));
         }
         return CGX_OK;
     }
@@ -325,7 +382,7 @@ int exchange_allgather(cgx_ctx *c, bool from_x) {
         Shard &s = c->sh[0];
         TRY(set_dev(s));
         const ncclDataType_t t = f32ref(c) ? ncclFloat : ncclDouble;
-        const void *send = from_x ? (const void *)s.x : (const void *)(s.pfull + s.row0 * es);
+        const void *send = from_x ? (const void *)s.x : (const void *)s.pown;
         NCCLT(ncclAllGather(send, s.pfull, (size_t)s.nloc, t, s.comm, s.stream));
         return CGX_OK;
     }
@@ -335,7 +392,7 @@ int exchange_allgather(cgx_ctx *c, bool from_x) {
         TRY(set_dev(d));
         for (auto &s : c->sh) {
             char *dst = d.pfull + s.row0 * es;
-            const char *src = from_x ? s.x : s.pfull + s.row0 * es;
+            const char *src = from_x ? s.x : s.pown;
             if (&s == &d && !from_x) continue;
             HIPT(hipMemcpyPeerAsync(dst, d.dev, src, s.dev, s.nloc * es, d.stream));
         }
@@ -389,7 +446,7 @@ int matvec_rows(cgx_ctx *c, Shard &s, const MatvecPlan &pl, const char *Arows, i
     } else {
         HIPT(matvec_f64(pl, reinterpret_cast<const double *>(Arows), c->lda, rows, c->lda,
                         reinterpret_cast<const double *>(vec), reinterpret_cast<double *>(s.Ap) + r0,
-                        fuse_dot ? reinterpret_cast<const double *>(s.pfull + s.row0 * 8) + r0 : nullptr,
+                        fuse_dot ? reinterpret_cast<const double *>(s.pown) + r0 : nullptr,
                         fuse_dot ? reinterpret_cast<double *>(slot(s, dot_slot)) : nullptr, s.ws, s.stream));
     }
     return CGX_OK;
@@ -427,7 +484,10 @@ int launch_matvec(cgx_ctx *c, Shard &s, const char *vec, bool with_dot, int dot_
     if (timing && s.ev_used >= kEvPairs) TRY(timing_resolve(c));
     if (timing) HIPT(hipEventRecord(s.ev_t[2 * s.ev_used], s.stream));
     const bool streamed = (c->flags & CGX_HOST_STREAM) != 0;
-    if (streamed) TRY(matvec_streamed(c, s, vec));
+    if (c->op == OP_POISSON)
+        HIPT(stencil5_f64(reinterpret_cast<const double *>(vec), s.nloc / c->m, c->m, reinterpret_cast<double *>(s.Ap),
+                          with_dot ? reinterpret_cast<double *>(slot(s, dot_slot)) : nullptr, s.ws, s.stream));
+    else if (streamed) TRY(matvec_streamed(c, s, vec));
     else TRY(matvec_rows(c, s, s.plan, s.A, 0, s.nloc, vec, with_dot && !f32ref(c), dot_slot));
     if (timing) {
         HIPT(hipEventRecord(s.ev_t[2 * s.ev_used + 1], s.stream));
@@ -435,11 +495,11 @@ int launch_matvec(cgx_ctx *c, Shard &s, const char *vec, bool with_dot, int dot_
     }
     if (with_dot && (f32ref(c) || streamed)) {
         if (f32ref(c))  // vecVec(p, Ap) sequential (serialConjugate.c:219)
-            HIPT(dot_ref_f32(s.nloc, reinterpret_cast<const float *>(s.pfull + s.row0 * 4),
+            HIPT(dot_ref_f32(s.nloc, reinterpret_cast<const float *>(s.pown),
                              reinterpret_cast<const float *>(s.Ap), reinterpret_cast<float *>(slot(s, dot_slot)),
                              s.stream));
         else
-            HIPT(dot_f64(s.nloc, reinterpret_cast<const double *>(s.pfull + s.row0 * 8),
+            HIPT(dot_f64(s.nloc, reinterpret_cast<const double *>(s.pown),
                          reinterpret_cast<const double *>(s.Ap), reinterpret_cast<double *>(slot(s, dot_slot)), s.ws,
                          s.stream));
     }
@@ -455,13 +515,13 @@ int do_begin(cgx_ctx *c) {
         TRY(set_dev(s));
         TRY(launch_matvec(c, s, s.pfull, false, 0));
         if (f32ref(c)) {
-            float *pown = reinterpret_cast<float *>(s.pfull + s.row0 * 4);
+            float *pown = reinterpret_cast<float *>(s.pown);
             HIPT(residual_ref_f32(s.nloc, reinterpret_cast<const float *>(s.b), reinterpret_cast<const float *>(s.Ap),
                                   reinterpret_cast<float *>(s.r), pown, s.stream));
             HIPT(dot_ref_f32(s.nloc, reinterpret_cast<const float *>(s.r), reinterpret_cast<const float *>(s.r),
                              reinterpret_cast<float *>(slot(s, os)), s.stream));
         } else {
-            double *pown = reinterpret_cast<double *>(s.pfull + s.row0 * 8);
+            double *pown = reinterpret_cast<double *>(s.pown);
             HIPT(residual_f64(s.nloc, reinterpret_cast<const double *>(s.b), reinterpret_cast<const double *>(s.Ap),
                               reinterpret_cast<double *>(s.r), pown, reinterpret_cast<double *>(slot(s, os)), s.ws,
                               s.stream));
@@ -508,7 +568,7 @@ int do_iteration(cgx_ctx *c, double eps, int *stop) {
         TRY(set_dev(s));
         if (f32ref(c)) {
             HIPT(update_xr_ref_f32(s.nloc, reinterpret_cast<float *>(s.x), reinterpret_cast<float *>(s.r),
-                                   reinterpret_cast<const float *>(s.pfull + s.row0 * 4),
+                                   reinterpret_cast<const float *>(s.pown),
                                    reinterpret_cast<const float *>(s.Ap),
                                    reinterpret_cast<const float *>(slot(s, S_RR + ring(k))),
                                    reinterpret_cast<const float *>(slot(s, pg)), s.stream));
@@ -516,7 +576,7 @@ int do_iteration(cgx_ctx *c, double eps, int *stop) {
                              reinterpret_cast<float *>(slot(s, ro)), s.stream));
         } else {
             HIPT(update_xr_f64(s.nloc, reinterpret_cast<double *>(s.x), reinterpret_cast<double *>(s.r),
-                               reinterpret_cast<const double *>(s.pfull + s.row0 * 8),
+                               reinterpret_cast<const double *>(s.pown),
                                reinterpret_cast<const double *>(s.Ap),
                                reinterpret_cast<const double *>(slot(s, S_RR + ring(k))),
                                reinterpret_cast<const double *>(slot(s, pg)), reinterpret_cast<double *>(slot(s, ro)),
@@ -540,11 +600,11 @@ int do_iteration(cgx_ctx *c, double eps, int *stop) {
     for (auto &s : c->sh) {  // p = r + (beta/rsold) p    serialConjugate.c:239-243
         TRY(set_dev(s));
         if (f32ref(c))
-            HIPT(update_p_ref_f32(s.nloc, reinterpret_cast<float *>(s.pfull + s.row0 * 4),
+            HIPT(update_p_ref_f32(s.nloc, reinterpret_cast<float *>(s.pown),
                                   reinterpret_cast<const float *>(s.r), reinterpret_cast<const float *>(slot(s, rg)),
                                   reinterpret_cast<const float *>(slot(s, S_RR + ring(k))), s.stream));
         else
-            HIPT(update_p_f64(s.nloc, reinterpret_cast<double *>(s.pfull + s.row0 * 8),
+            HIPT(update_p_f64(s.nloc, reinterpret_cast<double *>(s.pown),
                               reinterpret_cast<const double *>(s.r), reinterpret_cast<const double *>(slot(s, rg)),
                               reinterpret_cast<const double *>(slot(s, S_RR + ring(k))), s.stream));
     }
@@ -622,12 +682,34 @@ static int check_device(int device) {
     return CGX_OK;
 }
 
-int cgx_create(cgx_ctx **ctx, int64_t n, int device, int flags) {
+// Operator-generic constructors.  Dense: n unknowns, row blocks of n/P rows.
+// Poisson: n = m*m unknowns, slabs of m/P grid rows (n/P unknowns).
+static int check_op(int op, int64_t n, int64_t m, int parts, int flags) {
+    if (op == OP_POISSON) {
+        if (m < 1) return fail(CGX_ERR_ARG, "m must be >= 1");
+        if (m % parts != 0) return fail(CGX_ERR_SHAPE, "%lld is not divisible by %d", (long long)m, parts);
+        if (flags & (CGX_F32_REF | CGX_HOST_STREAM))
+            return fail(CGX_ERR_ARG, "the Poisson operator supports CGX_F64 (+CGX_TIMING) only");
+        return CGX_OK;
+    }
+    return check_n(n, parts);
+}
+
+static cgx_ctx *new_ctx_op(int op, int64_t n, int64_t m, int parts, int flags) {
+    cgx_ctx *c = new_ctx(n, parts, flags);
+    if (!c) return nullptr;
+    c->op = op;
+    c->m = m;
+    if (op == OP_POISSON) c->lda = m;
+    return c;
+}
+
+static int create_single(cgx_ctx **ctx, int op, int64_t n, int64_t m, int device, int flags) {
     if (!ctx) return fail(CGX_ERR_ARG, "ctx is NULL");
     *ctx = nullptr;
-    TRY(check_n(n, 1));
+    TRY(check_op(op, n, m, 1, flags));
     TRY(check_device(device));
-    cgx_ctx *c = new_ctx(n, 1, flags);
+    cgx_ctx *c = new_ctx_op(op, n, m, 1, flags);
     if (!c) return fail(CGX_ERR_NOMEM, "host allocation failed");
     c->mode = M_SINGLE;
     c->sh.resize(1);
@@ -638,13 +720,13 @@ int cgx_create(cgx_ctx **ctx, int64_t n, int device, int flags) {
     return finish_create(c, ctx);
 }
 
-int cgx_create_multi(cgx_ctx **ctx, int64_t n, int nshards, const int *devices, int flags) {
+static int create_multi(cgx_ctx **ctx, int op, int64_t n, int64_t m, int nshards, const int *devices, int flags) {
     if (!ctx || !devices) return fail(CGX_ERR_ARG, "ctx/devices is NULL");
     *ctx = nullptr;
     if (nshards < 1 || nshards > kMaxShards) return fail(CGX_ERR_ARG, "nshards must be in [1, %d]", kMaxShards);
-    TRY(check_n(n, nshards));
+    TRY(check_op(op, n, m, nshards, flags));
     for (int i = 0; i < nshards; ++i) TRY(check_device(devices[i]));
-    cgx_ctx *c = new_ctx(n, nshards, flags);
+    cgx_ctx *c = new_ctx_op(op, n, m, nshards, flags);
     if (!c) return fail(CGX_ERR_NOMEM, "host allocation failed");
     c->mode = nshards == 1 ? M_SINGLE : M_LOCAL;
     c->sh.resize(nshards);
@@ -666,24 +748,15 @@ int cgx_create_multi(cgx_ctx **ctx, int64_t n, int nshards, const int *devices, 
     return finish_create(c, ctx);
 }
 
-int cgx_get_unique_id(cgx_unique_id *id) {
-    if (!id) return fail(CGX_ERR_ARG, "id is NULL");
-    static_assert(sizeof(ncclUniqueId) == sizeof(cgx_unique_id), "unique id size");
-    ncclUniqueId u;
-    NCCLT(ncclGetUniqueId(&u));
-    std::memcpy(id, &u, sizeof u);
-    return CGX_OK;
-}
-
-int cgx_create_rank(cgx_ctx **ctx, int64_t n, int rank, int nranks, const cgx_unique_id *id, int device,
-                    int flags) {
+static int create_rank(cgx_ctx **ctx, int op, int64_t n, int64_t m, int rank, int nranks, const cgx_unique_id *id,
+                       int device, int flags) {
     if (!ctx || !id) return fail(CGX_ERR_ARG, "ctx/id is NULL");
     *ctx = nullptr;
-    TRY(check_n(n, nranks));
+    TRY(check_op(op, n, m, nranks, flags));
     if (rank < 0 || rank >= nranks) return fail(CGX_ERR_ARG, "rank %d not in [0, %d)", rank, nranks);
     if (nranks > S_TR - S_GATHER) return fail(CGX_ERR_ARG, "at most %d ranks", S_TR - S_GATHER);
     TRY(check_device(device));
-    cgx_ctx *c = new_ctx(n, nranks, flags);
+    cgx_ctx *c = new_ctx_op(op, n, m, nranks, flags);
     if (!c) return fail(CGX_ERR_NOMEM, "host allocation failed");
     c->mode = M_RCCL;
     c->sh.resize(1);
@@ -704,6 +777,66 @@ int cgx_create_rank(cgx_ctx **ctx, int64_t n, int rank, int nranks, const cgx_un
         return fail(CGX_ERR_RCCL, "ncclCommInitRank(rank %d of %d): %s", rank, nranks, ncclGetErrorString(nr));
     }
     return finish_create(c, ctx);
+}
+
+int cgx_create(cgx_ctx **ctx, int64_t n, int device, int flags) {
+    return create_single(ctx, OP_DENSE, n, 0, device, flags);
+}
+
+int cgx_create_multi(cgx_ctx **ctx, int64_t n, int nshards, const int *devices, int flags) {
+    return create_multi(ctx, OP_DENSE, n, 0, nshards, devices, flags);
+}
+
+int cgx_get_unique_id(cgx_unique_id *id) {
+    if (!id) return fail(CGX_ERR_ARG, "id is NULL");
+    static_assert(sizeof(ncclUniqueId) == sizeof(cgx_unique_id), "unique id size");
+    ncclUniqueId u;
+    NCCLT(ncclGetUniqueId(&u));
+    std::memcpy(id, &u, sizeof u);
+    return CGX_OK;
+}
+
+int cgx_create_rank(cgx_ctx **ctx, int64_t n, int rank, int nranks, const cgx_unique_id *id, int device,
+                    int flags) {
+    return create_rank(ctx, OP_DENSE, n, 0, rank, nranks, id, device, flags);
+}
+
+static int check_m(int64_t m) {
+    if (m < 1 || m > 46340 * 4) return fail(CGX_ERR_ARG, "grid width m out of range");
+    return CGX_OK;
+}
+
+int cgx_create_poisson(cgx_ctx **ctx, int64_t m, int device, int flags) {
+    TRY(check_m(m));
+    return create_single(ctx, OP_POISSON, m * m, m, device, flags);
+}
+
+int cgx_create_poisson_multi(cgx_ctx **ctx, int64_t m, int nshards, const int *devices, int flags) {
+    TRY(check_m(m));
+    return create_multi(ctx, OP_POISSON, m * m, m, nshards, devices, flags);
+}
+
+int cgx_create_poisson_rank(cgx_ctx **ctx, int64_t m, int rank, int nranks, const cgx_unique_id *id, int device,
+                            int flags) {
+    TRY(check_m(m));
+    return create_rank(ctx, OP_POISSON, m * m, m, rank, nranks, id, device, flags);
+}
+
+int cgx_fill(cgx_ctx *c, double b_value, double x_value) {
+    if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
+    for (auto &s : c->sh) {
+        TRY(set_dev(s));
+        if (f32ref(c)) {
+            HIPT(fill_f32(reinterpret_cast<float *>(s.b), s.nloc, (float)b_value, s.stream));
+            HIPT(fill_f32(reinterpret_cast<float *>(s.x), s.nloc, (float)x_value, s.stream));
+        } else {
+            HIPT(fill_f64(reinterpret_cast<double *>(s.b), s.nloc, b_value, s.stream));
+            HIPT(fill_f64(reinterpret_cast<double *>(s.x), s.nloc, x_value, s.stream));
+        }
+    }
+    TRY(sync_all(c));
+    c->state = ST_IDLE;
+    return CGX_OK;
 }
 
 int cgx_destroy(cgx_ctx *ctx) {
@@ -734,6 +867,7 @@ int cgx_set_rows(cgx_ctx *c, int64_t row0, int64_t nrows, const void *A_rows, in
     if (row0 < 0 || nrows < 0 || row0 + nrows > c->n)
         return fail(CGX_ERR_SHAPE, "rows [%lld, %lld) outside [0, %lld)", (long long)row0,
                     (long long)(row0 + nrows), (long long)c->n);
+    if (A_rows && c->op == OP_POISSON) return fail(CGX_ERR_ARG, "the Poisson operator is matrix-free: A must be NULL");
     if (A_rows && lda_host < c->n) return fail(CGX_ERR_ARG, "lda_host (%lld) < n", (long long)lda_host);
     const size_t es = (size_t)c->es;
     for (auto &s : c->sh) {
@@ -770,6 +904,7 @@ int cgx_set_system(cgx_ctx *c, const void *A, const void *b, const void *x0) {
 
 int cgx_generate_spd(cgx_ctx *c, uint64_t seed) {
     if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
+    if (c->op == OP_POISSON) return fail(CGX_ERR_ARG, "the Poisson operator has no matrix to generate (use cgx_fill)");
     for (auto &s : c->sh) {
         TRY(set_dev(s));
         if (s.A_host) {
@@ -900,7 +1035,7 @@ void *cgx_stream(cgx_ctx *c) { return c ? (void *)c->sh[0].stream : nullptr; }
 
 int cgx_set_matvec_plan(cgx_ctx *c, int rows_per_wave, int chunks_in_flight, int nontemporal, int blocks_per_cu) {
     if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
-    if (f32ref(c)) return fail(CGX_ERR_ARG, "the fp32-ref matVec has no tunable plan");
+    if (f32ref(c) || c->op != OP_DENSE) return fail(CGX_ERR_ARG, "only the fp64 dense matVec has a tunable plan");
     const int R = rows_per_wave, U = chunks_in_flight;
     if (R != 1 && R != 2 && R != 4 && R != 8) return fail(CGX_ERR_ARG, "rows_per_wave must be 1, 2, 4 or 8");
     if (U != 2 && U != 4 && U != 8) return fail(CGX_ERR_ARG, "chunks_in_flight must be 2, 4 or 8");

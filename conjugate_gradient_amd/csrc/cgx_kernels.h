@@ -50,6 +50,13 @@ hipError_t gen_spd_f64(int64_t n, int64_t lda, int64_t row0, int64_t nrows, uint
 // out = sum_{q<cnt} (8-byte slot q of in), in q order (one thread): rank-ordered combine.
 hipError_t sum_ordered_f64(const double *in, int cnt, double *out, hipStream_t s);
 
+// 5-point Poisson A.p on a slab of mloc grid rows of width m; ph has one halo
+// row above and below.  *dot_out = ph[m..] . Ap when dot_out != nullptr.
+hipError_t stencil5_f64(const double *ph, int64_t mloc, int64_t m, double *Ap, double *dot_out, const RedWs &ws,
+                        hipStream_t s);
+hipError_t fill_f64(double *p, int64_t n, double v, hipStream_t s);
+hipError_t fill_f32(float *p, int64_t n, float v, hipStream_t s);
+
 // ---- fp32, serialConjugate.c operation order ---------------------------------
 hipError_t matvec_ref_f32(const float *A, int64_t lda, int64_t rows, int64_t cols,
                           const float *v, float *out, hipStream_t s);

@@ -254,6 +254,57 @@ __global__ __launch_bounds__(kNT) void k_gen_spd(int64_t n, int64_t lda, int64_t
 
 // Scalars combined in rank order: ((in0 + in1) + in2) + ...  Inputs sit in
 // 8-byte slots (a float at the slot start for F32_REF): element q at in[q*stride].
+// ---------------------------------------------------------------------------
+// matrix-free 5-point Poisson A.p on a slab (configs[4]; no reference
+// counterpart).  ph = p with one halo row above and below: rows 0 and
+// mloc+1 are the neighbours' boundary rows (zero at the domain boundary).
+// Each block owns a contiguous run of grid rows and sweeps them in order so
+// the rows above/below are L2/MALL hits; a thread handles column pairs
+// (16-B loads of the centre/up/down rows, 8-B loads of the two side points).
+// Fused: *dot_out = p . Ap (same last-block reduction as the matVec).
+// ---------------------------------------------------------------------------
+template <bool VEC>
+__global__ __launch_bounds__(kNT) void k_stencil5_f64(const double *__restrict__ ph, int64_t mloc, int64_t m,
+                                                      double *__restrict__ Ap, double *dot_out, double *partials,
+                                                      unsigned *ticket) {
+    const int64_t rows_per_block = (mloc + gridDim.x - 1) / gridDim.x;
+    const int64_t i0 = (int64_t)blockIdx.x * rows_per_block;
+    const int64_t i1 = (i0 + rows_per_block < mloc) ? i0 + rows_per_block : mloc;
+    double acc = 0.0;
+    for (int64_t i = i0; i < i1; ++i) {
+        const double *up = ph + i * m, *ce = up + m, *dn = ce + m;
+        double *out = Ap + i * m;
+        if constexpr (VEC) {  // m even: every row starts 16-B aligned
+            for (int64_t q = threadIdx.x; q < (m >> 1); q += kNT) {
+                const int64_t j = 2 * q;
+                const d2 c = *reinterpret_cast<const d2 *>(ce + j);
+                const d2 u = *reinterpret_cast<const d2 *>(up + j);
+                const d2 d = *reinterpret_cast<const d2 *>(dn + j);
+                const double l = (j > 0) ? ce[j - 1] : 0.0;
+                const double r = (j + 2 < m) ? ce[j + 2] : 0.0;
+                d2 o;
+                o.x = 4.0 * c.x - u.x - d.x - l - c.y;
+                o.y = 4.0 * c.y - u.y - d.y - c.x - r;
+                *reinterpret_cast<d2 *>(out + j) = o;
+                if (dot_out) acc += c.x * o.x + c.y * o.y;
+            }
+        } else {
+            for (int64_t j = threadIdx.x; j < m; j += kNT) {
+                const double c = ce[j];
+                const double o = 4.0 * c - up[j] - dn[j] - ((j > 0) ? ce[j - 1] : 0.0) - ((j + 1 < m) ? ce[j + 1] : 0.0);
+                out[j] = o;
+                if (dot_out) acc += c * o;
+            }
+        }
+    }
+    if (dot_out) grid_sum_last_block(acc, partials, ticket, dot_out);
+}
+
+template <typename T>
+__global__ __launch_bounds__(kNT) void k_fill(T *p, int64_t n, T v) {
+    for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kNT) p[i] = v;
+}
+
 template <typename T>
 __global__ void k_sum_ordered(const T *in, int cnt, int stride, T *out) {
 #pragma clang fp contract(off)
@@ -516,6 +567,31 @@ hipError_t gen_spd_f32(int64_t n, int64_t lda, int64_t row0, int64_t nrows, uint
     if (nrows <= 0) return hipSuccess;
     hipLaunchKernelGGL(k_gen_spd<float>, dim3(grid_1d(nrows, 1, 65536)), dim3(kNT), 0, s, n, lda, row0,
                        nrows, mix64(seed), mix64(seed + 1), A, b);
+    return hipGetLastError();
+}
+
+hipError_t stencil5_f64(const double *ph, int64_t mloc, int64_t m, double *Ap, double *dot_out, const RedWs &ws,
+                        hipStream_t s) {
+    if (mloc <= 0) return hipSuccess;
+    const unsigned grid = (unsigned)std::min<int64_t>(mloc, 2048);
+    if ((m & 1) == 0)
+        hipLaunchKernelGGL(k_stencil5_f64<true>, dim3(grid), dim3(kNT), 0, s, ph, mloc, m, Ap, dot_out, ws.partials,
+                           ws.tickets + T_MATVEC);
+    else
+        hipLaunchKernelGGL(k_stencil5_f64<false>, dim3(grid), dim3(kNT), 0, s, ph, mloc, m, Ap, dot_out, ws.partials,
+                           ws.tickets + T_MATVEC);
+    return hipGetLastError();
+}
+
+hipError_t fill_f64(double *p, int64_t n, double v, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_fill<double>, dim3(grid_vec(n)), dim3(kNT), 0, s, p, n, v);
+    return hipGetLastError();
+}
+
+hipError_t fill_f32(float *p, int64_t n, float v, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_fill<float>, dim3(grid_vec(n)), dim3(kNT), 0, s, p, n, v);
     return hipGetLastError();
 }
 

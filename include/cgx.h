@@ -120,6 +120,18 @@ int cgx_get_unique_id(cgx_unique_id *id);
 int cgx_create_rank(cgx_ctx **ctx, int64_t n, int rank, int nranks,
                     const cgx_unique_id *id, int device, int flags);
 
+/* Matrix-free 5-point 2D Poisson operator (configs[4]; no reference
+ * counterpart): n = m*m unknowns on an m x m interior grid, Dirichlet zero
+ * boundary, (A u)_ij = 4u_ij - u_(i-1)j - u_(i+1)j - u_i(j-1) - u_i(j+1),
+ * natural row-major order.  Multi-GPU splits the grid into slabs of m/P grid
+ * rows (m % P == 0) and exchanges one halo row with each neighbour per
+ * iteration (ncclSend/Recv in rank mode) instead of allgathering p.
+ * CGX_F64 only; set b / x0 with cgx_fill or cgx_set_rows (A must be NULL). */
+int cgx_create_poisson(cgx_ctx **ctx, int64_t m, int device, int flags);
+int cgx_create_poisson_multi(cgx_ctx **ctx, int64_t m, int nshards, const int *devices, int flags);
+int cgx_create_poisson_rank(cgx_ctx **ctx, int64_t m, int rank, int nranks,
+                            const cgx_unique_id *id, int device, int flags);
+
 int cgx_destroy(cgx_ctx *ctx);
 int cgx_get_info(const cgx_ctx *ctx, cgx_info *info);
 
@@ -136,6 +148,8 @@ int cgx_set_system(cgx_ctx *ctx, const void *A, const void *b, const void *x0);
  *   A_ij = 0.5*(u(i,j)+u(j,i)) + n*[i==j],  b_i = u_b(i),  x0 = 0,
  * u = splitmix64-finalised counter hash -> 53-bit uniform in [0,1). */
 int cgx_generate_spd(cgx_ctx *ctx, uint64_t seed);
+/* b = b_value and x0 = x_value everywhere (e.g. the Poisson config: b = 1, x0 = 0). */
+int cgx_fill(cgx_ctx *ctx, double b_value, double x_value);
 /* x (n entries, replicated result like parallel_cg.c's local_vectorX). */
 int cgx_get_x(cgx_ctx *ctx, void *x);
 int cgx_set_x(cgx_ctx *ctx, const void *x);

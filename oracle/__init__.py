@@ -62,6 +62,9 @@ def lib() -> ctypes.CDLL:
         L.oracle_cg_f64.argtypes = [i64, vp, vp, vp, i64, f64, ctypes.POINTER(OracleStats)]
         L.oracle_cg_f64.restype = ctypes.c_int
         L.oracle_set_threads.argtypes = [ctypes.c_int]
+        L.oracle_poisson_apply.argtypes = [i64, vp, vp]
+        L.oracle_cg_poisson_f64.argtypes = [i64, vp, vp, i64, f64, ctypes.POINTER(OracleStats)]
+        L.oracle_cg_poisson_f64.restype = ctypes.c_int
         _LIB = L
     return _LIB
 
@@ -150,6 +153,43 @@ def cg_f64(A, b, x0, max_iter: int = -1, eps: float = 1e-10):
     if rc != 0:
         raise RuntimeError(f"oracle_cg_f64 rc={rc}")
     return x, st
+
+
+def poisson_apply(m: int, p: np.ndarray) -> np.ndarray:
+    p = np.ascontiguousarray(p, np.float64)
+    out = np.empty(m * m, np.float64)
+    lib().oracle_poisson_apply(m, _p(p), _p(out))
+    return out
+
+
+def cg_poisson_f64(m: int, b, x0, max_iter: int = -1, eps: float = 1e-10):
+    """Matrix-free 5-point Poisson CG in double; returns (x, OracleStats)."""
+    b = np.ascontiguousarray(b, np.float64)
+    x = np.array(x0, dtype=np.float64, copy=True)
+    st = OracleStats()
+    rc = lib().oracle_cg_poisson_f64(m, _p(b), _p(x), max_iter, eps, ctypes.byref(st))
+    if rc != 0:
+        raise RuntimeError(f"oracle_cg_poisson_f64 rc={rc}")
+    return x, st
+
+
+def poisson_dense(m: int) -> np.ndarray:
+    """The same operator as an explicit (m*m) x (m*m) matrix (small m only)."""
+    n = m * m
+    A = np.zeros((n, n))
+    for i in range(m):
+        for j in range(m):
+            k = i * m + j
+            A[k, k] = 4.0
+            if i > 0:
+                A[k, k - m] = -1.0
+            if i < m - 1:
+                A[k, k + m] = -1.0
+            if j > 0:
+                A[k, k - 1] = -1.0
+            if j < m - 1:
+                A[k, k + 1] = -1.0
+    return A
 
 
 def conjgrad_numpy(A, b, x, tol: float = 1e-10, max_iter: int | None = None):

@@ -315,3 +315,61 @@ int oracle_cg_f64(int64_t n, const double *A, const double *b, double *x,
     free(Av); free(r); free(p);
     return 0;
 }
+
+/* ======================================================================= */
+/* matrix-free 5-point Poisson (configs[4])                                 */
+/* ======================================================================= */
+void oracle_poisson_apply(int64_t m, const double *p, double *out) {
+#pragma omp parallel for schedule(static) num_threads(g_threads)
+    for (int64_t i = 0; i < m; ++i) {
+        for (int64_t j = 0; j < m; ++j) {
+            const size_t k = (size_t)i * m + j;
+            double v = 4.0 * p[k];
+            if (i > 0) v -= p[k - m];
+            if (i < m - 1) v -= p[k + m];
+            if (j > 0) v -= p[k - 1];
+            if (j < m - 1) v -= p[k + 1];
+            out[k] = v;
+        }
+    }
+}
+
+int oracle_cg_poisson_f64(int64_t m, const double *b, double *x, int64_t max_iter, double eps,
+                          oracle_stats *st) {
+    const int64_t n = m * m;
+    if (max_iter < 0) max_iter = n;
+    double *Av = (double *)malloc((size_t)n * sizeof(double));
+    double *r = (double *)malloc((size_t)n * sizeof(double));
+    double *p = (double *)malloc((size_t)n * sizeof(double));
+    if (!Av || !r || !p) { free(Av); free(r); free(p); return -1; }
+    double t0 = now_s();
+    oracle_poisson_apply(m, x, Av);
+    for (int64_t i = 0; i < n; ++i) { r[i] = b[i] - Av[i]; p[i] = r[i]; }
+    double rsold = oracle_dot_f64(n, r, r);
+    double t1 = now_s();
+    int64_t iters = 0;
+    int converged = 0;
+    double rr = rsold;
+    for (int64_t k = 0; k < max_iter; ++k) {
+        oracle_poisson_apply(m, p, Av);
+        double alpha = rsold / oracle_dot_f64(n, p, Av);
+        for (int64_t i = 0; i < n; ++i) x[i] = x[i] + alpha * p[i];
+        for (int64_t i = 0; i < n; ++i) r[i] = r[i] - alpha * Av[i];
+        rr = oracle_dot_f64(n, r, r);
+        iters = k + 1;
+        if (eps >= 0.0 && sqrt(rr) < eps) { converged = 1; break; }
+        double beta = rr / rsold;
+        for (int64_t i = 0; i < n; ++i) p[i] = r[i] + beta * p[i];
+        rsold = rr;
+    }
+    double t2 = now_s();
+    if (st) {
+        st->iterations = iters;
+        st->converged = converged;
+        st->rr = rr;
+        st->t_init_s = t1 - t0;
+        st->t_loop_s = t2 - t1;
+    }
+    free(Av); free(r); free(p);
+    return 0;
+}

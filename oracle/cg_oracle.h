@@ -82,6 +82,15 @@ int oracle_cg_f32ref(int64_t n, const float *A, const float *b, float *x,
 int oracle_cg_f64(int64_t n, const double *A, const double *b, double *x,
                   int64_t max_iter, double eps, oracle_stats *st);
 
+/* ---- matrix-free 2D Poisson (configs[4], no reference counterpart) ------ */
+/* out = A p for the 5-point Laplacian on an m x m interior grid, Dirichlet
+ * zero boundary, natural row-major order: 4 p_ij - p_(i-1)j - p_(i+1)j
+ * - p_i(j-1) - p_i(j+1) with p = 0 outside the grid. */
+void oracle_poisson_apply(int64_t m, const double *p, double *out);
+/* conjgrad.m's loop (oracle_cg_f64) with that operator; n = m*m. */
+int oracle_cg_poisson_f64(int64_t m, const double *b, double *x, int64_t max_iter, double eps,
+                          oracle_stats *st);
+
 /* threads used by oracle_cg_f64's matVec (rows are independent, so results
  * do not depend on it).  f32ref is always single-threaded, like the reference. */
 void oracle_set_threads(int nthreads);

@@ -226,3 +226,56 @@ def test_host_streamed_matvec(monkeypatch, shards):
     ref, sr = oracle.cg_f32ref(A32, b32, x032, nparts=len(shards) if shards else 1)
     assert st32.iterations == sr.iterations
     assert np.array_equal(x32, ref)
+
+
+# ---------------------------------------------------------------------------
+# matrix-free 5-point Poisson (configs[4]); oracle: oracle_cg_poisson_f64
+# ---------------------------------------------------------------------------
+@pytest.mark.parametrize("m,shards", [(1, None), (7, None), (64, None), (64, [0, 0]), (64, [0] * 4), (96, [0] * 8)])
+def test_poisson_matches_oracle(m, shards):
+    n = m * m
+    with cg.Solver(None, poisson_m=m, devices=shards) as s:
+        s.fill(1.0, 0.0)
+        x, st = s.solve(None, eps=1e-10)
+        rn, bn = s.residual_norm()
+    xo, so = oracle.cg_poisson_f64(m, np.ones(n), np.zeros(n), eps=1e-10)
+    assert st.iterations == so.iterations
+    assert rel(x, xo) <= TOL
+    assert rn <= 1e-9 * bn
+    assert np.linalg.norm(oracle.poisson_apply(m, x) - 1.0) <= 1e-9 * np.sqrt(n)
+
+
+def test_poisson_equals_dense_operator():
+    """The stencil is the explicit matrix: same solve through the dense path."""
+    m = 16
+    A = oracle.poisson_dense(m)
+    b = np.random.default_rng(0).random(m * m)
+    with cg.Solver(None, poisson_m=m) as s:
+        s.set_rows(0, None, b, np.zeros(m * m))
+        xs, sts = s.solve(None, eps=1e-12)
+    xd = np.zeros(m * m)
+    std = cg.conjugrad(A, b, xd, eps=1e-12)
+    assert sts.iterations == std.iterations
+    assert rel(xs, xd) <= 1e-12
+
+
+def test_poisson_rank_mode_world1_and_fixed_count():
+    m = 128
+    with cg.Solver(None, poisson_m=m, rank=0, nranks=1, unique_id=cg.get_unique_id()) as s:
+        s.fill(1.0, 0.0)
+        x, st = s.solve(None, eps=-1.0, max_iter=150)
+    xo, so = oracle.cg_poisson_f64(m, np.ones(m * m), np.zeros(m * m), eps=-1.0, max_iter=150)
+    assert st.iterations == so.iterations == 150
+    assert rel(x, xo) <= 1e-9
+
+
+def test_poisson_rejects_bad_use():
+    with pytest.raises(cg.CgxError):
+        cg.Solver(None, poisson_m=10, devices=[0, 0, 0])   # 10 % 3
+    with pytest.raises(cg.CgxError):
+        cg.Solver(None, poisson_m=8, flags=cg.CGX_F32_REF)
+    with cg.Solver(None, poisson_m=8) as s:
+        with pytest.raises(cg.CgxError):
+            s.generate_spd(1)
+        with pytest.raises(cg.CgxError):
+            s.set_rows(0, np.zeros((64, 64)), np.ones(64))

@@ -115,3 +115,17 @@ def test_fixed_count_mode():
     A, b, x0 = case("spd512", np.float64)
     _, st = oracle.cg_f64(A, b, x0, eps=-1.0, max_iter=12)
     assert st.iterations == 12 and st.converged == 0
+
+
+def test_poisson_oracle_is_the_laplacian():
+    m = 12
+    A = oracle.poisson_dense(m)
+    assert np.array_equal(A, A.T)
+    assert np.all(np.linalg.eigvalsh(A) > 0)
+    p = np.random.default_rng(2).random(m * m)
+    assert np.abs(A @ p - oracle.poisson_apply(m, p)).max() <= 1e-14
+    b = np.ones(m * m)
+    x, st = oracle.cg_poisson_f64(m, b, np.zeros(m * m), eps=1e-10)
+    xn, itn = oracle.conjgrad_numpy(A, b, np.zeros(m * m), tol=1e-10)
+    assert st.iterations == itn
+    assert np.linalg.norm(x - xn) <= 1e-12 * np.linalg.norm(xn)
