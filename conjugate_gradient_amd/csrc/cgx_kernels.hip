@@ -163,23 +163,72 @@ __global__ __launch_bounds__(kNT) void k_matvec_f64(
     if (pown) grid_sum_last_block(dacc, partials, ticket, dot_out);
 }
 
+// Vector kernels.  VEC: every pointer 16-B aligned -> 16-B loads/stores of
+// element pairs, two pairs in flight per thread per step; else scalar.  The
+// odd tail element (n odd) is done by thread 0 of block 0.  Sums are
+// per-thread in a fixed order, then the deterministic grid reduction.
+__device__ __forceinline__ d2 ld2(const double *p) { return *reinterpret_cast<const d2 *>(p); }
+__device__ __forceinline__ void st2(double *p, d2 v) { *reinterpret_cast<d2 *>(p) = v; }
+
+// Vector kernels.  VEC (every pointer 16-B aligned): a block step covers
+// kVU * kNT consecutive element pairs; each thread loads its kVU pairs of
+// every input (16-B loads, all issued before any store), computes, stores.
+// Otherwise a scalar grid-stride loop.  The odd tail element of the VEC
+// path is done by thread 0 of block 0.  Per-thread sums run in a fixed
+// order, then the deterministic grid reduction.
+constexpr int kVU = 4;
+
+#define CGX_VEC_LOOP_BEGIN                                                                   \
+    const int64_t npairs = n >> 1;                                                           \
+    const int64_t step = (int64_t)gridDim.x * kNT * kVU;                                     \
+    for (int64_t base = (int64_t)blockIdx.x * kNT * kVU + threadIdx.x; base < npairs; base += step) { \
+        bool ok[kVU];                                                                        \
+        _Pragma("unroll") for (int u = 0; u < kVU; ++u) ok[u] = base + u * kNT < npairs;
+#define CGX_VEC_LOOP_END }
+
 // residual x2 + vecVec (serialConjugate.c:210-212)
+template <bool VEC>
 __global__ __launch_bounds__(kNT) void k_residual_f64(int64_t n, const double *__restrict__ b,
                                                       const double *__restrict__ Ax,
                                                       double *__restrict__ r, double *__restrict__ p,
                                                       double *rr_out, double *partials,
                                                       unsigned *ticket) {
     double acc = 0.0;
-    for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kNT) {
-        const double ri = b[i] - Ax[i];
-        r[i] = ri;
-        if (p) p[i] = ri;
-        acc += ri * ri;
+    if constexpr (VEC) {
+        CGX_VEC_LOOP_BEGIN
+        d2 bv[kVU], av[kVU];
+#pragma unroll
+        for (int u = 0; u < kVU; ++u)
+            if (ok[u]) { const int64_t i = 2 * (base + u * kNT); bv[u] = ld2(b + i); av[u] = ld2(Ax + i); }
+#pragma unroll
+        for (int u = 0; u < kVU; ++u)
+            if (ok[u]) {
+                const int64_t i = 2 * (base + u * kNT);
+                const d2 ri = bv[u] - av[u];
+                st2(r + i, ri);
+                if (p) st2(p + i, ri);
+                acc += ri.x * ri.x + ri.y * ri.y;
+            }
+        CGX_VEC_LOOP_END
+        if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+            const double ri = b[n - 1] - Ax[n - 1];
+            r[n - 1] = ri;
+            if (p) p[n - 1] = ri;
+            acc += ri * ri;
+        }
+    } else {
+        for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kNT) {
+            const double ri = b[i] - Ax[i];
+            r[i] = ri;
+            if (p) p[i] = ri;
+            acc += ri * ri;
+        }
     }
     if (rr_out) grid_sum_last_block(acc, partials, ticket, rr_out);
 }
 
 // x += alpha p; r -= alpha Ap; r.r  (serialConjugate.c:219-234, conjgrad.m:8-11)
+template <bool VEC>
 __global__ __launch_bounds__(kNT) void k_update_xr_f64(int64_t n, double *__restrict__ x,
                                                        double *__restrict__ r,
                                                        const double *__restrict__ p,
@@ -189,30 +238,86 @@ __global__ __launch_bounds__(kNT) void k_update_xr_f64(int64_t n, double *__rest
                                                        unsigned *ticket) {
     const double alpha = *rsold / *pAp;
     double acc = 0.0;
-    for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kNT) {
-        x[i] = x[i] + alpha * p[i];
-        const double ri = r[i] - alpha * Ap[i];
-        r[i] = ri;
-        acc += ri * ri;
+    if constexpr (VEC) {
+        CGX_VEC_LOOP_BEGIN
+        d2 xv[kVU], rv[kVU], pv[kVU], av[kVU];
+#pragma unroll
+        for (int u = 0; u < kVU; ++u)
+            if (ok[u]) {
+                const int64_t i = 2 * (base + u * kNT);
+                xv[u] = ld2(x + i); rv[u] = ld2(r + i); pv[u] = ld2(p + i); av[u] = ld2(Ap + i);
+            }
+#pragma unroll
+        for (int u = 0; u < kVU; ++u)
+            if (ok[u]) {
+                const int64_t i = 2 * (base + u * kNT);
+                st2(x + i, xv[u] + alpha * pv[u]);
+                const d2 ri = rv[u] - alpha * av[u];
+                st2(r + i, ri);
+                acc += ri.x * ri.x + ri.y * ri.y;
+            }
+        CGX_VEC_LOOP_END
+        if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+            const int64_t i = n - 1;
+            x[i] = x[i] + alpha * p[i];
+            const double ri = r[i] - alpha * Ap[i];
+            r[i] = ri;
+            acc += ri * ri;
+        }
+    } else {
+        for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kNT) {
+            x[i] = x[i] + alpha * p[i];
+            const double ri = r[i] - alpha * Ap[i];
+            r[i] = ri;
+            acc += ri * ri;
+        }
     }
     grid_sum_last_block(acc, partials, ticket, rr_out);
 }
 
 // p = r + beta p  (serialConjugate.c:239-243, conjgrad.m:15)
+template <bool VEC>
 __global__ __launch_bounds__(kNT) void k_update_p_f64(int64_t n, double *__restrict__ p,
                                                       const double *__restrict__ r,
                                                       const double *rr, const double *rsold) {
     const double beta = *rr / *rsold;
-    for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kNT)
-        p[i] = r[i] + beta * p[i];
+    if constexpr (VEC) {
+        CGX_VEC_LOOP_BEGIN
+        d2 pv[kVU], rv[kVU];
+#pragma unroll
+        for (int u = 0; u < kVU; ++u)
+            if (ok[u]) { const int64_t i = 2 * (base + u * kNT); pv[u] = ld2(p + i); rv[u] = ld2(r + i); }
+#pragma unroll
+        for (int u = 0; u < kVU; ++u)
+            if (ok[u]) st2(p + 2 * (base + u * kNT), rv[u] + beta * pv[u]);
+        CGX_VEC_LOOP_END
+        if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) p[n - 1] = r[n - 1] + beta * p[n - 1];
+    } else {
+        for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kNT)
+            p[i] = r[i] + beta * p[i];
+    }
 }
 
+template <bool VEC>
 __global__ __launch_bounds__(kNT) void k_dot_f64(int64_t n, const double *__restrict__ a,
                                                  const double *__restrict__ b, double *out,
                                                  double *partials, unsigned *ticket) {
     double acc = 0.0;
-    for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kNT)
-        acc += a[i] * b[i];
+    if constexpr (VEC) {
+        CGX_VEC_LOOP_BEGIN
+        d2 av[kVU], bv[kVU];
+#pragma unroll
+        for (int u = 0; u < kVU; ++u)
+            if (ok[u]) { const int64_t i = 2 * (base + u * kNT); av[u] = ld2(a + i); bv[u] = ld2(b + i); }
+#pragma unroll
+        for (int u = 0; u < kVU; ++u)
+            if (ok[u]) acc += av[u].x * bv[u].x + av[u].y * bv[u].y;
+        CGX_VEC_LOOP_END
+        if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) acc += a[n - 1] * b[n - 1];
+    } else {
+        for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kNT)
+            acc += a[i] * b[i];
+    }
     grid_sum_last_block(acc, partials, ticket, out);
 }
 
@@ -263,10 +368,56 @@ __global__ __launch_bounds__(kNT) void k_gen_spd(int64_t n, int64_t lda, int64_t
 // (16-B loads of the centre/up/down rows, 8-B loads of the two side points).
 // Fused: *dot_out = p . Ap (same last-block reduction as the matVec).
 // ---------------------------------------------------------------------------
-template <bool VEC>
-__global__ __launch_bounds__(kNT) void k_stencil5_f64(const double *__restrict__ ph, int64_t mloc, int64_t m,
-                                                      double *__restrict__ Ap, double *dot_out, double *partials,
-                                                      unsigned *ticket) {
+// Even m: column-strip marching.  A block owns a strip of 2*kNT columns and a
+// run of rows; each thread holds a column pair and walks down the rows with
+// the up/centre rows in registers, so every p element is loaded once (plus
+// two halo rows per run).  The left/right neighbours come from the adjacent
+// lanes by wave shuffle; only lanes 0 / 63 load them (L1 hits).  The next
+// row is prefetched one step ahead.
+__global__ __launch_bounds__(kNT) void k_stencil5_strip_f64(const double *__restrict__ ph, int64_t mloc, int64_t m,
+                                                            int64_t nstrips, int64_t rows_per_block,
+                                                            double *__restrict__ Ap, double *dot_out,
+                                                            double *partials, unsigned *ticket) {
+    const int lane = threadIdx.x & 63;
+    const int64_t strip = blockIdx.x % nstrips, chunk = blockIdx.x / nstrips;
+    const int64_t j = strip * (2 * kNT) + 2 * threadIdx.x;
+    const bool valid = j < m;
+    const int64_t i0 = chunk * rows_per_block;
+    const int64_t i1 = (i0 + rows_per_block < mloc) ? i0 + rows_per_block : mloc;
+    double acc = 0.0;
+    if (i0 < i1) {
+        const d2 zero = (d2)(0.0);
+        const double *col = ph + j;
+        d2 up = valid ? ld2(col + i0 * m) : zero;
+        d2 ce = valid ? ld2(col + (i0 + 1) * m) : zero;
+        d2 dn = valid ? ld2(col + (i0 + 2) * m) : zero;
+        for (int64_t i = i0; i < i1; ++i) {
+            // prefetch the row after next while this row is computed
+            const d2 nx = (valid && i + 1 < i1) ? ld2(col + (i + 3) * m) : zero;
+            double l = __shfl_up(ce.y, 1, 64);
+            double r = __shfl_down(ce.x, 1, 64);
+            const double *crow = ph + (i + 1) * m;
+            if (lane == 0) l = (j > 0 && valid) ? crow[j - 1] : 0.0;
+            if (lane == 63) r = (j + 2 < m) ? crow[j + 2] : 0.0;
+            d2 o;
+            o.x = 4.0 * ce.x - up.x - dn.x - l - ce.y;
+            o.y = 4.0 * ce.y - up.y - dn.y - ce.x - r;
+            if (valid) {
+                st2(Ap + i * m + j, o);
+                if (dot_out) acc += ce.x * o.x + ce.y * o.y;
+            }
+            up = ce;
+            ce = dn;
+            dn = nx;
+        }
+    }
+    if (dot_out) grid_sum_last_block(acc, partials, ticket, dot_out);
+}
+
+// Odd m (rows not 16-B aligned): a block walks a run of rows, one column per thread.
+__global__ __launch_bounds__(kNT) void k_stencil5_rows_f64(const double *__restrict__ ph, int64_t mloc, int64_t m,
+                                                           double *__restrict__ Ap, double *dot_out, double *partials,
+                                                           unsigned *ticket) {
     const int64_t rows_per_block = (mloc + gridDim.x - 1) / gridDim.x;
     const int64_t i0 = (int64_t)blockIdx.x * rows_per_block;
     const int64_t i1 = (i0 + rows_per_block < mloc) ? i0 + rows_per_block : mloc;
@@ -274,27 +425,11 @@ __global__ __launch_bounds__(kNT) void k_stencil5_f64(const double *__restrict__
     for (int64_t i = i0; i < i1; ++i) {
         const double *up = ph + i * m, *ce = up + m, *dn = ce + m;
         double *out = Ap + i * m;
-        if constexpr (VEC) {  // m even: every row starts 16-B aligned
-            for (int64_t q = threadIdx.x; q < (m >> 1); q += kNT) {
-                const int64_t j = 2 * q;
-                const d2 c = *reinterpret_cast<const d2 *>(ce + j);
-                const d2 u = *reinterpret_cast<const d2 *>(up + j);
-                const d2 d = *reinterpret_cast<const d2 *>(dn + j);
-                const double l = (j > 0) ? ce[j - 1] : 0.0;
-                const double r = (j + 2 < m) ? ce[j + 2] : 0.0;
-                d2 o;
-                o.x = 4.0 * c.x - u.x - d.x - l - c.y;
-                o.y = 4.0 * c.y - u.y - d.y - c.x - r;
-                *reinterpret_cast<d2 *>(out + j) = o;
-                if (dot_out) acc += c.x * o.x + c.y * o.y;
-            }
-        } else {
-            for (int64_t j = threadIdx.x; j < m; j += kNT) {
-                const double c = ce[j];
-                const double o = 4.0 * c - up[j] - dn[j] - ((j > 0) ? ce[j - 1] : 0.0) - ((j + 1 < m) ? ce[j + 1] : 0.0);
-                out[j] = o;
-                if (dot_out) acc += c * o;
-            }
+        for (int64_t j = threadIdx.x; j < m; j += kNT) {
+            const double c = ce[j];
+            const double o = 4.0 * c - up[j] - dn[j] - ((j > 0) ? ce[j - 1] : 0.0) - ((j + 1 < m) ? ce[j + 1] : 0.0);
+            out[j] = o;
+            if (dot_out) acc += c * o;
         }
     }
     if (dot_out) grid_sum_last_block(acc, partials, ticket, dot_out);
@@ -446,8 +581,10 @@ unsigned grid_1d(int64_t n, int per_block, unsigned cap) {
     return (unsigned)g;
 }
 
-// Grid of the vector kernels: <= kMaxRedBlocks (the partial slots), ~4 blocks/CU.
-unsigned grid_vec(int64_t n) { return grid_1d(n, kNT, 1024); }
+// Grid of the vector kernels: <= kMaxRedBlocks (the partial slots), <= 8 blocks/CU.
+unsigned grid_vec(int64_t n) { return grid_1d((n + 1) / 2, kNT * kVU, 2048); }
+
+inline bool al16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 using MvFn = void (*)(const double *, int64_t, int64_t, int64_t, int64_t, const double *, double *,
                       const double *, double *, double *, unsigned *);
@@ -528,29 +665,34 @@ hipError_t matvec_f64(const MatvecPlan &pl, const double *A, int64_t lda, int64_
 
 hipError_t residual_f64(int64_t n, const double *b, const double *Ax, double *r, double *p,
                         double *rr_out, const RedWs &ws, hipStream_t s) {
-    hipLaunchKernelGGL(k_residual_f64, dim3(grid_vec(n)), dim3(kNT), 0, s, n, b, Ax, r, p, rr_out,
-                       ws.partials, ws.tickets + T_RESID);
+    const bool vec = al16(b) && al16(Ax) && al16(r) && al16(p);
+    hipLaunchKernelGGL(vec ? k_residual_f64<true> : k_residual_f64<false>, dim3(grid_vec(n)), dim3(kNT), 0, s, n, b,
+                       Ax, r, p, rr_out, ws.partials, ws.tickets + T_RESID);
     return hipGetLastError();
 }
 
 hipError_t update_xr_f64(int64_t n, double *x, double *r, const double *p, const double *Ap,
                          const double *rsold, const double *pAp, double *rr_out, const RedWs &ws,
                          hipStream_t s) {
-    hipLaunchKernelGGL(k_update_xr_f64, dim3(grid_vec(n)), dim3(kNT), 0, s, n, x, r, p, Ap, rsold, pAp,
-                       rr_out, ws.partials, ws.tickets + T_XR);
+    const bool vec = al16(x) && al16(r) && al16(p) && al16(Ap);
+    hipLaunchKernelGGL(vec ? k_update_xr_f64<true> : k_update_xr_f64<false>, dim3(grid_vec(n)), dim3(kNT), 0, s, n,
+                       x, r, p, Ap, rsold, pAp, rr_out, ws.partials, ws.tickets + T_XR);
     return hipGetLastError();
 }
 
 hipError_t update_p_f64(int64_t n, double *p, const double *r, const double *rr, const double *rsold,
                         hipStream_t s) {
-    hipLaunchKernelGGL(k_update_p_f64, dim3(grid_vec(n)), dim3(kNT), 0, s, n, p, r, rr, rsold);
+    const bool vec = al16(p) && al16(r);
+    hipLaunchKernelGGL(vec ? k_update_p_f64<true> : k_update_p_f64<false>, dim3(grid_vec(n)), dim3(kNT), 0, s, n, p,
+                       r, rr, rsold);
     return hipGetLastError();
 }
 
 hipError_t dot_f64(int64_t n, const double *a, const double *b, double *out, const RedWs &ws,
                    hipStream_t s) {
-    hipLaunchKernelGGL(k_dot_f64, dim3(grid_vec(n)), dim3(kNT), 0, s, n, a, b, out, ws.partials,
-                       ws.tickets + T_DOT);
+    const bool vec = al16(a) && al16(b);
+    hipLaunchKernelGGL(vec ? k_dot_f64<true> : k_dot_f64<false>, dim3(grid_vec(n)), dim3(kNT), 0, s, n, a, b, out,
+                       ws.partials, ws.tickets + T_DOT);
     return hipGetLastError();
 }
 
@@ -573,13 +715,21 @@ hipError_t gen_spd_f32(int64_t n, int64_t lda, int64_t row0, int64_t nrows, uint
 hipError_t stencil5_f64(const double *ph, int64_t mloc, int64_t m, double *Ap, double *dot_out, const RedWs &ws,
                         hipStream_t s) {
     if (mloc <= 0) return hipSuccess;
-    const unsigned grid = (unsigned)std::min<int64_t>(mloc, 2048);
-    if ((m & 1) == 0)
-        hipLaunchKernelGGL(k_stencil5_f64<true>, dim3(grid), dim3(kNT), 0, s, ph, mloc, m, Ap, dot_out, ws.partials,
+    if ((m & 1) == 0 && al16(ph) && al16(Ap)) {
+        const int64_t nstrips = (m + 2 * kNT - 1) / (2 * kNT);
+        int64_t chunks = std::max<int64_t>(1, 2048 / nstrips);
+        chunks = std::min<int64_t>(chunks, mloc);
+        const int64_t rpb = (mloc + chunks - 1) / chunks;
+        chunks = (mloc + rpb - 1) / rpb;
+        int64_t grid = nstrips * chunks;
+        if (grid > kMaxRedBlocks) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(k_stencil5_strip_f64, dim3((unsigned)grid), dim3(kNT), 0, s, ph, mloc, m, nstrips, rpb, Ap,
+                           dot_out, ws.partials, ws.tickets + T_MATVEC);
+    } else {
+        const unsigned grid = (unsigned)std::min<int64_t>(mloc, 2048);
+        hipLaunchKernelGGL(k_stencil5_rows_f64, dim3(grid), dim3(kNT), 0, s, ph, mloc, m, Ap, dot_out, ws.partials,
                            ws.tickets + T_MATVEC);
-    else
-        hipLaunchKernelGGL(k_stencil5_f64<false>, dim3(grid), dim3(kNT), 0, s, ph, mloc, m, Ap, dot_out, ws.partials,
-                           ws.tickets + T_MATVEC);
+    }
     return hipGetLastError();
 }
 
