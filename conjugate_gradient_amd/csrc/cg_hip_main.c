@@ -30,6 +30,7 @@
 #include <stdlib.h>
 #include <string.h>
 #include <time.h>
+#include <unistd.h>
 
 #include "cgx.h"
 #include "cgx_textio.h"
@@ -70,7 +71,9 @@ static int read_file(const char *path, int64_t count, int as_float, void *out, i
 
 int main(int argc, char **argv) {
     const double t_prog0 = now_s();
-    int gpus = 1, fp32ref = 0, print_x = 0, stats = 0, threads = 8;
+    int gpus = 1, fp32ref = 0, print_x = 0, stats = 0;
+    long ncpu = sysconf(_SC_NPROCESSORS_ONLN);
+    int threads = (int)(ncpu < 1 ? 1 : (ncpu > 16 ? 16 : ncpu)); /* text parsing threads */
     double eps = EPSILON_DEFAULT;
     long long max_iter = -1, n_opt = -1, spd_n = -1;
     unsigned long long seed = 42;

@@ -2,19 +2,94 @@
  * cgx_textio.c -- text reader for dimensions.txt / matrixA.txt / vectorb.txt /
  * initialguess.txt (see cgx_textio.h).  Host C, pthreads.
  *
- * Each number is converted on its own with strtof (== fscanf "%f",
- * serialConjugate.c:96) or strtod, so the result does not depend on how the
- * buffer is split among threads.  Separators are whitespace, ',' ';' and any
+ * Each number is converted on its own, exactly as strtof (== fscanf "%f",
+ * serialConjugate.c:96) or strtod would (an exact fast path below, those
+ * functions otherwise), so the result does not depend on how the buffer is
+ * split among threads.  Separators are whitespace, ',' ';' and any
  * byte >= 0x80 (so a stray UTF-8 BOM, as in the reference's
  * initialguess1.txt, is skipped rather than mis-parsed).
  */
 #define _GNU_SOURCE
 #include "cgx_textio.h"
 
+#include <math.h>
 #include <pthread.h>
+#include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+
+/* Exact fast path (Clinger): a token [+-]digits[.digits][(e|E)[+-]digits]
+ * with at most 19 significant digits m < 2^53 and decimal exponent |e| <= 22
+ * converts with ONE correctly rounded double operation, m * 10^e or
+ * m / 10^-e, both operands exact.  For float, the double is rounded once
+ * more; that is the correctly rounded float unless the double sits exactly
+ * on a float rounding midpoint, which is detected and sent to strtof.
+ * Anything else (long mantissas, big exponents, inf/nan, hex) uses
+ * strtof/strtod.  Returns 1 and sets *stop on success, 0 to fall back. */
+static const double kPow10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
+                                  1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
+
+static int fast_number(const char *p, const char *end, int as_float, void *out, int64_t idx, const char **stop) {
+    int neg = 0;
+    if (p < end && (*p == '-' || *p == '+')) { neg = (*p == '-'); ++p; }
+    uint64_t m = 0;
+    int sig = 0, frac = 0, any = 0;
+    while (p < end && *p >= '0' && *p <= '9') {
+        any = 1;
+        if (m == 0 && *p == '0') { ++p; continue; }  /* leading zeros */
+        if (++sig > 19) return 0;
+        m = m * 10 + (uint64_t)(*p - '0');
+        ++p;
+    }
+    if (p < end && *p == '.') {
+        ++p;
+        while (p < end && *p >= '0' && *p <= '9') {
+            any = 1;
+            if (m == 0 && *p == '0') { ++frac; ++p; continue; }
+            if (++sig > 19) return 0;
+            m = m * 10 + (uint64_t)(*p - '0');
+            ++frac;
+            ++p;
+        }
+    }
+    if (!any) return 0;
+    int e10 = -frac;
+    if (p < end && (*p == 'e' || *p == 'E')) {
+        ++p;
+        int eneg = 0, ev = 0, edig = 0;
+        if (p < end && (*p == '-' || *p == '+')) { eneg = (*p == '-'); ++p; }
+        while (p < end && *p >= '0' && *p <= '9') {
+            if (ev < 10000) ev = ev * 10 + (*p - '0');
+            ++edig;
+            ++p;
+        }
+        if (!edig) return 0;
+        e10 += eneg ? -ev : ev;
+    }
+    double d;
+    if (m == 0) {
+        d = 0.0;
+    } else {
+        if (m > (1ull << 53) || e10 < -22 || e10 > 22) return 0;
+        d = (double)m;
+        d = (e10 >= 0) ? d * kPow10[e10] : d / kPow10[-e10];
+    }
+    if (neg) d = -d;
+    if (as_float) {
+        const float f = (float)d;
+        if ((double)f != d) {
+            if (!isfinite(f) || fabs(d) < 1.1754943508222875e-38) return 0; /* overflow / subnormal */
+            const float g = nextafterf(f, ((double)f < d) ? INFINITY : -INFINITY);
+            if (((double)f + (double)g) * 0.5 == d) return 0;                  /* exact midpoint */
+        }
+        ((float *)out)[idx] = f;
+    } else {
+        ((double *)out)[idx] = d;
+    }
+    *stop = p;
+    return 1;
+}
 
 static int is_sep(unsigned char ch) {
     return ch == ' ' || ch == '\n' || ch == '\r' || ch == '\t' || ch == '\v' || ch == '\f' ||
@@ -84,10 +159,13 @@ static void *parse_job(void *arg) {
         if (p >= c->end) break;
         const char *tok_end = p;
         while (tok_end < c->end && !is_sep((unsigned char)*tok_end)) ++tok_end;
-        char *stop = NULL;
-        if (c->as_float) ((float *)c->out)[idx] = strtof(p, &stop);
-        else ((double *)c->out)[idx] = strtod(p, &stop);
-        if (stop != tok_end) { c->status = -3; return NULL; }
+        const char *fstop = NULL;
+        if (!fast_number(p, tok_end, c->as_float, c->out, idx, &fstop) || fstop != tok_end) {
+            char *stop = NULL;
+            if (c->as_float) ((float *)c->out)[idx] = strtof(p, &stop);
+            else ((double *)c->out)[idx] = strtod(p, &stop);
+            if (stop != tok_end) { c->status = -3; return NULL; }
+        }
         ++idx;
         p = tok_end;
     }

@@ -26,13 +26,16 @@
  * prints "iterations <k+1>" on stderr-free stdout line after the reference's
  * own timing line.
  */
+#define _POSIX_C_SOURCE 200809L
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
+#include <time.h>
 
 #define REF_ROWS 8192
 
 void conjugrad(float *matrixA, float *vectorB, float *vectorX); /* serialConjugate.c:180 */
+void initialize(float *vector, char *filename, int col_num);     /* serialConjugate.c:85  */
 float vecVec(float *vect1, float *vect2);                        /* serialConjugate.c:145 */
 
 static long g_sqrt_calls = 0;
@@ -50,7 +53,32 @@ static int read_f32(const char *path, float *dst, size_t count) {
     return 0;
 }
 
+
+static double now_s(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+/* serial_ref --initialize <file> <col_num> <out.f32>: time the reference's own
+ * text reader (ROWS * col_num values via fscanf "%f%*c", serialConjugate.c:96). */
+static int time_initialize(char *path, int cols, const char *out) {
+    float *v = malloc((size_t)REF_ROWS * cols * sizeof(float));
+    if (!v) return 3;
+    double t0 = now_s();
+    initialize(v, path, cols);
+    double t1 = now_s();
+    FILE *f = fopen(out, "wb");
+    if (!f || fwrite(v, sizeof(float), (size_t)REF_ROWS * cols, f) != (size_t)REF_ROWS * cols) return 6;
+    fclose(f);
+    printf("initialize_seconds %.6f\n", t1 - t0);
+    free(v);
+    return 0;
+}
+
 int main(int argc, char **argv) {
+    if (argc == 5 && strcmp(argv[1], "--initialize") == 0)
+        return time_initialize(argv[2], atoi(argv[3]), argv[4]);
     if (argc != 6) {
         fprintf(stderr, "usage: %s n A b x0 x_out\n", argv[0]);
         return 2;

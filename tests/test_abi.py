@@ -135,3 +135,48 @@ def test_cli_dims_file(built, tmp_path):
     f = [os.path.join(FIX, n) for n in ("matrixA.txt", "vectorb.txt", "initialguess.txt")]
     r = run_cli("--dims", str(d), *f)
     assert r.returncode == 1 and "3 and 2 must be same size" in r.stdout  # serialConjugate.c:55
+
+
+def test_text_reader_matches_libc_conversion(built, tmp_path):
+    """The exact fast path + fallback reproduces strtof / strtod bit for bit,
+    including decimals that sit next to float rounding midpoints."""
+    import ctypes
+    libc = ctypes.CDLL(None)
+    libc.strtof.restype = ctypes.c_float
+    libc.strtof.argtypes = [ctypes.c_char_p, ctypes.c_void_p]
+    libc.strtod.restype = ctypes.c_double
+    libc.strtod.argtypes = [ctypes.c_char_p, ctypes.c_void_p]
+    rng = np.random.default_rng(7)
+    toks = []
+    for _ in range(20000):
+        digits = int(rng.integers(1, 20))
+        mant = "".join(str(d) for d in rng.integers(0, 10, digits))
+        dot = int(rng.integers(0, digits + 1))
+        s = mant[:dot] + "." + mant[dot:] if dot < digits else mant
+        if rng.random() < 0.3:
+            s += f"e{int(rng.integers(-30, 31))}"
+        if rng.random() < 0.5:
+            s = "-" + s
+        toks.append(s)
+    # decimals within a few double ulps of float midpoints, 17-19 significant digits
+    f = rng.random(3000).astype(np.float32) * np.float32(1000)
+    g = np.nextafter(f, np.float32(np.inf))
+    for a, b in zip(f.astype(np.float64), g.astype(np.float64)):
+        mid = (a + b) / 2
+        for nd in (17, 18, 19):
+            toks.append(f"{mid:.{nd}g}")
+            toks.append(f"{np.nextafter(mid, np.inf):.{nd}g}")
+    toks += ["0", "-0.0", "0.0000", "1e22", "1e23", "3.4028235e38", "1e-40", "9007199254740993", "4.9e-324",
+             "inf", "-nan", "0x1p3", ".5", "5.", "+7"]
+    p = tmp_path / "mix.txt"
+    p.write_text("\n".join(toks) + "\n")
+    got32 = cg.read_text(str(p), len(toks), np.float32, threads=3)
+    got64 = cg.read_text(str(p), len(toks), np.float64, threads=3)
+    for i, t in enumerate(toks):
+        e32 = np.float32(libc.strtof(t.encode(), None))
+        e64 = libc.strtod(t.encode(), None)
+        if np.isnan(e32):
+            assert np.isnan(got32[i]) and np.isnan(got64[i]), t
+            continue
+        assert got32[i].view(np.uint32) == e32.view(np.uint32), (t, got32[i], e32)
+        assert np.float64(got64[i]).view(np.uint64) == np.float64(e64).view(np.uint64), (t, got64[i], e64)
