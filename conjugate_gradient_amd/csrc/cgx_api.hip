@@ -120,6 +120,9 @@ struct Shard {
     bool buf_used[kStreamBufs] = {};
     int next_buf = 0;
     MatvecPlan tile_plan;
+    // overlap of the p exchange with the own-column-block matVec
+    hipStream_t cstream = nullptr;
+    hipEvent_t ev_pready = nullptr, ev_gathered = nullptr;
 };
 
 }  // namespace
@@ -139,6 +142,7 @@ struct cgx_ctx {
     int converged = 0;
     double solve_ms = 0.0, matvec_ms = 0.0;
     int64_t matvec_count = 0, total_iters = 0;
+    bool overlap = false;  // own-column-block matVec while p is exchanged
 };
 
 namespace {
@@ -247,6 +251,12 @@ void free_shard(Shard &s) {
             if (s.ev_loaded[b][q]) (void)hipEventDestroy(s.ev_loaded[b][q]);
     }
     if (s.A_host) (void)hipHostFree(s.A_host);
+    if (s.cstream) {
+        (void)hipStreamSynchronize(s.cstream);
+        (void)hipStreamDestroy(s.cstream);
+    }
+    if (s.ev_pready) (void)hipEventDestroy(s.ev_pready);
+    if (s.ev_gathered) (void)hipEventDestroy(s.ev_gathered);
     if (s.stream) (void)hipStreamDestroy(s.stream);
     s = Shard();
 }
@@ -273,9 +283,35 @@ cgx_ctx *new_ctx(int64_t n, int nranks, int flags) {
     return c;
 }
 
+// Overlap p's exchange with the own-column-block part of the matVec: dense
+// fp64 resident A, more than one row block, every block aligned to the
+// matVec's 128-column chunks.  CGX_OVERLAP=0 disables it.
+bool can_overlap(const cgx_ctx *c) {
+    if (c->op != OP_DENSE || f32ref(c) || (c->flags & CGX_HOST_STREAM)) return false;
+    if (c->mode == M_SINGLE || (c->mode == M_RCCL && c->nranks == 1)) return false;
+    if (c->flags & CGX_NO_OVERLAP) return false;
+    const char *e = std::getenv("CGX_OVERLAP");
+    if (e && *e == '0') return false;
+    for (const auto &s : c->sh)
+        if ((s.row0 & 127) || (s.nloc & 127)) return false;
+    return true;
+}
+
+int alloc_overlap(cgx_ctx *c) {
+    for (auto &s : c->sh) {
+        TRY(set_dev(s));
+        HIPT(hipStreamCreateWithFlags(&s.cstream, hipStreamNonBlocking));
+        HIPT(hipEventCreateWithFlags(&s.ev_pready, hipEventDisableTiming));
+        HIPT(hipEventCreateWithFlags(&s.ev_gathered, hipEventDisableTiming));
+    }
+    return CGX_OK;
+}
+
 int finish_create(cgx_ctx *c, cgx_ctx **out) {
+    c->overlap = can_overlap(c);
     for (auto &s : c->sh) {
         int rc = alloc_shard(c, s);
+        if (rc == CGX_OK && c->overlap && &s == &c->sh.back()) rc = alloc_overlap(c);
         if (rc != CGX_OK) {
             std::string keep = g_err;
             for (auto &t : c->sh) free_shard(t);
@@ -549,17 +585,68 @@ int read_scalar(cgx_ctx *c, int gslot, double *out) {
     return CGX_OK;
 }
 
+// Overlapped exchange + matVec: p is allgathered on each shard's comm
+// stream while the compute stream multiplies the shard's own column block
+// (its own p is already local); the rest of the columns follow once the
+// gather has landed, accumulating into Ap with the fused p.Ap partial.
+int overlapped_matvec(cgx_ctx *c, int dot_slot) {
+    const size_t es = (size_t)c->es;
+    for (auto &s : c->sh) {
+        TRY(set_dev(s));
+        HIPT(hipEventRecord(s.ev_pready, s.stream));
+    }
+    if (c->mode == M_RCCL) {
+        Shard &s = c->sh[0];
+        HIPT(hipStreamWaitEvent(s.cstream, s.ev_pready, 0));
+        NCCLT(ncclAllGather(s.pown, s.pfull, (size_t)s.nloc, ncclDouble, s.comm, s.cstream));
+        HIPT(hipEventRecord(s.ev_gathered, s.cstream));
+    } else {
+        for (auto &d : c->sh) {
+            TRY(set_dev(d));
+            for (auto &s : c->sh) HIPT(hipStreamWaitEvent(d.cstream, s.ev_pready, 0));
+            for (auto &s : c->sh)
+                if (&s != &d)
+                    HIPT(hipMemcpyPeerAsync(d.pfull + s.row0 * es, d.dev, s.pown, s.dev, s.nloc * es, d.cstream));
+            HIPT(hipEventRecord(d.ev_gathered, d.cstream));
+        }
+    }
+    for (auto &s : c->sh) {
+        TRY(set_dev(s));
+        const bool timing = (c->flags & CGX_TIMING) && (&s == &c->sh[0]);
+        if (timing && s.ev_used >= kEvPairs) TRY(timing_resolve(c));
+        if (timing) HIPT(hipEventRecord(s.ev_t[2 * s.ev_used], s.stream));
+        const double *A = reinterpret_cast<const double *>(s.A);
+        const double *v = reinterpret_cast<const double *>(s.pfull);
+        double *Ap = reinterpret_cast<double *>(s.Ap);
+        HIPT(matvec_f64_cols(s.plan, A, c->lda, s.nloc, c->lda, s.row0, s.nloc, false, v, Ap, nullptr, nullptr,
+                             s.ws, s.stream));
+        HIPT(hipStreamWaitEvent(s.stream, s.ev_gathered, 0));
+        HIPT(matvec_f64_cols(s.plan, A, c->lda, s.nloc, c->lda, (s.row0 + s.nloc) % c->lda, c->lda - s.nloc, true,
+                             v, Ap, reinterpret_cast<const double *>(s.pown),
+                             reinterpret_cast<double *>(slot(s, dot_slot)), s.ws, s.stream));
+        if (timing) {
+            HIPT(hipEventRecord(s.ev_t[2 * s.ev_used + 1], s.stream));
+            s.ev_used++;
+        }
+    }
+    return CGX_OK;
+}
+
 // One loop iteration k (serialConjugate.c:215-244 / parallel_cg.c:290-323).
 // Returns 1 in *stop when sqrt(r.r) < eps ended the loop (before the p update,
 // as the reference breaks at :235-238).
 int do_iteration(cgx_ctx *c, double eps, int *stop) {
     const int64_t k = c->k;
     *stop = 0;
-    TRY(exchange_allgather(c, false));  // MPI_Allgather(local_p -> p)  parallel_cg.c:290
     const int pg = S_PAP + ring(k), pl = S_LPAP + ring(k);
-    for (auto &s : c->sh) {
-        TRY(set_dev(s));
-        TRY(launch_matvec(c, s, s.pfull, true, out_slot(c, pl, pg)));  // :215 / :292-293
+    if (c->overlap) {
+        TRY(overlapped_matvec(c, out_slot(c, pl, pg)));  // parallel_cg.c:290-293, overlapped
+    } else {
+        TRY(exchange_allgather(c, false));  // MPI_Allgather(local_p -> p)  parallel_cg.c:290
+        for (auto &s : c->sh) {
+            TRY(set_dev(s));
+            TRY(launch_matvec(c, s, s.pfull, true, out_slot(c, pl, pg)));  // :215 / :292-293
+        }
     }
     TRY(exchange_scalar(c, pl, pg));  // MPI_Allreduce(p.Ap)  parallel_cg.c:294
     const int rg = S_RR + ring(k + 1), rl = S_LRR + ring(k + 1);
@@ -616,6 +703,7 @@ int sync_all(cgx_ctx *c) {
         TRY(set_dev(s));
         HIPT(hipStreamSynchronize(s.stream));
         for (int q = 0; q < s.ncopy; ++q) HIPT(hipStreamSynchronize(s.copy[q]));
+        if (s.cstream) HIPT(hipStreamSynchronize(s.cstream));
     }
     return timing_resolve(c);
 }
@@ -856,7 +944,7 @@ int cgx_get_info(const cgx_ctx *c, cgx_info *info) {
     info->row0 = c->sh[0].row0;
     info->nrows = 0;
     for (auto &s : c->sh) info->nrows += s.nloc;
-    info->flags = c->flags;
+    info->flags = c->flags | (c->overlap ? CGX_OVERLAP_ACTIVE : 0);
     info->elem_bytes = c->es;
     return CGX_OK;
 }

@@ -32,6 +32,13 @@ MatvecPlan plan_matvec_f64(int device, int64_t rows, int R = 0, int U = 0, int n
 hipError_t matvec_f64(const MatvecPlan &pl, const double *A, int64_t lda, int64_t rows,
                       int64_t cols, const double *v, double *out, const double *pown,
                       double *dot_out, const RedWs &ws, hipStream_t s);
+// Columns [col_first, col_first+col_count) mod cols (all multiples of 128,
+// cols = the padded width): out[i] = (accumulate ? out[i] : 0) + partial row
+// sum; optional fused dot as above.  Used to overlap the p exchange with the
+// shard's own column block.
+hipError_t matvec_f64_cols(const MatvecPlan &pl, const double *A, int64_t lda, int64_t rows, int64_t cols,
+                           int64_t col_first, int64_t col_count, bool accumulate, const double *v, double *out,
+                           const double *pown, double *dot_out, const RedWs &ws, hipStream_t s);
 // r = b - Ax; p = r (if p); *rr_out = r.r (if rr_out)
 hipError_t residual_f64(int64_t n, const double *b, const double *Ax, double *r, double *p,
                         double *rr_out, const RedWs &ws, hipStream_t s);

@@ -92,17 +92,56 @@ __device__ __forceinline__ d2 load_a(const d2 *p) {
 // Wave w owns row groups g = w, w + waves, ...; a group is R consecutive rows.
 // Per step a lane holds U 16-B chunks of p and R*U 16-B chunks of A.
 // ---------------------------------------------------------------------------
+// Accumulate 128-column chunks [c0, c1) of R rows into acc (U chunks per step).
+template <int R, int U, bool NT>
+__device__ __forceinline__ void mv_chunks(const d2 *const (&arow)[R], const d2 *v2, int64_t c0, int64_t c1,
+                                          d2 (&acc)[R]) {
+    int64_t c = c0;
+    for (; c + U <= c1; c += U) {
+        d2 pv[U];
+        d2 av[R][U];
+#pragma unroll
+        for (int u = 0; u < U; ++u) pv[u] = v2[(c + u) * 64];
+#pragma unroll
+        for (int r = 0; r < R; ++r)
+#pragma unroll
+            for (int u = 0; u < U; ++u) av[r][u] = load_a<NT>(arow[r] + (c + u) * 64);
+#pragma unroll
+        for (int u = 0; u < U; ++u)
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                acc[r].x = __builtin_fma(av[r][u].x, pv[u].x, acc[r].x);
+                acc[r].y = __builtin_fma(av[r][u].y, pv[u].y, acc[r].y);
+            }
+    }
+    for (; c < c1; ++c) {
+        const d2 pv = v2[c * 64];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const d2 a = load_a<NT>(arow[r] + c * 64);
+            acc[r].x = __builtin_fma(a.x, pv.x, acc[r].x);
+            acc[r].y = __builtin_fma(a.y, pv.y, acc[r].y);
+        }
+    }
+}
+
+// Column range: the `ccount` 128-column chunks starting at chunk `cfirst`,
+// wrapping modulo the vec_cols/128 aligned chunks; `tail` adds the scalar
+// columns [vec_cols, cols).  `accumulate` adds the existing out[i] (the
+// overlap path computes the shard's own column block first, then the rest).
 template <int R, int U, bool NT>
 __global__ __launch_bounds__(kNT) void k_matvec_f64(
-    const double *__restrict__ A, int64_t lda, int64_t rows, int64_t cols, int64_t vec_cols,
-    const double *__restrict__ v, double *__restrict__ out, const double *__restrict__ pown,
-    double *dot_out, double *partials, unsigned *ticket) {
+    const double *__restrict__ A, int64_t lda, int64_t rows, int64_t cols, int64_t vec_cols, int64_t cfirst,
+    int64_t ccount, int tail, int accumulate, const double *__restrict__ v, double *__restrict__ out,
+    const double *__restrict__ pown, double *dot_out, double *partials, unsigned *ticket) {
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
     const int64_t ngroups = (rows + R - 1) / R;
     const int64_t wstride = (int64_t)gridDim.x * (kNT / 64);
     const int64_t nchunk = vec_cols >> 7;  // 16-B-aligned 128-column chunks
     const int64_t ctail = nchunk << 7;
+    const int64_t ca = cfirst, cb = (cfirst + ccount < nchunk) ? cfirst + ccount : nchunk;  // first piece
+    const int64_t wrap = cfirst + ccount - cb;                                              // wrapped piece
     const d2 *v2 = reinterpret_cast<const d2 *>(v) + lane;
     double dacc = 0.0;
 
@@ -117,38 +156,14 @@ __global__ __launch_bounds__(kNT) void k_matvec_f64(
             arow[r] = reinterpret_cast<const d2 *>(A + ridx[r] * lda) + lane;
             acc[r] = (d2)(0.0);
         }
-        int64_t c = 0;
-        for (; c + U <= nchunk; c += U) {
-            d2 pv[U];
-            d2 av[R][U];
+        mv_chunks<R, U, NT>(arow, v2, ca, cb, acc);
+        if (wrap > 0) mv_chunks<R, U, NT>(arow, v2, 0, wrap, acc);
+        if (tail)
+            for (int64_t j = ctail + lane; j < cols; j += 64) {
+                const double vj = v[j];
 #pragma unroll
-            for (int u = 0; u < U; ++u) pv[u] = v2[(c + u) * 64];
-#pragma unroll
-            for (int r = 0; r < R; ++r)
-#pragma unroll
-                for (int u = 0; u < U; ++u) av[r][u] = load_a<NT>(arow[r] + (c + u) * 64);
-#pragma unroll
-            for (int u = 0; u < U; ++u)
-#pragma unroll
-                for (int r = 0; r < R; ++r) {
-                    acc[r].x = __builtin_fma(av[r][u].x, pv[u].x, acc[r].x);
-                    acc[r].y = __builtin_fma(av[r][u].y, pv[u].y, acc[r].y);
-                }
-        }
-        for (; c < nchunk; ++c) {
-            const d2 pv = v2[c * 64];
-#pragma unroll
-            for (int r = 0; r < R; ++r) {
-                const d2 a = load_a<NT>(arow[r] + c * 64);
-                acc[r].x = __builtin_fma(a.x, pv.x, acc[r].x);
-                acc[r].y = __builtin_fma(a.y, pv.y, acc[r].y);
+                for (int r = 0; r < R; ++r) acc[r].x = __builtin_fma(A[ridx[r] * lda + j], vj, acc[r].x);
             }
-        }
-        for (int64_t j = ctail + lane; j < cols; j += 64) {
-            const double vj = v[j];
-#pragma unroll
-            for (int r = 0; r < R; ++r) acc[r].x = __builtin_fma(A[ridx[r] * lda + j], vj, acc[r].x);
-        }
         double mine = 0.0;
 #pragma unroll
         for (int r = 0; r < R; ++r) {
@@ -156,6 +171,7 @@ __global__ __launch_bounds__(kNT) void k_matvec_f64(
             if (lane == r) mine = s;
         }
         if (lane < R && r0 + lane < rows) {
+            if (accumulate) mine = out[r0 + lane] + mine;
             out[r0 + lane] = mine;
             if (pown) dacc += pown[r0 + lane] * mine;
         }
@@ -163,10 +179,6 @@ __global__ __launch_bounds__(kNT) void k_matvec_f64(
     if (pown) grid_sum_last_block(dacc, partials, ticket, dot_out);
 }
 
-// Vector kernels.  VEC: every pointer 16-B aligned -> 16-B loads/stores of
-// element pairs, two pairs in flight per thread per step; else scalar.  The
-// odd tail element (n odd) is done by thread 0 of block 0.  Sums are
-// per-thread in a fixed order, then the deterministic grid reduction.
 __device__ __forceinline__ d2 ld2(const double *p) { return *reinterpret_cast<const d2 *>(p); }
 __device__ __forceinline__ void st2(double *p, d2 v) { *reinterpret_cast<d2 *>(p) = v; }
 
@@ -586,8 +598,8 @@ unsigned grid_vec(int64_t n) { return grid_1d((n + 1) / 2, kNT * kVU, 2048); }
 
 inline bool al16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
-using MvFn = void (*)(const double *, int64_t, int64_t, int64_t, int64_t, const double *, double *,
-                      const double *, double *, double *, unsigned *);
+using MvFn = void (*)(const double *, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, int, int,
+                      const double *, double *, const double *, double *, double *, unsigned *);
 
 template <int R, int U>
 MvFn pick_nt(int nt) {
@@ -658,8 +670,22 @@ hipError_t matvec_f64(const MatvecPlan &pl, const double *A, int64_t lda, int64_
                          (lda & 1) == 0;
     const int64_t vec_cols = aligned ? (cols & ~int64_t(127)) : 0;
     MvFn fn = pick_mv(pl.R, pl.U, pl.nt);
-    hipLaunchKernelGGL(fn, dim3(pl.blocks), dim3(kNT), 0, s, A, lda, rows, cols, vec_cols, v, out, pown, dot_out,
-                       ws.partials, ws.tickets + T_MATVEC);
+    hipLaunchKernelGGL(fn, dim3(pl.blocks), dim3(kNT), 0, s, A, lda, rows, cols, vec_cols, int64_t(0),
+                       vec_cols >> 7, 1, 0, v, out, pown, dot_out, ws.partials, ws.tickets + T_MATVEC);
+    return hipGetLastError();
+}
+
+hipError_t matvec_f64_cols(const MatvecPlan &pl, const double *A, int64_t lda, int64_t rows, int64_t cols,
+                           int64_t col_first, int64_t col_count, bool accumulate, const double *v, double *out,
+                           const double *pown, double *dot_out, const RedWs &ws, hipStream_t s) {
+    if (rows <= 0) return hipSuccess;
+    if ((cols & 127) || (col_first & 127) || (col_count & 127) || (lda & 1) ||
+        ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(v)) & 15))
+        return hipErrorInvalidValue;
+    MvFn fn = pick_mv(pl.R, pl.U, pl.nt);
+    hipLaunchKernelGGL(fn, dim3(pl.blocks), dim3(kNT), 0, s, A, lda, rows, cols, cols, col_first >> 7,
+                       col_count >> 7, 0, accumulate ? 1 : 0, v, out, pown, dot_out, ws.partials,
+                       ws.tickets + T_MATVEC);
     return hipGetLastError();
 }
 

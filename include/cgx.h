@@ -65,6 +65,11 @@ extern "C" {
 #define CGX_F64          0x0   /* double data (default)                        */
 #define CGX_F32_REF      0x1   /* float data, bit-exact serialConjugate.c order */
 #define CGX_TIMING       0x100 /* time every matVec launch with HIP events      */
+#define CGX_NO_OVERLAP   0x400 /* multi-shard dense fp64: do not overlap the p
+                                  exchange with the own-column-block matVec
+                                  (on by default when every row block is a
+                                  multiple of 128 rows; env CGX_OVERLAP=0) */
+#define CGX_OVERLAP_ACTIVE 0x800 /* reported in cgx_info.flags when it is on */
 #define CGX_HOST_STREAM  0x200 /* keep A in pinned host memory and stream row
                                   tiles through the GPU every matVec (out-of-HBM
                                   systems; tile size CGX_STREAM_TILE_MB, default

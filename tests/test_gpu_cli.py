@@ -1,0 +1,81 @@
+"""The cg_hip program as a drop-in for serialConjugate / parallel_cg: same
+argv, same stdout lines, the reference's x with --fp32-ref (bit-exact, via
+--print-x), fp64 by default."""
+import os
+import subprocess
+
+import numpy as np
+import pytest
+
+import conjugate_gradient_amd as cg
+import oracle
+from _cases import FIX, case, golden_x
+
+pytestmark = pytest.mark.gpu
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu(built):
+    assert cg.device_count() >= 1
+
+
+def run(*args, timeout=300):
+    r = subprocess.run([cg.CLI_PATH, *args], capture_output=True, text=True, timeout=timeout)
+    assert r.returncode == 0, r.stdout + r.stderr
+    return r.stdout
+
+
+def printed_x(out, n, dtype):
+    lines = out.strip().splitlines()
+    return np.array([float(v) for v in lines[-n:]], dtype=dtype)
+
+
+@pytest.mark.parametrize("name,files", [
+    ("kat2", ("matrixA.txt", "vectorb.txt", "initialguess.txt")),
+    ("kat2_x0", ("matrixA.txt", "vectorb.txt", "initialguess1.txt")),
+    ("kat4", ("matrixA1.txt", "vectorb1.txt", "X0.txt")),
+])
+def test_cli_fp32ref_reference_fixtures(golden, name, files):
+    paths = [os.path.join(FIX, f) for f in files]
+    n = golden["cases"][name]["n"]
+    out = run("--fp32-ref", "--print-x", "--stats", *paths)
+    assert f"Computing cg of matrix size : {n * n}" in out          # serialConjugate.c:58
+    assert "average clock execution time in seconds:" in out        # serialConjugate.c:250
+    assert f"iterations: {golden['cases'][name]['ref_iterations']} converged: 1" in out
+    x = printed_x(out, n, np.float32)   # %.9g round-trips a float exactly
+    assert np.array_equal(x.view(np.uint32), golden_x(golden, name).view(np.uint32))
+
+
+def test_cli_dims_file_and_fp64(golden):
+    paths = [os.path.join(FIX, f) for f in ("matrixA.txt", "vectorb.txt", "initialguess.txt")]
+    out = run("--dims", os.path.join(FIX, "dimensions.txt"), "--eps", "1e-12", "--print-x", *paths)
+    x = printed_x(out, 2, np.float64)
+    assert np.allclose(x, [2 / 3, 1 / 3], rtol=0, atol=1e-12)
+
+
+def test_cli_generated_text_files_multi_gpu(golden, tmp_path):
+    """generateSPDmatrix(512) written as the MATLAB script writes it; the
+    parallel_cg.c-style run (--gpus 2: two row blocks) prints its lines."""
+    n = 512
+    A, b = oracle.spd_matlab(n, np.float64)
+    for name, arr, fmt in (("A.txt", A.ravel(), "%.4f"), ("b.txt", b, "%.4f"), ("x0.txt", np.zeros(n), "%.1f")):
+        arr.tofile(str(tmp_path / name), sep="\n", format=fmt)
+    paths = [str(tmp_path / f) for f in ("A.txt", "b.txt", "x0.txt")]
+    out = run("--fp32-ref", "--print-x", *paths)
+    x = printed_x(out, n, np.float32)
+    assert np.array_equal(x.view(np.uint32), golden_x(golden, "spd512").view(np.uint32))
+    out2 = run("--gpus", "2", "--stats", "--eps", "1e-10", "--print-x", *paths)
+    for line in ("cg method execution time in seconds:", "collective data distribution time in seconds:",
+                 "clock execution time in seconds:"):
+        assert line in out2                                        # parallel_cg.c:123-126, :334
+    x2 = printed_x(out2, n, np.float64)
+    A64, b64, x064 = case("spd512", np.float64)
+    xo, _ = oracle.cg_f64(A64, b64, x064, eps=1e-10)
+    assert np.linalg.norm(x2 - xo) <= 1e-10 * np.linalg.norm(xo)
+
+
+def test_cli_synthetic_spd():
+    out = run("--spd", "4096", "--stats", "--eps", "1e-10")
+    assert "Computing cg of matrix size : 16777216" in out
+    it = int(out.split("iterations:")[1].split()[0])
+    assert 3 <= it <= 20 and "converged: 1" in out

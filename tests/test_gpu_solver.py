@@ -279,3 +279,22 @@ def test_poisson_rejects_bad_use():
             s.generate_spd(1)
         with pytest.raises(cg.CgxError):
             s.set_rows(0, np.zeros((64, 64)), np.ones(64))
+
+
+@pytest.mark.parametrize("P", [2, 4, 8])
+def test_overlapped_exchange_matches(P):
+    """Own-column-block matVec overlapped with the p exchange (default when
+    blocks are 128-aligned) == the sequential exchange, to fp64 rounding of
+    the two-piece row sums; both == oracle."""
+    n = 2048
+    A, b = oracle.spd_hash(n, seed=11)
+    res = {}
+    for flags in (cg.CGX_F64, cg.CGX_F64 | cg.CGX_NO_OVERLAP):
+        with cg.Solver(n, flags=flags, devices=[0] * P) as s:
+            assert bool(s.info.flags & cg.CGX_OVERLAP_ACTIVE) == (not flags & cg.CGX_NO_OVERLAP)
+            s.set_system(A, b)
+            res[flags] = s.solve(None, eps=1e-10)
+    xo, so = oracle.cg_f64(A, b, np.zeros(n), eps=1e-10)
+    for x, st in res.values():
+        assert st.iterations == so.iterations
+        assert rel(x, xo) <= TOL
