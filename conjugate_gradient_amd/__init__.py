@@ -31,7 +31,7 @@ import subprocess
 import numpy as np
 
 __all__ = [
-    "CGX_F64", "CGX_F32_REF", "CGX_TIMING", "CGX_HOST_STREAM", "CGX_NO_OVERLAP", "CgxError", "Stats", "Solver", "lib", "build",
+    "CGX_F64", "CGX_F32_REF", "CGX_TIMING", "CGX_HOST_STREAM", "CGX_NO_OVERLAP", "CGX_COMM_P2P", "CgxError", "Stats", "Solver", "lib", "build",
     "conjugrad", "matVec", "vecVec", "residual", "update_xr", "update_p", "read_text",
     "count_text", "read_dims", "device_count", "get_unique_id", "DeviceArray",
 ]
@@ -42,6 +42,7 @@ CGX_TIMING = 0x100
 CGX_HOST_STREAM = 0x200
 CGX_NO_OVERLAP = 0x400
 CGX_OVERLAP_ACTIVE = 0x800
+CGX_COMM_P2P = 0x1000
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libcgx.so")

@@ -289,7 +289,7 @@ cgx_ctx *new_ctx(int64_t n, int nranks, int flags) {
 bool can_overlap(const cgx_ctx *c) {
     if (c->op != OP_DENSE || f32ref(c) || (c->flags & CGX_HOST_STREAM)) return false;
     if (c->mode == M_SINGLE || (c->mode == M_RCCL && c->nranks == 1)) return false;
-    if (c->flags & CGX_NO_OVERLAP) return false;
+    if (c->flags & (CGX_NO_OVERLAP | CGX_COMM_P2P)) return false;
     const char *e = std::getenv("CGX_OVERLAP");
     if (e && *e == '0') return false;
     for (const auto &s : c->sh)
@@ -401,10 +401,114 @@ int exchange_halo(cgx_ctx *c, bool from_x) {
     return CGX_OK;
 }
 
+inline bool p2p(const cgx_ctx *c) { return (c->flags & CGX_COMM_P2P) != 0; }
+
+// CGX_COMM_P2P: point-to-point_cg.c's exchange pattern, gather to rank 0 then
+// send from rank 0 to every rank (allGather :364-394 + BcastVector :239-256),
+// O(P) messages through rank 0.  ncclSend/Recv in rank mode, device copies
+// through shard 0 in LOCAL mode.
+int p2p_allgather(cgx_ctx *c, bool from_x) {
+    const size_t es = (size_t)c->es;
+    if (c->mode == M_RCCL) {
+        Shard &s = c->sh[0];
+        TRY(set_dev(s));
+        const ncclDataType_t t = f32ref(c) ? ncclFloat : ncclDouble;
+        const int P = c->nranks;
+        if (s.index == 0 && from_x)
+            HIPT(hipMemcpyAsync(s.pown, s.x, s.nloc * es, hipMemcpyDeviceToDevice, s.stream));
+        NCCLT(ncclGroupStart());
+        if (s.index != 0) {
+            NCCLT(ncclSend(from_x ? (const void *)s.x : (const void *)s.pown, (size_t)s.nloc, t, 0, s.comm, s.stream));
+        } else {
+            for (int q = 1; q < P; ++q)
+                NCCLT(ncclRecv(s.pfull + (size_t)q * s.nloc * es, (size_t)s.nloc, t, q, s.comm, s.stream));
+        }
+        NCCLT(ncclGroupEnd());
+        NCCLT(ncclGroupStart());
+        if (s.index == 0) {
+            for (int q = 1; q < P; ++q) NCCLT(ncclSend(s.pfull, (size_t)c->n, t, q, s.comm, s.stream));
+        } else {
+            NCCLT(ncclRecv(s.pfull, (size_t)c->n, t, 0, s.comm, s.stream));
+        }
+        NCCLT(ncclGroupEnd());
+        return CGX_OK;
+    }
+    TRY(local_barrier(c));
+    Shard &r0 = c->sh[0];
+    TRY(set_dev(r0));
+    for (auto &s : c->sh) {
+        if (&s == &r0 && !from_x) continue;
+        HIPT(hipMemcpyPeerAsync(r0.pfull + s.row0 * es, r0.dev, from_x ? s.x : s.pown, s.dev, s.nloc * es, r0.stream));
+    }
+    HIPT(hipEventRecord(r0.ev_sync, r0.stream));
+    for (auto &d : c->sh) {
+        if (&d == &r0) continue;
+        TRY(set_dev(d));
+        HIPT(hipStreamWaitEvent(d.stream, r0.ev_sync, 0));
+        HIPT(hipMemcpyPeerAsync(d.pfull, d.dev, r0.pfull, r0.dev, (size_t)c->n * es, d.stream));
+    }
+    return CGX_OK;
+}
+
+// allSum (point-to-point_cg.c:339-359): partials to rank 0, summed there in
+// rank order, the sum sent back to every rank (BcastVector(&s, 1)).
+int p2p_scalar(cgx_ctx *c, int lslot, int gslot) {
+    if (c->mode == M_RCCL) {
+        Shard &s = c->sh[0];
+        TRY(set_dev(s));
+        const int P = c->nranks;
+        if (s.index == 0) HIPT(hipMemcpyAsync(slot(s, S_GATHER), slot(s, lslot), 8, hipMemcpyDeviceToDevice, s.stream));
+        NCCLT(ncclGroupStart());
+        if (s.index != 0) {
+            NCCLT(ncclSend(slot(s, lslot), 1, ncclUint64, 0, s.comm, s.stream));
+        } else {
+            for (int q = 1; q < P; ++q) NCCLT(ncclRecv(slot(s, S_GATHER + q), 1, ncclUint64, q, s.comm, s.stream));
+        }
+        NCCLT(ncclGroupEnd());
+        if (s.index == 0) {
+            if (f32ref(c))
+                HIPT(sum_ordered_f32(reinterpret_cast<const float *>(slot(s, S_GATHER)), P,
+                                     reinterpret_cast<float *>(slot(s, gslot)), s.stream));
+            else
+                HIPT(sum_ordered_f64(reinterpret_cast<const double *>(slot(s, S_GATHER)), P,
+                                     reinterpret_cast<double *>(slot(s, gslot)), s.stream));
+        }
+        NCCLT(ncclGroupStart());
+        if (s.index == 0) {
+            for (int q = 1; q < P; ++q) NCCLT(ncclSend(slot(s, gslot), 1, ncclUint64, q, s.comm, s.stream));
+        } else {
+            NCCLT(ncclRecv(slot(s, gslot), 1, ncclUint64, 0, s.comm, s.stream));
+        }
+        NCCLT(ncclGroupEnd());
+        return CGX_OK;
+    }
+    TRY(local_barrier(c));
+    Shard &r0 = c->sh[0];
+    const int S = (int)c->sh.size();
+    TRY(set_dev(r0));
+    for (auto &s : c->sh)
+        HIPT(hipMemcpyPeerAsync(slot(r0, S_GATHER + s.index), r0.dev, slot(s, lslot), s.dev, 8, r0.stream));
+    if (f32ref(c))
+        HIPT(sum_ordered_f32(reinterpret_cast<const float *>(slot(r0, S_GATHER)), S,
+                             reinterpret_cast<float *>(slot(r0, gslot)), r0.stream));
+    else
+        HIPT(sum_ordered_f64(reinterpret_cast<const double *>(slot(r0, S_GATHER)), S,
+                             reinterpret_cast<double *>(slot(r0, gslot)), r0.stream));
+    HIPT(hipEventRecord(r0.ev_sync, r0.stream));
+    for (auto &d : c->sh) {
+        if (&d == &r0) continue;
+        TRY(set_dev(d));
+        HIPT(hipStreamWaitEvent(d.stream, r0.ev_sync, 0));
+        HIPT(hipMemcpyPeerAsync(slot(d, gslot), d.dev, slot(r0, gslot), r0.dev, 8, d.stream));
+    }
+    return CGX_OK;
+}
+
 // Every shard's pfull gets every shard's slice of `src(shard)` (its own slice
 // of a full-length buffer when in_place, else a separate local buffer).
 int exchange_allgather(cgx_ctx *c, bool from_x) {
     if (c->op == OP_POISSON) return exchange_halo(c, from_x);
+    if (p2p(c) && c->mode != M_SINGLE) return p2p_allgather(c, from_x);
     const size_t es = (size_t)c->es;
     if (c->mode == M_SINGLE) {
         if (from_x) {
@@ -439,6 +543,7 @@ int exchange_allgather(cgx_ctx *c, bool from_x) {
 // Combine the per-shard partials in slot `lslot` into the global slot `gslot`.
 int exchange_scalar(cgx_ctx *c, int lslot, int gslot) {
     if (c->mode == M_SINGLE) return CGX_OK;  // kernels wrote the global slot directly
+    if (p2p(c)) return p2p_scalar(c, lslot, gslot);
     const int S = (int)c->sh.size();
     if (c->mode == M_RCCL) {
         Shard &s = c->sh[0];
@@ -776,7 +881,7 @@ static int check_op(int op, int64_t n, int64_t m, int parts, int flags) {
     if (op == OP_POISSON) {
         if (m < 1) return fail(CGX_ERR_ARG, "m must be >= 1");
         if (m % parts != 0) return fail(CGX_ERR_SHAPE, "%lld is not divisible by %d", (long long)m, parts);
-        if (flags & (CGX_F32_REF | CGX_HOST_STREAM))
+        if (flags & (CGX_F32_REF | CGX_HOST_STREAM | CGX_COMM_P2P))
             return fail(CGX_ERR_ARG, "the Poisson operator supports CGX_F64 (+CGX_TIMING) only");
         return CGX_OK;
     }

@@ -70,6 +70,12 @@ extern "C" {
                                   (on by default when every row block is a
                                   multiple of 128 rows; env CGX_OVERLAP=0) */
 #define CGX_OVERLAP_ACTIVE 0x800 /* reported in cgx_info.flags when it is on */
+#define CGX_COMM_P2P     0x1000 /* point-to-point_cg.c's exchange instead of
+                                   collectives: gather to rank 0, then rank 0
+                                   sends to every rank (ncclSend/Recv; device
+                                   copies through shard 0 in multi-shard mode).
+                                   Scalars are summed in rank order.  For the
+                                   p2p-vs-collective comparison of the report. */
 #define CGX_HOST_STREAM  0x200 /* keep A in pinned host memory and stream row
                                   tiles through the GPU every matVec (out-of-HBM
                                   systems; tile size CGX_STREAM_TILE_MB, default

@@ -298,3 +298,30 @@ def test_overlapped_exchange_matches(P):
     for x, st in res.values():
         assert st.iterations == so.iterations
         assert rel(x, xo) <= TOL
+
+
+@pytest.mark.parametrize("P", [2, 4])
+def test_p2p_exchange_mode(P):
+    """CGX_COMM_P2P (point-to-point_cg.c's gather-to-root + send-to-all) gives
+    the collective mode's results bit for bit (both sum scalars in rank
+    order); F32_REF == oracle with P-part dots (point-to-point_cg.c allSum)."""
+    A, b, x0 = case("spd1024", np.float64)
+    out = {}
+    for flags in (cg.CGX_F64 | cg.CGX_NO_OVERLAP, cg.CGX_F64 | cg.CGX_COMM_P2P):
+        with cg.Solver(b.size, flags=flags, devices=[0] * P) as s:
+            s.set_system(A, b, x0)
+            out[flags] = s.solve(None, eps=1e-10)
+    (xa, sa), (xb, sb) = out.values()
+    assert sa.iterations == sb.iterations and np.array_equal(xa, xb)
+    A32, b32, x032 = case("spd1024")
+    with cg.Solver(b.size, flags=cg.CGX_F32_REF | cg.CGX_COMM_P2P, devices=[0] * P) as s:
+        s.set_system(A32, b32, x032)
+        x32, st32 = s.solve(None, eps=1e-6)
+    ref, sr = oracle.cg_f32ref(A32, b32, x032, nparts=P)
+    assert st32.iterations == sr.iterations and np.array_equal(x32, ref)
+    uid = cg.get_unique_id()
+    with cg.Solver(b.size, flags=cg.CGX_F64 | cg.CGX_COMM_P2P, rank=0, nranks=1, unique_id=uid) as s:
+        s.set_system(A, b, x0)
+        x1, s1 = s.solve(None, eps=1e-10)
+    xo, so = oracle.cg_f64(A, b, x0, eps=1e-10)
+    assert s1.iterations == so.iterations and rel(x1, xo) <= TOL
