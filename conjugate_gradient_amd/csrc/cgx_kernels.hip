@@ -81,10 +81,23 @@ __device__ __forceinline__ void grid_sum_last_block(double v, double *partials, 
     }
 }
 
-template <bool NT>
+// Load policy of the A stream (the only data a matVec reads once):
+//   0 plain global_load, 1 global_load ... nt (default),
+//   >= 2: buffer_load with cache-policy bits aux = kBufAux[POL] (2 nt,
+//   18 nt sc1, 19 sc0 nt sc1, 16 sc1, 0 none) through a per-row descriptor.
+constexpr int kBufAux[7] = {0, 0, 2, 18, 19, 16, 0};
+typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+
+template <int POL>
 __device__ __forceinline__ d2 load_a(const d2 *p) {
-    if constexpr (NT) return __builtin_nontemporal_load(p);
+    if constexpr (POL == 1) return __builtin_nontemporal_load(p);
     else return *p;
+}
+
+template <int POL>
+__device__ __forceinline__ d2 load_a_buf(__amdgpu_buffer_rsrc_t rs, int64_t chunk, int lane) {
+    const u4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)((chunk * 64 + lane) * 16), 0, kBufAux[POL]);
+    return __builtin_bit_cast(d2, v);
 }
 
 // ---------------------------------------------------------------------------
@@ -93,9 +106,9 @@ __device__ __forceinline__ d2 load_a(const d2 *p) {
 // Per step a lane holds U 16-B chunks of p and R*U 16-B chunks of A.
 // ---------------------------------------------------------------------------
 // Accumulate 128-column chunks [c0, c1) of R rows into acc (U chunks per step).
-template <int R, int U, bool NT>
-__device__ __forceinline__ void mv_chunks(const d2 *const (&arow)[R], const d2 *v2, int64_t c0, int64_t c1,
-                                          d2 (&acc)[R]) {
+template <int R, int U, int NT>
+__device__ __forceinline__ void mv_chunks(const d2 *const (&arow)[R], const __amdgpu_buffer_rsrc_t (&rs)[R],
+                                          int lane, const d2 *v2, int64_t c0, int64_t c1, d2 (&acc)[R]) {
     int64_t c = c0;
     for (; c + U <= c1; c += U) {
         d2 pv[U];
@@ -105,7 +118,10 @@ __device__ __forceinline__ void mv_chunks(const d2 *const (&arow)[R], const d2 *
 #pragma unroll
         for (int r = 0; r < R; ++r)
 #pragma unroll
-            for (int u = 0; u < U; ++u) av[r][u] = load_a<NT>(arow[r] + (c + u) * 64);
+            for (int u = 0; u < U; ++u) {
+                if constexpr (NT >= 2) av[r][u] = load_a_buf<NT>(rs[r], c + u, lane);
+                else av[r][u] = load_a<NT>(arow[r] + (c + u) * 64);
+            }
 #pragma unroll
         for (int u = 0; u < U; ++u)
 #pragma unroll
@@ -118,7 +134,9 @@ __device__ __forceinline__ void mv_chunks(const d2 *const (&arow)[R], const d2 *
         const d2 pv = v2[c * 64];
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            const d2 a = load_a<NT>(arow[r] + c * 64);
+            d2 a;
+            if constexpr (NT >= 2) a = load_a_buf<NT>(rs[r], c, lane);
+            else a = load_a<NT>(arow[r] + c * 64);
             acc[r].x = __builtin_fma(a.x, pv.x, acc[r].x);
             acc[r].y = __builtin_fma(a.y, pv.y, acc[r].y);
         }
@@ -129,7 +147,7 @@ __device__ __forceinline__ void mv_chunks(const d2 *const (&arow)[R], const d2 *
 // wrapping modulo the vec_cols/128 aligned chunks; `tail` adds the scalar
 // columns [vec_cols, cols).  `accumulate` adds the existing out[i] (the
 // overlap path computes the shard's own column block first, then the rest).
-template <int R, int U, bool NT>
+template <int R, int U, int NT>
 __global__ __launch_bounds__(kNT) void k_matvec_f64(
     const double *__restrict__ A, int64_t lda, int64_t rows, int64_t cols, int64_t vec_cols, int64_t cfirst,
     int64_t ccount, int tail, int accumulate, const double *__restrict__ v, double *__restrict__ out,
@@ -149,15 +167,20 @@ __global__ __launch_bounds__(kNT) void k_matvec_f64(
         const int64_t r0 = g * R;
         int64_t ridx[R];
         const d2 *arow[R];
+        __amdgpu_buffer_rsrc_t rs[R];
         d2 acc[R];
 #pragma unroll
         for (int r = 0; r < R; ++r) {
             ridx[r] = (r0 + r < rows) ? (r0 + r) : (rows - 1);
             arow[r] = reinterpret_cast<const d2 *>(A + ridx[r] * lda) + lane;
+            if constexpr (NT >= 2) {  // wave-uniform row base -> scalar descriptor, no waterfall
+                const int64_t row = (int64_t)__builtin_amdgcn_readfirstlane((int)ridx[r]);
+                rs[r] = __builtin_amdgcn_make_buffer_rsrc((void *)(A + row * lda), 0, (int)(lda * 8), 0x00020000);
+            }
             acc[r] = (d2)(0.0);
         }
-        mv_chunks<R, U, NT>(arow, v2, ca, cb, acc);
-        if (wrap > 0) mv_chunks<R, U, NT>(arow, v2, 0, wrap, acc);
+        mv_chunks<R, U, NT>(arow, rs, lane, v2, ca, cb, acc);
+        if (wrap > 0) mv_chunks<R, U, NT>(arow, rs, lane, v2, 0, wrap, acc);
         if (tail)
             for (int64_t j = ctail + lane; j < cols; j += 64) {
                 const double vj = v[j];
@@ -603,12 +626,24 @@ using MvFn = void (*)(const double *, int64_t, int64_t, int64_t, int64_t, int64_
 
 template <int R, int U>
 MvFn pick_nt(int nt) {
-    return nt ? k_matvec_f64<R, U, true> : k_matvec_f64<R, U, false>;
+    switch (nt) {
+        case 0: return k_matvec_f64<R, U, 0>;
+        case 2: return k_matvec_f64<R, U, 2>;
+        case 3: return k_matvec_f64<R, U, 3>;
+        case 4: return k_matvec_f64<R, U, 4>;
+        case 5: return k_matvec_f64<R, U, 5>;
+        case 6: return k_matvec_f64<R, U, 6>;
+        default: return k_matvec_f64<R, U, 1>;
+    }
+}
+template <int R, int U>
+MvFn pick_nt_basic(int nt) {
+    return nt == 0 ? k_matvec_f64<R, U, 0> : k_matvec_f64<R, U, 1>;
 }
 template <int R>
 MvFn pick_u(int U, int nt) {
     switch (U) {
-        case 2: return pick_nt<R, 2>(nt);
+        case 2: return pick_nt_basic<R, 2>(nt);
         case 8: return pick_nt<R, 8>(nt);
         default: return pick_nt<R, 4>(nt);
     }
@@ -637,7 +672,11 @@ MatvecPlan plan_matvec_f64(int device, int64_t rows, int R, int U, int nt, int b
     else if (rows >= 2 * want_waves) pl.R = 2;
     else pl.R = 1;
     pl.U = 8;
-    pl.nt = 1;
+    // buffer_load ... nt through per-row scalar descriptors: the same stream
+    // policy as global_load ... nt but no 64-bit row addresses in VGPRs (189
+    // vs 256 VGPRs at R=U=8: 2 waves/SIMD instead of 1); +0.5-1% measured
+    // (profiles/r01_sweep_policy*.jsonl).
+    pl.nt = 2;
     pl.R = env_int("CGX_MV_R", pl.R);
     pl.U = env_int("CGX_MV_U", pl.U);
     pl.nt = env_int("CGX_MV_NT", pl.nt);
@@ -646,6 +685,8 @@ MatvecPlan plan_matvec_f64(int device, int64_t rows, int R, int U, int nt, int b
     if (nt >= 0) pl.nt = nt;
     if (pl.R != 1 && pl.R != 2 && pl.R != 4 && pl.R != 8) pl.R = 4;
     if (pl.U != 2 && pl.U != 4 && pl.U != 8) pl.U = 4;
+    if (pl.nt < 0 || pl.nt > 6) pl.nt = 1;
+    if (pl.U == 2 && pl.nt >= 2) pl.nt = 1;  // buffer variants exist for U = 4, 8
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(pick_mv(pl.R, pl.U, pl.nt)),
                                                      kNT, 0) != hipSuccess || per_cu <= 0)
