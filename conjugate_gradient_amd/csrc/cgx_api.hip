@@ -767,12 +767,11 @@ int do_iteration(cgx_ctx *c, double eps, int *stop) {
             HIPT(dot_ref_f32(s.nloc, reinterpret_cast<const float *>(s.r), reinterpret_cast<const float *>(s.r),
                              reinterpret_cast<float *>(slot(s, ro)), s.stream));
         } else {
-            HIPT(update_xr_f64(s.nloc, reinterpret_cast<double *>(s.x), reinterpret_cast<double *>(s.r),
-                               reinterpret_cast<const double *>(s.pown),
-                               reinterpret_cast<const double *>(s.Ap),
-                               reinterpret_cast<const double *>(slot(s, S_RR + ring(k))),
-                               reinterpret_cast<const double *>(slot(s, pg)), reinterpret_cast<double *>(slot(s, ro)),
-                               s.ws, s.stream));
+            // r -= alpha Ap, r.r; x's update is deferred into the p update
+            HIPT(update_r_f64(s.nloc, reinterpret_cast<double *>(s.r), reinterpret_cast<const double *>(s.Ap),
+                              reinterpret_cast<const double *>(slot(s, S_RR + ring(k))),
+                              reinterpret_cast<const double *>(slot(s, pg)), reinterpret_cast<double *>(slot(s, ro)),
+                              s.ws, s.stream));
         }
     }
     TRY(exchange_scalar(c, rl, rg));  // MPI_Allreduce(r.r)  parallel_cg.c:313
@@ -786,6 +785,14 @@ int do_iteration(cgx_ctx *c, double eps, int *stop) {
             c->converged = 1;
             c->state = ST_CONVERGED;
             *stop = 1;
+            if (!f32ref(c))  // the deferred x += alpha p, without the p update
+                for (auto &s : c->sh) {
+                    TRY(set_dev(s));
+                    HIPT(update_xp_f64(s.nloc, reinterpret_cast<double *>(s.x), reinterpret_cast<double *>(s.pown),
+                                       reinterpret_cast<const double *>(s.r),
+                                       reinterpret_cast<const double *>(slot(s, S_RR + ring(k))),
+                                       reinterpret_cast<const double *>(slot(s, pg)), nullptr, s.stream));
+                }
             return CGX_OK;
         }
     }
@@ -795,10 +802,12 @@ int do_iteration(cgx_ctx *c, double eps, int *stop) {
             HIPT(update_p_ref_f32(s.nloc, reinterpret_cast<float *>(s.pown),
                                   reinterpret_cast<const float *>(s.r), reinterpret_cast<const float *>(slot(s, rg)),
                                   reinterpret_cast<const float *>(slot(s, S_RR + ring(k))), s.stream));
-        else
-            HIPT(update_p_f64(s.nloc, reinterpret_cast<double *>(s.pown),
-                              reinterpret_cast<const double *>(s.r), reinterpret_cast<const double *>(slot(s, rg)),
-                              reinterpret_cast<const double *>(slot(s, S_RR + ring(k))), s.stream));
+        else  // x += alpha p (deferred from the r update), then p = r + beta p
+            HIPT(update_xp_f64(s.nloc, reinterpret_cast<double *>(s.x), reinterpret_cast<double *>(s.pown),
+                               reinterpret_cast<const double *>(s.r),
+                               reinterpret_cast<const double *>(slot(s, S_RR + ring(k))),
+                               reinterpret_cast<const double *>(slot(s, pg)),
+                               reinterpret_cast<const double *>(slot(s, rg)), s.stream));
     }
     return CGX_OK;
 }

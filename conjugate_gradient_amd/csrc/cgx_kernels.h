@@ -49,6 +49,12 @@ hipError_t update_xr_f64(int64_t n, double *x, double *r, const double *p, const
 // p = r + (*rr / *rsold) p
 hipError_t update_p_f64(int64_t n, double *p, const double *r, const double *rr,
                         const double *rsold, hipStream_t s);
+// Solver split of the updates: r -= alpha Ap with *rr_out = r.r; then
+// x += alpha p and (rr != nullptr) p = r + (*rr / *rsold) p; alpha = *rsold / *pAp.
+hipError_t update_r_f64(int64_t n, double *r, const double *Ap, const double *rsold, const double *pAp,
+                        double *rr_out, const RedWs &ws, hipStream_t s);
+hipError_t update_xp_f64(int64_t n, double *x, double *p, const double *r, const double *rsold, const double *pAp,
+                         const double *rr, hipStream_t s);
 hipError_t dot_f64(int64_t n, const double *a, const double *b, double *out,
                    const RedWs &ws, hipStream_t s);
 // Rows [row0, row0+nrows) of the counter-hash SPD system; pad columns zeroed.

@@ -42,6 +42,14 @@ __device__ __forceinline__ double wave_sum(double v) {
 // Sum `v` over all threads of the grid.  Each block stores its total in
 // partials[blockIdx.x]; the last block to arrive sums the partials in index
 // order and writes *out.  Deterministic for a fixed grid.
+//
+// Hand-off (cdna_hip_programming.md Guideline 16, the write-through form):
+// the partial is stored write-through (8-B agent-scope atomic store = sc1),
+// the storing lane drains it (s_waitcnt vmcnt(0)) before its relaxed
+// agent-scope ticket add, and the block whose add returns gridDim-1 reads
+// every partial with sc1 loads (agent-scope atomic loads) -- no release /
+// acquire fence, so no per-block write-back of the L2's dirty lines (which
+// cost the r-update ~35 % of its time with a buffer_wbl2 per block).
 __device__ __forceinline__ void grid_sum_last_block(double v, double *partials, unsigned *ticket,
                                                     double *out) {
     __shared__ double red[kNT / 64];
@@ -54,21 +62,26 @@ __device__ __forceinline__ void grid_sum_last_block(double v, double *partials, 
         double t = red[0];
 #pragma unroll
         for (int w = 1; w < kNT / 64; ++w) t += red[w];
-        partials[blockIdx.x] = t;
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
+        __hip_atomic_store(partials + blockIdx.x, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-        unsigned prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        const unsigned prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         is_last = (prev == gridDim.x - 1);
     }
     __syncthreads();
     if (!is_last) return;
-    if (threadIdx.x == 0) {
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
-    }
-    __syncthreads();
+    // all of this thread's partials in flight at once (grid <= 8192 = 32 * kNT)
     double s = 0.0;
-    for (unsigned i = threadIdx.x; i < gridDim.x; i += kNT) s += partials[i];
+    for (unsigned i0 = threadIdx.x; i0 < gridDim.x; i0 += 8 * kNT) {
+        double pv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const unsigned i = i0 + u * kNT;
+            pv[u] = (i < gridDim.x) ? __hip_atomic_load(partials + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (i0 + u * kNT < gridDim.x) s += pv[u];
+    }
     s = wave_sum(s);
     if (lane == 0) red[wid] = s;
     __syncthreads();
@@ -204,6 +217,19 @@ __global__ __launch_bounds__(kNT) void k_matvec_f64(
 
 __device__ __forceinline__ d2 ld2(const double *p) { return *reinterpret_cast<const d2 *>(p); }
 __device__ __forceinline__ void st2(double *p, d2 v) { *reinterpret_cast<d2 *>(p) = v; }
+// Stream policy of the vector kernels (VP): 0 plain, 1 non-temporal stores,
+// 2 non-temporal loads and stores (default: -8 % time on the Poisson
+// vectors, 537 MB each; profiles/r01_vector_policy.txt).
+template <int VP>
+__device__ __forceinline__ d2 ldv(const double *p) {
+    if constexpr (VP >= 2) return __builtin_nontemporal_load(reinterpret_cast<const d2 *>(p));
+    else return *reinterpret_cast<const d2 *>(p);
+}
+template <int VP>
+__device__ __forceinline__ void stv(double *p, d2 v) {
+    if constexpr (VP >= 1) __builtin_nontemporal_store(v, reinterpret_cast<d2 *>(p));
+    else *reinterpret_cast<d2 *>(p) = v;
+}
 
 // Vector kernels.  VEC (every pointer 16-B aligned): a block step covers
 // kVU * kNT consecutive element pairs; each thread loads its kVU pairs of
@@ -263,7 +289,7 @@ __global__ __launch_bounds__(kNT) void k_residual_f64(int64_t n, const double *_
 }
 
 // x += alpha p; r -= alpha Ap; r.r  (serialConjugate.c:219-234, conjgrad.m:8-11)
-template <bool VEC>
+template <bool VEC, int VP = 0>
 __global__ __launch_bounds__(kNT) void k_update_xr_f64(int64_t n, double *__restrict__ x,
                                                        double *__restrict__ r,
                                                        const double *__restrict__ p,
@@ -280,15 +306,15 @@ __global__ __launch_bounds__(kNT) void k_update_xr_f64(int64_t n, double *__rest
         for (int u = 0; u < kVU; ++u)
             if (ok[u]) {
                 const int64_t i = 2 * (base + u * kNT);
-                xv[u] = ld2(x + i); rv[u] = ld2(r + i); pv[u] = ld2(p + i); av[u] = ld2(Ap + i);
+                xv[u] = ldv<VP>(x + i); rv[u] = ldv<VP>(r + i); pv[u] = ldv<VP>(p + i); av[u] = ldv<VP>(Ap + i);
             }
 #pragma unroll
         for (int u = 0; u < kVU; ++u)
             if (ok[u]) {
                 const int64_t i = 2 * (base + u * kNT);
-                st2(x + i, xv[u] + alpha * pv[u]);
+                stv<VP>(x + i, xv[u] + alpha * pv[u]);
                 const d2 ri = rv[u] - alpha * av[u];
-                st2(r + i, ri);
+                stv<VP>(r + i, ri);
                 acc += ri.x * ri.x + ri.y * ri.y;
             }
         CGX_VEC_LOOP_END
@@ -311,7 +337,7 @@ __global__ __launch_bounds__(kNT) void k_update_xr_f64(int64_t n, double *__rest
 }
 
 // p = r + beta p  (serialConjugate.c:239-243, conjgrad.m:15)
-template <bool VEC>
+template <bool VEC, int VP = 0>
 __global__ __launch_bounds__(kNT) void k_update_p_f64(int64_t n, double *__restrict__ p,
                                                       const double *__restrict__ r,
                                                       const double *rr, const double *rsold) {
@@ -321,15 +347,92 @@ __global__ __launch_bounds__(kNT) void k_update_p_f64(int64_t n, double *__restr
         d2 pv[kVU], rv[kVU];
 #pragma unroll
         for (int u = 0; u < kVU; ++u)
-            if (ok[u]) { const int64_t i = 2 * (base + u * kNT); pv[u] = ld2(p + i); rv[u] = ld2(r + i); }
+            if (ok[u]) { const int64_t i = 2 * (base + u * kNT); pv[u] = ldv<VP>(p + i); rv[u] = ldv<VP>(r + i); }
 #pragma unroll
         for (int u = 0; u < kVU; ++u)
-            if (ok[u]) st2(p + 2 * (base + u * kNT), rv[u] + beta * pv[u]);
+            if (ok[u]) stv<VP>(p + 2 * (base + u * kNT), rv[u] + beta * pv[u]);
         CGX_VEC_LOOP_END
         if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) p[n - 1] = r[n - 1] + beta * p[n - 1];
     } else {
         for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kNT)
             p[i] = r[i] + beta * p[i];
+    }
+}
+
+// The solver's split of the x/r/p updates (fp64): x's update moves into the
+// p update, which reads p anyway -- 24 + 40 B per element instead of 48 + 24.
+// r -= alpha Ap; r.r   (alpha = rsold / pAp)
+template <bool VEC, int VP = 2>
+__global__ __launch_bounds__(kNT) void k_update_r_f64(int64_t n, double *__restrict__ r, const double *__restrict__ Ap,
+                                                      const double *rsold, const double *pAp, double *rr_out,
+                                                      double *partials, unsigned *ticket) {
+    const double alpha = *rsold / *pAp;
+    double acc = 0.0;
+    if constexpr (VEC) {
+        CGX_VEC_LOOP_BEGIN
+        d2 rv[kVU], av[kVU];
+#pragma unroll
+        for (int u = 0; u < kVU; ++u)
+            if (ok[u]) { const int64_t i = 2 * (base + u * kNT); rv[u] = ldv<VP>(r + i); av[u] = ldv<VP>(Ap + i); }
+#pragma unroll
+        for (int u = 0; u < kVU; ++u)
+            if (ok[u]) {
+                const d2 ri = rv[u] - alpha * av[u];
+                stv<VP>(r + 2 * (base + u * kNT), ri);
+                acc += ri.x * ri.x + ri.y * ri.y;
+            }
+        CGX_VEC_LOOP_END
+        if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+            const double ri = r[n - 1] - alpha * Ap[n - 1];
+            r[n - 1] = ri;
+            acc += ri * ri;
+        }
+    } else {
+        for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kNT) {
+            const double ri = r[i] - alpha * Ap[i];
+            r[i] = ri;
+            acc += ri * ri;
+        }
+    }
+    grid_sum_last_block(acc, partials, ticket, rr_out);
+}
+
+// x += alpha p (alpha = rsold / pAp); then, if rr != nullptr, p = r + (rr / rsold) p.
+template <bool VEC, int VP = 2>
+__global__ __launch_bounds__(kNT) void k_update_xp_f64(int64_t n, double *__restrict__ x, double *__restrict__ p,
+                                                       const double *__restrict__ r, const double *rsold,
+                                                       const double *pAp, const double *rr) {
+    const double alpha = *rsold / *pAp;
+    const bool upd_p = rr != nullptr;
+    const double beta = upd_p ? *rr / *rsold : 0.0;
+    if constexpr (VEC) {
+        CGX_VEC_LOOP_BEGIN
+        d2 xv[kVU], pv[kVU], rv[kVU];
+#pragma unroll
+        for (int u = 0; u < kVU; ++u)
+            if (ok[u]) {
+                const int64_t i = 2 * (base + u * kNT);
+                xv[u] = ldv<VP>(x + i);
+                pv[u] = ldv<VP>(p + i);
+                if (upd_p) rv[u] = ldv<VP>(r + i);
+            }
+#pragma unroll
+        for (int u = 0; u < kVU; ++u)
+            if (ok[u]) {
+                const int64_t i = 2 * (base + u * kNT);
+                stv<VP>(x + i, xv[u] + alpha * pv[u]);
+                if (upd_p) stv<VP>(p + i, rv[u] + beta * pv[u]);
+            }
+        CGX_VEC_LOOP_END
+        if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+            x[n - 1] = x[n - 1] + alpha * p[n - 1];
+            if (upd_p) p[n - 1] = r[n - 1] + beta * p[n - 1];
+        }
+    } else {
+        for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kNT) {
+            x[i] = x[i] + alpha * p[i];
+            if (upd_p) p[i] = r[i] + beta * p[i];
+        }
     }
 }
 
@@ -742,16 +845,37 @@ hipError_t update_xr_f64(int64_t n, double *x, double *r, const double *p, const
                          const double *rsold, const double *pAp, double *rr_out, const RedWs &ws,
                          hipStream_t s) {
     const bool vec = al16(x) && al16(r) && al16(p) && al16(Ap);
-    hipLaunchKernelGGL(vec ? k_update_xr_f64<true> : k_update_xr_f64<false>, dim3(grid_vec(n)), dim3(kNT), 0, s, n,
-                       x, r, p, Ap, rsold, pAp, rr_out, ws.partials, ws.tickets + T_XR);
+    const int vp = env_int("CGX_VEC_POLICY", 2);
+    auto fn = !vec ? k_update_xr_f64<false> : vp == 1 ? k_update_xr_f64<true, 1>
+                                            : vp == 2 ? k_update_xr_f64<true, 2> : k_update_xr_f64<true, 0>;
+    hipLaunchKernelGGL(fn, dim3(grid_vec(n)), dim3(kNT), 0, s, n, x, r, p, Ap, rsold, pAp, rr_out, ws.partials,
+                       ws.tickets + T_XR);
     return hipGetLastError();
 }
 
 hipError_t update_p_f64(int64_t n, double *p, const double *r, const double *rr, const double *rsold,
                         hipStream_t s) {
     const bool vec = al16(p) && al16(r);
-    hipLaunchKernelGGL(vec ? k_update_p_f64<true> : k_update_p_f64<false>, dim3(grid_vec(n)), dim3(kNT), 0, s, n, p,
-                       r, rr, rsold);
+    const int vp = env_int("CGX_VEC_POLICY", 2);
+    auto fn = !vec ? k_update_p_f64<false> : vp == 1 ? k_update_p_f64<true, 1>
+                                           : vp == 2 ? k_update_p_f64<true, 2> : k_update_p_f64<true, 0>;
+    hipLaunchKernelGGL(fn, dim3(grid_vec(n)), dim3(kNT), 0, s, n, p, r, rr, rsold);
+    return hipGetLastError();
+}
+
+hipError_t update_r_f64(int64_t n, double *r, const double *Ap, const double *rsold, const double *pAp,
+                        double *rr_out, const RedWs &ws, hipStream_t s) {
+    const bool vec = al16(r) && al16(Ap);
+    hipLaunchKernelGGL(vec ? k_update_r_f64<true> : k_update_r_f64<false>, dim3(grid_vec(n)), dim3(kNT), 0, s, n, r,
+                       Ap, rsold, pAp, rr_out, ws.partials, ws.tickets + T_XR);
+    return hipGetLastError();
+}
+
+hipError_t update_xp_f64(int64_t n, double *x, double *p, const double *r, const double *rsold, const double *pAp,
+                         const double *rr, hipStream_t s) {
+    const bool vec = al16(x) && al16(p) && al16(r);
+    hipLaunchKernelGGL(vec ? k_update_xp_f64<true> : k_update_xp_f64<false>, dim3(grid_vec(n)), dim3(kNT), 0, s, n, x,
+                       p, r, rsold, pAp, rr);
     return hipGetLastError();
 }
 
