@@ -243,7 +243,8 @@ def main(argv=None) -> int:
                          f"row-block over {world} GPU(s), fixed-count iterations") if stream else
                         (f"configs[4]: matrix-free 5-point Poisson CG, m={m} (N={n}), b=1, x0=0, slabs over {world} "
                          f"GPU(s), halo exchange, fixed-count iterations") if poisson else
-                        f"configs[2]: N={n} dense SPD fp64 CG, row-block over {world} GPU(s), fixed-count iterations",
+                        (f"configs[{1 if n == 16384 else 2}]: N={n} dense SPD fp64 CG, row-block over {world} GPU(s), "
+                         f"fixed-count iterations"),
             "n": n,
             "rows_per_gpu": nloc,
             "parallelism": f"rowblock{world}",

@@ -325,3 +325,35 @@ def test_p2p_exchange_mode(P):
         x1, s1 = s.solve(None, eps=1e-10)
     xo, so = oracle.cg_f64(A, b, x0, eps=1e-10)
     assert s1.iterations == so.iterations and rel(x1, xo) <= TOL
+
+
+@pytest.mark.parametrize("n,P", [(1, 1), (3, 3), (1001, 7), (1000, 8), (640, 5)])
+def test_ragged_sizes_and_blocks(n, P):
+    """Odd n, row blocks of odd length (unaligned vector slices -> scalar
+    kernels), blocks not 128-aligned (no overlap): fp64 within 1e-10 of the
+    oracle, F32_REF bit-exact to the P-part oracle."""
+    A, b = oracle.spd_hash(n, seed=n)
+    with cg.Solver(n, devices=[0] * P) as s:
+        s.set_system(A, b)
+        x, st = s.solve(None, eps=1e-10)
+    xo, so = oracle.cg_f64(A, b, np.zeros(n), eps=1e-10)
+    assert st.iterations == so.iterations and rel(x, xo) <= TOL
+    A32, b32 = A.astype(np.float32), b.astype(np.float32)
+    with cg.Solver(n, flags=cg.CGX_F32_REF, devices=[0] * P) as s:
+        s.set_system(A32, b32)
+        x32, st32 = s.solve(None, eps=1e-6)
+    ref, sr = oracle.cg_f32ref(A32, b32, np.zeros(n, np.float32), nparts=P)
+    assert st32.iterations == sr.iterations and np.array_equal(x32, ref)
+
+
+def test_max_iter_cap_and_nonconvergence():
+    """Loop bound k < n (serialConjugate.c:213): a system that cannot meet eps
+    stops after exactly n iterations, unconverged."""
+    A, b, x0 = case("kat4", np.float64)
+    x = x0.copy()
+    st = cg.conjugrad(A, b, x, eps=0.0)           # sqrt(rr) < 0 never holds
+    assert st.iterations == 4 and st.converged == 0
+    assert np.allclose(x, [-1, 1, -1, 1], atol=1e-10)
+    x = x0.copy()
+    st = cg.conjugrad(A, b, x, eps=1e-12, max_iter=2)
+    assert st.iterations == 2 and st.converged == 0
