@@ -135,6 +135,24 @@ def cpu_baseline(n: int, iters: int = 5, threads_gen: int = 16) -> dict:
     }
 
 
+def cpu_baseline_poisson(m: int, iters: int = 3) -> dict:
+    """Oracle matrix-free Poisson CG (fp64 restatement), 1 host core."""
+    import numpy as np
+
+    import oracle
+    oracle.set_threads(1)
+    n = m * m
+    _, st = oracle.cg_poisson_f64(m, np.ones(n), np.zeros(n), max_iter=iters, eps=-1.0)
+    return {
+        "value": iters / st.t_loop_s,
+        "unit": "iterations/s",
+        "cores": 1,
+        "kind": "port",
+        "sample": (f"{iters} iterations of the same m={m} Poisson CG (fp64, oracle/cg_oracle.c "
+                   f"oracle_cg_poisson_f64; no reference counterpart exists), single thread; loop {st.t_loop_s:.2f} s"),
+    }
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
@@ -271,7 +289,9 @@ def main(argv=None) -> int:
         "check": {"relres": rnorm / bnorm},
         "iteration_gbps": (88.0 * n / (elapsed / args.steps) / 1e9) if poisson else None,
     }
-    if world == 1 and not args.no_cpu and not stream and not poisson:
+    if world == 1 and not args.no_cpu and poisson:
+        out["cpu_baseline"] = cpu_baseline_poisson(m)
+    elif world == 1 and not args.no_cpu and not stream:
         out["cpu_baseline"] = cpu_baseline(args.cpu_n or n)
     print(json.dumps(out), flush=True)
     if dist:

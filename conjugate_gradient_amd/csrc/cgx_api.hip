@@ -82,6 +82,8 @@ constexpr int kScalSlots = 136;  // 16 ring slots, up to 112 gathered partials, 
 constexpr int kMaxShards = 32;
 constexpr int S_RR = 0, S_PAP = 4, S_LRR = 8, S_LPAP = 12, S_GATHER = 16;
 constexpr int S_TR = 128, S_TB = 129, S_LTR = 130, S_LTB = 131;  // true-residual check
+constexpr int S_KDONE = 132, S_RRFINAL = 133;  // device-side convergence: k+1 at the break, r.r there
+constexpr int kLookRing = 8;                    // pinned slots for the host's lagged convergence checks
 inline int ring(int64_t j) { return (int)(j & 3); }
 
 enum Mode { M_SINGLE = 0, M_LOCAL = 1, M_RCCL = 2 };
@@ -120,6 +122,7 @@ struct Shard {
     bool buf_used[kStreamBufs] = {};
     int next_buf = 0;
     MatvecPlan tile_plan;
+    hipEvent_t ev_look[8] = {};  // lagged convergence checks (kLookRing)
     // overlap of the p exchange with the own-column-block matVec
     hipStream_t cstream = nullptr;
     hipEvent_t ev_pready = nullptr, ev_gathered = nullptr;
@@ -218,7 +221,8 @@ int alloc_shard(cgx_ctx *c, Shard &s) {
     HIPT(hipMemsetAsync(s.scal, 0, kScalSlots * 8, s.stream));
     HIPT(hipMemsetAsync(s.ws.tickets, 0, kTickets * sizeof(unsigned), s.stream));
     if (s.xfull) HIPT(hipMemsetAsync(s.xfull, 0, xlen * es, s.stream));
-    HIPT(hipHostMalloc(reinterpret_cast<void **>(&s.h_pin), 64, hipHostMallocDefault));
+    HIPT(hipHostMalloc(reinterpret_cast<void **>(&s.h_pin), 8 * (8 + kLookRing), hipHostMallocDefault));
+    for (int q = 0; q < kLookRing; ++q) HIPT(hipEventCreateWithFlags(&s.ev_look[q], hipEventDisableTiming));
     if (c->flags & CGX_TIMING) {
         s.ev_t.resize(2 * kEvPairs);
         for (auto &e : s.ev_t) HIPT(hipEventCreate(&e));
@@ -256,6 +260,8 @@ void free_shard(Shard &s) {
         (void)hipStreamDestroy(s.cstream);
     }
     if (s.ev_pready) (void)hipEventDestroy(s.ev_pready);
+    for (auto e : s.ev_look)
+        if (e) (void)hipEventDestroy(e);
     if (s.ev_gathered) (void)hipEventDestroy(s.ev_gathered);
     if (s.stream) (void)hipStreamDestroy(s.stream);
     s = Shard();
@@ -580,7 +586,7 @@ inline int out_slot(const cgx_ctx *c, int lslot, int gslot) { return c->mode == 
 // ---- the iteration pieces ----------------------------------------------------------
 // One tile of the matVec: rows [r0, r0+rows) of this shard, A rows at `Arows`.
 int matvec_rows(cgx_ctx *c, Shard &s, const MatvecPlan &pl, const char *Arows, int64_t r0, int64_t rows,
-                const char *vec, bool fuse_dot, int dot_slot) {
+                const char *vec, bool fuse_dot, int dot_slot, bool gated = false) {
     if (f32ref(c)) {
         HIPT(matvec_ref_f32(reinterpret_cast<const float *>(Arows), c->lda, rows, c->n,
                             reinterpret_cast<const float *>(vec), reinterpret_cast<float *>(s.Ap) + r0, s.stream));
@@ -588,7 +594,8 @@ int matvec_rows(cgx_ctx *c, Shard &s, const MatvecPlan &pl, const char *Arows, i
         HIPT(matvec_f64(pl, reinterpret_cast<const double *>(Arows), c->lda, rows, c->lda,
                         reinterpret_cast<const double *>(vec), reinterpret_cast<double *>(s.Ap) + r0,
                         fuse_dot ? reinterpret_cast<const double *>(s.pown) + r0 : nullptr,
-                        fuse_dot ? reinterpret_cast<double *>(slot(s, dot_slot)) : nullptr, s.ws, s.stream));
+                        fuse_dot ? reinterpret_cast<double *>(slot(s, dot_slot)) : nullptr, s.ws, s.stream,
+                        gated ? reinterpret_cast<const int64_t *>(slot(s, S_KDONE)) : nullptr));
     }
     return CGX_OK;
 }
@@ -620,16 +627,21 @@ int matvec_streamed(cgx_ctx *c, Shard &s, const char *vec) {
     return CGX_OK;
 }
 
-int launch_matvec(cgx_ctx *c, Shard &s, const char *vec, bool with_dot, int dot_slot) {
+inline const int64_t *gate_of(const Shard &s, bool gated) {
+    return gated ? reinterpret_cast<const int64_t *>(slot(s, S_KDONE)) : nullptr;
+}
+
+int launch_matvec(cgx_ctx *c, Shard &s, const char *vec, bool with_dot, int dot_slot, bool gated = false) {
     const bool timing = (c->flags & CGX_TIMING) && (&s == &c->sh[0]);
     if (timing && s.ev_used >= kEvPairs) TRY(timing_resolve(c));
     if (timing) HIPT(hipEventRecord(s.ev_t[2 * s.ev_used], s.stream));
     const bool streamed = (c->flags & CGX_HOST_STREAM) != 0;
     if (c->op == OP_POISSON)
         HIPT(stencil5_f64(reinterpret_cast<const double *>(vec), s.nloc / c->m, c->m, reinterpret_cast<double *>(s.Ap),
-                          with_dot ? reinterpret_cast<double *>(slot(s, dot_slot)) : nullptr, s.ws, s.stream));
+                          with_dot ? reinterpret_cast<double *>(slot(s, dot_slot)) : nullptr, s.ws, s.stream,
+                          gate_of(s, gated)));
     else if (streamed) TRY(matvec_streamed(c, s, vec));
-    else TRY(matvec_rows(c, s, s.plan, s.A, 0, s.nloc, vec, with_dot && !f32ref(c), dot_slot));
+    else TRY(matvec_rows(c, s, s.plan, s.A, 0, s.nloc, vec, with_dot && !f32ref(c), dot_slot, gated));
     if (timing) {
         HIPT(hipEventRecord(s.ev_t[2 * s.ev_used + 1], s.stream));
         s.ev_used++;
@@ -669,6 +681,10 @@ int do_begin(cgx_ctx *c) {
         }
     }
     TRY(exchange_scalar(c, ls, gs));
+    for (auto &s : c->sh) {  // device-side convergence record: not converged
+        TRY(set_dev(s));
+        HIPT(hipMemsetAsync(slot(s, S_KDONE), 0, 16, s.stream));
+    }
     c->k = 0;
     c->converged = 0;
     c->state = ST_BEGUN;
@@ -694,7 +710,7 @@ int read_scalar(cgx_ctx *c, int gslot, double *out) {
 // stream while the compute stream multiplies the shard's own column block
 // (its own p is already local); the rest of the columns follow once the
 // gather has landed, accumulating into Ap with the fused p.Ap partial.
-int overlapped_matvec(cgx_ctx *c, int dot_slot) {
+int overlapped_matvec(cgx_ctx *c, int dot_slot, bool gated) {
     const size_t es = (size_t)c->es;
     for (auto &s : c->sh) {
         TRY(set_dev(s));
@@ -724,11 +740,11 @@ int overlapped_matvec(cgx_ctx *c, int dot_slot) {
         const double *v = reinterpret_cast<const double *>(s.pfull);
         double *Ap = reinterpret_cast<double *>(s.Ap);
         HIPT(matvec_f64_cols(s.plan, A, c->lda, s.nloc, c->lda, s.row0, s.nloc, false, v, Ap, nullptr, nullptr,
-                             s.ws, s.stream));
+                             s.ws, s.stream, gate_of(s, gated)));
         HIPT(hipStreamWaitEvent(s.stream, s.ev_gathered, 0));
         HIPT(matvec_f64_cols(s.plan, A, c->lda, s.nloc, c->lda, (s.row0 + s.nloc) % c->lda, c->lda - s.nloc, true,
                              v, Ap, reinterpret_cast<const double *>(s.pown),
-                             reinterpret_cast<double *>(slot(s, dot_slot)), s.ws, s.stream));
+                             reinterpret_cast<double *>(slot(s, dot_slot)), s.ws, s.stream, gate_of(s, gated)));
         if (timing) {
             HIPT(hipEventRecord(s.ev_t[2 * s.ev_used + 1], s.stream));
             s.ev_used++;
@@ -740,17 +756,19 @@ int overlapped_matvec(cgx_ctx *c, int dot_slot) {
 // One loop iteration k (serialConjugate.c:215-244 / parallel_cg.c:290-323).
 // Returns 1 in *stop when sqrt(r.r) < eps ended the loop (before the p update,
 // as the reference breaks at :235-238).
-int do_iteration(cgx_ctx *c, double eps, int *stop) {
+// gated: fp64 device-side convergence (the host does not read r.r here; the
+// update kernel decides sqrt(r.r) < eps and later kernels skip themselves).
+int do_iteration(cgx_ctx *c, double eps, int *stop, bool gated = false) {
     const int64_t k = c->k;
     *stop = 0;
     const int pg = S_PAP + ring(k), pl = S_LPAP + ring(k);
     if (c->overlap) {
-        TRY(overlapped_matvec(c, out_slot(c, pl, pg)));  // parallel_cg.c:290-293, overlapped
+        TRY(overlapped_matvec(c, out_slot(c, pl, pg), gated));  // parallel_cg.c:290-293, overlapped
     } else {
         TRY(exchange_allgather(c, false));  // MPI_Allgather(local_p -> p)  parallel_cg.c:290
         for (auto &s : c->sh) {
             TRY(set_dev(s));
-            TRY(launch_matvec(c, s, s.pfull, true, out_slot(c, pl, pg)));  // :215 / :292-293
+            TRY(launch_matvec(c, s, s.pfull, true, out_slot(c, pl, pg), gated));  // :215 / :292-293
         }
     }
     TRY(exchange_scalar(c, pl, pg));  // MPI_Allreduce(p.Ap)  parallel_cg.c:294
@@ -771,12 +789,25 @@ int do_iteration(cgx_ctx *c, double eps, int *stop) {
             HIPT(update_r_f64(s.nloc, reinterpret_cast<double *>(s.r), reinterpret_cast<const double *>(s.Ap),
                               reinterpret_cast<const double *>(slot(s, S_RR + ring(k))),
                               reinterpret_cast<const double *>(slot(s, pg)), reinterpret_cast<double *>(slot(s, ro)),
-                              s.ws, s.stream));
+                              s.ws, s.stream, gate_of(s, gated)));
         }
     }
     TRY(exchange_scalar(c, rl, rg));  // MPI_Allreduce(r.r)  parallel_cg.c:313
     c->k = k + 1;
     c->total_iters += 1;
+    if (gated) {  // x (+ p unless converged) on the device, stopping rule decided there
+        for (auto &s : c->sh) {
+            TRY(set_dev(s));
+            HIPT(update_xp_f64(s.nloc, reinterpret_cast<double *>(s.x), reinterpret_cast<double *>(s.pown),
+                               reinterpret_cast<const double *>(s.r),
+                               reinterpret_cast<const double *>(slot(s, S_RR + ring(k))),
+                               reinterpret_cast<const double *>(slot(s, pg)),
+                               reinterpret_cast<const double *>(slot(s, rg)), s.stream, eps, k,
+                               reinterpret_cast<int64_t *>(slot(s, S_KDONE)),
+                               reinterpret_cast<double *>(slot(s, S_RRFINAL))));
+        }
+        return CGX_OK;
+    }
     if (eps >= 0.0) {  // if (sqrt(beta) < EPSILON) break;  serialConjugate.c:235-238
         double rr = 0.0;
         TRY(read_scalar(c, rg, &rr));
@@ -1167,9 +1198,61 @@ int cgx_solve_begin(cgx_ctx *c) {
     return do_begin(c);
 }
 
+// Convergence-tested iterations without a host round trip per iteration:
+// the update kernel decides sqrt(r.r) < eps on the device and records k+1;
+// queued later iterations skip themselves.  The host keeps `look` iterations
+// in flight and reads the record of an older iteration (pinned memory,
+// event-ordered), so at most `look` no-op iterations are ever enqueued.
+static int iterate_gated(cgx_ctx *c, int64_t count, double eps, int64_t *done, int *converged) {
+    Shard &s0 = c->sh[0];
+    const char *la = std::getenv("CGX_LOOKAHEAD");
+    const int look = std::max(1, std::min(kLookRing - 1, (la && *la) ? std::atoi(la) : 2));
+    const int64_t k0 = c->k;
+    int64_t issued = 0, kd = 0;
+    int64_t *pin = reinterpret_cast<int64_t *>(s0.h_pin) + 8;  // kLookRing slots after read_scalar's
+    for (; issued < count && kd == 0; ++issued) {
+        int stop = 0;
+        TRY(do_iteration(c, eps, &stop, /*gated=*/true));
+        TRY(set_dev(s0));
+        const int q = (int)(issued % kLookRing);
+        HIPT(hipMemcpyAsync(pin + q, slot(s0, S_KDONE), 8, hipMemcpyDeviceToHost, s0.stream));
+        HIPT(hipEventRecord(s0.ev_look[q], s0.stream));
+        if (issued >= look) {
+            const int qq = (int)((issued - look) % kLookRing);
+            HIPT(hipEventSynchronize(s0.ev_look[qq]));
+            kd = pin[qq];
+        }
+    }
+    TRY(sync_all(c));
+    double rrf = 0.0;
+    int64_t kdev = 0;
+    TRY(set_dev(s0));
+    HIPT(hipMemcpy(&kdev, slot(s0, S_KDONE), 8, hipMemcpyDeviceToHost));
+    const int64_t did = kdev ? (kdev - k0) : issued;
+    c->total_iters += did - issued;  // do_iteration counted every enqueued one
+    if (kdev) {
+        TRY(read_scalar(c, S_RRFINAL, &rrf));
+        c->last_rr = rrf;
+        c->k = kdev;
+        c->converged = 1;
+        c->state = ST_CONVERGED;
+    } else {
+        double rr = 0.0;
+        TRY(read_scalar(c, S_RR + ring(c->k), &rr));
+        c->last_rr = rr;
+    }
+    if (done) *done = did;
+    if (converged) *converged = c->converged;
+    return CGX_OK;
+}
+
 int cgx_iterate(cgx_ctx *c, int64_t count, double eps, int64_t *done, int *converged) {
     if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
     if (c->state == ST_IDLE) return fail(CGX_ERR_STATE, "cgx_iterate before cgx_solve_begin");
+    const char *gv = std::getenv("CGX_GATED");
+    const bool gate_ok = !(gv && *gv == '0');
+    if (c->state == ST_BEGUN && count > 0 && eps >= 0.0 && !f32ref(c) && !(c->flags & CGX_HOST_STREAM) && gate_ok)
+        return iterate_gated(c, count, eps, done, converged);
     int64_t did = 0;
     for (; did < count && c->state == ST_BEGUN; ++did) {
         int stop = 0;

@@ -29,16 +29,19 @@ MatvecPlan plan_matvec_f64(int device, int64_t rows, int R = 0, int U = 0, int n
 // ---- fp64 -------------------------------------------------------------------
 // out[i] = sum_j A[i*lda+j] v[j]; if pown != nullptr also *dot_out = pown . out
 // (last-block reduction, fixed order).
+// gate (optional): device word; when non-zero the kernel returns at once
+// (device-side convergence gating of queued iterations).
 hipError_t matvec_f64(const MatvecPlan &pl, const double *A, int64_t lda, int64_t rows,
                       int64_t cols, const double *v, double *out, const double *pown,
-                      double *dot_out, const RedWs &ws, hipStream_t s);
+                      double *dot_out, const RedWs &ws, hipStream_t s, const int64_t *gate = nullptr);
 // Columns [col_first, col_first+col_count) mod cols (all multiples of 128,
 // cols = the padded width): out[i] = (accumulate ? out[i] : 0) + partial row
 // sum; optional fused dot as above.  Used to overlap the p exchange with the
 // shard's own column block.
 hipError_t matvec_f64_cols(const MatvecPlan &pl, const double *A, int64_t lda, int64_t rows, int64_t cols,
                            int64_t col_first, int64_t col_count, bool accumulate, const double *v, double *out,
-                           const double *pown, double *dot_out, const RedWs &ws, hipStream_t s);
+                           const double *pown, double *dot_out, const RedWs &ws, hipStream_t s,
+                           const int64_t *gate = nullptr);
 // r = b - Ax; p = r (if p); *rr_out = r.r (if rr_out)
 hipError_t residual_f64(int64_t n, const double *b, const double *Ax, double *r, double *p,
                         double *rr_out, const RedWs &ws, hipStream_t s);
@@ -51,10 +54,14 @@ hipError_t update_p_f64(int64_t n, double *p, const double *r, const double *rr,
                         const double *rsold, hipStream_t s);
 // Solver split of the updates: r -= alpha Ap with *rr_out = r.r; then
 // x += alpha p and (rr != nullptr) p = r + (*rr / *rsold) p; alpha = *rsold / *pAp.
+// With kdone != nullptr update_xp also decides sqrt(*rr) < eps on the device:
+// on convergence it skips the p update and stores *kdone = k+1, *rrfinal = *rr;
+// once *kdone is in (0, k] both kernels (update_r via gate) do nothing.
 hipError_t update_r_f64(int64_t n, double *r, const double *Ap, const double *rsold, const double *pAp,
-                        double *rr_out, const RedWs &ws, hipStream_t s);
+                        double *rr_out, const RedWs &ws, hipStream_t s, const int64_t *gate = nullptr);
 hipError_t update_xp_f64(int64_t n, double *x, double *p, const double *r, const double *rsold, const double *pAp,
-                         const double *rr, hipStream_t s);
+                         const double *rr, hipStream_t s, double eps = -1.0, int64_t k = 0,
+                         int64_t *kdone = nullptr, double *rrfinal = nullptr);
 hipError_t dot_f64(int64_t n, const double *a, const double *b, double *out,
                    const RedWs &ws, hipStream_t s);
 // Rows [row0, row0+nrows) of the counter-hash SPD system; pad columns zeroed.
@@ -66,7 +73,7 @@ hipError_t sum_ordered_f64(const double *in, int cnt, double *out, hipStream_t s
 // 5-point Poisson A.p on a slab of mloc grid rows of width m; ph has one halo
 // row above and below.  *dot_out = ph[m..] . Ap when dot_out != nullptr.
 hipError_t stencil5_f64(const double *ph, int64_t mloc, int64_t m, double *Ap, double *dot_out, const RedWs &ws,
-                        hipStream_t s);
+                        hipStream_t s, const int64_t *gate = nullptr);
 hipError_t fill_f64(double *p, int64_t n, double v, hipStream_t s);
 hipError_t fill_f32(float *p, int64_t n, float v, hipStream_t s);
 

@@ -164,7 +164,8 @@ template <int R, int U, int NT>
 __global__ __launch_bounds__(kNT) void k_matvec_f64(
     const double *__restrict__ A, int64_t lda, int64_t rows, int64_t cols, int64_t vec_cols, int64_t cfirst,
     int64_t ccount, int tail, int accumulate, const double *__restrict__ v, double *__restrict__ out,
-    const double *__restrict__ pown, double *dot_out, double *partials, unsigned *ticket) {
+    const double *__restrict__ pown, double *dot_out, double *partials, unsigned *ticket, const int64_t *gate) {
+    if (gate && *gate) return;  // the solve converged in an earlier iteration (device-side gating)
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
     const int64_t ngroups = (rows + R - 1) / R;
@@ -365,7 +366,8 @@ __global__ __launch_bounds__(kNT) void k_update_p_f64(int64_t n, double *__restr
 template <bool VEC, int VP = 2>
 __global__ __launch_bounds__(kNT) void k_update_r_f64(int64_t n, double *__restrict__ r, const double *__restrict__ Ap,
                                                       const double *rsold, const double *pAp, double *rr_out,
-                                                      double *partials, unsigned *ticket) {
+                                                      double *partials, unsigned *ticket, const int64_t *gate) {
+    if (gate && *gate) return;
     const double alpha = *rsold / *pAp;
     double acc = 0.0;
     if constexpr (VEC) {
@@ -398,12 +400,35 @@ __global__ __launch_bounds__(kNT) void k_update_r_f64(int64_t n, double *__restr
 }
 
 // x += alpha p (alpha = rsold / pAp); then, if rr != nullptr, p = r + (rr / rsold) p.
+// With cv.kdone != nullptr (device-side gating) the kernel also makes the
+// reference's stopping decision, `sqrt(r.r) < EPSILON` (serialConjugate.c:235):
+// on convergence it does only the x update and records k+1 and r.r; in a
+// later iteration (kdone in (0, k]) it does nothing.
+struct ConvArgs {
+    double eps = -1.0;
+    int64_t k = 0;
+    int64_t *kdone = nullptr;   // 0 = not converged, else the loop-iteration count
+    double *rrfinal = nullptr;
+};
+
 template <bool VEC, int VP = 2>
 __global__ __launch_bounds__(kNT) void k_update_xp_f64(int64_t n, double *__restrict__ x, double *__restrict__ p,
                                                        const double *__restrict__ r, const double *rsold,
-                                                       const double *pAp, const double *rr) {
+                                                       const double *pAp, const double *rr, ConvArgs cv) {
+    bool upd_p = rr != nullptr;
+    if (cv.kdone) {
+        const int64_t kd = *cv.kdone;
+        if (kd != 0 && kd <= cv.k) return;
+        const double rrn = *rr;
+        if (cv.eps >= 0.0 && sqrt(rrn) < cv.eps) {
+            upd_p = false;
+            if (blockIdx.x == 0 && threadIdx.x == 0) {
+                *cv.rrfinal = rrn;
+                *cv.kdone = cv.k + 1;
+            }
+        }
+    }
     const double alpha = *rsold / *pAp;
-    const bool upd_p = rr != nullptr;
     const double beta = upd_p ? *rr / *rsold : 0.0;
     if constexpr (VEC) {
         CGX_VEC_LOOP_BEGIN
@@ -515,7 +540,8 @@ __global__ __launch_bounds__(kNT) void k_gen_spd(int64_t n, int64_t lda, int64_t
 __global__ __launch_bounds__(kNT) void k_stencil5_strip_f64(const double *__restrict__ ph, int64_t mloc, int64_t m,
                                                             int64_t nstrips, int64_t rows_per_block,
                                                             double *__restrict__ Ap, double *dot_out,
-                                                            double *partials, unsigned *ticket) {
+                                                            double *partials, unsigned *ticket, const int64_t *gate) {
+    if (gate && *gate) return;
     const int lane = threadIdx.x & 63;
     const int64_t strip = blockIdx.x % nstrips, chunk = blockIdx.x / nstrips;
     const int64_t j = strip * (2 * kNT) + 2 * threadIdx.x;
@@ -555,7 +581,8 @@ __global__ __launch_bounds__(kNT) void k_stencil5_strip_f64(const double *__rest
 // Odd m (rows not 16-B aligned): a block walks a run of rows, one column per thread.
 __global__ __launch_bounds__(kNT) void k_stencil5_rows_f64(const double *__restrict__ ph, int64_t mloc, int64_t m,
                                                            double *__restrict__ Ap, double *dot_out, double *partials,
-                                                           unsigned *ticket) {
+                                                           unsigned *ticket, const int64_t *gate) {
+    if (gate && *gate) return;
     const int64_t rows_per_block = (mloc + gridDim.x - 1) / gridDim.x;
     const int64_t i0 = (int64_t)blockIdx.x * rows_per_block;
     const int64_t i1 = (i0 + rows_per_block < mloc) ? i0 + rows_per_block : mloc;
@@ -725,7 +752,7 @@ unsigned grid_vec(int64_t n) { return grid_1d((n + 1) / 2, kNT * kVU, 2048); }
 inline bool al16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
 
 using MvFn = void (*)(const double *, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, int, int,
-                      const double *, double *, const double *, double *, double *, unsigned *);
+                      const double *, double *, const double *, double *, double *, unsigned *, const int64_t *);
 
 template <int R, int U>
 MvFn pick_nt(int nt) {
@@ -806,7 +833,7 @@ MatvecPlan plan_matvec_f64(int device, int64_t rows, int R, int U, int nt, int b
 
 hipError_t matvec_f64(const MatvecPlan &pl, const double *A, int64_t lda, int64_t rows, int64_t cols,
                       const double *v, double *out, const double *pown, double *dot_out,
-                      const RedWs &ws, hipStream_t s) {
+                      const RedWs &ws, hipStream_t s, const int64_t *gate) {
     if (rows <= 0) return hipSuccess;
     // The vector path needs 16-B-aligned rows and p; otherwise every column
     // goes through the scalar tail loop.
@@ -815,13 +842,14 @@ hipError_t matvec_f64(const MatvecPlan &pl, const double *A, int64_t lda, int64_
     const int64_t vec_cols = aligned ? (cols & ~int64_t(127)) : 0;
     MvFn fn = pick_mv(pl.R, pl.U, pl.nt);
     hipLaunchKernelGGL(fn, dim3(pl.blocks), dim3(kNT), 0, s, A, lda, rows, cols, vec_cols, int64_t(0),
-                       vec_cols >> 7, 1, 0, v, out, pown, dot_out, ws.partials, ws.tickets + T_MATVEC);
+                       vec_cols >> 7, 1, 0, v, out, pown, dot_out, ws.partials, ws.tickets + T_MATVEC, gate);
     return hipGetLastError();
 }
 
 hipError_t matvec_f64_cols(const MatvecPlan &pl, const double *A, int64_t lda, int64_t rows, int64_t cols,
                            int64_t col_first, int64_t col_count, bool accumulate, const double *v, double *out,
-                           const double *pown, double *dot_out, const RedWs &ws, hipStream_t s) {
+                           const double *pown, double *dot_out, const RedWs &ws, hipStream_t s,
+                           const int64_t *gate) {
     if (rows <= 0) return hipSuccess;
     if ((cols & 127) || (col_first & 127) || (col_count & 127) || (lda & 1) ||
         ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(v)) & 15))
@@ -829,7 +857,7 @@ hipError_t matvec_f64_cols(const MatvecPlan &pl, const double *A, int64_t lda, i
     MvFn fn = pick_mv(pl.R, pl.U, pl.nt);
     hipLaunchKernelGGL(fn, dim3(pl.blocks), dim3(kNT), 0, s, A, lda, rows, cols, cols, col_first >> 7,
                        col_count >> 7, 0, accumulate ? 1 : 0, v, out, pown, dot_out, ws.partials,
-                       ws.tickets + T_MATVEC);
+                       ws.tickets + T_MATVEC, gate);
     return hipGetLastError();
 }
 
@@ -864,18 +892,23 @@ hipError_t update_p_f64(int64_t n, double *p, const double *r, const double *rr,
 }
 
 hipError_t update_r_f64(int64_t n, double *r, const double *Ap, const double *rsold, const double *pAp,
-                        double *rr_out, const RedWs &ws, hipStream_t s) {
+                        double *rr_out, const RedWs &ws, hipStream_t s, const int64_t *gate) {
     const bool vec = al16(r) && al16(Ap);
     hipLaunchKernelGGL(vec ? k_update_r_f64<true> : k_update_r_f64<false>, dim3(grid_vec(n)), dim3(kNT), 0, s, n, r,
-                       Ap, rsold, pAp, rr_out, ws.partials, ws.tickets + T_XR);
+                       Ap, rsold, pAp, rr_out, ws.partials, ws.tickets + T_XR, gate);
     return hipGetLastError();
 }
 
 hipError_t update_xp_f64(int64_t n, double *x, double *p, const double *r, const double *rsold, const double *pAp,
-                         const double *rr, hipStream_t s) {
+                         const double *rr, hipStream_t s, double eps, int64_t k, int64_t *kdone, double *rrfinal) {
     const bool vec = al16(x) && al16(p) && al16(r);
+    ConvArgs cv;
+    cv.eps = eps;
+    cv.k = k;
+    cv.kdone = kdone;
+    cv.rrfinal = rrfinal;
     hipLaunchKernelGGL(vec ? k_update_xp_f64<true> : k_update_xp_f64<false>, dim3(grid_vec(n)), dim3(kNT), 0, s, n, x,
-                       p, r, rsold, pAp, rr);
+                       p, r, rsold, pAp, rr, cv);
     return hipGetLastError();
 }
 
@@ -904,7 +937,7 @@ hipError_t gen_spd_f32(int64_t n, int64_t lda, int64_t row0, int64_t nrows, uint
 }
 
 hipError_t stencil5_f64(const double *ph, int64_t mloc, int64_t m, double *Ap, double *dot_out, const RedWs &ws,
-                        hipStream_t s) {
+                        hipStream_t s, const int64_t *gate) {
     if (mloc <= 0) return hipSuccess;
     if ((m & 1) == 0 && al16(ph) && al16(Ap)) {
         const int64_t nstrips = (m + 2 * kNT - 1) / (2 * kNT);
@@ -915,11 +948,11 @@ hipError_t stencil5_f64(const double *ph, int64_t mloc, int64_t m, double *Ap, d
         int64_t grid = nstrips * chunks;
         if (grid > kMaxRedBlocks) return hipErrorInvalidValue;
         hipLaunchKernelGGL(k_stencil5_strip_f64, dim3((unsigned)grid), dim3(kNT), 0, s, ph, mloc, m, nstrips, rpb, Ap,
-                           dot_out, ws.partials, ws.tickets + T_MATVEC);
+                           dot_out, ws.partials, ws.tickets + T_MATVEC, gate);
     } else {
         const unsigned grid = (unsigned)std::min<int64_t>(mloc, 2048);
         hipLaunchKernelGGL(k_stencil5_rows_f64, dim3(grid), dim3(kNT), 0, s, ph, mloc, m, Ap, dot_out, ws.partials,
-                           ws.tickets + T_MATVEC);
+                           ws.tickets + T_MATVEC, gate);
     }
     return hipGetLastError();
 }

@@ -357,3 +357,27 @@ def test_max_iter_cap_and_nonconvergence():
     x = x0.copy()
     st = cg.conjugrad(A, b, x, eps=1e-12, max_iter=2)
     assert st.iterations == 2 and st.converged == 0
+
+
+@pytest.mark.parametrize("shards", [None, [0, 0, 0, 0]])
+def test_device_gated_convergence_matches_host_checked(monkeypatch, shards):
+    """Device-side stopping decision (default for fp64) == the host-checked
+    loop (CGX_GATED=0): same loop count, same x bits, no extra iteration
+    leaks into x; stats report the converged count and r.r."""
+    A, b = oracle.spd_hash(2048, seed=3)
+    res = {}
+    for gated in ("1", "0"):
+        monkeypatch.setenv("CGX_GATED", gated)
+        for look in ("1", "2", "5"):
+            monkeypatch.setenv("CGX_LOOKAHEAD", look)
+            with cg.Solver(2048, devices=shards) as s:
+                s.set_system(A, b)
+                x, st = s.solve(None, eps=1e-10)
+                res[(gated, look)] = (x, st.iterations, st.converged, st.rr, s.stats().total_iterations)
+    ref = res[("0", "1")]
+    for key, (x, it, conv, rr, tot) in res.items():
+        assert it == ref[1] and conv == 1 and tot == it, key
+        assert np.array_equal(x, ref[0]), key
+        assert rr == ref[3] and np.sqrt(rr) < 1e-10
+    xo, so = oracle.cg_f64(A, b, np.zeros(2048), eps=1e-10)
+    assert ref[1] == so.iterations and rel(ref[0], xo) <= TOL
