@@ -156,11 +156,71 @@ __device__ __forceinline__ void mv_chunks(const d2 *const (&arow)[R], const __am
     }
 }
 
+// Software-pipelined variant: the loads of step c+U are issued before the
+// FMAs of step c (two register sets, ping-pong), so a wave always has a
+// step's loads in flight.
+template <int R, int U, int NT>
+__device__ __forceinline__ void mv_load_step(const d2 *const (&arow)[R], const __amdgpu_buffer_rsrc_t (&rs)[R], int lane,
+                                             const d2 *v2, int64_t c, d2 (&pv)[U], d2 (&av)[R][U]) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) pv[u] = v2[(c + u) * 64];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if constexpr (NT >= 2) av[r][u] = load_a_buf<NT>(rs[r], c + u, lane);
+            else av[r][u] = load_a<NT>(arow[r] + (c + u) * 64);
+        }
+}
+
+template <int R, int U>
+__device__ __forceinline__ void mv_fma_step(const d2 (&pv)[U], const d2 (&av)[R][U], d2 (&acc)[R]) {
+#pragma unroll
+    for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            acc[r].x = __builtin_fma(av[r][u].x, pv[u].x, acc[r].x);
+            acc[r].y = __builtin_fma(av[r][u].y, pv[u].y, acc[r].y);
+        }
+}
+
+template <int R, int U, int NT>
+__device__ __forceinline__ void mv_chunks_pipe(const d2 *const (&arow)[R], const __amdgpu_buffer_rsrc_t (&rs)[R],
+                                               int lane, const d2 *v2, int64_t c0, int64_t c1, d2 (&acc)[R]) {
+    d2 pa[U], aa[R][U], pb[U], ab[R][U];
+    int64_t c = c0;
+    if (c + U <= c1) mv_load_step<R, U, NT>(arow, rs, lane, v2, c, pa, aa);
+    while (c + U <= c1) {
+        const bool more = c + 2 * U <= c1;
+        if (more) mv_load_step<R, U, NT>(arow, rs, lane, v2, c + U, pb, ab);
+        mv_fma_step<R, U>(pa, aa, acc);
+        c += U;
+        if (!more) break;
+        const bool more2 = c + 2 * U <= c1;
+        if (more2) mv_load_step<R, U, NT>(arow, rs, lane, v2, c + U, pa, aa);
+        mv_fma_step<R, U>(pb, ab, acc);
+        c += U;
+        if (!more2) break;
+    }
+    // remaining single chunks
+    for (; c < c1; ++c) {
+        const d2 pv = v2[c * 64];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            d2 a;
+            if constexpr (NT >= 2) a = load_a_buf<NT>(rs[r], c, lane);
+            else a = load_a<NT>(arow[r] + c * 64);
+            acc[r].x = __builtin_fma(a.x, pv.x, acc[r].x);
+            acc[r].y = __builtin_fma(a.y, pv.y, acc[r].y);
+        }
+    }
+}
+
 // Column range: the `ccount` 128-column chunks starting at chunk `cfirst`,
 // wrapping modulo the vec_cols/128 aligned chunks; `tail` adds the scalar
 // columns [vec_cols, cols).  `accumulate` adds the existing out[i] (the
 // overlap path computes the shard's own column block first, then the rest).
-template <int R, int U, int NT>
+template <int R, int U, int NT, bool PIPE = false>
 __global__ __launch_bounds__(kNT) void k_matvec_f64(
     const double *__restrict__ A, int64_t lda, int64_t rows, int64_t cols, int64_t vec_cols, int64_t cfirst,
     int64_t ccount, int tail, int accumulate, const double *__restrict__ v, double *__restrict__ out,
@@ -193,8 +253,13 @@ __global__ __launch_bounds__(kNT) void k_matvec_f64(
             }
             acc[r] = (d2)(0.0);
         }
-        mv_chunks<R, U, NT>(arow, rs, lane, v2, ca, cb, acc);
-        if (wrap > 0) mv_chunks<R, U, NT>(arow, rs, lane, v2, 0, wrap, acc);
+        if constexpr (PIPE) {
+            mv_chunks_pipe<R, U, NT>(arow, rs, lane, v2, ca, cb, acc);
+            if (wrap > 0) mv_chunks_pipe<R, U, NT>(arow, rs, lane, v2, 0, wrap, acc);
+        } else {
+            mv_chunks<R, U, NT>(arow, rs, lane, v2, ca, cb, acc);
+            if (wrap > 0) mv_chunks<R, U, NT>(arow, rs, lane, v2, 0, wrap, acc);
+        }
         if (tail)
             for (int64_t j = ctail + lane; j < cols; j += 64) {
                 const double vj = v[j];
@@ -763,6 +828,8 @@ MvFn pick_nt(int nt) {
         case 4: return k_matvec_f64<R, U, 4>;
         case 5: return k_matvec_f64<R, U, 5>;
         case 6: return k_matvec_f64<R, U, 6>;
+        case 7: return k_matvec_f64<R, U, 2, true>;  // pipelined, buffer nt
+        case 8: return k_matvec_f64<R, U, 1, true>;  // pipelined, global nt
         default: return k_matvec_f64<R, U, 1>;
     }
 }
@@ -792,21 +859,17 @@ MvFn pick_mv(int R, int U, int nt) {
 MatvecPlan plan_matvec_f64(int device, int64_t rows, int R, int U, int nt, int blocks_per_cu) {
     MatvecPlan pl;
     const int cus = cu_count(device);
-    // Rows per wave: the most rows that still leave >= 4 row groups (waves)
-    // per CU.  Measured on MI355X (profiles/r01_sweep_*): with nt loads R=8,
-    // U=8 is best or within 1% of best from 8192 to 65536 rows (7.0-7.06 TB/s);
-    // default-policy loads are 11% slower (6.2-6.3 TB/s).
+    // Software-pipelined (loads of step c+U issued before the FMAs of step c),
+    // 2 rows per wave, U=8, global_load ... nt: 256 VGPRs, one wave per SIMD,
+    // 32 KiB of A in flight per wave.  Measured on MI355X, interleaved against
+    // every (R, U, policy) of the unpipelined kernel (profiles/r01_sweep_pipe*):
+    // 7.24 TB/s at 65536^2 (unpipelined best R=8,U=8,buffer-nt: 7.09),
+    // 7.21 TB/s on an 8192 x 65536 row block (7.05), 6.81 TB/s at 16384^2 (6.60).
+    // R=1 when there are fewer than 2 rows per resident wave.
     const int64_t want_waves = (int64_t)cus * 4;
-    if (rows >= 8 * want_waves) pl.R = 8;
-    else if (rows >= 4 * want_waves) pl.R = 4;
-    else if (rows >= 2 * want_waves) pl.R = 2;
-    else pl.R = 1;
+    pl.R = rows >= 2 * want_waves ? 2 : 1;
     pl.U = 8;
-    // buffer_load ... nt through per-row scalar descriptors: the same stream
-    // policy as global_load ... nt but no 64-bit row addresses in VGPRs (189
-    // vs 256 VGPRs at R=U=8: 2 waves/SIMD instead of 1); +0.5-1% measured
-    // (profiles/r01_sweep_policy*.jsonl).
-    pl.nt = 2;
+    pl.nt = 8;
     pl.R = env_int("CGX_MV_R", pl.R);
     pl.U = env_int("CGX_MV_U", pl.U);
     pl.nt = env_int("CGX_MV_NT", pl.nt);
@@ -815,7 +878,7 @@ MatvecPlan plan_matvec_f64(int device, int64_t rows, int R, int U, int nt, int b
     if (nt >= 0) pl.nt = nt;
     if (pl.R != 1 && pl.R != 2 && pl.R != 4 && pl.R != 8) pl.R = 4;
     if (pl.U != 2 && pl.U != 4 && pl.U != 8) pl.U = 4;
-    if (pl.nt < 0 || pl.nt > 6) pl.nt = 1;
+    if (pl.nt < 0 || pl.nt > 8) pl.nt = 1;
     if (pl.U == 2 && pl.nt >= 2) pl.nt = 1;  // buffer variants exist for U = 4, 8
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(pick_mv(pl.R, pl.U, pl.nt)),

@@ -179,8 +179,9 @@ int cgx_synchronize(cgx_ctx *ctx);
 void *cgx_stream(cgx_ctx *ctx);
 /* Tuning of the fp64 matVec (k_matvec_f64): rows per wave (1,2,4,8), 128-column
  * chunks in flight per row (2,4,8), the A load policy (0 plain, 1 non-temporal
- * global loads = default, 2..6 buffer loads with cache bits nt / nt sc1 /
- * sc0 nt sc1 / sc1 / none; 2..6 need chunks 4 or 8), resident
+ * global loads, 2..6 buffer loads with cache bits nt / nt sc1 / sc0 nt sc1 /
+ * sc1 / none, 7 software-pipelined buffer nt, 8 software-pipelined global nt
+ * = default; 2..8 need chunks 4 or 8), resident
  * blocks per CU for the grid (<= 0: occupancy query).  Results do not depend
  * on the plan's R/U/nt; the p.Ap partial order depends on the grid size. */
 int cgx_set_matvec_plan(cgx_ctx *ctx, int rows_per_wave, int chunks_in_flight, int nontemporal,
