@@ -159,6 +159,36 @@ def test_n16384_against_cpu_oracle():
     assert rn <= TOL * bn
 
 
+@pytest.mark.parametrize("P", [1, 8])
+def test_n65536_full_size_against_cpu_oracle(P):
+    """BASELINE.json's headline size, N=65536 (34.4 GB of A): one row block,
+    and the 8-GPU partition (8 blocks of 8192 rows) as 8 shards on this GPU.
+    Same loop count as conjgrad.m at tol 1e-10, x within 1e-10 of the fp64
+    oracle (16 host threads), true residual ||b-Ax|| <= 1e-10 ||b||."""
+    n = 65536
+    with cg.Solver(n, devices=[0] * P if P > 1 else None) as s:
+        s.generate_spd(seed=42)
+        x, st = s.solve(None, eps=1e-10)
+        rn, bn = s.residual_norm()
+    xo, so = _oracle_n65536()
+    assert st.converged and st.iterations == so.iterations
+    assert rel(x, xo) <= TOL
+    assert rn <= TOL * bn
+
+
+_ORACLE_CACHE = {}
+
+
+def _oracle_n65536():
+    if "x" not in _ORACLE_CACHE:
+        n = 65536
+        oracle.set_threads(16)
+        A, b = oracle.spd_hash(n, seed=42)
+        _ORACLE_CACHE["x"] = oracle.cg_f64(A, b, np.zeros(n), eps=1e-10)
+        del A
+    return _ORACLE_CACHE["x"]
+
+
 def test_solve_in_pieces_and_fixed_count():
     """cgx_solve_begin + cgx_iterate == cgx_solve; eps < 0 runs exactly max_iter."""
     A, b, x0 = case("spd1024", np.float64)
