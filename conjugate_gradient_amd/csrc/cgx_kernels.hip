@@ -220,6 +220,122 @@ __device__ __forceinline__ void mv_chunks_pipe(const d2 *const (&arow)[R], const
 // wrapping modulo the vec_cols/128 aligned chunks; `tail` adds the scalar
 // columns [vec_cols, cols).  `accumulate` adds the existing out[i] (the
 // overlap path computes the shard's own column block first, then the rest).
+// Flattened pipelined matVec: a wave walks (row group, step) pairs as one
+// stream, so the loads of the next group's first step are already in flight
+// while the current group's last FMAs, row sums and stores run (mv_chunks_pipe
+// drains at every group boundary: 1/16 of the steps at N=16384).  Row bases
+// are wave-uniform (readfirstlane), so each A load is an SGPR base plus a
+// 32-bit lane offset.  Requires both column pieces to be multiples of U
+// chunks (the host picks the plain kernel otherwise).
+template <int R, int U, int NT>
+__device__ __forceinline__ void mv_flat_load(const double *const (&base)[R], const __amdgpu_buffer_rsrc_t (&rs)[R],
+                                             int lane, const d2 *v2, int64_t c, d2 (&pv)[U], d2 (&av)[R][U]) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) pv[u] = v2[(c + u) * 64];
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            if constexpr (NT >= 2) {
+                av[r][u] = load_a_buf<NT>(rs[r], c + u, lane);
+            } else {
+                const uint32_t off = (uint32_t)(((c + u) * 64 + lane) * 16);
+                av[r][u] = load_a<NT>(reinterpret_cast<const d2 *>(reinterpret_cast<const char *>(base[r]) + off));
+            }
+        }
+}
+
+template <int R, int U, int NT>
+__global__ __launch_bounds__(kNT) void k_matvec_f64_flat(
+    const double *__restrict__ A, int64_t lda, int64_t rows, int64_t cols, int64_t vec_cols, int64_t cfirst,
+    int64_t ccount, int tail, int accumulate, const double *__restrict__ v, double *__restrict__ out,
+    const double *__restrict__ pown, double *dot_out, double *partials, unsigned *ticket, const int64_t *gate) {
+    if (gate && *gate) return;
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t ngroups = (rows + R - 1) / R;
+    const int64_t wstride = (int64_t)gridDim.x * (kNT / 64);
+    const int64_t nchunk = vec_cols >> 7;
+    const int64_t ctail = nchunk << 7;
+    const int64_t ca = cfirst, cb = (cfirst + ccount < nchunk) ? cfirst + ccount : nchunk;
+    const int64_t piece1 = cb - ca;
+    const int64_t S = (piece1 + (cfirst + ccount - cb)) / U;  // steps per row group
+    const d2 *v2 = reinterpret_cast<const d2 *>(v) + lane;
+    double dacc = 0.0;
+
+    // load cursor (group lg, step ls) and its row bases
+    int64_t lg = (int64_t)blockIdx.x * (kNT / 64) + wid, ls = 0;
+    const double *lbase[R];
+    __amdgpu_buffer_rsrc_t lrs[R];
+    auto set_rows = [&](int64_t g) {
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int64_t row = (g * R + r < rows) ? g * R + r : rows - 1;
+            lbase[r] = A + row * lda;
+            if constexpr (NT >= 2)
+                lrs[r] = __builtin_amdgcn_make_buffer_rsrc((void *)lbase[r], 0, (int)(lda * 8), 0x00020000);
+        }
+    };
+    auto col_of = [&](int64_t s) -> int64_t {
+        const int64_t o = s * U;
+        return o < piece1 ? ca + o : o - piece1;
+    };
+    // compute cursor (group cg, step cs)
+    int64_t cg = lg, cs = 0;
+    d2 acc[R];
+#pragma unroll
+    for (int r = 0; r < R; ++r) acc[r] = (d2)(0.0);
+    auto finish_group = [&]() {
+        const int64_t r0 = cg * R;
+        if (tail)
+            for (int64_t j = ctail + lane; j < cols; j += 64) {
+                const double vj = v[j];
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const int64_t row = (r0 + r < rows) ? r0 + r : rows - 1;
+                    acc[r].x = __builtin_fma(A[row * lda + j], vj, acc[r].x);
+                }
+            }
+        double mine = 0.0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const double s = wave_sum(acc[r].x + acc[r].y);
+            if (lane == r) mine = s;
+            acc[r] = (d2)(0.0);
+        }
+        if (lane < R && r0 + lane < rows) {
+            if (accumulate) mine = out[r0 + lane] + mine;
+            out[r0 + lane] = mine;
+            if (pown) dacc += pown[r0 + lane] * mine;
+        }
+    };
+
+    if (lg < ngroups && S > 0) {
+        d2 pa[U], aa[R][U], pb[U], ab[R][U];
+        set_rows(lg);
+        mv_flat_load<R, U, NT>(lbase, lrs, lane, v2, col_of(0), pa, aa);
+        for (;;) {
+            // ---- set A is in flight: issue B = next step, then consume A
+            if (++ls == S) { ls = 0; lg += wstride; if (lg < ngroups) set_rows(lg); }
+            bool more = lg < ngroups;
+            if (more) mv_flat_load<R, U, NT>(lbase, lrs, lane, v2, col_of(ls), pb, ab);
+            mv_fma_step<R, U>(pa, aa, acc);
+            if (++cs == S) { finish_group(); cs = 0; cg += wstride; }
+            if (!more) break;
+            // ---- set B is in flight: issue A = next step, then consume B
+            if (++ls == S) { ls = 0; lg += wstride; if (lg < ngroups) set_rows(lg); }
+            more = lg < ngroups;
+            if (more) mv_flat_load<R, U, NT>(lbase, lrs, lane, v2, col_of(ls), pa, aa);
+            mv_fma_step<R, U>(pb, ab, acc);
+            if (++cs == S) { finish_group(); cs = 0; cg += wstride; }
+            if (!more) break;
+        }
+    } else if (lg < ngroups) {  // no full chunks (vec_cols < 128): tail columns only
+        for (; cg < ngroups; cg += wstride) finish_group();
+    }
+    if (pown) grid_sum_last_block(dacc, partials, ticket, dot_out);
+}
+
 template <int R, int U, int NT, bool PIPE = false>
 __global__ __launch_bounds__(kNT) void k_matvec_f64(
     const double *__restrict__ A, int64_t lda, int64_t rows, int64_t cols, int64_t vec_cols, int64_t cfirst,
@@ -830,6 +946,8 @@ MvFn pick_nt(int nt) {
         case 6: return k_matvec_f64<R, U, 6>;
         case 7: return k_matvec_f64<R, U, 2, true>;  // pipelined, buffer nt
         case 8: return k_matvec_f64<R, U, 1, true>;  // pipelined, global nt
+        case 9: return k_matvec_f64_flat<R, U, 1>;    // flattened pipeline, global nt
+        case 10: return k_matvec_f64_flat<R, U, 2>;   // flattened pipeline, buffer nt
         default: return k_matvec_f64<R, U, 1>;
     }
 }
@@ -844,6 +962,15 @@ MvFn pick_u(int U, int nt) {
         case 8: return pick_nt<R, 8>(nt);
         default: return pick_nt<R, 4>(nt);
     }
+}
+// The flattened kernels need both column pieces to be whole steps of U
+// chunks; otherwise the per-group pipelined kernel takes the launch.
+int mv_policy(const MatvecPlan &pl, int64_t nchunk, int64_t cfirst, int64_t ccount) {
+    if (pl.nt < 9) return pl.nt;
+    const int64_t cb = std::min(cfirst + ccount, nchunk);
+    const int64_t p1 = cb - cfirst, p2 = cfirst + ccount - cb;
+    if (p1 % pl.U || p2 % pl.U) return pl.nt == 9 ? 8 : 7;
+    return pl.nt;
 }
 MvFn pick_mv(int R, int U, int nt) {
     switch (R) {
@@ -878,7 +1005,7 @@ MatvecPlan plan_matvec_f64(int device, int64_t rows, int R, int U, int nt, int b
     if (nt >= 0) pl.nt = nt;
     if (pl.R != 1 && pl.R != 2 && pl.R != 4 && pl.R != 8) pl.R = 4;
     if (pl.U != 2 && pl.U != 4 && pl.U != 8) pl.U = 4;
-    if (pl.nt < 0 || pl.nt > 8) pl.nt = 1;
+    if (pl.nt < 0 || pl.nt > 10) pl.nt = 1;
     if (pl.U == 2 && pl.nt >= 2) pl.nt = 1;  // buffer variants exist for U = 4, 8
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(pick_mv(pl.R, pl.U, pl.nt)),
@@ -903,7 +1030,7 @@ hipError_t matvec_f64(const MatvecPlan &pl, const double *A, int64_t lda, int64_
     const bool aligned = ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(v)) & 15) == 0 &&
                          (lda & 1) == 0;
     const int64_t vec_cols = aligned ? (cols & ~int64_t(127)) : 0;
-    MvFn fn = pick_mv(pl.R, pl.U, pl.nt);
+    MvFn fn = pick_mv(pl.R, pl.U, mv_policy(pl, vec_cols >> 7, 0, vec_cols >> 7));
     hipLaunchKernelGGL(fn, dim3(pl.blocks), dim3(kNT), 0, s, A, lda, rows, cols, vec_cols, int64_t(0),
                        vec_cols >> 7, 1, 0, v, out, pown, dot_out, ws.partials, ws.tickets + T_MATVEC, gate);
     return hipGetLastError();
@@ -917,7 +1044,7 @@ hipError_t matvec_f64_cols(const MatvecPlan &pl, const double *A, int64_t lda, i
     if ((cols & 127) || (col_first & 127) || (col_count & 127) || (lda & 1) ||
         ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(v)) & 15))
         return hipErrorInvalidValue;
-    MvFn fn = pick_mv(pl.R, pl.U, pl.nt);
+    MvFn fn = pick_mv(pl.R, pl.U, mv_policy(pl, cols >> 7, col_first >> 7, col_count >> 7));
     hipLaunchKernelGGL(fn, dim3(pl.blocks), dim3(kNT), 0, s, A, lda, rows, cols, cols, col_first >> 7,
                        col_count >> 7, 0, accumulate ? 1 : 0, v, out, pown, dot_out, ws.partials,
                        ws.tickets + T_MATVEC, gate);

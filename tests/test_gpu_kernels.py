@@ -107,3 +107,33 @@ def test_dot_and_updates_f64(n):
     r_ref = r - alpha * Ap
     np.testing.assert_allclose(r_d.to_host(), r_ref, rtol=1e-13, atol=1e-15)
     assert abs(rr_d.to_host()[0] - r_ref @ r_ref) <= F64_TOL * (r_ref @ r_ref)
+
+
+MV_PLANS = [(R, U, nt) for R in (1, 2, 4, 8) for U in (4, 8) for nt in (0, 1, 2, 7, 8, 9, 10)
+            if not (R == 8 and U == 8 and nt >= 7)] + [(R, 2, nt) for R in (1, 4) for nt in (0, 1)]
+
+
+@pytest.mark.parametrize("rows,cols", [(300, 1000), (1000, 1024), (517, 2176), (2048, 4096), (8192, 3200)])
+def test_matvec_f64_every_plan_bitwise_equal(monkeypatch, rows, cols):
+    """Every (rows per wave, chunks in flight, load policy) plan, including the
+    software-pipelined (7, 8) and flattened (9, 10) kernels and their fallback
+    when the chunk count is not a multiple of U, gives the same row sums bit
+    for bit: each lane accumulates its columns in ascending order whatever the
+    plan.  The default plan is checked against the fp64 oracle."""
+    rng = np.random.default_rng(rows + cols)
+    A = rng.random((rows, cols)) - 0.5
+    v = rng.random(cols)
+    A_d, v_d = dev(A), dev(v)
+    ref = oracle.matvec_f64(A, v)
+    out = cg.DeviceArray(rows)
+    cg.matVec(A_d, v_d, out, rows, cols)
+    base = out.to_host()
+    bound = F64_TOL * (np.abs(A) @ np.abs(v))
+    assert np.all(np.abs(base - ref) <= bound)
+    for R, U, nt in MV_PLANS:
+        monkeypatch.setenv("CGX_MV_R", str(R))
+        monkeypatch.setenv("CGX_MV_U", str(U))
+        monkeypatch.setenv("CGX_MV_NT", str(nt))
+        out = cg.DeviceArray(rows)
+        cg.matVec(A_d, v_d, out, rows, cols)
+        assert np.array_equal(out.to_host(), base), (R, U, nt)
