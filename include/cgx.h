@@ -181,7 +181,8 @@ void *cgx_stream(cgx_ctx *ctx);
  * chunks in flight per row (2,4,8), the A load policy (0 plain, 1 non-temporal
  * global loads, 2..6 buffer loads with cache bits nt / nt sc1 / sc0 nt sc1 /
  * sc1 / none, 7 software-pipelined buffer nt, 8 software-pipelined global nt
- * = default; 2..8 need chunks 4 or 8), resident
+ * = default, 9 / 10 flattened pipeline global / buffer nt; 2..10 need chunks
+ * 4 or 8), resident
  * blocks per CU for the grid (<= 0: occupancy query).  Results do not depend
  * on the plan's R/U/nt; the p.Ap partial order depends on the grid size. */
 int cgx_set_matvec_plan(cgx_ctx *ctx, int rows_per_wave, int chunks_in_flight, int nontemporal,
