@@ -194,6 +194,7 @@ def main(argv=None) -> int:
         solver = cg.Solver(n, device=0, flags=flags, poisson_m=m)
     nloc = solver.info.nrows
     overlap_on = bool(solver.info.flags & cg.CGX_OVERLAP_ACTIVE)
+    fused = bool(solver.info.flags & cg.CGX_FUSED_ACTIVE)
     plan = None if poisson else solver.matvec_plan()
 
     if poisson:
@@ -236,7 +237,13 @@ def main(argv=None) -> int:
         return 0
 
     # stencil: read the slab once (+2 halo rows), write Ap; dense: SURVEY.md s8(d)
-    bytes_launch = (16 * nloc + 16 * m) if poisson else matvec_bytes(n, nloc)
+    # fused Poisson: the timed kernel is k_poisson_xr_f64 (reads p_k with its two
+    # halo rows, x and r; writes x and r); unfused: the stencil (p -> Ap).
+    # dense: SURVEY.md s8(d)
+    if poisson:
+        bytes_launch = (40 * nloc + 16 * m) if fused else (16 * nloc + 16 * m)
+    else:
+        bytes_launch = matvec_bytes(n, nloc)
     achieved = bytes_launch / (mv_ms * 1e-3) / 1e9
     traffic = None if (stream or poisson) else pmc_traffic(n, world)
     peak = H2D_PEAK_GBS if stream else HBM_PEAK_GBS
@@ -282,12 +289,14 @@ def main(argv=None) -> int:
             "unit": "GB/s",
             "frac": achieved / peak,
             "traffic": traffic,
-            "kernel": "k_stencil5_f64" if poisson else "k_matvec_f64",
+            "kernel": ("k_poisson_xr_f64" if fused else "k_stencil5_f64") if poisson else "k_matvec_f64",
             "plan": plan,
             "algorithmic_bytes_per_launch": bytes_launch,
         },
         "check": {"relres": rnorm / bnorm},
-        "iteration_gbps": (88.0 * n / (elapsed / args.steps) / 1e9) if poisson else None,
+        # algorithmic bytes of a whole iteration: 64 B/point fused (r, p_{k-1} -> p_k;
+        # p_k, x, r -> x, r), 80 B/point for the stencil / r / x,p split
+        "iteration_gbps": ((64.0 if fused else 80.0) * n / (elapsed / args.steps) / 1e9) if poisson else None,
     }
     if world == 1 and not args.no_cpu and poisson:
         out["cpu_baseline"] = cpu_baseline_poisson(m)

@@ -103,6 +103,9 @@ struct Shard {
     char *A = nullptr, *b = nullptr, *x = nullptr, *r = nullptr, *Ap = nullptr, *pfull = nullptr,
          *xfull = nullptr, *scal = nullptr;
     char *pown = nullptr;  // this shard's p: pfull + row0 (dense) or the slab interior (Poisson)
+    // fused Poisson iteration: r with halo rows (r = rh + one row) and a
+    // second p slab; p_k lives in pfull for even k, in p2 for odd k
+    char *rh = nullptr, *p2 = nullptr;
     RedWs ws{nullptr, nullptr};
     double *h_pin = nullptr;
     MatvecPlan plan;
@@ -146,6 +149,7 @@ struct cgx_ctx {
     double solve_ms = 0.0, matvec_ms = 0.0;
     int64_t matvec_count = 0, total_iters = 0;
     bool overlap = false;  // own-column-block matVec while p is exchanged
+    bool fused = false;    // Poisson: two-kernel fused iteration (k_poisson_p + k_poisson_xr)
 };
 
 namespace {
@@ -199,7 +203,15 @@ int alloc_shard(cgx_ctx *c, Shard &s) {
     }
     TRY(dmalloc(&s.b, s.nloc * es));
     TRY(dmalloc(&s.x, s.nloc * es));
-    TRY(dmalloc(&s.r, s.nloc * es));
+    if (c->op == OP_POISSON) {  // r with halo rows (the fused iteration exchanges r, not p)
+        TRY(dmalloc(&s.rh, (s.nloc + 2 * c->m) * es));
+        HIPT(hipMemsetAsync(s.rh, 0, (s.nloc + 2 * c->m) * es, s.stream));
+        s.r = s.rh + c->m * es;
+        TRY(dmalloc(&s.p2, (s.nloc + 2 * c->m) * es));
+        HIPT(hipMemsetAsync(s.p2, 0, (s.nloc + 2 * c->m) * es, s.stream));
+    } else {
+        TRY(dmalloc(&s.r, s.nloc * es));
+    }
     TRY(dmalloc(&s.Ap, s.nloc * es));
     // full-length p (dense) or the slab with one halo row above and below (Poisson)
     const int64_t plen = (c->op == OP_POISSON) ? s.nloc + 2 * c->m : c->lda;
@@ -236,7 +248,7 @@ void free_shard(Shard &s) {
     (void)hipSetDevice(s.dev);
     if (s.stream) (void)hipStreamSynchronize(s.stream);
     if (s.comm) ncclCommDestroy(s.comm);
-    for (char *p : {s.A, s.b, s.x, s.r, s.Ap, s.pfull, s.xfull, s.scal})
+    for (char *p : {s.A, s.b, s.x, s.rh ? s.rh : s.r, s.p2, s.Ap, s.pfull, s.xfull, s.scal})
         if (p) (void)hipFree(p);
     if (s.ws.partials) (void)hipFree(s.ws.partials);
     if (s.ws.tickets) (void)hipFree(s.ws.tickets);
@@ -315,6 +327,10 @@ int alloc_overlap(cgx_ctx *c) {
 
 int finish_create(cgx_ctx *c, cgx_ctx **out) {
     c->overlap = can_overlap(c);
+    if (c->op == OP_POISSON) {  // CGX_POISSON_FUSED=0: the three-kernel split (stencil, r, x/p)
+        const char *e = std::getenv("CGX_POISSON_FUSED");
+        c->fused = !(e && *e == '0') && poisson_fusable(c->sh[0].nloc / c->m, c->m);
+    }
     for (auto &s : c->sh) {
         int rc = alloc_shard(c, s);
         if (rc == CGX_OK && c->overlap && &s == &c->sh.back()) rc = alloc_overlap(c);
@@ -364,13 +380,21 @@ int local_barrier(cgx_ctx *c) {
 // Poisson: refresh the two halo rows of every slab from its neighbours
 // (ncclSend/Recv of one grid row each way in rank mode, device copies in
 // LOCAL mode); from_x first copies x into the slab interior (for A x0).
+int exchange_halo_of(cgx_ctx *c, char *Shard::*slab);
 int exchange_halo(cgx_ctx *c, bool from_x) {
-    const size_t es = (size_t)c->es, row = (size_t)c->m * es;
+    const size_t es = (size_t)c->es;
     if (from_x)
         for (auto &s : c->sh) {
             TRY(set_dev(s));
             HIPT(hipMemcpyAsync(s.pown, s.x, s.nloc * es, hipMemcpyDeviceToDevice, s.stream));
         }
+    return exchange_halo_of(c, &Shard::pfull);
+}
+
+// The halo rows of the slab buffer `slab` (row 0 and row mloc+1 around the
+// mloc interior rows) from the neighbouring slabs' boundary rows.
+int exchange_halo_of(cgx_ctx *c, char *Shard::*slab) {
+    const size_t row = (size_t)c->m * (size_t)c->es;
     if (c->mode == M_SINGLE) return CGX_OK;
     const int64_t mloc = c->sh[0].nloc / c->m;
     if (c->mode == M_RCCL) {
@@ -378,14 +402,15 @@ int exchange_halo(cgx_ctx *c, bool from_x) {
         if (c->nranks == 1) return CGX_OK;
         TRY(set_dev(s));
         const int g = s.index;
+        char *base = s.*slab, *own = base + row;
         NCCLT(ncclGroupStart());
         if (g > 0) {
-            NCCLT(ncclSend(s.pown, (size_t)c->m, ncclDouble, g - 1, s.comm, s.stream));
-            NCCLT(ncclRecv(s.pfull, (size_t)c->m, ncclDouble, g - 1, s.comm, s.stream));
+            NCCLT(ncclSend(own, (size_t)c->m, ncclDouble, g - 1, s.comm, s.stream));
+            NCCLT(ncclRecv(base, (size_t)c->m, ncclDouble, g - 1, s.comm, s.stream));
         }
         if (g < c->nranks - 1) {
-            NCCLT(ncclSend(s.pown + (size_t)(mloc - 1) * row, (size_t)c->m, ncclDouble, g + 1, s.comm, s.stream));
-            NCCLT(ncclRecv(s.pown + (size_t)mloc * row, (size_t)c->m, ncclDouble, g + 1, s.comm, s.stream));
+            NCCLT(ncclSend(own + (size_t)(mloc - 1) * row, (size_t)c->m, ncclDouble, g + 1, s.comm, s.stream));
+            NCCLT(ncclRecv(own + (size_t)mloc * row, (size_t)c->m, ncclDouble, g + 1, s.comm, s.stream));
         }
         NCCLT(ncclGroupEnd());
         return CGX_OK;
@@ -397,11 +422,11 @@ int exchange_halo(cgx_ctx *c, bool from_x) {
         TRY(set_dev(d));
         if (q > 0) {
             const Shard &u = c->sh[q - 1];
-            HIPT(hipMemcpyPeerAsync(d.pfull, d.dev, u.pown + (size_t)(mloc - 1) * row, u.dev, row, d.stream));
+            HIPT(hipMemcpyPeerAsync(d.*slab, d.dev, u.*slab + (size_t)mloc * row, u.dev, row, d.stream));
         }
         if (q < S - 1) {
             const Shard &w = c->sh[q + 1];
-            HIPT(hipMemcpyPeerAsync(d.pown + (size_t)mloc * row, d.dev, w.pown, w.dev, row, d.stream));
+            HIPT(hipMemcpyPeerAsync(d.*slab + (size_t)(mloc + 1) * row, d.dev, w.*slab + row, w.dev, row, d.stream));
         }
     }
     return CGX_OK;
@@ -681,6 +706,7 @@ int do_begin(cgx_ctx *c) {
         }
     }
     TRY(exchange_scalar(c, ls, gs));
+    if (c->fused) TRY(exchange_halo_of(c, &Shard::rh));  // r0's halo rows for k_poisson_p
     for (auto &s : c->sh) {  // device-side convergence record: not converged
         TRY(set_dev(s));
         HIPT(hipMemsetAsync(slot(s, S_KDONE), 0, 16, s.stream));
@@ -753,12 +779,69 @@ int overlapped_matvec(cgx_ctx *c, int dot_slot, bool gated) {
     return CGX_OK;
 }
 
+// Fused Poisson iteration k (conjgrad.m's loop, two kernels, 64 B per grid
+// point; see k_poisson_p_f64 / k_poisson_xr_f64):
+//   p_k = r_k + beta p_{k-1}, p_k . A p_k      (gated: first decides the
+//                                               previous iteration's stop)
+//   allreduce(p.Ap)
+//   x += alpha p_k, r -= alpha A p_k, r.r
+//   allreduce(r.r); host-checked stop; r's halo rows for the next iteration.
+// x is current after every iteration, so a converged solve needs no extra pass.
+int do_iteration_poisson(cgx_ctx *c, double eps, int *stop, bool gated) {
+    const int64_t k = c->k;
+    *stop = 0;
+    const int64_t m = c->m;
+    const int pg = S_PAP + ring(k), pl = S_LPAP + ring(k);
+    const int rk = S_RR + ring(k), rkm1 = S_RR + ring(k + 3);  // r.r of iterations k, k-1
+    auto D = [](void *p) { return reinterpret_cast<double *>(p); };
+    for (auto &s : c->sh) {
+        TRY(set_dev(s));
+        char *pold = (k & 1) ? s.pfull : s.p2, *pnew = (k & 1) ? s.p2 : s.pfull;
+        HIPT(poisson_p_f64(D(s.rh), D(pold), D(pnew), s.nloc / m, m, D(slot(s, rk)), D(slot(s, rkm1)), k == 0,
+                           D(slot(s, out_slot(c, pl, pg))), s.ws, s.stream, gated ? eps : -1.0, k,
+                           gated ? reinterpret_cast<int64_t *>(slot(s, S_KDONE)) : nullptr,
+                           gated ? D(slot(s, S_RRFINAL)) : nullptr));
+    }
+    TRY(exchange_scalar(c, pl, pg));
+    const int rg = S_RR + ring(k + 1), rl = S_LRR + ring(k + 1);
+    const int ro = out_slot(c, rl, rg);
+    for (auto &s : c->sh) {
+        TRY(set_dev(s));
+        const bool timing = (c->flags & CGX_TIMING) && (&s == &c->sh[0]);
+        if (timing && s.ev_used >= kEvPairs) TRY(timing_resolve(c));
+        if (timing) HIPT(hipEventRecord(s.ev_t[2 * s.ev_used], s.stream));
+        char *pnew = (k & 1) ? s.p2 : s.pfull;
+        HIPT(poisson_xr_f64(D(pnew), D(s.x), D(s.r), s.nloc / m, m, D(slot(s, rk)), D(slot(s, pg)), D(slot(s, ro)),
+                            s.ws, s.stream, gate_of(s, gated)));
+        if (timing) {
+            HIPT(hipEventRecord(s.ev_t[2 * s.ev_used + 1], s.stream));
+            s.ev_used++;
+        }
+    }
+    TRY(exchange_scalar(c, rl, rg));
+    c->k = k + 1;
+    c->total_iters += 1;
+    if (!gated && eps >= 0.0) {
+        double rr = 0.0;
+        TRY(read_scalar(c, rg, &rr));
+        c->last_rr = rr;
+        if (std::sqrt(rr) < eps) {
+            c->converged = 1;
+            c->state = ST_CONVERGED;
+            *stop = 1;
+            return CGX_OK;
+        }
+    }
+    return exchange_halo_of(c, &Shard::rh);
+}
+
 // One loop iteration k (serialConjugate.c:215-244 / parallel_cg.c:290-323).
 // Returns 1 in *stop when sqrt(r.r) < eps ended the loop (before the p update,
 // as the reference breaks at :235-238).
 // gated: fp64 device-side convergence (the host does not read r.r here; the
 // update kernel decides sqrt(r.r) < eps and later kernels skip themselves).
 int do_iteration(cgx_ctx *c, double eps, int *stop, bool gated = false) {
+    if (c->fused) return do_iteration_poisson(c, eps, stop, gated);
     const int64_t k = c->k;
     *stop = 0;
     const int pg = S_PAP + ring(k), pl = S_LPAP + ring(k);
@@ -1089,7 +1172,7 @@ int cgx_get_info(const cgx_ctx *c, cgx_info *info) {
     info->row0 = c->sh[0].row0;
     info->nrows = 0;
     for (auto &s : c->sh) info->nrows += s.nloc;
-    info->flags = c->flags | (c->overlap ? CGX_OVERLAP_ACTIVE : 0);
+    info->flags = c->flags | (c->overlap ? CGX_OVERLAP_ACTIVE : 0) | (c->fused ? CGX_FUSED_ACTIVE : 0);
     info->elem_bytes = c->es;
     return CGX_OK;
 }
@@ -1240,6 +1323,13 @@ static int iterate_gated(cgx_ctx *c, int64_t count, double eps, int64_t *done, i
         double rr = 0.0;
         TRY(read_scalar(c, S_RR + ring(c->k), &rr));
         c->last_rr = rr;
+        // The fused Poisson iteration decides a stop one iteration later (at
+        // the start of the next k_poisson_p); the last issued iteration's
+        // r.r is tested here.  (The dense kernels already tested it.)
+        if (c->fused && eps >= 0.0 && std::sqrt(rr) < eps) {
+            c->converged = 1;
+            c->state = ST_CONVERGED;
+        }
     }
     if (done) *done = did;
     if (converged) *converged = c->converged;

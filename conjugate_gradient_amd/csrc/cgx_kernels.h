@@ -74,6 +74,15 @@ hipError_t sum_ordered_f64(const double *in, int cnt, double *out, hipStream_t s
 // row above and below.  *dot_out = ph[m..] . Ap when dot_out != nullptr.
 hipError_t stencil5_f64(const double *ph, int64_t mloc, int64_t m, double *Ap, double *dot_out, const RedWs &ws,
                         hipStream_t s, const int64_t *gate = nullptr);
+// Fused Poisson CG iteration (even m, 16-B-aligned buffers; see the kernels).
+// rh, poh, pnh: r, p_{k-1}, p_k slabs with one halo row above and below.
+bool poisson_fusable(int64_t mloc, int64_t m);
+hipError_t poisson_p_f64(const double *rh, const double *poh, double *pnh, int64_t mloc, int64_t m, const double *rr,
+                         const double *rsold, bool first, double *pap_out, const RedWs &ws, hipStream_t s,
+                         double eps = -1.0, int64_t k = 0, int64_t *kdone = nullptr, double *rrfinal = nullptr);
+hipError_t poisson_xr_f64(const double *pnh, double *x, double *r, int64_t mloc, int64_t m, const double *rsold,
+                          const double *pAp, double *rr_out, const RedWs &ws, hipStream_t s,
+                          const int64_t *gate = nullptr);
 hipError_t fill_f64(double *p, int64_t n, double v, hipStream_t s);
 hipError_t fill_f32(float *p, int64_t n, float v, hipStream_t s);
 
