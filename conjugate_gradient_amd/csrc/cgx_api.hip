@@ -306,10 +306,14 @@ cgx_ctx *new_ctx(int64_t n, int nranks, int flags) {
 // matVec's 128-column chunks.  CGX_OVERLAP=0 disables it.
 bool can_overlap(const cgx_ctx *c) {
     if (c->op != OP_DENSE || f32ref(c) || (c->flags & CGX_HOST_STREAM)) return false;
-    if (c->mode == M_SINGLE || (c->mode == M_RCCL && c->nranks == 1)) return false;
     if (c->flags & (CGX_NO_OVERLAP | CGX_COMM_P2P)) return false;
     const char *e = std::getenv("CGX_OVERLAP");
     if (e && *e == '0') return false;
+    // CGX_OVERLAP=force: also at world size 1 in rank mode (the in-place
+    // allgather on the comm stream and the event hand-offs run with nothing to
+    // exchange), so one GPU can execute the rank-mode overlap path.
+    const bool force = e && std::strcmp(e, "force") == 0;
+    if (c->mode == M_SINGLE || (c->mode == M_RCCL && c->nranks == 1 && !force)) return false;
     for (const auto &s : c->sh)
         if ((s.row0 & 127) || (s.nloc & 127)) return false;
     return true;

@@ -91,15 +91,28 @@ def test_row_block_shards_f64(golden, name, P):
     assert rel(x, xo) <= TOL
 
 
-def test_rccl_rank_mode_world1():
-    """The one-process-per-GPU path (RCCL allgather/allreduce) at world size 1."""
+@pytest.mark.parametrize("mode", ["collective", "overlap", "p2p"])
+def test_rccl_rank_mode_world1(monkeypatch, mode):
+    """The one-process-per-GPU path (RCCL allgather/allreduce) at world size 1:
+    plain collectives; the overlapped exchange forced on (CGX_OVERLAP=force:
+    in-place ncclAllGather on the comm stream, event hand-offs, own-block then
+    remaining-columns matVec with a zero-width second piece); the
+    point-to-point_cg.c pattern (CGX_COMM_P2P)."""
     A, b, x0 = case("spd1024", np.float64)
+    if mode == "overlap":
+        monkeypatch.setenv("CGX_OVERLAP", "force")
+    flags = cg.CGX_F64 | (cg.CGX_COMM_P2P if mode == "p2p" else 0)
     uid = cg.get_unique_id()
-    with cg.Solver(b.size, rank=0, nranks=1, unique_id=uid, device=0) as s:
+    with cg.Solver(b.size, rank=0, nranks=1, unique_id=uid, device=0, flags=flags) as s:
+        assert bool(s.info.flags & cg.CGX_OVERLAP_ACTIVE) == (mode == "overlap")
         s.set_system(A, b, x0)
         x, st = s.solve(None, eps=1e-10)
+        rn, bn = s.residual_norm()
     xo, so = oracle.cg_f64(A, b, x0, eps=1e-10)
     assert st.iterations == so.iterations and rel(x, xo) <= TOL
+    assert rn <= TOL * bn
+    if mode != "collective":
+        return
     with cg.Solver(b.size, rank=0, nranks=1, unique_id=cg.get_unique_id(), flags=cg.CGX_F32_REF) as s:
         A32, b32, x032 = case("spd1024")
         s.set_system(A32, b32, x032)
