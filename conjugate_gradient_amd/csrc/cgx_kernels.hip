@@ -337,6 +337,259 @@ __global__ __launch_bounds__(kNT) void k_matvec_f64_flat(
     if (pown) grid_sum_last_block(dacc, partials, ticket, dot_out);
 }
 
+// Policies 12 / 13: the pipelined matVec with wave-uniform row bases.  The
+// wave id is readfirstlane'd, so a row group's row addresses live in SGPRs;
+// every A and p load is `global_load ... v_off, s[base]` with one 32-bit lane
+// offset kept opaque to loop strength reduction (which otherwise builds a
+// 64-bit per-lane pointer per row).  13 also stages each step's p chunks in a
+// double-buffered LDS tile shared by the block's waves (one barrier a step);
+// every wave of a block then walks the same number of row groups.
+__device__ __forceinline__ d2 ldg_nt(const double *base, uint32_t off) {
+    asm volatile("" : "+v"(off));
+    return __builtin_nontemporal_load(reinterpret_cast<const d2 *>(reinterpret_cast<const char *>(base) + off));
+}
+__device__ __forceinline__ d2 ldg(const double *base, uint32_t off) {
+    asm volatile("" : "+v"(off));
+    return *reinterpret_cast<const d2 *>(reinterpret_cast<const char *>(base) + off);
+}
+
+template <int R, int U, bool LDSP>
+__global__ __launch_bounds__(kNT) void k_matvec_f64_sb(
+    const double *__restrict__ A, int64_t lda, int64_t rows, int64_t cols, int64_t vec_cols, int64_t cfirst,
+    int64_t ccount, int tail, int accumulate, const double *__restrict__ v, double *__restrict__ out,
+    const double *__restrict__ pown, double *dot_out, double *partials, unsigned *ticket, const int64_t *gate) {
+    constexpr int W = kNT / 64, UW = LDSP ? U / W : 1;
+    static_assert(!LDSP || U % W == 0, "U chunks shared by the block's waves");
+    __shared__ d2 sp[LDSP ? 2 : 1][LDSP ? U : 1][64];
+    if (gate && *gate) return;
+    const int lane = threadIdx.x & 63;
+    const uint32_t loff = (uint32_t)lane * 16;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t ngroups = (rows + R - 1) / R;
+    const int64_t nchunk = vec_cols >> 7;
+    const int64_t ctail = nchunk << 7;
+    const int64_t ca = cfirst, cb = (cfirst + ccount < nchunk) ? cfirst + ccount : nchunk;
+    const int64_t piece1 = cb - ca;
+    const int64_t S = (piece1 + (cfirst + ccount - cb)) / U;  // whole steps (host guarantees no remainder)
+    auto col_of = [&](int64_t s) -> int64_t {
+        const int64_t o = s * U;
+        return o < piece1 ? ca + o : o - piece1;
+    };
+    double dacc = 0.0;
+    // LDSP: block-uniform loop (all waves take part in every barrier)
+    const int64_t gstep = (int64_t)gridDim.x * W;
+    for (int64_t gb = (int64_t)blockIdx.x * W + (LDSP ? 0 : wid); LDSP ? gb < ngroups : gb < ngroups; gb += gstep) {
+        const int64_t g = LDSP ? gb + wid : gb;
+        const bool live = g < ngroups;
+        const int64_t r0 = (live ? g : ngroups - 1) * R;
+        const double *rb[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) rb[r] = A + ((r0 + r < rows) ? r0 + r : rows - 1) * lda;
+        d2 acc[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[r] = (d2)(0.0);
+        if (S > 0) {
+            d2 aa[R][U], ab[R][U], pa[LDSP ? 1 : U], pb[LDSP ? 1 : U], pt[UW];
+            int buf = 0;
+            auto load_step = [&](int64_t c, d2 (&av)[R][U], d2 (&pv)[LDSP ? 1 : U]) {
+                if constexpr (LDSP) {
+#pragma unroll
+                    for (int q = 0; q < UW; ++q) pt[q] = ldg(v + (c + wid * UW + q) * 128, loff);
+                } else {
+#pragma unroll
+                    for (int u = 0; u < U; ++u) pv[u] = ldg(v + (c + u) * 128, loff);
+                }
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+#pragma unroll
+                    for (int u = 0; u < U; ++u) av[r][u] = ldg_nt(rb[r] + (c + u) * 128, loff);
+            };
+            auto fma_step = [&](const d2 (&av)[R][U], const d2 (&pv)[LDSP ? 1 : U]) {
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    d2 p;
+                    if constexpr (LDSP) p = sp[buf][u][lane];
+                    else p = pv[u];
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        acc[r].x = __builtin_fma(av[r][u].x, p.x, acc[r].x);
+                        acc[r].y = __builtin_fma(av[r][u].y, p.y, acc[r].y);
+                    }
+                }
+            };
+            load_step(col_of(0), aa, pa);
+            if constexpr (LDSP) {
+#pragma unroll
+                for (int q = 0; q < UW; ++q) sp[0][wid * UW + q][lane] = pt[q];
+                __syncthreads();
+            }
+            for (int64_t s = 0;;) {
+                // set A in flight: issue B (step s+1), consume A
+                bool more = s + 1 < S;
+                if (more) load_step(col_of(s + 1), ab, pb);
+                fma_step(aa, pa);
+                if constexpr (LDSP) {
+                    if (more) {
+#pragma unroll
+                        for (int q = 0; q < UW; ++q) sp[buf ^ 1][wid * UW + q][lane] = pt[q];
+                    }
+                    __syncthreads();
+                    buf ^= 1;
+                }
+                if (!more) break;
+                ++s;
+                // set B in flight: issue A (step s+1), consume B
+                more = s + 1 < S;
+                if (more) load_step(col_of(s + 1), aa, pa);
+                fma_step(ab, pb);
+                if constexpr (LDSP) {
+                    if (more) {
+#pragma unroll
+                        for (int q = 0; q < UW; ++q) sp[buf ^ 1][wid * UW + q][lane] = pt[q];
+                    }
+                    __syncthreads();
+                    buf ^= 1;
+                }
+                if (!more) break;
+                ++s;
+            }
+        }
+        if (tail)
+            for (int64_t j = ctail + lane; j < cols; j += 64) {
+                const double vj = v[j];
+#pragma unroll
+                for (int r = 0; r < R; ++r) acc[r].x = __builtin_fma(rb[r][j], vj, acc[r].x);
+            }
+        double mine = 0.0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const double sr = wave_sum(acc[r].x + acc[r].y);
+            if (lane == r) mine = sr;
+        }
+        if (live && lane < R && r0 + lane < rows) {
+            if (accumulate) mine = out[r0 + lane] + mine;
+            out[r0 + lane] = mine;
+            if (pown) dacc += pown[r0 + lane] * mine;
+        }
+    }
+    if (pown) grid_sum_last_block(dacc, partials, ticket, dot_out);
+}
+
+// LDS-staged p (policy 11; the north star's "LDS staging of the p-vector
+// tile"): per step the block's 4 waves load the step's U p chunks once
+// (U/4 chunks each) into a double-buffered LDS tile, one barrier, and every
+// wave reads its p from LDS, so p costs one global load per block per chunk
+// instead of one per wave.  A is software-pipelined as in policy 8 (the next
+// step's A loads are issued before this step's FMAs).  All waves of a block
+// walk the same number of row groups (waves past the last group keep loading
+// and synchronising but store nothing).  Both column pieces must be whole
+// steps of U chunks (the host falls back to policy 8 otherwise).
+template <int R, int U>
+__global__ __launch_bounds__(kNT) void k_matvec_f64_lds(
+    const double *__restrict__ A, int64_t lda, int64_t rows, int64_t cols, int64_t vec_cols, int64_t cfirst,
+    int64_t ccount, int tail, int accumulate, const double *__restrict__ v, double *__restrict__ out,
+    const double *__restrict__ pown, double *dot_out, double *partials, unsigned *ticket, const int64_t *gate) {
+    static_assert(U % (kNT / 64) == 0, "U chunks shared by the block's waves");
+    constexpr int W = kNT / 64, UW = U / W;
+    __shared__ d2 sp[2][U][64];
+    if (gate && *gate) return;
+    const int lane = threadIdx.x & 63;
+    const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    const int64_t ngroups = (rows + R - 1) / R;
+    const int64_t nchunk = vec_cols >> 7;
+    const int64_t ctail = nchunk << 7;
+    const int64_t ca = cfirst, cb = (cfirst + ccount < nchunk) ? cfirst + ccount : nchunk;
+    const int64_t piece1 = cb - ca;
+    const int64_t S = (piece1 + (cfirst + ccount - cb)) / U;
+    const d2 *v2 = reinterpret_cast<const d2 *>(v) + lane;
+    auto col_of = [&](int64_t s) -> int64_t {
+        const int64_t o = s * U;
+        return o < piece1 ? ca + o : o - piece1;
+    };
+    double dacc = 0.0;
+    for (int64_t gb = (int64_t)blockIdx.x * W; gb < ngroups; gb += (int64_t)gridDim.x * W) {
+        const int64_t g = gb + wid;
+        const bool live = g < ngroups;
+        const int64_t r0 = (live ? g : ngroups - 1) * R;
+        const d2 *arow[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const int64_t row = (r0 + r < rows) ? r0 + r : rows - 1;
+            arow[r] = reinterpret_cast<const d2 *>(A + row * lda) + lane;
+        }
+        d2 acc[R];
+#pragma unroll
+        for (int r = 0; r < R; ++r) acc[r] = (d2)(0.0);
+        if (S > 0) {
+            d2 aa[R][U], ab[R][U], pt[UW];
+            int buf = 0;
+            // prologue: A and this wave's share of p for step 0
+            {
+                const int64_t c = col_of(0);
+#pragma unroll
+                for (int r = 0; r < R; ++r)
+#pragma unroll
+                    for (int u = 0; u < U; ++u) aa[r][u] = load_a<1>(arow[r] + (c + u) * 64);
+#pragma unroll
+                for (int q = 0; q < UW; ++q) sp[0][wid * UW + q][lane] = v2[(c + wid * UW + q) * 64];
+            }
+            __syncthreads();
+            for (int64_t s = 0; s < S; ++s) {
+                const bool more = s + 1 < S;
+                if (more) {  // next step: A into the other register set, p share into registers
+                    const int64_t c = col_of(s + 1);
+#pragma unroll
+                    for (int r = 0; r < R; ++r)
+#pragma unroll
+                        for (int u = 0; u < U; ++u) ab[r][u] = load_a<1>(arow[r] + (c + u) * 64);
+#pragma unroll
+                    for (int q = 0; q < UW; ++q) pt[q] = v2[(c + wid * UW + q) * 64];
+                }
+#pragma unroll
+                for (int u = 0; u < U; ++u) {
+                    const d2 pv = sp[buf][u][lane];
+#pragma unroll
+                    for (int r = 0; r < R; ++r) {
+                        acc[r].x = __builtin_fma(aa[r][u].x, pv.x, acc[r].x);
+                        acc[r].y = __builtin_fma(aa[r][u].y, pv.y, acc[r].y);
+                    }
+                }
+                if (more) {
+#pragma unroll
+                    for (int q = 0; q < UW; ++q) sp[buf ^ 1][wid * UW + q][lane] = pt[q];
+#pragma unroll
+                    for (int r = 0; r < R; ++r)
+#pragma unroll
+                        for (int u = 0; u < U; ++u) aa[r][u] = ab[r][u];
+                }
+                __syncthreads();
+                buf ^= 1;
+            }
+        }
+        if (tail)
+            for (int64_t j = ctail + lane; j < cols; j += 64) {
+                const double vj = v[j];
+#pragma unroll
+                for (int r = 0; r < R; ++r) {
+                    const int64_t row = (r0 + r < rows) ? r0 + r : rows - 1;
+                    acc[r].x = __builtin_fma(A[row * lda + j], vj, acc[r].x);
+                }
+            }
+        double mine = 0.0;
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            const double sr = wave_sum(acc[r].x + acc[r].y);
+            if (lane == r) mine = sr;
+        }
+        if (live && lane < R && r0 + lane < rows) {
+            if (accumulate) mine = out[r0 + lane] + mine;
+            out[r0 + lane] = mine;
+            if (pown) dacc += pown[r0 + lane] * mine;
+        }
+    }
+    if (pown) grid_sum_last_block(dacc, partials, ticket, dot_out);
+}
+
 template <int R, int U, int NT, bool PIPE = false>
 __global__ __launch_bounds__(kNT) void k_matvec_f64(
     const double *__restrict__ A, int64_t lda, int64_t rows, int64_t cols, int64_t vec_cols, int64_t cfirst,
@@ -1244,6 +1497,9 @@ MvFn pick_nt(int nt) {
         case 8: return k_matvec_f64<R, U, 1, true>;  // pipelined, global nt
         case 9: return k_matvec_f64_flat<R, U, 1>;    // flattened pipeline, global nt
         case 10: return k_matvec_f64_flat<R, U, 2>;   // flattened pipeline, buffer nt
+        case 11: return k_matvec_f64_lds<R, U>;       // LDS-staged p, pipelined A
+        case 12: return k_matvec_f64_sb<R, U, false>;  // pipelined, SGPR row bases
+        case 13: return k_matvec_f64_sb<R, U, true>;   // + LDS-staged p
         default: return k_matvec_f64<R, U, 1>;
     }
 }
@@ -1265,7 +1521,7 @@ int mv_policy(const MatvecPlan &pl, int64_t nchunk, int64_t cfirst, int64_t ccou
     if (pl.nt < 9) return pl.nt;
     const int64_t cb = std::min(cfirst + ccount, nchunk);
     const int64_t p1 = cb - cfirst, p2 = cfirst + ccount - cb;
-    if (p1 % pl.U || p2 % pl.U) return pl.nt == 9 ? 8 : 7;
+    if (p1 % pl.U || p2 % pl.U) return pl.nt == 10 ? 7 : 8;  // 9, 11-13 need whole steps
     return pl.nt;
 }
 MvFn pick_mv(int R, int U, int nt) {
@@ -1301,7 +1557,7 @@ MatvecPlan plan_matvec_f64(int device, int64_t rows, int R, int U, int nt, int b
     if (nt >= 0) pl.nt = nt;
     if (pl.R != 1 && pl.R != 2 && pl.R != 4 && pl.R != 8) pl.R = 4;
     if (pl.U != 2 && pl.U != 4 && pl.U != 8) pl.U = 4;
-    if (pl.nt < 0 || pl.nt > 10) pl.nt = 1;
+    if (pl.nt < 0 || pl.nt > 13) pl.nt = 1;
     if (pl.U == 2 && pl.nt >= 2) pl.nt = 1;  // buffer variants exist for U = 4, 8
     int per_cu = 0;
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, reinterpret_cast<const void *>(pick_mv(pl.R, pl.U, pl.nt)),

@@ -185,7 +185,8 @@ void *cgx_stream(cgx_ctx *ctx);
  * chunks in flight per row (2,4,8), the A load policy (0 plain, 1 non-temporal
  * global loads, 2..6 buffer loads with cache bits nt / nt sc1 / sc0 nt sc1 /
  * sc1 / none, 7 software-pipelined buffer nt, 8 software-pipelined global nt
- * = default, 9 / 10 flattened pipeline global / buffer nt; 2..10 need chunks
+ * = default, 9 / 10 flattened pipeline global / buffer nt, 11 LDS-staged p,
+ * 12 SGPR row bases, 13 SGPR row bases + LDS-staged p; 2..13 need chunks
  * 4 or 8), resident
  * blocks per CU for the grid (<= 0: occupancy query).  Results do not depend
  * on the plan's R/U/nt; the p.Ap partial order depends on the grid size. */

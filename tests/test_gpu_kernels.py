@@ -109,7 +109,7 @@ def test_dot_and_updates_f64(n):
     assert abs(rr_d.to_host()[0] - r_ref @ r_ref) <= F64_TOL * (r_ref @ r_ref)
 
 
-MV_PLANS = [(R, U, nt) for R in (1, 2, 4, 8) for U in (4, 8) for nt in (0, 1, 2, 7, 8, 9, 10)
+MV_PLANS = [(R, U, nt) for R in (1, 2, 4, 8) for U in (4, 8) for nt in (0, 1, 2, 7, 8, 9, 10, 11, 12, 13)
             if not (R == 8 and U == 8 and nt >= 7)] + [(R, 2, nt) for R in (1, 4) for nt in (0, 1)]
 
 
