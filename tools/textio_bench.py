@@ -7,7 +7,9 @@ The reference function is called from the unmodified serialConjugate.c object
 through oracle/_ref/serial_ref --initialize (this container only: the
 reference does not travel).  Values must agree bit for bit (float).
 
-  python tools/textio_bench.py [--n 8192] [--threads 1,4,8] [--out profiles/r01_textio_n8192.json]
+  python tools/textio_bench.py [--n 8192] [--threads 1,4,8] [--reps 3] [--out profiles/r01_textio_n8192.json]
+
+Each thread count is timed --reps times after one warm-up read (median reported).
 """
 import argparse
 import json
@@ -30,6 +32,7 @@ def main():
     ap.add_argument("--n", type=int, default=8192)
     ap.add_argument("--threads", default="1,4,8")
     ap.add_argument("--out", default=None)
+    ap.add_argument("--reps", type=int, default=3, help="runs per thread count (the median is reported)")
     args = ap.parse_args()
     n = args.n
     exe = oracle.ref_binary()
@@ -45,12 +48,17 @@ def main():
         size = os.path.getsize(path)
         res = {"n": n, "file_bytes": size, "values": n * n, "write_s": t_write, "host_cpus": os.cpu_count()}
         ours = {}
+        cg.read_text(path, n * n, np.float32, threads=1)  # warm the page cache and the mapping path
         for t in map(int, args.threads.split(",")):
-            t0 = time.perf_counter()
-            v = cg.read_text(path, n * n, np.float32, threads=t)
-            dt = time.perf_counter() - t0
+            times = []
+            for _ in range(args.reps):
+                t0 = time.perf_counter()
+                v = cg.read_text(path, n * n, np.float32, threads=t)
+                times.append(time.perf_counter() - t0)
+            dt = sorted(times)[len(times) // 2]
             ours[t] = v
             res[f"cgx_text_read_t{t}_s"] = dt
+            res[f"cgx_text_read_t{t}_s_all"] = times
             res[f"cgx_text_read_t{t}_MBps"] = size / dt / 1e6
         for t in ours:
             assert np.array_equal(ours[t], next(iter(ours.values())))
