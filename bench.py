@@ -38,6 +38,10 @@ import platform
 import sys
 import time
 
+# before torch (and its libgomp) loads: the oracle's OpenMP loops in the CPU
+# legs need passive waiting to scale (see oracle/__init__.py)
+os.environ.setdefault("OMP_WAIT_POLICY", "PASSIVE")
+
 ROOT = os.path.dirname(os.path.abspath(__file__))
 sys.path.insert(0, ROOT)
 
@@ -132,6 +136,27 @@ def cpu_baseline(n: int, iters: int = 5, threads_gen: int = 16) -> dict:
                    f"initial residual matVec excluded; loop {st.t_loop_s:.2f} s, init {st.t_init_s:.2f} s; "
                    f"host CPU: {cpu}, {os.cpu_count()} logical CPUs visible"),
         "matvec_gbps_est": iters * 4.0 * n * n / st.t_loop_s / 1e9,
+    }
+
+
+def cpu_baseline_mt(n: int, iters: int = 3, threads: int = 16) -> dict:
+    """SURVEY.md s8(d)'s optional non-reference leg: the fp64 oracle (conjgrad.m
+    order, row-parallel matVec) on `threads` host cores, same system."""
+    import numpy as np
+
+    import oracle
+    oracle.set_threads(threads)
+    A, b = oracle.spd_hash(n, seed=SEED, dtype=np.float64)
+    _, st = oracle.cg_f64(A, b, np.zeros(n), max_iter=iters, eps=-1.0)
+    del A
+    return {
+        "value": iters / st.t_loop_s,
+        "unit": "iterations/s",
+        "cores": threads,
+        "kind": "port",
+        "sample": (f"{iters} CG iterations of the same N={n} system in fp64 (oracle_cg_f64, matVec rows split over "
+                   f"{threads} threads; not the reference's algorithm order), loop {st.t_loop_s:.2f} s"),
+        "matvec_gbps_est": iters * 8.0 * n * n / st.t_loop_s / 1e9,
     }
 
 
@@ -302,6 +327,7 @@ def main(argv=None) -> int:
         out["cpu_baseline"] = cpu_baseline_poisson(m)
     elif world == 1 and not args.no_cpu and not stream:
         out["cpu_baseline"] = cpu_baseline(args.cpu_n or n)
+        out["cpu_baseline_mt"] = cpu_baseline_mt(args.cpu_n or n)
     print(json.dumps(out), flush=True)
     if dist:
         dist.barrier()

@@ -16,6 +16,12 @@ import ctypes
 import os
 import subprocess
 
+# liboracle's OpenMP loops (generator, fp64 matVec): with the default active
+# wait policy, idle team threads spin and the matVec ran SLOWER on 8 threads
+# than on 1 in this container (2.3 vs 5.3 GB/s); passive waiting scales
+# (43.7 GB/s on 8).  Read by libgomp when it is first loaded.
+os.environ.setdefault("OMP_WAIT_POLICY", "PASSIVE")
+
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
