@@ -1132,7 +1132,7 @@ __device__ __forceinline__ double pns(const double *rrow, const double *prow, in
 }
 
 // RBn output rows starting at interior row i: pm, pc carry p_k rows h = i, i+1.
-template <int RBn, bool NT, bool FIRST>
+template <int RBn, bool NT, bool FIRST, bool HT>
 __device__ __forceinline__ void poisson_p_step(const double *__restrict__ rh, const double *__restrict__ poh,
                                                double *__restrict__ pnh, int64_t mloc, int64_t m, int64_t i,
                                                const StripLane &L, double beta, d2 &pm, d2 &pc, double &acc,
@@ -1143,7 +1143,10 @@ __device__ __forceinline__ void poisson_p_step(const double *__restrict__ rh, co
 #pragma unroll
     for (int t = 0; t < RBn; ++t) {
         const int64_t hc = (i + t + 1) * m;  // centre row (halo coordinates) of output row i+t
-        pr[t] = pnv<NT, FIRST>(rh + hc + m, poh + hc + m, L, beta);
+        // HT: the last two rows are the next item's first two (its halo):
+        // default-policy loads keep them in L2 for the block that reads them next
+        pr[t] = (HT && t >= RBn - 2) ? pnv<false, FIRST>(rh + hc + m, poh + hc + m, L, beta)
+                                     : pnv<NT, FIRST>(rh + hc + m, poh + hc + m, L, beta);
         el[t] = L.has_l ? pns<FIRST>(rh + hc, poh + hc, L.jw - 1, beta) : 0.0;
         er[t] = L.has_r ? pns<FIRST>(rh + hc, poh + hc, L.jw + 128, beta) : 0.0;
     }
@@ -1178,7 +1181,7 @@ __device__ __forceinline__ void poisson_p_step(const double *__restrict__ rh, co
     }
 }
 
-template <int RB, bool NT, bool FIRST>
+template <int RB, bool NT, bool FIRST, bool HT>
 __device__ __forceinline__ double poisson_p_body(const double *__restrict__ rh, const double *__restrict__ poh,
                                                  double *__restrict__ pnh, int64_t mloc, int64_t m, int64_t nstrips,
                                                  int64_t rpi, int64_t nitems, double beta, double *edge) {
@@ -1188,21 +1191,21 @@ __device__ __forceinline__ double poisson_p_body(const double *__restrict__ rh, 
         const StripLane L = strip_lane(w, nstrips, m);
         const int64_t i0 = (w / nstrips) * rpi;
         const int64_t i1 = (i0 + rpi < mloc) ? i0 + rpi : mloc;
-        d2 pm = pnv<NT, FIRST>(rh + i0 * m, poh + i0 * m, L, beta);
-        d2 pc = pnv<NT, FIRST>(rh + (i0 + 1) * m, poh + (i0 + 1) * m, L, beta);
+        d2 pm = pnv<NT && !HT, FIRST>(rh + i0 * m, poh + i0 * m, L, beta);
+        d2 pc = pnv<NT && !HT, FIRST>(rh + (i0 + 1) * m, poh + (i0 + 1) * m, L, beta);
         if (L.valid && i0 == 0) sts2<NT>(pnh, L.off, pm);  // top halo row of p_k
         int64_t i = i0;
         for (; i + RB <= i1; i += RB, par ^= 1)
-            poisson_p_step<RB, NT, FIRST>(rh, poh, pnh, mloc, m, i, L, beta, pm, pc, acc,
+            poisson_p_step<RB, NT, FIRST, HT>(rh, poh, pnh, mloc, m, i, L, beta, pm, pc, acc,
                                           edge + par * (kWaves * 2 * kEdgeRB));
         for (; i < i1; ++i, par ^= 1)
-            poisson_p_step<1, NT, FIRST>(rh, poh, pnh, mloc, m, i, L, beta, pm, pc, acc,
+            poisson_p_step<1, NT, FIRST, HT>(rh, poh, pnh, mloc, m, i, L, beta, pm, pc, acc,
                                          edge + par * (kWaves * 2 * kEdgeRB));
     }
     return acc;
 }
 
-template <int RB, bool NT>
+template <int RB, bool NT, bool HT>
 __global__ __launch_bounds__(kNT) void k_poisson_p_f64(const double *__restrict__ rh, const double *__restrict__ poh,
                                                        double *__restrict__ pnh, int64_t mloc, int64_t m,
                                                        int64_t nstrips, int64_t rpi, int64_t nitems, const double *rr,
@@ -1221,16 +1224,16 @@ __global__ __launch_bounds__(kNT) void k_poisson_p_f64(const double *__restrict_
         }
     }
     // p_0 = r_0 (first) has its own instantiation: no p_{k-1} loads
-    const double acc = first ? poisson_p_body<RB, NT, true>(rh, poh, pnh, mloc, m, nstrips, rpi, nitems, 0.0, edge)
-                             : poisson_p_body<RB, NT, false>(rh, poh, pnh, mloc, m, nstrips, rpi, nitems,
-                                                             *rr / *rsold, edge);
+    const double acc = first ? poisson_p_body<RB, NT, true, HT>(rh, poh, pnh, mloc, m, nstrips, rpi, nitems, 0.0, edge)
+                             : poisson_p_body<RB, NT, false, HT>(rh, poh, pnh, mloc, m, nstrips, rpi, nitems,
+                                                                 *rr / *rsold, edge);
     grid_sum_last_block(acc, partials, ticket, dot_out);
 }
 
 // k_poisson_xr_f64 (iteration k): alpha = *rsold / *pAp; x += alpha p_k and
 // r -= alpha A p_k with A p_k recomputed from p_k (halo included);
 // *rr_out = r.r.  Skipped once *gate != 0.
-template <int RBn, bool NT>
+template <int RBn, bool NT, bool HT>
 __device__ __forceinline__ void poisson_xr_step(const double *__restrict__ pnh, double *__restrict__ x,
                                                 double *__restrict__ r, int64_t m, int64_t i, const StripLane &L,
                                                 double alpha, d2 &pm, d2 &pc, double &acc, double *eb) {
@@ -1240,7 +1243,7 @@ __device__ __forceinline__ void poisson_xr_step(const double *__restrict__ pnh, 
 #pragma unroll
     for (int t = 0; t < RBn; ++t) {
         const int64_t hc = (i + t + 1) * m, ic = (i + t) * m;
-        pr[t] = keep(L.valid, lds2<NT>(pnh + hc + m, L.off));
+        pr[t] = keep(L.valid, (HT && t >= RBn - 2) ? lds2<false>(pnh + hc + m, L.off) : lds2<NT>(pnh + hc + m, L.off));
         xv[t] = lds2<NT>(x + ic, L.off);
         rv[t] = lds2<NT>(r + ic, L.off);
         el[t] = L.has_l ? pnh[hc + L.jw - 1] : 0.0;
@@ -1282,7 +1285,7 @@ __device__ __forceinline__ void poisson_xr_step(const double *__restrict__ pnh, 
     }
 }
 
-template <int RB, bool NT>
+template <int RB, bool NT, bool HT>
 __global__ __launch_bounds__(kNT) void k_poisson_xr_f64(const double *__restrict__ pnh, double *__restrict__ x,
                                                         double *__restrict__ r, int64_t mloc, int64_t m,
                                                         int64_t nstrips, int64_t rpi, int64_t nitems,
@@ -1298,13 +1301,13 @@ __global__ __launch_bounds__(kNT) void k_poisson_xr_f64(const double *__restrict
         const StripLane L = strip_lane(w, nstrips, m);
         const int64_t i0 = (w / nstrips) * rpi;
         const int64_t i1 = (i0 + rpi < mloc) ? i0 + rpi : mloc;
-        d2 pm = keep(L.valid, lds2<NT>(pnh + i0 * m, L.off));
-        d2 pc = keep(L.valid, lds2<NT>(pnh + (i0 + 1) * m, L.off));
+        d2 pm = keep(L.valid, lds2<NT && !HT>(pnh + i0 * m, L.off));
+        d2 pc = keep(L.valid, lds2<NT && !HT>(pnh + (i0 + 1) * m, L.off));
         int64_t i = i0;
         for (; i + RB <= i1; i += RB, par ^= 1)
-            poisson_xr_step<RB, NT>(pnh, x, r, m, i, L, alpha, pm, pc, acc, edge + par * (kWaves * 2 * kEdgeRB));
+            poisson_xr_step<RB, NT, HT>(pnh, x, r, m, i, L, alpha, pm, pc, acc, edge + par * (kWaves * 2 * kEdgeRB));
         for (; i < i1; ++i, par ^= 1)
-            poisson_xr_step<1, NT>(pnh, x, r, m, i, L, alpha, pm, pc, acc, edge + par * (kWaves * 2 * kEdgeRB));
+            poisson_xr_step<1, NT, HT>(pnh, x, r, m, i, L, alpha, pm, pc, acc, edge + par * (kWaves * 2 * kEdgeRB));
     }
     grid_sum_last_block(acc, partials, ticket, rr_out);
 }
@@ -1707,13 +1710,14 @@ hipError_t stencil5_f64(const double *ph, int64_t mloc, int64_t m, double *Ap, d
 // short items keep the rows in flight in a narrow band (64- and 128-row items
 // are 7-20 % slower).
 struct PoissonPlan {
-    int rb, nt;
+    int rb, nt, ht;
     int64_t nstrips, rpi, nitems, grid;
 };
 static PoissonPlan poisson_plan(int64_t mloc, int64_t m) {
     PoissonPlan p;
     p.rb = env_int("CGX_STENCIL_RB", 8);
     p.nt = env_int("CGX_STENCIL_NT", 1);
+    p.ht = env_int("CGX_STENCIL_HALO_T", 1);
     p.nstrips = (m + 2 * kNT - 1) / (2 * kNT);
     p.rpi = std::max(1, env_int("CGX_STENCIL_ROWS", 8));
     p.nitems = p.nstrips * ((mloc + p.rpi - 1) / p.rpi);
@@ -1749,7 +1753,8 @@ template <int RB>
 static void launch_poisson_p(const PoissonPlan &pl, hipStream_t s, const double *rh, const double *poh, double *pnh,
                              int64_t mloc, int64_t m, const double *rr, const double *rsold, int first, ConvArgs cv,
                              double *pap_out, const RedWs &ws) {
-    auto fn = pl.nt ? k_poisson_p_f64<RB, true> : k_poisson_p_f64<RB, false>;
+    auto fn = pl.nt ? (pl.ht ? k_poisson_p_f64<RB, true, true> : k_poisson_p_f64<RB, true, false>)
+                    : k_poisson_p_f64<RB, false, false>;
     const int64_t grid = resident_grid(reinterpret_cast<const void *>(fn), pl.nitems);
     hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(kNT), 0, s, rh, poh, pnh, mloc, m, pl.nstrips, pl.rpi,
                        pl.nitems, rr, rsold, first, cv, pap_out, ws.partials, ws.tickets + T_MATVEC);
@@ -1758,7 +1763,8 @@ template <int RB>
 static void launch_poisson_xr(const PoissonPlan &pl, hipStream_t s, const double *pnh, double *x, double *r,
                               int64_t mloc, int64_t m, const double *rsold, const double *pAp, double *rr_out,
                               const RedWs &ws, const int64_t *gate) {
-    auto fn = pl.nt ? k_poisson_xr_f64<RB, true> : k_poisson_xr_f64<RB, false>;
+    auto fn = pl.nt ? (pl.ht ? k_poisson_xr_f64<RB, true, true> : k_poisson_xr_f64<RB, true, false>)
+                    : k_poisson_xr_f64<RB, false, false>;
     const int64_t grid = resident_grid(reinterpret_cast<const void *>(fn), pl.nitems);
     hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(kNT), 0, s, pnh, x, r, mloc, m, pl.nstrips, pl.rpi,
                        pl.nitems, rsold, pAp, rr_out, ws.partials, ws.tickets + T_XR, gate);
