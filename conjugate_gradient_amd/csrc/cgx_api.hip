@@ -82,6 +82,7 @@ constexpr int kScalSlots = 136;  // 16 ring slots, up to 112 gathered partials, 
 constexpr int kMaxShards = 32;
 constexpr int S_RR = 0, S_PAP = 4, S_LRR = 8, S_LPAP = 12, S_GATHER = 16;
 constexpr int S_TR = 128, S_TB = 129, S_LTR = 130, S_LTB = 131;  // true-residual check
+constexpr int S_XNZ = 134;  // rank mode: count of ranks whose x0 is not all zeros
 constexpr int S_KDONE = 132, S_RRFINAL = 133;  // device-side convergence: k+1 at the break, r.r there
 constexpr int kLookRing = 8;                    // pinned slots for the host's lagged convergence checks
 inline int ring(int64_t j) { return (int)(j & 3); }
@@ -106,6 +107,7 @@ struct Shard {
     // fused Poisson iteration: r with halo rows (r = rh + one row) and a
     // second p slab; p_k lives in pfull for even k, in p2 for odd k
     char *rh = nullptr, *p2 = nullptr;
+    bool x_zero = true;  // x is known to be all zeros (x0 = 0: the first A x is skipped)
     RedWs ws{nullptr, nullptr};
     double *h_pin = nullptr;
     MatvecPlan plan;
@@ -688,14 +690,44 @@ int launch_matvec(cgx_ctx *c, Shard &s, const char *vec, bool with_dot, int dot_
     return CGX_OK;
 }
 
+// Whether x0 is all zeros on every shard (every rank in rank mode: one
+// int64 allreduce, so all ranks take the same branch of do_begin).
+int x0_is_zero(cgx_ctx *c, bool *zero) {
+    bool local = true;
+    for (auto &s : c->sh) local = local && s.x_zero;
+    if (c->mode != M_RCCL || c->nranks == 1) {
+        *zero = local;
+        return CGX_OK;
+    }
+    Shard &s = c->sh[0];
+    TRY(set_dev(s));
+    int64_t *pin = reinterpret_cast<int64_t *>(s.h_pin);
+    pin[0] = local ? 0 : 1;
+    HIPT(hipMemcpyAsync(slot(s, S_XNZ), pin, 8, hipMemcpyHostToDevice, s.stream));
+    NCCLT(ncclAllReduce(slot(s, S_XNZ), slot(s, S_XNZ), 1, ncclInt64, ncclSum, s.comm, s.stream));
+    HIPT(hipMemcpyAsync(pin, slot(s, S_XNZ), 8, hipMemcpyDeviceToHost, s.stream));
+    HIPT(hipStreamSynchronize(s.stream));
+    *zero = pin[0] == 0;
+    return CGX_OK;
+}
+
 int do_begin(cgx_ctx *c) {
     // r0 = p0 = b - A x0; rr0 = r0.r0   (serialConjugate.c:209-212, parallel_cg.c:283-287)
-    TRY(exchange_allgather(c, /*from_x=*/true));  // full x0 into pfull
+    // With x0 = 0 (the reference's usual initialguess, and the bench's) A x0 is
+    // exactly zero, so the exchange and the matVec are skipped: r0 = b - 0 = b
+    // bit for bit, one matVec fewer per solve.
+    bool zero = false;
+    TRY(x0_is_zero(c, &zero));
+    if (!zero) TRY(exchange_allgather(c, /*from_x=*/true));  // full x0 into pfull
     const int gs = S_RR + ring(0), ls = S_LRR + ring(0);
     const int os = out_slot(c, ls, gs);
     for (auto &s : c->sh) {
         TRY(set_dev(s));
-        TRY(launch_matvec(c, s, s.pfull, false, 0));
+        if (zero)
+            HIPT(hipMemsetAsync(s.Ap, 0, (size_t)s.nloc * c->es, s.stream));
+        else
+            TRY(launch_matvec(c, s, s.pfull, false, 0));
+        s.x_zero = false;  // the iterations update x
         if (f32ref(c)) {
             float *pown = reinterpret_cast<float *>(s.pown);
             HIPT(residual_ref_f32(s.nloc, reinterpret_cast<const float *>(s.b), reinterpret_cast<const float *>(s.Ap),
@@ -1153,6 +1185,7 @@ int cgx_fill(cgx_ctx *c, double b_value, double x_value) {
             HIPT(fill_f64(reinterpret_cast<double *>(s.b), s.nloc, b_value, s.stream));
             HIPT(fill_f64(reinterpret_cast<double *>(s.x), s.nloc, x_value, s.stream));
         }
+        s.x_zero = x_value == 0.0;
     }
     TRY(sync_all(c));
     c->state = ST_IDLE;
@@ -1208,9 +1241,17 @@ int cgx_set_rows(cgx_ctx *c, int64_t row0, int64_t nrows, const void *A_rows, in
         if (b_rows)
             HIPT(hipMemcpyAsync(s.b + (lo - s.row0) * es, static_cast<const char *>(b_rows) + (lo - row0) * es,
                                 (hi - lo) * es, hipMemcpyHostToDevice, s.stream));
-        if (x_rows)
+        if (x_rows) {
             HIPT(hipMemcpyAsync(s.x + (lo - s.row0) * es, static_cast<const char *>(x_rows) + (lo - row0) * es,
                                 (hi - lo) * es, hipMemcpyHostToDevice, s.stream));
+            bool zeros = true;  // +0 / -0 only (A x is then exactly zero)
+            const char *xs = static_cast<const char *>(x_rows) + (lo - row0) * es;
+            for (int64_t i = 0; i < hi - lo && zeros; ++i)
+                zeros = es == 4 ? reinterpret_cast<const float *>(xs)[i] == 0.0f
+                                : reinterpret_cast<const double *>(xs)[i] == 0.0;
+            const bool whole = lo == s.row0 && hi == s.row0 + s.nloc;
+            s.x_zero = whole ? zeros : (s.x_zero && zeros);
+        }
         HIPT(hipStreamSynchronize(s.stream));
     }
     c->state = ST_IDLE;
@@ -1251,6 +1292,7 @@ int cgx_generate_spd(cgx_ctx *c, uint64_t seed) {
                              reinterpret_cast<double *>(s.b), s.stream));
         }
         HIPT(hipMemsetAsync(s.x, 0, s.nloc * c->es, s.stream));
+        s.x_zero = true;
     }
     TRY(sync_all(c));
     c->state = ST_IDLE;

@@ -224,13 +224,39 @@ def test_solve_in_pieces_and_fixed_count():
 
 
 def test_timing_events_count():
+    """CGX_TIMING times every matVec launch.  With x0 = 0 the initial A x0 is
+    skipped (exactly zero); with any other x0 it runs."""
     n = 4096
     with cg.Solver(n, flags=cg.CGX_F64 | cg.CGX_TIMING) as s:
         s.generate_spd(1)
         s.solve(None, eps=-1.0, max_iter=5)
         st = s.stats()
-    assert st.matvec_count == 6  # initial residual + 5 iterations
-    assert st.matvec_ms > 0
+        assert st.matvec_count == 5  # x0 = 0: 5 iterations, no initial matVec
+        assert st.matvec_ms > 0
+        s.reset_timing()
+        s.solve(np.full(n, 0.5), eps=-1.0, max_iter=5)
+        assert s.stats().matvec_count == 6  # initial residual + 5 iterations
+
+
+@pytest.mark.parametrize("shards", [None, [0, 0]])
+def test_zero_x0_skips_initial_matvec_same_result(shards):
+    """Skipping A x0 for x0 = 0 changes nothing: the same x, bit for bit, as a
+    solve from x0 = [0, ..., 0, 0] with the last entry first set nonzero and
+    then zeroed (partial set_rows), which keeps the initial matVec."""
+    A, b, x0 = case("spd1024", np.float64)
+    n = b.size
+    res = []
+    for partial in (False, True):
+        with cg.Solver(n, devices=shards, flags=cg.CGX_F64 | cg.CGX_TIMING) as s:
+            s.set_system(A, b, np.full(n, 1.0) if partial else x0)
+            if partial:  # zero x through partial writes: the library cannot know it is all zeros
+                s.set_rows(0, None, None, np.zeros(300))
+                s.set_rows(300, None, None, np.zeros(n - 300))
+            x, st = s.solve(None, eps=1e-10)
+            res.append((x, st.iterations, s.stats().matvec_count))
+    (x1, it1, mv1), (x2, it2, mv2) = res
+    assert it1 == it2 and np.array_equal(x1, x2)
+    assert mv2 == mv1 + 1
 
 
 def test_errors_are_reported():
@@ -255,7 +281,7 @@ def test_host_streamed_matvec(monkeypatch, shards):
     with cg.Solver(n, flags=flags, devices=shards) as s:
         s.set_system(A, b)
         x, st = s.solve(None, eps=1e-10)
-        assert s.stats().matvec_count == st.iterations + 1
+        assert s.stats().matvec_count == st.iterations  # x0 = 0: no initial A x0
     with cg.Solver(n, flags=cg.CGX_F64 | cg.CGX_HOST_STREAM, devices=shards) as s:
         s.generate_spd(seed=5)  # generated tile by tile on the device, kept on the host
         xg, stg = s.solve(None, eps=1e-10)
