@@ -465,6 +465,27 @@ def test_ragged_sizes_and_blocks(n, P):
     assert st32.iterations == sr.iterations and np.array_equal(x32, ref)
 
 
+@pytest.mark.parametrize("n,P,seed", [(777, 3, 1), (1000, 4, 2), (2304, 2, 3)])
+def test_f32ref_bit_exact_many_iterations(n, P, seed):
+    """A harder system than generateSPDmatrix (eigenvalues spread over two
+    decades, so 30-80 iterations instead of 4-5) from a nonzero x0: the
+    F32_REF path must still reproduce the reference's loop bit for bit,
+    iteration after iteration, with the P-part dot order."""
+    rng = np.random.default_rng(seed)
+    Q, _ = np.linalg.qr(rng.standard_normal((n, n)))
+    lam = np.logspace(0, 2, n)
+    A = ((Q * lam) @ Q.T).astype(np.float32)
+    A = (A + A.T) / np.float32(2)
+    b = rng.random(n, dtype=np.float32)
+    x0 = (rng.random(n, dtype=np.float32) - np.float32(0.5))
+    with cg.Solver(n, flags=cg.CGX_F32_REF, devices=[0] * P) as s:
+        s.set_system(A, b, x0)
+        x, st = s.solve(None, eps=1e-4)
+    ref, sr = oracle.cg_f32ref(A, b, x0, eps=1e-4, nparts=P)
+    assert st.iterations == sr.iterations and st.iterations >= 20
+    assert np.array_equal(x.view(np.uint32), ref.view(np.uint32))
+
+
 def test_max_iter_cap_and_nonconvergence():
     """Loop bound k < n (serialConjugate.c:213): a system that cannot meet eps
     stops after exactly n iterations, unconverged."""
