@@ -33,6 +33,7 @@
 #include <cstdio>
 #include <cstdlib>
 #include <cstring>
+#include <initializer_list>
 #include <mutex>
 #include <new>
 #include <string>
@@ -152,6 +153,8 @@ struct cgx_ctx {
     int64_t matvec_count = 0, total_iters = 0;
     bool overlap = false;  // own-column-block matVec while p is exchanged
     bool fused = false;    // Poisson: two-kernel fused iteration (k_poisson_p + k_poisson_xr)
+    bool halo_overlap = false;  // fused Poisson, several slabs: r's halo exchange overlaps k_poisson_p
+    bool halo_pending = false;  // an overlapped r halo exchange is in flight on the comm streams
 };
 
 namespace {
@@ -336,10 +339,14 @@ int finish_create(cgx_ctx *c, cgx_ctx **out) {
     if (c->op == OP_POISSON) {  // CGX_POISSON_FUSED=0: the three-kernel split (stencil, r, x/p)
         const char *e = std::getenv("CGX_POISSON_FUSED");
         c->fused = !(e && *e == '0') && poisson_fusable(c->sh[0].nloc / c->m, c->m);
+        const char *h = std::getenv("CGX_HALO_OVERLAP");
+        const bool force = h && std::strcmp(h, "force") == 0;  // also at world size 1 in rank mode
+        c->halo_overlap = c->fused && !(h && *h == '0') && c->mode != M_SINGLE &&
+                          !(c->mode == M_RCCL && c->nranks == 1 && !force);
     }
     for (auto &s : c->sh) {
         int rc = alloc_shard(c, s);
-        if (rc == CGX_OK && c->overlap && &s == &c->sh.back()) rc = alloc_overlap(c);
+        if (rc == CGX_OK && (c->overlap || c->halo_overlap) && &s == &c->sh.back()) rc = alloc_overlap(c);
         if (rc != CGX_OK) {
             std::string keep = g_err;
             for (auto &t : c->sh) free_shard(t);
@@ -690,6 +697,8 @@ int launch_matvec(cgx_ctx *c, Shard &s, const char *vec, bool with_dot, int dot_
     return CGX_OK;
 }
 
+int settle_halo(cgx_ctx *c);
+
 // Whether x0 is all zeros on every shard (every rank in rank mode: one
 // int64 allreduce, so all ranks take the same branch of do_begin).
 int x0_is_zero(cgx_ctx *c, bool *zero) {
@@ -716,6 +725,7 @@ int do_begin(cgx_ctx *c) {
     // With x0 = 0 (the reference's usual initialguess, and the bench's) A x0 is
     // exactly zero, so the exchange and the matVec are skipped: r0 = b - 0 = b
     // bit for bit, one matVec fewer per solve.
+    TRY(settle_halo(c));
     bool zero = false;
     TRY(x0_is_zero(c, &zero));
     if (!zero) TRY(exchange_allgather(c, /*from_x=*/true));  // full x0 into pfull
@@ -815,6 +825,67 @@ int overlapped_matvec(cgx_ctx *c, int dot_slot, bool gated) {
     return CGX_OK;
 }
 
+// Overlapped r halo exchange (several slabs): on the comm streams, after
+// everything already on the compute streams (the r update and the r.r
+// allreduce, so two RCCL operations never run at once).  The next
+// k_poisson_p runs its interior runs meanwhile and waits for ev_gathered
+// before its two edge runs.
+int exchange_halo_async(cgx_ctx *c) {
+    const size_t row = (size_t)c->m * (size_t)c->es;
+    const int64_t mloc = c->sh[0].nloc / c->m;
+    for (auto &s : c->sh) {
+        TRY(set_dev(s));
+        HIPT(hipEventRecord(s.ev_pready, s.stream));
+    }
+    if (c->mode == M_RCCL) {
+        Shard &s = c->sh[0];
+        const int g = s.index;
+        char *base = s.rh, *own = base + row;
+        HIPT(hipStreamWaitEvent(s.cstream, s.ev_pready, 0));
+        NCCLT(ncclGroupStart());
+        if (g > 0) {
+            NCCLT(ncclSend(own, (size_t)c->m, ncclDouble, g - 1, s.comm, s.cstream));
+            NCCLT(ncclRecv(base, (size_t)c->m, ncclDouble, g - 1, s.comm, s.cstream));
+        }
+        if (g < c->nranks - 1) {
+            NCCLT(ncclSend(own + (size_t)(mloc - 1) * row, (size_t)c->m, ncclDouble, g + 1, s.comm, s.cstream));
+            NCCLT(ncclRecv(own + (size_t)mloc * row, (size_t)c->m, ncclDouble, g + 1, s.comm, s.cstream));
+        }
+        NCCLT(ncclGroupEnd());
+        HIPT(hipEventRecord(s.ev_gathered, s.cstream));
+    } else {
+        const int S = (int)c->sh.size();
+        for (int q = 0; q < S; ++q) {
+            Shard &d = c->sh[q];
+            TRY(set_dev(d));
+            for (auto &s : c->sh) HIPT(hipStreamWaitEvent(d.cstream, s.ev_pready, 0));
+            if (q > 0) {
+                const Shard &u = c->sh[q - 1];
+                HIPT(hipMemcpyPeerAsync(d.rh, d.dev, u.rh + (size_t)mloc * row, u.dev, row, d.cstream));
+            }
+            if (q < S - 1) {
+                const Shard &w = c->sh[q + 1];
+                HIPT(hipMemcpyPeerAsync(d.rh + (size_t)(mloc + 1) * row, d.dev, w.rh + row, w.dev, row, d.cstream));
+            }
+            HIPT(hipEventRecord(d.ev_gathered, d.cstream));
+        }
+    }
+    c->halo_pending = true;
+    return CGX_OK;
+}
+
+// Order every compute stream after an overlapped halo exchange still in
+// flight (before anything else touches r or its halo rows).
+int settle_halo(cgx_ctx *c) {
+    if (!c->halo_pending) return CGX_OK;
+    for (auto &s : c->sh) {
+        TRY(set_dev(s));
+        HIPT(hipStreamWaitEvent(s.stream, s.ev_gathered, 0));
+    }
+    c->halo_pending = false;
+    return CGX_OK;
+}
+
 // Fused Poisson iteration k (conjgrad.m's loop, two kernels, 64 B per grid
 // point; see k_poisson_p_f64 / k_poisson_xr_f64):
 //   p_k = r_k + beta p_{k-1}, p_k . A p_k      (gated: first decides the
@@ -830,14 +901,19 @@ int do_iteration_poisson(cgx_ctx *c, double eps, int *stop, bool gated) {
     const int pg = S_PAP + ring(k), pl = S_LPAP + ring(k);
     const int rk = S_RR + ring(k), rkm1 = S_RR + ring(k + 3);  // r.r of iterations k, k-1
     auto D = [](void *p) { return reinterpret_cast<double *>(p); };
+    const bool split = c->halo_pending;  // interior runs while the r halo exchange is in flight
     for (auto &s : c->sh) {
         TRY(set_dev(s));
         char *pold = (k & 1) ? s.pfull : s.p2, *pnew = (k & 1) ? s.p2 : s.pfull;
-        HIPT(poisson_p_f64(D(s.rh), D(pold), D(pnew), s.nloc / m, m, D(slot(s, rk)), D(slot(s, rkm1)), k == 0,
-                           D(slot(s, out_slot(c, pl, pg))), s.ws, s.stream, gated ? eps : -1.0, k,
-                           gated ? reinterpret_cast<int64_t *>(slot(s, S_KDONE)) : nullptr,
-                           gated ? D(slot(s, S_RRFINAL)) : nullptr));
+        for (int part : split ? std::initializer_list<int>{1, 2} : std::initializer_list<int>{0}) {
+            if (part == 2) HIPT(hipStreamWaitEvent(s.stream, s.ev_gathered, 0));
+            HIPT(poisson_p_f64(D(s.rh), D(pold), D(pnew), s.nloc / m, m, D(slot(s, rk)), D(slot(s, rkm1)), k == 0,
+                               D(slot(s, out_slot(c, pl, pg))), s.ws, s.stream, gated ? eps : -1.0, k,
+                               gated ? reinterpret_cast<int64_t *>(slot(s, S_KDONE)) : nullptr,
+                               gated ? D(slot(s, S_RRFINAL)) : nullptr, part));
+        }
     }
+    c->halo_pending = false;
     TRY(exchange_scalar(c, pl, pg));
     const int rg = S_RR + ring(k + 1), rl = S_LRR + ring(k + 1);
     const int ro = out_slot(c, rl, rg);
@@ -868,7 +944,7 @@ int do_iteration_poisson(cgx_ctx *c, double eps, int *stop, bool gated) {
             return CGX_OK;
         }
     }
-    return exchange_halo_of(c, &Shard::rh);
+    return c->halo_overlap ? exchange_halo_async(c) : exchange_halo_of(c, &Shard::rh);
 }
 
 // One loop iteration k (serialConjugate.c:215-244 / parallel_cg.c:290-323).
@@ -1483,6 +1559,7 @@ int cgx_get_matvec_plan(cgx_ctx *c, int *rows_per_wave, int *chunks_in_flight, i
 int cgx_residual_norm(cgx_ctx *c, double *rnorm, double *bnorm) {
     if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
     // ||b - A x|| with the current x: allgather x, matVec, residual, two dots.
+    TRY(settle_halo(c));
     TRY(exchange_allgather(c, /*from_x=*/true));
     const int tro = out_slot(c, S_LTR, S_TR), tbo = out_slot(c, S_LTB, S_TB);
     for (auto &s : c->sh) {

@@ -79,7 +79,8 @@ hipError_t stencil5_f64(const double *ph, int64_t mloc, int64_t m, double *Ap, d
 bool poisson_fusable(int64_t mloc, int64_t m);
 hipError_t poisson_p_f64(const double *rh, const double *poh, double *pnh, int64_t mloc, int64_t m, const double *rr,
                          const double *rsold, bool first, double *pap_out, const RedWs &ws, hipStream_t s,
-                         double eps = -1.0, int64_t k = 0, int64_t *kdone = nullptr, double *rrfinal = nullptr);
+                         double eps = -1.0, int64_t k = 0, int64_t *kdone = nullptr, double *rrfinal = nullptr,
+                         int part = 0);  // part: 0 all rows; 1 interior runs; 2 the two edge runs (+= part 1's p.Ap)
 hipError_t poisson_xr_f64(const double *pnh, double *x, double *r, int64_t mloc, int64_t m, const double *rsold,
                           const double *pAp, double *rr_out, const RedWs &ws, hipStream_t s,
                           const int64_t *gate = nullptr);

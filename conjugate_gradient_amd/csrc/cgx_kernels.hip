@@ -52,7 +52,7 @@ __device__ __forceinline__ double wave_sum(double v) {
 // acquire fence, so no per-block write-back of the L2's dirty lines (which
 // cost the r-update ~35 % of its time with a buffer_wbl2 per block).
 __device__ __forceinline__ void grid_sum_last_block(double v, double *partials, unsigned *ticket,
-                                                    double *out) {
+                                                    double *out, bool add_to_out = false) {
     __shared__ double red[kNT / 64];
     __shared__ int is_last;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
@@ -90,7 +90,7 @@ __device__ __forceinline__ void grid_sum_last_block(double v, double *partials, 
         double t = red[0];
 #pragma unroll
         for (int w = 1; w < kNT / 64; ++w) t += red[w];
-        *out = t;
+        *out = add_to_out ? *out + t : t;
         __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }
 }
@@ -1181,13 +1181,21 @@ __device__ __forceinline__ void poisson_p_step(const double *__restrict__ rh, co
     }
 }
 
+// Work items [w0, w0+cnt1) then [w2, w2+cnt2) (the whole slab, or, when
+// the r halo exchange overlaps the kernel, the slab's interior runs first
+// and its two edge runs after the exchange).
+struct ItemRanges {
+    int64_t w0, cnt1, w2, cnt2;
+};
+
 template <int RB, bool NT, bool FIRST, bool HT>
 __device__ __forceinline__ double poisson_p_body(const double *__restrict__ rh, const double *__restrict__ poh,
                                                  double *__restrict__ pnh, int64_t mloc, int64_t m, int64_t nstrips,
-                                                 int64_t rpi, int64_t nitems, double beta, double *edge) {
+                                                 int64_t rpi, ItemRanges ir, double beta, double *edge) {
     double acc = 0.0;
     int par = 0;
-    for (int64_t w = blockIdx.x; w < nitems; w += gridDim.x) {
+    for (int64_t v = blockIdx.x; v < ir.cnt1 + ir.cnt2; v += gridDim.x) {
+        const int64_t w = v < ir.cnt1 ? ir.w0 + v : ir.w2 + (v - ir.cnt1);
         const StripLane L = strip_lane(w, nstrips, m);
         const int64_t i0 = (w / nstrips) * rpi;
         const int64_t i1 = (i0 + rpi < mloc) ? i0 + rpi : mloc;
@@ -1208,9 +1216,9 @@ __device__ __forceinline__ double poisson_p_body(const double *__restrict__ rh, 
 template <int RB, bool NT, bool HT>
 __global__ __launch_bounds__(kNT) void k_poisson_p_f64(const double *__restrict__ rh, const double *__restrict__ poh,
                                                        double *__restrict__ pnh, int64_t mloc, int64_t m,
-                                                       int64_t nstrips, int64_t rpi, int64_t nitems, const double *rr,
+                                                       int64_t nstrips, int64_t rpi, ItemRanges ir, const double *rr,
                                                        const double *rsold, int first, ConvArgs cv, double *dot_out,
-                                                       double *partials, unsigned *ticket) {
+                                                       int add_to_out, double *partials, unsigned *ticket) {
     static_assert(RB <= kEdgeRB, "edge buffer");
     __shared__ double edge[2 * kWaves * 2 * kEdgeRB];
     if (cv.kdone) {
@@ -1224,10 +1232,10 @@ __global__ __launch_bounds__(kNT) void k_poisson_p_f64(const double *__restrict_
         }
     }
     // p_0 = r_0 (first) has its own instantiation: no p_{k-1} loads
-    const double acc = first ? poisson_p_body<RB, NT, true, HT>(rh, poh, pnh, mloc, m, nstrips, rpi, nitems, 0.0, edge)
-                             : poisson_p_body<RB, NT, false, HT>(rh, poh, pnh, mloc, m, nstrips, rpi, nitems,
+    const double acc = first ? poisson_p_body<RB, NT, true, HT>(rh, poh, pnh, mloc, m, nstrips, rpi, ir, 0.0, edge)
+                             : poisson_p_body<RB, NT, false, HT>(rh, poh, pnh, mloc, m, nstrips, rpi, ir,
                                                                  *rr / *rsold, edge);
-    grid_sum_last_block(acc, partials, ticket, dot_out);
+    grid_sum_last_block(acc, partials, ticket, dot_out, add_to_out != 0);
 }
 
 // k_poisson_xr_f64 (iteration k): alpha = *rsold / *pAp; x += alpha p_k and
@@ -1752,12 +1760,12 @@ bool poisson_fusable(int64_t mloc, int64_t m) { return mloc > 0 && m > 0 && (m &
 template <int RB>
 static void launch_poisson_p(const PoissonPlan &pl, hipStream_t s, const double *rh, const double *poh, double *pnh,
                              int64_t mloc, int64_t m, const double *rr, const double *rsold, int first, ConvArgs cv,
-                             double *pap_out, const RedWs &ws) {
+                             double *pap_out, const RedWs &ws, ItemRanges ir, int add_to_out) {
     auto fn = pl.nt ? (pl.ht ? k_poisson_p_f64<RB, true, true> : k_poisson_p_f64<RB, true, false>)
                     : k_poisson_p_f64<RB, false, false>;
-    const int64_t grid = resident_grid(reinterpret_cast<const void *>(fn), pl.nitems);
-    hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(kNT), 0, s, rh, poh, pnh, mloc, m, pl.nstrips, pl.rpi,
-                       pl.nitems, rr, rsold, first, cv, pap_out, ws.partials, ws.tickets + T_MATVEC);
+    const int64_t grid = resident_grid(reinterpret_cast<const void *>(fn), ir.cnt1 + ir.cnt2);
+    hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(kNT), 0, s, rh, poh, pnh, mloc, m, pl.nstrips, pl.rpi, ir, rr,
+                       rsold, first, cv, pap_out, add_to_out, ws.partials, ws.tickets + T_MATVEC);
 }
 template <int RB>
 static void launch_poisson_xr(const PoissonPlan &pl, hipStream_t s, const double *pnh, double *x, double *r,
@@ -1772,7 +1780,7 @@ static void launch_poisson_xr(const PoissonPlan &pl, hipStream_t s, const double
 
 hipError_t poisson_p_f64(const double *rh, const double *poh, double *pnh, int64_t mloc, int64_t m, const double *rr,
                          const double *rsold, bool first, double *pap_out, const RedWs &ws, hipStream_t s, double eps,
-                         int64_t k, int64_t *kdone, double *rrfinal) {
+                         int64_t k, int64_t *kdone, double *rrfinal, int part) {
     if (!poisson_fusable(mloc, m) || !al16(rh) || !al16(pnh) || (!first && !al16(poh))) return hipErrorInvalidValue;
     ConvArgs cv;
     cv.eps = eps;
@@ -1780,11 +1788,23 @@ hipError_t poisson_p_f64(const double *rh, const double *poh, double *pnh, int64
     cv.kdone = kdone;
     cv.rrfinal = rrfinal;
     const PoissonPlan pl = poisson_plan(mloc, m);
+    const int64_t nruns = pl.nitems / pl.nstrips, ns = pl.nstrips;
+    // part 0: every item; 1: runs 1..nruns-2 (no halo row read); 2: runs 0 and
+    // nruns-1, adding to part 1's p.Ap when part 1 had items
+    ItemRanges ir{0, pl.nitems, 0, 0};
+    int add = 0;
+    if (part == 1) {
+        if (nruns <= 2) return hipSuccess;
+        ir = ItemRanges{ns, (nruns - 2) * ns, 0, 0};
+    } else if (part == 2) {
+        ir = ItemRanges{0, ns, (nruns - 1) * ns, nruns > 1 ? ns : 0};
+        add = nruns > 2;
+    }
     switch (pl.rb) {
-        case 1: launch_poisson_p<1>(pl, s, rh, poh, pnh, mloc, m, rr, rsold, first, cv, pap_out, ws); break;
-        case 2: launch_poisson_p<2>(pl, s, rh, poh, pnh, mloc, m, rr, rsold, first, cv, pap_out, ws); break;
-        case 8: launch_poisson_p<8>(pl, s, rh, poh, pnh, mloc, m, rr, rsold, first, cv, pap_out, ws); break;
-        default: launch_poisson_p<4>(pl, s, rh, poh, pnh, mloc, m, rr, rsold, first, cv, pap_out, ws); break;
+        case 1: launch_poisson_p<1>(pl, s, rh, poh, pnh, mloc, m, rr, rsold, first, cv, pap_out, ws, ir, add); break;
+        case 2: launch_poisson_p<2>(pl, s, rh, poh, pnh, mloc, m, rr, rsold, first, cv, pap_out, ws, ir, add); break;
+        case 8: launch_poisson_p<8>(pl, s, rh, poh, pnh, mloc, m, rr, rsold, first, cv, pap_out, ws, ir, add); break;
+        default: launch_poisson_p<4>(pl, s, rh, poh, pnh, mloc, m, rr, rsold, first, cv, pap_out, ws, ir, add); break;
     }
     return hipGetLastError();
 }

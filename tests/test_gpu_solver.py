@@ -344,6 +344,28 @@ def test_poisson_fused_iteration_matches_split(monkeypatch, shards, gated):
         assert not s.info.flags & cg.CGX_FUSED_ACTIVE
 
 
+@pytest.mark.parametrize("m,P,eps", [(96, 4, 1e-10), (256, 2, 1e-8), (64, 8, 1e-10)])
+def test_poisson_halo_overlap_matches(monkeypatch, m, P, eps):
+    """Several slabs: r's halo exchange runs on the comm streams while
+    k_poisson_p does the slab's interior runs; its two edge runs follow the
+    exchange and add their p.Ap share.  Same loop count and x (to 1e-12) as the
+    exchange-then-kernel order (CGX_HALO_OVERLAP=0), gated and host-checked.
+    (eps above the attainable-residual floor: see test_poisson_matches_oracle.)"""
+    n = m * m
+    xo, so = oracle.cg_poisson_f64(m, np.ones(n), np.zeros(n), eps=eps)
+    for gated in ("1", "0"):
+        monkeypatch.setenv("CGX_GATED", gated)
+        res = []
+        for ov in ("1", "0"):
+            monkeypatch.setenv("CGX_HALO_OVERLAP", ov)
+            with cg.Solver(None, poisson_m=m, devices=[0] * P) as s:
+                s.fill(1.0, 0.0)
+                res.append(s.solve(None, eps=eps))
+        (x1, st1), (x0, st0) = res
+        assert st1.iterations == st0.iterations == so.iterations
+        assert rel(x1, x0) <= 1e-12 and rel(x1, xo) <= TOL
+
+
 def test_poisson_fused_in_pieces_and_iteration_cap():
     """Iterations issued in several cgx_iterate calls (fixed count, then
     convergence-tested) give the one-call solve; a cap that stops exactly at
@@ -378,7 +400,12 @@ def test_poisson_equals_dense_operator():
     assert rel(xs, xd) <= 1e-12
 
 
-def test_poisson_rank_mode_world1_and_fixed_count():
+@pytest.mark.parametrize("halo", ["default", "force"])
+def test_poisson_rank_mode_world1_and_fixed_count(monkeypatch, halo):
+    """Rank mode at world size 1; `force` also runs the overlapped r halo
+    exchange (empty ncclSend/Recv group on the comm stream, split k_poisson_p)."""
+    if halo == "force":
+        monkeypatch.setenv("CGX_HALO_OVERLAP", "force")
     m = 128
     with cg.Solver(None, poisson_m=m, rank=0, nranks=1, unique_id=cg.get_unique_id()) as s:
         s.fill(1.0, 0.0)
@@ -386,6 +413,11 @@ def test_poisson_rank_mode_world1_and_fixed_count():
     xo, so = oracle.cg_poisson_f64(m, np.ones(m * m), np.zeros(m * m), eps=-1.0, max_iter=150)
     assert st.iterations == so.iterations == 150
     assert rel(x, xo) <= 1e-9
+    with cg.Solver(None, poisson_m=m, rank=0, nranks=1, unique_id=cg.get_unique_id()) as s:
+        s.fill(1.0, 0.0)
+        x, st = s.solve(None, eps=1e-8)  # convergence-tested (device-gated)
+    xo, so = oracle.cg_poisson_f64(m, np.ones(m * m), np.zeros(m * m), eps=1e-8)
+    assert st.converged and st.iterations == so.iterations and rel(x, xo) <= TOL
 
 
 def test_poisson_rejects_bad_use():
