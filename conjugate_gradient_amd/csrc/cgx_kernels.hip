@@ -4,9 +4,11 @@
 // 172-245) become:
 //   k_matvec_f64      matVec (+ the p.Ap vecVec fused into its epilogue)
 //   k_residual_f64    residual x2 + r.r      (serialConjugate.c:209-212)
-//   k_update_xr_f64   scalarVec+vecAdd (x), scalarVec+vecSub (r), r.r
-//                     (serialConjugate.c:219-234)
-//   k_update_p_f64    scalarVec+vecAdd (p)   (serialConjugate.c:239-243)
+//   k_update_r_f64    scalarVec+vecSub (r), r.r       (serialConjugate.c:226-234)
+//   k_update_xp_f64   scalarVec+vecAdd (x, deferred) and (p) (:221-225, :239-243),
+//                     with the device-side stop decision
+//   k_update_xr_f64 / k_update_p_f64   the same split as the reference (kernel-level ABI)
+//   k_poisson_p_f64 / k_poisson_xr_f64 the fused matrix-free Poisson iteration
 // and, for CGX_F32_REF, kernels that keep the reference's exact fp32
 // operation order (sequential per-row and per-dot accumulation, every
 // multiply and add rounded separately: `#pragma clang fp contract(off)`).
@@ -16,10 +18,12 @@
 // 1-KiB, 128-column chunk of a row per instruction), R rows per wave share
 // each p chunk held in registers (p re-reads hit L1/L2: p is <= 1 MiB), U
 // chunks per row are in flight per lane, and the grid is sized to the
-// resident-wave capacity and grid-strides over row groups.  No MFMA: a GEMV
-// has no reuse of A.  Reductions are deterministic: per-block partials in
-// fixed slots, summed in index order by the last block to arrive (agent-scope
-// release/acquire, cdna_hip_programming.md Guideline 16).
+// resident-wave capacity and grid-strides over row groups; the next step's
+// loads are issued before the current step's FMAs (software pipeline).  No
+// MFMA: a GEMV has no reuse of A.  Reductions are deterministic: per-block
+// partials in fixed slots, summed in index order by the last block to arrive
+// (write-through sc1 partials and a relaxed ticket, the fence-free form of
+// cdna_hip_programming.md Guideline 16).
 #include "cgx_kernels.h"
 
 #include <algorithm>
@@ -96,9 +100,12 @@ __device__ __forceinline__ void grid_sum_last_block(double v, double *partials, 
 }
 
 // Load policy of the A stream (the only data a matVec reads once):
-//   0 plain global_load, 1 global_load ... nt (default),
-//   >= 2: buffer_load with cache-policy bits aux = kBufAux[POL] (2 nt,
-//   18 nt sc1, 19 sc0 nt sc1, 16 sc1, 0 none) through a per-row descriptor.
+//   0 plain global_load, 1 global_load ... nt,
+//   2..6: buffer_load with cache-policy bits aux = kBufAux[POL] (2 nt,
+//   18 nt sc1, 19 sc0 nt sc1, 16 sc1, 0 none) through a per-row descriptor;
+//   7 / 8: software-pipelined, buffer / global nt (8 = the default plan);
+//   9 / 10 flattened pipeline; 11 LDS-staged p; 12 / 13 SGPR row bases
+//   (+ LDS p).  All give the same row sums bit for bit.
 constexpr int kBufAux[7] = {0, 0, 2, 18, 19, 16, 0};
 typedef unsigned int u4 __attribute__((ext_vector_type(4)));
 
