@@ -1303,7 +1303,7 @@ __device__ __forceinline__ void poisson_xr_step(const double *__restrict__ pnh, 
 template <int RB, bool NT, bool HT>
 __global__ __launch_bounds__(kNT) void k_poisson_xr_f64(const double *__restrict__ pnh, double *__restrict__ x,
                                                         double *__restrict__ r, int64_t mloc, int64_t m,
-                                                        int64_t nstrips, int64_t rpi, int64_t nitems,
+                                                        int64_t nstrips, int64_t rpi, int64_t nitems, int reverse,
                                                         const double *rsold, const double *pAp, double *rr_out,
                                                         double *partials, unsigned *ticket, const int64_t *gate) {
     static_assert(RB <= kEdgeRB, "edge buffer");
@@ -1312,7 +1312,11 @@ __global__ __launch_bounds__(kNT) void k_poisson_xr_f64(const double *__restrict
     const double alpha = *rsold / *pAp;
     double acc = 0.0;
     int par = 0;
-    for (int64_t w = blockIdx.x; w < nitems; w += gridDim.x) {
+    for (int64_t v = blockIdx.x; v < nitems; v += gridDim.x) {
+        // reverse: walk the slab from its end, where the previous kernel
+        // (k_poisson_p, forward) last wrote p_k, so the first bytes read may
+        // still sit in the 256 MB MALL
+        const int64_t w = reverse ? nitems - 1 - v : v;
         const StripLane L = strip_lane(w, nstrips, m);
         const int64_t i0 = (w / nstrips) * rpi;
         const int64_t i1 = (i0 + rpi < mloc) ? i0 + rpi : mloc;
@@ -1782,7 +1786,8 @@ static void launch_poisson_xr(const PoissonPlan &pl, hipStream_t s, const double
                     : k_poisson_xr_f64<RB, false, false>;
     const int64_t grid = resident_grid(reinterpret_cast<const void *>(fn), pl.nitems);
     hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(kNT), 0, s, pnh, x, r, mloc, m, pl.nstrips, pl.rpi,
-                       pl.nitems, rsold, pAp, rr_out, ws.partials, ws.tickets + T_XR, gate);
+                       pl.nitems, env_int("CGX_STENCIL_REVERSE", 1), rsold, pAp, rr_out, ws.partials,
+                       ws.tickets + T_XR, gate);
 }
 
 hipError_t poisson_p_f64(const double *rh, const double *poh, double *pnh, int64_t mloc, int64_t m, const double *rr,
