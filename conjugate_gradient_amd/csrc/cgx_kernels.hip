@@ -1370,36 +1370,93 @@ __global__ void k_sum_ordered(const T *in, int cnt, int stride, T *out) {
 // ---------------------------------------------------------------------------
 // matVec: one lane per row, columns in ascending order, out = ((0 + a0 v0) + a1 v1) + ...
 // A 64x64 tile is staged through LDS so the global reads stay coalesced.
+// One lane per row keeps the reference's order: out[i] = ((0 + a_i0 v_0) +
+// a_i1 v_1) + ..., every product and sum rounded to float.  A wave owns 64
+// rows and walks 64 x 128 tiles: the next tile is loaded into registers
+// (32 float4 loads per lane, coalesced 512-B row pieces, all issued at once)
+// while the current one is consumed from LDS, then written to the other LDS
+// buffer (row stride 129 floats: conflict-free when lane t walks row t).
+constexpr int kRefTC = 128;  // tile columns
 __global__ __launch_bounds__(64) void k_matvec_ref_f32(const float *__restrict__ A, int64_t lda,
                                                        int64_t rows, int64_t cols,
                                                        const float *__restrict__ v,
                                                        float *__restrict__ out) {
 #pragma clang fp contract(off)
-    __shared__ float tile[64][65];
-    __shared__ float pv[64];
+    __shared__ float tile[2][64][kRefTC + 1];
+    __shared__ float pv[2][kRefTC];
+    typedef float f4 __attribute__((ext_vector_type(4)));
     const int t = threadIdx.x;
     const int64_t row0 = (int64_t)blockIdx.x * 64;
-    float acc = 0.0f;
-    for (int64_t c0 = 0; c0 < cols; c0 += 64) {
-        const int w = (cols - c0 < 64) ? (int)(cols - c0) : 64;
-        for (int i = 0; i < 64; ++i) {
-            const int64_t rr = row0 + i;
-            tile[i][t] = (rr < rows && t < w) ? A[rr * lda + c0 + t] : 0.0f;
+    const int q = t & 31;          // column quad of this lane within a tile row
+    const int rsub = t >> 5;       // 0/1: which of two rows this lane loads per step
+    const bool vec_ok = (lda & 3) == 0 && ((reinterpret_cast<uintptr_t>(A) & 15) == 0);
+    const int64_t ntiles = (cols + kRefTC - 1) / kRefTC;
+    f4 nx[32];
+    float pn[2];
+    auto load_tile = [&](int64_t c0) {
+        const int w = (cols - c0 < kRefTC) ? (int)(cols - c0) : kRefTC;
+        if (vec_ok && row0 + 64 <= rows && w == kRefTC) {  // whole tile: 32 unconditional 16-B loads
+            const float *base = A + (row0 + rsub) * lda + c0 + 4 * q;
+#pragma unroll
+            for (int k = 0; k < 32; ++k) nx[k] = *reinterpret_cast<const f4 *>(base + (int64_t)(2 * k) * lda);
+            pn[0] = v[c0 + t];
+            pn[1] = v[c0 + t + 64];
+            return;
         }
-        pv[t] = (t < w) ? v[c0 + t] : 0.0f;
+#pragma unroll
+        for (int k = 0; k < 32; ++k) {
+            const int64_t rr = row0 + 2 * k + rsub;
+            const int c = 4 * q;
+            f4 val = (f4)(0.0f);
+            if (rr < rows) {
+                if (vec_ok && c + 4 <= w) {
+                    val = *reinterpret_cast<const f4 *>(A + rr * lda + c0 + c);
+                } else {
+                    for (int e = 0; e < 4; ++e)
+                        if (c + e < w) val[e] = A[rr * lda + c0 + c + e];
+                }
+            }
+            nx[k] = val;
+        }
+        pn[0] = (t < w) ? v[c0 + t] : 0.0f;
+        pn[1] = (t + 64 < w) ? v[c0 + t + 64] : 0.0f;
+    };
+    auto store_tile = [&](int b) {
+#pragma unroll
+        for (int k = 0; k < 32; ++k) {
+            float *dst = &tile[b][2 * k + rsub][4 * q];
+            dst[0] = nx[k][0];
+            dst[1] = nx[k][1];
+            dst[2] = nx[k][2];
+            dst[3] = nx[k][3];
+        }
+        pv[b][t] = pn[0];
+        pv[b][t + 64] = pn[1];
+    };
+    float acc = 0.0f;
+    if (ntiles > 0) {
+        load_tile(0);
+        store_tile(0);
         __syncthreads();
-        if (w == 64) {
+    }
+    for (int64_t tt = 0; tt < ntiles; ++tt) {
+        const int b = (int)(tt & 1);
+        const int64_t c0 = tt * kRefTC;
+        const int w = (cols - c0 < kRefTC) ? (int)(cols - c0) : kRefTC;
+        if (tt + 1 < ntiles) load_tile(c0 + kRefTC);  // in flight during the chain below
+        if (w == kRefTC) {
 #pragma unroll 16
-            for (int j = 0; j < 64; ++j) {
-                const float prod = tile[t][j] * pv[j];
+            for (int j = 0; j < kRefTC; ++j) {
+                const float prod = tile[b][t][j] * pv[b][j];
                 acc = acc + prod;
             }
         } else {
             for (int j = 0; j < w; ++j) {
-                const float prod = tile[t][j] * pv[j];
+                const float prod = tile[b][t][j] * pv[b][j];
                 acc = acc + prod;
             }
         }
+        if (tt + 1 < ntiles) store_tile(b ^ 1);
         __syncthreads();
     }
     if (row0 + t < rows) out[row0 + t] = acc;
@@ -1410,18 +1467,40 @@ __global__ __launch_bounds__(64) void k_matvec_ref_f32(const float *__restrict__
 __global__ __launch_bounds__(64) void k_dot_ref_f32(int64_t n, const float *__restrict__ a,
                                                     const float *__restrict__ b, float *out) {
 #pragma clang fp contract(off)
+    // One wave.  The products of 8 chunks of 64 (each rounded to float, as
+    // serialConjugate.c:150 forms them) go to LDS; then every lane walks them
+    // in index order with 16-B broadcast reads and adds them one by one, the
+    // reference's single sequential sum (all lanes hold the same s).
+    constexpr int B = 8;
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    __shared__ f4 sp[B * 64 / 4];
+    float *spf = reinterpret_cast<float *>(sp);
     const int lane = threadIdx.x;
     float s = 0.0f;
-    for (int64_t c0 = 0; c0 < n; c0 += 64) {
-        const float prod = (c0 + lane < n) ? a[c0 + lane] * b[c0 + lane] : 0.0f;
-        const int pb = __float_as_int(prod);
-        if (n - c0 >= 64) {
+    for (int64_t c0 = 0; c0 < n; c0 += 64 * B) {
+        float pr[B];
 #pragma unroll
-            for (int j = 0; j < 64; ++j) s = s + __int_as_float(__builtin_amdgcn_readlane(pb, j));
-        } else {
-            const int w = (int)(n - c0);
-            for (int j = 0; j < w; ++j) s = s + __int_as_float(__builtin_amdgcn_readlane(pb, j));
+        for (int u = 0; u < B; ++u) {
+            const int64_t i = c0 + u * 64 + lane;
+            pr[u] = i < n ? a[i] * b[i] : 0.0f;
         }
+#pragma unroll
+        for (int u = 0; u < B; ++u) spf[u * 64 + lane] = pr[u];
+        __syncthreads();
+        const int64_t left = n - c0;
+        if (left >= 64 * B) {
+#pragma unroll 8
+            for (int q = 0; q < B * 16; ++q) {
+                const f4 v = sp[q];
+                s = s + v.x;
+                s = s + v.y;
+                s = s + v.z;
+                s = s + v.w;
+            }
+        } else {
+            for (int i = 0; i < (int)left; ++i) s = s + spf[i];
+        }
+        __syncthreads();
     }
     if (lane == 0) *out = s;
 }
