@@ -188,10 +188,10 @@ def main(argv=None) -> int:
                          "stream: configs[3], A kept in pinned host memory and streamed every matVec; "
                          "poisson: configs[4], matrix-free 5-point Poisson on an m x m grid (b=1, x0=0)")
     ap.add_argument("--m", type=int, default=8192, help="Poisson grid width (n = m*m)")
-    ap.add_argument("--comm", choices=["collective", "p2p", "nooverlap"], default="collective",
+    ap.add_argument("--comm", choices=["collective", "p2p", "nooverlap", "deterministic"], default="collective",
                     help="exchange: RCCL collectives with the p allgather overlapped (default), "
-                         "point-to-point_cg.c's gather-to-root + send-to-all (p2p), or collectives "
-                         "without overlap")
+                         "point-to-point_cg.c's gather-to-root + send-to-all (p2p), collectives "
+                         "without overlap, or the scalars combined in rank order (deterministic)")
     ap.add_argument("--n", type=int, default=None, help="system size (default 65536 dense, 131072 stream)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-n", type=int, default=None, help="N for the CPU baseline (default: --n)")
@@ -211,7 +211,8 @@ def main(argv=None) -> int:
     if (m if poisson else n) % world:
         raise SystemExit(f"{m if poisson else n} is not divisible by {world}")
     flags = cg.CGX_F64 | cg.CGX_TIMING | (cg.CGX_HOST_STREAM if stream else 0)
-    flags |= {"collective": 0, "p2p": cg.CGX_COMM_P2P, "nooverlap": cg.CGX_NO_OVERLAP}[args.comm]
+    flags |= {"collective": 0, "p2p": cg.CGX_COMM_P2P, "nooverlap": cg.CGX_NO_OVERLAP,
+              "deterministic": cg.CGX_DETERMINISTIC}[args.comm]
     if use_dist:
         uid = bcast_bytes(dist, cg.get_unique_id() if rank == 0 else None)
         solver = cg.Solver(n, rank=rank, nranks=world, unique_id=uid, device=local_rank, flags=flags, poisson_m=m)
@@ -301,6 +302,8 @@ def main(argv=None) -> int:
             "exchange": ("none (single GPU)" if not use_dist or world == 1 else
                          "RCCL halo ncclSend/Recv + 2x allreduce" if poisson else
                          "point-to-point_cg.c pattern: ncclSend/Recv via rank 0" if args.comm == "p2p" else
+                         "RCCL allgather(p) overlapped + rank-ordered scalar combine (allgather of partials)"
+                         if args.comm == "deterministic" else
                          "RCCL allgather(p) overlapped with own-block matVec + 2x allreduce"
                          if overlap_on else "RCCL allgather(p) + 2x allreduce"),
         },

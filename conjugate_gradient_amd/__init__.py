@@ -43,6 +43,7 @@ CGX_HOST_STREAM = 0x200
 CGX_NO_OVERLAP = 0x400
 CGX_OVERLAP_ACTIVE = 0x800
 CGX_FUSED_ACTIVE = 0x2000
+CGX_DETERMINISTIC = 0x4000
 CGX_COMM_P2P = 0x1000
 
 _HERE = os.path.dirname(os.path.abspath(__file__))

@@ -601,6 +601,12 @@ int exchange_scalar(cgx_ctx *c, int lslot, int gslot) {
             NCCLT(ncclAllGather(slot(s, lslot), slot(s, S_GATHER), 1, ncclUint64, s.comm, s.stream));
             HIPT(sum_ordered_f32(reinterpret_cast<const float *>(slot(s, S_GATHER)), c->nranks,
                                  reinterpret_cast<float *>(slot(s, gslot)), s.stream));
+        } else if (c->flags & CGX_DETERMINISTIC) {
+            // fp64, rank-order sum: the same bits as the multi-shard mode with the
+            // same partition, whatever algorithm RCCL would pick for an allreduce
+            NCCLT(ncclAllGather(slot(s, lslot), slot(s, S_GATHER), 1, ncclUint64, s.comm, s.stream));
+            HIPT(sum_ordered_f64(reinterpret_cast<const double *>(slot(s, S_GATHER)), c->nranks,
+                                 reinterpret_cast<double *>(slot(s, gslot)), s.stream));
         } else {
             NCCLT(ncclAllReduce(slot(s, lslot), slot(s, gslot), 1, ncclDouble, ncclSum, s.comm, s.stream));
         }

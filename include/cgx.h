@@ -80,6 +80,13 @@ extern "C" {
                                    copies through shard 0 in multi-shard mode).
                                    Scalars are summed in rank order.  For the
                                    p2p-vs-collective comparison of the report. */
+#define CGX_DETERMINISTIC 0x4000 /* rank mode, fp64: combine the two scalars by
+                                    allgathering the per-rank partials and
+                                    summing them in rank order (as multi-shard
+                                    mode always does) instead of ncclAllReduce:
+                                    results independent of RCCL's algorithm and
+                                    bitwise equal to the multi-shard run with the
+                                    same partition */
 #define CGX_HOST_STREAM  0x200 /* keep A in pinned host memory and stream row
                                   tiles through the GPU every matVec (out-of-HBM
                                   systems; tile size CGX_STREAM_TILE_MB, default

@@ -91,7 +91,7 @@ def test_row_block_shards_f64(golden, name, P):
     assert rel(x, xo) <= TOL
 
 
-@pytest.mark.parametrize("mode", ["collective", "overlap", "p2p"])
+@pytest.mark.parametrize("mode", ["collective", "overlap", "p2p", "deterministic"])
 def test_rccl_rank_mode_world1(monkeypatch, mode):
     """The one-process-per-GPU path (RCCL allgather/allreduce) at world size 1:
     plain collectives; the overlapped exchange forced on (CGX_OVERLAP=force:
@@ -101,7 +101,7 @@ def test_rccl_rank_mode_world1(monkeypatch, mode):
     A, b, x0 = case("spd1024", np.float64)
     if mode == "overlap":
         monkeypatch.setenv("CGX_OVERLAP", "force")
-    flags = cg.CGX_F64 | (cg.CGX_COMM_P2P if mode == "p2p" else 0)
+    flags = cg.CGX_F64 | {"p2p": cg.CGX_COMM_P2P, "deterministic": cg.CGX_DETERMINISTIC}.get(mode, 0)
     uid = cg.get_unique_id()
     with cg.Solver(b.size, rank=0, nranks=1, unique_id=uid, device=0, flags=flags) as s:
         assert bool(s.info.flags & cg.CGX_OVERLAP_ACTIVE) == (mode == "overlap")
@@ -111,6 +111,10 @@ def test_rccl_rank_mode_world1(monkeypatch, mode):
     xo, so = oracle.cg_f64(A, b, x0, eps=1e-10)
     assert st.iterations == so.iterations and rel(x, xo) <= TOL
     assert rn <= TOL * bn
+    if mode == "deterministic":  # rank-order combine: the single-shard bits
+        xs = x0.copy()
+        cg.conjugrad(A, b, xs, eps=1e-10)
+        assert np.array_equal(x, xs)
     if mode != "collective":
         return
     with cg.Solver(b.size, rank=0, nranks=1, unique_id=cg.get_unique_id(), flags=cg.CGX_F32_REF) as s:
