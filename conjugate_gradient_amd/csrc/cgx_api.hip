@@ -111,6 +111,9 @@ struct Shard {
     bool x_zero = true;  // x is known to be all zeros (x0 = 0: the first A x is skipped)
     RedWs ws{nullptr, nullptr};
     double *h_pin = nullptr;
+    // convergence record {kdone, bits of r.r there} in host-mapped coherent
+    // memory: the deciding kernel stores it, the host reads it after an event
+    int64_t *h_rec = nullptr, *d_rec = nullptr;
     MatvecPlan plan;
     hipEvent_t ev_sync = nullptr;  // cross-shard ordering (LOCAL mode)
     std::vector<hipEvent_t> ev_t;  // timing pairs (CGX_TIMING)
@@ -243,6 +246,9 @@ int alloc_shard(cgx_ctx *c, Shard &s) {
     HIPT(hipMemsetAsync(s.ws.tickets, 0, kTickets * sizeof(unsigned), s.stream));
     if (s.xfull) HIPT(hipMemsetAsync(s.xfull, 0, xlen * es, s.stream));
     HIPT(hipHostMalloc(reinterpret_cast<void **>(&s.h_pin), 8 * (8 + kLookRing), hipHostMallocDefault));
+    HIPT(hipHostMalloc(reinterpret_cast<void **>(&s.h_rec), 16, hipHostMallocMapped | hipHostMallocCoherent));
+    HIPT(hipHostGetDevicePointer(reinterpret_cast<void **>(&s.d_rec), s.h_rec, 0));
+    s.h_rec[0] = s.h_rec[1] = 0;
     for (int q = 0; q < kLookRing; ++q) HIPT(hipEventCreateWithFlags(&s.ev_look[q], hipEventDisableTiming));
     if (c->flags & CGX_TIMING) {
         s.ev_t.resize(2 * kEvPairs);
@@ -262,6 +268,7 @@ void free_shard(Shard &s) {
     if (s.ws.partials) (void)hipFree(s.ws.partials);
     if (s.ws.tickets) (void)hipFree(s.ws.tickets);
     if (s.h_pin) (void)hipHostFree(s.h_pin);
+    if (s.h_rec) (void)hipHostFree(s.h_rec);
     for (auto e : s.ev_t) (void)hipEventDestroy(e);
     if (s.ev_sync) (void)hipEventDestroy(s.ev_sync);
     for (int q = 0; q < kMaxCopyStreams; ++q)
@@ -675,6 +682,11 @@ int matvec_streamed(cgx_ctx *c, Shard &s, const char *vec) {
     return CGX_OK;
 }
 
+// The host-mapped convergence record: written by shard 0's deciding kernel only.
+inline int64_t *rec_of(const cgx_ctx *c, const Shard &s, bool gated) {
+    return (gated && &s == &c->sh[0]) ? s.d_rec : nullptr;
+}
+
 inline const int64_t *gate_of(const Shard &s, bool gated) {
     return gated ? reinterpret_cast<const int64_t *>(slot(s, S_KDONE)) : nullptr;
 }
@@ -766,6 +778,7 @@ int do_begin(cgx_ctx *c) {
     for (auto &s : c->sh) {  // device-side convergence record: not converged
         TRY(set_dev(s));
         HIPT(hipMemsetAsync(slot(s, S_KDONE), 0, 16, s.stream));
+        s.h_rec[0] = s.h_rec[1] = 0;  // no kernel of this solve has run yet (do_begin follows a sync)
     }
     c->k = 0;
     c->converged = 0;
@@ -920,7 +933,7 @@ int do_iteration_poisson(cgx_ctx *c, double eps, int *stop, bool gated) {
             HIPT(poisson_p_f64(D(s.rh), D(pold), D(pnew), s.nloc / m, m, D(slot(s, rk)), D(slot(s, rkm1)), k == 0,
                                D(slot(s, out_slot(c, pl, pg))), s.ws, s.stream, gated ? eps : -1.0, k,
                                gated ? reinterpret_cast<int64_t *>(slot(s, S_KDONE)) : nullptr,
-                               gated ? D(slot(s, S_RRFINAL)) : nullptr, part));
+                               gated ? D(slot(s, S_RRFINAL)) : nullptr, part, rec_of(c, s, gated)));
         }
     }
     c->halo_pending = false;
@@ -1009,7 +1022,7 @@ int do_iteration(cgx_ctx *c, double eps, int *stop, bool gated = false) {
                                reinterpret_cast<const double *>(slot(s, pg)),
                                reinterpret_cast<const double *>(slot(s, rg)), s.stream, eps, k,
                                reinterpret_cast<int64_t *>(slot(s, S_KDONE)),
-                               reinterpret_cast<double *>(slot(s, S_RRFINAL))));
+                               reinterpret_cast<double *>(slot(s, S_RRFINAL)), rec_of(c, s, gated)));
         }
         return CGX_OK;
     }
@@ -1424,29 +1437,26 @@ static int iterate_gated(cgx_ctx *c, int64_t count, double eps, int64_t *done, i
     const int look = std::max(1, std::min(kLookRing - 1, (la && *la) ? std::atoi(la) : 2));
     const int64_t k0 = c->k;
     int64_t issued = 0, kd = 0;
-    int64_t *pin = reinterpret_cast<int64_t *>(s0.h_pin) + 8;  // kLookRing slots after read_scalar's
+    volatile int64_t *rec = s0.h_rec;  // {kdone, r.r bits}, stored by the deciding kernel
     for (; issued < count && kd == 0; ++issued) {
         int stop = 0;
         TRY(do_iteration(c, eps, &stop, /*gated=*/true));
         TRY(set_dev(s0));
         const int q = (int)(issued % kLookRing);
-        HIPT(hipMemcpyAsync(pin + q, slot(s0, S_KDONE), 8, hipMemcpyDeviceToHost, s0.stream));
         HIPT(hipEventRecord(s0.ev_look[q], s0.stream));
         if (issued >= look) {
-            const int qq = (int)((issued - look) % kLookRing);
-            HIPT(hipEventSynchronize(s0.ev_look[qq]));
-            kd = pin[qq];
+            HIPT(hipEventSynchronize(s0.ev_look[(issued - look) % kLookRing]));
+            kd = rec[0];  // the record of iteration issued-look or earlier
         }
     }
     TRY(sync_all(c));
-    double rrf = 0.0;
-    int64_t kdev = 0;
-    TRY(set_dev(s0));
-    HIPT(hipMemcpy(&kdev, slot(s0, S_KDONE), 8, hipMemcpyDeviceToHost));
+    const int64_t kdev = rec[0];
     const int64_t did = kdev ? (kdev - k0) : issued;
     c->total_iters += did - issued;  // do_iteration counted every enqueued one
     if (kdev) {
-        TRY(read_scalar(c, S_RRFINAL, &rrf));
+        const int64_t bits = rec[1];
+        double rrf;
+        std::memcpy(&rrf, &bits, 8);
         c->last_rr = rrf;
         c->k = kdev;
         c->converged = 1;

@@ -55,13 +55,14 @@ hipError_t update_p_f64(int64_t n, double *p, const double *r, const double *rr,
 // Solver split of the updates: r -= alpha Ap with *rr_out = r.r; then
 // x += alpha p and (rr != nullptr) p = r + (*rr / *rsold) p; alpha = *rsold / *pAp.
 // With kdone != nullptr update_xp also decides sqrt(*rr) < eps on the device:
-// on convergence it skips the p update and stores *kdone = k+1, *rrfinal = *rr;
+// on convergence it skips the p update and stores *kdone = k+1, *rrfinal = *rr
+// (and the same pair into hrec[0..1], host-mapped memory, when hrec != nullptr);
 // once *kdone is in (0, k] both kernels (update_r via gate) do nothing.
 hipError_t update_r_f64(int64_t n, double *r, const double *Ap, const double *rsold, const double *pAp,
                         double *rr_out, const RedWs &ws, hipStream_t s, const int64_t *gate = nullptr);
 hipError_t update_xp_f64(int64_t n, double *x, double *p, const double *r, const double *rsold, const double *pAp,
                          const double *rr, hipStream_t s, double eps = -1.0, int64_t k = 0,
-                         int64_t *kdone = nullptr, double *rrfinal = nullptr);
+                         int64_t *kdone = nullptr, double *rrfinal = nullptr, int64_t *hrec = nullptr);
 hipError_t dot_f64(int64_t n, const double *a, const double *b, double *out,
                    const RedWs &ws, hipStream_t s);
 // Rows [row0, row0+nrows) of the counter-hash SPD system; pad columns zeroed.
@@ -80,7 +81,7 @@ bool poisson_fusable(int64_t mloc, int64_t m);
 hipError_t poisson_p_f64(const double *rh, const double *poh, double *pnh, int64_t mloc, int64_t m, const double *rr,
                          const double *rsold, bool first, double *pap_out, const RedWs &ws, hipStream_t s,
                          double eps = -1.0, int64_t k = 0, int64_t *kdone = nullptr, double *rrfinal = nullptr,
-                         int part = 0);  // part: 0 all rows; 1 interior runs; 2 the two edge runs (+= part 1's p.Ap)
+                         int part = 0, int64_t *hrec = nullptr);  // part: 0 all rows; 1 interior runs; 2 the two edge runs (+= part 1's p.Ap)
 hipError_t poisson_xr_f64(const double *pnh, double *x, double *r, int64_t mloc, int64_t m, const double *rsold,
                           const double *pAp, double *rr_out, const RedWs &ws, hipStream_t s,
                           const int64_t *gate = nullptr);

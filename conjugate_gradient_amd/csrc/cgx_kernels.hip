@@ -851,7 +851,19 @@ struct ConvArgs {
     int64_t k = 0;
     int64_t *kdone = nullptr;   // 0 = not converged, else the loop-iteration count
     double *rrfinal = nullptr;
+    int64_t *hrec = nullptr;    // host-mapped copy of {kdone, rrfinal}: read by the host without a copy
 };
+
+// The convergence record: device slots for later launches' gates, and the
+// host-mapped copy the host reads after an event (no per-iteration D2H copy).
+__device__ __forceinline__ void record_convergence(const ConvArgs &cv, int64_t kdone, double rr) {
+    *cv.rrfinal = rr;
+    *cv.kdone = kdone;
+    if (cv.hrec) {
+        __hip_atomic_store(cv.hrec + 1, __double_as_longlong(rr), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(cv.hrec, kdone, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
 
 template <bool VEC, int VP = 2>
 __global__ __launch_bounds__(kNT) void k_update_xp_f64(int64_t n, double *__restrict__ x, double *__restrict__ p,
@@ -864,10 +876,7 @@ __global__ __launch_bounds__(kNT) void k_update_xp_f64(int64_t n, double *__rest
         const double rrn = *rr;
         if (cv.eps >= 0.0 && sqrt(rrn) < cv.eps) {
             upd_p = false;
-            if (blockIdx.x == 0 && threadIdx.x == 0) {
-                *cv.rrfinal = rrn;
-                *cv.kdone = cv.k + 1;
-            }
+            if (blockIdx.x == 0 && threadIdx.x == 0) record_convergence(cv, cv.k + 1, rrn);
         }
     }
     const double alpha = *rsold / *pAp;
@@ -1231,10 +1240,7 @@ __global__ __launch_bounds__(kNT) void k_poisson_p_f64(const double *__restrict_
     if (cv.kdone) {
         if (*cv.kdone != 0) return;
         if (!first && cv.eps >= 0.0 && sqrt(*rr) < cv.eps) {  // the same decision in every block
-            if (blockIdx.x == 0 && threadIdx.x == 0) {
-                *cv.rrfinal = *rr;
-                *cv.kdone = cv.k;
-            }
+            if (blockIdx.x == 0 && threadIdx.x == 0) record_convergence(cv, cv.k, *rr);
             return;
         }
     }
@@ -1743,13 +1749,15 @@ hipError_t update_r_f64(int64_t n, double *r, const double *Ap, const double *rs
 }
 
 hipError_t update_xp_f64(int64_t n, double *x, double *p, const double *r, const double *rsold, const double *pAp,
-                         const double *rr, hipStream_t s, double eps, int64_t k, int64_t *kdone, double *rrfinal) {
+                         const double *rr, hipStream_t s, double eps, int64_t k, int64_t *kdone, double *rrfinal,
+                         int64_t *hrec) {
     const bool vec = al16(x) && al16(p) && al16(r);
     ConvArgs cv;
     cv.eps = eps;
     cv.k = k;
     cv.kdone = kdone;
     cv.rrfinal = rrfinal;
+    cv.hrec = hrec;
     hipLaunchKernelGGL(vec ? k_update_xp_f64<true> : k_update_xp_f64<false>, dim3(grid_vec(n)), dim3(kNT), 0, s, n, x,
                        p, r, rsold, pAp, rr, cv);
     return hipGetLastError();
@@ -1871,13 +1879,14 @@ static void launch_poisson_xr(const PoissonPlan &pl, hipStream_t s, const double
 
 hipError_t poisson_p_f64(const double *rh, const double *poh, double *pnh, int64_t mloc, int64_t m, const double *rr,
                          const double *rsold, bool first, double *pap_out, const RedWs &ws, hipStream_t s, double eps,
-                         int64_t k, int64_t *kdone, double *rrfinal, int part) {
+                         int64_t k, int64_t *kdone, double *rrfinal, int part, int64_t *hrec) {
     if (!poisson_fusable(mloc, m) || !al16(rh) || !al16(pnh) || (!first && !al16(poh))) return hipErrorInvalidValue;
     ConvArgs cv;
     cv.eps = eps;
     cv.k = k;
     cv.kdone = kdone;
     cv.rrfinal = rrfinal;
+    cv.hrec = hrec;
     const PoissonPlan pl = poisson_plan(mloc, m);
     const int64_t nruns = pl.nitems / pl.nstrips, ns = pl.nstrips;
     // part 0: every item; 1: runs 1..nruns-2 (no halo row read); 2: runs 0 and

@@ -14,7 +14,8 @@ import conjugate_gradient_amd as cg  # noqa: E402
 
 def main():
     out = []
-    for n in (1024, 4096, 16384):
+    sizes = [int(a) for a in sys.argv[1:]] or [512, 1024, 2048, 4096, 8192, 16384]
+    for n in sizes:
         s = cg.Solver(n)
         s.generate_spd(42)
         t = {"1": [], "0": []}
