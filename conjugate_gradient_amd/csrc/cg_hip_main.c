@@ -25,6 +25,7 @@
  * parsing), --spd N [--seed S] (on-device synthetic system instead of files).
  */
 #define _POSIX_C_SOURCE 200809L
+#include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
@@ -69,6 +70,28 @@ static int read_file(const char *path, int64_t count, int as_float, void *out, i
     return rc;
 }
 
+/* Context creation (HIP runtime start, device buffers) runs on its own thread
+ * while the text files are parsed: the two are independent until the H2D. */
+typedef struct {
+    int64_t n;
+    int gpus, flags, rc;
+    cgx_ctx *ctx;
+} create_job;
+
+static void *create_ctx(void *arg) {
+    create_job *j = (create_job *)arg;
+    if (j->gpus == 1) {
+        j->rc = cgx_create(&j->ctx, j->n, 0, j->flags);
+    } else {
+        int devs[32];
+        int ndev = 0;
+        cgx_device_count(&ndev);
+        for (int g = 0; g < j->gpus; ++g) devs[g] = ndev > 0 ? g % ndev : 0;
+        j->rc = cgx_create_multi(&j->ctx, j->n, j->gpus, devs, j->flags);
+    }
+    return NULL;
+}
+
 int main(int argc, char **argv) {
     const double t_prog0 = now_s();
     int gpus = 1, fp32ref = 0, print_x = 0, stats = 0;
@@ -106,6 +129,7 @@ int main(int argc, char **argv) {
         return 1;
     }
     if (gpus < 1) { fprintf(stderr, "--gpus must be >= 1\n"); return 2; }
+    if (gpus > 32) { fprintf(stderr, "--gpus must be <= 32\n"); return 2; }
 
     /* ---- N ---------------------------------------------------------------- */
     int64_t n = 0;
@@ -139,23 +163,21 @@ int main(int argc, char **argv) {
         A = malloc((size_t)n * (size_t)n * es);
         b = malloc((size_t)n * es);
         if (!A || !b) { fprintf(stderr, "can't allocate memory for vector\n"); return 1; }
-        if (read_file(pos[0], n * n, fp32ref, A, threads) || read_file(pos[1], n, fp32ref, b, threads) ||
-            read_file(pos[2], n, fp32ref, x, 1))
-            return 1;
     }
-
-    cgx_ctx *ctx = NULL;
-    int rc;
-    if (gpus == 1) {
-        rc = cgx_create(&ctx, n, 0, flags);
-    } else {
-        int devs[32];
-        if (gpus > 32) { fprintf(stderr, "--gpus must be <= 32\n"); return 2; }
-        int ndev = 0;
-        cgx_device_count(&ndev);
-        for (int g = 0; g < gpus; ++g) devs[g] = ndev > 0 ? g % ndev : 0;
-        rc = cgx_create_multi(&ctx, n, gpus, devs, flags);
+    create_job job = {n, gpus, flags, CGX_OK, NULL};
+    pthread_t creator;
+    const int threaded = pthread_create(&creator, NULL, create_ctx, &job) == 0;
+    if (!threaded) create_ctx(&job);
+    const int read_rc = spd_n > 0 ? 0
+                        : (read_file(pos[0], n * n, fp32ref, A, threads) ||
+                           read_file(pos[1], n, fp32ref, b, threads) || read_file(pos[2], n, fp32ref, x, 1));
+    if (threaded) pthread_join(creator, NULL);  /* before any exit: HIP may be starting up on it */
+    if (read_rc) {
+        if (job.ctx) cgx_destroy(job.ctx);
+        return 1;
     }
+    cgx_ctx *ctx = job.ctx;
+    int rc = job.rc;
     if (rc != CGX_OK) return die_cgx(rc, "cgx_create");
 
     double t_dist0 = now_s(), t_dist1;
