@@ -76,10 +76,14 @@ typedef struct {
     int64_t n;
     int gpus, flags, rc;
     cgx_ctx *ctx;
+    double t_rt, t_done;  /* when the HIP runtime was up / creation finished (now_s) */
 } create_job;
 
 static void *create_ctx(void *arg) {
     create_job *j = (create_job *)arg;
+    int ndev0 = 0;
+    cgx_device_count(&ndev0); /* starts the HIP runtime */
+    j->t_rt = now_s();
     if (j->gpus == 1) {
         j->rc = cgx_create(&j->ctx, j->n, 0, j->flags);
     } else {
@@ -89,6 +93,7 @@ static void *create_ctx(void *arg) {
         for (int g = 0; g < j->gpus; ++g) devs[g] = ndev > 0 ? g % ndev : 0;
         j->rc = cgx_create_multi(&j->ctx, j->n, j->gpus, devs, j->flags);
     }
+    j->t_done = now_s();
     return NULL;
 }
 
@@ -164,13 +169,15 @@ int main(int argc, char **argv) {
         b = malloc((size_t)n * es);
         if (!A || !b) { fprintf(stderr, "can't allocate memory for vector\n"); return 1; }
     }
-    create_job job = {n, gpus, flags, CGX_OK, NULL};
+    create_job job = {n, gpus, flags, CGX_OK, NULL, 0.0, 0.0};
+    const double t_start = now_s();
     pthread_t creator;
     const int threaded = pthread_create(&creator, NULL, create_ctx, &job) == 0;
     if (!threaded) create_ctx(&job);
     const int read_rc = spd_n > 0 ? 0
                         : (read_file(pos[0], n * n, fp32ref, A, threads) ||
                            read_file(pos[1], n, fp32ref, b, threads) || read_file(pos[2], n, fp32ref, x, 1));
+    const double t_read = now_s();
     if (threaded) pthread_join(creator, NULL);  /* before any exit: HIP may be starting up on it */
     if (read_rc) {
         if (job.ctx) cgx_destroy(job.ctx);
@@ -199,6 +206,12 @@ int main(int argc, char **argv) {
     if (rc != CGX_OK) return die_cgx(rc, "cgx_solve");
     rc = cgx_get_x(ctx, x);
     if (rc != CGX_OK) return die_cgx(rc, "cgx_get_x");
+    if (getenv("CGX_CLI_TIMES")) /* phase breakdown, seconds since program start */
+        fprintf(stderr,
+                "{\"setup_s\": %.6f, \"read_s\": %.6f, \"hip_runtime_s\": %.6f, \"create_s\": %.6f, \"distribute_s\": %.6f, "
+                "\"solve_s\": %.6f, \"to_x_s\": %.6f}\n",
+                t_start - t_prog0, t_read - t_start, job.t_rt - t_start, job.t_done - t_start, t_dist1 - t_dist0, st.solve_ms / 1e3,
+                now_s() - t_prog0);
 
     if (gpus > 1) {
         printf("cg method execution time in seconds: %f\n", st.solve_ms / 1e3);

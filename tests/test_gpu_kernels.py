@@ -25,8 +25,11 @@ def _gpu(built):
     assert cg.device_count() >= 1, "no GPU visible: the HIP path must run"
 
 
-@pytest.mark.parametrize("rows,cols", [(1, 1), (2, 2), (5, 3), (64, 64), (300, 257), (1000, 1000), (8192, 96)])
-def test_matvec_ref_f32_bitwise(rows, cols):
+@pytest.mark.parametrize("variant", ["1", "2"])  # CGX_REF_MV: 64-row x 128 tiles / 16-row x 512 tiles (default)
+@pytest.mark.parametrize("rows,cols", [(1, 1), (2, 2), (5, 3), (64, 64), (300, 257), (1000, 1000), (8192, 96),
+                                       (16, 512), (17, 513), (33, 1536), (48, 1025), (100, 4100)])
+def test_matvec_ref_f32_bitwise(monkeypatch, variant, rows, cols):
+    monkeypatch.setenv("CGX_REF_MV", variant)
     rng = np.random.default_rng(rows * 7 + cols)
     A = rng.random((rows, cols), dtype=np.float32) - 0.5
     v = rng.random(cols, dtype=np.float32)
@@ -36,8 +39,10 @@ def test_matvec_ref_f32_bitwise(rows, cols):
     assert np.array_equal(out.to_host().view(np.uint32), ref.view(np.uint32))
 
 
-@pytest.mark.parametrize("n", [1, 63, 64, 65, 1000, 8192, 20000])
-def test_dot_ref_f32_bitwise(n):
+@pytest.mark.parametrize("variant", ["1", "2"])  # CGX_REF_DOT: one wave / 4 waves, loads off the chain (default)
+@pytest.mark.parametrize("n", [1, 63, 64, 65, 1000, 4096, 4097, 8192, 8193, 20000])
+def test_dot_ref_f32_bitwise(monkeypatch, variant, n):
+    monkeypatch.setenv("CGX_REF_DOT", variant)
     rng = np.random.default_rng(n)
     a = rng.random(n, dtype=np.float32) - 0.5
     b = rng.random(n, dtype=np.float32)

@@ -68,9 +68,14 @@ def main():
                     "reference_stdout": out.strip().splitlines()[0]})
         # cg_hip: the whole program
         t0 = time.perf_counter()
-        out = subprocess.run([cg.CLI_PATH, "--fp32-ref", "--print-x", "--stats", "--threads", str(a.threads),
-                              paths["A"], paths["b"], paths["x0"]], check=True, capture_output=True, text=True).stdout
+        proc = subprocess.run([cg.CLI_PATH, "--fp32-ref", "--print-x", "--stats", "--threads", str(a.threads),
+                               paths["A"], paths["b"], paths["x0"]], check=True, capture_output=True, text=True,
+                              env=dict(os.environ, CGX_CLI_TIMES="1"))
         t_cli = time.perf_counter() - t0
+        out = proc.stdout
+        phases = [ln for ln in proc.stderr.splitlines() if ln.startswith("{")]
+        if phases:
+            res["cg_hip_phases_s"] = json.loads(phases[-1])
         lines = out.strip().splitlines()
         x = np.array([float(v) for v in lines[-n:]], dtype=np.float32)
         xr = np.fromfile(xref, dtype=np.float32)
