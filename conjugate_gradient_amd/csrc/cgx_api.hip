@@ -1446,7 +1446,15 @@ static int iterate_gated(cgx_ctx *c, int64_t count, double eps, int64_t *done, i
         HIPT(hipEventRecord(s0.ev_look[q], s0.stream));
         if (issued >= look) {
             HIPT(hipEventSynchronize(s0.ev_look[(issued - look) % kLookRing]));
-            kd = rec[0];  // the record of iteration issued-look or earlier
+            // Only a record left by an iteration the event covers counts: the
+            // host-mapped word may already show a later iteration's decision,
+            // and acting on that would make the number of enqueued iterations
+            // (and so of collectives) depend on timing, rank by rank.  The
+            // record's k is the deciding launch's iteration index (dense: the
+            // converged iteration + 1, Poisson: the next iteration), so
+            // k <= the synced iteration means that launch is covered.
+            const int64_t r = rec[0];
+            if (r != 0 && r <= k0 + (issued - look)) kd = r;
         }
     }
     TRY(sync_all(c));

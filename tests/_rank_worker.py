@@ -1,0 +1,79 @@
+"""One rank of a multi-rank RCCL job on a single GPU (tests/test_gpu_multirank.py).
+
+RCCL refuses two ranks on one device of one host ("Duplicate GPU detected");
+the parent gives every rank its own NCCL_HOSTID, so RCCL sees P hosts and
+carries the exchange over its socket transport on the loopback interface.
+The data path is then host-staged instead of xGMI, but everything libcgx does
+in rank mode runs at world size P: the in-place ncclAllGather into each
+rank's row-block slot, the scalar allreduces, the overlapped exchange on the
+comm stream, the p2p pattern, the rank-ordered combine, the Poisson halo
+ncclSend/Recv, and the final x allgather.
+
+  python tests/_rank_worker.py MODE N P RANK UIDFILE OUTPREFIX
+"""
+import json
+import os
+import sys
+import time
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.dirname(HERE))
+sys.path.insert(0, HERE)
+
+import conjugate_gradient_amd as cg  # noqa: E402
+from _cases import case  # noqa: E402
+
+
+def main():
+    mode, n, P, rank, uidfile, out = sys.argv[1], int(sys.argv[2]), int(sys.argv[3]), int(sys.argv[4]), \
+        sys.argv[5], sys.argv[6]
+    if rank == 0:
+        uid = cg.get_unique_id()
+        with open(uidfile + ".tmp", "wb") as f:
+            f.write(uid)
+        os.rename(uidfile + ".tmp", uidfile)
+    else:
+        t0 = time.time()
+        while not os.path.exists(uidfile):
+            if time.time() - t0 > 60:
+                raise SystemExit("no unique id from rank 0")
+            time.sleep(0.05)
+        with open(uidfile, "rb") as f:
+            uid = f.read()
+    res = {"rank": rank}
+    if mode.startswith("poisson"):
+        m = n
+        with cg.Solver(None, poisson_m=m, rank=rank, nranks=P, unique_id=uid, device=0) as s:
+            s.fill(1.0, 0.0)
+            eps = 1e-8 if mode == "poisson_eps" else -1.0
+            x, st = s.solve(None, eps=eps, max_iter=-1 if eps > 0 else 120)
+            res.update(iterations=st.iterations, converged=st.converged)
+    else:
+        flags = {"f32ref": cg.CGX_F32_REF, "p2p": cg.CGX_COMM_P2P, "nooverlap": cg.CGX_NO_OVERLAP,
+                 "deterministic": cg.CGX_DETERMINISTIC, "p2p_f32ref": cg.CGX_F32_REF | cg.CGX_COMM_P2P}.get(
+            mode, cg.CGX_F64)
+        if not flags & cg.CGX_F32_REF:
+            flags |= cg.CGX_F64
+        f32 = bool(flags & cg.CGX_F32_REF)
+        A, b, x0 = case(f"spd{n}", np.float32 if f32 else np.float64)
+        with cg.Solver(n, rank=rank, nranks=P, unique_id=uid, device=0, flags=flags) as s:
+            res["overlap"] = bool(s.info.flags & cg.CGX_OVERLAP_ACTIVE)
+            res["nrows"] = s.info.nrows
+            s.set_system(A, b, x0)
+            x, st = s.solve(None, eps=1e-6 if f32 else 1e-10)
+            rn, bn = s.residual_norm()
+            res.update(iterations=st.iterations, converged=st.converged, relres=rn / bn)
+            if mode == "collective":  # a fixed-count run from a nonzero x0 (initial exchange + matVec)
+                s.set_x(np.full(n, 0.25))
+                _, st2 = s.solve(None, eps=-1.0, max_iter=5)
+                res["fixed_iterations"] = st2.iterations
+                res["fixed_relres"] = float(np.divide(*s.residual_norm()))
+    np.save(out + f"_x{rank}.npy", x)
+    with open(out + f"_r{rank}.json", "w") as f:
+        json.dump(res, f)
+
+
+if __name__ == "__main__":
+    main()

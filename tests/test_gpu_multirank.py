@@ -1,0 +1,144 @@
+"""Rank mode (one process per rank, RCCL) at world size 2 and 4 on one GPU.
+
+The driver's N = 2/4/8 bench runs use one process per GPU over RCCL.  One
+GPU box cannot run that placement (RCCL refuses two ranks on one device of
+one host), so each rank here gets its own NCCL_HOSTID: RCCL then sees P hosts
+and moves the data over its socket transport on the loopback interface.  The
+transport differs from xGMI; libcgx's rank-mode logic is what is checked:
+row-block offsets, the in-place allgather slots, the overlapped exchange on
+the comm stream, the scalar combines, the p2p pattern, the Poisson halo
+exchange and the final x allgather (tests/_rank_worker.py).
+
+Pins: fp64 x vs the fp64 oracle (conjgrad.m order) to 1e-10 with its loop
+count; CGX_DETERMINISTIC bitwise equal to the multi-shard run with the same
+partition; CGX_F32_REF bitwise equal to the oracle's P-part
+(point-to-point_cg.c allSum order) restatement; every rank ends with the
+same x.
+"""
+import json
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+import conjugate_gradient_amd as cg
+import oracle
+from _cases import case
+
+pytestmark = pytest.mark.gpu
+HERE = os.path.dirname(os.path.abspath(__file__))
+TOL = 1e-10
+
+
+def rel(a, b):
+    return float(np.linalg.norm(a - b) / np.linalg.norm(b))
+
+
+@pytest.fixture(scope="module", autouse=True)
+def _gpu(built):
+    assert cg.device_count() >= 1, "no GPU visible: the HIP path must run"
+
+
+def run_ranks(tmp_path, mode, n, P, timeout=150):
+    uidfile = str(tmp_path / "uid.bin")
+    out = str(tmp_path / mode)
+    procs = []
+    for r in range(P):
+        env = dict(os.environ, NCCL_HOSTID=f"cgx-test-host-{r}", NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1",
+                   HSA_ENABLE_IPC_MODE_LEGACY="0")
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "_rank_worker.py"), mode, str(n), str(P),
+                                       str(r), uidfile, out], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True))
+    logs = []
+    try:
+        for p in procs:
+            logs.append(p.communicate(timeout=timeout)[0])
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    for r, p in enumerate(procs):
+        assert p.returncode == 0, f"rank {r} exited {p.returncode}:\n{logs[r][-3000:]}"
+    xs = [np.load(out + f"_x{r}.npy") for r in range(P)]
+    res = []
+    for r in range(P):
+        with open(out + f"_r{r}.json") as f:
+            res.append(json.load(f))
+    for r in range(1, P):  # every rank holds the same allgathered x
+        assert np.array_equal(xs[r], xs[0])
+        assert res[r]["iterations"] == res[0]["iterations"]
+    return xs[0], res
+
+
+@pytest.mark.timeout(200)
+@pytest.mark.parametrize("P", [2, 4])
+@pytest.mark.parametrize("mode", ["collective", "nooverlap", "p2p", "deterministic"])
+def test_rank_mode_f64(tmp_path, mode, P):
+    n = 1024
+    x, res = run_ranks(tmp_path, mode, n, P)
+    assert res[0]["nrows"] == n // P
+    assert res[0]["overlap"] == (mode in ("collective", "deterministic"))  # row blocks are multiples of 128
+    A, b, x0 = case(f"spd{n}", np.float64)
+    xo, so = oracle.cg_f64(A, b, x0, eps=1e-10)
+    assert res[0]["iterations"] == so.iterations
+    assert rel(x, xo) <= TOL and res[0]["relres"] <= TOL
+    if mode == "deterministic":  # rank-ordered scalar combine == the multi-shard bits
+        xs = x0.copy()
+        cg.conjugrad(A, b, xs, eps=1e-10, shards=[0] * P)
+        assert np.array_equal(x, xs)
+    if mode == "collective":
+        assert res[0]["fixed_iterations"] == 5 and res[0]["fixed_relres"] < 1.0
+
+
+@pytest.mark.timeout(200)
+@pytest.mark.parametrize("mode", ["f32ref", "p2p_f32ref"])
+def test_rank_mode_f32ref_bitwise(tmp_path, mode):
+    n, P = 2048, 4
+    x, res = run_ranks(tmp_path, mode, n, P)
+    A, b, x0 = case(f"spd{n}")
+    xo, so = oracle.cg_f32ref(A, b, x0, eps=1e-6, nparts=P)
+    assert res[0]["iterations"] == so.iterations
+    assert np.array_equal(x.view(np.uint32), xo.view(np.uint32))
+
+
+@pytest.mark.timeout(200)
+@pytest.mark.parametrize("mode", ["poisson", "poisson_eps"])
+def test_rank_mode_poisson_halo(tmp_path, mode):
+    m, P = 128, 4
+    x, res = run_ranks(tmp_path, mode, m, P)
+    eps = 1e-8 if mode == "poisson_eps" else -1.0
+    xo, so = oracle.cg_poisson_f64(m, np.ones(m * m), np.zeros(m * m), eps=eps,
+                                   max_iter=-1 if eps > 0 else 120)
+    assert res[0]["iterations"] == so.iterations
+    assert rel(x, xo) <= (TOL if eps > 0 else 1e-9)
+
+
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("workload", ["dense", "poisson"])
+def test_bench_under_torchrun_world2(workload):
+    """The driver's N>1 command shape (torch.distributed.run, one process per
+    rank, RCCL inside libcgx, gloo control plane), at world size 2 on this GPU."""
+    import socket
+    s = socket.socket()
+    s.bind(("127.0.0.1", 0))
+    port = s.getsockname()[1]
+    s.close()
+    args = ["--gpus", "2", "--steps", "4", "--warmup", "1", "--no-cpu"]
+    args += ["--n", "4096"] if workload == "dense" else ["--workload", "poisson", "--m", "512"]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
+           "--master-addr", "127.0.0.1", "--master-port", str(port),
+           os.path.join(HERE, "_bench_rank_wrapper.py")] + args
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=200,
+                       env=dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0"))
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1, p.stdout[-2000:]  # rank 0 only
+    out = json.loads(lines[0])
+    assert out["n_gpus"] == 2 and out["steps"] == 4 and out["value"] > 0
+    assert out["config"]["rows_per_gpu"] == (2048 if workload == "dense" else 512 * 512 // 2)
+    assert out["check"]["relres"] < 1.0
+    if workload == "dense":
+        assert "allgather" in out["config"]["exchange"]
