@@ -187,12 +187,15 @@ def main(argv=None) -> int:
                     help="dense: configs[2], A resident in HBM (default); "
                          "stream: configs[3], A kept in pinned host memory and streamed every matVec; "
                          "poisson: configs[4], matrix-free 5-point Poisson on an m x m grid (b=1, x0=0)")
-    ap.add_argument("--m", type=int, default=8192, help="Poisson grid width (n = m*m)")
+    # --size / --grid: aliases that torch.distributed.run's own parser does not
+    # mistake for abbreviations of its options (--n, --m are ambiguous there)
+    ap.add_argument("--m", "--grid", dest="m", type=int, default=8192, help="Poisson grid width (n = m*m)")
     ap.add_argument("--comm", choices=["collective", "p2p", "nooverlap", "deterministic"], default="collective",
                     help="exchange: RCCL collectives with the p allgather overlapped (default), "
                          "point-to-point_cg.c's gather-to-root + send-to-all (p2p), collectives "
                          "without overlap, or the scalars combined in rank order (deterministic)")
-    ap.add_argument("--n", type=int, default=None, help="system size (default 65536 dense, 131072 stream)")
+    ap.add_argument("--n", "--size", dest="n", type=int, default=None,
+                    help="system size (default 65536 dense, 131072 stream)")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-n", type=int, default=None, help="N for the CPU baseline (default: --n)")
     args = ap.parse_args(argv)
