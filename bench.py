@@ -97,12 +97,12 @@ def matvec_bytes(n: int, nloc: int) -> int:
     return 8 * nloc * n + 8 * n + 8 * nloc
 
 
-def pmc_traffic(n: int, nranks: int) -> float | None:
+def pmc_traffic(n: int, nranks: int, suffix: str = "") -> float | None:
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     try:
         with open(path) as f:
             s = json.load(f)
-        key = f"n{n}_g{nranks}"
+        key = f"n{n}_g{nranks}{suffix}"
         return float(s[key]["hbm_bytes_per_matvec"]) if key in s else None
     except (OSError, ValueError, KeyError):
         return None
@@ -183,8 +183,10 @@ def main(argv=None) -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=["dense", "stream", "poisson"], default="dense",
+    ap.add_argument("--workload", choices=["dense", "symmetric", "stream", "poisson"], default="dense",
                     help="dense: configs[2], A resident in HBM (default); "
+                         "symmetric: configs[2]'s system with A kept as its upper triangle (CGX_SYMMETRIC, "
+                         "one GPU, half the matVec bytes); "
                          "stream: configs[3], A kept in pinned host memory and streamed every matVec; "
                          "poisson: configs[4], matrix-free 5-point Poisson on an m x m grid (b=1, x0=0)")
     # --size / --grid: aliases that torch.distributed.run's own parser does not
@@ -209,11 +211,14 @@ def main(argv=None) -> int:
     import conjugate_gradient_amd as cg
     stream = args.workload == "stream"
     poisson = args.workload == "poisson"
+    symmetric = args.workload == "symmetric"
+    if symmetric and world > 1:
+        raise SystemExit("--workload symmetric runs on one GPU")
     m = args.m if poisson else None
     n = m * m if poisson else (args.n or (131072 if stream else 65536))
     if (m if poisson else n) % world:
         raise SystemExit(f"{m if poisson else n} is not divisible by {world}")
-    flags = cg.CGX_F64 | cg.CGX_TIMING | (cg.CGX_HOST_STREAM if stream else 0)
+    flags = cg.CGX_F64 | cg.CGX_TIMING | (cg.CGX_HOST_STREAM if stream else 0) | (cg.CGX_SYMMETRIC if symmetric else 0)
     flags |= {"collective": 0, "p2p": cg.CGX_COMM_P2P, "nooverlap": cg.CGX_NO_OVERLAP,
               "deterministic": cg.CGX_DETERMINISTIC}[args.comm]
     if use_dist:
@@ -224,7 +229,7 @@ def main(argv=None) -> int:
     nloc = solver.info.nrows
     overlap_on = bool(solver.info.flags & cg.CGX_OVERLAP_ACTIVE)
     fused = bool(solver.info.flags & cg.CGX_FUSED_ACTIVE)
-    plan = None if poisson else solver.matvec_plan()
+    plan = None if (poisson or symmetric) else solver.matvec_plan()
 
     if poisson:
         solver.fill(1.0, 0.0)
@@ -271,10 +276,13 @@ def main(argv=None) -> int:
     # dense: SURVEY.md s8(d)
     if poisson:
         bytes_launch = (40 * nloc + 16 * m) if fused else (16 * nloc + 16 * m)
+    elif symmetric:  # the stored tiles + p + y (the per-tile partials are extra traffic, not algorithmic)
+        lda = (n + 127) // 128 * 128
+        bytes_launch = 8 * (lda // 128) * (lda // 128 + 1) // 2 * 128 * 128 + 8 * n + 8 * n
     else:
         bytes_launch = matvec_bytes(n, nloc)
     achieved = bytes_launch / (mv_ms * 1e-3) / 1e9
-    traffic = None if (stream or poisson) else pmc_traffic(n, world)
+    traffic = None if (stream or poisson) else pmc_traffic(n, world, "_symmetric" if symmetric else "")
     peak = H2D_PEAK_GBS if stream else HBM_PEAK_GBS
     iters_per_s = args.steps / elapsed
     out = {
@@ -297,6 +305,8 @@ def main(argv=None) -> int:
                          f"row-block over {world} GPU(s), fixed-count iterations") if stream else
                         (f"configs[4]: matrix-free 5-point Poisson CG, m={m} (N={n}), b=1, x0=0, slabs over {world} "
                          f"GPU(s), halo exchange, fixed-count iterations") if poisson else
+                        (f"configs[{1 if n == 16384 else 2}] system, A stored as its upper triangle (128x128 tiles, "
+                         f"CGX_SYMMETRIC), N={n} dense SPD fp64 CG on 1 GPU, fixed-count iterations") if symmetric else
                         (f"configs[{1 if n == 16384 else 2}]: N={n} dense SPD fp64 CG, row-block over {world} GPU(s), "
                          f"fixed-count iterations"),
             "n": n,
@@ -320,7 +330,8 @@ def main(argv=None) -> int:
             "unit": "GB/s",
             "frac": achieved / peak,
             "traffic": traffic,
-            "kernel": ("k_poisson_xr_f64" if fused else "k_stencil5_f64") if poisson else "k_matvec_f64",
+            "kernel": (("k_poisson_xr_f64" if fused else "k_stencil5_f64") if poisson else
+                       "k_symv_f64 + k_symv_reduce_f64" if symmetric else "k_matvec_f64"),
             "plan": plan,
             "algorithmic_bytes_per_launch": bytes_launch,
         },
@@ -331,7 +342,7 @@ def main(argv=None) -> int:
     }
     if world == 1 and not args.no_cpu and poisson:
         out["cpu_baseline"] = cpu_baseline_poisson(m)
-    elif world == 1 and not args.no_cpu and not stream:
+    elif world == 1 and not args.no_cpu and not stream and not symmetric:
         out["cpu_baseline"] = cpu_baseline(args.cpu_n or n)
         out["cpu_baseline_mt"] = cpu_baseline_mt(args.cpu_n or n)
     print(json.dumps(out), flush=True)

@@ -31,7 +31,7 @@ import subprocess
 import numpy as np
 
 __all__ = [
-    "CGX_F64", "CGX_F32_REF", "CGX_TIMING", "CGX_HOST_STREAM", "CGX_NO_OVERLAP", "CGX_COMM_P2P", "CgxError", "Stats", "Solver", "lib", "build",
+    "CGX_F64", "CGX_F32_REF", "CGX_TIMING", "CGX_HOST_STREAM", "CGX_NO_OVERLAP", "CGX_COMM_P2P", "CGX_SYMMETRIC", "CgxError", "Stats", "Solver", "lib", "build",
     "conjugrad", "matVec", "vecVec", "residual", "update_xr", "update_p", "read_text",
     "count_text", "read_dims", "device_count", "get_unique_id", "DeviceArray",
 ]
@@ -45,6 +45,7 @@ CGX_OVERLAP_ACTIVE = 0x800
 CGX_FUSED_ACTIVE = 0x2000
 CGX_DETERMINISTIC = 0x4000
 CGX_COMM_P2P = 0x1000
+CGX_SYMMETRIC = 0x8000
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libcgx.so")

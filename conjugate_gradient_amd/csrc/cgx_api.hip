@@ -115,6 +115,11 @@ struct Shard {
     // memory: the deciding kernel stores it, the host reads it after an event
     int64_t *h_rec = nullptr, *d_rec = nullptr;
     MatvecPlan plan;
+    // CGX_SYMMETRIC: A = the upper-triangle tiles; per-tile row / column
+    // partials of a matVec; a staging buffer for rows copied from the host
+    char *sym_prow = nullptr, *sym_pcol = nullptr, *sym_stage = nullptr;
+    int64_t sym_stage_rows = 0;
+    int sym_grid = 0;
     hipEvent_t ev_sync = nullptr;  // cross-shard ordering (LOCAL mode)
     std::vector<hipEvent_t> ev_t;  // timing pairs (CGX_TIMING)
     int ev_used = 0;
@@ -205,6 +210,14 @@ int alloc_shard(cgx_ctx *c, Shard &s) {
         }
         for (int q = 0; q < s.ncopy; ++q) HIPT(hipStreamCreateWithFlags(&s.copy[q], hipStreamNonBlocking));
         if (!f32ref(c)) s.tile_plan = plan_matvec_f64(s.dev, s.tile_rows);
+    } else if (c->flags & CGX_SYMMETRIC) {
+        const int64_t ntiles = sym_tiles(c->lda);
+        const size_t tbytes = (size_t)ntiles * 128 * 128 * 8;
+        TRY(dmalloc(&s.A, tbytes));
+        HIPT(hipMemsetAsync(s.A, 0, tbytes, s.stream));  // padding rows / columns stay zero
+        TRY(dmalloc(&s.sym_prow, (size_t)ntiles * 128 * 8));
+        TRY(dmalloc(&s.sym_pcol, (size_t)ntiles * 128 * 8));
+        s.sym_grid = sym_grid(s.dev);
     } else {
         TRY(dmalloc(&s.A, abytes));
         HIPT(hipMemsetAsync(s.A, 0, abytes, s.stream));  // zero padding columns
@@ -254,7 +267,7 @@ int alloc_shard(cgx_ctx *c, Shard &s) {
         s.ev_t.resize(2 * kEvPairs);
         for (auto &e : s.ev_t) HIPT(hipEventCreate(&e));
     }
-    if (!f32ref(c) && c->op == OP_DENSE) s.plan = plan_matvec_f64(s.dev, s.nloc);
+    if (!f32ref(c) && c->op == OP_DENSE && !(c->flags & CGX_SYMMETRIC)) s.plan = plan_matvec_f64(s.dev, s.nloc);
     HIPT(hipStreamSynchronize(s.stream));
     return CGX_OK;
 }
@@ -263,7 +276,8 @@ void free_shard(Shard &s) {
     (void)hipSetDevice(s.dev);
     if (s.stream) (void)hipStreamSynchronize(s.stream);
     if (s.comm) ncclCommDestroy(s.comm);
-    for (char *p : {s.A, s.b, s.x, s.rh ? s.rh : s.r, s.p2, s.Ap, s.pfull, s.xfull, s.scal})
+    for (char *p : {s.A, s.b, s.x, s.rh ? s.rh : s.r, s.p2, s.Ap, s.pfull, s.xfull, s.scal, s.sym_prow, s.sym_pcol,
+                    s.sym_stage})
         if (p) (void)hipFree(p);
     if (s.ws.partials) (void)hipFree(s.ws.partials);
     if (s.ws.tickets) (void)hipFree(s.ws.tickets);
@@ -701,6 +715,13 @@ int launch_matvec(cgx_ctx *c, Shard &s, const char *vec, bool with_dot, int dot_
                           with_dot ? reinterpret_cast<double *>(slot(s, dot_slot)) : nullptr, s.ws, s.stream,
                           gate_of(s, gated)));
     else if (streamed) TRY(matvec_streamed(c, s, vec));
+    else if (c->flags & CGX_SYMMETRIC)
+        HIPT(symv_f64(reinterpret_cast<const double *>(s.A), c->n, c->lda, s.sym_grid,
+                      reinterpret_cast<const double *>(vec), reinterpret_cast<double *>(s.sym_prow),
+                      reinterpret_cast<double *>(s.sym_pcol), reinterpret_cast<double *>(s.Ap),
+                      with_dot ? reinterpret_cast<const double *>(s.pown) : nullptr,
+                      with_dot ? reinterpret_cast<double *>(slot(s, dot_slot)) : nullptr, s.ws, s.stream,
+                      gate_of(s, gated)));
     else TRY(matvec_rows(c, s, s.plan, s.A, 0, s.nloc, vec, with_dot && !f32ref(c), dot_slot, gated));
     if (timing) {
         HIPT(hipEventRecord(s.ev_t[2 * s.ev_used + 1], s.stream));
@@ -1143,6 +1164,8 @@ static int check_op(int op, int64_t n, int64_t m, int parts, int flags) {
             return fail(CGX_ERR_ARG, "the Poisson operator supports CGX_F64 (+CGX_TIMING) only");
         return CGX_OK;
     }
+    if ((flags & CGX_SYMMETRIC) && (parts != 1 || (flags & (CGX_F32_REF | CGX_HOST_STREAM))))
+        return fail(CGX_ERR_ARG, "CGX_SYMMETRIC: fp64 on one GPU only (no CGX_F32_REF / CGX_HOST_STREAM)");
     return check_n(n, parts);
 }
 
@@ -1332,6 +1355,21 @@ int cgx_set_rows(cgx_ctx *c, int64_t row0, int64_t nrows, const void *A_rows, in
                 std::memcpy(dst, static_cast<const char *>(A_rows) + (size_t)(i - row0) * lda_host * es, (size_t)c->n * es);
                 if (c->lda > c->n) std::memset(dst + (size_t)c->n * es, 0, (size_t)(c->lda - c->n) * es);
             }
+        } else if (A_rows && (c->flags & CGX_SYMMETRIC)) {
+            // rows through a staging buffer, then packed into the tiles
+            if (!s.sym_stage) {
+                s.sym_stage_rows = std::max<int64_t>(1, std::min<int64_t>(c->n, (int64_t)(128 << 20) / (c->lda * 8)));
+                HIPT(hipMalloc(&s.sym_stage, (size_t)s.sym_stage_rows * c->lda * 8));
+            }
+            for (int64_t i0 = lo; i0 < hi; i0 += s.sym_stage_rows) {
+                const int64_t k = std::min(s.sym_stage_rows, hi - i0);
+                HIPT(hipMemcpy2DAsync(s.sym_stage, (size_t)c->lda * 8,
+                                      static_cast<const char *>(A_rows) + (size_t)(i0 - row0) * lda_host * 8,
+                                      (size_t)lda_host * 8, (size_t)c->n * 8, (size_t)k, hipMemcpyHostToDevice,
+                                      s.stream));
+                HIPT(sym_pack_f64(reinterpret_cast<const double *>(s.sym_stage), c->lda, i0, k, c->n, c->lda,
+                                  reinterpret_cast<double *>(s.A), s.stream));
+            }
         } else if (A_rows)
             HIPT(hipMemcpy2DAsync(s.A + (size_t)(lo - s.row0) * c->lda * es, (size_t)c->lda * es,
                                   static_cast<const char *>(A_rows) + (size_t)(lo - row0) * lda_host * es,
@@ -1383,6 +1421,9 @@ int cgx_generate_spd(cgx_ctx *c, uint64_t seed) {
                                     hipMemcpyDeviceToHost, s.stream));
             }
             HIPT(hipStreamSynchronize(s.stream));
+        } else if (c->flags & CGX_SYMMETRIC) {
+            HIPT(gen_spd_sym_f64(c->n, c->lda, seed, reinterpret_cast<double *>(s.A), reinterpret_cast<double *>(s.b),
+                                 s.stream));
         } else if (f32ref(c)) {
             HIPT(gen_spd_f32(c->n, c->lda, s.row0, s.nloc, seed, reinterpret_cast<float *>(s.A),
                              reinterpret_cast<float *>(s.b), s.stream));
@@ -1560,7 +1601,8 @@ void *cgx_stream(cgx_ctx *c) { return c ? (void *)c->sh[0].stream : nullptr; }
 
 int cgx_set_matvec_plan(cgx_ctx *c, int rows_per_wave, int chunks_in_flight, int nontemporal, int blocks_per_cu) {
     if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
-    if (f32ref(c) || c->op != OP_DENSE) return fail(CGX_ERR_ARG, "only the fp64 dense matVec has a tunable plan");
+    if (f32ref(c) || c->op != OP_DENSE || (c->flags & CGX_SYMMETRIC))
+        return fail(CGX_ERR_ARG, "only the fp64 row-major dense matVec has a tunable plan");
     const int R = rows_per_wave, U = chunks_in_flight;
     if (R != 1 && R != 2 && R != 4 && R != 8) return fail(CGX_ERR_ARG, "rows_per_wave must be 1, 2, 4 or 8");
     if (U != 2 && U != 4 && U != 8) return fail(CGX_ERR_ARG, "chunks_in_flight must be 2, 4 or 8");

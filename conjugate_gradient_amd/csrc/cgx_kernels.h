@@ -88,6 +88,21 @@ hipError_t poisson_xr_f64(const double *pnh, double *x, double *r, int64_t mloc,
 hipError_t fill_f64(double *p, int64_t n, double v, hipStream_t s);
 hipError_t fill_f32(float *p, int64_t n, float v, hipStream_t s);
 
+// ---- CGX_SYMMETRIC: A as the upper triangle of 128 x 128 tiles ---------------
+// (layout: cgx_kernels.hip).  lda is a multiple of 128; At holds sym_tiles(lda)
+// tiles of 128*128 doubles; prow/pcol sym_tiles(lda)*128 doubles each.
+int64_t sym_tiles(int64_t lda);
+int sym_grid(int device);
+// y = A p (rows [0, n)), *dot_out = pown . y when pown != nullptr
+hipError_t symv_f64(const double *At, int64_t n, int64_t lda, int grid, const double *p, double *prow, double *pcol,
+                    double *y, const double *pown, double *dot_out, const RedWs &ws, hipStream_t s,
+                    const int64_t *gate = nullptr);
+// rows [row0, row0+nrows) of A (row-major, leading dimension ld) into the tiles
+hipError_t sym_pack_f64(const double *rows, int64_t ld, int64_t row0, int64_t nrows, int64_t n, int64_t lda,
+                        double *At, hipStream_t s);
+// the counter-hash SPD system of gen_spd_f64, packed; b for all n rows
+hipError_t gen_spd_sym_f64(int64_t n, int64_t lda, uint64_t seed, double *At, double *b, hipStream_t s);
+
 // ---- fp32, serialConjugate.c operation order ---------------------------------
 hipError_t matvec_ref_f32(const float *A, int64_t lda, int64_t rows, int64_t cols,
                           const float *v, float *out, hipStream_t s);

@@ -87,6 +87,15 @@ extern "C" {
                                     results independent of RCCL's algorithm and
                                     bitwise equal to the multi-shard run with the
                                     same partition */
+#define CGX_SYMMETRIC    0x8000 /* fp64, one GPU: keep only the upper triangle of
+                                   A, in 128 x 128 tiles, and compute A.p from
+                                   it (half the bytes per matVec).  CG requires
+                                   a symmetric A; this mode reads only
+                                   A[i][j] for j >= 128*(i/128) (the lower
+                                   triangle outside the diagonal tiles is never
+                                   read).  Sums run in a different order than
+                                   the row-major kernel: results agree to fp64
+                                   rounding, deterministically. */
 #define CGX_HOST_STREAM  0x200 /* keep A in pinned host memory and stream row
                                   tiles through the GPU every matVec (out-of-HBM
                                   systems; tile size CGX_STREAM_TILE_MB, default
