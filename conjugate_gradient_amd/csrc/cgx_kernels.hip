@@ -2470,8 +2470,8 @@ hipError_t symv_f64(const double *At, int64_t n, int64_t lda, int grid, const do
     if (lda % kSymT || grid <= 0 || ((reinterpret_cast<uintptr_t>(At) | reinterpret_cast<uintptr_t>(p)) & 15))
         return hipErrorInvalidValue;
     const int64_t per = (ntiles + grid - 1) / grid;
-    hipLaunchKernelGGL(env_int("CGX_SYM_NT", 1) ? k_symv_f64<1> : k_symv_f64<0>, dim3(grid), dim3(kSymNT), 0, s, At,
-                       nt, ntiles, per, p, prow, pcol, gate);
+    auto fn = env_int("CGX_SYM_NT", 1) ? k_symv_f64<1> : k_symv_f64<0>;
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(kSymNT), 0, s, At, nt, ntiles, per, p, prow, pcol, gate);
     hipLaunchKernelGGL(k_symv_reduce_f64, dim3(grid_1d(n, 64, kMaxRedBlocks)), dim3(kNT), 0, s, n, nt, per, prow,
                        pcol, y, pown, dot_out, ws.partials, ws.tickets + T_MATVEC, gate);
     return hipGetLastError();
