@@ -117,7 +117,10 @@ __device__ __forceinline__ d2 load_a(const d2 *p) {
 
 template <int POL>
 __device__ __forceinline__ d2 load_a_buf(__amdgpu_buffer_rsrc_t rs, int64_t chunk, int lane) {
-    const u4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, (int)((chunk * 64 + lane) * 16), 0, kBufAux[POL]);
+    // loop-invariant voffset, the chunk in soffset (wave-uniform): no per-step
+    // VGPR address arithmetic, which the register allocator otherwise places
+    // in registers the previous step's loads still write (forcing a wait)
+    const u4 v = __builtin_amdgcn_raw_buffer_load_b128(rs, lane * 16, (int)(chunk * 1024), kBufAux[POL]);
     return __builtin_bit_cast(d2, v);
 }
 
@@ -237,9 +240,15 @@ __device__ __forceinline__ void mv_chunks_pipe(const d2 *const (&arow)[R], const
 // chunks (the host picks the plain kernel otherwise).
 template <int R, int U, int NT>
 __device__ __forceinline__ void mv_flat_load(const double *const (&base)[R], const __amdgpu_buffer_rsrc_t (&rs)[R],
-                                             int lane, const d2 *v2, int64_t c, d2 (&pv)[U], d2 (&av)[R][U]) {
+                                             __amdgpu_buffer_rsrc_t prs, int lane, const d2 *v2, int64_t c,
+                                             d2 (&pv)[U], d2 (&av)[R][U]) {
 #pragma unroll
-    for (int u = 0; u < U; ++u) pv[u] = v2[(c + u) * 64];
+    for (int u = 0; u < U; ++u) {
+        if constexpr (NT >= 2)
+            pv[u] = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(prs, lane * 16, (int)((c + u) * 1024), 0));
+        else
+            pv[u] = v2[(c + u) * 64];
+    }
 #pragma unroll
     for (int r = 0; r < R; ++r)
 #pragma unroll
@@ -261,40 +270,44 @@ __global__ __launch_bounds__(kNT) void k_matvec_f64_flat(
     if (gate && *gate) return;
     const int lane = threadIdx.x & 63;
     const int wid = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-    const int64_t ngroups = (rows + R - 1) / R;
-    const int64_t wstride = (int64_t)gridDim.x * (kNT / 64);
-    const int64_t nchunk = vec_cols >> 7;
-    const int64_t ctail = nchunk << 7;
-    const int64_t ca = cfirst, cb = (cfirst + ccount < nchunk) ? cfirst + ccount : nchunk;
-    const int64_t piece1 = cb - ca;
-    const int64_t S = (piece1 + (cfirst + ccount - cb)) / U;  // steps per row group
+    // group / step / chunk counters are 32-bit (rows, chunks < 2^31): their
+    // compares stay on the scalar unit; 64-bit ones went through VGPRs that
+    // the allocator took from in-flight load destinations (a wait each step)
+    const int ngroups = (int)((rows + R - 1) / R);
+    const int wstride = (int)gridDim.x * (kNT / 64);
+    const int nchunk = (int)(vec_cols >> 7);
+    const int64_t ctail = (int64_t)nchunk << 7;
+    const int ca = (int)cfirst, cb = (cfirst + ccount < nchunk) ? (int)(cfirst + ccount) : nchunk;
+    const int piece1 = cb - ca;
+    const int S = (int)((piece1 + (cfirst + ccount - cb)) / U);  // steps per row group
     const d2 *v2 = reinterpret_cast<const d2 *>(v) + lane;
+    const __amdgpu_buffer_rsrc_t prs = __builtin_amdgcn_make_buffer_rsrc((void *)v, 0, (int)(nchunk * 1024), 0x00020000);
     double dacc = 0.0;
 
     // load cursor (group lg, step ls) and its row bases
-    int64_t lg = (int64_t)blockIdx.x * (kNT / 64) + wid, ls = 0;
+    int lg = (int)blockIdx.x * (kNT / 64) + wid, ls = 0;
     const double *lbase[R];
     __amdgpu_buffer_rsrc_t lrs[R];
-    auto set_rows = [&](int64_t g) {
+    auto set_rows = [&](int g) {
 #pragma unroll
         for (int r = 0; r < R; ++r) {
-            const int64_t row = (g * R + r < rows) ? g * R + r : rows - 1;
-            lbase[r] = A + row * lda;
+            const int row = (g * R + r < (int)rows) ? g * R + r : (int)rows - 1;
+            lbase[r] = A + (int64_t)row * lda;
             if constexpr (NT >= 2)
                 lrs[r] = __builtin_amdgcn_make_buffer_rsrc((void *)lbase[r], 0, (int)(lda * 8), 0x00020000);
         }
     };
-    auto col_of = [&](int64_t s) -> int64_t {
-        const int64_t o = s * U;
+    auto col_of = [&](int s) -> int {
+        const int o = s * U;
         return o < piece1 ? ca + o : o - piece1;
     };
     // compute cursor (group cg, step cs)
-    int64_t cg = lg, cs = 0;
+    int cg = lg, cs = 0;
     d2 acc[R];
 #pragma unroll
     for (int r = 0; r < R; ++r) acc[r] = (d2)(0.0);
     auto finish_group = [&]() {
-        const int64_t r0 = cg * R;
+        const int64_t r0 = (int64_t)cg * R;
         if (tail)
             for (int64_t j = ctail + lane; j < cols; j += 64) {
                 const double vj = v[j];
@@ -321,22 +334,45 @@ __global__ __launch_bounds__(kNT) void k_matvec_f64_flat(
     if (lg < ngroups && S > 0) {
         d2 pa[U], aa[R][U], pb[U], ab[R][U];
         set_rows(lg);
-        mv_flat_load<R, U, NT>(lbase, lrs, lane, v2, col_of(0), pa, aa);
+        mv_flat_load<R, U, NT>(lbase, lrs, prs, lane, v2, col_of(0), pa, aa);
+        // The load cursor stops at the wave's last step, which is then loaded
+        // again (16 KiB per wave, once): every step issues the same loads, so
+        // the compiler's wait counts never assume the next set is absent (a
+        // conditional load made them drain it before each step's FMAs).
+        bool loading = true;
+        auto advance = [&]() {
+            if (loading && ++ls == S) {
+                if (lg + wstride < ngroups) {
+                    ls = 0;
+                    lg += wstride;
+                    set_rows(lg);
+                } else {
+                    ls = S - 1;
+                    loading = false;
+                }
+            }
+        };
         for (;;) {
             // ---- set A is in flight: issue B = next step, then consume A
-            if (++ls == S) { ls = 0; lg += wstride; if (lg < ngroups) set_rows(lg); }
-            bool more = lg < ngroups;
-            if (more) mv_flat_load<R, U, NT>(lbase, lrs, lane, v2, col_of(ls), pb, ab);
+            advance();
+            mv_flat_load<R, U, NT>(lbase, lrs, prs, lane, v2, col_of(ls), pb, ab);
             mv_fma_step<R, U>(pa, aa, acc);
-            if (++cs == S) { finish_group(); cs = 0; cg += wstride; }
-            if (!more) break;
+            if (++cs == S) {
+                finish_group();
+                cs = 0;
+                cg += wstride;
+                if (cg >= ngroups) break;
+            }
             // ---- set B is in flight: issue A = next step, then consume B
-            if (++ls == S) { ls = 0; lg += wstride; if (lg < ngroups) set_rows(lg); }
-            more = lg < ngroups;
-            if (more) mv_flat_load<R, U, NT>(lbase, lrs, lane, v2, col_of(ls), pa, aa);
+            advance();
+            mv_flat_load<R, U, NT>(lbase, lrs, prs, lane, v2, col_of(ls), pa, aa);
             mv_fma_step<R, U>(pb, ab, acc);
-            if (++cs == S) { finish_group(); cs = 0; cg += wstride; }
-            if (!more) break;
+            if (++cs == S) {
+                finish_group();
+                cs = 0;
+                cg += wstride;
+                if (cg >= ngroups) break;
+            }
         }
     } else if (lg < ngroups) {  // no full chunks (vec_cols < 128): tail columns only
         for (; cg < ngroups; cg += wstride) finish_group();
