@@ -26,6 +26,7 @@
 //   GATHER+q: the partial of shard q (ordered combine)
 #include <hip/hip_runtime.h>
 #include <rccl/rccl.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
 
 #include <chrono>
 #include <cmath>
@@ -308,6 +309,15 @@ void free_shard(Shard &s) {
     if (s.stream) (void)hipStreamDestroy(s.stream);
     s = Shard();
 }
+
+// roctx range over an API call (rocprofv3 --marker-trace shows the solve
+// phases on the timeline; a no-op without a tool attached).
+struct Range {
+    explicit Range(const char *name) { roctxRangePushA(name); }
+    ~Range() { roctxRangePop(); }
+    Range(const Range &) = delete;
+    Range &operator=(const Range &) = delete;
+};
 
 int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
 
@@ -1338,6 +1348,7 @@ int cgx_get_info(const cgx_ctx *c, cgx_info *info) {
 
 int cgx_set_rows(cgx_ctx *c, int64_t row0, int64_t nrows, const void *A_rows, int64_t lda_host,
                  const void *b_rows, const void *x_rows) {
+    const Range range_("cgx_set_rows");
     if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
     if (row0 < 0 || nrows < 0 || row0 + nrows > c->n)
         return fail(CGX_ERR_SHAPE, "rows [%lld, %lld) outside [0, %lld)", (long long)row0,
@@ -1401,6 +1412,7 @@ int cgx_set_system(cgx_ctx *c, const void *A, const void *b, const void *x0) {
 }
 
 int cgx_generate_spd(cgx_ctx *c, uint64_t seed) {
+    const Range range_("cgx_generate_spd");
     if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
     if (c->op == OP_POISSON) return fail(CGX_ERR_ARG, "the Poisson operator has no matrix to generate (use cgx_fill)");
     for (auto &s : c->sh) {
@@ -1445,6 +1457,7 @@ int cgx_set_x(cgx_ctx *c, const void *x) {
 }
 
 int cgx_get_x(cgx_ctx *c, void *x) {
+    const Range range_("cgx_get_x");
     if (!c || !x) return fail(CGX_ERR_ARG, "NULL argument");
     const size_t es = (size_t)c->es;
     if (c->mode == M_RCCL && c->nranks > 1) {
@@ -1463,6 +1476,7 @@ int cgx_get_x(cgx_ctx *c, void *x) {
 }
 
 int cgx_solve_begin(cgx_ctx *c) {
+    const Range range_("cgx_solve_begin");
     if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
     return do_begin(c);
 }
@@ -1528,6 +1542,7 @@ static int iterate_gated(cgx_ctx *c, int64_t count, double eps, int64_t *done, i
 }
 
 int cgx_iterate(cgx_ctx *c, int64_t count, double eps, int64_t *done, int *converged) {
+    const Range range_("cgx_iterate");
     if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
     if (c->state == ST_IDLE) return fail(CGX_ERR_STATE, "cgx_iterate before cgx_solve_begin");
     const char *gv = std::getenv("CGX_GATED");
@@ -1549,6 +1564,7 @@ int cgx_iterate(cgx_ctx *c, int64_t count, double eps, int64_t *done, int *conve
 }
 
 int cgx_solve(cgx_ctx *c, void *x_inout, double eps, int64_t max_iter, cgx_stats *st) {
+    const Range range_("cgx_solve");
     if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
     if (x_inout) TRY(cgx_set_x(c, x_inout));
     TRY(sync_all(c));
@@ -1627,6 +1643,7 @@ int cgx_get_matvec_plan(cgx_ctx *c, int *rows_per_wave, int *chunks_in_flight, i
 }
 
 int cgx_residual_norm(cgx_ctx *c, double *rnorm, double *bnorm) {
+    const Range range_("cgx_residual_norm");
     if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
     // ||b - A x|| with the current x: allgather x, matVec, residual, two dots.
     TRY(settle_halo(c));
