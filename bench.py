@@ -223,7 +223,12 @@ def main(argv=None) -> int:
               "deterministic": cg.CGX_DETERMINISTIC}[args.comm]
     if use_dist:
         uid = bcast_bytes(dist, cg.get_unique_id() if rank == 0 else None)
-        solver = cg.Solver(n, rank=rank, nranks=world, unique_id=uid, device=local_rank, flags=flags, poisson_m=m)
+        # one GPU per process: LOCAL_RANK indexes the visible devices; if the
+        # launcher already narrowed the visibility per rank (one device seen),
+        # that device is the rank's
+        ndev = max(1, cg.device_count())
+        solver = cg.Solver(n, rank=rank, nranks=world, unique_id=uid, device=local_rank % ndev, flags=flags,
+                           poisson_m=m)
     else:
         solver = cg.Solver(n, device=0, flags=flags, poisson_m=m)
     nloc = solver.info.nrows
