@@ -88,6 +88,7 @@ constexpr int S_XNZ = 134;  // rank mode: count of ranks whose x0 is not all zer
 constexpr int S_KDONE = 132, S_RRFINAL = 133;  // device-side convergence: k+1 at the break, r.r there
 constexpr int kLookRing = 8;                    // pinned slots for the host's lagged convergence checks
 inline int ring(int64_t j) { return (int)(j & 3); }
+constexpr int kGraphIters = 4;  // a multiple of the ring period (and of the Poisson slab alternation)
 
 enum Mode { M_SINGLE = 0, M_LOCAL = 1, M_RCCL = 2 };
 enum Op { OP_DENSE = 0, OP_POISSON = 1 };
@@ -164,6 +165,10 @@ struct cgx_ctx {
     bool fused = false;    // Poisson: two-kernel fused iteration (k_poisson_p + k_poisson_xr)
     bool halo_overlap = false;  // fused Poisson, several slabs: r's halo exchange overlaps k_poisson_p
     bool halo_pending = false;  // an overlapped r halo exchange is in flight on the comm streams
+    // fixed-count iterations replayed from a hipGraph (one GPU): kGraphIters
+    // iterations captured once, the period of the scalar rings
+    hipGraphExec_t graph = nullptr;
+    bool graph_failed = false;
 };
 
 namespace {
@@ -1326,6 +1331,7 @@ int cgx_fill(cgx_ctx *c, double b_value, double x_value) {
 
 int cgx_destroy(cgx_ctx *ctx) {
     if (!ctx) return CGX_OK;
+    if (ctx->graph) (void)hipGraphExecDestroy(ctx->graph);
     for (auto &s : ctx->sh) free_shard(s);
     delete ctx;
     return CGX_OK;
@@ -1481,6 +1487,56 @@ int cgx_solve_begin(cgx_ctx *c) {
     return do_begin(c);
 }
 
+// Fixed-count iterations from a hipGraph: one GPU (no exchange, no host
+// reads inside an iteration), no per-launch timing events.  kGraphIters
+// iterations are captured once per context, from an iteration k >= 1 that
+// is a multiple of kGraphIters: every launch argument then repeats with that
+// period (scalar ring slots, Poisson slab parity; k == 0 alone differs), so
+// the same graph replays at k, k + 4, ...  The kernels and their order are
+// the stream path's, so the results are bitwise the same (tested).  Opt-in
+// (CGX_GRAPH=1): replays measured 1-5 % SLOWER than stream launches at
+// N = 512-16384 and on Poisson grids (profiles/r01_graph_ab.jsonl; the
+// launches are already queued ahead of a GPU-bound loop).  A capture that
+// fails falls back to stream launches.
+static bool graph_ok(const cgx_ctx *c) {
+    const char *e = std::getenv("CGX_GRAPH");
+    if (!(e && *e == '1')) return false;
+    return c->mode == M_SINGLE && !c->graph_failed && !(c->flags & (CGX_TIMING | CGX_HOST_STREAM));
+}
+
+static int graph_block(cgx_ctx *c, bool *ran) {
+    *ran = false;
+    Shard &s = c->sh[0];
+    TRY(set_dev(s));
+    if (!c->graph) {
+        const int64_t k0 = c->k, t0 = c->total_iters;
+        HIPT(hipStreamBeginCapture(s.stream, hipStreamCaptureModeThreadLocal));
+        int rc = CGX_OK;
+        for (int i = 0; i < kGraphIters && rc == CGX_OK; ++i) {
+            int stop = 0;
+            rc = do_iteration(c, -1.0, &stop);
+        }
+        hipGraph_t g = nullptr;
+        const hipError_t ec = hipStreamEndCapture(s.stream, &g);
+        c->k = k0;
+        c->total_iters = t0;
+        if (rc == CGX_OK && ec == hipSuccess && g && hipGraphInstantiate(&c->graph, g, nullptr, nullptr, 0) == hipSuccess) {
+            (void)hipGraphDestroy(g);
+        } else {
+            if (g) (void)hipGraphDestroy(g);
+            (void)hipGetLastError();
+            c->graph = nullptr;
+            c->graph_failed = true;  // stream launches from now on
+            return CGX_OK;
+        }
+    }
+    HIPT(hipGraphLaunch(c->graph, s.stream));
+    c->k += kGraphIters;
+    c->total_iters += kGraphIters;
+    *ran = true;
+    return CGX_OK;
+}
+
 // Convergence-tested iterations without a host round trip per iteration:
 // the update kernel decides sqrt(r.r) < eps on the device and records k+1;
 // queued later iterations skip themselves.  The host keeps `look` iterations
@@ -1550,13 +1606,20 @@ int cgx_iterate(cgx_ctx *c, int64_t count, double eps, int64_t *done, int *conve
     if (c->state == ST_BEGUN && count > 0 && eps >= 0.0 && !f32ref(c) && !(c->flags & CGX_HOST_STREAM) && gate_ok)
         return iterate_gated(c, count, eps, done, converged);
     int64_t did = 0;
-    for (; did < count && c->state == ST_BEGUN; ++did) {
+    const bool use_graph = eps < 0.0 && graph_ok(c);
+    while (did < count && c->state == ST_BEGUN) {
+        if (use_graph && c->k >= kGraphIters && c->k % kGraphIters == 0 && count - did >= kGraphIters) {
+            bool ran = false;
+            TRY(graph_block(c, &ran));
+            if (ran) {
+                did += kGraphIters;
+                continue;
+            }
+        }
         int stop = 0;
         TRY(do_iteration(c, eps, &stop));
-        if (stop) {
-            ++did;
-            break;
-        }
+        ++did;
+        if (stop) break;
     }
     if (done) *done = did;
     if (converged) *converged = c->converged;
@@ -1628,6 +1691,10 @@ int cgx_set_matvec_plan(cgx_ctx *c, int rows_per_wave, int chunks_in_flight, int
         TRY(set_dev(s));
         MatvecPlan pl = plan_matvec_f64(s.dev, s.nloc, R, U, nontemporal, blocks_per_cu);
         s.plan = pl;
+    }
+    if (c->graph) {  // the captured launches carry the old plan
+        HIPT(hipGraphExecDestroy(c->graph));
+        c->graph = nullptr;
     }
     return CGX_OK;
 }

@@ -557,3 +557,38 @@ def test_device_gated_convergence_matches_host_checked(monkeypatch, shards):
         assert rr == ref[3] and np.sqrt(rr) < 1e-10
     xo, so = oracle.cg_f64(A, b, np.zeros(2048), eps=1e-10)
     assert ref[1] == so.iterations and rel(ref[0], xo) <= TOL
+
+
+@pytest.mark.parametrize("kind", ["dense", "f32ref", "poisson"])
+def test_graph_replay_bitwise_equals_stream_launches(monkeypatch, kind):
+    """Fixed-count iterations replayed from the hipGraph (CGX_GRAPH=1, one GPU)
+    give the stream path's x bit for bit, for counts that start and end off
+    the graph's 4-iteration period."""
+    def run(graph, counts):
+        monkeypatch.setenv("CGX_GRAPH", "1" if graph else "0")
+        if kind == "poisson":
+            s = cg.Solver(None, poisson_m=130)
+            s.fill(1.0, 0.0)
+        else:
+            s = cg.Solver(1000, flags=cg.CGX_F32_REF if kind == "f32ref" else cg.CGX_F64)
+            s.generate_spd(7)
+        with s:
+            s.begin()
+            for c in counts:
+                s.iterate(c)
+            return s.get_x()
+    counts = [3, 11, 4, 9]
+    xg, xs = run(True, counts), run(False, counts)
+    assert np.array_equal(xg.view(np.uint8), xs.view(np.uint8))
+
+
+def test_poisson_fixed_count_is_deterministic():
+    """The same fixed-count Poisson solve twice on one context: x bit for bit
+    (fixed-order reductions; x0 reset, since begin() starts from the current x)."""
+    xs = []
+    with cg.Solver(None, poisson_m=520) as s:
+        for _ in range(2):
+            s.fill(1.0, 0.0)
+            x, _ = s.solve(None, eps=-1.0, max_iter=25)
+            xs.append(x)
+    assert np.array_equal(xs[0].view(np.uint8), xs[1].view(np.uint8))
