@@ -183,11 +183,13 @@ def main(argv=None) -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
-    ap.add_argument("--workload", choices=["dense", "symmetric", "stream", "poisson"], default="dense",
+    ap.add_argument("--workload", choices=["dense", "symmetric", "stream", "stream_symmetric", "poisson"],
+                    default="dense",
                     help="dense: configs[2], A resident in HBM (default); "
                          "symmetric: configs[2]'s system with A kept as its upper triangle (CGX_SYMMETRIC, "
                          "one GPU, half the matVec bytes); "
                          "stream: configs[3], A kept in pinned host memory and streamed every matVec; "
+                         "stream_symmetric: configs[3] with only the upper-triangle tiles streamed; "
                          "poisson: configs[4], matrix-free 5-point Poisson on an m x m grid (b=1, x0=0)")
     # --size / --grid: aliases that torch.distributed.run's own parser does not
     # mistake for abbreviations of its options (--n, --m are ambiguous there)
@@ -209,11 +211,11 @@ def main(argv=None) -> int:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
 
     import conjugate_gradient_amd as cg
-    stream = args.workload == "stream"
+    stream = args.workload in ("stream", "stream_symmetric")
     poisson = args.workload == "poisson"
-    symmetric = args.workload == "symmetric"
+    symmetric = args.workload in ("symmetric", "stream_symmetric")
     if symmetric and world > 1:
-        raise SystemExit("--workload symmetric runs on one GPU")
+        raise SystemExit(f"--workload {args.workload} runs on one GPU")
     m = args.m if poisson else None
     n = m * m if poisson else (args.n or (131072 if stream else 65536))
     if (m if poisson else n) % world:
@@ -306,8 +308,9 @@ def main(argv=None) -> int:
                  f"synthetic: generateSPDmatrix.m-style dense SPD (0.5(R+R')+nI, counter hash, seed {SEED}) "
                  f"generated on device; x0 = 0"),
         "config": {
-            "workload": (f"configs[3]: N={n} dense SPD fp64 CG, A streamed from pinned host memory every matVec, "
-                         f"row-block over {world} GPU(s), fixed-count iterations") if stream else
+            "workload": (f"configs[3]: N={n} dense SPD fp64 CG, A streamed from pinned host memory every matVec"
+                         + (" as its upper-triangle tiles (CGX_SYMMETRIC)" if symmetric else "")
+                         + f", row-block over {world} GPU(s), fixed-count iterations") if stream else
                         (f"configs[4]: matrix-free 5-point Poisson CG, m={m} (N={n}), b=1, x0=0, slabs over {world} "
                          f"GPU(s), halo exchange, fixed-count iterations") if poisson else
                         (f"configs[{1 if n == 16384 else 2}] system, A stored as its upper triangle (128x128 tiles, "
@@ -336,6 +339,7 @@ def main(argv=None) -> int:
             "frac": achieved / peak,
             "traffic": traffic,
             "kernel": (("k_poisson_xr_f64" if fused else "k_stencil5_f64") if poisson else
+                       "H2D copies + k_symv_f64 per chunk + k_symv_reduce_f64" if (symmetric and stream) else
                        "k_symv_f64 + k_symv_reduce_f64" if symmetric else "k_matvec_f64"),
             "plan": plan,
             "algorithmic_bytes_per_launch": bytes_launch,

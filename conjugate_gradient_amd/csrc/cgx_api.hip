@@ -197,6 +197,28 @@ int alloc_shard(cgx_ctx *c, Shard &s) {
     };
     if (c->op == OP_POISSON) {
         // matrix-free: no A
+    } else if ((c->flags & CGX_SYMMETRIC) && (c->flags & CGX_HOST_STREAM)) {
+        // the upper-triangle tiles in pinned host memory, streamed in chunks of
+        // whole tiles through kStreamBufs device buffers (tile_rows = tiles per chunk)
+        const int64_t ntiles = sym_tiles(c->lda), tb = 128 * 128 * 8;
+        hipError_t e = hipHostMalloc(reinterpret_cast<void **>(&s.A_host), (size_t)ntiles * tb, hipHostMallocDefault);
+        if (e != hipSuccess)
+            return fail(CGX_ERR_NOMEM, "hipHostMalloc(%lld bytes) for streamed tiles: %s", (long long)(ntiles * tb),
+                        hipGetErrorString(e));
+        const char *tmb = std::getenv("CGX_STREAM_TILE_MB");
+        const int64_t chunk_bytes = (int64_t)((tmb && *tmb) ? std::atoll(tmb) : 256) << 20;
+        s.tile_rows = std::max<int64_t>(1, std::min<int64_t>(ntiles, chunk_bytes / tb));
+        const char *nc = std::getenv("CGX_STREAM_COPIES");
+        s.ncopy = std::max(1, std::min(kMaxCopyStreams, (nc && *nc) ? std::atoi(nc) : 2));
+        for (int b = 0; b < kStreamBufs; ++b) {
+            TRY(dmalloc(&s.tile[b], (size_t)s.tile_rows * tb));
+            HIPT(hipEventCreateWithFlags(&s.ev_free[b], hipEventDisableTiming));
+            for (int q = 0; q < s.ncopy; ++q) HIPT(hipEventCreateWithFlags(&s.ev_loaded[b][q], hipEventDisableTiming));
+        }
+        for (int q = 0; q < s.ncopy; ++q) HIPT(hipStreamCreateWithFlags(&s.copy[q], hipStreamNonBlocking));
+        TRY(dmalloc(&s.sym_prow, (size_t)ntiles * 128 * 8));
+        TRY(dmalloc(&s.sym_pcol, (size_t)ntiles * 128 * 8));
+        s.sym_grid = sym_grid(s.dev);
     } else if (c->flags & CGX_HOST_STREAM) {
         // A in pinned host memory, kStreamBufs device tiles of ~CGX_STREAM_TILE_MB.
         hipError_t e = hipHostMalloc(reinterpret_cast<void **>(&s.A_host), abytes ? abytes : 16, hipHostMallocDefault);
@@ -711,6 +733,40 @@ int matvec_streamed(cgx_ctx *c, Shard &s, const char *vec) {
     return CGX_OK;
 }
 
+// CGX_SYMMETRIC | CGX_HOST_STREAM: the upper-triangle tiles stream from
+// pinned host memory in chunks (the same buffer rotation and copy streams as
+// matvec_streamed); each chunk's k_symv_f64 writes per-tile row and column
+// partials, and one reduce (with the fused p.Ap) follows the last chunk.
+int matvec_sym_streamed(cgx_ctx *c, Shard &s, const char *vec, bool with_dot, int dot_slot, const int64_t *gate) {
+    const int64_t ntiles = sym_tiles(c->lda), tb = 128 * 128 * 8;
+    const double *p = reinterpret_cast<const double *>(vec);
+    for (int64_t q0 = 0; q0 < ntiles; q0 += s.tile_rows) {
+        const int64_t cnt = std::min(s.tile_rows, ntiles - q0);
+        const int b = s.next_buf;
+        s.next_buf = (s.next_buf + 1) % kStreamBufs;
+        const int64_t bytes = cnt * tb;
+        const char *src = s.A_host + (size_t)q0 * tb;
+        const int64_t part = (bytes / s.ncopy + 4095) & ~int64_t(4095);
+        for (int q = 0; q < s.ncopy; ++q) {
+            const int64_t lo = std::min<int64_t>(bytes, q * part), hi = std::min<int64_t>(bytes, lo + part);
+            if (s.buf_used[b]) HIPT(hipStreamWaitEvent(s.copy[q], s.ev_free[b], 0));
+            if (hi > lo) HIPT(hipMemcpyAsync(s.tile[b] + lo, src + lo, hi - lo, hipMemcpyHostToDevice, s.copy[q]));
+            HIPT(hipEventRecord(s.ev_loaded[b][q], s.copy[q]));
+            HIPT(hipStreamWaitEvent(s.stream, s.ev_loaded[b][q], 0));
+        }
+        HIPT(symv_tiles_f64(reinterpret_cast<const double *>(s.tile[b]), q0, cnt, c->lda, s.sym_grid, true, p,
+                            reinterpret_cast<double *>(s.sym_prow), reinterpret_cast<double *>(s.sym_pcol), s.stream,
+                            gate));
+        HIPT(hipEventRecord(s.ev_free[b], s.stream));
+        s.buf_used[b] = true;
+    }
+    HIPT(symv_reduce_f64(c->n, c->lda, 1, reinterpret_cast<const double *>(s.sym_prow),
+                         reinterpret_cast<const double *>(s.sym_pcol), reinterpret_cast<double *>(s.Ap),
+                         with_dot ? reinterpret_cast<const double *>(s.pown) : nullptr,
+                         with_dot ? reinterpret_cast<double *>(slot(s, dot_slot)) : nullptr, s.ws, s.stream, gate));
+    return CGX_OK;
+}
+
 // The host-mapped convergence record: written by shard 0's deciding kernel only.
 inline int64_t *rec_of(const cgx_ctx *c, const Shard &s, bool gated) {
     return (gated && &s == &c->sh[0]) ? s.d_rec : nullptr;
@@ -729,6 +785,8 @@ int launch_matvec(cgx_ctx *c, Shard &s, const char *vec, bool with_dot, int dot_
         HIPT(stencil5_f64(reinterpret_cast<const double *>(vec), s.nloc / c->m, c->m, reinterpret_cast<double *>(s.Ap),
                           with_dot ? reinterpret_cast<double *>(slot(s, dot_slot)) : nullptr, s.ws, s.stream,
                           gate_of(s, gated)));
+    else if (streamed && (c->flags & CGX_SYMMETRIC))
+        TRY(matvec_sym_streamed(c, s, vec, with_dot, dot_slot, gate_of(s, gated)));
     else if (streamed) TRY(matvec_streamed(c, s, vec));
     else if (c->flags & CGX_SYMMETRIC)
         HIPT(symv_f64(reinterpret_cast<const double *>(s.A), c->n, c->lda, s.sym_grid,
@@ -742,7 +800,7 @@ int launch_matvec(cgx_ctx *c, Shard &s, const char *vec, bool with_dot, int dot_
         HIPT(hipEventRecord(s.ev_t[2 * s.ev_used + 1], s.stream));
         s.ev_used++;
     }
-    if (with_dot && (f32ref(c) || streamed)) {
+    if (with_dot && (f32ref(c) || (streamed && !(c->flags & CGX_SYMMETRIC)))) {
         if (f32ref(c))  // vecVec(p, Ap) sequential (serialConjugate.c:219)
             HIPT(dot_ref_f32(s.nloc, reinterpret_cast<const float *>(s.pown),
                              reinterpret_cast<const float *>(s.Ap), reinterpret_cast<float *>(slot(s, dot_slot)),
@@ -1179,8 +1237,8 @@ static int check_op(int op, int64_t n, int64_t m, int parts, int flags) {
             return fail(CGX_ERR_ARG, "the Poisson operator supports CGX_F64 (+CGX_TIMING) only");
         return CGX_OK;
     }
-    if ((flags & CGX_SYMMETRIC) && (parts != 1 || (flags & (CGX_F32_REF | CGX_HOST_STREAM))))
-        return fail(CGX_ERR_ARG, "CGX_SYMMETRIC: fp64 on one GPU only (no CGX_F32_REF / CGX_HOST_STREAM)");
+    if ((flags & CGX_SYMMETRIC) && (parts != 1 || (flags & CGX_F32_REF)))
+        return fail(CGX_ERR_ARG, "CGX_SYMMETRIC: fp64 on one GPU only (no CGX_F32_REF)");
     return check_n(n, parts);
 }
 
@@ -1366,7 +1424,19 @@ int cgx_set_rows(cgx_ctx *c, int64_t row0, int64_t nrows, const void *A_rows, in
         const int64_t lo = std::max(row0, s.row0), hi = std::min(row0 + nrows, s.row0 + s.nloc);
         if (hi <= lo) continue;
         TRY(set_dev(s));
-        if (A_rows && s.A_host) {
+        if (A_rows && s.A_host && (c->flags & CGX_SYMMETRIC)) {
+            // pack on the host: row i supplies columns 128*(i/128) .. lda-1 of its tile row
+            const int64_t nt = c->lda / 128;
+            double *At = reinterpret_cast<double *>(s.A_host);
+            for (int64_t i = lo; i < hi; ++i) {
+                const double *row = static_cast<const double *>(A_rows) + (size_t)(i - row0) * lda_host;
+                const int64_t I = i / 128;
+                const int r = (int)(i % 128);
+                for (int64_t j = I * 128; j < c->lda; ++j)
+                    At[(sym_off_h(I, nt) + j / 128 - I) * 128 * 128 + sym_pos_h(r, (int)(j % 128))] =
+                        j < c->n ? row[j] : 0.0;
+            }
+        } else if (A_rows && s.A_host) {
             for (int64_t i = lo; i < hi; ++i) {
                 char *dst = s.A_host + (size_t)(i - s.row0) * c->lda * es;
                 std::memcpy(dst, static_cast<const char *>(A_rows) + (size_t)(i - row0) * lda_host * es, (size_t)c->n * es);
@@ -1423,7 +1493,19 @@ int cgx_generate_spd(cgx_ctx *c, uint64_t seed) {
     if (c->op == OP_POISSON) return fail(CGX_ERR_ARG, "the Poisson operator has no matrix to generate (use cgx_fill)");
     for (auto &s : c->sh) {
         TRY(set_dev(s));
-        if (s.A_host) {
+        if (s.A_host && (c->flags & CGX_SYMMETRIC)) {
+            // the packed tiles chunk by chunk on the device, then to the host copy
+            const int64_t ntiles = sym_tiles(c->lda), tb = 128 * 128 * 8;
+            for (int64_t q0 = 0; q0 < ntiles; q0 += s.tile_rows) {
+                const int64_t cnt = std::min(s.tile_rows, ntiles - q0);
+                HIPT(gen_spd_sym_tiles_f64(c->n, c->lda, seed, q0, cnt, reinterpret_cast<double *>(s.tile[0]),
+                                           s.stream));
+                HIPT(hipMemcpyAsync(s.A_host + (size_t)q0 * tb, s.tile[0], (size_t)cnt * tb, hipMemcpyDeviceToHost,
+                                    s.stream));
+            }
+            HIPT(gen_b_f64(c->n, seed, reinterpret_cast<double *>(s.b), s.stream));
+            HIPT(hipStreamSynchronize(s.stream));
+        } else if (s.A_host) {
             // Generate each tile on the device and move it to the host copy of A;
             // b is generated for the whole block first (rows are independent).
             const int64_t row_bytes = c->lda * (int64_t)c->es;

@@ -102,6 +102,23 @@ hipError_t sym_pack_f64(const double *rows, int64_t ld, int64_t row0, int64_t nr
                         double *At, hipStream_t s);
 // the counter-hash SPD system of gen_spd_f64, packed; b for all n rows
 hipError_t gen_spd_sym_f64(int64_t n, int64_t lda, uint64_t seed, double *At, double *b, hipStream_t s);
+// Streamed pieces (CGX_SYMMETRIC | CGX_HOST_STREAM): tiles [q_base, q_base+count)
+// held in At (At[0] = tile q_base).  tile_runs: row partials per tile (then
+// reduce with per = 1).
+hipError_t gen_spd_sym_tiles_f64(int64_t n, int64_t lda, uint64_t seed, int64_t q_base, int64_t count, double *At,
+                                 hipStream_t s);
+hipError_t gen_b_f64(int64_t n, uint64_t seed, double *b, hipStream_t s);
+hipError_t symv_tiles_f64(const double *At, int64_t q_base, int64_t count, int64_t lda, int grid, bool tile_runs,
+                          const double *p, double *prow, double *pcol, hipStream_t s, const int64_t *gate = nullptr);
+hipError_t symv_reduce_f64(int64_t n, int64_t lda, int64_t per, const double *prow, const double *pcol, double *y,
+                           const double *pown, double *dot_out, const RedWs &ws, hipStream_t s,
+                           const int64_t *gate = nullptr);
+// host copies of the layout helpers (tile index, element offset in a tile)
+inline int64_t sym_off_h(int64_t I, int64_t nt) { return I * nt - I * (I - 1) / 2; }
+inline int64_t sym_pos_h(int r, int c) {  // kSymNT = 512: (8 tr + rr, 4 tc + 2 cc + e)
+    const int t = (r / 8) * 32 + (c >> 2), k = (r % 8) * 2 + ((c >> 1) & 1);
+    return ((int64_t)k * 512 + t) * 2 + (c & 1);
+}
 
 // ---- fp32, serialConjugate.c operation order ---------------------------------
 hipError_t matvec_ref_f32(const float *A, int64_t lda, int64_t rows, int64_t cols,

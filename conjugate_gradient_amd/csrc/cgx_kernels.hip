@@ -1803,6 +1803,7 @@ constexpr int kSymK = 2 * kSymRPT;                      // d2 loads per thread p
 constexpr int kSymTR = kSymT / kSymRPT;                 // thread rows per tile (32)
 constexpr int64_t kSymTileD2 = kSymT * kSymT / 2;
 static_assert((kSymRPT == 8 || kSymRPT == 4) && kSymNT / kSymTR == 32, "row reduction: 8 or 4 rows x 32 lanes");
+static_assert(kSymNT == 512 && kSymRPT == 8, "sym_pos_h (cgx_kernels.h) assumes 512 threads, 8 rows per thread");
 
 __host__ __device__ __forceinline__ int64_t sym_off(int64_t I, int64_t nt) { return I * nt - I * (I - 1) / 2; }
 
@@ -1834,11 +1835,12 @@ struct SymSlot {
 // registers are recomputed per tile -- recomputed ones landed in registers
 // the slot loads had just written, and the compiler's wait for them drained
 // the loads in flight at the top of every iteration.
+// qa: the tile's index in At (At may hold a range of tiles starting at q_base).
 template <int NTL>
-__device__ __forceinline__ void sym_load(SymSlot &S, const double *At, __amdgpu_buffer_rsrc_t prs, int64_t q,
+__device__ __forceinline__ void sym_load(SymSlot &S, const double *At, __amdgpu_buffer_rsrc_t prs, int64_t qa,
                                          int64_t I, int64_t J, int t, int tr, int tc) {
     const __amdgpu_buffer_rsrc_t trs =
-        __builtin_amdgcn_make_buffer_rsrc((void *)(At + q * (int64_t)kSymT * kSymT), 0, kSymT * kSymT * 8, 0x00020000);
+        __builtin_amdgcn_make_buffer_rsrc((void *)(At + qa * (int64_t)kSymT * kSymT), 0, kSymT * kSymT * 8, 0x00020000);
 #pragma unroll
     for (int k = 0; k < kSymK; ++k)
         S.a[k] = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(trs, t * 16, k * kSymNT * 16,
@@ -1937,15 +1939,19 @@ __device__ __forceinline__ void sym_tile(const SymSlot &S, int64_t q, double (*c
 // slot in (the wait lands at the copy) and against __syncthreads(): all
 // within 1 % (tools/sym_ab.py).
 template <int NTL>
-__global__ __launch_bounds__(kSymNT) void k_symv_f64(const double *__restrict__ At, int64_t nt, int64_t ntiles,
-                                                     int64_t per, const double *__restrict__ p,
-                                                     double *__restrict__ prow, double *__restrict__ pcol,
-                                                     const int64_t *gate) {
+// Tiles [q_base, q_base + count) of the triangle, At holding exactly those
+// (a streamed chunk) or all of them (q_base = 0).  tile_runs: every tile is
+// its own run (its row partials written per tile): chunk boundaries then do
+// not matter to the reduce, which is told per = 1.
+__global__ __launch_bounds__(kSymNT) void k_symv_f64(const double *__restrict__ At, int64_t nt, int64_t q_base,
+                                                     int64_t count, int64_t per, int tile_runs,
+                                                     const double *__restrict__ p, double *__restrict__ prow,
+                                                     double *__restrict__ pcol, const int64_t *gate) {
     if (gate && *gate) return;
     __shared__ double cs[2][kSymTR][kSymT];
     const int t = threadIdx.x, tr = t >> 5, tc = t & 31;
-    const int64_t q0 = (int64_t)blockIdx.x * per;
-    const int64_t q1 = (q0 + per < ntiles) ? q0 + per : ntiles;
+    const int64_t q0 = q_base + (int64_t)blockIdx.x * per;
+    const int64_t q1 = (q0 + per < q_base + count) ? q0 + per : q_base + count;
     if (q0 >= q1) return;
     int64_t Ic, Jc;  // tile q
     sym_tile_ij(q0, nt, Ic, Jc);
@@ -1955,7 +1961,7 @@ __global__ __launch_bounds__(kSymNT) void k_symv_f64(const double *__restrict__ 
     double racc = 0.0;
     int64_t qrun = q0;
     SymSlot S0, S1;
-    sym_load<NTL>(S0, At, prs, q0, Ic, Jc, t, tr, tc);
+    sym_load<NTL>(S0, At, prs, q0 - q_base, Ic, Jc, t, tr, tc);
     // Every load is issued unconditionally (past the range end a slot
     // reloads the last tile): with a conditional load block the compiler's
     // wait counts at the merge assume no newer loads and drain the next
@@ -1964,16 +1970,18 @@ __global__ __launch_bounds__(kSymNT) void k_symv_f64(const double *__restrict__ 
         int64_t I1 = Ic, J1 = Jc;
         sym_next(I1, J1, nt);
         const bool va = q + 1 < q1;
-        sym_load<NTL>(S1, At, prs, va ? q + 1 : q, va ? I1 : Ic, va ? J1 : Jc, t, tr, tc);
+        sym_load<NTL>(S1, At, prs, (va ? q + 1 : q) - q_base, va ? I1 : Ic, va ? J1 : Jc, t, tr, tc);
         __builtin_amdgcn_sched_barrier(0);  // the loads go out before this tile's arithmetic
-        sym_tile(S0, q, cs, buf, prow, pcol, t, tr, tc, racc, qrun, !va || I1 != Ic);
+        if (tile_runs) qrun = q;
+        sym_tile(S0, q, cs, buf, prow, pcol, t, tr, tc, racc, qrun, tile_runs || !va || I1 != Ic);
         if (!va) break;
         int64_t I2 = I1, J2 = J1;
         sym_next(I2, J2, nt);
         const bool vb = q + 2 < q1;
-        sym_load<NTL>(S0, At, prs, vb ? q + 2 : q + 1, vb ? I2 : I1, vb ? J2 : J1, t, tr, tc);
+        sym_load<NTL>(S0, At, prs, (vb ? q + 2 : q + 1) - q_base, vb ? I2 : I1, vb ? J2 : J1, t, tr, tc);
         __builtin_amdgcn_sched_barrier(0);
-        sym_tile(S1, q + 1, cs, buf, prow, pcol, t, tr, tc, racc, qrun, !vb || I2 != I1);
+        if (tile_runs) qrun = q + 1;
+        sym_tile(S1, q + 1, cs, buf, prow, pcol, t, tr, tc, racc, qrun, tile_runs || !vb || I2 != I1);
         Ic = I2;
         Jc = J2;
     }
@@ -2040,13 +2048,14 @@ __global__ __launch_bounds__(kNT) void k_sym_pack_f64(const double *__restrict__
 }
 
 // The counter-hash SPD system (k_gen_spd's values) straight into the tiles.
-__global__ __launch_bounds__(kSymNT) void k_gen_spd_sym(int64_t n, int64_t nt, int64_t ntiles, uint64_t salt,
-                                                        double *__restrict__ At) {
+// Tiles [q_base, q_base + count) into At (At[0] = tile q_base).
+__global__ __launch_bounds__(kSymNT) void k_gen_spd_sym(int64_t n, int64_t nt, int64_t q_base, int64_t count,
+                                                        uint64_t salt, double *__restrict__ At) {
 #pragma clang fp contract(off)
-    for (int64_t q = blockIdx.x; q < ntiles; q += gridDim.x) {
+    for (int64_t qi = blockIdx.x; qi < count; qi += gridDim.x) {
         int64_t I, J;
-        sym_tile_ij(q, nt, I, J);
-        d2 *tile = reinterpret_cast<d2 *>(At) + q * kSymTileD2;
+        sym_tile_ij(q_base + qi, nt, I, J);
+        d2 *tile = reinterpret_cast<d2 *>(At) + qi * kSymTileD2;
         const int t = threadIdx.x, tr = t >> 5, tc = t & 31;
         for (int k = 0; k < kSymK; ++k) {
             const uint64_t i = (uint64_t)(I * kSymT + tr * kSymRPT + (k >> 1));
@@ -2502,14 +2511,30 @@ int sym_grid(int device) {
 hipError_t symv_f64(const double *At, int64_t n, int64_t lda, int grid, const double *p, double *prow, double *pcol,
                     double *y, const double *pown, double *dot_out, const RedWs &ws, hipStream_t s,
                     const int64_t *gate) {
-    const int64_t nt = lda / kSymT, ntiles = sym_tiles(lda);
-    if (lda % kSymT || grid <= 0 || ((reinterpret_cast<uintptr_t>(At) | reinterpret_cast<uintptr_t>(p)) & 15))
-        return hipErrorInvalidValue;
+    const int64_t ntiles = sym_tiles(lda);
+    if (grid <= 0) return hipErrorInvalidValue;
     const int64_t per = (ntiles + grid - 1) / grid;
+    hipError_t e = symv_tiles_f64(At, 0, ntiles, lda, grid, false, p, prow, pcol, s, gate);
+    if (e != hipSuccess) return e;
+    return symv_reduce_f64(n, lda, per, prow, pcol, y, pown, dot_out, ws, s, gate);
+}
+
+hipError_t symv_tiles_f64(const double *At, int64_t q_base, int64_t count, int64_t lda, int grid, bool tile_runs,
+                          const double *p, double *prow, double *pcol, hipStream_t s, const int64_t *gate) {
+    if (lda % kSymT || grid <= 0 || count <= 0 ||
+        ((reinterpret_cast<uintptr_t>(At) | reinterpret_cast<uintptr_t>(p)) & 15))
+        return hipErrorInvalidValue;
+    const int64_t per = (count + grid - 1) / grid;
     auto fn = env_int("CGX_SYM_NT", 1) ? k_symv_f64<1> : k_symv_f64<0>;
-    hipLaunchKernelGGL(fn, dim3(grid), dim3(kSymNT), 0, s, At, nt, ntiles, per, p, prow, pcol, gate);
-    hipLaunchKernelGGL(k_symv_reduce_f64, dim3(grid_1d(n, 64, kMaxRedBlocks)), dim3(kNT), 0, s, n, nt, per, prow,
-                       pcol, y, pown, dot_out, ws.partials, ws.tickets + T_MATVEC, gate);
+    hipLaunchKernelGGL(fn, dim3(grid), dim3(kSymNT), 0, s, At, lda / kSymT, q_base, count, per, tile_runs ? 1 : 0, p,
+                       prow, pcol, gate);
+    return hipGetLastError();
+}
+
+hipError_t symv_reduce_f64(int64_t n, int64_t lda, int64_t per, const double *prow, const double *pcol, double *y,
+                           const double *pown, double *dot_out, const RedWs &ws, hipStream_t s, const int64_t *gate) {
+    hipLaunchKernelGGL(k_symv_reduce_f64, dim3(grid_1d(n, 64, kMaxRedBlocks)), dim3(kNT), 0, s, n, lda / kSymT, per,
+                       prow, pcol, y, pown, dot_out, ws.partials, ws.tickets + T_MATVEC, gate);
     return hipGetLastError();
 }
 
@@ -2522,9 +2547,21 @@ hipError_t sym_pack_f64(const double *rows, int64_t ld, int64_t row0, int64_t nr
 }
 
 hipError_t gen_spd_sym_f64(int64_t n, int64_t lda, uint64_t seed, double *At, double *b, hipStream_t s) {
-    const int64_t ntiles = sym_tiles(lda);
-    hipLaunchKernelGGL(k_gen_spd_sym, dim3((unsigned)std::min<int64_t>(ntiles, 65536)), dim3(kSymNT), 0, s, n,
-                       lda / kSymT, ntiles, mix64(seed), At);
+    hipError_t e = gen_spd_sym_tiles_f64(n, lda, seed, 0, sym_tiles(lda), At, s);
+    if (e != hipSuccess) return e;
+    hipLaunchKernelGGL(k_gen_b, dim3(grid_vec(n)), dim3(kNT), 0, s, 0, n, mix64(seed + 1), b);
+    return hipGetLastError();
+}
+
+hipError_t gen_spd_sym_tiles_f64(int64_t n, int64_t lda, uint64_t seed, int64_t q_base, int64_t count, double *At,
+                                 hipStream_t s) {
+    if (count <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gen_spd_sym, dim3((unsigned)std::min<int64_t>(count, 65536)), dim3(kSymNT), 0, s, n,
+                       lda / kSymT, q_base, count, mix64(seed), At);
+    return hipGetLastError();
+}
+
+hipError_t gen_b_f64(int64_t n, uint64_t seed, double *b, hipStream_t s) {
     hipLaunchKernelGGL(k_gen_b, dim3(grid_vec(n)), dim3(kNT), 0, s, 0, n, mix64(seed + 1), b);
     return hipGetLastError();
 }

@@ -93,7 +93,9 @@ extern "C" {
                                    a symmetric A; this mode reads only
                                    A[i][j] for j >= 128*(i/128) (the lower
                                    triangle outside the diagonal tiles is never
-                                   read).  Sums run in a different order than
+                                   read).  With CGX_HOST_STREAM the tiles stay
+                                   in pinned host memory and stream in chunks.
+                                   Sums run in a different order than
                                    the row-major kernel: results agree to fp64
                                    rounding, deterministically. */
 #define CGX_HOST_STREAM  0x200 /* keep A in pinned host memory and stream row

@@ -98,10 +98,36 @@ def test_symmetric_rows_in_pieces_and_fixed_count():
 
 
 def test_symmetric_rejects_unsupported():
-    for kw in ({"flags": SYM, "devices": [0, 0]}, {"flags": cg.CGX_F32_REF | cg.CGX_SYMMETRIC},
-               {"flags": SYM | cg.CGX_HOST_STREAM}):
+    for kw in ({"flags": SYM, "devices": [0, 0]}, {"flags": cg.CGX_F32_REF | cg.CGX_SYMMETRIC}):
         with pytest.raises(cg.CgxError):
             cg.Solver(1024, **kw)
     with cg.Solver(1024, flags=SYM) as s:
         with pytest.raises(cg.CgxError):
             s.set_matvec_plan(2, 8)
+
+
+@pytest.mark.parametrize("name", ["kat4", "spd1024", "spd2048"])
+def test_symmetric_host_streamed_solve(monkeypatch, golden, name):
+    """CGX_SYMMETRIC | CGX_HOST_STREAM: the tiles stream from pinned host
+    memory in 1 MiB chunks (8 tiles, so many chunks per matVec, ragged last)."""
+    monkeypatch.setenv("CGX_STREAM_TILE_MB", "1")
+    A, b, x0 = case(name, np.float64)
+    with cg.Solver(b.size, flags=SYM | cg.CGX_HOST_STREAM) as s:
+        s.set_system(A, b, x0)
+        x, st = s.solve(None, eps=1e-10)
+    xo, so = oracle.cg_f64(A, b, x0, eps=1e-10)
+    assert st.iterations == so.iterations == golden["cases"][name]["conjgrad_m_f64_iterations"]
+    assert rel(x, xo) <= TOL
+
+
+def test_symmetric_host_streamed_generator_matches_resident(monkeypatch):
+    monkeypatch.setenv("CGX_STREAM_TILE_MB", "3")
+    n = 5000
+    with cg.Solver(n, flags=SYM | cg.CGX_HOST_STREAM) as s:
+        s.generate_spd(42)
+        xs, ss = s.solve(None, eps=1e-10)
+    with cg.Solver(n, flags=SYM) as d:
+        d.generate_spd(42)
+        xd, sd = d.solve(None, eps=1e-10)
+    assert ss.iterations == sd.iterations
+    assert rel(xs, xd) <= 1e-12
