@@ -22,7 +22,10 @@
  * --fp32-ref, which reproduces serialConjugate.c's float results bit for bit.
  *
  * Extra options: --eps E, --max-iter M, --print-x, --stats, --threads T (text
- * parsing), --spd N [--seed S] (on-device synthetic system instead of files).
+ * parsing), --spd N [--seed S] (on-device synthetic system instead of files),
+ * --symmetric (fp64, one GPU: keep only A's upper-triangle tiles, half the
+ * bytes per matVec; CG's A is symmetric by contract, the lower triangle
+ * outside the diagonal tiles is not read).
  */
 #define _POSIX_C_SOURCE 200809L
 #include <pthread.h>
@@ -46,7 +49,7 @@ static double now_s(void) {
 
 static void usage(const char *prog) {
     fprintf(stderr,
-            "usage: %s [--gpus P] [--fp32-ref] [--eps E] [--max-iter M] [--dims FILE] [--n N]\n"
+            "usage: %s [--gpus P] [--fp32-ref | --symmetric] [--eps E] [--max-iter M] [--dims FILE] [--n N]\n"
             "          [--threads T] [--print-x] [--stats] matrixA vectorb initialguess\n"
             "       %s --spd N [--seed S] [--gpus P] [--eps E] [--max-iter M] [--stats]\n",
             prog, prog);
@@ -99,7 +102,7 @@ static void *create_ctx(void *arg) {
 
 int main(int argc, char **argv) {
     const double t_prog0 = now_s();
-    int gpus = 1, fp32ref = 0, print_x = 0, stats = 0;
+    int gpus = 1, fp32ref = 0, symmetric = 0, print_x = 0, stats = 0;
     long ncpu = sysconf(_SC_NPROCESSORS_ONLN);
     int threads = (int)(ncpu < 1 ? 1 : (ncpu > 16 ? 16 : ncpu)); /* text parsing threads */
     double eps = EPSILON_DEFAULT;
@@ -114,6 +117,7 @@ int main(int argc, char **argv) {
         int has_val = (i + 1 < argc);
         if (!strcmp(a, "--gpus") && has_val) gpus = atoi(argv[++i]);
         else if (!strcmp(a, "--fp32-ref")) fp32ref = 1;
+        else if (!strcmp(a, "--symmetric")) symmetric = 1;
         else if (!strcmp(a, "--eps") && has_val) eps = strtod(argv[++i], NULL);
         else if (!strcmp(a, "--max-iter") && has_val) max_iter = strtoll(argv[++i], NULL, 10);
         else if (!strcmp(a, "--dims") && has_val) dims_path = argv[++i];
@@ -135,6 +139,10 @@ int main(int argc, char **argv) {
     }
     if (gpus < 1) { fprintf(stderr, "--gpus must be >= 1\n"); return 2; }
     if (gpus > 32) { fprintf(stderr, "--gpus must be <= 32\n"); return 2; }
+    if (symmetric && (fp32ref || gpus != 1)) {
+        fprintf(stderr, "--symmetric is fp64 on one GPU (no --fp32-ref, --gpus 1)\n");
+        return 2;
+    }
 
     /* ---- N ---------------------------------------------------------------- */
     int64_t n = 0;
@@ -156,7 +164,7 @@ int main(int argc, char **argv) {
     printf("Computing cg of matrix size : %lld\n", (long long)n * (long long)n); /* serialConjugate.c:58 */
     fflush(stdout);
 
-    const int flags = fp32ref ? CGX_F32_REF : CGX_F64;
+    const int flags = fp32ref ? CGX_F32_REF : (CGX_F64 | (symmetric ? CGX_SYMMETRIC : 0));
     const size_t es = fp32ref ? 4 : 8;
     void *x = malloc((size_t)n * es);
     void *A = NULL, *b = NULL;

@@ -72,6 +72,12 @@ def test_cli_generated_text_files_multi_gpu(golden, tmp_path):
     A64, b64, x064 = case("spd512", np.float64)
     xo, _ = oracle.cg_f64(A64, b64, x064, eps=1e-10)
     assert np.linalg.norm(x2 - xo) <= 1e-10 * np.linalg.norm(xo)
+    # --symmetric: the same files, only the upper-triangle tiles kept
+    out3 = run("--symmetric", "--stats", "--eps", "1e-10", "--print-x", *paths)
+    x3 = printed_x(out3, n, np.float64)
+    assert np.linalg.norm(x3 - xo) <= 1e-10 * np.linalg.norm(xo)
+    r = subprocess.run([cg.CLI_PATH, "--symmetric", "--fp32-ref", *paths], capture_output=True, text=True)
+    assert r.returncode == 2
 
 
 def test_cli_synthetic_spd():
