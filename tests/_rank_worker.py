@@ -23,6 +23,7 @@ sys.path.insert(0, os.path.dirname(HERE))
 sys.path.insert(0, HERE)
 
 import conjugate_gradient_amd as cg  # noqa: E402
+import oracle  # noqa: E402
 from _cases import case  # noqa: E402
 
 
@@ -57,7 +58,11 @@ def main():
         if not flags & cg.CGX_F32_REF:
             flags |= cg.CGX_F64
         f32 = bool(flags & cg.CGX_F32_REF)
-        A, b, x0 = case(f"spd{n}", np.float32 if f32 else np.float64)
+        if mode == "sized":  # any n: generateSPDmatrix(n) from the oracle's MATLAB-compatible generator
+            A, b = oracle.spd_matlab(n, np.float64)
+            x0 = np.zeros(n)
+        else:
+            A, b, x0 = case(f"spd{n}", np.float32 if f32 else np.float64)
         with cg.Solver(n, rank=rank, nranks=P, unique_id=uid, device=0, flags=flags) as s:
             res["overlap"] = bool(s.info.flags & cg.CGX_OVERLAP_ACTIVE)
             res["nrows"] = s.info.nrows

@@ -180,3 +180,14 @@ def test_text_reader_matches_libc_conversion(built, tmp_path):
             continue
         assert got32[i].view(np.uint32) == e32.view(np.uint32), (t, got32[i], e32)
         assert np.float64(got64[i]).view(np.uint64) == np.float64(e64).view(np.uint64), (t, got64[i], e64)
+
+
+def test_flag_constants_match_header():
+    """The Python mirror's CGX_* flag and error values are the header's."""
+    import re
+    with open(os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "include", "cgx.h")) as f:
+        hdr = dict((m.group(1), int(m.group(2), 0)) for m in re.finditer(r"#define\s+(CGX_[A-Z0-9_]+)\s+(-?0x[0-9a-fA-F]+|-?\d+)", f.read()))
+    names = [k for k in dir(cg) if k.startswith("CGX_")]
+    assert names
+    for k in names:
+        assert k in hdr and getattr(cg, k) == hdr[k], k

@@ -94,6 +94,20 @@ def test_rank_mode_f64(tmp_path, mode, P):
 
 
 @pytest.mark.timeout(200)
+@pytest.mark.parametrize("n,P", [(1000, 2), (2000, 4), (4096, 4)])
+def test_rank_mode_f64_sizes(tmp_path, n, P):
+    """Row blocks that are not multiples of 128 rows (no overlap, ragged
+    chunks) and a larger system, collective exchange."""
+    x, res = run_ranks(tmp_path, "sized", n, P)
+    assert res[0]["nrows"] == n // P
+    assert res[0]["overlap"] == ((n // P) % 128 == 0)
+    A, b = oracle.spd_matlab(n, np.float64)
+    xo, so = oracle.cg_f64(A, b, np.zeros(n), eps=1e-10)
+    assert res[0]["iterations"] == so.iterations
+    assert rel(x, xo) <= TOL and res[0]["relres"] <= TOL
+
+
+@pytest.mark.timeout(200)
 @pytest.mark.parametrize("mode", ["f32ref", "p2p_f32ref"])
 def test_rank_mode_f32ref_bitwise(tmp_path, mode):
     n, P = 2048, 4
