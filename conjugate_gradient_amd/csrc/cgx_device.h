@@ -1,0 +1,181 @@
+// cgx_device.h -- internal to libcgx: device and host helpers shared by the
+// kernel files (cgx_matvec.hip, cgx_vector.hip, cgx_poisson.hip,
+// cgx_ref_f32.hip, cgx_symv.hip).  Not part of the C ABI (include/cgx.h).
+#pragma once
+
+#include "cgx_kernels.h"
+
+#include <cstdint>
+#include <cstdlib>
+#include <mutex>
+
+namespace cgx {
+
+typedef double d2 __attribute__((ext_vector_type(2)));
+
+constexpr int kNT = 256;  // threads per block for the fp64 kernels
+
+__device__ __forceinline__ double wave_sum(double v) {
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);
+    return v;
+}
+
+// Sum `v` over all threads of the grid.  Each block stores its total in
+// partials[blockIdx.x]; the last block to arrive sums the partials in index
+// order and writes *out.  Deterministic for a fixed grid.
+//
+// Hand-off (cdna_hip_programming.md Guideline 16, the write-through form):
+// the partial is stored write-through (8-B agent-scope atomic store = sc1),
+// the storing lane drains it (s_waitcnt vmcnt(0)) before its relaxed
+// agent-scope ticket add, and the block whose add returns gridDim-1 reads
+// every partial with sc1 loads (agent-scope atomic loads) -- no release /
+// acquire fence, so no per-block write-back of the L2's dirty lines (which
+// cost the r-update ~35 % of its time with a buffer_wbl2 per block).
+__device__ __forceinline__ void grid_sum_last_block(double v, double *partials, unsigned *ticket,
+                                                    double *out, bool add_to_out = false) {
+    __shared__ double red[kNT / 64];
+    __shared__ int is_last;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    v = wave_sum(v);
+    if (lane == 0) red[wid] = v;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = red[0];
+#pragma unroll
+        for (int w = 1; w < kNT / 64; ++w) t += red[w];
+        __hip_atomic_store(partials + blockIdx.x, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        is_last = (prev == gridDim.x - 1);
+    }
+    __syncthreads();
+    if (!is_last) return;
+    // all of this thread's partials in flight at once (grid <= 8192 = 32 * kNT)
+    double s = 0.0;
+    for (unsigned i0 = threadIdx.x; i0 < gridDim.x; i0 += 8 * kNT) {
+        double pv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const unsigned i = i0 + u * kNT;
+            pv[u] = (i < gridDim.x) ? __hip_atomic_load(partials + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (i0 + u * kNT < gridDim.x) s += pv[u];
+    }
+    s = wave_sum(s);
+    if (lane == 0) red[wid] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = red[0];
+#pragma unroll
+        for (int w = 1; w < kNT / 64; ++w) t += red[w];
+        *out = add_to_out ? *out + t : t;
+        __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+}
+
+__device__ __forceinline__ d2 ld2(const double *p) { return *reinterpret_cast<const d2 *>(p); }
+__device__ __forceinline__ void st2(double *p, d2 v) { *reinterpret_cast<d2 *>(p) = v; }
+
+// Stream policy of the vector kernels (VP): 0 plain, 1 non-temporal stores,
+// 2 non-temporal loads and stores (default: -8 % time on the Poisson
+// vectors, 537 MB each; profiles/r01_vector_policy.txt).
+template <int VP>
+__device__ __forceinline__ d2 ldv(const double *p) {
+    if constexpr (VP >= 2) return __builtin_nontemporal_load(reinterpret_cast<const d2 *>(p));
+    else return *reinterpret_cast<const d2 *>(p);
+}
+template <int VP>
+__device__ __forceinline__ void stv(double *p, d2 v) {
+    if constexpr (VP >= 1) __builtin_nontemporal_store(v, reinterpret_cast<d2 *>(p));
+    else *reinterpret_cast<d2 *>(p) = v;
+}
+
+// Vector kernels.  VEC (every pointer 16-B aligned): a block step covers
+// kVU * kNT consecutive element pairs; each thread loads its kVU pairs of
+// every input (16-B loads, all issued before any store), computes, stores.
+// Otherwise a scalar grid-stride loop.  The odd tail element of the VEC
+// path is done by thread 0 of block 0.  Per-thread sums run in a fixed
+// order, then the deterministic grid reduction.
+constexpr int kVU = 4;
+
+#define CGX_VEC_LOOP_BEGIN                                                                   \
+    const int64_t npairs = n >> 1;                                                           \
+    const int64_t step = (int64_t)gridDim.x * kNT * kVU;                                     \
+    for (int64_t base = (int64_t)blockIdx.x * kNT * kVU + threadIdx.x; base < npairs; base += step) { \
+        bool ok[kVU];                                                                        \
+        _Pragma("unroll") for (int u = 0; u < kVU; ++u) ok[u] = base + u * kNT < npairs;
+#define CGX_VEC_LOOP_END }
+
+// The device-side stopping decision of k_update_xp_f64 / k_poisson_p_f64
+// (serialConjugate.c:235): eps < 0 disables it; kdone / rrfinal are device
+// slots read by later launches' gates.
+struct ConvArgs {
+    double eps = -1.0;
+    int64_t k = 0;
+    int64_t *kdone = nullptr;   // 0 = not converged, else the loop-iteration count
+    double *rrfinal = nullptr;
+    int64_t *hrec = nullptr;    // host-mapped copy of {kdone, rrfinal}: read by the host without a copy
+};
+
+// The convergence record: device slots for later launches' gates, and the
+// host-mapped copy the host reads after an event (no per-iteration D2H copy).
+__device__ __forceinline__ void record_convergence(const ConvArgs &cv, int64_t kdone, double rr) {
+    *cv.rrfinal = rr;
+    *cv.kdone = kdone;
+    if (cv.hrec) {
+        __hip_atomic_store(cv.hrec + 1, __double_as_longlong(rr), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+        __hip_atomic_store(cv.hrec, kdone, __ATOMIC_RELEASE, __HIP_MEMORY_SCOPE_SYSTEM);
+    }
+}
+
+// ---------------------------------------------------------------------------
+// counter-hash SPD generator (generateSPDmatrix.m:4-17 distribution)
+// ---------------------------------------------------------------------------
+__host__ __device__ __forceinline__ uint64_t mix64(uint64_t z) {
+    z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+    z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+    return z ^ (z >> 31);
+}
+__device__ __forceinline__ double u01(uint64_t salt, uint64_t i, uint64_t j) {
+    const uint64_t h = mix64(((i << 32) | (j & 0xffffffffull)) ^ salt);
+    return (double)(h >> 11) * 0x1.0p-53;
+}
+
+// ---------------------------------------------------------------------------
+// host helpers
+// ---------------------------------------------------------------------------
+inline int cu_count(int device) {
+    static std::mutex mu;
+    static int cus[64] = {};
+    std::lock_guard<std::mutex> lk(mu);
+    if (device < 0 || device >= 64) return 256;
+    if (cus[device] == 0) {
+        int v = 0;
+        if (hipDeviceGetAttribute(&v, hipDeviceAttributeMultiprocessorCount, device) != hipSuccess || v <= 0)
+            v = 256;
+        cus[device] = v;
+    }
+    return cus[device];
+}
+
+inline int env_int(const char *name, int dflt) {
+    const char *s = std::getenv(name);
+    return (s && *s) ? std::atoi(s) : dflt;
+}
+
+inline unsigned grid_1d(int64_t n, int per_block, unsigned cap) {
+    int64_t g = (n + per_block - 1) / per_block;
+    if (g < 1) g = 1;
+    if (g > (int64_t)cap) g = cap;
+    return (unsigned)g;
+}
+
+// Grid of the vector kernels: <= kMaxRedBlocks (the partial slots), <= 8 blocks/CU.
+inline unsigned grid_vec(int64_t n) { return grid_1d((n + 1) / 2, kNT * kVU, 2048); }
+
+inline bool al16(const void *p) { return (reinterpret_cast<uintptr_t>(p) & 15) == 0; }
+
+}  // namespace cgx

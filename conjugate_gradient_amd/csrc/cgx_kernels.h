@@ -89,7 +89,7 @@ hipError_t fill_f64(double *p, int64_t n, double v, hipStream_t s);
 hipError_t fill_f32(float *p, int64_t n, float v, hipStream_t s);
 
 // ---- CGX_SYMMETRIC: A as the upper triangle of 128 x 128 tiles ---------------
-// (layout: cgx_kernels.hip).  lda is a multiple of 128; At holds sym_tiles(lda)
+// (layout: cgx_symv.hip).  lda is a multiple of 128; At holds sym_tiles(lda)
 // tiles of 128*128 doubles; prow/pcol sym_tiles(lda)*128 doubles each.
 int64_t sym_tiles(int64_t lda);
 int sym_grid(int device);

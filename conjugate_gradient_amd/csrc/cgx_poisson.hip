@@ -1,0 +1,532 @@
+// cgx_poisson.hip -- matrix-free 5-point Poisson operator (configs[4]) and
+// the fused two-kernel Poisson CG iteration.
+#include "cgx_device.h"
+
+#include <algorithm>
+
+namespace cgx {
+namespace {
+
+// ---------------------------------------------------------------------------
+// matrix-free 5-point Poisson A.p on a slab (configs[4]; no reference
+// counterpart).  ph = p with one halo row above and below: rows 0 and
+// mloc+1 are the neighbours' boundary rows (zero at the domain boundary).
+// Each block owns a contiguous run of grid rows and sweeps them in order so
+// the rows above/below are L2/MALL hits; a thread handles column pairs
+// (16-B loads of the centre/up/down rows, 8-B loads of the two side points).
+// Fused: *dot_out = p . Ap (same last-block reduction as the matVec).
+// ---------------------------------------------------------------------------
+// Even m: column-strip marching.  A block owns a strip of 2*kNT columns and a
+// run of rows; each thread holds a column pair and walks down the rows with
+// the up/centre rows in registers, so every p element is loaded once (plus
+// two halo rows per run).  The left/right neighbours come from the adjacent
+// lanes by wave shuffle; only lanes 0 / 63 load them (L1 hits).  The next
+// row is prefetched one step ahead.
+__global__ __launch_bounds__(kNT) void k_stencil5_strip_f64(const double *__restrict__ ph, int64_t mloc, int64_t m,
+                                                            int64_t nstrips, int64_t rows_per_block,
+                                                            double *__restrict__ Ap, double *dot_out,
+                                                            double *partials, unsigned *ticket, const int64_t *gate) {
+    if (gate && *gate) return;
+    const int lane = threadIdx.x & 63;
+    const int64_t strip = blockIdx.x % nstrips, chunk = blockIdx.x / nstrips;
+    const int64_t j = strip * (2 * kNT) + 2 * threadIdx.x;
+    const bool valid = j < m;
+    const int64_t i0 = chunk * rows_per_block;
+    const int64_t i1 = (i0 + rows_per_block < mloc) ? i0 + rows_per_block : mloc;
+    double acc = 0.0;
+    if (i0 < i1) {
+        const d2 zero = (d2)(0.0);
+        const double *col = ph + j;
+        d2 up = valid ? ld2(col + i0 * m) : zero;
+        d2 ce = valid ? ld2(col + (i0 + 1) * m) : zero;
+        d2 dn = valid ? ld2(col + (i0 + 2) * m) : zero;
+        for (int64_t i = i0; i < i1; ++i) {
+            // prefetch the row after next while this row is computed
+            const d2 nx = (valid && i + 1 < i1) ? ld2(col + (i + 3) * m) : zero;
+            double l = __shfl_up(ce.y, 1, 64);
+            double r = __shfl_down(ce.x, 1, 64);
+            const double *crow = ph + (i + 1) * m;
+            if (lane == 0) l = (j > 0 && valid) ? crow[j - 1] : 0.0;
+            if (lane == 63) r = (j + 2 < m) ? crow[j + 2] : 0.0;
+            d2 o;
+            o.x = 4.0 * ce.x - up.x - dn.x - l - ce.y;
+            o.y = 4.0 * ce.y - up.y - dn.y - ce.x - r;
+            if (valid) {
+                st2(Ap + i * m + j, o);
+                if (dot_out) acc += ce.x * o.x + ce.y * o.y;
+            }
+            up = ce;
+            ce = dn;
+            dn = nx;
+        }
+    }
+    if (dot_out) grid_sum_last_block(acc, partials, ticket, dot_out);
+}
+
+// Odd m (rows not 16-B aligned): a block walks a run of rows, one column per thread.
+// Fused Poisson iteration (even m): two strip-marching kernels per CG
+// iteration instead of stencil + r update + x/p update, so no Ap vector
+// exists.  A p_k is recomputed by the second kernel from p_k (5 flops per
+// point against 16 B of an Ap round trip).  Bytes per grid point per
+// iteration: 24 (k_poisson_p: r, p_{k-1} -> p_k) + 40 (k_poisson_xr: p_k,
+// x, r -> x, r) = 64, against 80 for the three-kernel split.
+//
+// k_poisson_p_f64 (iteration k):  p_k = r_k + beta p_{k-1} (p_0 = r_0) into
+// the other p buffer (the window reads p_{k-1} rows owned by neighbouring
+// blocks, so the update cannot be in place), including the slab's halo rows
+// (computed from the exchanged r halo and the p_{k-1} halo this kernel wrote
+// one iteration earlier; zero at the domain boundary), and
+// *dot_out = p_k . A p_k.  With cv.kdone it first decides the previous
+// iteration's sqrt(r.r) < eps (device-side gating): on convergence it stores
+// *kdone = k, *rrfinal = r.r and does nothing else; x is already final.
+
+// Work items are (strip of 2*kNT columns, run of `rpi` rows), numbered strip-
+// fastest, and blocks take them grid-stride: the items in flight at any time
+// are consecutive, i.e. a narrow band of grid rows, so the vectors are
+// streamed roughly in address order instead of from ~2048 places at once.
+// Each item's run is walked RB rows per step: all loads of a step (RB new p
+// rows, RB rows of each streamed vector, the lane-0/63 side points) are
+// issued before its arithmetic.  Streamed vectors use non-temporal loads and
+// stores (NT), as the vector kernels do.
+// Addresses: a wave-uniform row base plus the lane's 32-bit byte offset
+// (lanes past the last column load column 0 and their values are zeroed),
+// so a step of RB rows is straight-line code: no per-row or per-lane branch
+// between its loads and its arithmetic except around the stores.  The side
+// points j-1 of lane 0 and j+2 of lane 63 are wave-uniform addresses.
+// Row base + lane offset with the offset made opaque to the optimiser (an
+// empty asm on the VGPR), so loop strength reduction cannot fold it into a
+// per-lane 64-bit pointer induction variable: every access keeps the
+// `global_load ... vOff, s[base]` form, with the row stepping in SGPRs.
+template <bool NT>
+__device__ __forceinline__ d2 lds2(const double *row, uint32_t off) {
+    asm volatile("" : "+v"(off));
+    const d2 *p = reinterpret_cast<const d2 *>(reinterpret_cast<const char *>(row) + off);
+    if constexpr (NT) return __builtin_nontemporal_load(p);
+    else return *p;
+}
+template <bool NT>
+__device__ __forceinline__ void sts2(double *row, uint32_t off, d2 v) {
+    asm volatile("" : "+v"(off));
+    d2 *p = reinterpret_cast<d2 *>(reinterpret_cast<char *>(row) + off);
+    if constexpr (NT) __builtin_nontemporal_store(v, p);
+    else *p = v;
+}
+
+// One lane's view of a work item: column pair j, j+1 (byte offset `off`,
+// 0 for lanes past the grid), its wave wv and the wave's first column jw.
+// Side points: lane 0 needs column j-1, lane 63 column j+2.  Inside a block
+// they come from the neighbouring wave through LDS (one barrier per step);
+// only the block's outer edges (wave 0 left, wave 3 right) load them, from
+// wave-uniform addresses.  Loading every wave's side points from memory
+// costs a 64-128 B line per 8-B value: +25 % of the fetched bytes (PMC).
+struct StripLane {
+    bool valid, has_l, has_r;
+    int wv;
+    uint32_t off;
+    int64_t jw;
+};
+constexpr int kWaves = kNT / 64;
+__device__ __forceinline__ StripLane strip_lane(int64_t w, int64_t nstrips, int64_t m) {
+    StripLane L;
+    L.wv = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+    L.jw = (w % nstrips) * (2 * kNT) + L.wv * 128;
+    const int64_t j = L.jw + 2 * (threadIdx.x & 63);
+    L.valid = j < m;
+    L.off = L.valid ? (uint32_t)(j * 8) : 0u;
+    L.has_l = L.wv == 0 && L.jw > 0;
+    L.has_r = L.wv == kWaves - 1 && L.jw + 128 < m;
+    return L;
+}
+__device__ __forceinline__ d2 keep(bool valid, d2 v) {
+    d2 o;
+    o.x = valid ? v.x : 0.0;
+    o.y = valid ? v.y : 0.0;
+    return o;
+}
+
+// LDS edge exchange: eb[(wave * 2 + side) * 8 + t], side 0 = the wave's first
+// value (lane 0's .x), side 1 = its last (lane 63's .y); two halves by step
+// parity so one barrier per step suffices.
+constexpr int kEdgeRB = 8;
+template <int RBn>
+__device__ __forceinline__ void edges_put(double *eb, const StripLane &L, const d2 (&ce)[RBn]) {
+    const int lane = threadIdx.x & 63;
+#pragma unroll
+    for (int t = 0; t < RBn; ++t) {
+        if (lane == 0) eb[(L.wv * 2 + 0) * kEdgeRB + t] = ce[t].x;
+        if (lane == 63) eb[(L.wv * 2 + 1) * kEdgeRB + t] = ce[t].y;
+    }
+}
+__device__ __forceinline__ double edge_l(const double *eb, const StripLane &L, int t, double outer) {
+    return L.wv > 0 ? eb[((L.wv - 1) * 2 + 1) * kEdgeRB + t] : outer;
+}
+__device__ __forceinline__ double edge_r(const double *eb, const StripLane &L, int t, double outer) {
+    return L.wv < kWaves - 1 ? eb[((L.wv + 1) * 2 + 0) * kEdgeRB + t] : outer;
+}
+
+// p_k rows (FIRST: p_0 = r_0)
+template <bool NT, bool FIRST>
+__device__ __forceinline__ d2 pnv(const double *rrow, const double *prow, const StripLane &L, double beta) {
+    const d2 rv = lds2<NT>(rrow, L.off);
+    if constexpr (FIRST) return keep(L.valid, rv);
+    const d2 pv = lds2<NT>(prow, L.off);
+    d2 o;
+    o.x = __builtin_fma(beta, pv.x, rv.x);
+    o.y = __builtin_fma(beta, pv.y, rv.y);
+    return keep(L.valid, o);
+}
+template <bool FIRST>
+__device__ __forceinline__ double pns(const double *rrow, const double *prow, int64_t col, double beta) {
+    if constexpr (FIRST) return rrow[col];
+    else return __builtin_fma(beta, prow[col], rrow[col]);
+}
+
+// RBn output rows starting at interior row i: pm, pc carry p_k rows h = i, i+1.
+template <int RBn, bool NT, bool FIRST, bool HT>
+__device__ __forceinline__ void poisson_p_step(const double *__restrict__ rh, const double *__restrict__ poh,
+                                               double *__restrict__ pnh, int64_t mloc, int64_t m, int64_t i,
+                                               const StripLane &L, double beta, d2 &pm, d2 &pc, double &acc,
+                                               double *eb) {
+    const int lane = threadIdx.x & 63;
+    d2 pr[RBn], ce[RBn];
+    double el[RBn], er[RBn];
+#pragma unroll
+    for (int t = 0; t < RBn; ++t) {
+        const int64_t hc = (i + t + 1) * m;  // centre row (halo coordinates) of output row i+t
+        // HT: the last two rows are the next item's first two (its halo):
+        // default-policy loads keep them in L2 for the block that reads them next
+        pr[t] = (HT && t >= RBn - 2) ? pnv<false, FIRST>(rh + hc + m, poh + hc + m, L, beta)
+                                     : pnv<NT, FIRST>(rh + hc + m, poh + hc + m, L, beta);
+        el[t] = L.has_l ? pns<FIRST>(rh + hc, poh + hc, L.jw - 1, beta) : 0.0;
+        er[t] = L.has_r ? pns<FIRST>(rh + hc, poh + hc, L.jw + 128, beta) : 0.0;
+    }
+#pragma unroll
+    for (int t = 0; t < RBn; ++t) ce[t] = t == 0 ? pc : pr[t - 1];
+    edges_put<RBn>(eb, L, ce);
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < RBn; ++t) {
+        const d2 up = t == 0 ? pm : (t == 1 ? pc : pr[t - 2]);
+        const d2 dn = pr[t];
+        const double lw = edge_l(eb, L, t, el[t]), rw = edge_r(eb, L, t, er[t]);
+        double l = __shfl_up(ce[t].y, 1, 64);
+        double r = __shfl_down(ce[t].x, 1, 64);
+        l = lane == 0 ? lw : l;
+        r = lane == 63 ? rw : r;
+        d2 o;
+        o.x = 4.0 * ce[t].x - up.x - dn.x - l - ce[t].y;
+        o.y = 4.0 * ce[t].y - up.y - dn.y - ce[t].x - r;
+        acc += ce[t].x * o.x + ce[t].y * o.y;  // zero on lanes past the grid
+        if (L.valid) {
+            sts2<NT>(pnh + (i + t + 1) * m, L.off, ce[t]);
+            if (i + t == mloc - 1) sts2<NT>(pnh + (mloc + 1) * m, L.off, dn);  // bottom halo row of p_k
+        }
+    }
+    if constexpr (RBn >= 2) {
+        pm = pr[RBn - 2];
+        pc = pr[RBn - 1];
+    } else {
+        pm = pc;
+        pc = pr[0];
+    }
+}
+
+// Work items [w0, w0+cnt1) then [w2, w2+cnt2) (the whole slab, or, when
+// the r halo exchange overlaps the kernel, the slab's interior runs first
+// and its two edge runs after the exchange).
+struct ItemRanges {
+    int64_t w0, cnt1, w2, cnt2;
+};
+
+template <int RB, bool NT, bool FIRST, bool HT>
+__device__ __forceinline__ double poisson_p_body(const double *__restrict__ rh, const double *__restrict__ poh,
+                                                 double *__restrict__ pnh, int64_t mloc, int64_t m, int64_t nstrips,
+                                                 int64_t rpi, ItemRanges ir, double beta, double *edge) {
+    double acc = 0.0;
+    int par = 0;
+    for (int64_t v = blockIdx.x; v < ir.cnt1 + ir.cnt2; v += gridDim.x) {
+        const int64_t w = v < ir.cnt1 ? ir.w0 + v : ir.w2 + (v - ir.cnt1);
+        const StripLane L = strip_lane(w, nstrips, m);
+        const int64_t i0 = (w / nstrips) * rpi;
+        const int64_t i1 = (i0 + rpi < mloc) ? i0 + rpi : mloc;
+        d2 pm = pnv<NT && !HT, FIRST>(rh + i0 * m, poh + i0 * m, L, beta);
+        d2 pc = pnv<NT && !HT, FIRST>(rh + (i0 + 1) * m, poh + (i0 + 1) * m, L, beta);
+        if (L.valid && i0 == 0) sts2<NT>(pnh, L.off, pm);  // top halo row of p_k
+        int64_t i = i0;
+        for (; i + RB <= i1; i += RB, par ^= 1)
+            poisson_p_step<RB, NT, FIRST, HT>(rh, poh, pnh, mloc, m, i, L, beta, pm, pc, acc,
+                                          edge + par * (kWaves * 2 * kEdgeRB));
+        for (; i < i1; ++i, par ^= 1)
+            poisson_p_step<1, NT, FIRST, HT>(rh, poh, pnh, mloc, m, i, L, beta, pm, pc, acc,
+                                         edge + par * (kWaves * 2 * kEdgeRB));
+    }
+    return acc;
+}
+
+template <int RB, bool NT, bool HT>
+__global__ __launch_bounds__(kNT) void k_poisson_p_f64(const double *__restrict__ rh, const double *__restrict__ poh,
+                                                       double *__restrict__ pnh, int64_t mloc, int64_t m,
+                                                       int64_t nstrips, int64_t rpi, ItemRanges ir, const double *rr,
+                                                       const double *rsold, int first, ConvArgs cv, double *dot_out,
+                                                       int add_to_out, double *partials, unsigned *ticket) {
+    static_assert(RB <= kEdgeRB, "edge buffer");
+    __shared__ double edge[2 * kWaves * 2 * kEdgeRB];
+    if (cv.kdone) {
+        if (*cv.kdone != 0) return;
+        if (!first && cv.eps >= 0.0 && sqrt(*rr) < cv.eps) {  // the same decision in every block
+            if (blockIdx.x == 0 && threadIdx.x == 0) record_convergence(cv, cv.k, *rr);
+            return;
+        }
+    }
+    // p_0 = r_0 (first) has its own instantiation: no p_{k-1} loads
+    const double acc = first ? poisson_p_body<RB, NT, true, HT>(rh, poh, pnh, mloc, m, nstrips, rpi, ir, 0.0, edge)
+                             : poisson_p_body<RB, NT, false, HT>(rh, poh, pnh, mloc, m, nstrips, rpi, ir,
+                                                                 *rr / *rsold, edge);
+    grid_sum_last_block(acc, partials, ticket, dot_out, add_to_out != 0);
+}
+
+// k_poisson_xr_f64 (iteration k): alpha = *rsold / *pAp; x += alpha p_k and
+// r -= alpha A p_k with A p_k recomputed from p_k (halo included);
+// *rr_out = r.r.  Skipped once *gate != 0.
+template <int RBn, bool NT, bool HT>
+__device__ __forceinline__ void poisson_xr_step(const double *__restrict__ pnh, double *__restrict__ x,
+                                                double *__restrict__ r, int64_t m, int64_t i, const StripLane &L,
+                                                double alpha, d2 &pm, d2 &pc, double &acc, double *eb) {
+    const int lane = threadIdx.x & 63;
+    d2 pr[RBn], xv[RBn], rv[RBn], ce[RBn];
+    double el[RBn], er[RBn];
+#pragma unroll
+    for (int t = 0; t < RBn; ++t) {
+        const int64_t hc = (i + t + 1) * m, ic = (i + t) * m;
+        pr[t] = keep(L.valid, (HT && t >= RBn - 2) ? lds2<false>(pnh + hc + m, L.off) : lds2<NT>(pnh + hc + m, L.off));
+        xv[t] = lds2<NT>(x + ic, L.off);
+        rv[t] = lds2<NT>(r + ic, L.off);
+        el[t] = L.has_l ? pnh[hc + L.jw - 1] : 0.0;
+        er[t] = L.has_r ? pnh[hc + L.jw + 128] : 0.0;
+    }
+#pragma unroll
+    for (int t = 0; t < RBn; ++t) ce[t] = t == 0 ? pc : pr[t - 1];
+    edges_put<RBn>(eb, L, ce);
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < RBn; ++t) {
+        const d2 up = t == 0 ? pm : (t == 1 ? pc : pr[t - 2]);
+        const d2 dn = pr[t];
+        const double lw = edge_l(eb, L, t, el[t]), rw = edge_r(eb, L, t, er[t]);
+        double l = __shfl_up(ce[t].y, 1, 64);
+        double rt = __shfl_down(ce[t].x, 1, 64);
+        l = lane == 0 ? lw : l;
+        rt = lane == 63 ? rw : rt;
+        d2 o;
+        o.x = 4.0 * ce[t].x - up.x - dn.x - l - ce[t].y;
+        o.y = 4.0 * ce[t].y - up.y - dn.y - ce[t].x - rt;
+        d2 xn, rn;
+        xn.x = __builtin_fma(alpha, ce[t].x, xv[t].x);
+        xn.y = __builtin_fma(alpha, ce[t].y, xv[t].y);
+        rn.x = __builtin_fma(-alpha, o.x, rv[t].x);
+        rn.y = __builtin_fma(-alpha, o.y, rv[t].y);
+        acc += L.valid ? rn.x * rn.x + rn.y * rn.y : 0.0;
+        if (L.valid) {
+            sts2<NT>(x + (i + t) * m, L.off, xn);
+            sts2<NT>(r + (i + t) * m, L.off, rn);
+        }
+    }
+    if constexpr (RBn >= 2) {
+        pm = pr[RBn - 2];
+        pc = pr[RBn - 1];
+    } else {
+        pm = pc;
+        pc = pr[0];
+    }
+}
+
+template <int RB, bool NT, bool HT>
+__global__ __launch_bounds__(kNT) void k_poisson_xr_f64(const double *__restrict__ pnh, double *__restrict__ x,
+                                                        double *__restrict__ r, int64_t mloc, int64_t m,
+                                                        int64_t nstrips, int64_t rpi, int64_t nitems, int reverse,
+                                                        const double *rsold, const double *pAp, double *rr_out,
+                                                        double *partials, unsigned *ticket, const int64_t *gate) {
+    static_assert(RB <= kEdgeRB, "edge buffer");
+    __shared__ double edge[2 * kWaves * 2 * kEdgeRB];
+    if (gate && *gate) return;
+    const double alpha = *rsold / *pAp;
+    double acc = 0.0;
+    int par = 0;
+    for (int64_t v = blockIdx.x; v < nitems; v += gridDim.x) {
+        // reverse: walk the slab from its end, where the previous kernel
+        // (k_poisson_p, forward) last wrote p_k, so the first bytes read may
+        // still sit in the 256 MB MALL
+        const int64_t w = reverse ? nitems - 1 - v : v;
+        const StripLane L = strip_lane(w, nstrips, m);
+        const int64_t i0 = (w / nstrips) * rpi;
+        const int64_t i1 = (i0 + rpi < mloc) ? i0 + rpi : mloc;
+        d2 pm = keep(L.valid, lds2<NT && !HT>(pnh + i0 * m, L.off));
+        d2 pc = keep(L.valid, lds2<NT && !HT>(pnh + (i0 + 1) * m, L.off));
+        int64_t i = i0;
+        for (; i + RB <= i1; i += RB, par ^= 1)
+            poisson_xr_step<RB, NT, HT>(pnh, x, r, m, i, L, alpha, pm, pc, acc, edge + par * (kWaves * 2 * kEdgeRB));
+        for (; i < i1; ++i, par ^= 1)
+            poisson_xr_step<1, NT, HT>(pnh, x, r, m, i, L, alpha, pm, pc, acc, edge + par * (kWaves * 2 * kEdgeRB));
+    }
+    grid_sum_last_block(acc, partials, ticket, rr_out);
+}
+
+__global__ __launch_bounds__(kNT) void k_stencil5_rows_f64(const double *__restrict__ ph, int64_t mloc, int64_t m,
+                                                           double *__restrict__ Ap, double *dot_out, double *partials,
+                                                           unsigned *ticket, const int64_t *gate) {
+    if (gate && *gate) return;
+    const int64_t rows_per_block = (mloc + gridDim.x - 1) / gridDim.x;
+    const int64_t i0 = (int64_t)blockIdx.x * rows_per_block;
+    const int64_t i1 = (i0 + rows_per_block < mloc) ? i0 + rows_per_block : mloc;
+    double acc = 0.0;
+    for (int64_t i = i0; i < i1; ++i) {
+        const double *up = ph + i * m, *ce = up + m, *dn = ce + m;
+        double *out = Ap + i * m;
+        for (int64_t j = threadIdx.x; j < m; j += kNT) {
+            const double c = ce[j];
+            const double o = 4.0 * c - up[j] - dn[j] - ((j > 0) ? ce[j - 1] : 0.0) - ((j + 1 < m) ? ce[j + 1] : 0.0);
+            out[j] = o;
+            if (dot_out) acc += c * o;
+        }
+    }
+    if (dot_out) grid_sum_last_block(acc, partials, ticket, dot_out);
+}
+
+}  // namespace
+
+hipError_t stencil5_f64(const double *ph, int64_t mloc, int64_t m, double *Ap, double *dot_out, const RedWs &ws,
+                        hipStream_t s, const int64_t *gate) {
+    if (mloc <= 0) return hipSuccess;
+    if ((m & 1) == 0 && al16(ph) && al16(Ap)) {
+        const int64_t nstrips = (m + 2 * kNT - 1) / (2 * kNT);
+        int64_t chunks = std::max<int64_t>(1, 2048 / nstrips);
+        chunks = std::min<int64_t>(chunks, mloc);
+        const int64_t rpb = (mloc + chunks - 1) / chunks;
+        chunks = (mloc + rpb - 1) / rpb;
+        int64_t grid = nstrips * chunks;
+        if (grid > kMaxRedBlocks) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(k_stencil5_strip_f64, dim3((unsigned)grid), dim3(kNT), 0, s, ph, mloc, m, nstrips, rpb, Ap,
+                           dot_out, ws.partials, ws.tickets + T_MATVEC, gate);
+    } else {
+        const unsigned grid = (unsigned)std::min<int64_t>(mloc, 2048);
+        hipLaunchKernelGGL(k_stencil5_rows_f64, dim3(grid), dim3(kNT), 0, s, ph, mloc, m, Ap, dot_out, ws.partials,
+                           ws.tickets + T_MATVEC, gate);
+    }
+    return hipGetLastError();
+}
+
+// Fused Poisson kernels: rows per step RB (CGX_STENCIL_RB: 1, 2, 4, 8), rows
+// per work item (CGX_STENCIL_ROWS), resident blocks (CGX_STENCIL_BLOCKS), NT
+// streams (CGX_STENCIL_NT=0: default-policy loads/stores).  Defaults RB=8,
+// 8-row items, occupancy-sized grid: measured at m=8192 over RB 2..8, items
+// of 8..128 rows and 1024..4096 blocks (profiles/r01_sweep_poisson*.jsonl);
+// short items keep the rows in flight in a narrow band (64- and 128-row items
+// are 7-20 % slower).
+struct PoissonPlan {
+    int rb, nt, ht;
+    int64_t nstrips, rpi, nitems, grid;
+};
+static PoissonPlan poisson_plan(int64_t mloc, int64_t m) {
+    PoissonPlan p;
+    p.rb = env_int("CGX_STENCIL_RB", 8);
+    p.nt = env_int("CGX_STENCIL_NT", 1);
+    p.ht = env_int("CGX_STENCIL_HALO_T", 1);
+    p.nstrips = (m + 2 * kNT - 1) / (2 * kNT);
+    p.rpi = std::max(1, env_int("CGX_STENCIL_ROWS", 8));
+    p.nitems = p.nstrips * ((mloc + p.rpi - 1) / p.rpi);
+    p.grid = 0;  // set per kernel from its occupancy (resident_grid)
+    return p;
+}
+
+// Every block resident at once (occupancy x CUs), capped by the work items
+// and the reduction slots; CGX_STENCIL_BLOCKS overrides.
+static int64_t resident_grid(const void *fn, int64_t nitems) {
+    int dev = 0, per_cu = 0;
+    (void)hipGetDevice(&dev);
+    static std::mutex mu;
+    static std::vector<std::pair<std::pair<const void *, int>, int>> cache;
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        for (auto &e : cache)
+            if (e.first.first == fn && e.first.second == dev) per_cu = e.second;
+        if (per_cu == 0) {
+            if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kNT, 0) != hipSuccess || per_cu <= 0)
+                per_cu = 4;
+            cache.push_back({{fn, dev}, per_cu});
+        }
+    }
+    int64_t g = (int64_t)per_cu * cu_count(dev);
+    g = env_int("CGX_STENCIL_BLOCKS", (int)g);
+    return std::max<int64_t>(1, std::min<int64_t>({g, nitems, kMaxRedBlocks}));
+}
+
+bool poisson_fusable(int64_t mloc, int64_t m) { return mloc > 0 && m > 0 && (m & 1) == 0; }
+
+template <int RB>
+static void launch_poisson_p(const PoissonPlan &pl, hipStream_t s, const double *rh, const double *poh, double *pnh,
+                             int64_t mloc, int64_t m, const double *rr, const double *rsold, int first, ConvArgs cv,
+                             double *pap_out, const RedWs &ws, ItemRanges ir, int add_to_out) {
+    auto fn = pl.nt ? (pl.ht ? k_poisson_p_f64<RB, true, true> : k_poisson_p_f64<RB, true, false>)
+                    : k_poisson_p_f64<RB, false, false>;
+    const int64_t grid = resident_grid(reinterpret_cast<const void *>(fn), ir.cnt1 + ir.cnt2);
+    hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(kNT), 0, s, rh, poh, pnh, mloc, m, pl.nstrips, pl.rpi, ir, rr,
+                       rsold, first, cv, pap_out, add_to_out, ws.partials, ws.tickets + T_MATVEC);
+}
+template <int RB>
+static void launch_poisson_xr(const PoissonPlan &pl, hipStream_t s, const double *pnh, double *x, double *r,
+                              int64_t mloc, int64_t m, const double *rsold, const double *pAp, double *rr_out,
+                              const RedWs &ws, const int64_t *gate) {
+    auto fn = pl.nt ? (pl.ht ? k_poisson_xr_f64<RB, true, true> : k_poisson_xr_f64<RB, true, false>)
+                    : k_poisson_xr_f64<RB, false, false>;
+    const int64_t grid = resident_grid(reinterpret_cast<const void *>(fn), pl.nitems);
+    hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(kNT), 0, s, pnh, x, r, mloc, m, pl.nstrips, pl.rpi,
+                       pl.nitems, env_int("CGX_STENCIL_REVERSE", 1), rsold, pAp, rr_out, ws.partials,
+                       ws.tickets + T_XR, gate);
+}
+
+hipError_t poisson_p_f64(const double *rh, const double *poh, double *pnh, int64_t mloc, int64_t m, const double *rr,
+                         const double *rsold, bool first, double *pap_out, const RedWs &ws, hipStream_t s, double eps,
+                         int64_t k, int64_t *kdone, double *rrfinal, int part, int64_t *hrec) {
+    if (!poisson_fusable(mloc, m) || !al16(rh) || !al16(pnh) || (!first && !al16(poh))) return hipErrorInvalidValue;
+    ConvArgs cv;
+    cv.eps = eps;
+    cv.k = k;
+    cv.kdone = kdone;
+    cv.rrfinal = rrfinal;
+    cv.hrec = hrec;
+    const PoissonPlan pl = poisson_plan(mloc, m);
+    const int64_t nruns = pl.nitems / pl.nstrips, ns = pl.nstrips;
+    // part 0: every item; 1: runs 1..nruns-2 (no halo row read); 2: runs 0 and
+    // nruns-1, adding to part 1's p.Ap when part 1 had items
+    ItemRanges ir{0, pl.nitems, 0, 0};
+    int add = 0;
+    if (part == 1) {
+        if (nruns <= 2) return hipSuccess;
+        ir = ItemRanges{ns, (nruns - 2) * ns, 0, 0};
+    } else if (part == 2) {
+        ir = ItemRanges{0, ns, (nruns - 1) * ns, nruns > 1 ? ns : 0};
+        add = nruns > 2;
+    }
+    switch (pl.rb) {
+        case 1: launch_poisson_p<1>(pl, s, rh, poh, pnh, mloc, m, rr, rsold, first, cv, pap_out, ws, ir, add); break;
+        case 2: launch_poisson_p<2>(pl, s, rh, poh, pnh, mloc, m, rr, rsold, first, cv, pap_out, ws, ir, add); break;
+        case 8: launch_poisson_p<8>(pl, s, rh, poh, pnh, mloc, m, rr, rsold, first, cv, pap_out, ws, ir, add); break;
+        default: launch_poisson_p<4>(pl, s, rh, poh, pnh, mloc, m, rr, rsold, first, cv, pap_out, ws, ir, add); break;
+    }
+    return hipGetLastError();
+}
+
+hipError_t poisson_xr_f64(const double *pnh, double *x, double *r, int64_t mloc, int64_t m, const double *rsold,
+                          const double *pAp, double *rr_out, const RedWs &ws, hipStream_t s, const int64_t *gate) {
+    if (!poisson_fusable(mloc, m) || !al16(pnh) || !al16(x) || !al16(r)) return hipErrorInvalidValue;
+    const PoissonPlan pl = poisson_plan(mloc, m);
+    switch (pl.rb) {
+        case 1: launch_poisson_xr<1>(pl, s, pnh, x, r, mloc, m, rsold, pAp, rr_out, ws, gate); break;
+        case 2: launch_poisson_xr<2>(pl, s, pnh, x, r, mloc, m, rsold, pAp, rr_out, ws, gate); break;
+        case 8: launch_poisson_xr<8>(pl, s, pnh, x, r, mloc, m, rsold, pAp, rr_out, ws, gate); break;
+        default: launch_poisson_xr<4>(pl, s, pnh, x, r, mloc, m, rsold, pAp, rr_out, ws, gate); break;
+    }
+    return hipGetLastError();
+}
+
+}  // namespace cgx

@@ -1,0 +1,380 @@
+// cgx_vector.hip -- the fp64 BLAS-1 kernels of the CG iteration (residual,
+// the x/r/p updates with the device-side stopping decision, dot), the
+// counter-hash SPD generator, fill and the rank-ordered scalar sum.
+// serialConjugate.c:122-177 (vecVec, scalarVec, vecAdd, vecSub) and :209-243.
+#include "cgx_device.h"
+
+namespace cgx {
+namespace {
+
+// residual x2 + vecVec (serialConjugate.c:210-212)
+template <bool VEC>
+__global__ __launch_bounds__(kNT) void k_residual_f64(int64_t n, const double *__restrict__ b,
+                                                      const double *__restrict__ Ax,
+                                                      double *__restrict__ r, double *__restrict__ p,
+                                                      double *rr_out, double *partials,
+                                                      unsigned *ticket) {
+    double acc = 0.0;
+    if constexpr (VEC) {
+        CGX_VEC_LOOP_BEGIN
+        d2 bv[kVU], av[kVU];
+#pragma unroll
+        for (int u = 0; u < kVU; ++u)
+            if (ok[u]) { const int64_t i = 2 * (base + u * kNT); bv[u] = ld2(b + i); av[u] = ld2(Ax + i); }
+#pragma unroll
+        for (int u = 0; u < kVU; ++u)
+            if (ok[u]) {
+                const int64_t i = 2 * (base + u * kNT);
+                const d2 ri = bv[u] - av[u];
+                st2(r + i, ri);
+                if (p) st2(p + i, ri);
+                acc += ri.x * ri.x + ri.y * ri.y;
+            }
+        CGX_VEC_LOOP_END
+        if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+            const double ri = b[n - 1] - Ax[n - 1];
+            r[n - 1] = ri;
+            if (p) p[n - 1] = ri;
+            acc += ri * ri;
+        }
+    } else {
+        for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kNT) {
+            const double ri = b[i] - Ax[i];
+            r[i] = ri;
+            if (p) p[i] = ri;
+            acc += ri * ri;
+        }
+    }
+    if (rr_out) grid_sum_last_block(acc, partials, ticket, rr_out);
+}
+
+// x += alpha p; r -= alpha Ap; r.r  (serialConjugate.c:219-234, conjgrad.m:8-11)
+template <bool VEC, int VP = 0>
+__global__ __launch_bounds__(kNT) void k_update_xr_f64(int64_t n, double *__restrict__ x,
+                                                       double *__restrict__ r,
+                                                       const double *__restrict__ p,
+                                                       const double *__restrict__ Ap,
+                                                       const double *rsold, const double *pAp,
+                                                       double *rr_out, double *partials,
+                                                       unsigned *ticket) {
+    const double alpha = *rsold / *pAp;
+    double acc = 0.0;
+    if constexpr (VEC) {
+        CGX_VEC_LOOP_BEGIN
+        d2 xv[kVU], rv[kVU], pv[kVU], av[kVU];
+#pragma unroll
+        for (int u = 0; u < kVU; ++u)
+            if (ok[u]) {
+                const int64_t i = 2 * (base + u * kNT);
+                xv[u] = ldv<VP>(x + i); rv[u] = ldv<VP>(r + i); pv[u] = ldv<VP>(p + i); av[u] = ldv<VP>(Ap + i);
+            }
+#pragma unroll
+        for (int u = 0; u < kVU; ++u)
+            if (ok[u]) {
+                const int64_t i = 2 * (base + u * kNT);
+                stv<VP>(x + i, xv[u] + alpha * pv[u]);
+                const d2 ri = rv[u] - alpha * av[u];
+                stv<VP>(r + i, ri);
+                acc += ri.x * ri.x + ri.y * ri.y;
+            }
+        CGX_VEC_LOOP_END
+        if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+            const int64_t i = n - 1;
+            x[i] = x[i] + alpha * p[i];
+            const double ri = r[i] - alpha * Ap[i];
+            r[i] = ri;
+            acc += ri * ri;
+        }
+    } else {
+        for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kNT) {
+            x[i] = x[i] + alpha * p[i];
+            const double ri = r[i] - alpha * Ap[i];
+            r[i] = ri;
+            acc += ri * ri;
+        }
+    }
+    grid_sum_last_block(acc, partials, ticket, rr_out);
+}
+
+// p = r + beta p  (serialConjugate.c:239-243, conjgrad.m:15)
+template <bool VEC, int VP = 0>
+__global__ __launch_bounds__(kNT) void k_update_p_f64(int64_t n, double *__restrict__ p,
+                                                      const double *__restrict__ r,
+                                                      const double *rr, const double *rsold) {
+    const double beta = *rr / *rsold;
+    if constexpr (VEC) {
+        CGX_VEC_LOOP_BEGIN
+        d2 pv[kVU], rv[kVU];
+#pragma unroll
+        for (int u = 0; u < kVU; ++u)
+            if (ok[u]) { const int64_t i = 2 * (base + u * kNT); pv[u] = ldv<VP>(p + i); rv[u] = ldv<VP>(r + i); }
+#pragma unroll
+        for (int u = 0; u < kVU; ++u)
+            if (ok[u]) stv<VP>(p + 2 * (base + u * kNT), rv[u] + beta * pv[u]);
+        CGX_VEC_LOOP_END
+        if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) p[n - 1] = r[n - 1] + beta * p[n - 1];
+    } else {
+        for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kNT)
+            p[i] = r[i] + beta * p[i];
+    }
+}
+
+// The solver's split of the x/r/p updates (fp64): x's update moves into the
+// p update, which reads p anyway -- 24 + 40 B per element instead of 48 + 24.
+// r -= alpha Ap; r.r   (alpha = rsold / pAp)
+template <bool VEC, int VP = 2>
+__global__ __launch_bounds__(kNT) void k_update_r_f64(int64_t n, double *__restrict__ r, const double *__restrict__ Ap,
+                                                      const double *rsold, const double *pAp, double *rr_out,
+                                                      double *partials, unsigned *ticket, const int64_t *gate) {
+    if (gate && *gate) return;
+    const double alpha = *rsold / *pAp;
+    double acc = 0.0;
+    if constexpr (VEC) {
+        CGX_VEC_LOOP_BEGIN
+        d2 rv[kVU], av[kVU];
+#pragma unroll
+        for (int u = 0; u < kVU; ++u)
+            if (ok[u]) { const int64_t i = 2 * (base + u * kNT); rv[u] = ldv<VP>(r + i); av[u] = ldv<VP>(Ap + i); }
+#pragma unroll
+        for (int u = 0; u < kVU; ++u)
+            if (ok[u]) {
+                const d2 ri = rv[u] - alpha * av[u];
+                stv<VP>(r + 2 * (base + u * kNT), ri);
+                acc += ri.x * ri.x + ri.y * ri.y;
+            }
+        CGX_VEC_LOOP_END
+        if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+            const double ri = r[n - 1] - alpha * Ap[n - 1];
+            r[n - 1] = ri;
+            acc += ri * ri;
+        }
+    } else {
+        for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kNT) {
+            const double ri = r[i] - alpha * Ap[i];
+            r[i] = ri;
+            acc += ri * ri;
+        }
+    }
+    grid_sum_last_block(acc, partials, ticket, rr_out);
+}
+
+// x += alpha p (alpha = rsold / pAp); then, if rr != nullptr, p = r + (rr / rsold) p.
+// With cv.kdone != nullptr (device-side gating) the kernel also makes the
+// reference's stopping decision, `sqrt(r.r) < EPSILON` (serialConjugate.c:235):
+// on convergence it does only the x update and records k+1 and r.r; in a
+// later iteration (kdone in (0, k]) it does nothing.
+
+template <bool VEC, int VP = 2>
+__global__ __launch_bounds__(kNT) void k_update_xp_f64(int64_t n, double *__restrict__ x, double *__restrict__ p,
+                                                       const double *__restrict__ r, const double *rsold,
+                                                       const double *pAp, const double *rr, ConvArgs cv) {
+    bool upd_p = rr != nullptr;
+    if (cv.kdone) {
+        const int64_t kd = *cv.kdone;
+        if (kd != 0 && kd <= cv.k) return;
+        const double rrn = *rr;
+        if (cv.eps >= 0.0 && sqrt(rrn) < cv.eps) {
+            upd_p = false;
+            if (blockIdx.x == 0 && threadIdx.x == 0) record_convergence(cv, cv.k + 1, rrn);
+        }
+    }
+    const double alpha = *rsold / *pAp;
+    const double beta = upd_p ? *rr / *rsold : 0.0;
+    if constexpr (VEC) {
+        CGX_VEC_LOOP_BEGIN
+        d2 xv[kVU], pv[kVU], rv[kVU];
+#pragma unroll
+        for (int u = 0; u < kVU; ++u)
+            if (ok[u]) {
+                const int64_t i = 2 * (base + u * kNT);
+                xv[u] = ldv<VP>(x + i);
+                pv[u] = ldv<VP>(p + i);
+                if (upd_p) rv[u] = ldv<VP>(r + i);
+            }
+#pragma unroll
+        for (int u = 0; u < kVU; ++u)
+            if (ok[u]) {
+                const int64_t i = 2 * (base + u * kNT);
+                stv<VP>(x + i, xv[u] + alpha * pv[u]);
+                if (upd_p) stv<VP>(p + i, rv[u] + beta * pv[u]);
+            }
+        CGX_VEC_LOOP_END
+        if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+            x[n - 1] = x[n - 1] + alpha * p[n - 1];
+            if (upd_p) p[n - 1] = r[n - 1] + beta * p[n - 1];
+        }
+    } else {
+        for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kNT) {
+            x[i] = x[i] + alpha * p[i];
+            if (upd_p) p[i] = r[i] + beta * p[i];
+        }
+    }
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(kNT) void k_dot_f64(int64_t n, const double *__restrict__ a,
+                                                 const double *__restrict__ b, double *out,
+                                                 double *partials, unsigned *ticket) {
+    double acc = 0.0;
+    if constexpr (VEC) {
+        CGX_VEC_LOOP_BEGIN
+        d2 av[kVU], bv[kVU];
+#pragma unroll
+        for (int u = 0; u < kVU; ++u)
+            if (ok[u]) { const int64_t i = 2 * (base + u * kNT); av[u] = ld2(a + i); bv[u] = ld2(b + i); }
+#pragma unroll
+        for (int u = 0; u < kVU; ++u)
+            if (ok[u]) acc += av[u].x * bv[u].x + av[u].y * bv[u].y;
+        CGX_VEC_LOOP_END
+        if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) acc += a[n - 1] * b[n - 1];
+    } else {
+        for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kNT)
+            acc += a[i] * b[i];
+    }
+    grid_sum_last_block(acc, partials, ticket, out);
+}
+
+// counter-hash SPD generator (generateSPDmatrix.m:4-17 distribution)
+// ---------------------------------------------------------------------------
+
+template <typename T>
+__global__ __launch_bounds__(kNT) void k_gen_spd(int64_t n, int64_t lda, int64_t row0, int64_t nrows,
+                                                 uint64_t salt, uint64_t salt_b, T *A, T *b) {
+#pragma clang fp contract(off)
+    for (int64_t rr = blockIdx.x; rr < nrows; rr += gridDim.x) {
+        const uint64_t i = (uint64_t)(row0 + rr);
+        T *row = A + rr * lda;
+        for (int64_t jj = threadIdx.x; jj < lda; jj += kNT) {
+            double val = 0.0;
+            if (jj < n) {
+                const uint64_t j = (uint64_t)jj;
+                val = 0.5 * (u01(salt, i, j) + u01(salt, j, i));
+                if (i == j) val = val + (double)n;
+            }
+            row[jj] = (T)val;
+        }
+        if (threadIdx.x == 0) {
+            const uint64_t h = mix64(i ^ salt_b);
+            b[rr] = (T)((double)(h >> 11) * 0x1.0p-53);
+        }
+    }
+}
+
+template <typename T>
+__global__ __launch_bounds__(kNT) void k_fill(T *p, int64_t n, T v) {
+    for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kNT) p[i] = v;
+}
+
+// Scalars combined in rank order: ((in0 + in1) + in2) + ...  Inputs sit in
+// 8-byte slots (a float at the slot start for F32_REF): element q at in[q*stride].
+
+template <typename T>
+__global__ void k_sum_ordered(const T *in, int cnt, int stride, T *out) {
+#pragma clang fp contract(off)
+    T s = in[0];
+    for (int q = 1; q < cnt; ++q) s = s + in[q * stride];
+    *out = s;
+}
+
+}  // namespace
+
+hipError_t residual_f64(int64_t n, const double *b, const double *Ax, double *r, double *p,
+                        double *rr_out, const RedWs &ws, hipStream_t s) {
+    const bool vec = al16(b) && al16(Ax) && al16(r) && al16(p);
+    hipLaunchKernelGGL(vec ? k_residual_f64<true> : k_residual_f64<false>, dim3(grid_vec(n)), dim3(kNT), 0, s, n, b,
+                       Ax, r, p, rr_out, ws.partials, ws.tickets + T_RESID);
+    return hipGetLastError();
+}
+
+hipError_t update_xr_f64(int64_t n, double *x, double *r, const double *p, const double *Ap,
+                         const double *rsold, const double *pAp, double *rr_out, const RedWs &ws,
+                         hipStream_t s) {
+    const bool vec = al16(x) && al16(r) && al16(p) && al16(Ap);
+    const int vp = env_int("CGX_VEC_POLICY", 2);
+    auto fn = !vec ? k_update_xr_f64<false> : vp == 1 ? k_update_xr_f64<true, 1>
+                                            : vp == 2 ? k_update_xr_f64<true, 2> : k_update_xr_f64<true, 0>;
+    hipLaunchKernelGGL(fn, dim3(grid_vec(n)), dim3(kNT), 0, s, n, x, r, p, Ap, rsold, pAp, rr_out, ws.partials,
+                       ws.tickets + T_XR);
+    return hipGetLastError();
+}
+
+hipError_t update_p_f64(int64_t n, double *p, const double *r, const double *rr, const double *rsold,
+                        hipStream_t s) {
+    const bool vec = al16(p) && al16(r);
+    const int vp = env_int("CGX_VEC_POLICY", 2);
+    auto fn = !vec ? k_update_p_f64<false> : vp == 1 ? k_update_p_f64<true, 1>
+                                           : vp == 2 ? k_update_p_f64<true, 2> : k_update_p_f64<true, 0>;
+    hipLaunchKernelGGL(fn, dim3(grid_vec(n)), dim3(kNT), 0, s, n, p, r, rr, rsold);
+    return hipGetLastError();
+}
+
+hipError_t update_r_f64(int64_t n, double *r, const double *Ap, const double *rsold, const double *pAp,
+                        double *rr_out, const RedWs &ws, hipStream_t s, const int64_t *gate) {
+    const bool vec = al16(r) && al16(Ap);
+    hipLaunchKernelGGL(vec ? k_update_r_f64<true> : k_update_r_f64<false>, dim3(grid_vec(n)), dim3(kNT), 0, s, n, r,
+                       Ap, rsold, pAp, rr_out, ws.partials, ws.tickets + T_XR, gate);
+    return hipGetLastError();
+}
+
+hipError_t update_xp_f64(int64_t n, double *x, double *p, const double *r, const double *rsold, const double *pAp,
+                         const double *rr, hipStream_t s, double eps, int64_t k, int64_t *kdone, double *rrfinal,
+                         int64_t *hrec) {
+    const bool vec = al16(x) && al16(p) && al16(r);
+    ConvArgs cv;
+    cv.eps = eps;
+    cv.k = k;
+    cv.kdone = kdone;
+    cv.rrfinal = rrfinal;
+    cv.hrec = hrec;
+    hipLaunchKernelGGL(vec ? k_update_xp_f64<true> : k_update_xp_f64<false>, dim3(grid_vec(n)), dim3(kNT), 0, s, n, x,
+                       p, r, rsold, pAp, rr, cv);
+    return hipGetLastError();
+}
+
+hipError_t dot_f64(int64_t n, const double *a, const double *b, double *out, const RedWs &ws,
+                   hipStream_t s) {
+    const bool vec = al16(a) && al16(b);
+    hipLaunchKernelGGL(vec ? k_dot_f64<true> : k_dot_f64<false>, dim3(grid_vec(n)), dim3(kNT), 0, s, n, a, b, out,
+                       ws.partials, ws.tickets + T_DOT);
+    return hipGetLastError();
+}
+
+hipError_t gen_spd_f64(int64_t n, int64_t lda, int64_t row0, int64_t nrows, uint64_t seed, double *A,
+                       double *b, hipStream_t s) {
+    if (nrows <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gen_spd<double>, dim3(grid_1d(nrows, 1, 65536)), dim3(kNT), 0, s, n, lda, row0,
+                       nrows, mix64(seed), mix64(seed + 1), A, b);
+    return hipGetLastError();
+}
+
+hipError_t gen_spd_f32(int64_t n, int64_t lda, int64_t row0, int64_t nrows, uint64_t seed, float *A,
+                       float *b, hipStream_t s) {
+    if (nrows <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_gen_spd<float>, dim3(grid_1d(nrows, 1, 65536)), dim3(kNT), 0, s, n, lda, row0,
+                       nrows, mix64(seed), mix64(seed + 1), A, b);
+    return hipGetLastError();
+}
+
+hipError_t fill_f64(double *p, int64_t n, double v, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_fill<double>, dim3(grid_vec(n)), dim3(kNT), 0, s, p, n, v);
+    return hipGetLastError();
+}
+
+hipError_t fill_f32(float *p, int64_t n, float v, hipStream_t s) {
+    if (n <= 0) return hipSuccess;
+    hipLaunchKernelGGL(k_fill<float>, dim3(grid_vec(n)), dim3(kNT), 0, s, p, n, v);
+    return hipGetLastError();
+}
+
+hipError_t sum_ordered_f64(const double *in, int cnt, double *out, hipStream_t s) {
+    hipLaunchKernelGGL(k_sum_ordered<double>, dim3(1), dim3(1), 0, s, in, cnt, 1, out);
+    return hipGetLastError();
+}
+
+hipError_t sum_ordered_f32(const float *in, int cnt, float *out, hipStream_t s) {
+    hipLaunchKernelGGL(k_sum_ordered<float>, dim3(1), dim3(1), 0, s, in, cnt, 2, out);
+    return hipGetLastError();
+}
+
+}  // namespace cgx
