@@ -183,6 +183,7 @@ int set_dev(const Shard &s) {
 
 int alloc_shard(cgx_ctx *c, Shard &s) {
     TRY(set_dev(s));
+    HIPT(preload_kernels());
     const size_t es = (size_t)c->es;
     HIPT(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
     HIPT(hipEventCreateWithFlags(&s.ev_sync, hipEventDisableTiming));

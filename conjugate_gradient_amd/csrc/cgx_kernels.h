@@ -3,6 +3,7 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
+#include <initializer_list>
 
 namespace cgx {
 
@@ -133,5 +134,22 @@ hipError_t update_p_ref_f32(int64_t n, float *p, const float *r, const float *rr
 hipError_t gen_spd_f32(int64_t n, int64_t lda, int64_t row0, int64_t nrows, uint64_t seed,
                        float *A, float *b, hipStream_t s);
 hipError_t sum_ordered_f32(const float *in, int cnt, float *out, hipStream_t s);
+
+// Each kernel file is its own code object, which HIP loads on a device at
+// the first use of one of its kernels.  preload_kernels() loads all of them
+// on the current device at context creation (overlapped with the CLI's file
+// parsing), so no first launch inside a timed solve pays for a load.
+hipError_t preload_matvec();
+hipError_t preload_vector();
+hipError_t preload_poisson();
+hipError_t preload_ref_f32();
+hipError_t preload_symv();
+inline hipError_t preload_kernels() {
+    for (auto f : {preload_matvec, preload_vector, preload_poisson, preload_ref_f32, preload_symv}) {
+        const hipError_t e = f();
+        if (e != hipSuccess) return e;
+    }
+    return hipSuccess;
+}
 
 }  // namespace cgx

@@ -742,4 +742,10 @@ hipError_t matvec_f64_cols(const MatvecPlan &pl, const double *A, int64_t lda, i
     return hipGetLastError();
 }
 
+// Load this file's code object on the current device now (see preload_kernels).
+hipError_t preload_matvec() {
+    hipFuncAttributes a;
+    return hipFuncGetAttributes(&a, reinterpret_cast<const void *>(k_matvec_f64<2, 8, 1, true>));
+}
+
 }  // namespace cgx

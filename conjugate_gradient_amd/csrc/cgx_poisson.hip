@@ -529,4 +529,10 @@ hipError_t poisson_xr_f64(const double *pnh, double *x, double *r, int64_t mloc,
     return hipGetLastError();
 }
 
+// Load this file's code object on the current device now (see preload_kernels).
+hipError_t preload_poisson() {
+    hipFuncAttributes a;
+    return hipFuncGetAttributes(&a, reinterpret_cast<const void *>(k_stencil5_strip_f64));
+}
+
 }  // namespace cgx

@@ -393,4 +393,10 @@ hipError_t update_p_ref_f32(int64_t n, float *p, const float *r, const float *rr
     return hipGetLastError();
 }
 
+// Load this file's code object on the current device now (see preload_kernels).
+hipError_t preload_ref_f32() {
+    hipFuncAttributes a;
+    return hipFuncGetAttributes(&a, reinterpret_cast<const void *>(k_matvec_ref_f32_r16));
+}
+
 }  // namespace cgx

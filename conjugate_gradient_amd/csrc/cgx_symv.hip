@@ -388,4 +388,10 @@ hipError_t gen_b_f64(int64_t n, uint64_t seed, double *b, hipStream_t s) {
     return hipGetLastError();
 }
 
+// Load this file's code object on the current device now (see preload_kernels).
+hipError_t preload_symv() {
+    hipFuncAttributes a;
+    return hipFuncGetAttributes(&a, reinterpret_cast<const void *>(k_symv_f64<1>));
+}
+
 }  // namespace cgx

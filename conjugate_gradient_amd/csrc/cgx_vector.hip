@@ -377,4 +377,10 @@ hipError_t sum_ordered_f32(const float *in, int cnt, float *out, hipStream_t s) 
     return hipGetLastError();
 }
 
+// Load this file's code object on the current device now (see preload_kernels).
+hipError_t preload_vector() {
+    hipFuncAttributes a;
+    return hipFuncGetAttributes(&a, reinterpret_cast<const void *>(k_fill<double>));
+}
+
 }  // namespace cgx

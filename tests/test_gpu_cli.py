@@ -46,6 +46,26 @@ def test_cli_fp32ref_reference_fixtures(golden, name, files):
     assert np.array_equal(x.view(np.uint32), golden_x(golden, name).view(np.uint32))
 
 
+def test_cli_full_teardown_same_output(golden, tmp_path):
+    """The default fast exit (no teardown after the output is flushed) and the
+    full teardown (CGX_CLI_FAST_EXIT=0) print the same x and exit 0; the phase
+    line reports which ran.  Stdout to a file checks the flush before _exit."""
+    paths = [os.path.join(FIX, f) for f in ("matrixA1.txt", "vectorb1.txt", "X0.txt")]
+    outs = {}
+    for mode in ("1", "0"):
+        dst = tmp_path / f"out{mode}.txt"
+        with open(dst, "w") as f:
+            r = subprocess.run([cg.CLI_PATH, "--fp32-ref", "--print-x", "--stats", *paths], stdout=f,
+                               stderr=subprocess.PIPE, text=True, timeout=300,
+                               env=dict(os.environ, CGX_CLI_FAST_EXIT=mode, CGX_CLI_TIMES="1"))
+        assert r.returncode == 0, r.stderr
+        assert f'"fast_exit": {mode}' in r.stderr
+        outs[mode] = dst.read_text().splitlines()
+    assert len(outs["1"]) == len(outs["0"]) and outs["1"][-4:] == outs["0"][-4:]
+    assert np.array_equal(printed_x("\n".join(outs["1"]), 4, np.float32).view(np.uint32),
+                          golden_x(golden, "kat4").view(np.uint32))
+
+
 def test_cli_dims_file_and_fp64(golden):
     paths = [os.path.join(FIX, f) for f in ("matrixA.txt", "vectorb.txt", "initialguess.txt")]
     out = run("--dims", os.path.join(FIX, "dimensions.txt"), "--eps", "1e-12", "--print-x", *paths)

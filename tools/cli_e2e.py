@@ -7,7 +7,8 @@ larger): generateSPDmatrix(n) written as the MATLAB script writes it
     reader) and its conjugrad() on the parsed system (serial_ref solve mode),
     single thread, timed separately;
   - cg_hip --fp32-ref --print-x on the same three files, wall time of the
-    whole program (parse + H2D + GPU solve + print).
+    whole program (parse + H2D + GPU solve + print), with its default fast
+    exit and with the full teardown (CGX_CLI_FAST_EXIT=0).
 The x vectors must be identical bit for bit.  oracle/_ref is the reference
 compiled here from its sources (it travels with the repo snapshot; the
 reference sources do not).
@@ -66,24 +67,46 @@ def main():
         res.update({"reference_initialize_s": t_init, "reference_conjugrad_process_s": t_solve,
                     "reference_total_s": t_init + t_solve, "reference_iterations": ref_iters,
                     "reference_stdout": out.strip().splitlines()[0]})
-        # cg_hip: the whole program
-        t0 = time.perf_counter()
-        proc = subprocess.run([cg.CLI_PATH, "--fp32-ref", "--print-x", "--stats", "--threads", str(a.threads),
-                               paths["A"], paths["b"], paths["x0"]], check=True, capture_output=True, text=True,
-                              env=dict(os.environ, CGX_CLI_TIMES="1"))
-        t_cli = time.perf_counter() - t0
-        out = proc.stdout
-        phases = [ln for ln in proc.stderr.splitlines() if ln.startswith("{")]
-        if phases:
-            res["cg_hip_phases_s"] = json.loads(phases[-1])
+        # cg_hip: the whole program, default (fast exit: no teardown after the
+        # output is flushed) and CGX_CLI_FAST_EXIT=0 (full teardown), alternating
+        runs = {"fast": [], "teardown": []}
+        phases = {}
+        out = ""
+        for rep in range(5):
+            for mode in ("fast", "teardown"):
+                env = dict(os.environ, CGX_CLI_TIMES="1", CGX_CLI_FAST_EXIT="1" if mode == "fast" else "0")
+                t0 = time.perf_counter()
+                proc = subprocess.run([cg.CLI_PATH, "--fp32-ref", "--print-x", "--stats", "--threads", str(a.threads),
+                                       paths["A"], paths["b"], paths["x0"]], check=True, capture_output=True,
+                                      text=True, env=env)
+                runs[mode].append(time.perf_counter() - t0)
+                ph = [ln for ln in proc.stderr.splitlines() if ln.startswith("{")]
+                if ph:
+                    rec = json.loads(ph[-1])
+                    rec["process_s"] = runs[mode][-1]
+                    rec["after_output_s"] = rec["process_s"] - rec["printed_s"]  # teardown + exit, as seen outside
+                    phases.setdefault(mode, []).append(rec)
+                if mode == "fast":
+                    out = proc.stdout
+        med = {k: sorted(v)[len(v) // 2] for k, v in runs.items()}
+        res["cg_hip_phases_s"] = phases.get("fast", [])
+        res["cg_hip_phases_full_teardown_s"] = phases.get("teardown", [])
+        for mode in ("fast", "teardown"):
+            aft = sorted(r["after_output_s"] for r in phases.get(mode, []))
+            if aft:
+                res[f"cg_hip_after_output_med_s_{mode}"] = aft[len(aft) // 2]
         lines = out.strip().splitlines()
         x = np.array([float(v) for v in lines[-n:]], dtype=np.float32)
         xr = np.fromfile(xref, dtype=np.float32)
-        res.update({"cg_hip_total_s": t_cli, "cg_hip_stdout_head": lines[:4],
+        t_cli = med["fast"]
+        res.update({"cg_hip_total_s": t_cli, "cg_hip_total_runs_s": runs["fast"],
+                    "cg_hip_total_full_teardown_s": med["teardown"],
+                    "cg_hip_total_full_teardown_runs_s": runs["teardown"], "cg_hip_stdout_head": lines[:4],
                     "x_bit_identical": bool(np.array_equal(x.view(np.uint32), xr.view(np.uint32))),
                     "speedup_total": (t_init + t_solve) / t_cli, "threads": a.threads,
                     "note": "reference_conjugrad_process_s includes the harness reading raw float files "
-                            "and embedding the system (n <= 8192); the reference itself is single-threaded"})
+                            "and embedding the system (n <= 8192); the reference itself is single-threaded; "
+                            "cg_hip times are medians of 5 alternating runs per mode"})
     print(json.dumps(res, indent=1))
     if a.out:
         with open(a.out, "w") as f:
