@@ -1,4 +1,4 @@
-"""Rank mode (one process per rank, RCCL) at world size 2 and 4 on one GPU.
+"""Rank mode (one process per rank, RCCL) at world size 2, 4 and 8 on one GPU.
 
 The driver's N = 2/4/8 bench runs use one process per GPU over RCCL.  One
 GPU box cannot run that placement (RCCL refuses two ranks on one device of
@@ -128,6 +128,38 @@ def test_rank_mode_poisson_halo(tmp_path, mode):
                                    max_iter=-1 if eps > 0 else 120)
     assert res[0]["iterations"] == so.iterations
     assert rel(x, xo) <= (TOL if eps > 0 else 1e-9)
+
+
+@pytest.mark.timeout(240)
+@pytest.mark.parametrize("mode", ["collective", "p2p", "deterministic", "f32ref", "poisson_eps"])
+def test_rank_mode_world8(tmp_path, mode):
+    """The driver's largest placement, 8 ranks (here on one GPU): 8 row
+    blocks of 128 / 256 rows, the p2p pattern's 7 sends per exchange, 8
+    gathered partials, 8 Poisson slabs of 16 rows."""
+    P = 8
+    if mode == "poisson_eps":
+        m = 128
+        x, res = run_ranks(tmp_path, mode, m, P, timeout=200)
+        xo, so = oracle.cg_poisson_f64(m, np.ones(m * m), np.zeros(m * m), eps=1e-8, max_iter=-1)
+        assert res[0]["iterations"] == so.iterations and rel(x, xo) <= TOL
+        return
+    n = 2048 if mode == "f32ref" else 1024
+    x, res = run_ranks(tmp_path, mode, n, P, timeout=200)
+    assert res[0]["nrows"] == n // P
+    if mode == "f32ref":
+        A, b, x0 = case(f"spd{n}")
+        xo, so = oracle.cg_f32ref(A, b, x0, eps=1e-6, nparts=P)
+        assert res[0]["iterations"] == so.iterations
+        assert np.array_equal(x.view(np.uint32), xo.view(np.uint32))
+        return
+    A, b, x0 = case(f"spd{n}", np.float64)
+    xo, so = oracle.cg_f64(A, b, x0, eps=1e-10)
+    assert res[0]["iterations"] == so.iterations
+    assert rel(x, xo) <= TOL and res[0]["relres"] <= TOL
+    if mode == "deterministic":
+        xs = x0.copy()
+        cg.conjugrad(A, b, xs, eps=1e-10, shards=[0] * P)
+        assert np.array_equal(x, xs)
 
 
 @pytest.mark.timeout(240)
