@@ -272,12 +272,9 @@ int alloc_shard(cgx_ctx *c, Shard &s) {
     if (c->mode == M_RCCL && c->nranks > 1) TRY(dmalloc(&s.xfull, xlen * es));
     char *part = nullptr, *tick = nullptr;
     TRY(dmalloc(&part, kMaxRedBlocks * sizeof(double)));
+    s.ws.partials = reinterpret_cast<double *>(part);  // owned by the shard from here (free_shard)
     TRY(dmalloc(&tick, kTickets * sizeof(unsigned)));
-    s.ws.partials = reinterpret_cast<double *>(part);
     s.ws.tickets = reinterpret_cast<unsigned *>(tick);
-    // b = 0 with one of our own kernels: the first launch from libcgx's code
-    // object loads it (several ms for all the kernel variants), so that cost
-    // lands in context creation, not in the first solve's timing.
     if (es == 4) HIPT(fill_f32(reinterpret_cast<float *>(s.b), s.nloc, 0.0f, s.stream));
     else HIPT(fill_f64(reinterpret_cast<double *>(s.b), s.nloc, 0.0, s.stream));
     HIPT(hipMemsetAsync(s.x, 0, s.nloc * es, s.stream));
@@ -1174,10 +1171,17 @@ int dev_ws(RedWs *out) {
     HIPT(hipGetDevice(&dev));
     if (dev < 0 || dev >= 64) return fail(CGX_ERR_ARG, "device id %d out of range", dev);
     std::lock_guard<std::mutex> lk(g_ws_mu);
-    if (!g_ws[dev].partials) {
-        HIPT(hipMalloc(&g_ws[dev].partials, kMaxRedBlocks * sizeof(double)));
-        HIPT(hipMalloc(&g_ws[dev].tickets, kTickets * sizeof(unsigned)));
-        HIPT(hipMemset(g_ws[dev].tickets, 0, kTickets * sizeof(unsigned)));
+    if (!g_ws[dev].partials) {  // both buffers, or neither (a failed call leaves nothing half-made)
+        RedWs w{nullptr, nullptr};
+        hipError_t e = hipMalloc(&w.partials, kMaxRedBlocks * sizeof(double));
+        if (e == hipSuccess) e = hipMalloc(&w.tickets, kTickets * sizeof(unsigned));
+        if (e == hipSuccess) e = hipMemset(w.tickets, 0, kTickets * sizeof(unsigned));
+        if (e != hipSuccess) {
+            if (w.partials) (void)hipFree(w.partials);
+            if (w.tickets) (void)hipFree(w.tickets);
+            return fail(CGX_ERR_NOMEM, "reduction workspace on device %d: %s", dev, hipGetErrorString(e));
+        }
+        g_ws[dev] = w;
     }
     *out = g_ws[dev];
     return CGX_OK;

@@ -217,7 +217,10 @@ int cgx_get_matvec_plan(cgx_ctx *ctx, int *rows_per_wave, int *chunks_in_flight,
 int cgx_residual_norm(cgx_ctx *ctx, double *rnorm, double *bnorm);
 
 /* ---- kernel-level entry points (device pointers; unit parity) -------------- */
-/* dtype: CGX_F64 or CGX_F32_REF.  stream: hipStream_t or NULL. */
+/* dtype: CGX_F64 or CGX_F32_REF.  stream: hipStream_t or NULL.
+ * The reducing calls (cgx_dot, cgx_residual, cgx_update_xr) share one
+ * reduction workspace per device: issue them on one stream per device (or
+ * order the streams), as the reference's single-threaded calls are ordered. */
 int cgx_dev_malloc(void **ptr, size_t bytes);
 int cgx_dev_free(void *ptr);
 int cgx_memcpy_h2d(void *dst, const void *src, size_t bytes);
