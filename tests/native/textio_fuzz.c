@@ -1,0 +1,178 @@
+/*
+ * textio_fuzz.c -- randomized check of cgx_text_read (conjugate_gradient_amd/
+ * csrc/cgx_textio.c) under AddressSanitizer / UndefinedBehaviorSanitizer
+ * (built by tests/test_textio_fuzz.py on the host; test infrastructure).
+ *
+ * Each case writes a file of random tokens -- well-formed numbers of every
+ * shape the fast path and the strtod/strtof fallback take (long mantissas,
+ * big exponents, float midpoints, subnormals, inf/nan, hex), and malformed
+ * ones -- separated by random runs of the accepted separators, sometimes
+ * with a UTF-8 BOM, sometimes without a trailing separator, sometimes padded
+ * so the file ends exactly on a page boundary.  Expected values come from
+ * strtof / strtod on each token (what fscanf("%f") does in
+ * serialConjugate.c:96); the reader must return them bit for bit, for 1 and
+ * several threads, or -3 when a token in the requested range is not a whole
+ * number, or -2 when the file holds fewer numbers than requested.
+ *
+ *   textio_fuzz <tmpdir> <cases> <seed>     exit 0 = all cases passed
+ */
+#define _GNU_SOURCE
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <unistd.h>
+
+#include "cgx_textio.h"
+
+static uint64_t g_s;
+static uint64_t rnd(void) {
+    g_s ^= g_s << 13;
+    g_s ^= g_s >> 7;
+    g_s ^= g_s << 17;
+    return g_s;
+}
+static int rint_(int n) { return (int)(rnd() % (uint64_t)n); }
+
+static int digits(char *o, int n, int nonzero_first) {
+    for (int i = 0; i < n; ++i) o[i] = (char)('0' + ((i == 0 && nonzero_first) ? 1 + rint_(9) : rint_(10)));
+    return n;
+}
+
+/* a random token into o (NUL-terminated); returns its length */
+static int token(char *o) {
+    static const char *special[] = {"nan", "-inf", "inf", "INF", "0x1p3", "1e", "--1", "1.2.3", ".", "e5", "+",
+                                    "1e+", "0.5f", "3.4028235e38", "3.4028236e38", "1.17549435e-38",
+                                    "1e-45", "7.006492e-46", "2.5e-324", "1.7976931348623157e308", "1e309",
+                                    "0.1", "-0", "-0.0e0", "16777217", "0.3333333432674408"};
+    const int kind = rint_(20);
+    if (kind == 0) return sprintf(o, "%s", special[rint_((int)(sizeof special / sizeof *special))]);
+    int n = 0;
+    if (rint_(3) == 0) o[n++] = rint_(2) ? '-' : '+';
+    if (kind == 1) { /* a long mantissa */
+        n += digits(o + n, 20 + rint_(280), 1);
+    } else if (kind == 2) { /* a float rounding midpoint, printed exactly */
+        const float f = (float)(rnd() % 1000000) / 1024.0f + 1.0f;
+        const double mid = (double)f + (double)(nextafterf(f, 2 * f) - f) / 2.0;
+        n += sprintf(o + n, "%.17g", mid);
+    } else {
+        if (rint_(8)) n += digits(o + n, 1 + rint_(kind == 3 ? 19 : 8), rint_(2));
+        if (rint_(2)) {
+            o[n++] = '.';
+            n += digits(o + n, rint_(kind == 4 ? 25 : 8), 0);
+        }
+        if (rint_(3) == 0) {
+            o[n++] = rint_(2) ? 'e' : 'E';
+            if (rint_(2)) o[n++] = rint_(2) ? '-' : '+';
+            n += digits(o + n, rint_(4), 0);
+        }
+        if (n == 0) o[n++] = '7';
+    }
+    o[n] = '\0';
+    return n;
+}
+
+static const char kSeps[] = " \n\r\t,;";
+
+int main(int argc, char **argv) {
+    if (argc != 4) return 2;
+    const char *dir = argv[1];
+    const int cases = atoi(argv[2]);
+    g_s = 0x9E3779B97F4A7C15ull ^ (uint64_t)atoll(argv[3]);
+    char path[4096];
+    snprintf(path, sizeof path, "%s/fuzz_%d.txt", dir, (int)getpid());
+    enum { kMaxTok = 400 };
+    static char toks[kMaxTok][320];
+    int fails = 0, n_malformed = 0, n_short = 0, n_page = 0, n_slow = 0;
+    for (int c = 0; c < cases; ++c) {
+        const int nt = 1 + rint_(kMaxTok - 1);
+        const int clean = rint_(3) != 0; /* mostly files whose tokens are all numbers */
+        FILE *f = fopen(path, "wb");
+        if (!f) return 2;
+        long bytes = 0;
+        if (rint_(10) == 0) bytes += fprintf(f, "\xEF\xBB\xBF");
+        int ntok = 0;
+        for (int i = 0; i < nt; ++i) {
+            char *t = toks[ntok];
+            int len;
+            for (;;) { /* clean files: only tokens strtod consumes whole */
+                len = token(t);
+                if (!clean) break;
+                char *stop;
+                (void)strtod(t, &stop);
+                if (stop == t + len) break;
+            }
+            bytes += fprintf(f, "%s", t);
+            ++ntok;
+            const int last = i == nt - 1;
+            if (!last || rint_(4)) { /* separators (none after the last token sometimes) */
+                const int ns = 1 + (rint_(4) == 0 ? rint_(3) : 0);
+                for (int q = 0; q < ns; ++q) {
+                    fputc(kSeps[rint_((int)sizeof kSeps - 1)], f);
+                    ++bytes;
+                }
+            }
+        }
+        if (rint_(8) == 0) { /* end exactly on a page boundary, last token touching it */
+            const long pad = (4096 - (bytes + 1) % 4096) % 4096;
+            for (long q = 0; q < pad; ++q) fputc(' ', f);
+            ++n_page;
+            fputc('5', f);
+            snprintf(toks[ntok++], 320, "5");
+        }
+        fclose(f);
+        if (cgx_text_count(path) != ntok) {
+            fprintf(stderr, "case %d: count %lld != %d\n", c, (long long)cgx_text_count(path), ntok);
+            ++fails;
+            continue;
+        }
+        const int64_t want = rint_(5) == 0 ? ntok + 1 + rint_(3) : 1 + rint_(ntok);
+        for (int as_float = 0; as_float < 2; ++as_float) {
+            int exp_rc = 0;
+            double *ed = calloc((size_t)want + 1, sizeof(double));
+            float *ef = calloc((size_t)want + 1, sizeof(float));
+            for (int64_t i = 0; i < want && i < ntok; ++i) {
+                char *stop;
+                const size_t len = strlen(toks[i]);
+                if (as_float) ef[i] = strtof(toks[i], &stop);
+                else ed[i] = strtod(toks[i], &stop);
+                if (stop != toks[i] + len && exp_rc == 0) exp_rc = -3;
+            }
+            if (want > ntok && exp_rc == 0) exp_rc = -2;
+            if (as_float == 0) {
+                n_malformed += exp_rc == -3;
+                n_short += exp_rc == -2;
+                for (int64_t i = 0; i < want && i < ntok; ++i) n_slow += strlen(toks[i]) > 20;
+            }
+            for (int threads = 1; threads <= 5; threads += 4) {
+                void *out = calloc((size_t)want + 1, 8);
+                const int rc = cgx_text_read(path, want, as_float, out, threads);
+                int bad = 0;
+                if ((rc == 0) != (exp_rc == 0) || (exp_rc == -2 && rc != -2)) bad = 1;
+                if (rc == 0 && exp_rc == 0)
+                    for (int64_t i = 0; i < want; ++i) {
+                        const int same = as_float ? !memcmp((float *)out + i, ef + i, 4) : !memcmp((double *)out + i, ed + i, 8);
+                        if (!same) {
+                            fprintf(stderr, "case %d token %lld '%s' (%s, %d threads): value differs\n", c,
+                                    (long long)i, toks[i], as_float ? "float" : "double", threads);
+                            bad = 1;
+                            break;
+                        }
+                    }
+                if (bad) {
+                    fprintf(stderr, "case %d: rc %d expected %d (want %lld of %d, %s, %d threads)\n", c, rc, exp_rc,
+                            (long long)want, ntok, as_float ? "float" : "double", threads);
+                    ++fails;
+                }
+                free(out);
+            }
+            free(ed);
+            free(ef);
+        }
+    }
+    unlink(path);
+    printf("cases %d failures %d (malformed %d, short %d, page-end %d, long tokens %d)\n", cases, fails,
+           n_malformed, n_short, n_page, n_slow);
+    return fails ? 1 : 0;
+}
