@@ -28,6 +28,7 @@
  * outside the diagonal tiles is not read).
  */
 #define _POSIX_C_SOURCE 200809L
+#include <errno.h>
 #include <pthread.h>
 #include <stdint.h>
 #include <stdio.h>
@@ -100,6 +101,25 @@ static void *create_ctx(void *arg) {
     return NULL;
 }
 
+/* Whole-string numeric option values: "--eps abc" or "--gpus 2x" is an
+ * error (exit 2), not a silent 0. */
+static int opt_ll(const char *name, const char *v, long long *out) {
+    char *end = NULL;
+    errno = 0;
+    const long long x = strtoll(v, &end, 10);
+    if (!*v || *end || errno) { fprintf(stderr, "%s: not an integer: '%s'\n", name, v); return 0; }
+    *out = x;
+    return 1;
+}
+static int opt_double(const char *name, const char *v, double *out) {
+    char *end = NULL;
+    errno = 0;
+    const double x = strtod(v, &end);
+    if (!*v || *end || errno) { fprintf(stderr, "%s: not a number: '%s'\n", name, v); return 0; }
+    *out = x;
+    return 1;
+}
+
 int main(int argc, char **argv) {
     const double t_prog0 = now_s();
     int gpus = 1, fp32ref = 0, symmetric = 0, print_x = 0, stats = 0;
@@ -112,20 +132,31 @@ int main(int argc, char **argv) {
     const char *pos[3];
     int npos = 0;
 
+    long long v = 0;
     for (int i = 1; i < argc; ++i) {
         const char *a = argv[i];
         int has_val = (i + 1 < argc);
-        if (!strcmp(a, "--gpus") && has_val) gpus = atoi(argv[++i]);
-        else if (!strcmp(a, "--fp32-ref")) fp32ref = 1;
+        if (!strcmp(a, "--gpus") && has_val) {
+            if (!opt_ll(a, argv[++i], &v)) return 2;
+            gpus = (v < 0 || v > 1000) ? -1 : (int)v;
+        } else if (!strcmp(a, "--fp32-ref")) fp32ref = 1;
         else if (!strcmp(a, "--symmetric")) symmetric = 1;
-        else if (!strcmp(a, "--eps") && has_val) eps = strtod(argv[++i], NULL);
-        else if (!strcmp(a, "--max-iter") && has_val) max_iter = strtoll(argv[++i], NULL, 10);
-        else if (!strcmp(a, "--dims") && has_val) dims_path = argv[++i];
-        else if (!strcmp(a, "--n") && has_val) n_opt = strtoll(argv[++i], NULL, 10);
-        else if (!strcmp(a, "--threads") && has_val) threads = atoi(argv[++i]);
-        else if (!strcmp(a, "--spd") && has_val) spd_n = strtoll(argv[++i], NULL, 10);
-        else if (!strcmp(a, "--seed") && has_val) seed = strtoull(argv[++i], NULL, 10);
-        else if (!strcmp(a, "--print-x")) print_x = 1;
+        else if (!strcmp(a, "--eps") && has_val) {
+            if (!opt_double(a, argv[++i], &eps)) return 2;
+        } else if (!strcmp(a, "--max-iter") && has_val) {
+            if (!opt_ll(a, argv[++i], &max_iter)) return 2;
+        } else if (!strcmp(a, "--dims") && has_val) dims_path = argv[++i];
+        else if (!strcmp(a, "--n") && has_val) {
+            if (!opt_ll(a, argv[++i], &n_opt)) return 2;
+        } else if (!strcmp(a, "--threads") && has_val) {
+            if (!opt_ll(a, argv[++i], &v)) return 2;
+            threads = v < 1 ? 1 : (v > 256 ? 256 : (int)v);
+        } else if (!strcmp(a, "--spd") && has_val) {
+            if (!opt_ll(a, argv[++i], &spd_n)) return 2;
+        } else if (!strcmp(a, "--seed") && has_val) {
+            if (!opt_ll(a, argv[++i], &v)) return 2;
+            seed = (unsigned long long)v;
+        } else if (!strcmp(a, "--print-x")) print_x = 1;
         else if (!strcmp(a, "--stats")) stats = 1;
         else if (!strcmp(a, "-h") || !strcmp(a, "--help")) { usage(argv[0]); return 0; }
         else if (a[0] == '-' && a[1] == '-') { usage(argv[0]); return 2; }

@@ -129,6 +129,14 @@ def test_cli_not_divisible(built):
     assert r.returncode == 1 and "4 is not divisible by 3" in r.stdout  # parallel_cg.c:88
 
 
+@pytest.mark.parametrize("opt,val", [("--eps", "abc"), ("--gpus", "2x"), ("--n", "12.5"), ("--max-iter", ""),
+                                     ("--seed", "0x"), ("--threads", "four")])
+def test_cli_rejects_non_numeric_options(built, opt, val):
+    f = [os.path.join(FIX, n) for n in ("matrixA1.txt", "vectorb1.txt", "X0.txt")]
+    r = run_cli(opt, val, *f)
+    assert r.returncode == 2 and opt in r.stderr, r.stdout + r.stderr
+
+
 def test_cli_dims_file(built, tmp_path):
     d = tmp_path / "dims.txt"
     d.write_text("3\n2\n3\n1\n")
