@@ -27,7 +27,9 @@ HBM bytes per launch from rocprofv3 PMC counters (profiles/pmc_summary.json,
 FETCH_SIZE doubled per the gfx950 correction) when a summary for this
 workload exists, else null.  `cpu_baseline` times the oracle's fp32-ref
 restatement of serialConjugate.c (bit-identical to it, tests/test_oracle.py)
-on one host core, on a bounded sample: 5 iterations of the same system (~10 s).
+on one host core, on a bounded sample: 5 iterations of the same system (~10 s);
+`cpu_baseline_reference` runs serialConjugate.c itself (oracle/_ref, built
+from the reference's sources) at its compiled N=8192 in the same run.
 """
 from __future__ import annotations
 
@@ -157,6 +159,51 @@ def cpu_baseline_mt(n: int, iters: int = 3, threads: int = 16) -> dict:
         "sample": (f"{iters} CG iterations of the same N={n} system in fp64 (oracle_cg_f64, matVec rows split over "
                    f"{threads} threads; not the reference's algorithm order), loop {st.t_loop_s:.2f} s"),
         "matvec_gbps_est": iters * 8.0 * n * n / st.t_loop_s / 1e9,
+    }
+
+
+def cpu_baseline_reference(n_ref: int = 8192, n_bench: int = 65536) -> dict | None:
+    """serialConjugate.c itself (unmodified, compiled by oracle/Makefile into
+    oracle/_ref/serial_ref), timed in the same run on this host: its
+    conjugrad() at its compiled size ROWS=8192 (serialConjugate.c:29) on the
+    same generator's fp32 system, to convergence (EPSILON 1e-6), timed by its
+    own clock() line (serialConjugate.c:208,249-251; the initial residual
+    matVec included).  None when the reference build is absent."""
+    import re
+    import subprocess
+    import tempfile
+
+    import numpy as np
+
+    import oracle
+    exe = oracle.ref_binary()
+    if not exe:
+        return None
+    oracle.set_threads(16)
+    A, b = oracle.spd_hash(n_ref, seed=SEED, dtype=np.float32)
+    with tempfile.TemporaryDirectory(dir="/tmp") as td:
+        paths = [os.path.join(td, k) for k in ("A.f32", "b.f32", "x0.f32", "x.f32")]
+        A.tofile(paths[0])
+        b.tofile(paths[1])
+        np.zeros(n_ref, np.float32).tofile(paths[2])
+        del A
+        out = subprocess.run([exe, str(n_ref), *paths], check=True, capture_output=True, text=True,
+                             timeout=300).stdout
+    t = float(re.search(r"average clock execution time in seconds: ([0-9.eE+-]+)", out).group(1))
+    k = int(re.search(r"iterations (\d+)", out).group(1))
+    value = k / t
+    return {
+        "value": value,
+        "unit": "iterations/s",
+        "cores": 1,
+        "kind": "reference",
+        "n": n_ref,
+        "sample": (f"serialConjugate.c unmodified (oracle/_ref/serial_ref) at its compiled N={n_ref}, fp32, the same "
+                   f"generator's system: {k} loop iterations plus the initial residual matVec in {t:.3f} s by its own "
+                   f"clock() line, single thread"),
+        "matvec_gbps_est": (k + 1) * 4.0 * n_ref * n_ref / t / 1e9,
+        # per-iteration work is the N^2 matVec: the same core at the bench's N
+        "scaled_to_bench_n": value * (n_ref / n_bench) ** 2,
     }
 
 
@@ -354,6 +401,9 @@ def main(argv=None) -> int:
     elif world == 1 and not args.no_cpu and not stream and not symmetric:
         out["cpu_baseline"] = cpu_baseline(args.cpu_n or n)
         out["cpu_baseline_mt"] = cpu_baseline_mt(args.cpu_n or n)
+        ref = cpu_baseline_reference(n_bench=n)
+        if ref:
+            out["cpu_baseline_reference"] = ref
     print(json.dumps(out), flush=True)
     if dist:
         dist.barrier()

@@ -129,3 +129,20 @@ def test_poisson_oracle_is_the_laplacian():
     xn, itn = oracle.conjgrad_numpy(A, b, np.zeros(m * m), tol=1e-10)
     assert st.iterations == itn
     assert np.linalg.norm(x - xn) <= 1e-12 * np.linalg.norm(xn)
+
+
+def test_bench_reference_baseline_leg():
+    """bench.py's cpu_baseline_reference: serialConjugate.c itself (oracle/_ref)
+    at its compiled N=8192 on the bench generator's fp32 system; the same
+    loop count as the bit-exact restatement on that system."""
+    if not oracle.ref_binary():
+        pytest.skip("oracle/_ref/serial_ref not built (no /root/reference here)")
+    import os
+    import sys
+    sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+    import bench
+    r = bench.cpu_baseline_reference()
+    assert r["kind"] == "reference" and r["cores"] == 1 and r["n"] == 8192 and r["value"] > 0
+    A, b = oracle.spd_hash(8192, seed=bench.SEED, dtype=np.float32)
+    _, st = oracle.cg_f32ref(A, b, np.zeros(8192, np.float32), eps=1e-6)
+    assert f"{st.iterations} loop iterations" in r["sample"]
