@@ -95,6 +95,7 @@ enum Op { OP_DENSE = 0, OP_POISSON = 1 };
 enum State { ST_IDLE = 0, ST_BEGUN = 1, ST_CONVERGED = 2 };
 
 constexpr int kEvPairs = 256;
+constexpr size_t kXStageMax = 64u << 20;
 constexpr int kStreamBufs = 3;
 constexpr int kMaxCopyStreams = 4;
 
@@ -113,6 +114,10 @@ struct Shard {
     bool x_zero = true;  // x is known to be all zeros (x0 = 0: the first A x is skipped)
     RedWs ws{nullptr, nullptr};
     double *h_pin = nullptr;
+    // pinned staging for cgx_get_x (x of this shard, or all of x in rank
+    // mode), allocated with the context so the first D2H of a solve's result
+    // does not set up HIP's pageable-copy path (~7 ms); null above kXStageMax
+    char *h_x = nullptr;
     // convergence record {kdone, bits of r.r there} in host-mapped coherent
     // memory: the deciding kernel stores it, the host reads it after an event
     int64_t *h_rec = nullptr, *d_rec = nullptr;
@@ -183,7 +188,14 @@ int set_dev(const Shard &s) {
 
 int alloc_shard(cgx_ctx *c, Shard &s) {
     TRY(set_dev(s));
-    HIPT(preload_kernels());
+    {  // the code objects this context launches from (fp64 residual checks use the vector kernels too)
+        unsigned set = PL_VECTOR;
+        if (c->op == OP_POISSON) set |= PL_POISSON;
+        else if (f32ref(c)) set |= PL_REF_F32;
+        else if (c->flags & CGX_SYMMETRIC) set |= PL_SYMV;
+        else set |= PL_MATVEC;
+        HIPT(preload_kernels(set));
+    }
     const size_t es = (size_t)c->es;
     HIPT(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
     HIPT(hipEventCreateWithFlags(&s.ev_sync, hipEventDisableTiming));
@@ -285,6 +297,17 @@ int alloc_shard(cgx_ctx *c, Shard &s) {
     HIPT(hipMemsetAsync(s.ws.tickets, 0, kTickets * sizeof(unsigned), s.stream));
     if (s.xfull) HIPT(hipMemsetAsync(s.xfull, 0, xlen * es, s.stream));
     HIPT(hipHostMalloc(reinterpret_cast<void **>(&s.h_pin), 8 * (8 + kLookRing), hipHostMallocDefault));
+    {
+        const size_t xb = (size_t)(s.xfull ? xlen : s.nloc) * es;
+        if (xb <= kXStageMax) {
+            HIPT(hipHostMalloc(reinterpret_cast<void **>(&s.h_x), xb ? xb : 16, hipHostMallocDefault));
+            // one device-to-host copy now: the first one of a process sets up
+            // the copy path (~8 ms, measured in cg_hip's get_x), which would
+            // otherwise land on the first cgx_get_x
+            HIPT(hipMemcpyAsync(s.h_x, s.pfull, std::min<size_t>(xb, (size_t)plen * es), hipMemcpyDeviceToHost,
+                                s.stream));
+        }
+    }
     HIPT(hipHostMalloc(reinterpret_cast<void **>(&s.h_rec), 16, hipHostMallocMapped | hipHostMallocCoherent));
     HIPT(hipHostGetDevicePointer(reinterpret_cast<void **>(&s.d_rec), s.h_rec, 0));
     s.h_rec[0] = s.h_rec[1] = 0;
@@ -308,6 +331,7 @@ void free_shard(Shard &s) {
     if (s.ws.partials) (void)hipFree(s.ws.partials);
     if (s.ws.tickets) (void)hipFree(s.ws.tickets);
     if (s.h_pin) (void)hipHostFree(s.h_pin);
+    if (s.h_x) (void)hipHostFree(s.h_x);
     if (s.h_rec) (void)hipHostFree(s.h_rec);
     for (auto e : s.ev_t) (void)hipEventDestroy(e);
     if (s.ev_sync) (void)hipEventDestroy(s.ev_sync);
@@ -1462,6 +1486,12 @@ int cgx_set_rows(cgx_ctx *c, int64_t row0, int64_t nrows, const void *A_rows, in
                 HIPT(sym_pack_f64(reinterpret_cast<const double *>(s.sym_stage), c->lda, i0, k, c->n, c->lda,
                                   reinterpret_cast<double *>(s.A), s.stream));
             }
+        } else if (A_rows && lda_host == c->lda && c->lda == c->n) {
+            // same row pitch on both sides: one contiguous copy (a pitched copy
+            // of the same bytes ran at a third of the rate from pinned memory)
+            HIPT(hipMemcpyAsync(s.A + (size_t)(lo - s.row0) * c->lda * es,
+                                static_cast<const char *>(A_rows) + (size_t)(lo - row0) * lda_host * es,
+                                (size_t)(hi - lo) * c->lda * es, hipMemcpyHostToDevice, s.stream));
         } else if (A_rows)
             HIPT(hipMemcpy2DAsync(s.A + (size_t)(lo - s.row0) * c->lda * es, (size_t)c->lda * es,
                                   static_cast<const char *>(A_rows) + (size_t)(lo - row0) * lda_host * es,
@@ -1557,15 +1587,20 @@ int cgx_get_x(cgx_ctx *c, void *x) {
         Shard &s = c->sh[0];
         TRY(set_dev(s));
         NCCLT(ncclAllGather(s.x, s.xfull, (size_t)s.nloc, f32ref(c) ? ncclFloat : ncclDouble, s.comm, s.stream));
-        HIPT(hipMemcpyAsync(x, s.xfull, (size_t)c->n * es, hipMemcpyDeviceToHost, s.stream));
+        HIPT(hipMemcpyAsync(s.h_x ? s.h_x : x, s.xfull, (size_t)c->n * es, hipMemcpyDeviceToHost, s.stream));
         HIPT(hipStreamSynchronize(s.stream));
+        if (s.h_x) std::memcpy(x, s.h_x, (size_t)c->n * es);
         return CGX_OK;
     }
     for (auto &s : c->sh) {
         TRY(set_dev(s));
-        HIPT(hipMemcpyAsync(static_cast<char *>(x) + s.row0 * es, s.x, s.nloc * es, hipMemcpyDeviceToHost, s.stream));
+        HIPT(hipMemcpyAsync(s.h_x ? s.h_x : static_cast<char *>(x) + s.row0 * es, s.x, s.nloc * es,
+                            hipMemcpyDeviceToHost, s.stream));
     }
-    return sync_all(c);
+    TRY(sync_all(c));
+    for (auto &s : c->sh)
+        if (s.h_x) std::memcpy(static_cast<char *>(x) + s.row0 * es, s.h_x, s.nloc * es);
+    return CGX_OK;
 }
 
 int cgx_solve_begin(cgx_ctx *c) {

@@ -3,7 +3,6 @@
 #pragma once
 #include <hip/hip_runtime.h>
 #include <cstdint>
-#include <initializer_list>
 
 namespace cgx {
 
@@ -136,19 +135,25 @@ hipError_t gen_spd_f32(int64_t n, int64_t lda, int64_t row0, int64_t nrows, uint
 hipError_t sum_ordered_f32(const float *in, int cnt, float *out, hipStream_t s);
 
 // Each kernel file is its own code object, which HIP loads on a device at
-// the first use of one of its kernels.  preload_kernels() loads all of them
-// on the current device at context creation (overlapped with the CLI's file
-// parsing), so no first launch inside a timed solve pays for a load.
+// the first use of one of its kernels.  preload_kernels() loads the ones a
+// context will launch from on the current device at context creation
+// (overlapped with the CLI's file parsing), so no first launch inside a
+// timed solve pays for a load.
 hipError_t preload_matvec();
 hipError_t preload_vector();
 hipError_t preload_poisson();
 hipError_t preload_ref_f32();
 hipError_t preload_symv();
-inline hipError_t preload_kernels() {
-    for (auto f : {preload_matvec, preload_vector, preload_poisson, preload_ref_f32, preload_symv}) {
-        const hipError_t e = f();
-        if (e != hipSuccess) return e;
-    }
+enum PreloadSet : unsigned { PL_MATVEC = 1, PL_VECTOR = 2, PL_POISSON = 4, PL_REF_F32 = 8, PL_SYMV = 16 };
+inline hipError_t preload_kernels(unsigned set) {
+    const struct { unsigned bit; hipError_t (*fn)(); } all[] = {
+        {PL_MATVEC, preload_matvec}, {PL_VECTOR, preload_vector}, {PL_POISSON, preload_poisson},
+        {PL_REF_F32, preload_ref_f32}, {PL_SYMV, preload_symv}};
+    for (const auto &e : all)
+        if (set & e.bit) {
+            const hipError_t r = e.fn();
+            if (r != hipSuccess) return r;
+        }
     return hipSuccess;
 }
 

@@ -48,8 +48,10 @@ def test_cli_fp32ref_reference_fixtures(golden, name, files):
 
 def test_cli_full_teardown_same_output(golden, tmp_path):
     """The default fast exit (no teardown after the output is flushed) and the
-    full teardown (CGX_CLI_FAST_EXIT=0) print the same x and exit 0; the phase
-    line reports which ran.  Stdout to a file checks the flush before _exit."""
+    full teardown (CGX_CLI_FAST_EXIT=0), with A in huge pages (default) or
+    malloc'd (CGX_CLI_HUGEPAGES=0), print the same x and exit 0; the phase
+    line reports which ran.  Stdout to a file checks the flush before
+    _exit."""
     paths = [os.path.join(FIX, f) for f in ("matrixA1.txt", "vectorb1.txt", "X0.txt")]
     outs = {}
     for mode in ("1", "0"):
@@ -57,7 +59,7 @@ def test_cli_full_teardown_same_output(golden, tmp_path):
         with open(dst, "w") as f:
             r = subprocess.run([cg.CLI_PATH, "--fp32-ref", "--print-x", "--stats", *paths], stdout=f,
                                stderr=subprocess.PIPE, text=True, timeout=300,
-                               env=dict(os.environ, CGX_CLI_FAST_EXIT=mode, CGX_CLI_TIMES="1"))
+                               env=dict(os.environ, CGX_CLI_FAST_EXIT=mode, CGX_CLI_HUGEPAGES=mode, CGX_CLI_TIMES="1"))
         assert r.returncode == 0, r.stderr
         assert f'"fast_exit": {mode}' in r.stderr
         outs[mode] = dst.read_text().splitlines()

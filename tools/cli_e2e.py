@@ -8,7 +8,8 @@ larger): generateSPDmatrix(n) written as the MATLAB script writes it
     single thread, timed separately;
   - cg_hip --fp32-ref --print-x on the same three files, wall time of the
     whole program (parse + H2D + GPU solve + print), with its default fast
-    exit and with the full teardown (CGX_CLI_FAST_EXIT=0).
+    exit and A in huge pages, with A malloc'd (CGX_CLI_HUGEPAGES=0), and
+    with the full teardown (CGX_CLI_FAST_EXIT=0).
 The x vectors must be identical bit for bit.  oracle/_ref is the reference
 compiled here from its sources (it travels with the repo snapshot; the
 reference sources do not).
@@ -67,14 +68,16 @@ def main():
         res.update({"reference_initialize_s": t_init, "reference_conjugrad_process_s": t_solve,
                     "reference_total_s": t_init + t_solve, "reference_iterations": ref_iters,
                     "reference_stdout": out.strip().splitlines()[0]})
-        # cg_hip: the whole program, default (fast exit: no teardown after the
-        # output is flushed) and CGX_CLI_FAST_EXIT=0 (full teardown), alternating
-        runs = {"fast": [], "teardown": []}
+        # cg_hip: the whole program, alternating: the defaults (A in huge pages,
+        # fast exit after the output is flushed), A malloc'd
+        # (CGX_CLI_HUGEPAGES=0), and the full teardown (CGX_CLI_FAST_EXIT=0)
+        modes = {"fast": {}, "no_hugepages": {"CGX_CLI_HUGEPAGES": "0"}, "teardown": {"CGX_CLI_FAST_EXIT": "0"}}
+        runs = {k: [] for k in modes}
         phases = {}
         out = ""
         for rep in range(5):
-            for mode in ("fast", "teardown"):
-                env = dict(os.environ, CGX_CLI_TIMES="1", CGX_CLI_FAST_EXIT="1" if mode == "fast" else "0")
+            for mode, extra in modes.items():
+                env = dict(os.environ, CGX_CLI_TIMES="1", **extra)
                 t0 = time.perf_counter()
                 proc = subprocess.run([cg.CLI_PATH, "--fp32-ref", "--print-x", "--stats", "--threads", str(a.threads),
                                        paths["A"], paths["b"], paths["x0"]], check=True, capture_output=True,
@@ -90,17 +93,22 @@ def main():
                     out = proc.stdout
         med = {k: sorted(v)[len(v) // 2] for k, v in runs.items()}
         res["cg_hip_phases_s"] = phases.get("fast", [])
+        res["cg_hip_phases_no_hugepages_s"] = phases.get("no_hugepages", [])
         res["cg_hip_phases_full_teardown_s"] = phases.get("teardown", [])
-        for mode in ("fast", "teardown"):
-            aft = sorted(r["after_output_s"] for r in phases.get(mode, []))
-            if aft:
-                res[f"cg_hip_after_output_med_s_{mode}"] = aft[len(aft) // 2]
+        for mode in modes:
+            recs = phases.get(mode, [])
+            for r in recs:  # the critical path once HIP is up: context, distribution, solve, x back
+                r["after_hip_up_to_x_s"] = r["to_x_s"] - r["hip_runtime_s"]
+            for key in ("after_output_s", "distribute_s", "read_s", "free_s", "get_x_s", "after_hip_up_to_x_s"):
+                v = sorted(r[key] for r in recs)
+                if v:
+                    res[f"cg_hip_{key[:-2]}_med_s_{mode}"] = v[len(v) // 2]
         lines = out.strip().splitlines()
         x = np.array([float(v) for v in lines[-n:]], dtype=np.float32)
         xr = np.fromfile(xref, dtype=np.float32)
         t_cli = med["fast"]
         res.update({"cg_hip_total_s": t_cli, "cg_hip_total_runs_s": runs["fast"],
-                    "cg_hip_total_full_teardown_s": med["teardown"],
+                    "cg_hip_total_no_hugepages_s": med["no_hugepages"], "cg_hip_total_full_teardown_s": med["teardown"],
                     "cg_hip_total_full_teardown_runs_s": runs["teardown"], "cg_hip_stdout_head": lines[:4],
                     "x_bit_identical": bool(np.array_equal(x.view(np.uint32), xr.view(np.uint32))),
                     "speedup_total": (t_init + t_solve) / t_cli, "threads": a.threads,
