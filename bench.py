@@ -230,6 +230,8 @@ def main(argv=None) -> int:
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=20)
     ap.add_argument("--warmup", type=int, default=3)
+    ap.add_argument("--settle", type=float, default=3.0,
+                    help="seconds to idle after setting up the system, before the warmup steps")
     ap.add_argument("--workload", choices=["dense", "symmetric", "stream", "stream_symmetric", "poisson"],
                     default="dense",
                     help="dense: configs[2], A resident in HBM (default); "
@@ -289,6 +291,14 @@ def main(argv=None) -> int:
         solver.fill(1.0, 0.0)
     else:
         solver.generate_spd(SEED)
+    solver.synchronize()
+    # Settle before the warmup: a process that starts right after another
+    # one freed tens of GB measured its matVec 2-5 % slower (the release of
+    # that memory shares HBM with it); with a few seconds of gap every run
+    # read the same rate (profiles/r01_bench_variance.json).  Setup only: no
+    # step is skipped or added.
+    if args.settle > 0:
+        time.sleep(args.settle)
     solver.begin()
     if args.warmup:
         solver.iterate(args.warmup, eps=-1.0)
