@@ -1,5 +1,6 @@
-// cgx_api.hip -- the C ABI of include/cgx.h: contexts, row-block shards,
-// per-iteration exchange, and the conjugrad driver loop.
+// cgx_api.hip -- the C ABI of include/cgx.h: errors and devices, and the
+// kernel-level entry points; the rest of the ABI lives in cgx_setup.hip,
+// cgx_exchange.hip and cgx_iterate.hip (shared types: cgx_ctx.h).
 //
 // Reference mapping:
 //   conjugrad()              serialConjugate.c:180-259 / parallel_cg.c:248-345
@@ -24,29 +25,9 @@
 //   RR(j)   = r_j.r_j (global)      PAP(k) = p_k.Ap_k (global)   ring of 4
 //   LRR(j), LPAP(k): this shard's partials when an exchange follows
 //   GATHER+q: the partial of shard q (ordered combine)
-#include <hip/hip_runtime.h>
-#include <rccl/rccl.h>
-#include <rocprofiler-sdk-roctx/roctx.h>
+#include "cgx_ctx.h"
 
-#include <chrono>
-#include <cmath>
-#include <cstdarg>
-#include <cstdio>
-#include <cstdlib>
-#include <cstring>
-#include <initializer_list>
-#include <mutex>
-#include <new>
-#include <string>
-#include <vector>
-#include <algorithm>
-
-#include "cgx.h"
-#include "cgx_kernels.h"
-
-using namespace cgx;
-
-namespace {
+namespace cgxh {
 
 thread_local char g_err[1024] = "";
 
@@ -56,1135 +37,6 @@ int fail(int code, const char *fmt, ...) {
     vsnprintf(g_err, sizeof g_err, fmt, ap);
     va_end(ap);
     return code;
-}
-
-#define HIPT(expr)                                                                              \
-    do {                                                                                        \
-        hipError_t e_ = (expr);                                                                 \
-        if (e_ != hipSuccess)                                                                   \
-            return fail(CGX_ERR_HIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, \
-                        __LINE__);                                                              \
-    } while (0)
-
-#define NCCLT(expr)                                                                               \
-    do {                                                                                          \
-        ncclResult_t e_ = (expr);                                                                 \
-        if (e_ != ncclSuccess)                                                                    \
-            return fail(CGX_ERR_RCCL, "%s: %s (%s:%d)", #expr, ncclGetErrorString(e_), __FILE__, \
-                        __LINE__);                                                                \
-    } while (0)
-
-#define TRY(expr)                          \
-    do {                                   \
-        int rc_ = (expr);                  \
-        if (rc_ != CGX_OK) return rc_;     \
-    } while (0)
-
-constexpr int kScalSlots = 136;  // 16 ring slots, up to 112 gathered partials, 4 aux
-constexpr int kMaxShards = 32;
-constexpr int S_RR = 0, S_PAP = 4, S_LRR = 8, S_LPAP = 12, S_GATHER = 16;
-constexpr int S_TR = 128, S_TB = 129, S_LTR = 130, S_LTB = 131;  // true-residual check
-constexpr int S_XNZ = 134;  // rank mode: count of ranks whose x0 is not all zeros
-constexpr int S_KDONE = 132, S_RRFINAL = 133;  // device-side convergence: k+1 at the break, r.r there
-constexpr int kLookRing = 8;                    // pinned slots for the host's lagged convergence checks
-inline int ring(int64_t j) { return (int)(j & 3); }
-constexpr int kGraphIters = 4;  // a multiple of the ring period (and of the Poisson slab alternation)
-
-enum Mode { M_SINGLE = 0, M_LOCAL = 1, M_RCCL = 2 };
-enum Op { OP_DENSE = 0, OP_POISSON = 1 };
-enum State { ST_IDLE = 0, ST_BEGUN = 1, ST_CONVERGED = 2 };
-
-constexpr int kEvPairs = 256;
-constexpr size_t kXStageMax = 64u << 20;
-constexpr int kStreamBufs = 3;
-constexpr int kMaxCopyStreams = 4;
-
-struct Shard {
-    int dev = 0;
-    int index = 0;  // global row-block index
-    int64_t row0 = 0, nloc = 0;
-    hipStream_t stream = nullptr;
-    ncclComm_t comm = nullptr;
-    char *A = nullptr, *b = nullptr, *x = nullptr, *r = nullptr, *Ap = nullptr, *pfull = nullptr,
-         *xfull = nullptr, *scal = nullptr;
-    char *pown = nullptr;  // this shard's p: pfull + row0 (dense) or the slab interior (Poisson)
-    // fused Poisson iteration: r with halo rows (r = rh + one row) and a
-    // second p slab; p_k lives in pfull for even k, in p2 for odd k
-    char *rh = nullptr, *p2 = nullptr;
-    bool x_zero = true;  // x is known to be all zeros (x0 = 0: the first A x is skipped)
-    RedWs ws{nullptr, nullptr};
-    double *h_pin = nullptr;
-    // pinned staging for cgx_get_x (x of this shard, or all of x in rank
-    // mode), allocated with the context so the first D2H of a solve's result
-    // does not set up HIP's pageable-copy path (~7 ms); null above kXStageMax
-    char *h_x = nullptr;
-    // convergence record {kdone, bits of r.r there} in host-mapped coherent
-    // memory: the deciding kernel stores it, the host reads it after an event
-    int64_t *h_rec = nullptr, *d_rec = nullptr;
-    MatvecPlan plan;
-    // CGX_SYMMETRIC: A = the upper-triangle tiles; per-tile row / column
-    // partials of a matVec; a staging buffer for rows copied from the host
-    char *sym_prow = nullptr, *sym_pcol = nullptr, *sym_stage = nullptr;
-    int64_t sym_stage_rows = 0;
-    int sym_grid = 0;
-    hipEvent_t ev_sync = nullptr;  // cross-shard ordering (LOCAL mode)
-    std::vector<hipEvent_t> ev_t;  // timing pairs (CGX_TIMING)
-    int ev_used = 0;
-    // CGX_HOST_STREAM: A stays in pinned host memory; row tiles are copied
-    // into kStreamBufs device buffers on `ncopy` copy streams while the
-    // compute stream multiplies the previous tiles.
-    char *A_host = nullptr;
-    int64_t tile_rows = 0;
-    char *tile[kStreamBufs] = {};
-    int ncopy = 0;
-    hipStream_t copy[kMaxCopyStreams] = {};
-    hipEvent_t ev_loaded[kStreamBufs][kMaxCopyStreams] = {};
-    hipEvent_t ev_free[kStreamBufs] = {};
-    bool buf_used[kStreamBufs] = {};
-    int next_buf = 0;
-    MatvecPlan tile_plan;
-    hipEvent_t ev_look[8] = {};  // lagged convergence checks (kLookRing)
-    // overlap of the p exchange with the own-column-block matVec
-    hipStream_t cstream = nullptr;
-    hipEvent_t ev_pready = nullptr, ev_gathered = nullptr;
-};
-
-}  // namespace
-
-struct cgx_ctx {
-    int64_t n = 0, lda = 0;
-    int op = 0;        // OP_DENSE or OP_POISSON
-    int64_t m = 0;     // Poisson grid width (n = m*m)
-    int nranks = 1;
-    int flags = 0;
-    int es = 8;
-    Mode mode = M_SINGLE;
-    std::vector<Shard> sh;
-    State state = ST_IDLE;
-    int64_t k = 0;  // iterations of the current solve
-    double last_rr = 0.0;
-    int converged = 0;
-    double solve_ms = 0.0, matvec_ms = 0.0;
-    int64_t matvec_count = 0, total_iters = 0;
-    bool overlap = false;  // own-column-block matVec while p is exchanged
-    bool fused = false;    // Poisson: two-kernel fused iteration (k_poisson_p + k_poisson_xr)
-    bool halo_overlap = false;  // fused Poisson, several slabs: r's halo exchange overlaps k_poisson_p
-    bool halo_pending = false;  // an overlapped r halo exchange is in flight on the comm streams
-    // fixed-count iterations replayed from a hipGraph (one GPU): kGraphIters
-    // iterations captured once, the period of the scalar rings
-    hipGraphExec_t graph = nullptr;
-    bool graph_failed = false;
-};
-
-namespace {
-
-inline bool f32ref(const cgx_ctx *c) { return (c->flags & CGX_F32_REF) != 0; }
-inline void *slot(const Shard &s, int i) { return s.scal + 8 * i; }
-
-int set_dev(const Shard &s) {
-    HIPT(hipSetDevice(s.dev));
-    return CGX_OK;
-}
-
-int alloc_shard(cgx_ctx *c, Shard &s) {
-    TRY(set_dev(s));
-    {  // the code objects this context launches from (fp64 residual checks use the vector kernels too)
-        unsigned set = PL_VECTOR;
-        if (c->op == OP_POISSON) set |= PL_POISSON;
-        else if (f32ref(c)) set |= PL_REF_F32;
-        else if (c->flags & CGX_SYMMETRIC) set |= PL_SYMV;
-        else set |= PL_MATVEC;
-        HIPT(preload_kernels(set));
-    }
-    const size_t es = (size_t)c->es;
-    HIPT(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
-    HIPT(hipEventCreateWithFlags(&s.ev_sync, hipEventDisableTiming));
-    const size_t abytes = (size_t)s.nloc * (size_t)c->lda * es;
-    auto dmalloc = [&](char **p, size_t bytes) -> int {
-        if (bytes == 0) bytes = 16;
-        hipError_t e = hipMalloc(p, bytes);
-        if (e != hipSuccess)
-            return fail(CGX_ERR_NOMEM, "hipMalloc(%zu bytes) on device %d: %s", bytes, s.dev,
-                        hipGetErrorString(e));
-        return CGX_OK;
-    };
-    if (c->op == OP_POISSON) {
-        // matrix-free: no A
-    } else if ((c->flags & CGX_SYMMETRIC) && (c->flags & CGX_HOST_STREAM)) {
-        // the upper-triangle tiles in pinned host memory, streamed in chunks of
-        // whole tiles through kStreamBufs device buffers (tile_rows = tiles per chunk)
-        const int64_t ntiles = sym_tiles(c->lda), tb = 128 * 128 * 8;
-        hipError_t e = hipHostMalloc(reinterpret_cast<void **>(&s.A_host), (size_t)ntiles * tb, hipHostMallocDefault);
-        if (e != hipSuccess)
-            return fail(CGX_ERR_NOMEM, "hipHostMalloc(%lld bytes) for streamed tiles: %s", (long long)(ntiles * tb),
-                        hipGetErrorString(e));
-        const char *tmb = std::getenv("CGX_STREAM_TILE_MB");
-        const int64_t chunk_bytes = (int64_t)((tmb && *tmb) ? std::atoll(tmb) : 256) << 20;
-        s.tile_rows = std::max<int64_t>(1, std::min<int64_t>(ntiles, chunk_bytes / tb));
-        const char *nc = std::getenv("CGX_STREAM_COPIES");
-        s.ncopy = std::max(1, std::min(kMaxCopyStreams, (nc && *nc) ? std::atoi(nc) : 2));
-        for (int b = 0; b < kStreamBufs; ++b) {
-            TRY(dmalloc(&s.tile[b], (size_t)s.tile_rows * tb));
-            HIPT(hipEventCreateWithFlags(&s.ev_free[b], hipEventDisableTiming));
-            for (int q = 0; q < s.ncopy; ++q) HIPT(hipEventCreateWithFlags(&s.ev_loaded[b][q], hipEventDisableTiming));
-        }
-        for (int q = 0; q < s.ncopy; ++q) HIPT(hipStreamCreateWithFlags(&s.copy[q], hipStreamNonBlocking));
-        TRY(dmalloc(&s.sym_prow, (size_t)ntiles * 128 * 8));
-        TRY(dmalloc(&s.sym_pcol, (size_t)ntiles * 128 * 8));
-        s.sym_grid = sym_grid(s.dev);
-    } else if (c->flags & CGX_HOST_STREAM) {
-        // A in pinned host memory, kStreamBufs device tiles of ~CGX_STREAM_TILE_MB.
-        hipError_t e = hipHostMalloc(reinterpret_cast<void **>(&s.A_host), abytes ? abytes : 16, hipHostMallocDefault);
-        if (e != hipSuccess)
-            return fail(CGX_ERR_NOMEM, "hipHostMalloc(%zu bytes) for streamed A: %s", abytes, hipGetErrorString(e));
-        const int64_t row_bytes = c->lda * (int64_t)es;
-        const char *tmb = std::getenv("CGX_STREAM_TILE_MB");
-        const int64_t tile_bytes = (int64_t)((tmb && *tmb) ? std::atoll(tmb) : 256) << 20;
-        s.tile_rows = std::max<int64_t>(1, std::min<int64_t>(s.nloc, tile_bytes / row_bytes));
-        const char *nc = std::getenv("CGX_STREAM_COPIES");
-        s.ncopy = std::max(1, std::min(kMaxCopyStreams, (nc && *nc) ? std::atoi(nc) : 2));
-        for (int b = 0; b < kStreamBufs; ++b) {
-            TRY(dmalloc(&s.tile[b], (size_t)s.tile_rows * row_bytes));
-            HIPT(hipMemsetAsync(s.tile[b], 0, (size_t)s.tile_rows * row_bytes, s.stream));
-            HIPT(hipEventCreateWithFlags(&s.ev_free[b], hipEventDisableTiming));
-            for (int q = 0; q < s.ncopy; ++q) HIPT(hipEventCreateWithFlags(&s.ev_loaded[b][q], hipEventDisableTiming));
-        }
-        for (int q = 0; q < s.ncopy; ++q) HIPT(hipStreamCreateWithFlags(&s.copy[q], hipStreamNonBlocking));
-        if (!f32ref(c)) s.tile_plan = plan_matvec_f64(s.dev, s.tile_rows);
-    } else if (c->flags & CGX_SYMMETRIC) {
-        const int64_t ntiles = sym_tiles(c->lda);
-        const size_t tbytes = (size_t)ntiles * 128 * 128 * 8;
-        TRY(dmalloc(&s.A, tbytes));
-        HIPT(hipMemsetAsync(s.A, 0, tbytes, s.stream));  // padding rows / columns stay zero
-        TRY(dmalloc(&s.sym_prow, (size_t)ntiles * 128 * 8));
-        TRY(dmalloc(&s.sym_pcol, (size_t)ntiles * 128 * 8));
-        s.sym_grid = sym_grid(s.dev);
-    } else {
-        TRY(dmalloc(&s.A, abytes));
-        HIPT(hipMemsetAsync(s.A, 0, abytes, s.stream));  // zero padding columns
-    }
-    TRY(dmalloc(&s.b, s.nloc * es));
-    TRY(dmalloc(&s.x, s.nloc * es));
-    if (c->op == OP_POISSON) {  // r with halo rows (the fused iteration exchanges r, not p)
-        TRY(dmalloc(&s.rh, (s.nloc + 2 * c->m) * es));
-        HIPT(hipMemsetAsync(s.rh, 0, (s.nloc + 2 * c->m) * es, s.stream));
-        s.r = s.rh + c->m * es;
-        TRY(dmalloc(&s.p2, (s.nloc + 2 * c->m) * es));
-        HIPT(hipMemsetAsync(s.p2, 0, (s.nloc + 2 * c->m) * es, s.stream));
-    } else {
-        TRY(dmalloc(&s.r, s.nloc * es));
-    }
-    TRY(dmalloc(&s.Ap, s.nloc * es));
-    // full-length p (dense) or the slab with one halo row above and below (Poisson)
-    const int64_t plen = (c->op == OP_POISSON) ? s.nloc + 2 * c->m : c->lda;
-    const int64_t xlen = (c->op == OP_POISSON) ? c->n : c->lda;
-    TRY(dmalloc(&s.pfull, plen * es));
-    s.pown = (c->op == OP_POISSON) ? s.pfull + c->m * es : s.pfull + s.row0 * es;
-    TRY(dmalloc(&s.scal, kScalSlots * 8));
-    if (c->mode == M_RCCL && c->nranks > 1) TRY(dmalloc(&s.xfull, xlen * es));
-    char *part = nullptr, *tick = nullptr;
-    TRY(dmalloc(&part, kMaxRedBlocks * sizeof(double)));
-    s.ws.partials = reinterpret_cast<double *>(part);  // owned by the shard from here (free_shard)
-    TRY(dmalloc(&tick, kTickets * sizeof(unsigned)));
-    s.ws.tickets = reinterpret_cast<unsigned *>(tick);
-    if (es == 4) HIPT(fill_f32(reinterpret_cast<float *>(s.b), s.nloc, 0.0f, s.stream));
-    else HIPT(fill_f64(reinterpret_cast<double *>(s.b), s.nloc, 0.0, s.stream));
-    HIPT(hipMemsetAsync(s.x, 0, s.nloc * es, s.stream));
-    HIPT(hipMemsetAsync(s.r, 0, s.nloc * es, s.stream));
-    HIPT(hipMemsetAsync(s.Ap, 0, s.nloc * es, s.stream));
-    HIPT(hipMemsetAsync(s.pfull, 0, plen * es, s.stream));
-    HIPT(hipMemsetAsync(s.scal, 0, kScalSlots * 8, s.stream));
-    HIPT(hipMemsetAsync(s.ws.tickets, 0, kTickets * sizeof(unsigned), s.stream));
-    if (s.xfull) HIPT(hipMemsetAsync(s.xfull, 0, xlen * es, s.stream));
-    HIPT(hipHostMalloc(reinterpret_cast<void **>(&s.h_pin), 8 * (8 + kLookRing), hipHostMallocDefault));
-    {
-        const size_t xb = (size_t)(s.xfull ? xlen : s.nloc) * es;
-        if (xb <= kXStageMax) {
-            HIPT(hipHostMalloc(reinterpret_cast<void **>(&s.h_x), xb ? xb : 16, hipHostMallocDefault));
-            // one device-to-host copy now: the first one of a process sets up
-            // the copy path (~8 ms, measured in cg_hip's get_x), which would
-            // otherwise land on the first cgx_get_x
-            HIPT(hipMemcpyAsync(s.h_x, s.pfull, std::min<size_t>(xb, (size_t)plen * es), hipMemcpyDeviceToHost,
-                                s.stream));
-        }
-    }
-    HIPT(hipHostMalloc(reinterpret_cast<void **>(&s.h_rec), 16, hipHostMallocMapped | hipHostMallocCoherent));
-    HIPT(hipHostGetDevicePointer(reinterpret_cast<void **>(&s.d_rec), s.h_rec, 0));
-    s.h_rec[0] = s.h_rec[1] = 0;
-    for (int q = 0; q < kLookRing; ++q) HIPT(hipEventCreateWithFlags(&s.ev_look[q], hipEventDisableTiming));
-    if (c->flags & CGX_TIMING) {
-        s.ev_t.resize(2 * kEvPairs);
-        for (auto &e : s.ev_t) HIPT(hipEventCreate(&e));
-    }
-    if (!f32ref(c) && c->op == OP_DENSE && !(c->flags & CGX_SYMMETRIC)) s.plan = plan_matvec_f64(s.dev, s.nloc);
-    HIPT(hipStreamSynchronize(s.stream));
-    return CGX_OK;
-}
-
-void free_shard(Shard &s) {
-    (void)hipSetDevice(s.dev);
-    if (s.stream) (void)hipStreamSynchronize(s.stream);
-    if (s.comm) ncclCommDestroy(s.comm);
-    for (char *p : {s.A, s.b, s.x, s.rh ? s.rh : s.r, s.p2, s.Ap, s.pfull, s.xfull, s.scal, s.sym_prow, s.sym_pcol,
-                    s.sym_stage})
-        if (p) (void)hipFree(p);
-    if (s.ws.partials) (void)hipFree(s.ws.partials);
-    if (s.ws.tickets) (void)hipFree(s.ws.tickets);
-    if (s.h_pin) (void)hipHostFree(s.h_pin);
-    if (s.h_x) (void)hipHostFree(s.h_x);
-    if (s.h_rec) (void)hipHostFree(s.h_rec);
-    for (auto e : s.ev_t) (void)hipEventDestroy(e);
-    if (s.ev_sync) (void)hipEventDestroy(s.ev_sync);
-    for (int q = 0; q < kMaxCopyStreams; ++q)
-        if (s.copy[q]) {
-            (void)hipStreamSynchronize(s.copy[q]);
-            (void)hipStreamDestroy(s.copy[q]);
-        }
-    for (int b = 0; b < kStreamBufs; ++b) {
-        if (s.tile[b]) (void)hipFree(s.tile[b]);
-        if (s.ev_free[b]) (void)hipEventDestroy(s.ev_free[b]);
-        for (int q = 0; q < kMaxCopyStreams; ++q)
-            if (s.ev_loaded[b][q]) (void)hipEventDestroy(s.ev_loaded[b][q]);
-    }
-    if (s.A_host) (void)hipHostFree(s.A_host);
-    if (s.cstream) {
-        (void)hipStreamSynchronize(s.cstream);
-        (void)hipStreamDestroy(s.cstream);
-    }
-    if (s.ev_pready) (void)hipEventDestroy(s.ev_pready);
-    for (auto e : s.ev_look)
-        if (e) (void)hipEventDestroy(e);
-    if (s.ev_gathered) (void)hipEventDestroy(s.ev_gathered);
-    if (s.stream) (void)hipStreamDestroy(s.stream);
-    s = Shard();
-}
-
-// roctx range over an API call (rocprofv3 --marker-trace shows the solve
-// phases on the timeline; a no-op without a tool attached).
-struct Range {
-    explicit Range(const char *name) { roctxRangePushA(name); }
-    ~Range() { roctxRangePop(); }
-    Range(const Range &) = delete;
-    Range &operator=(const Range &) = delete;
-};
-
-int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
-
-int check_n(int64_t n, int nranks) {
-    if (n < 1) return fail(CGX_ERR_ARG, "n must be >= 1 (got %lld)", (long long)n);
-    if (nranks < 1) return fail(CGX_ERR_ARG, "nranks must be >= 1");
-    if (n % nranks != 0)  // parallel_cg.c:86-90
-        return fail(CGX_ERR_SHAPE, "%lld is not divisible by %d", (long long)n, nranks);
-    if (n > (int64_t)0xffffffffLL) return fail(CGX_ERR_ARG, "n too large");
-    return CGX_OK;
-}
-
-cgx_ctx *new_ctx(int64_t n, int nranks, int flags) {
-    cgx_ctx *c = new (std::nothrow) cgx_ctx();
-    if (!c) return nullptr;
-    c->n = n;
-    c->lda = round_up(n, 128);
-    c->nranks = nranks;
-    c->flags = flags;
-    c->es = (flags & CGX_F32_REF) ? 4 : 8;
-    return c;
-}
-
-// Overlap p's exchange with the own-column-block part of the matVec: dense
-// fp64 resident A, more than one row block, every block aligned to the
-// matVec's 128-column chunks.  CGX_OVERLAP=0 disables it.
-bool can_overlap(const cgx_ctx *c) {
-    if (c->op != OP_DENSE || f32ref(c) || (c->flags & CGX_HOST_STREAM)) return false;
-    if (c->flags & (CGX_NO_OVERLAP | CGX_COMM_P2P)) return false;
-    const char *e = std::getenv("CGX_OVERLAP");
-    if (e && *e == '0') return false;
-    // CGX_OVERLAP=force: also at world size 1 in rank mode (the in-place
-    // allgather on the comm stream and the event hand-offs run with nothing to
-    // exchange), so one GPU can execute the rank-mode overlap path.
-    const bool force = e && std::strcmp(e, "force") == 0;
-    if (c->mode == M_SINGLE || (c->mode == M_RCCL && c->nranks == 1 && !force)) return false;
-    for (const auto &s : c->sh)
-        if ((s.row0 & 127) || (s.nloc & 127)) return false;
-    return true;
-}
-
-int alloc_overlap(cgx_ctx *c) {
-    for (auto &s : c->sh) {
-        TRY(set_dev(s));
-        HIPT(hipStreamCreateWithFlags(&s.cstream, hipStreamNonBlocking));
-        HIPT(hipEventCreateWithFlags(&s.ev_pready, hipEventDisableTiming));
-        HIPT(hipEventCreateWithFlags(&s.ev_gathered, hipEventDisableTiming));
-    }
-    return CGX_OK;
-}
-
-int finish_create(cgx_ctx *c, cgx_ctx **out) {
-    c->overlap = can_overlap(c);
-    if (c->op == OP_POISSON) {  // CGX_POISSON_FUSED=0: the three-kernel split (stencil, r, x/p)
-        const char *e = std::getenv("CGX_POISSON_FUSED");
-        c->fused = !(e && *e == '0') && poisson_fusable(c->sh[0].nloc / c->m, c->m);
-        const char *h = std::getenv("CGX_HALO_OVERLAP");
-        const bool force = h && std::strcmp(h, "force") == 0;  // also at world size 1 in rank mode
-        c->halo_overlap = c->fused && !(h && *h == '0') && c->mode != M_SINGLE &&
-                          !(c->mode == M_RCCL && c->nranks == 1 && !force);
-    }
-    for (auto &s : c->sh) {
-        int rc = alloc_shard(c, s);
-        if (rc == CGX_OK && (c->overlap || c->halo_overlap) && &s == &c->sh.back()) rc = alloc_overlap(c);
-        if (rc != CGX_OK) {
-            std::string keep = g_err;
-            for (auto &t : c->sh) free_shard(t);
-            delete c;
-            snprintf(g_err, sizeof g_err, "%s", keep.c_str());
-            return rc;
-        }
-    }
-    *out = c;
-    return CGX_OK;
-}
-
-// ---- timing -------------------------------------------------------------------
-int timing_resolve(cgx_ctx *c) {
-    if (!(c->flags & CGX_TIMING)) return CGX_OK;
-    Shard &s = c->sh[0];
-    TRY(set_dev(s));
-    for (int i = 0; i < s.ev_used; ++i) {
-        float ms = 0.f;
-        HIPT(hipEventSynchronize(s.ev_t[2 * i + 1]));
-        HIPT(hipEventElapsedTime(&ms, s.ev_t[2 * i], s.ev_t[2 * i + 1]));
-        c->matvec_ms += ms;
-        c->matvec_count += 1;
-    }
-    s.ev_used = 0;
-    return CGX_OK;
-}
-
-// ---- exchange ---------------------------------------------------------------------
-// Make every shard's stream wait for the work already queued on all shards.
-int local_barrier(cgx_ctx *c) {
-    for (auto &s : c->sh) {
-        TRY(set_dev(s));
-        HIPT(hipEventRecord(s.ev_sync, s.stream));
-    }
-    for (auto &d : c->sh) {
-        TRY(set_dev(d));
-        for (auto &s : c->sh)
-            if (&s != &d) HIPT(hipStreamWaitEvent(d.stream, s.ev_sync, 0));
-    }
-    return CGX_OK;
-}
-
-// Poisson: refresh the two halo rows of every slab from its neighbours
-// (ncclSend/Recv of one grid row each way in rank mode, device copies in
-// LOCAL mode); from_x first copies x into the slab interior (for A x0).
-int exchange_halo_of(cgx_ctx *c, char *Shard::*slab);
-int exchange_halo(cgx_ctx *c, bool from_x) {
-    const size_t es = (size_t)c->es;
-    if (from_x)
-        for (auto &s : c->sh) {
-            TRY(set_dev(s));
-            HIPT(hipMemcpyAsync(s.pown, s.x, s.nloc * es, hipMemcpyDeviceToDevice, s.stream));
-        }
-    return exchange_halo_of(c, &Shard::pfull);
-}
-
-// The halo rows of the slab buffer `slab` (row 0 and row mloc+1 around the
-// mloc interior rows) from the neighbouring slabs' boundary rows.
-int exchange_halo_of(cgx_ctx *c, char *Shard::*slab) {
-    const size_t row = (size_t)c->m * (size_t)c->es;
-    if (c->mode == M_SINGLE) return CGX_OK;
-    const int64_t mloc = c->sh[0].nloc / c->m;
-    if (c->mode == M_RCCL) {
-        Shard &s = c->sh[0];
-        if (c->nranks == 1) return CGX_OK;
-        TRY(set_dev(s));
-        const int g = s.index;
-        char *base = s.*slab, *own = base + row;
-        NCCLT(ncclGroupStart());
-        if (g > 0) {
-            NCCLT(ncclSend(own, (size_t)c->m, ncclDouble, g - 1, s.comm, s.stream));
-            NCCLT(ncclRecv(base, (size_t)c->m, ncclDouble, g - 1, s.comm, s.stream));
-        }
-        if (g < c->nranks - 1) {
-            NCCLT(ncclSend(own + (size_t)(mloc - 1) * row, (size_t)c->m, ncclDouble, g + 1, s.comm, s.stream));
-            NCCLT(ncclRecv(own + (size_t)mloc * row, (size_t)c->m, ncclDouble, g + 1, s.comm, s.stream));
-        }
-        NCCLT(ncclGroupEnd());
-        return CGX_OK;
-    }
-    TRY(local_barrier(c));
-    const int S = (int)c->sh.size();
-    for (int q = 0; q < S; ++q) {
-        Shard &d = c->sh[q];
-        TRY(set_dev(d));
-        if (q > 0) {
-            const Shard &u = c->sh[q - 1];
-            HIPT(hipMemcpyPeerAsync(d.*slab, d.dev, u.*slab + (size_t)mloc * row, u.dev, row, d.stream));
-        }
-        if (q < S - 1) {
-            const Shard &w = c->sh[q + 1];
-            HIPT(hipMemcpyPeerAsync(d.*slab + (size_t)(mloc + 1) * row, d.dev, w.*slab + row, w.dev, row, d.stream));
-        }
-    }
-    return CGX_OK;
-}
-
-inline bool p2p(const cgx_ctx *c) { return (c->flags & CGX_COMM_P2P) != 0; }
-
-// CGX_COMM_P2P: point-to-point_cg.c's exchange pattern, gather to rank 0 then
-// send from rank 0 to every rank (allGather :364-394 + BcastVector :239-256),
-// O(P) messages through rank 0.  ncclSend/Recv in rank mode, device copies
-// through shard 0 in LOCAL mode.
-int p2p_allgather(cgx_ctx *c, bool from_x) {
-    const size_t es = (size_t)c->es;
-    if (c->mode == M_RCCL) {
-        Shard &s = c->sh[0];
-        TRY(set_dev(s));
-        const ncclDataType_t t = f32ref(c) ? ncclFloat : ncclDouble;
-        const int P = c->nranks;
-        if (s.index == 0 && from_x)
-            HIPT(hipMemcpyAsync(s.pown, s.x, s.nloc * es, hipMemcpyDeviceToDevice, s.stream));
-        NCCLT(ncclGroupStart());
-        if (s.index != 0) {
-            NCCLT(ncclSend(from_x ? (const void *)s.x : (const void *)s.pown, (size_t)s.nloc, t, 0, s.comm, s.stream));
-        } else {
-            for (int q = 1; q < P; ++q)
-                NCCLT(ncclRecv(s.pfull + (size_t)q * s.nloc * es, (size_t)s.nloc, t, q, s.comm, s.stream));
-        }
-        NCCLT(ncclGroupEnd());
-        NCCLT(ncclGroupStart());
-        if (s.index == 0) {
-            for (int q = 1; q < P; ++q) NCCLT(ncclSend(s.pfull, (size_t)c->n, t, q, s.comm, s.stream));
-        } else {
-            NCCLT(ncclRecv(s.pfull, (size_t)c->n, t, 0, s.comm, s.stream));
-        }
-        NCCLT(ncclGroupEnd());
-        return CGX_OK;
-    }
-    TRY(local_barrier(c));
-    Shard &r0 = c->sh[0];
-    TRY(set_dev(r0));
-    for (auto &s : c->sh) {
-        if (&s == &r0 && !from_x) continue;
-        HIPT(hipMemcpyPeerAsync(r0.pfull + s.row0 * es, r0.dev, from_x ? s.x : s.pown, s.dev, s.nloc * es, r0.stream));
-    }
-    HIPT(hipEventRecord(r0.ev_sync, r0.stream));
-    for (auto &d : c->sh) {
-        if (&d == &r0) continue;
-        TRY(set_dev(d));
-        HIPT(hipStreamWaitEvent(d.stream, r0.ev_sync, 0));
-        HIPT(hipMemcpyPeerAsync(d.pfull, d.dev, r0.pfull, r0.dev, (size_t)c->n * es, d.stream));
-    }
-    return CGX_OK;
-}
-
-// allSum (point-to-point_cg.c:339-359): partials to rank 0, summed there in
-// rank order, the sum sent back to every rank (BcastVector(&s, 1)).
-int p2p_scalar(cgx_ctx *c, int lslot, int gslot) {
-    if (c->mode == M_RCCL) {
-        Shard &s = c->sh[0];
-        TRY(set_dev(s));
-        const int P = c->nranks;
-        if (s.index == 0) HIPT(hipMemcpyAsync(slot(s, S_GATHER), slot(s, lslot), 8, hipMemcpyDeviceToDevice, s.stream));
-        NCCLT(ncclGroupStart());
-        if (s.index != 0) {
-            NCCLT(ncclSend(slot(s, lslot), 1, ncclUint64, 0, s.comm, s.stream));
-        } else {
-            for (int q = 1; q < P; ++q) NCCLT(ncclRecv(slot(s, S_GATHER + q), 1, ncclUint64, q, s.comm, s.stream));
-        }
-        NCCLT(ncclGroupEnd());
-        if (s.index == 0) {
-            if (f32ref(c))
-                HIPT(sum_ordered_f32(reinterpret_cast<const float *>(slot(s, S_GATHER)), P,
-                                     reinterpret_cast<float *>(slot(s, gslot)), s.stream));
-            else
-                HIPT(sum_ordered_f64(reinterpret_cast<const double *>(slot(s, S_GATHER)), P,
-                                     reinterpret_cast<double *>(slot(s, gslot)), s.stream));
-        }
-        NCCLT(ncclGroupStart());
-        if (s.index == 0) {
-            for (int q = 1; q < P; ++q) NCCLT(ncclSend(slot(s, gslot), 1, ncclUint64, q, s.comm, s.stream));
-        } else {
-            NCCLT(ncclRecv(slot(s, gslot), 1, ncclUint64, 0, s.comm, s.stream));
-        }
-        NCCLT(ncclGroupEnd());
-        return CGX_OK;
-    }
-    TRY(local_barrier(c));
-    Shard &r0 = c->sh[0];
-    const int S = (int)c->sh.size();
-    TRY(set_dev(r0));
-    for (auto &s : c->sh)
-        HIPT(hipMemcpyPeerAsync(slot(r0, S_GATHER + s.index), r0.dev, slot(s, lslot), s.dev, 8, r0.stream));
-    if (f32ref(c))
-        HIPT(sum_ordered_f32(reinterpret_cast<const float *>(slot(r0, S_GATHER)), S,
-                             reinterpret_cast<float *>(slot(r0, gslot)), r0.stream));
-    else
-        HIPT(sum_ordered_f64(reinterpret_cast<const double *>(slot(r0, S_GATHER)), S,
-                             reinterpret_cast<double *>(slot(r0, gslot)), r0.stream));
-    HIPT(hipEventRecord(r0.ev_sync, r0.stream));
-    for (auto &d : c->sh) {
-        if (&d == &r0) continue;
-        TRY(set_dev(d));
-        HIPT(hipStreamWaitEvent(d.stream, r0.ev_sync, 0));
-        HIPT(hipMemcpyPeerAsync(slot(d, gslot), d.dev, slot(r0, gslot), r0.dev, 8, d.stream));
-    }
-    return CGX_OK;
-}
-
-// Every shard's pfull gets every shard's slice of `src(shard)` (its own slice
-// of a full-length buffer when in_place, else a separate local buffer).
-int exchange_allgather(cgx_ctx *c, bool from_x) {
-    if (c->op == OP_POISSON) return exchange_halo(c, from_x);
-    if (p2p(c) && c->mode != M_SINGLE) return p2p_allgather(c, from_x);
-    const size_t es = (size_t)c->es;
-    if (c->mode == M_SINGLE) {
-        if (from_x) {
-            Shard &s = c->sh[0];
-            TRY(set_dev(s));
-            HIPT(hipMemcpyAsync(s.pown, s.x, s.nloc * es, hipMemcpyDeviceToDevice, s.stream));
-        }
-        return CGX_OK;
-    }
-    if (c->mode == M_RCCL) {
-        Shard &s = c->sh[0];
-        TRY(set_dev(s));
-        const ncclDataType_t t = f32ref(c) ? ncclFloat : ncclDouble;
-        const void *send = from_x ? (const void *)s.x : (const void *)s.pown;
-        NCCLT(ncclAllGather(send, s.pfull, (size_t)s.nloc, t, s.comm, s.stream));
-        return CGX_OK;
-    }
-    // LOCAL: device-to-device copies after all producers are done.
-    TRY(local_barrier(c));
-    for (auto &d : c->sh) {
-        TRY(set_dev(d));
-        for (auto &s : c->sh) {
-            char *dst = d.pfull + s.row0 * es;
-            const char *src = from_x ? s.x : s.pown;
-            if (&s == &d && !from_x) continue;
-            HIPT(hipMemcpyPeerAsync(dst, d.dev, src, s.dev, s.nloc * es, d.stream));
-        }
-    }
-    return CGX_OK;
-}
-
-// Combine the per-shard partials in slot `lslot` into the global slot `gslot`.
-int exchange_scalar(cgx_ctx *c, int lslot, int gslot) {
-    if (c->mode == M_SINGLE) return CGX_OK;  // kernels wrote the global slot directly
-    if (p2p(c)) return p2p_scalar(c, lslot, gslot);
-    const int S = (int)c->sh.size();
-    if (c->mode == M_RCCL) {
-        Shard &s = c->sh[0];
-        TRY(set_dev(s));
-        if (f32ref(c)) {
-            // point-to-point_cg.c allSum order: gather the partials, sum in rank order
-            NCCLT(ncclAllGather(slot(s, lslot), slot(s, S_GATHER), 1, ncclUint64, s.comm, s.stream));
-            HIPT(sum_ordered_f32(reinterpret_cast<const float *>(slot(s, S_GATHER)), c->nranks,
-                                 reinterpret_cast<float *>(slot(s, gslot)), s.stream));
-        } else if (c->flags & CGX_DETERMINISTIC) {
-            // fp64, rank-order sum: the same bits as the multi-shard mode with the
-            // same partition, whatever algorithm RCCL would pick for an allreduce
-            NCCLT(ncclAllGather(slot(s, lslot), slot(s, S_GATHER), 1, ncclUint64, s.comm, s.stream));
-            HIPT(sum_ordered_f64(reinterpret_cast<const double *>(slot(s, S_GATHER)), c->nranks,
-                                 reinterpret_cast<double *>(slot(s, gslot)), s.stream));
-        } else {
-            NCCLT(ncclAllReduce(slot(s, lslot), slot(s, gslot), 1, ncclDouble, ncclSum, s.comm, s.stream));
-        }
-        return CGX_OK;
-    }
-    TRY(local_barrier(c));
-    for (auto &d : c->sh) {
-        TRY(set_dev(d));
-        for (auto &s : c->sh)
-            HIPT(hipMemcpyPeerAsync(slot(d, S_GATHER + s.index), d.dev, slot(s, lslot), s.dev, 8, d.stream));
-        if (f32ref(c))
-            HIPT(sum_ordered_f32(reinterpret_cast<const float *>(slot(d, S_GATHER)), S,
-                                 reinterpret_cast<float *>(slot(d, gslot)), d.stream));
-        else
-            HIPT(sum_ordered_f64(reinterpret_cast<const double *>(slot(d, S_GATHER)), S,
-                                 reinterpret_cast<double *>(slot(d, gslot)), d.stream));
-    }
-    return CGX_OK;
-}
-
-// Where a kernel writes its (partial) scalar: the global slot directly when
-// there is nothing to combine, else the shard-local slot.
-inline int out_slot(const cgx_ctx *c, int lslot, int gslot) { return c->mode == M_SINGLE ? gslot : lslot; }
-
-// ---- the iteration pieces ----------------------------------------------------------
-// One tile of the matVec: rows [r0, r0+rows) of this shard, A rows at `Arows`.
-int matvec_rows(cgx_ctx *c, Shard &s, const MatvecPlan &pl, const char *Arows, int64_t r0, int64_t rows,
-                const char *vec, bool fuse_dot, int dot_slot, bool gated = false) {
-    if (f32ref(c)) {
-        HIPT(matvec_ref_f32(reinterpret_cast<const float *>(Arows), c->lda, rows, c->n,
-                            reinterpret_cast<const float *>(vec), reinterpret_cast<float *>(s.Ap) + r0, s.stream));
-    } else {
-        HIPT(matvec_f64(pl, reinterpret_cast<const double *>(Arows), c->lda, rows, c->lda,
-                        reinterpret_cast<const double *>(vec), reinterpret_cast<double *>(s.Ap) + r0,
-                        fuse_dot ? reinterpret_cast<const double *>(s.pown) + r0 : nullptr,
-                        fuse_dot ? reinterpret_cast<double *>(slot(s, dot_slot)) : nullptr, s.ws, s.stream,
-                        gated ? reinterpret_cast<const int64_t *>(slot(s, S_KDONE)) : nullptr));
-    }
-    return CGX_OK;
-}
-
-// CGX_HOST_STREAM matVec: tile t goes to buffer (next_buf++ % kStreamBufs);
-// its copy waits until the kernel that last read that buffer is done (A is
-// read-only, so copies of the next iteration's first tiles overlap this
-// iteration's vector work); its kernel waits for the copy.
-int matvec_streamed(cgx_ctx *c, Shard &s, const char *vec) {
-    const int64_t row_bytes = c->lda * (int64_t)c->es;
-    for (int64_t r0 = 0; r0 < s.nloc; r0 += s.tile_rows) {
-        const int64_t rows = std::min(s.tile_rows, s.nloc - r0);
-        const int b = s.next_buf;
-        s.next_buf = (s.next_buf + 1) % kStreamBufs;
-        const int64_t bytes = rows * row_bytes;
-        const char *src = s.A_host + (size_t)r0 * row_bytes;
-        const int64_t part = (bytes / s.ncopy + 4095) & ~int64_t(4095);
-        for (int q = 0; q < s.ncopy; ++q) {
-            const int64_t lo = std::min<int64_t>(bytes, q * part), hi = std::min<int64_t>(bytes, lo + part);
-            if (s.buf_used[b]) HIPT(hipStreamWaitEvent(s.copy[q], s.ev_free[b], 0));
-            if (hi > lo) HIPT(hipMemcpyAsync(s.tile[b] + lo, src + lo, hi - lo, hipMemcpyHostToDevice, s.copy[q]));
-            HIPT(hipEventRecord(s.ev_loaded[b][q], s.copy[q]));
-            HIPT(hipStreamWaitEvent(s.stream, s.ev_loaded[b][q], 0));
-        }
-        TRY(matvec_rows(c, s, s.tile_plan, s.tile[b], r0, rows, vec, false, 0));
-        HIPT(hipEventRecord(s.ev_free[b], s.stream));
-        s.buf_used[b] = true;
-    }
-    return CGX_OK;
-}
-
-// CGX_SYMMETRIC | CGX_HOST_STREAM: the upper-triangle tiles stream from
-// pinned host memory in chunks (the same buffer rotation and copy streams as
-// matvec_streamed); each chunk's k_symv_f64 writes per-tile row and column
-// partials, and one reduce (with the fused p.Ap) follows the last chunk.
-int matvec_sym_streamed(cgx_ctx *c, Shard &s, const char *vec, bool with_dot, int dot_slot, const int64_t *gate) {
-    const int64_t ntiles = sym_tiles(c->lda), tb = 128 * 128 * 8;
-    const double *p = reinterpret_cast<const double *>(vec);
-    for (int64_t q0 = 0; q0 < ntiles; q0 += s.tile_rows) {
-        const int64_t cnt = std::min(s.tile_rows, ntiles - q0);
-        const int b = s.next_buf;
-        s.next_buf = (s.next_buf + 1) % kStreamBufs;
-        const int64_t bytes = cnt * tb;
-        const char *src = s.A_host + (size_t)q0 * tb;
-        const int64_t part = (bytes / s.ncopy + 4095) & ~int64_t(4095);
-        for (int q = 0; q < s.ncopy; ++q) {
-            const int64_t lo = std::min<int64_t>(bytes, q * part), hi = std::min<int64_t>(bytes, lo + part);
-            if (s.buf_used[b]) HIPT(hipStreamWaitEvent(s.copy[q], s.ev_free[b], 0));
-            if (hi > lo) HIPT(hipMemcpyAsync(s.tile[b] + lo, src + lo, hi - lo, hipMemcpyHostToDevice, s.copy[q]));
-            HIPT(hipEventRecord(s.ev_loaded[b][q], s.copy[q]));
-            HIPT(hipStreamWaitEvent(s.stream, s.ev_loaded[b][q], 0));
-        }
-        HIPT(symv_tiles_f64(reinterpret_cast<const double *>(s.tile[b]), q0, cnt, c->lda, s.sym_grid, true, p,
-                            reinterpret_cast<double *>(s.sym_prow), reinterpret_cast<double *>(s.sym_pcol), s.stream,
-                            gate));
-        HIPT(hipEventRecord(s.ev_free[b], s.stream));
-        s.buf_used[b] = true;
-    }
-    HIPT(symv_reduce_f64(c->n, c->lda, 1, reinterpret_cast<const double *>(s.sym_prow),
-                         reinterpret_cast<const double *>(s.sym_pcol), reinterpret_cast<double *>(s.Ap),
-                         with_dot ? reinterpret_cast<const double *>(s.pown) : nullptr,
-                         with_dot ? reinterpret_cast<double *>(slot(s, dot_slot)) : nullptr, s.ws, s.stream, gate));
-    return CGX_OK;
-}
-
-// The host-mapped convergence record: written by shard 0's deciding kernel only.
-inline int64_t *rec_of(const cgx_ctx *c, const Shard &s, bool gated) {
-    return (gated && &s == &c->sh[0]) ? s.d_rec : nullptr;
-}
-
-inline const int64_t *gate_of(const Shard &s, bool gated) {
-    return gated ? reinterpret_cast<const int64_t *>(slot(s, S_KDONE)) : nullptr;
-}
-
-int launch_matvec(cgx_ctx *c, Shard &s, const char *vec, bool with_dot, int dot_slot, bool gated = false) {
-    const bool timing = (c->flags & CGX_TIMING) && (&s == &c->sh[0]);
-    if (timing && s.ev_used >= kEvPairs) TRY(timing_resolve(c));
-    if (timing) HIPT(hipEventRecord(s.ev_t[2 * s.ev_used], s.stream));
-    const bool streamed = (c->flags & CGX_HOST_STREAM) != 0;
-    if (c->op == OP_POISSON)
-        HIPT(stencil5_f64(reinterpret_cast<const double *>(vec), s.nloc / c->m, c->m, reinterpret_cast<double *>(s.Ap),
-                          with_dot ? reinterpret_cast<double *>(slot(s, dot_slot)) : nullptr, s.ws, s.stream,
-                          gate_of(s, gated)));
-    else if (streamed && (c->flags & CGX_SYMMETRIC))
-        TRY(matvec_sym_streamed(c, s, vec, with_dot, dot_slot, gate_of(s, gated)));
-    else if (streamed) TRY(matvec_streamed(c, s, vec));
-    else if (c->flags & CGX_SYMMETRIC)
-        HIPT(symv_f64(reinterpret_cast<const double *>(s.A), c->n, c->lda, s.sym_grid,
-                      reinterpret_cast<const double *>(vec), reinterpret_cast<double *>(s.sym_prow),
-                      reinterpret_cast<double *>(s.sym_pcol), reinterpret_cast<double *>(s.Ap),
-                      with_dot ? reinterpret_cast<const double *>(s.pown) : nullptr,
-                      with_dot ? reinterpret_cast<double *>(slot(s, dot_slot)) : nullptr, s.ws, s.stream,
-                      gate_of(s, gated)));
-    else TRY(matvec_rows(c, s, s.plan, s.A, 0, s.nloc, vec, with_dot && !f32ref(c), dot_slot, gated));
-    if (timing) {
-        HIPT(hipEventRecord(s.ev_t[2 * s.ev_used + 1], s.stream));
-        s.ev_used++;
-    }
-    if (with_dot && (f32ref(c) || (streamed && !(c->flags & CGX_SYMMETRIC)))) {
-        if (f32ref(c))  // vecVec(p, Ap) sequential (serialConjugate.c:219)
-            HIPT(dot_ref_f32(s.nloc, reinterpret_cast<const float *>(s.pown),
-                             reinterpret_cast<const float *>(s.Ap), reinterpret_cast<float *>(slot(s, dot_slot)),
-                             s.stream));
-        else
-            HIPT(dot_f64(s.nloc, reinterpret_cast<const double *>(s.pown),
-                         reinterpret_cast<const double *>(s.Ap), reinterpret_cast<double *>(slot(s, dot_slot)), s.ws,
-                         s.stream));
-    }
-    return CGX_OK;
-}
-
-int settle_halo(cgx_ctx *c);
-
-// Whether x0 is all zeros on every shard (every rank in rank mode: one
-// int64 allreduce, so all ranks take the same branch of do_begin).
-int x0_is_zero(cgx_ctx *c, bool *zero) {
-    bool local = true;
-    for (auto &s : c->sh) local = local && s.x_zero;
-    if (c->mode != M_RCCL || c->nranks == 1) {
-        *zero = local;
-        return CGX_OK;
-    }
-    Shard &s = c->sh[0];
-    TRY(set_dev(s));
-    int64_t *pin = reinterpret_cast<int64_t *>(s.h_pin);
-    pin[0] = local ? 0 : 1;
-    HIPT(hipMemcpyAsync(slot(s, S_XNZ), pin, 8, hipMemcpyHostToDevice, s.stream));
-    NCCLT(ncclAllReduce(slot(s, S_XNZ), slot(s, S_XNZ), 1, ncclInt64, ncclSum, s.comm, s.stream));
-    HIPT(hipMemcpyAsync(pin, slot(s, S_XNZ), 8, hipMemcpyDeviceToHost, s.stream));
-    HIPT(hipStreamSynchronize(s.stream));
-    *zero = pin[0] == 0;
-    return CGX_OK;
-}
-
-int do_begin(cgx_ctx *c) {
-    // r0 = p0 = b - A x0; rr0 = r0.r0   (serialConjugate.c:209-212, parallel_cg.c:283-287)
-    // With x0 = 0 (the reference's usual initialguess, and the bench's) A x0 is
-    // exactly zero, so the exchange and the matVec are skipped: r0 = b - 0 = b
-    // bit for bit, one matVec fewer per solve.
-    TRY(settle_halo(c));
-    bool zero = false;
-    TRY(x0_is_zero(c, &zero));
-    if (!zero) TRY(exchange_allgather(c, /*from_x=*/true));  // full x0 into pfull
-    const int gs = S_RR + ring(0), ls = S_LRR + ring(0);
-    const int os = out_slot(c, ls, gs);
-    for (auto &s : c->sh) {
-        TRY(set_dev(s));
-        if (zero)
-            HIPT(hipMemsetAsync(s.Ap, 0, (size_t)s.nloc * c->es, s.stream));
-        else
-            TRY(launch_matvec(c, s, s.pfull, false, 0));
-        s.x_zero = false;  // the iterations update x
-        if (f32ref(c)) {
-            float *pown = reinterpret_cast<float *>(s.pown);
-            HIPT(residual_ref_f32(s.nloc, reinterpret_cast<const float *>(s.b), reinterpret_cast<const float *>(s.Ap),
-                                  reinterpret_cast<float *>(s.r), pown, s.stream));
-            HIPT(dot_ref_f32(s.nloc, reinterpret_cast<const float *>(s.r), reinterpret_cast<const float *>(s.r),
-                             reinterpret_cast<float *>(slot(s, os)), s.stream));
-        } else {
-            double *pown = reinterpret_cast<double *>(s.pown);
-            HIPT(residual_f64(s.nloc, reinterpret_cast<const double *>(s.b), reinterpret_cast<const double *>(s.Ap),
-                              reinterpret_cast<double *>(s.r), pown, reinterpret_cast<double *>(slot(s, os)), s.ws,
-                              s.stream));
-        }
-    }
-    TRY(exchange_scalar(c, ls, gs));
-    if (c->fused) TRY(exchange_halo_of(c, &Shard::rh));  // r0's halo rows for k_poisson_p
-    for (auto &s : c->sh) {  // device-side convergence record: not converged
-        TRY(set_dev(s));
-        HIPT(hipMemsetAsync(slot(s, S_KDONE), 0, 16, s.stream));
-        s.h_rec[0] = s.h_rec[1] = 0;  // no kernel of this solve has run yet (do_begin follows a sync)
-    }
-    c->k = 0;
-    c->converged = 0;
-    c->state = ST_BEGUN;
-    return CGX_OK;
-}
-
-int read_scalar(cgx_ctx *c, int gslot, double *out) {
-    Shard &s = c->sh[0];
-    TRY(set_dev(s));
-    HIPT(hipMemcpyAsync(s.h_pin, slot(s, gslot), 8, hipMemcpyDeviceToHost, s.stream));
-    HIPT(hipStreamSynchronize(s.stream));
-    if (f32ref(c)) {
-        float f;
-        std::memcpy(&f, s.h_pin, 4);
-        *out = (double)f;
-    } else {
-        *out = s.h_pin[0];
-    }
-    return CGX_OK;
-}
-
-// Overlapped exchange + matVec: p is allgathered on each shard's comm
-// stream while the compute stream multiplies the shard's own column block
-// (its own p is already local); the rest of the columns follow once the
-// gather has landed, accumulating into Ap with the fused p.Ap partial.
-int overlapped_matvec(cgx_ctx *c, int dot_slot, bool gated) {
-    const size_t es = (size_t)c->es;
-    for (auto &s : c->sh) {
-        TRY(set_dev(s));
-        HIPT(hipEventRecord(s.ev_pready, s.stream));
-    }
-    if (c->mode == M_RCCL) {
-        Shard &s = c->sh[0];
-        HIPT(hipStreamWaitEvent(s.cstream, s.ev_pready, 0));
-        NCCLT(ncclAllGather(s.pown, s.pfull, (size_t)s.nloc, ncclDouble, s.comm, s.cstream));
-        HIPT(hipEventRecord(s.ev_gathered, s.cstream));
-    } else {
-        for (auto &d : c->sh) {
-            TRY(set_dev(d));
-            for (auto &s : c->sh) HIPT(hipStreamWaitEvent(d.cstream, s.ev_pready, 0));
-            for (auto &s : c->sh)
-                if (&s != &d)
-                    HIPT(hipMemcpyPeerAsync(d.pfull + s.row0 * es, d.dev, s.pown, s.dev, s.nloc * es, d.cstream));
-            HIPT(hipEventRecord(d.ev_gathered, d.cstream));
-        }
-    }
-    for (auto &s : c->sh) {
-        TRY(set_dev(s));
-        const bool timing = (c->flags & CGX_TIMING) && (&s == &c->sh[0]);
-        if (timing && s.ev_used >= kEvPairs) TRY(timing_resolve(c));
-        if (timing) HIPT(hipEventRecord(s.ev_t[2 * s.ev_used], s.stream));
-        const double *A = reinterpret_cast<const double *>(s.A);
-        const double *v = reinterpret_cast<const double *>(s.pfull);
-        double *Ap = reinterpret_cast<double *>(s.Ap);
-        HIPT(matvec_f64_cols(s.plan, A, c->lda, s.nloc, c->lda, s.row0, s.nloc, false, v, Ap, nullptr, nullptr,
-                             s.ws, s.stream, gate_of(s, gated)));
-        HIPT(hipStreamWaitEvent(s.stream, s.ev_gathered, 0));
-        HIPT(matvec_f64_cols(s.plan, A, c->lda, s.nloc, c->lda, (s.row0 + s.nloc) % c->lda, c->lda - s.nloc, true,
-                             v, Ap, reinterpret_cast<const double *>(s.pown),
-                             reinterpret_cast<double *>(slot(s, dot_slot)), s.ws, s.stream, gate_of(s, gated)));
-        if (timing) {
-            HIPT(hipEventRecord(s.ev_t[2 * s.ev_used + 1], s.stream));
-            s.ev_used++;
-        }
-    }
-    return CGX_OK;
-}
-
-// Overlapped r halo exchange (several slabs): on the comm streams, after
-// everything already on the compute streams (the r update and the r.r
-// allreduce, so two RCCL operations never run at once).  The next
-// k_poisson_p runs its interior runs meanwhile and waits for ev_gathered
-// before its two edge runs.
-int exchange_halo_async(cgx_ctx *c) {
-    const size_t row = (size_t)c->m * (size_t)c->es;
-    const int64_t mloc = c->sh[0].nloc / c->m;
-    for (auto &s : c->sh) {
-        TRY(set_dev(s));
-        HIPT(hipEventRecord(s.ev_pready, s.stream));
-    }
-    if (c->mode == M_RCCL) {
-        Shard &s = c->sh[0];
-        const int g = s.index;
-        char *base = s.rh, *own = base + row;
-        HIPT(hipStreamWaitEvent(s.cstream, s.ev_pready, 0));
-        NCCLT(ncclGroupStart());
-        if (g > 0) {
-            NCCLT(ncclSend(own, (size_t)c->m, ncclDouble, g - 1, s.comm, s.cstream));
-            NCCLT(ncclRecv(base, (size_t)c->m, ncclDouble, g - 1, s.comm, s.cstream));
-        }
-        if (g < c->nranks - 1) {
-            NCCLT(ncclSend(own + (size_t)(mloc - 1) * row, (size_t)c->m, ncclDouble, g + 1, s.comm, s.cstream));
-            NCCLT(ncclRecv(own + (size_t)mloc * row, (size_t)c->m, ncclDouble, g + 1, s.comm, s.cstream));
-        }
-        NCCLT(ncclGroupEnd());
-        HIPT(hipEventRecord(s.ev_gathered, s.cstream));
-    } else {
-        const int S = (int)c->sh.size();
-        for (int q = 0; q < S; ++q) {
-            Shard &d = c->sh[q];
-            TRY(set_dev(d));
-            for (auto &s : c->sh) HIPT(hipStreamWaitEvent(d.cstream, s.ev_pready, 0));
-            if (q > 0) {
-                const Shard &u = c->sh[q - 1];
-                HIPT(hipMemcpyPeerAsync(d.rh, d.dev, u.rh + (size_t)mloc * row, u.dev, row, d.cstream));
-            }
-            if (q < S - 1) {
-                const Shard &w = c->sh[q + 1];
-                HIPT(hipMemcpyPeerAsync(d.rh + (size_t)(mloc + 1) * row, d.dev, w.rh + row, w.dev, row, d.cstream));
-            }
-            HIPT(hipEventRecord(d.ev_gathered, d.cstream));
-        }
-    }
-    c->halo_pending = true;
-    return CGX_OK;
-}
-
-// Order every compute stream after an overlapped halo exchange still in
-// flight (before anything else touches r or its halo rows).
-int settle_halo(cgx_ctx *c) {
-    if (!c->halo_pending) return CGX_OK;
-    for (auto &s : c->sh) {
-        TRY(set_dev(s));
-        HIPT(hipStreamWaitEvent(s.stream, s.ev_gathered, 0));
-    }
-    c->halo_pending = false;
-    return CGX_OK;
-}
-
-// Fused Poisson iteration k (conjgrad.m's loop, two kernels, 64 B per grid
-// point; see k_poisson_p_f64 / k_poisson_xr_f64):
-//   p_k = r_k + beta p_{k-1}, p_k . A p_k      (gated: first decides the
-//                                               previous iteration's stop)
-//   allreduce(p.Ap)
-//   x += alpha p_k, r -= alpha A p_k, r.r
-//   allreduce(r.r); host-checked stop; r's halo rows for the next iteration.
-// x is current after every iteration, so a converged solve needs no extra pass.
-int do_iteration_poisson(cgx_ctx *c, double eps, int *stop, bool gated) {
-    const int64_t k = c->k;
-    *stop = 0;
-    const int64_t m = c->m;
-    const int pg = S_PAP + ring(k), pl = S_LPAP + ring(k);
-    const int rk = S_RR + ring(k), rkm1 = S_RR + ring(k + 3);  // r.r of iterations k, k-1
-    auto D = [](void *p) { return reinterpret_cast<double *>(p); };
-    const bool split = c->halo_pending;  // interior runs while the r halo exchange is in flight
-    for (auto &s : c->sh) {
-        TRY(set_dev(s));
-        char *pold = (k & 1) ? s.pfull : s.p2, *pnew = (k & 1) ? s.p2 : s.pfull;
-        for (int part : split ? std::initializer_list<int>{1, 2} : std::initializer_list<int>{0}) {
-            if (part == 2) HIPT(hipStreamWaitEvent(s.stream, s.ev_gathered, 0));
-            HIPT(poisson_p_f64(D(s.rh), D(pold), D(pnew), s.nloc / m, m, D(slot(s, rk)), D(slot(s, rkm1)), k == 0,
-                               D(slot(s, out_slot(c, pl, pg))), s.ws, s.stream, gated ? eps : -1.0, k,
-                               gated ? reinterpret_cast<int64_t *>(slot(s, S_KDONE)) : nullptr,
-                               gated ? D(slot(s, S_RRFINAL)) : nullptr, part, rec_of(c, s, gated)));
-        }
-    }
-    c->halo_pending = false;
-    TRY(exchange_scalar(c, pl, pg));
-    const int rg = S_RR + ring(k + 1), rl = S_LRR + ring(k + 1);
-    const int ro = out_slot(c, rl, rg);
-    for (auto &s : c->sh) {
-        TRY(set_dev(s));
-        const bool timing = (c->flags & CGX_TIMING) && (&s == &c->sh[0]);
-        if (timing && s.ev_used >= kEvPairs) TRY(timing_resolve(c));
-        if (timing) HIPT(hipEventRecord(s.ev_t[2 * s.ev_used], s.stream));
-        char *pnew = (k & 1) ? s.p2 : s.pfull;
-        HIPT(poisson_xr_f64(D(pnew), D(s.x), D(s.r), s.nloc / m, m, D(slot(s, rk)), D(slot(s, pg)), D(slot(s, ro)),
-                            s.ws, s.stream, gate_of(s, gated)));
-        if (timing) {
-            HIPT(hipEventRecord(s.ev_t[2 * s.ev_used + 1], s.stream));
-            s.ev_used++;
-        }
-    }
-    TRY(exchange_scalar(c, rl, rg));
-    c->k = k + 1;
-    c->total_iters += 1;
-    if (!gated && eps >= 0.0) {
-        double rr = 0.0;
-        TRY(read_scalar(c, rg, &rr));
-        c->last_rr = rr;
-        if (std::sqrt(rr) < eps) {
-            c->converged = 1;
-            c->state = ST_CONVERGED;
-            *stop = 1;
-            return CGX_OK;
-        }
-    }
-    return c->halo_overlap ? exchange_halo_async(c) : exchange_halo_of(c, &Shard::rh);
-}
-
-// One loop iteration k (serialConjugate.c:215-244 / parallel_cg.c:290-323).
-// Returns 1 in *stop when sqrt(r.r) < eps ended the loop (before the p update,
-// as the reference breaks at :235-238).
-// gated: fp64 device-side convergence (the host does not read r.r here; the
-// update kernel decides sqrt(r.r) < eps and later kernels skip themselves).
-int do_iteration(cgx_ctx *c, double eps, int *stop, bool gated = false) {
-    if (c->fused) return do_iteration_poisson(c, eps, stop, gated);
-    const int64_t k = c->k;
-    *stop = 0;
-    const int pg = S_PAP + ring(k), pl = S_LPAP + ring(k);
-    if (c->overlap) {
-        TRY(overlapped_matvec(c, out_slot(c, pl, pg), gated));  // parallel_cg.c:290-293, overlapped
-    } else {
-        TRY(exchange_allgather(c, false));  // MPI_Allgather(local_p -> p)  parallel_cg.c:290
-        for (auto &s : c->sh) {
-            TRY(set_dev(s));
-            TRY(launch_matvec(c, s, s.pfull, true, out_slot(c, pl, pg), gated));  // :215 / :292-293
-        }
-    }
-    TRY(exchange_scalar(c, pl, pg));  // MPI_Allreduce(p.Ap)  parallel_cg.c:294
-    const int rg = S_RR + ring(k + 1), rl = S_LRR + ring(k + 1);
-    const int ro = out_slot(c, rl, rg);
-    for (auto &s : c->sh) {
-        TRY(set_dev(s));
-        if (f32ref(c)) {
-            HIPT(update_xr_ref_f32(s.nloc, reinterpret_cast<float *>(s.x), reinterpret_cast<float *>(s.r),
-                                   reinterpret_cast<const float *>(s.pown),
-                                   reinterpret_cast<const float *>(s.Ap),
-                                   reinterpret_cast<const float *>(slot(s, S_RR + ring(k))),
-                                   reinterpret_cast<const float *>(slot(s, pg)), s.stream));
-            HIPT(dot_ref_f32(s.nloc, reinterpret_cast<const float *>(s.r), reinterpret_cast<const float *>(s.r),
-                             reinterpret_cast<float *>(slot(s, ro)), s.stream));
-        } else {
-            // r -= alpha Ap, r.r; x's update is deferred into the p update
-            HIPT(update_r_f64(s.nloc, reinterpret_cast<double *>(s.r), reinterpret_cast<const double *>(s.Ap),
-                              reinterpret_cast<const double *>(slot(s, S_RR + ring(k))),
-                              reinterpret_cast<const double *>(slot(s, pg)), reinterpret_cast<double *>(slot(s, ro)),
-                              s.ws, s.stream, gate_of(s, gated)));
-        }
-    }
-    TRY(exchange_scalar(c, rl, rg));  // MPI_Allreduce(r.r)  parallel_cg.c:313
-    c->k = k + 1;
-    c->total_iters += 1;
-    if (gated) {  // x (+ p unless converged) on the device, stopping rule decided there
-        for (auto &s : c->sh) {
-            TRY(set_dev(s));
-            HIPT(update_xp_f64(s.nloc, reinterpret_cast<double *>(s.x), reinterpret_cast<double *>(s.pown),
-                               reinterpret_cast<const double *>(s.r),
-                               reinterpret_cast<const double *>(slot(s, S_RR + ring(k))),
-                               reinterpret_cast<const double *>(slot(s, pg)),
-                               reinterpret_cast<const double *>(slot(s, rg)), s.stream, eps, k,
-                               reinterpret_cast<int64_t *>(slot(s, S_KDONE)),
-                               reinterpret_cast<double *>(slot(s, S_RRFINAL)), rec_of(c, s, gated)));
-        }
-        return CGX_OK;
-    }
-    if (eps >= 0.0) {  // if (sqrt(beta) < EPSILON) break;  serialConjugate.c:235-238
-        double rr = 0.0;
-        TRY(read_scalar(c, rg, &rr));
-        c->last_rr = rr;
-        if (std::sqrt(rr) < eps) {
-            c->converged = 1;
-            c->state = ST_CONVERGED;
-            *stop = 1;
-            if (!f32ref(c))  // the deferred x += alpha p, without the p update
-                for (auto &s : c->sh) {
-                    TRY(set_dev(s));
-                    HIPT(update_xp_f64(s.nloc, reinterpret_cast<double *>(s.x), reinterpret_cast<double *>(s.pown),
-                                       reinterpret_cast<const double *>(s.r),
-                                       reinterpret_cast<const double *>(slot(s, S_RR + ring(k))),
-                                       reinterpret_cast<const double *>(slot(s, pg)), nullptr, s.stream));
-                }
-            return CGX_OK;
-        }
-    }
-    for (auto &s : c->sh) {  // p = r + (beta/rsold) p    serialConjugate.c:239-243
-        TRY(set_dev(s));
-        if (f32ref(c))
-            HIPT(update_p_ref_f32(s.nloc, reinterpret_cast<float *>(s.pown),
-                                  reinterpret_cast<const float *>(s.r), reinterpret_cast<const float *>(slot(s, rg)),
-                                  reinterpret_cast<const float *>(slot(s, S_RR + ring(k))), s.stream));
-        else  // x += alpha p (deferred from the r update), then p = r + beta p
-            HIPT(update_xp_f64(s.nloc, reinterpret_cast<double *>(s.x), reinterpret_cast<double *>(s.pown),
-                               reinterpret_cast<const double *>(s.r),
-                               reinterpret_cast<const double *>(slot(s, S_RR + ring(k))),
-                               reinterpret_cast<const double *>(slot(s, pg)),
-                               reinterpret_cast<const double *>(slot(s, rg)), s.stream));
-    }
-    return CGX_OK;
-}
-
-int sync_all(cgx_ctx *c) {
-    for (auto &s : c->sh) {
-        TRY(set_dev(s));
-        HIPT(hipStreamSynchronize(s.stream));
-        for (int q = 0; q < s.ncopy; ++q) HIPT(hipStreamSynchronize(s.copy[q]));
-        if (s.cstream) HIPT(hipStreamSynchronize(s.cstream));
-    }
-    return timing_resolve(c);
 }
 
 // Per-device workspace for the kernel-level entry points.
@@ -1216,11 +68,8 @@ int check_dtype(int dtype) {
     return CGX_OK;
 }
 
-}  // namespace
+}  // namespace cgxh
 
-// =====================================================================================
-// C ABI
-// =====================================================================================
 extern "C" {
 
 const char *cgx_strerror(int code) {
@@ -1246,624 +95,6 @@ int cgx_device_count(int *count) {
     hipError_t e = hipGetDeviceCount(&n);
     if (e != hipSuccess) n = 0;
     *count = n;
-    return CGX_OK;
-}
-
-static int check_device(int device) {
-    int n = 0;
-    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(CGX_ERR_NODEV, "no HIP device visible");
-    if (device < 0 || device >= n) return fail(CGX_ERR_ARG, "device %d out of range (%d visible)", device, n);
-    return CGX_OK;
-}
-
-// Operator-generic constructors.  Dense: n unknowns, row blocks of n/P rows.
-// Poisson: n = m*m unknowns, slabs of m/P grid rows (n/P unknowns).
-static int check_op(int op, int64_t n, int64_t m, int parts, int flags) {
-    if (op == OP_POISSON) {
-        if (m < 1) return fail(CGX_ERR_ARG, "m must be >= 1");
-        if (m % parts != 0) return fail(CGX_ERR_SHAPE, "%lld is not divisible by %d", (long long)m, parts);
-        if (flags & (CGX_F32_REF | CGX_HOST_STREAM | CGX_COMM_P2P))
-            return fail(CGX_ERR_ARG, "the Poisson operator supports CGX_F64 (+CGX_TIMING) only");
-        return CGX_OK;
-    }
-    if ((flags & CGX_SYMMETRIC) && (parts != 1 || (flags & CGX_F32_REF)))
-        return fail(CGX_ERR_ARG, "CGX_SYMMETRIC: fp64 on one GPU only (no CGX_F32_REF)");
-    return check_n(n, parts);
-}
-
-static cgx_ctx *new_ctx_op(int op, int64_t n, int64_t m, int parts, int flags) {
-    cgx_ctx *c = new_ctx(n, parts, flags);
-    if (!c) return nullptr;
-    c->op = op;
-    c->m = m;
-    if (op == OP_POISSON) c->lda = m;
-    return c;
-}
-
-static int create_single(cgx_ctx **ctx, int op, int64_t n, int64_t m, int device, int flags) {
-    if (!ctx) return fail(CGX_ERR_ARG, "ctx is NULL");
-    *ctx = nullptr;
-    TRY(check_op(op, n, m, 1, flags));
-    TRY(check_device(device));
-    cgx_ctx *c = new_ctx_op(op, n, m, 1, flags);
-    if (!c) return fail(CGX_ERR_NOMEM, "host allocation failed");
-    c->mode = M_SINGLE;
-    c->sh.resize(1);
-    c->sh[0].dev = device;
-    c->sh[0].index = 0;
-    c->sh[0].row0 = 0;
-    c->sh[0].nloc = n;
-    return finish_create(c, ctx);
-}
-
-static int create_multi(cgx_ctx **ctx, int op, int64_t n, int64_t m, int nshards, const int *devices, int flags) {
-    if (!ctx || !devices) return fail(CGX_ERR_ARG, "ctx/devices is NULL");
-    *ctx = nullptr;
-    if (nshards < 1 || nshards > kMaxShards) return fail(CGX_ERR_ARG, "nshards must be in [1, %d]", kMaxShards);
-    TRY(check_op(op, n, m, nshards, flags));
-    for (int i = 0; i < nshards; ++i) TRY(check_device(devices[i]));
-    cgx_ctx *c = new_ctx_op(op, n, m, nshards, flags);
-    if (!c) return fail(CGX_ERR_NOMEM, "host allocation failed");
-    c->mode = nshards == 1 ? M_SINGLE : M_LOCAL;
-    c->sh.resize(nshards);
-    const int64_t loc = n / nshards;
-    for (int i = 0; i < nshards; ++i) {
-        c->sh[i].dev = devices[i];
-        c->sh[i].index = i;
-        c->sh[i].row0 = (int64_t)i * loc;
-        c->sh[i].nloc = loc;
-    }
-    // Peer access between distinct devices (xGMI); repeated devices need none.
-    for (int i = 0; i < nshards; ++i)
-        for (int j = 0; j < nshards; ++j)
-            if (devices[i] != devices[j]) {
-                (void)hipSetDevice(devices[i]);
-                hipError_t e = hipDeviceEnablePeerAccess(devices[j], 0);
-                if (e == hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
-            }
-    return finish_create(c, ctx);
-}
-
-static int create_rank(cgx_ctx **ctx, int op, int64_t n, int64_t m, int rank, int nranks, const cgx_unique_id *id,
-                       int device, int flags) {
-    if (!ctx || !id) return fail(CGX_ERR_ARG, "ctx/id is NULL");
-    *ctx = nullptr;
-    TRY(check_op(op, n, m, nranks, flags));
-    if (rank < 0 || rank >= nranks) return fail(CGX_ERR_ARG, "rank %d not in [0, %d)", rank, nranks);
-    if (nranks > S_TR - S_GATHER) return fail(CGX_ERR_ARG, "at most %d ranks", S_TR - S_GATHER);
-    TRY(check_device(device));
-    cgx_ctx *c = new_ctx_op(op, n, m, nranks, flags);
-    if (!c) return fail(CGX_ERR_NOMEM, "host allocation failed");
-    c->mode = M_RCCL;
-    c->sh.resize(1);
-    Shard &s = c->sh[0];
-    s.dev = device;
-    s.index = rank;
-    s.nloc = n / nranks;
-    s.row0 = (int64_t)rank * s.nloc;
-    if (hipSetDevice(device) != hipSuccess) {
-        delete c;
-        return fail(CGX_ERR_HIP, "hipSetDevice(%d) failed", device);
-    }
-    ncclUniqueId u;
-    std::memcpy(&u, id, sizeof u);
-    ncclResult_t nr = ncclCommInitRank(&s.comm, nranks, u, rank);
-    if (nr != ncclSuccess) {
-        delete c;
-        return fail(CGX_ERR_RCCL, "ncclCommInitRank(rank %d of %d): %s", rank, nranks, ncclGetErrorString(nr));
-    }
-    return finish_create(c, ctx);
-}
-
-int cgx_create(cgx_ctx **ctx, int64_t n, int device, int flags) {
-    return create_single(ctx, OP_DENSE, n, 0, device, flags);
-}
-
-int cgx_create_multi(cgx_ctx **ctx, int64_t n, int nshards, const int *devices, int flags) {
-    return create_multi(ctx, OP_DENSE, n, 0, nshards, devices, flags);
-}
-
-int cgx_get_unique_id(cgx_unique_id *id) {
-    if (!id) return fail(CGX_ERR_ARG, "id is NULL");
-    static_assert(sizeof(ncclUniqueId) == sizeof(cgx_unique_id), "unique id size");
-    ncclUniqueId u;
-    NCCLT(ncclGetUniqueId(&u));
-    std::memcpy(id, &u, sizeof u);
-    return CGX_OK;
-}
-
-int cgx_create_rank(cgx_ctx **ctx, int64_t n, int rank, int nranks, const cgx_unique_id *id, int device,
-                    int flags) {
-    return create_rank(ctx, OP_DENSE, n, 0, rank, nranks, id, device, flags);
-}
-
-static int check_m(int64_t m) {
-    if (m < 1 || m > 46340 * 4) return fail(CGX_ERR_ARG, "grid width m out of range");
-    return CGX_OK;
-}
-
-int cgx_create_poisson(cgx_ctx **ctx, int64_t m, int device, int flags) {
-    TRY(check_m(m));
-    return create_single(ctx, OP_POISSON, m * m, m, device, flags);
-}
-
-int cgx_create_poisson_multi(cgx_ctx **ctx, int64_t m, int nshards, const int *devices, int flags) {
-    TRY(check_m(m));
-    return create_multi(ctx, OP_POISSON, m * m, m, nshards, devices, flags);
-}
-
-int cgx_create_poisson_rank(cgx_ctx **ctx, int64_t m, int rank, int nranks, const cgx_unique_id *id, int device,
-                            int flags) {
-    TRY(check_m(m));
-    return create_rank(ctx, OP_POISSON, m * m, m, rank, nranks, id, device, flags);
-}
-
-int cgx_fill(cgx_ctx *c, double b_value, double x_value) {
-    if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
-    for (auto &s : c->sh) {
-        TRY(set_dev(s));
-        if (f32ref(c)) {
-            HIPT(fill_f32(reinterpret_cast<float *>(s.b), s.nloc, (float)b_value, s.stream));
-            HIPT(fill_f32(reinterpret_cast<float *>(s.x), s.nloc, (float)x_value, s.stream));
-        } else {
-            HIPT(fill_f64(reinterpret_cast<double *>(s.b), s.nloc, b_value, s.stream));
-            HIPT(fill_f64(reinterpret_cast<double *>(s.x), s.nloc, x_value, s.stream));
-        }
-        s.x_zero = x_value == 0.0;
-    }
-    TRY(sync_all(c));
-    c->state = ST_IDLE;
-    return CGX_OK;
-}
-
-int cgx_destroy(cgx_ctx *ctx) {
-    if (!ctx) return CGX_OK;
-    if (ctx->graph) (void)hipGraphExecDestroy(ctx->graph);
-    for (auto &s : ctx->sh) free_shard(s);
-    delete ctx;
-    return CGX_OK;
-}
-
-int cgx_get_info(const cgx_ctx *c, cgx_info *info) {
-    if (!c || !info) return fail(CGX_ERR_ARG, "NULL argument");
-    info->n = c->n;
-    info->lda = c->lda;
-    info->nranks = c->nranks;
-    info->nshards = (int)c->sh.size();
-    info->rank0 = c->sh[0].index;
-    info->row0 = c->sh[0].row0;
-    info->nrows = 0;
-    for (auto &s : c->sh) info->nrows += s.nloc;
-    info->flags = c->flags | (c->overlap ? CGX_OVERLAP_ACTIVE : 0) | (c->fused ? CGX_FUSED_ACTIVE : 0);
-    info->elem_bytes = c->es;
-    return CGX_OK;
-}
-
-int cgx_set_rows(cgx_ctx *c, int64_t row0, int64_t nrows, const void *A_rows, int64_t lda_host,
-                 const void *b_rows, const void *x_rows) {
-    const Range range_("cgx_set_rows");
-    if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
-    if (row0 < 0 || nrows < 0 || row0 + nrows > c->n)
-        return fail(CGX_ERR_SHAPE, "rows [%lld, %lld) outside [0, %lld)", (long long)row0,
-                    (long long)(row0 + nrows), (long long)c->n);
-    if (A_rows && c->op == OP_POISSON) return fail(CGX_ERR_ARG, "the Poisson operator is matrix-free: A must be NULL");
-    if (A_rows && lda_host < c->n) return fail(CGX_ERR_ARG, "lda_host (%lld) < n", (long long)lda_host);
-    const size_t es = (size_t)c->es;
-    for (auto &s : c->sh) {
-        const int64_t lo = std::max(row0, s.row0), hi = std::min(row0 + nrows, s.row0 + s.nloc);
-        if (hi <= lo) continue;
-        TRY(set_dev(s));
-        if (A_rows && s.A_host && (c->flags & CGX_SYMMETRIC)) {
-            // pack on the host: row i supplies columns 128*(i/128) .. lda-1 of its tile row
-            const int64_t nt = c->lda / 128;
-            double *At = reinterpret_cast<double *>(s.A_host);
-            for (int64_t i = lo; i < hi; ++i) {
-                const double *row = static_cast<const double *>(A_rows) + (size_t)(i - row0) * lda_host;
-                const int64_t I = i / 128;
-                const int r = (int)(i % 128);
-                for (int64_t j = I * 128; j < c->lda; ++j)
-                    At[(sym_off_h(I, nt) + j / 128 - I) * 128 * 128 + sym_pos_h(r, (int)(j % 128))] =
-                        j < c->n ? row[j] : 0.0;
-            }
-        } else if (A_rows && s.A_host) {
-            for (int64_t i = lo; i < hi; ++i) {
-                char *dst = s.A_host + (size_t)(i - s.row0) * c->lda * es;
-                std::memcpy(dst, static_cast<const char *>(A_rows) + (size_t)(i - row0) * lda_host * es, (size_t)c->n * es);
-                if (c->lda > c->n) std::memset(dst + (size_t)c->n * es, 0, (size_t)(c->lda - c->n) * es);
-            }
-        } else if (A_rows && (c->flags & CGX_SYMMETRIC)) {
-            // rows through a staging buffer, then packed into the tiles
-            if (!s.sym_stage) {
-                s.sym_stage_rows = std::max<int64_t>(1, std::min<int64_t>(c->n, (int64_t)(128 << 20) / (c->lda * 8)));
-                HIPT(hipMalloc(&s.sym_stage, (size_t)s.sym_stage_rows * c->lda * 8));
-            }
-            for (int64_t i0 = lo; i0 < hi; i0 += s.sym_stage_rows) {
-                const int64_t k = std::min(s.sym_stage_rows, hi - i0);
-                HIPT(hipMemcpy2DAsync(s.sym_stage, (size_t)c->lda * 8,
-                                      static_cast<const char *>(A_rows) + (size_t)(i0 - row0) * lda_host * 8,
-                                      (size_t)lda_host * 8, (size_t)c->n * 8, (size_t)k, hipMemcpyHostToDevice,
-                                      s.stream));
-                HIPT(sym_pack_f64(reinterpret_cast<const double *>(s.sym_stage), c->lda, i0, k, c->n, c->lda,
-                                  reinterpret_cast<double *>(s.A), s.stream));
-            }
-        } else if (A_rows && lda_host == c->lda && c->lda == c->n) {
-            // same row pitch on both sides: one contiguous copy (a pitched copy
-            // of the same bytes ran at a third of the rate from pinned memory)
-            HIPT(hipMemcpyAsync(s.A + (size_t)(lo - s.row0) * c->lda * es,
-                                static_cast<const char *>(A_rows) + (size_t)(lo - row0) * lda_host * es,
-                                (size_t)(hi - lo) * c->lda * es, hipMemcpyHostToDevice, s.stream));
-        } else if (A_rows)
-            HIPT(hipMemcpy2DAsync(s.A + (size_t)(lo - s.row0) * c->lda * es, (size_t)c->lda * es,
-                                  static_cast<const char *>(A_rows) + (size_t)(lo - row0) * lda_host * es,
-                                  (size_t)lda_host * es, (size_t)c->n * es, (size_t)(hi - lo), hipMemcpyHostToDevice,
-                                  s.stream));
-        if (b_rows)
-            HIPT(hipMemcpyAsync(s.b + (lo - s.row0) * es, static_cast<const char *>(b_rows) + (lo - row0) * es,
-                                (hi - lo) * es, hipMemcpyHostToDevice, s.stream));
-        if (x_rows) {
-            HIPT(hipMemcpyAsync(s.x + (lo - s.row0) * es, static_cast<const char *>(x_rows) + (lo - row0) * es,
-                                (hi - lo) * es, hipMemcpyHostToDevice, s.stream));
-            bool zeros = true;  // +0 / -0 only (A x is then exactly zero)
-            const char *xs = static_cast<const char *>(x_rows) + (lo - row0) * es;
-            for (int64_t i = 0; i < hi - lo && zeros; ++i)
-                zeros = es == 4 ? reinterpret_cast<const float *>(xs)[i] == 0.0f
-                                : reinterpret_cast<const double *>(xs)[i] == 0.0;
-            const bool whole = lo == s.row0 && hi == s.row0 + s.nloc;
-            s.x_zero = whole ? zeros : (s.x_zero && zeros);
-        }
-        HIPT(hipStreamSynchronize(s.stream));
-    }
-    c->state = ST_IDLE;
-    return CGX_OK;
-}
-
-int cgx_set_system(cgx_ctx *c, const void *A, const void *b, const void *x0) {
-    if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
-    return cgx_set_rows(c, 0, c->n, A, c->n, b, x0);
-}
-
-int cgx_generate_spd(cgx_ctx *c, uint64_t seed) {
-    const Range range_("cgx_generate_spd");
-    if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
-    if (c->op == OP_POISSON) return fail(CGX_ERR_ARG, "the Poisson operator has no matrix to generate (use cgx_fill)");
-    for (auto &s : c->sh) {
-        TRY(set_dev(s));
-        if (s.A_host && (c->flags & CGX_SYMMETRIC)) {
-            // the packed tiles chunk by chunk on the device, then to the host copy
-            const int64_t ntiles = sym_tiles(c->lda), tb = 128 * 128 * 8;
-            for (int64_t q0 = 0; q0 < ntiles; q0 += s.tile_rows) {
-                const int64_t cnt = std::min(s.tile_rows, ntiles - q0);
-                HIPT(gen_spd_sym_tiles_f64(c->n, c->lda, seed, q0, cnt, reinterpret_cast<double *>(s.tile[0]),
-                                           s.stream));
-                HIPT(hipMemcpyAsync(s.A_host + (size_t)q0 * tb, s.tile[0], (size_t)cnt * tb, hipMemcpyDeviceToHost,
-                                    s.stream));
-            }
-            HIPT(gen_b_f64(c->n, seed, reinterpret_cast<double *>(s.b), s.stream));
-            HIPT(hipStreamSynchronize(s.stream));
-        } else if (s.A_host) {
-            // Generate each tile on the device and move it to the host copy of A;
-            // b is generated for the whole block first (rows are independent).
-            const int64_t row_bytes = c->lda * (int64_t)c->es;
-            for (int64_t r0 = 0; r0 < s.nloc; r0 += s.tile_rows) {
-                const int64_t rows = std::min(s.tile_rows, s.nloc - r0);
-                if (f32ref(c))
-                    HIPT(gen_spd_f32(c->n, c->lda, s.row0 + r0, rows, seed, reinterpret_cast<float *>(s.tile[0]),
-                                     reinterpret_cast<float *>(s.b) + r0, s.stream));
-                else
-                    HIPT(gen_spd_f64(c->n, c->lda, s.row0 + r0, rows, seed, reinterpret_cast<double *>(s.tile[0]),
-                                     reinterpret_cast<double *>(s.b) + r0, s.stream));
-                HIPT(hipMemcpyAsync(s.A_host + (size_t)r0 * row_bytes, s.tile[0], (size_t)rows * row_bytes,
-                                    hipMemcpyDeviceToHost, s.stream));
-            }
-            HIPT(hipStreamSynchronize(s.stream));
-        } else if (c->flags & CGX_SYMMETRIC) {
-            HIPT(gen_spd_sym_f64(c->n, c->lda, seed, reinterpret_cast<double *>(s.A), reinterpret_cast<double *>(s.b),
-                                 s.stream));
-        } else if (f32ref(c)) {
-            HIPT(gen_spd_f32(c->n, c->lda, s.row0, s.nloc, seed, reinterpret_cast<float *>(s.A),
-                             reinterpret_cast<float *>(s.b), s.stream));
-        } else {
-            HIPT(gen_spd_f64(c->n, c->lda, s.row0, s.nloc, seed, reinterpret_cast<double *>(s.A),
-                             reinterpret_cast<double *>(s.b), s.stream));
-        }
-        HIPT(hipMemsetAsync(s.x, 0, s.nloc * c->es, s.stream));
-        s.x_zero = true;
-    }
-    TRY(sync_all(c));
-    c->state = ST_IDLE;
-    return CGX_OK;
-}
-
-int cgx_set_x(cgx_ctx *c, const void *x) {
-    if (!c || !x) return fail(CGX_ERR_ARG, "NULL argument");
-    return cgx_set_rows(c, 0, c->n, nullptr, c->n, nullptr, x);
-}
-
-int cgx_get_x(cgx_ctx *c, void *x) {
-    const Range range_("cgx_get_x");
-    if (!c || !x) return fail(CGX_ERR_ARG, "NULL argument");
-    const size_t es = (size_t)c->es;
-    if (c->mode == M_RCCL && c->nranks > 1) {
-        Shard &s = c->sh[0];
-        TRY(set_dev(s));
-        NCCLT(ncclAllGather(s.x, s.xfull, (size_t)s.nloc, f32ref(c) ? ncclFloat : ncclDouble, s.comm, s.stream));
-        HIPT(hipMemcpyAsync(s.h_x ? s.h_x : x, s.xfull, (size_t)c->n * es, hipMemcpyDeviceToHost, s.stream));
-        HIPT(hipStreamSynchronize(s.stream));
-        if (s.h_x) std::memcpy(x, s.h_x, (size_t)c->n * es);
-        return CGX_OK;
-    }
-    for (auto &s : c->sh) {
-        TRY(set_dev(s));
-        HIPT(hipMemcpyAsync(s.h_x ? s.h_x : static_cast<char *>(x) + s.row0 * es, s.x, s.nloc * es,
-                            hipMemcpyDeviceToHost, s.stream));
-    }
-    TRY(sync_all(c));
-    for (auto &s : c->sh)
-        if (s.h_x) std::memcpy(static_cast<char *>(x) + s.row0 * es, s.h_x, s.nloc * es);
-    return CGX_OK;
-}
-
-int cgx_solve_begin(cgx_ctx *c) {
-    const Range range_("cgx_solve_begin");
-    if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
-    return do_begin(c);
-}
-
-// Fixed-count iterations from a hipGraph: one GPU (no exchange, no host
-// reads inside an iteration), no per-launch timing events.  kGraphIters
-// iterations are captured once per context, from an iteration k >= 1 that
-// is a multiple of kGraphIters: every launch argument then repeats with that
-// period (scalar ring slots, Poisson slab parity; k == 0 alone differs), so
-// the same graph replays at k, k + 4, ...  The kernels and their order are
-// the stream path's, so the results are bitwise the same (tested).  Opt-in
-// (CGX_GRAPH=1): replays measured 1-5 % SLOWER than stream launches at
-// N = 512-16384 and on Poisson grids (profiles/r01_graph_ab.jsonl; the
-// launches are already queued ahead of a GPU-bound loop).  A capture that
-// fails falls back to stream launches.
-static bool graph_ok(const cgx_ctx *c) {
-    const char *e = std::getenv("CGX_GRAPH");
-    if (!(e && *e == '1')) return false;
-    return c->mode == M_SINGLE && !c->graph_failed && !(c->flags & (CGX_TIMING | CGX_HOST_STREAM));
-}
-
-static int graph_block(cgx_ctx *c, bool *ran) {
-    *ran = false;
-    Shard &s = c->sh[0];
-    TRY(set_dev(s));
-    if (!c->graph) {
-        const int64_t k0 = c->k, t0 = c->total_iters;
-        HIPT(hipStreamBeginCapture(s.stream, hipStreamCaptureModeThreadLocal));
-        int rc = CGX_OK;
-        for (int i = 0; i < kGraphIters && rc == CGX_OK; ++i) {
-            int stop = 0;
-            rc = do_iteration(c, -1.0, &stop);
-        }
-        hipGraph_t g = nullptr;
-        const hipError_t ec = hipStreamEndCapture(s.stream, &g);
-        c->k = k0;
-        c->total_iters = t0;
-        if (rc == CGX_OK && ec == hipSuccess && g && hipGraphInstantiate(&c->graph, g, nullptr, nullptr, 0) == hipSuccess) {
-            (void)hipGraphDestroy(g);
-        } else {
-            if (g) (void)hipGraphDestroy(g);
-            (void)hipGetLastError();
-            c->graph = nullptr;
-            c->graph_failed = true;  // stream launches from now on
-            return CGX_OK;
-        }
-    }
-    HIPT(hipGraphLaunch(c->graph, s.stream));
-    c->k += kGraphIters;
-    c->total_iters += kGraphIters;
-    *ran = true;
-    return CGX_OK;
-}
-
-// Convergence-tested iterations without a host round trip per iteration:
-// the update kernel decides sqrt(r.r) < eps on the device and records k+1;
-// queued later iterations skip themselves.  The host keeps `look` iterations
-// in flight and reads the record of an older iteration (pinned memory,
-// event-ordered), so at most `look` no-op iterations are ever enqueued.
-static int iterate_gated(cgx_ctx *c, int64_t count, double eps, int64_t *done, int *converged) {
-    Shard &s0 = c->sh[0];
-    const char *la = std::getenv("CGX_LOOKAHEAD");
-    const int look = std::max(1, std::min(kLookRing - 1, (la && *la) ? std::atoi(la) : 2));
-    const int64_t k0 = c->k;
-    int64_t issued = 0, kd = 0;
-    volatile int64_t *rec = s0.h_rec;  // {kdone, r.r bits}, stored by the deciding kernel
-    for (; issued < count && kd == 0; ++issued) {
-        int stop = 0;
-        TRY(do_iteration(c, eps, &stop, /*gated=*/true));
-        TRY(set_dev(s0));
-        const int q = (int)(issued % kLookRing);
-        HIPT(hipEventRecord(s0.ev_look[q], s0.stream));
-        if (issued >= look) {
-            HIPT(hipEventSynchronize(s0.ev_look[(issued - look) % kLookRing]));
-            // Only a record left by an iteration the event covers counts: the
-            // host-mapped word may already show a later iteration's decision,
-            // and acting on that would make the number of enqueued iterations
-            // (and so of collectives) depend on timing, rank by rank.  The
-            // record's k is the deciding launch's iteration index (dense: the
-            // converged iteration + 1, Poisson: the next iteration), so
-            // k <= the synced iteration means that launch is covered.
-            const int64_t r = rec[0];
-            if (r != 0 && r <= k0 + (issued - look)) kd = r;
-        }
-    }
-    TRY(sync_all(c));
-    const int64_t kdev = rec[0];
-    const int64_t did = kdev ? (kdev - k0) : issued;
-    c->total_iters += did - issued;  // do_iteration counted every enqueued one
-    if (kdev) {
-        const int64_t bits = rec[1];
-        double rrf;
-        std::memcpy(&rrf, &bits, 8);
-        c->last_rr = rrf;
-        c->k = kdev;
-        c->converged = 1;
-        c->state = ST_CONVERGED;
-    } else {
-        double rr = 0.0;
-        TRY(read_scalar(c, S_RR + ring(c->k), &rr));
-        c->last_rr = rr;
-        // The fused Poisson iteration decides a stop one iteration later (at
-        // the start of the next k_poisson_p); the last issued iteration's
-        // r.r is tested here.  (The dense kernels already tested it.)
-        if (c->fused && eps >= 0.0 && std::sqrt(rr) < eps) {
-            c->converged = 1;
-            c->state = ST_CONVERGED;
-        }
-    }
-    if (done) *done = did;
-    if (converged) *converged = c->converged;
-    return CGX_OK;
-}
-
-int cgx_iterate(cgx_ctx *c, int64_t count, double eps, int64_t *done, int *converged) {
-    const Range range_("cgx_iterate");
-    if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
-    if (c->state == ST_IDLE) return fail(CGX_ERR_STATE, "cgx_iterate before cgx_solve_begin");
-    const char *gv = std::getenv("CGX_GATED");
-    const bool gate_ok = !(gv && *gv == '0');
-    if (c->state == ST_BEGUN && count > 0 && eps >= 0.0 && !f32ref(c) && !(c->flags & CGX_HOST_STREAM) && gate_ok)
-        return iterate_gated(c, count, eps, done, converged);
-    int64_t did = 0;
-    const bool use_graph = eps < 0.0 && graph_ok(c);
-    while (did < count && c->state == ST_BEGUN) {
-        if (use_graph && c->k >= kGraphIters && c->k % kGraphIters == 0 && count - did >= kGraphIters) {
-            bool ran = false;
-            TRY(graph_block(c, &ran));
-            if (ran) {
-                did += kGraphIters;
-                continue;
-            }
-        }
-        int stop = 0;
-        TRY(do_iteration(c, eps, &stop));
-        ++did;
-        if (stop) break;
-    }
-    if (done) *done = did;
-    if (converged) *converged = c->converged;
-    return CGX_OK;
-}
-
-int cgx_solve(cgx_ctx *c, void *x_inout, double eps, int64_t max_iter, cgx_stats *st) {
-    const Range range_("cgx_solve");
-    if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
-    if (x_inout) TRY(cgx_set_x(c, x_inout));
-    TRY(sync_all(c));
-    const auto t0 = std::chrono::steady_clock::now();
-    TRY(do_begin(c));
-    const int64_t cap = max_iter < 0 ? c->n : max_iter;  // for(k=0; k<ROWS; ++k)
-    int64_t done = 0;
-    int conv = 0;
-    TRY(cgx_iterate(c, cap, eps, &done, &conv));
-    TRY(sync_all(c));
-    const auto t1 = std::chrono::steady_clock::now();
-    c->solve_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
-    if (eps < 0.0 && c->k > 0) {
-        double rr = 0.0;
-        TRY(read_scalar(c, S_RR + ring(c->k), &rr));
-        c->last_rr = rr;
-    }
-    if (x_inout) TRY(cgx_get_x(c, x_inout));
-    if (st) TRY(cgx_get_stats(c, st));
-    return CGX_OK;
-}
-
-int cgx_get_stats(cgx_ctx *c, cgx_stats *st) {
-    if (!c || !st) return fail(CGX_ERR_ARG, "NULL argument");
-    TRY(sync_all(c));
-    st->iterations = c->k;
-    st->converged = c->converged;
-    st->rr = c->last_rr;
-    st->solve_ms = c->solve_ms;
-    st->matvec_ms = c->matvec_ms;
-    st->matvec_count = c->matvec_count;
-    st->total_iterations = c->total_iters;
-    return CGX_OK;
-}
-
-int cgx_reset_timing(cgx_ctx *c) {
-    if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
-    TRY(sync_all(c));
-    c->matvec_ms = 0.0;
-    c->matvec_count = 0;
-    return CGX_OK;
-}
-
-int cgx_synchronize(cgx_ctx *c) {
-    if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
-    return sync_all(c);
-}
-
-void *cgx_stream(cgx_ctx *c) { return c ? (void *)c->sh[0].stream : nullptr; }
-
-int cgx_set_matvec_plan(cgx_ctx *c, int rows_per_wave, int chunks_in_flight, int nontemporal, int blocks_per_cu) {
-    if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
-    if (f32ref(c) || c->op != OP_DENSE || (c->flags & CGX_SYMMETRIC))
-        return fail(CGX_ERR_ARG, "only the fp64 row-major dense matVec has a tunable plan");
-    const int R = rows_per_wave, U = chunks_in_flight;
-    if (R != 1 && R != 2 && R != 4 && R != 8) return fail(CGX_ERR_ARG, "rows_per_wave must be 1, 2, 4 or 8");
-    if (U != 2 && U != 4 && U != 8) return fail(CGX_ERR_ARG, "chunks_in_flight must be 2, 4 or 8");
-    if (nontemporal < 0 || nontemporal > 13 || (nontemporal >= 2 && U == 2))
-        return fail(CGX_ERR_ARG, "load policy must be 0..13 (2..13 need chunks_in_flight 4 or 8)");
-    for (auto &s : c->sh) {
-        TRY(set_dev(s));
-        MatvecPlan pl = plan_matvec_f64(s.dev, s.nloc, R, U, nontemporal, blocks_per_cu);
-        s.plan = pl;
-    }
-    if (c->graph) {  // the captured launches carry the old plan
-        HIPT(hipGraphExecDestroy(c->graph));
-        c->graph = nullptr;
-    }
-    return CGX_OK;
-}
-
-int cgx_get_matvec_plan(cgx_ctx *c, int *rows_per_wave, int *chunks_in_flight, int *nontemporal, int *blocks) {
-    if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
-    const MatvecPlan &pl = c->sh[0].plan;
-    if (rows_per_wave) *rows_per_wave = pl.R;
-    if (chunks_in_flight) *chunks_in_flight = pl.U;
-    if (nontemporal) *nontemporal = pl.nt;
-    if (blocks) *blocks = pl.blocks;
-    return CGX_OK;
-}
-
-int cgx_residual_norm(cgx_ctx *c, double *rnorm, double *bnorm) {
-    const Range range_("cgx_residual_norm");
-    if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
-    // ||b - A x|| with the current x: allgather x, matVec, residual, two dots.
-    TRY(settle_halo(c));
-    TRY(exchange_allgather(c, /*from_x=*/true));
-    const int tro = out_slot(c, S_LTR, S_TR), tbo = out_slot(c, S_LTB, S_TB);
-    for (auto &s : c->sh) {
-        TRY(set_dev(s));
-        TRY(launch_matvec(c, s, s.pfull, false, 0));
-        if (f32ref(c)) {
-            HIPT(residual_ref_f32(s.nloc, reinterpret_cast<const float *>(s.b), reinterpret_cast<const float *>(s.Ap),
-                                  reinterpret_cast<float *>(s.r), nullptr, s.stream));
-            HIPT(dot_ref_f32(s.nloc, reinterpret_cast<const float *>(s.r), reinterpret_cast<const float *>(s.r),
-                             reinterpret_cast<float *>(slot(s, tro)), s.stream));
-            HIPT(dot_ref_f32(s.nloc, reinterpret_cast<const float *>(s.b), reinterpret_cast<const float *>(s.b),
-                             reinterpret_cast<float *>(slot(s, tbo)), s.stream));
-        } else {
-            HIPT(residual_f64(s.nloc, reinterpret_cast<const double *>(s.b), reinterpret_cast<const double *>(s.Ap),
-                              reinterpret_cast<double *>(s.r), nullptr, reinterpret_cast<double *>(slot(s, tro)), s.ws,
-                              s.stream));
-            HIPT(dot_f64(s.nloc, reinterpret_cast<const double *>(s.b), reinterpret_cast<const double *>(s.b),
-                         reinterpret_cast<double *>(slot(s, tbo)), s.ws, s.stream));
-        }
-    }
-    TRY(exchange_scalar(c, S_LTR, S_TR));
-    TRY(exchange_scalar(c, S_LTB, S_TB));
-    double rr = 0.0, bb = 0.0;
-    TRY(read_scalar(c, S_TR, &rr));
-    TRY(read_scalar(c, S_TB, &bb));
-    if (rnorm) *rnorm = std::sqrt(rr);
-    if (bnorm) *bnorm = std::sqrt(bb);
-    c->state = ST_IDLE;  // r and p were overwritten
     return CGX_OK;
 }
 

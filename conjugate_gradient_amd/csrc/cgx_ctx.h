@@ -1,0 +1,223 @@
+// cgx_ctx.h -- internal to libcgx: the context and shard types, the error
+// plumbing, and the functions the host-side files share:
+//   cgx_setup.hip     contexts and shards: create, destroy, data in and out
+//   cgx_exchange.hip  the per-iteration exchanges (RCCL / device copies / p2p)
+//   cgx_iterate.hip   the conjugrad loop: begin, iterations, gating, solve
+//   cgx_api.hip       errors, devices and the kernel-level entry points
+// Not part of the C ABI (include/cgx.h).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+#include <rocprofiler-sdk-roctx/roctx.h>
+
+#include <chrono>
+#include <cmath>
+#include <cstdarg>
+#include <cstdio>
+#include <cstdlib>
+#include <cstring>
+#include <initializer_list>
+#include <mutex>
+#include <new>
+#include <string>
+#include <vector>
+#include <algorithm>
+
+#include "cgx.h"
+#include "cgx_kernels.h"
+
+using namespace cgx;
+
+namespace cgxh {
+extern thread_local char g_err[1024];
+int fail(int code, const char *fmt, ...);
+}  // namespace cgxh
+
+#define HIPT(expr)                                                                              \
+    do {                                                                                        \
+        hipError_t e_ = (expr);                                                                 \
+        if (e_ != hipSuccess)                                                                   \
+            return fail(CGX_ERR_HIP, "%s: %s (%s:%d)", #expr, hipGetErrorString(e_), __FILE__, \
+                        __LINE__);                                                              \
+    } while (0)
+
+#define NCCLT(expr)                                                                               \
+    do {                                                                                          \
+        ncclResult_t e_ = (expr);                                                                 \
+        if (e_ != ncclSuccess)                                                                    \
+            return fail(CGX_ERR_RCCL, "%s: %s (%s:%d)", #expr, ncclGetErrorString(e_), __FILE__, \
+                        __LINE__);                                                                \
+    } while (0)
+
+#define TRY(expr)                          \
+    do {                                   \
+        int rc_ = (expr);                  \
+        if (rc_ != CGX_OK) return rc_;     \
+    } while (0)
+
+namespace cgxh {
+
+constexpr int kScalSlots = 136;  // 16 ring slots, up to 112 gathered partials, 4 aux
+constexpr int kMaxShards = 32;
+constexpr int S_RR = 0, S_PAP = 4, S_LRR = 8, S_LPAP = 12, S_GATHER = 16;
+constexpr int S_TR = 128, S_TB = 129, S_LTR = 130, S_LTB = 131;  // true-residual check
+constexpr int S_XNZ = 134;  // rank mode: count of ranks whose x0 is not all zeros
+constexpr int S_KDONE = 132, S_RRFINAL = 133;  // device-side convergence: k+1 at the break, r.r there
+constexpr int kLookRing = 8;                    // pinned slots for the host's lagged convergence checks
+inline int ring(int64_t j) { return (int)(j & 3); }
+constexpr int kGraphIters = 4;  // a multiple of the ring period (and of the Poisson slab alternation)
+
+enum Mode { M_SINGLE = 0, M_LOCAL = 1, M_RCCL = 2 };
+enum Op { OP_DENSE = 0, OP_POISSON = 1 };
+enum State { ST_IDLE = 0, ST_BEGUN = 1, ST_CONVERGED = 2 };
+
+constexpr int kEvPairs = 256;
+constexpr size_t kXStageMax = 64u << 20;
+constexpr int kStreamBufs = 3;
+constexpr int kMaxCopyStreams = 4;
+
+struct Shard {
+    int dev = 0;
+    int index = 0;  // global row-block index
+    int64_t row0 = 0, nloc = 0;
+    hipStream_t stream = nullptr;
+    ncclComm_t comm = nullptr;
+    char *A = nullptr, *b = nullptr, *x = nullptr, *r = nullptr, *Ap = nullptr, *pfull = nullptr,
+         *xfull = nullptr, *scal = nullptr;
+    char *pown = nullptr;  // this shard's p: pfull + row0 (dense) or the slab interior (Poisson)
+    // fused Poisson iteration: r with halo rows (r = rh + one row) and a
+    // second p slab; p_k lives in pfull for even k, in p2 for odd k
+    char *rh = nullptr, *p2 = nullptr;
+    bool x_zero = true;  // x is known to be all zeros (x0 = 0: the first A x is skipped)
+    RedWs ws{nullptr, nullptr};
+    double *h_pin = nullptr;
+    // pinned staging for cgx_get_x (x of this shard, or all of x in rank
+    // mode), allocated with the context so the first D2H of a solve's result
+    // does not set up HIP's pageable-copy path (~7 ms); null above kXStageMax
+    char *h_x = nullptr;
+    // convergence record {kdone, bits of r.r there} in host-mapped coherent
+    // memory: the deciding kernel stores it, the host reads it after an event
+    int64_t *h_rec = nullptr, *d_rec = nullptr;
+    MatvecPlan plan;
+    // CGX_SYMMETRIC: A = the upper-triangle tiles; per-tile row / column
+    // partials of a matVec; a staging buffer for rows copied from the host
+    char *sym_prow = nullptr, *sym_pcol = nullptr, *sym_stage = nullptr;
+    int64_t sym_stage_rows = 0;
+    int sym_grid = 0;
+    hipEvent_t ev_sync = nullptr;  // cross-shard ordering (LOCAL mode)
+    std::vector<hipEvent_t> ev_t;  // timing pairs (CGX_TIMING)
+    int ev_used = 0;
+    // CGX_HOST_STREAM: A stays in pinned host memory; row tiles are copied
+    // into kStreamBufs device buffers on `ncopy` copy streams while the
+    // compute stream multiplies the previous tiles.
+    char *A_host = nullptr;
+    int64_t tile_rows = 0;
+    char *tile[kStreamBufs] = {};
+    int ncopy = 0;
+    hipStream_t copy[kMaxCopyStreams] = {};
+    hipEvent_t ev_loaded[kStreamBufs][kMaxCopyStreams] = {};
+    hipEvent_t ev_free[kStreamBufs] = {};
+    bool buf_used[kStreamBufs] = {};
+    int next_buf = 0;
+    MatvecPlan tile_plan;
+    hipEvent_t ev_look[8] = {};  // lagged convergence checks (kLookRing)
+    // overlap of the p exchange with the own-column-block matVec
+    hipStream_t cstream = nullptr;
+    hipEvent_t ev_pready = nullptr, ev_gathered = nullptr;
+};
+
+}  // namespace cgxh
+
+using namespace cgxh;
+
+struct cgx_ctx {
+    int64_t n = 0, lda = 0;
+    int op = 0;        // OP_DENSE or OP_POISSON
+    int64_t m = 0;     // Poisson grid width (n = m*m)
+    int nranks = 1;
+    int flags = 0;
+    int es = 8;
+    Mode mode = M_SINGLE;
+    std::vector<Shard> sh;
+    State state = ST_IDLE;
+    int64_t k = 0;  // iterations of the current solve
+    double last_rr = 0.0;
+    int converged = 0;
+    double solve_ms = 0.0, matvec_ms = 0.0;
+    int64_t matvec_count = 0, total_iters = 0;
+    bool overlap = false;  // own-column-block matVec while p is exchanged
+    bool fused = false;    // Poisson: two-kernel fused iteration (k_poisson_p + k_poisson_xr)
+    bool halo_overlap = false;  // fused Poisson, several slabs: r's halo exchange overlaps k_poisson_p
+    bool halo_pending = false;  // an overlapped r halo exchange is in flight on the comm streams
+    // fixed-count iterations replayed from a hipGraph (one GPU): kGraphIters
+    // iterations captured once, the period of the scalar rings
+    hipGraphExec_t graph = nullptr;
+    bool graph_failed = false;
+};
+
+namespace cgxh {
+
+inline bool f32ref(const cgx_ctx *c) { return (c->flags & CGX_F32_REF) != 0; }
+inline void *slot(const Shard &s, int i) { return s.scal + 8 * i; }
+inline bool p2p(const cgx_ctx *c) { return (c->flags & CGX_COMM_P2P) != 0; }
+// Where a kernel writes its (partial) scalar: the global slot directly when
+// there is nothing to combine, else the shard-local slot.
+inline int out_slot(const cgx_ctx *c, int lslot, int gslot) { return c->mode == M_SINGLE ? gslot : lslot; }
+inline int64_t *rec_of(const cgx_ctx *c, const Shard &s, bool gated) {
+    return (gated && &s == &c->sh[0]) ? s.d_rec : nullptr;
+}
+
+inline const int64_t *gate_of(const Shard &s, bool gated) {
+    return gated ? reinterpret_cast<const int64_t *>(slot(s, S_KDONE)) : nullptr;
+}
+
+// roctx range over an API call (rocprofv3 --marker-trace shows the solve
+// phases on the timeline; a no-op without a tool attached).
+struct Range {
+    explicit Range(const char *name) { roctxRangePushA(name); }
+    ~Range() { roctxRangePop(); }
+    Range(const Range &) = delete;
+    Range &operator=(const Range &) = delete;
+};
+
+inline int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
+
+// cgx_setup.hip
+int set_dev(const Shard &s);
+int alloc_shard(cgx_ctx *c, Shard &s);
+void free_shard(Shard &s);
+int check_n(int64_t n, int nranks);
+cgx_ctx *new_ctx(int64_t n, int nranks, int flags);
+bool can_overlap(const cgx_ctx *c);
+int alloc_overlap(cgx_ctx *c);
+int finish_create(cgx_ctx *c, cgx_ctx **out);
+// cgx_exchange.hip
+int timing_resolve(cgx_ctx *c);
+int local_barrier(cgx_ctx *c);
+int exchange_halo(cgx_ctx *c, bool from_x);
+int exchange_halo_of(cgx_ctx *c, char *Shard::*slab);
+int p2p_allgather(cgx_ctx *c, bool from_x);
+int p2p_scalar(cgx_ctx *c, int lslot, int gslot);
+int exchange_allgather(cgx_ctx *c, bool from_x);
+int exchange_scalar(cgx_ctx *c, int lslot, int gslot);
+int overlapped_matvec(cgx_ctx *c, int dot_slot, bool gated);
+int exchange_halo_async(cgx_ctx *c);
+int settle_halo(cgx_ctx *c);
+int sync_all(cgx_ctx *c);
+// cgx_iterate.hip
+int matvec_rows(cgx_ctx *c, Shard &s, const MatvecPlan &pl, const char *Arows, int64_t r0, int64_t rows,
+                const char *vec, bool fuse_dot, int dot_slot, bool gated = false);
+int matvec_streamed(cgx_ctx *c, Shard &s, const char *vec);
+int matvec_sym_streamed(cgx_ctx *c, Shard &s, const char *vec, bool with_dot, int dot_slot, const int64_t *gate);
+int launch_matvec(cgx_ctx *c, Shard &s, const char *vec, bool with_dot, int dot_slot, bool gated = false);
+int x0_is_zero(cgx_ctx *c, bool *zero);
+int do_begin(cgx_ctx *c);
+int read_scalar(cgx_ctx *c, int gslot, double *out);
+int do_iteration_poisson(cgx_ctx *c, double eps, int *stop, bool gated);
+int do_iteration(cgx_ctx *c, double eps, int *stop, bool gated = false);
+// cgx_api.hip
+int dev_ws(RedWs *out);
+int check_dtype(int dtype);
+
+}  // namespace cgxh

@@ -1,0 +1,394 @@
+// cgx_exchange.hip -- the per-iteration exchanges (cgx_ctx.h):
+//   MPI_Allgather(local_p -> p)   parallel_cg.c:290-291 -> exchange_allgather
+//   MPI_Allreduce(p.Ap), (r.r)    parallel_cg.c:287,294,313 -> exchange_scalar
+//   point-to-point_cg.c:239-256,339-394 (CGX_COMM_P2P) -> p2p_allgather / p2p_scalar
+// in RCCL rank mode, by device copies in multi-shard mode; the overlap of
+// p's exchange with the own-column-block matVec; the Poisson halo rows.
+#include "cgx_ctx.h"
+
+namespace cgxh {
+
+// ---- timing -------------------------------------------------------------------
+int timing_resolve(cgx_ctx *c) {
+    if (!(c->flags & CGX_TIMING)) return CGX_OK;
+    Shard &s = c->sh[0];
+    TRY(set_dev(s));
+    for (int i = 0; i < s.ev_used; ++i) {
+        float ms = 0.f;
+        HIPT(hipEventSynchronize(s.ev_t[2 * i + 1]));
+        HIPT(hipEventElapsedTime(&ms, s.ev_t[2 * i], s.ev_t[2 * i + 1]));
+        c->matvec_ms += ms;
+        c->matvec_count += 1;
+    }
+    s.ev_used = 0;
+    return CGX_OK;
+}
+
+// ---- exchange ---------------------------------------------------------------------
+// Make every shard's stream wait for the work already queued on all shards.
+int local_barrier(cgx_ctx *c) {
+    for (auto &s : c->sh) {
+        TRY(set_dev(s));
+        HIPT(hipEventRecord(s.ev_sync, s.stream));
+    }
+    for (auto &d : c->sh) {
+        TRY(set_dev(d));
+        for (auto &s : c->sh)
+            if (&s != &d) HIPT(hipStreamWaitEvent(d.stream, s.ev_sync, 0));
+    }
+    return CGX_OK;
+}
+
+// Poisson: refresh the two halo rows of every slab from its neighbours
+// (ncclSend/Recv of one grid row each way in rank mode, device copies in
+// LOCAL mode); from_x first copies x into the slab interior (for A x0).
+int exchange_halo_of(cgx_ctx *c, char *Shard::*slab);
+int exchange_halo(cgx_ctx *c, bool from_x) {
+    const size_t es = (size_t)c->es;
+    if (from_x)
+        for (auto &s : c->sh) {
+            TRY(set_dev(s));
+            HIPT(hipMemcpyAsync(s.pown, s.x, s.nloc * es, hipMemcpyDeviceToDevice, s.stream));
+        }
+    return exchange_halo_of(c, &Shard::pfull);
+}
+
+// The halo rows of the slab buffer `slab` (row 0 and row mloc+1 around the
+// mloc interior rows) from the neighbouring slabs' boundary rows.
+int exchange_halo_of(cgx_ctx *c, char *Shard::*slab) {
+    const size_t row = (size_t)c->m * (size_t)c->es;
+    if (c->mode == M_SINGLE) return CGX_OK;
+    const int64_t mloc = c->sh[0].nloc / c->m;
+    if (c->mode == M_RCCL) {
+        Shard &s = c->sh[0];
+        if (c->nranks == 1) return CGX_OK;
+        TRY(set_dev(s));
+        const int g = s.index;
+        char *base = s.*slab, *own = base + row;
+        NCCLT(ncclGroupStart());
+        if (g > 0) {
+            NCCLT(ncclSend(own, (size_t)c->m, ncclDouble, g - 1, s.comm, s.stream));
+            NCCLT(ncclRecv(base, (size_t)c->m, ncclDouble, g - 1, s.comm, s.stream));
+        }
+        if (g < c->nranks - 1) {
+            NCCLT(ncclSend(own + (size_t)(mloc - 1) * row, (size_t)c->m, ncclDouble, g + 1, s.comm, s.stream));
+            NCCLT(ncclRecv(own + (size_t)mloc * row, (size_t)c->m, ncclDouble, g + 1, s.comm, s.stream));
+        }
+        NCCLT(ncclGroupEnd());
+        return CGX_OK;
+    }
+    TRY(local_barrier(c));
+    const int S = (int)c->sh.size();
+    for (int q = 0; q < S; ++q) {
+        Shard &d = c->sh[q];
+        TRY(set_dev(d));
+        if (q > 0) {
+            const Shard &u = c->sh[q - 1];
+            HIPT(hipMemcpyPeerAsync(d.*slab, d.dev, u.*slab + (size_t)mloc * row, u.dev, row, d.stream));
+        }
+        if (q < S - 1) {
+            const Shard &w = c->sh[q + 1];
+            HIPT(hipMemcpyPeerAsync(d.*slab + (size_t)(mloc + 1) * row, d.dev, w.*slab + row, w.dev, row, d.stream));
+        }
+    }
+    return CGX_OK;
+}
+
+// CGX_COMM_P2P: point-to-point_cg.c's exchange pattern, gather to rank 0 then
+// send from rank 0 to every rank (allGather :364-394 + BcastVector :239-256),
+// O(P) messages through rank 0.  ncclSend/Recv in rank mode, device copies
+// through shard 0 in LOCAL mode.
+int p2p_allgather(cgx_ctx *c, bool from_x) {
+    const size_t es = (size_t)c->es;
+    if (c->mode == M_RCCL) {
+        Shard &s = c->sh[0];
+        TRY(set_dev(s));
+        const ncclDataType_t t = f32ref(c) ? ncclFloat : ncclDouble;
+        const int P = c->nranks;
+        if (s.index == 0 && from_x)
+            HIPT(hipMemcpyAsync(s.pown, s.x, s.nloc * es, hipMemcpyDeviceToDevice, s.stream));
+        NCCLT(ncclGroupStart());
+        if (s.index != 0) {
+            NCCLT(ncclSend(from_x ? (const void *)s.x : (const void *)s.pown, (size_t)s.nloc, t, 0, s.comm, s.stream));
+        } else {
+            for (int q = 1; q < P; ++q)
+                NCCLT(ncclRecv(s.pfull + (size_t)q * s.nloc * es, (size_t)s.nloc, t, q, s.comm, s.stream));
+        }
+        NCCLT(ncclGroupEnd());
+        NCCLT(ncclGroupStart());
+        if (s.index == 0) {
+            for (int q = 1; q < P; ++q) NCCLT(ncclSend(s.pfull, (size_t)c->n, t, q, s.comm, s.stream));
+        } else {
+            NCCLT(ncclRecv(s.pfull, (size_t)c->n, t, 0, s.comm, s.stream));
+        }
+        NCCLT(ncclGroupEnd());
+        return CGX_OK;
+    }
+    TRY(local_barrier(c));
+    Shard &r0 = c->sh[0];
+    TRY(set_dev(r0));
+    for (auto &s : c->sh) {
+        if (&s == &r0 && !from_x) continue;
+        HIPT(hipMemcpyPeerAsync(r0.pfull + s.row0 * es, r0.dev, from_x ? s.x : s.pown, s.dev, s.nloc * es, r0.stream));
+    }
+    HIPT(hipEventRecord(r0.ev_sync, r0.stream));
+    for (auto &d : c->sh) {
+        if (&d == &r0) continue;
+        TRY(set_dev(d));
+        HIPT(hipStreamWaitEvent(d.stream, r0.ev_sync, 0));
+        HIPT(hipMemcpyPeerAsync(d.pfull, d.dev, r0.pfull, r0.dev, (size_t)c->n * es, d.stream));
+    }
+    return CGX_OK;
+}
+
+// allSum (point-to-point_cg.c:339-359): partials to rank 0, summed there in
+// rank order, the sum sent back to every rank (BcastVector(&s, 1)).
+int p2p_scalar(cgx_ctx *c, int lslot, int gslot) {
+    if (c->mode == M_RCCL) {
+        Shard &s = c->sh[0];
+        TRY(set_dev(s));
+        const int P = c->nranks;
+        if (s.index == 0) HIPT(hipMemcpyAsync(slot(s, S_GATHER), slot(s, lslot), 8, hipMemcpyDeviceToDevice, s.stream));
+        NCCLT(ncclGroupStart());
+        if (s.index != 0) {
+            NCCLT(ncclSend(slot(s, lslot), 1, ncclUint64, 0, s.comm, s.stream));
+        } else {
+            for (int q = 1; q < P; ++q) NCCLT(ncclRecv(slot(s, S_GATHER + q), 1, ncclUint64, q, s.comm, s.stream));
+        }
+        NCCLT(ncclGroupEnd());
+        if (s.index == 0) {
+            if (f32ref(c))
+                HIPT(sum_ordered_f32(reinterpret_cast<const float *>(slot(s, S_GATHER)), P,
+                                     reinterpret_cast<float *>(slot(s, gslot)), s.stream));
+            else
+                HIPT(sum_ordered_f64(reinterpret_cast<const double *>(slot(s, S_GATHER)), P,
+                                     reinterpret_cast<double *>(slot(s, gslot)), s.stream));
+        }
+        NCCLT(ncclGroupStart());
+        if (s.index == 0) {
+            for (int q = 1; q < P; ++q) NCCLT(ncclSend(slot(s, gslot), 1, ncclUint64, q, s.comm, s.stream));
+        } else {
+            NCCLT(ncclRecv(slot(s, gslot), 1, ncclUint64, 0, s.comm, s.stream));
+        }
+        NCCLT(ncclGroupEnd());
+        return CGX_OK;
+    }
+    TRY(local_barrier(c));
+    Shard &r0 = c->sh[0];
+    const int S = (int)c->sh.size();
+    TRY(set_dev(r0));
+    for (auto &s : c->sh)
+        HIPT(hipMemcpyPeerAsync(slot(r0, S_GATHER + s.index), r0.dev, slot(s, lslot), s.dev, 8, r0.stream));
+    if (f32ref(c))
+        HIPT(sum_ordered_f32(reinterpret_cast<const float *>(slot(r0, S_GATHER)), S,
+                             reinterpret_cast<float *>(slot(r0, gslot)), r0.stream));
+    else
+        HIPT(sum_ordered_f64(reinterpret_cast<const double *>(slot(r0, S_GATHER)), S,
+                             reinterpret_cast<double *>(slot(r0, gslot)), r0.stream));
+    HIPT(hipEventRecord(r0.ev_sync, r0.stream));
+    for (auto &d : c->sh) {
+        if (&d == &r0) continue;
+        TRY(set_dev(d));
+        HIPT(hipStreamWaitEvent(d.stream, r0.ev_sync, 0));
+        HIPT(hipMemcpyPeerAsync(slot(d, gslot), d.dev, slot(r0, gslot), r0.dev, 8, d.stream));
+    }
+    return CGX_OK;
+}
+
+// Every shard's pfull gets every shard's slice of `src(shard)` (its own slice
+// of a full-length buffer when in_place, else a separate local buffer).
+int exchange_allgather(cgx_ctx *c, bool from_x) {
+    if (c->op == OP_POISSON) return exchange_halo(c, from_x);
+    if (p2p(c) && c->mode != M_SINGLE) return p2p_allgather(c, from_x);
+    const size_t es = (size_t)c->es;
+    if (c->mode == M_SINGLE) {
+        if (from_x) {
+            Shard &s = c->sh[0];
+            TRY(set_dev(s));
+            HIPT(hipMemcpyAsync(s.pown, s.x, s.nloc * es, hipMemcpyDeviceToDevice, s.stream));
+        }
+        return CGX_OK;
+    }
+    if (c->mode == M_RCCL) {
+        Shard &s = c->sh[0];
+        TRY(set_dev(s));
+        const ncclDataType_t t = f32ref(c) ? ncclFloat : ncclDouble;
+        const void *send = from_x ? (const void *)s.x : (const void *)s.pown;
+        NCCLT(ncclAllGather(send, s.pfull, (size_t)s.nloc, t, s.comm, s.stream));
+        return CGX_OK;
+    }
+    // LOCAL: device-to-device copies after all producers are done.
+    TRY(local_barrier(c));
+    for (auto &d : c->sh) {
+        TRY(set_dev(d));
+        for (auto &s : c->sh) {
+            char *dst = d.pfull + s.row0 * es;
+            const char *src = from_x ? s.x : s.pown;
+            if (&s == &d && !from_x) continue;
+            HIPT(hipMemcpyPeerAsync(dst, d.dev, src, s.dev, s.nloc * es, d.stream));
+        }
+    }
+    return CGX_OK;
+}
+
+// Combine the per-shard partials in slot `lslot` into the global slot `gslot`.
+int exchange_scalar(cgx_ctx *c, int lslot, int gslot) {
+    if (c->mode == M_SINGLE) return CGX_OK;  // kernels wrote the global slot directly
+    if (p2p(c)) return p2p_scalar(c, lslot, gslot);
+    const int S = (int)c->sh.size();
+    if (c->mode == M_RCCL) {
+        Shard &s = c->sh[0];
+        TRY(set_dev(s));
+        if (f32ref(c)) {
+            // point-to-point_cg.c allSum order: gather the partials, sum in rank order
+            NCCLT(ncclAllGather(slot(s, lslot), slot(s, S_GATHER), 1, ncclUint64, s.comm, s.stream));
+            HIPT(sum_ordered_f32(reinterpret_cast<const float *>(slot(s, S_GATHER)), c->nranks,
+                                 reinterpret_cast<float *>(slot(s, gslot)), s.stream));
+        } else if (c->flags & CGX_DETERMINISTIC) {
+            // fp64, rank-order sum: the same bits as the multi-shard mode with the
+            // same partition, whatever algorithm RCCL would pick for an allreduce
+            NCCLT(ncclAllGather(slot(s, lslot), slot(s, S_GATHER), 1, ncclUint64, s.comm, s.stream));
+            HIPT(sum_ordered_f64(reinterpret_cast<const double *>(slot(s, S_GATHER)), c->nranks,
+                                 reinterpret_cast<double *>(slot(s, gslot)), s.stream));
+        } else {
+            NCCLT(ncclAllReduce(slot(s, lslot), slot(s, gslot), 1, ncclDouble, ncclSum, s.comm, s.stream));
+        }
+        return CGX_OK;
+    }
+    TRY(local_barrier(c));
+    for (auto &d : c->sh) {
+        TRY(set_dev(d));
+        for (auto &s : c->sh)
+            HIPT(hipMemcpyPeerAsync(slot(d, S_GATHER + s.index), d.dev, slot(s, lslot), s.dev, 8, d.stream));
+        if (f32ref(c))
+            HIPT(sum_ordered_f32(reinterpret_cast<const float *>(slot(d, S_GATHER)), S,
+                                 reinterpret_cast<float *>(slot(d, gslot)), d.stream));
+        else
+            HIPT(sum_ordered_f64(reinterpret_cast<const double *>(slot(d, S_GATHER)), S,
+                                 reinterpret_cast<double *>(slot(d, gslot)), d.stream));
+    }
+    return CGX_OK;
+}
+
+// Where a kernel writes its (partial) scalar: the global slot directly when
+// there is nothing to combine, else the shard-local slot.
+
+// Overlapped exchange + matVec: p is allgathered on each shard's comm
+// stream while the compute stream multiplies the shard's own column block
+// (its own p is already local); the rest of the columns follow once the
+// gather has landed, accumulating into Ap with the fused p.Ap partial.
+int overlapped_matvec(cgx_ctx *c, int dot_slot, bool gated) {
+    const size_t es = (size_t)c->es;
+    for (auto &s : c->sh) {
+        TRY(set_dev(s));
+        HIPT(hipEventRecord(s.ev_pready, s.stream));
+    }
+    if (c->mode == M_RCCL) {
+        Shard &s = c->sh[0];
+        HIPT(hipStreamWaitEvent(s.cstream, s.ev_pready, 0));
+        NCCLT(ncclAllGather(s.pown, s.pfull, (size_t)s.nloc, ncclDouble, s.comm, s.cstream));
+        HIPT(hipEventRecord(s.ev_gathered, s.cstream));
+    } else {
+        for (auto &d : c->sh) {
+            TRY(set_dev(d));
+            for (auto &s : c->sh) HIPT(hipStreamWaitEvent(d.cstream, s.ev_pready, 0));
+            for (auto &s : c->sh)
+                if (&s != &d)
+                    HIPT(hipMemcpyPeerAsync(d.pfull + s.row0 * es, d.dev, s.pown, s.dev, s.nloc * es, d.cstream));
+            HIPT(hipEventRecord(d.ev_gathered, d.cstream));
+        }
+    }
+    for (auto &s : c->sh) {
+        TRY(set_dev(s));
+        const bool timing = (c->flags & CGX_TIMING) && (&s == &c->sh[0]);
+        if (timing && s.ev_used >= kEvPairs) TRY(timing_resolve(c));
+        if (timing) HIPT(hipEventRecord(s.ev_t[2 * s.ev_used], s.stream));
+        const double *A = reinterpret_cast<const double *>(s.A);
+        const double *v = reinterpret_cast<const double *>(s.pfull);
+        double *Ap = reinterpret_cast<double *>(s.Ap);
+        HIPT(matvec_f64_cols(s.plan, A, c->lda, s.nloc, c->lda, s.row0, s.nloc, false, v, Ap, nullptr, nullptr,
+                             s.ws, s.stream, gate_of(s, gated)));
+        HIPT(hipStreamWaitEvent(s.stream, s.ev_gathered, 0));
+        HIPT(matvec_f64_cols(s.plan, A, c->lda, s.nloc, c->lda, (s.row0 + s.nloc) % c->lda, c->lda - s.nloc, true,
+                             v, Ap, reinterpret_cast<const double *>(s.pown),
+                             reinterpret_cast<double *>(slot(s, dot_slot)), s.ws, s.stream, gate_of(s, gated)));
+        if (timing) {
+            HIPT(hipEventRecord(s.ev_t[2 * s.ev_used + 1], s.stream));
+            s.ev_used++;
+        }
+    }
+    return CGX_OK;
+}
+
+// Overlapped r halo exchange (several slabs): on the comm streams, after
+// everything already on the compute streams (the r update and the r.r
+// allreduce, so two RCCL operations never run at once).  The next
+// k_poisson_p runs its interior runs meanwhile and waits for ev_gathered
+// before its two edge runs.
+int exchange_halo_async(cgx_ctx *c) {
+    const size_t row = (size_t)c->m * (size_t)c->es;
+    const int64_t mloc = c->sh[0].nloc / c->m;
+    for (auto &s : c->sh) {
+        TRY(set_dev(s));
+        HIPT(hipEventRecord(s.ev_pready, s.stream));
+    }
+    if (c->mode == M_RCCL) {
+        Shard &s = c->sh[0];
+        const int g = s.index;
+        char *base = s.rh, *own = base + row;
+        HIPT(hipStreamWaitEvent(s.cstream, s.ev_pready, 0));
+        NCCLT(ncclGroupStart());
+        if (g > 0) {
+            NCCLT(ncclSend(own, (size_t)c->m, ncclDouble, g - 1, s.comm, s.cstream));
+            NCCLT(ncclRecv(base, (size_t)c->m, ncclDouble, g - 1, s.comm, s.cstream));
+        }
+        if (g < c->nranks - 1) {
+            NCCLT(ncclSend(own + (size_t)(mloc - 1) * row, (size_t)c->m, ncclDouble, g + 1, s.comm, s.cstream));
+            NCCLT(ncclRecv(own + (size_t)mloc * row, (size_t)c->m, ncclDouble, g + 1, s.comm, s.cstream));
+        }
+        NCCLT(ncclGroupEnd());
+        HIPT(hipEventRecord(s.ev_gathered, s.cstream));
+    } else {
+        const int S = (int)c->sh.size();
+        for (int q = 0; q < S; ++q) {
+            Shard &d = c->sh[q];
+            TRY(set_dev(d));
+            for (auto &s : c->sh) HIPT(hipStreamWaitEvent(d.cstream, s.ev_pready, 0));
+            if (q > 0) {
+                const Shard &u = c->sh[q - 1];
+                HIPT(hipMemcpyPeerAsync(d.rh, d.dev, u.rh + (size_t)mloc * row, u.dev, row, d.cstream));
+            }
+            if (q < S - 1) {
+                const Shard &w = c->sh[q + 1];
+                HIPT(hipMemcpyPeerAsync(d.rh + (size_t)(mloc + 1) * row, d.dev, w.rh + row, w.dev, row, d.cstream));
+            }
+            HIPT(hipEventRecord(d.ev_gathered, d.cstream));
+        }
+    }
+    c->halo_pending = true;
+    return CGX_OK;
+}
+
+// Order every compute stream after an overlapped halo exchange still in
+// flight (before anything else touches r or its halo rows).
+int settle_halo(cgx_ctx *c) {
+    if (!c->halo_pending) return CGX_OK;
+    for (auto &s : c->sh) {
+        TRY(set_dev(s));
+        HIPT(hipStreamWaitEvent(s.stream, s.ev_gathered, 0));
+    }
+    c->halo_pending = false;
+    return CGX_OK;
+}
+
+int sync_all(cgx_ctx *c) {
+    for (auto &s : c->sh) {
+        TRY(set_dev(s));
+        HIPT(hipStreamSynchronize(s.stream));
+        for (int q = 0; q < s.ncopy; ++q) HIPT(hipStreamSynchronize(s.copy[q]));
+        if (s.cstream) HIPT(hipStreamSynchronize(s.cstream));
+    }
+    return timing_resolve(c);
+}
+
+}  // namespace cgxh

@@ -1,0 +1,628 @@
+// cgx_iterate.hip -- the conjugrad loop (cgx_ctx.h):
+//   conjugrad()  serialConjugate.c:180-259 / parallel_cg.c:248-345
+//     -> cgx_solve = cgx_solve_begin (:209-212) + cgx_iterate (:213-245)
+// the matVec dispatch (resident, host-streamed, symmetric, Poisson), the
+// iteration with its stopping test on the host or on the device (gating),
+// hipGraph replay, and the true-residual check.
+#include "cgx_ctx.h"
+
+namespace cgxh {
+
+// ---- the iteration pieces ----------------------------------------------------------
+// One tile of the matVec: rows [r0, r0+rows) of this shard, A rows at `Arows`.
+int matvec_rows(cgx_ctx *c, Shard &s, const MatvecPlan &pl, const char *Arows, int64_t r0, int64_t rows,
+                const char *vec, bool fuse_dot, int dot_slot, bool gated) {
+    if (f32ref(c)) {
+        HIPT(matvec_ref_f32(reinterpret_cast<const float *>(Arows), c->lda, rows, c->n,
+                            reinterpret_cast<const float *>(vec), reinterpret_cast<float *>(s.Ap) + r0, s.stream));
+    } else {
+        HIPT(matvec_f64(pl, reinterpret_cast<const double *>(Arows), c->lda, rows, c->lda,
+                        reinterpret_cast<const double *>(vec), reinterpret_cast<double *>(s.Ap) + r0,
+                        fuse_dot ? reinterpret_cast<const double *>(s.pown) + r0 : nullptr,
+                        fuse_dot ? reinterpret_cast<double *>(slot(s, dot_slot)) : nullptr, s.ws, s.stream,
+                        gated ? reinterpret_cast<const int64_t *>(slot(s, S_KDONE)) : nullptr));
+    }
+    return CGX_OK;
+}
+
+// CGX_HOST_STREAM matVec: tile t goes to buffer (next_buf++ % kStreamBufs);
+// its copy waits until the kernel that last read that buffer is done (A is
+// read-only, so copies of the next iteration's first tiles overlap this
+// iteration's vector work); its kernel waits for the copy.
+int matvec_streamed(cgx_ctx *c, Shard &s, const char *vec) {
+    const int64_t row_bytes = c->lda * (int64_t)c->es;
+    for (int64_t r0 = 0; r0 < s.nloc; r0 += s.tile_rows) {
+        const int64_t rows = std::min(s.tile_rows, s.nloc - r0);
+        const int b = s.next_buf;
+        s.next_buf = (s.next_buf + 1) % kStreamBufs;
+        const int64_t bytes = rows * row_bytes;
+        const char *src = s.A_host + (size_t)r0 * row_bytes;
+        const int64_t part = (bytes / s.ncopy + 4095) & ~int64_t(4095);
+        for (int q = 0; q < s.ncopy; ++q) {
+            const int64_t lo = std::min<int64_t>(bytes, q * part), hi = std::min<int64_t>(bytes, lo + part);
+            if (s.buf_used[b]) HIPT(hipStreamWaitEvent(s.copy[q], s.ev_free[b], 0));
+            if (hi > lo) HIPT(hipMemcpyAsync(s.tile[b] + lo, src + lo, hi - lo, hipMemcpyHostToDevice, s.copy[q]));
+            HIPT(hipEventRecord(s.ev_loaded[b][q], s.copy[q]));
+            HIPT(hipStreamWaitEvent(s.stream, s.ev_loaded[b][q], 0));
+        }
+        TRY(matvec_rows(c, s, s.tile_plan, s.tile[b], r0, rows, vec, false, 0));
+        HIPT(hipEventRecord(s.ev_free[b], s.stream));
+        s.buf_used[b] = true;
+    }
+    return CGX_OK;
+}
+
+// CGX_SYMMETRIC | CGX_HOST_STREAM: the upper-triangle tiles stream from
+// pinned host memory in chunks (the same buffer rotation and copy streams as
+// matvec_streamed); each chunk's k_symv_f64 writes per-tile row and column
+// partials, and one reduce (with the fused p.Ap) follows the last chunk.
+int matvec_sym_streamed(cgx_ctx *c, Shard &s, const char *vec, bool with_dot, int dot_slot, const int64_t *gate) {
+    const int64_t ntiles = sym_tiles(c->lda), tb = 128 * 128 * 8;
+    const double *p = reinterpret_cast<const double *>(vec);
+    for (int64_t q0 = 0; q0 < ntiles; q0 += s.tile_rows) {
+        const int64_t cnt = std::min(s.tile_rows, ntiles - q0);
+        const int b = s.next_buf;
+        s.next_buf = (s.next_buf + 1) % kStreamBufs;
+        const int64_t bytes = cnt * tb;
+        const char *src = s.A_host + (size_t)q0 * tb;
+        const int64_t part = (bytes / s.ncopy + 4095) & ~int64_t(4095);
+        for (int q = 0; q < s.ncopy; ++q) {
+            const int64_t lo = std::min<int64_t>(bytes, q * part), hi = std::min<int64_t>(bytes, lo + part);
+            if (s.buf_used[b]) HIPT(hipStreamWaitEvent(s.copy[q], s.ev_free[b], 0));
+            if (hi > lo) HIPT(hipMemcpyAsync(s.tile[b] + lo, src + lo, hi - lo, hipMemcpyHostToDevice, s.copy[q]));
+            HIPT(hipEventRecord(s.ev_loaded[b][q], s.copy[q]));
+            HIPT(hipStreamWaitEvent(s.stream, s.ev_loaded[b][q], 0));
+        }
+        HIPT(symv_tiles_f64(reinterpret_cast<const double *>(s.tile[b]), q0, cnt, c->lda, s.sym_grid, true, p,
+                            reinterpret_cast<double *>(s.sym_prow), reinterpret_cast<double *>(s.sym_pcol), s.stream,
+                            gate));
+        HIPT(hipEventRecord(s.ev_free[b], s.stream));
+        s.buf_used[b] = true;
+    }
+    HIPT(symv_reduce_f64(c->n, c->lda, 1, reinterpret_cast<const double *>(s.sym_prow),
+                         reinterpret_cast<const double *>(s.sym_pcol), reinterpret_cast<double *>(s.Ap),
+                         with_dot ? reinterpret_cast<const double *>(s.pown) : nullptr,
+                         with_dot ? reinterpret_cast<double *>(slot(s, dot_slot)) : nullptr, s.ws, s.stream, gate));
+    return CGX_OK;
+}
+
+// The host-mapped convergence record: written by shard 0's deciding kernel only.
+
+int launch_matvec(cgx_ctx *c, Shard &s, const char *vec, bool with_dot, int dot_slot, bool gated) {
+    const bool timing = (c->flags & CGX_TIMING) && (&s == &c->sh[0]);
+    if (timing && s.ev_used >= kEvPairs) TRY(timing_resolve(c));
+    if (timing) HIPT(hipEventRecord(s.ev_t[2 * s.ev_used], s.stream));
+    const bool streamed = (c->flags & CGX_HOST_STREAM) != 0;
+    if (c->op == OP_POISSON)
+        HIPT(stencil5_f64(reinterpret_cast<const double *>(vec), s.nloc / c->m, c->m, reinterpret_cast<double *>(s.Ap),
+                          with_dot ? reinterpret_cast<double *>(slot(s, dot_slot)) : nullptr, s.ws, s.stream,
+                          gate_of(s, gated)));
+    else if (streamed && (c->flags & CGX_SYMMETRIC))
+        TRY(matvec_sym_streamed(c, s, vec, with_dot, dot_slot, gate_of(s, gated)));
+    else if (streamed) TRY(matvec_streamed(c, s, vec));
+    else if (c->flags & CGX_SYMMETRIC)
+        HIPT(symv_f64(reinterpret_cast<const double *>(s.A), c->n, c->lda, s.sym_grid,
+                      reinterpret_cast<const double *>(vec), reinterpret_cast<double *>(s.sym_prow),
+                      reinterpret_cast<double *>(s.sym_pcol), reinterpret_cast<double *>(s.Ap),
+                      with_dot ? reinterpret_cast<const double *>(s.pown) : nullptr,
+                      with_dot ? reinterpret_cast<double *>(slot(s, dot_slot)) : nullptr, s.ws, s.stream,
+                      gate_of(s, gated)));
+    else TRY(matvec_rows(c, s, s.plan, s.A, 0, s.nloc, vec, with_dot && !f32ref(c), dot_slot, gated));
+    if (timing) {
+        HIPT(hipEventRecord(s.ev_t[2 * s.ev_used + 1], s.stream));
+        s.ev_used++;
+    }
+    if (with_dot && (f32ref(c) || (streamed && !(c->flags & CGX_SYMMETRIC)))) {
+        if (f32ref(c))  // vecVec(p, Ap) sequential (serialConjugate.c:219)
+            HIPT(dot_ref_f32(s.nloc, reinterpret_cast<const float *>(s.pown),
+                             reinterpret_cast<const float *>(s.Ap), reinterpret_cast<float *>(slot(s, dot_slot)),
+                             s.stream));
+        else
+            HIPT(dot_f64(s.nloc, reinterpret_cast<const double *>(s.pown),
+                         reinterpret_cast<const double *>(s.Ap), reinterpret_cast<double *>(slot(s, dot_slot)), s.ws,
+                         s.stream));
+    }
+    return CGX_OK;
+}
+
+// Whether x0 is all zeros on every shard (every rank in rank mode: one
+// int64 allreduce, so all ranks take the same branch of do_begin).
+int x0_is_zero(cgx_ctx *c, bool *zero) {
+    bool local = true;
+    for (auto &s : c->sh) local = local && s.x_zero;
+    if (c->mode != M_RCCL || c->nranks == 1) {
+        *zero = local;
+        return CGX_OK;
+    }
+    Shard &s = c->sh[0];
+    TRY(set_dev(s));
+    int64_t *pin = reinterpret_cast<int64_t *>(s.h_pin);
+    pin[0] = local ? 0 : 1;
+    HIPT(hipMemcpyAsync(slot(s, S_XNZ), pin, 8, hipMemcpyHostToDevice, s.stream));
+    NCCLT(ncclAllReduce(slot(s, S_XNZ), slot(s, S_XNZ), 1, ncclInt64, ncclSum, s.comm, s.stream));
+    HIPT(hipMemcpyAsync(pin, slot(s, S_XNZ), 8, hipMemcpyDeviceToHost, s.stream));
+    HIPT(hipStreamSynchronize(s.stream));
+    *zero = pin[0] == 0;
+    return CGX_OK;
+}
+
+int do_begin(cgx_ctx *c) {
+    // r0 = p0 = b - A x0; rr0 = r0.r0   (serialConjugate.c:209-212, parallel_cg.c:283-287)
+    // With x0 = 0 (the reference's usual initialguess, and the bench's) A x0 is
+    // exactly zero, so the exchange and the matVec are skipped: r0 = b - 0 = b
+    // bit for bit, one matVec fewer per solve.
+    TRY(settle_halo(c));
+    bool zero = false;
+    TRY(x0_is_zero(c, &zero));
+    if (!zero) TRY(exchange_allgather(c, /*from_x=*/true));  // full x0 into pfull
+    const int gs = S_RR + ring(0), ls = S_LRR + ring(0);
+    const int os = out_slot(c, ls, gs);
+    for (auto &s : c->sh) {
+        TRY(set_dev(s));
+        if (zero)
+            HIPT(hipMemsetAsync(s.Ap, 0, (size_t)s.nloc * c->es, s.stream));
+        else
+            TRY(launch_matvec(c, s, s.pfull, false, 0));
+        s.x_zero = false;  // the iterations update x
+        if (f32ref(c)) {
+            float *pown = reinterpret_cast<float *>(s.pown);
+            HIPT(residual_ref_f32(s.nloc, reinterpret_cast<const float *>(s.b), reinterpret_cast<const float *>(s.Ap),
+                                  reinterpret_cast<float *>(s.r), pown, s.stream));
+            HIPT(dot_ref_f32(s.nloc, reinterpret_cast<const float *>(s.r), reinterpret_cast<const float *>(s.r),
+                             reinterpret_cast<float *>(slot(s, os)), s.stream));
+        } else {
+            double *pown = reinterpret_cast<double *>(s.pown);
+            HIPT(residual_f64(s.nloc, reinterpret_cast<const double *>(s.b), reinterpret_cast<const double *>(s.Ap),
+                              reinterpret_cast<double *>(s.r), pown, reinterpret_cast<double *>(slot(s, os)), s.ws,
+                              s.stream));
+        }
+    }
+    TRY(exchange_scalar(c, ls, gs));
+    if (c->fused) TRY(exchange_halo_of(c, &Shard::rh));  // r0's halo rows for k_poisson_p
+    for (auto &s : c->sh) {  // device-side convergence record: not converged
+        TRY(set_dev(s));
+        HIPT(hipMemsetAsync(slot(s, S_KDONE), 0, 16, s.stream));
+        s.h_rec[0] = s.h_rec[1] = 0;  // no kernel of this solve has run yet (do_begin follows a sync)
+    }
+    c->k = 0;
+    c->converged = 0;
+    c->state = ST_BEGUN;
+    return CGX_OK;
+}
+
+int read_scalar(cgx_ctx *c, int gslot, double *out) {
+    Shard &s = c->sh[0];
+    TRY(set_dev(s));
+    HIPT(hipMemcpyAsync(s.h_pin, slot(s, gslot), 8, hipMemcpyDeviceToHost, s.stream));
+    HIPT(hipStreamSynchronize(s.stream));
+    if (f32ref(c)) {
+        float f;
+        std::memcpy(&f, s.h_pin, 4);
+        *out = (double)f;
+    } else {
+        *out = s.h_pin[0];
+    }
+    return CGX_OK;
+}
+
+// Fused Poisson iteration k (conjgrad.m's loop, two kernels, 64 B per grid
+// point; see k_poisson_p_f64 / k_poisson_xr_f64):
+//   p_k = r_k + beta p_{k-1}, p_k . A p_k      (gated: first decides the
+//                                               previous iteration's stop)
+//   allreduce(p.Ap)
+//   x += alpha p_k, r -= alpha A p_k, r.r
+//   allreduce(r.r); host-checked stop; r's halo rows for the next iteration.
+// x is current after every iteration, so a converged solve needs no extra pass.
+int do_iteration_poisson(cgx_ctx *c, double eps, int *stop, bool gated) {
+    const int64_t k = c->k;
+    *stop = 0;
+    const int64_t m = c->m;
+    const int pg = S_PAP + ring(k), pl = S_LPAP + ring(k);
+    const int rk = S_RR + ring(k), rkm1 = S_RR + ring(k + 3);  // r.r of iterations k, k-1
+    auto D = [](void *p) { return reinterpret_cast<double *>(p); };
+    const bool split = c->halo_pending;  // interior runs while the r halo exchange is in flight
+    for (auto &s : c->sh) {
+        TRY(set_dev(s));
+        char *pold = (k & 1) ? s.pfull : s.p2, *pnew = (k & 1) ? s.p2 : s.pfull;
+        for (int part : split ? std::initializer_list<int>{1, 2} : std::initializer_list<int>{0}) {
+            if (part == 2) HIPT(hipStreamWaitEvent(s.stream, s.ev_gathered, 0));
+            HIPT(poisson_p_f64(D(s.rh), D(pold), D(pnew), s.nloc / m, m, D(slot(s, rk)), D(slot(s, rkm1)), k == 0,
+                               D(slot(s, out_slot(c, pl, pg))), s.ws, s.stream, gated ? eps : -1.0, k,
+                               gated ? reinterpret_cast<int64_t *>(slot(s, S_KDONE)) : nullptr,
+                               gated ? D(slot(s, S_RRFINAL)) : nullptr, part, rec_of(c, s, gated)));
+        }
+    }
+    c->halo_pending = false;
+    TRY(exchange_scalar(c, pl, pg));
+    const int rg = S_RR + ring(k + 1), rl = S_LRR + ring(k + 1);
+    const int ro = out_slot(c, rl, rg);
+    for (auto &s : c->sh) {
+        TRY(set_dev(s));
+        const bool timing = (c->flags & CGX_TIMING) && (&s == &c->sh[0]);
+        if (timing && s.ev_used >= kEvPairs) TRY(timing_resolve(c));
+        if (timing) HIPT(hipEventRecord(s.ev_t[2 * s.ev_used], s.stream));
+        char *pnew = (k & 1) ? s.p2 : s.pfull;
+        HIPT(poisson_xr_f64(D(pnew), D(s.x), D(s.r), s.nloc / m, m, D(slot(s, rk)), D(slot(s, pg)), D(slot(s, ro)),
+                            s.ws, s.stream, gate_of(s, gated)));
+        if (timing) {
+            HIPT(hipEventRecord(s.ev_t[2 * s.ev_used + 1], s.stream));
+            s.ev_used++;
+        }
+    }
+    TRY(exchange_scalar(c, rl, rg));
+    c->k = k + 1;
+    c->total_iters += 1;
+    if (!gated && eps >= 0.0) {
+        double rr = 0.0;
+        TRY(read_scalar(c, rg, &rr));
+        c->last_rr = rr;
+        if (std::sqrt(rr) < eps) {
+            c->converged = 1;
+            c->state = ST_CONVERGED;
+            *stop = 1;
+            return CGX_OK;
+        }
+    }
+    return c->halo_overlap ? exchange_halo_async(c) : exchange_halo_of(c, &Shard::rh);
+}
+
+// One loop iteration k (serialConjugate.c:215-244 / parallel_cg.c:290-323).
+// Returns 1 in *stop when sqrt(r.r) < eps ended the loop (before the p update,
+// as the reference breaks at :235-238).
+// gated: fp64 device-side convergence (the host does not read r.r here; the
+// update kernel decides sqrt(r.r) < eps and later kernels skip themselves).
+int do_iteration(cgx_ctx *c, double eps, int *stop, bool gated) {
+    if (c->fused) return do_iteration_poisson(c, eps, stop, gated);
+    const int64_t k = c->k;
+    *stop = 0;
+    const int pg = S_PAP + ring(k), pl = S_LPAP + ring(k);
+    if (c->overlap) {
+        TRY(overlapped_matvec(c, out_slot(c, pl, pg), gated));  // parallel_cg.c:290-293, overlapped
+    } else {
+        TRY(exchange_allgather(c, false));  // MPI_Allgather(local_p -> p)  parallel_cg.c:290
+        for (auto &s : c->sh) {
+            TRY(set_dev(s));
+            TRY(launch_matvec(c, s, s.pfull, true, out_slot(c, pl, pg), gated));  // :215 / :292-293
+        }
+    }
+    TRY(exchange_scalar(c, pl, pg));  // MPI_Allreduce(p.Ap)  parallel_cg.c:294
+    const int rg = S_RR + ring(k + 1), rl = S_LRR + ring(k + 1);
+    const int ro = out_slot(c, rl, rg);
+    for (auto &s : c->sh) {
+        TRY(set_dev(s));
+        if (f32ref(c)) {
+            HIPT(update_xr_ref_f32(s.nloc, reinterpret_cast<float *>(s.x), reinterpret_cast<float *>(s.r),
+                                   reinterpret_cast<const float *>(s.pown),
+                                   reinterpret_cast<const float *>(s.Ap),
+                                   reinterpret_cast<const float *>(slot(s, S_RR + ring(k))),
+                                   reinterpret_cast<const float *>(slot(s, pg)), s.stream));
+            HIPT(dot_ref_f32(s.nloc, reinterpret_cast<const float *>(s.r), reinterpret_cast<const float *>(s.r),
+                             reinterpret_cast<float *>(slot(s, ro)), s.stream));
+        } else {
+            // r -= alpha Ap, r.r; x's update is deferred into the p update
+            HIPT(update_r_f64(s.nloc, reinterpret_cast<double *>(s.r), reinterpret_cast<const double *>(s.Ap),
+                              reinterpret_cast<const double *>(slot(s, S_RR + ring(k))),
+                              reinterpret_cast<const double *>(slot(s, pg)), reinterpret_cast<double *>(slot(s, ro)),
+                              s.ws, s.stream, gate_of(s, gated)));
+        }
+    }
+    TRY(exchange_scalar(c, rl, rg));  // MPI_Allreduce(r.r)  parallel_cg.c:313
+    c->k = k + 1;
+    c->total_iters += 1;
+    if (gated) {  // x (+ p unless converged) on the device, stopping rule decided there
+        for (auto &s : c->sh) {
+            TRY(set_dev(s));
+            HIPT(update_xp_f64(s.nloc, reinterpret_cast<double *>(s.x), reinterpret_cast<double *>(s.pown),
+                               reinterpret_cast<const double *>(s.r),
+                               reinterpret_cast<const double *>(slot(s, S_RR + ring(k))),
+                               reinterpret_cast<const double *>(slot(s, pg)),
+                               reinterpret_cast<const double *>(slot(s, rg)), s.stream, eps, k,
+                               reinterpret_cast<int64_t *>(slot(s, S_KDONE)),
+                               reinterpret_cast<double *>(slot(s, S_RRFINAL)), rec_of(c, s, gated)));
+        }
+        return CGX_OK;
+    }
+    if (eps >= 0.0) {  // if (sqrt(beta) < EPSILON) break;  serialConjugate.c:235-238
+        double rr = 0.0;
+        TRY(read_scalar(c, rg, &rr));
+        c->last_rr = rr;
+        if (std::sqrt(rr) < eps) {
+            c->converged = 1;
+            c->state = ST_CONVERGED;
+            *stop = 1;
+            if (!f32ref(c))  // the deferred x += alpha p, without the p update
+                for (auto &s : c->sh) {
+                    TRY(set_dev(s));
+                    HIPT(update_xp_f64(s.nloc, reinterpret_cast<double *>(s.x), reinterpret_cast<double *>(s.pown),
+                                       reinterpret_cast<const double *>(s.r),
+                                       reinterpret_cast<const double *>(slot(s, S_RR + ring(k))),
+                                       reinterpret_cast<const double *>(slot(s, pg)), nullptr, s.stream));
+                }
+            return CGX_OK;
+        }
+    }
+    for (auto &s : c->sh) {  // p = r + (beta/rsold) p    serialConjugate.c:239-243
+        TRY(set_dev(s));
+        if (f32ref(c))
+            HIPT(update_p_ref_f32(s.nloc, reinterpret_cast<float *>(s.pown),
+                                  reinterpret_cast<const float *>(s.r), reinterpret_cast<const float *>(slot(s, rg)),
+                                  reinterpret_cast<const float *>(slot(s, S_RR + ring(k))), s.stream));
+        else  // x += alpha p (deferred from the r update), then p = r + beta p
+            HIPT(update_xp_f64(s.nloc, reinterpret_cast<double *>(s.x), reinterpret_cast<double *>(s.pown),
+                               reinterpret_cast<const double *>(s.r),
+                               reinterpret_cast<const double *>(slot(s, S_RR + ring(k))),
+                               reinterpret_cast<const double *>(slot(s, pg)),
+                               reinterpret_cast<const double *>(slot(s, rg)), s.stream));
+    }
+    return CGX_OK;
+}
+
+}  // namespace cgxh
+
+extern "C" {
+
+int cgx_solve_begin(cgx_ctx *c) {
+    const Range range_("cgx_solve_begin");
+    if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
+    return do_begin(c);
+}
+
+// Fixed-count iterations from a hipGraph: one GPU (no exchange, no host
+// reads inside an iteration), no per-launch timing events.  kGraphIters
+// iterations are captured once per context, from an iteration k >= 1 that
+// is a multiple of kGraphIters: every launch argument then repeats with that
+// period (scalar ring slots, Poisson slab parity; k == 0 alone differs), so
+// the same graph replays at k, k + 4, ...  The kernels and their order are
+// the stream path's, so the results are bitwise the same (tested).  Opt-in
+// (CGX_GRAPH=1): replays measured 1-5 % SLOWER than stream launches at
+// N = 512-16384 and on Poisson grids (profiles/r01_graph_ab.jsonl; the
+// launches are already queued ahead of a GPU-bound loop).  A capture that
+// fails falls back to stream launches.
+static bool graph_ok(const cgx_ctx *c) {
+    const char *e = std::getenv("CGX_GRAPH");
+    if (!(e && *e == '1')) return false;
+    return c->mode == M_SINGLE && !c->graph_failed && !(c->flags & (CGX_TIMING | CGX_HOST_STREAM));
+}
+
+static int graph_block(cgx_ctx *c, bool *ran) {
+    *ran = false;
+    Shard &s = c->sh[0];
+    TRY(set_dev(s));
+    if (!c->graph) {
+        const int64_t k0 = c->k, t0 = c->total_iters;
+        HIPT(hipStreamBeginCapture(s.stream, hipStreamCaptureModeThreadLocal));
+        int rc = CGX_OK;
+        for (int i = 0; i < kGraphIters && rc == CGX_OK; ++i) {
+            int stop = 0;
+            rc = do_iteration(c, -1.0, &stop);
+        }
+        hipGraph_t g = nullptr;
+        const hipError_t ec = hipStreamEndCapture(s.stream, &g);
+        c->k = k0;
+        c->total_iters = t0;
+        if (rc == CGX_OK && ec == hipSuccess && g && hipGraphInstantiate(&c->graph, g, nullptr, nullptr, 0) == hipSuccess) {
+            (void)hipGraphDestroy(g);
+        } else {
+            if (g) (void)hipGraphDestroy(g);
+            (void)hipGetLastError();
+            c->graph = nullptr;
+            c->graph_failed = true;  // stream launches from now on
+            return CGX_OK;
+        }
+    }
+    HIPT(hipGraphLaunch(c->graph, s.stream));
+    c->k += kGraphIters;
+    c->total_iters += kGraphIters;
+    *ran = true;
+    return CGX_OK;
+}
+
+// Convergence-tested iterations without a host round trip per iteration:
+// the update kernel decides sqrt(r.r) < eps on the device and records k+1;
+// queued later iterations skip themselves.  The host keeps `look` iterations
+// in flight and reads the record of an older iteration (pinned memory,
+// event-ordered), so at most `look` no-op iterations are ever enqueued.
+static int iterate_gated(cgx_ctx *c, int64_t count, double eps, int64_t *done, int *converged) {
+    Shard &s0 = c->sh[0];
+    const char *la = std::getenv("CGX_LOOKAHEAD");
+    const int look = std::max(1, std::min(kLookRing - 1, (la && *la) ? std::atoi(la) : 2));
+    const int64_t k0 = c->k;
+    int64_t issued = 0, kd = 0;
+    volatile int64_t *rec = s0.h_rec;  // {kdone, r.r bits}, stored by the deciding kernel
+    for (; issued < count && kd == 0; ++issued) {
+        int stop = 0;
+        TRY(do_iteration(c, eps, &stop, /*gated=*/true));
+        TRY(set_dev(s0));
+        const int q = (int)(issued % kLookRing);
+        HIPT(hipEventRecord(s0.ev_look[q], s0.stream));
+        if (issued >= look) {
+            HIPT(hipEventSynchronize(s0.ev_look[(issued - look) % kLookRing]));
+            // Only a record left by an iteration the event covers counts: the
+            // host-mapped word may already show a later iteration's decision,
+            // and acting on that would make the number of enqueued iterations
+            // (and so of collectives) depend on timing, rank by rank.  The
+            // record's k is the deciding launch's iteration index (dense: the
+            // converged iteration + 1, Poisson: the next iteration), so
+            // k <= the synced iteration means that launch is covered.
+            const int64_t r = rec[0];
+            if (r != 0 && r <= k0 + (issued - look)) kd = r;
+        }
+    }
+    TRY(sync_all(c));
+    const int64_t kdev = rec[0];
+    const int64_t did = kdev ? (kdev - k0) : issued;
+    c->total_iters += did - issued;  // do_iteration counted every enqueued one
+    if (kdev) {
+        const int64_t bits = rec[1];
+        double rrf;
+        std::memcpy(&rrf, &bits, 8);
+        c->last_rr = rrf;
+        c->k = kdev;
+        c->converged = 1;
+        c->state = ST_CONVERGED;
+    } else {
+        double rr = 0.0;
+        TRY(read_scalar(c, S_RR + ring(c->k), &rr));
+        c->last_rr = rr;
+        // The fused Poisson iteration decides a stop one iteration later (at
+        // the start of the next k_poisson_p); the last issued iteration's
+        // r.r is tested here.  (The dense kernels already tested it.)
+        if (c->fused && eps >= 0.0 && std::sqrt(rr) < eps) {
+            c->converged = 1;
+            c->state = ST_CONVERGED;
+        }
+    }
+    if (done) *done = did;
+    if (converged) *converged = c->converged;
+    return CGX_OK;
+}
+
+int cgx_iterate(cgx_ctx *c, int64_t count, double eps, int64_t *done, int *converged) {
+    const Range range_("cgx_iterate");
+    if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
+    if (c->state == ST_IDLE) return fail(CGX_ERR_STATE, "cgx_iterate before cgx_solve_begin");
+    const char *gv = std::getenv("CGX_GATED");
+    const bool gate_ok = !(gv && *gv == '0');
+    if (c->state == ST_BEGUN && count > 0 && eps >= 0.0 && !f32ref(c) && !(c->flags & CGX_HOST_STREAM) && gate_ok)
+        return iterate_gated(c, count, eps, done, converged);
+    int64_t did = 0;
+    const bool use_graph = eps < 0.0 && graph_ok(c);
+    while (did < count && c->state == ST_BEGUN) {
+        if (use_graph && c->k >= kGraphIters && c->k % kGraphIters == 0 && count - did >= kGraphIters) {
+            bool ran = false;
+            TRY(graph_block(c, &ran));
+            if (ran) {
+                did += kGraphIters;
+                continue;
+            }
+        }
+        int stop = 0;
+        TRY(do_iteration(c, eps, &stop));
+        ++did;
+        if (stop) break;
+    }
+    if (done) *done = did;
+    if (converged) *converged = c->converged;
+    return CGX_OK;
+}
+
+int cgx_solve(cgx_ctx *c, void *x_inout, double eps, int64_t max_iter, cgx_stats *st) {
+    const Range range_("cgx_solve");
+    if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
+    if (x_inout) TRY(cgx_set_x(c, x_inout));
+    TRY(sync_all(c));
+    const auto t0 = std::chrono::steady_clock::now();
+    TRY(do_begin(c));
+    const int64_t cap = max_iter < 0 ? c->n : max_iter;  // for(k=0; k<ROWS; ++k)
+    int64_t done = 0;
+    int conv = 0;
+    TRY(cgx_iterate(c, cap, eps, &done, &conv));
+    TRY(sync_all(c));
+    const auto t1 = std::chrono::steady_clock::now();
+    c->solve_ms = std::chrono::duration<double, std::milli>(t1 - t0).count();
+    if (eps < 0.0 && c->k > 0) {
+        double rr = 0.0;
+        TRY(read_scalar(c, S_RR + ring(c->k), &rr));
+        c->last_rr = rr;
+    }
+    if (x_inout) TRY(cgx_get_x(c, x_inout));
+    if (st) TRY(cgx_get_stats(c, st));
+    return CGX_OK;
+}
+
+int cgx_get_stats(cgx_ctx *c, cgx_stats *st) {
+    if (!c || !st) return fail(CGX_ERR_ARG, "NULL argument");
+    TRY(sync_all(c));
+    st->iterations = c->k;
+    st->converged = c->converged;
+    st->rr = c->last_rr;
+    st->solve_ms = c->solve_ms;
+    st->matvec_ms = c->matvec_ms;
+    st->matvec_count = c->matvec_count;
+    st->total_iterations = c->total_iters;
+    return CGX_OK;
+}
+
+int cgx_reset_timing(cgx_ctx *c) {
+    if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
+    TRY(sync_all(c));
+    c->matvec_ms = 0.0;
+    c->matvec_count = 0;
+    return CGX_OK;
+}
+
+int cgx_synchronize(cgx_ctx *c) {
+    if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
+    return sync_all(c);
+}
+
+void *cgx_stream(cgx_ctx *c) { return c ? (void *)c->sh[0].stream : nullptr; }
+
+int cgx_set_matvec_plan(cgx_ctx *c, int rows_per_wave, int chunks_in_flight, int nontemporal, int blocks_per_cu) {
+    if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
+    if (f32ref(c) || c->op != OP_DENSE || (c->flags & CGX_SYMMETRIC))
+        return fail(CGX_ERR_ARG, "only the fp64 row-major dense matVec has a tunable plan");
+    const int R = rows_per_wave, U = chunks_in_flight;
+    if (R != 1 && R != 2 && R != 4 && R != 8) return fail(CGX_ERR_ARG, "rows_per_wave must be 1, 2, 4 or 8");
+    if (U != 2 && U != 4 && U != 8) return fail(CGX_ERR_ARG, "chunks_in_flight must be 2, 4 or 8");
+    if (nontemporal < 0 || nontemporal > 13 || (nontemporal >= 2 && U == 2))
+        return fail(CGX_ERR_ARG, "load policy must be 0..13 (2..13 need chunks_in_flight 4 or 8)");
+    for (auto &s : c->sh) {
+        TRY(set_dev(s));
+        MatvecPlan pl = plan_matvec_f64(s.dev, s.nloc, R, U, nontemporal, blocks_per_cu);
+        s.plan = pl;
+    }
+    if (c->graph) {  // the captured launches carry the old plan
+        HIPT(hipGraphExecDestroy(c->graph));
+        c->graph = nullptr;
+    }
+    return CGX_OK;
+}
+
+int cgx_get_matvec_plan(cgx_ctx *c, int *rows_per_wave, int *chunks_in_flight, int *nontemporal, int *blocks) {
+    if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
+    const MatvecPlan &pl = c->sh[0].plan;
+    if (rows_per_wave) *rows_per_wave = pl.R;
+    if (chunks_in_flight) *chunks_in_flight = pl.U;
+    if (nontemporal) *nontemporal = pl.nt;
+    if (blocks) *blocks = pl.blocks;
+    return CGX_OK;
+}
+
+int cgx_residual_norm(cgx_ctx *c, double *rnorm, double *bnorm) {
+    const Range range_("cgx_residual_norm");
+    if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
+    // ||b - A x|| with the current x: allgather x, matVec, residual, two dots.
+    TRY(settle_halo(c));
+    TRY(exchange_allgather(c, /*from_x=*/true));
+    const int tro = out_slot(c, S_LTR, S_TR), tbo = out_slot(c, S_LTB, S_TB);
+    for (auto &s : c->sh) {
+        TRY(set_dev(s));
+        TRY(launch_matvec(c, s, s.pfull, false, 0));
+        if (f32ref(c)) {
+            HIPT(residual_ref_f32(s.nloc, reinterpret_cast<const float *>(s.b), reinterpret_cast<const float *>(s.Ap),
+                                  reinterpret_cast<float *>(s.r), nullptr, s.stream));
+            HIPT(dot_ref_f32(s.nloc, reinterpret_cast<const float *>(s.r), reinterpret_cast<const float *>(s.r),
+                             reinterpret_cast<float *>(slot(s, tro)), s.stream));
+            HIPT(dot_ref_f32(s.nloc, reinterpret_cast<const float *>(s.b), reinterpret_cast<const float *>(s.b),
+                             reinterpret_cast<float *>(slot(s, tbo)), s.stream));
+        } else {
+            HIPT(residual_f64(s.nloc, reinterpret_cast<const double *>(s.b), reinterpret_cast<const double *>(s.Ap),
+                              reinterpret_cast<double *>(s.r), nullptr, reinterpret_cast<double *>(slot(s, tro)), s.ws,
+                              s.stream));
+            HIPT(dot_f64(s.nloc, reinterpret_cast<const double *>(s.b), reinterpret_cast<const double *>(s.b),
+                         reinterpret_cast<double *>(slot(s, tbo)), s.ws, s.stream));
+        }
+    }
+    TRY(exchange_scalar(c, S_LTR, S_TR));
+    TRY(exchange_scalar(c, S_LTB, S_TB));
+    double rr = 0.0, bb = 0.0;
+    TRY(read_scalar(c, S_TR, &rr));
+    TRY(read_scalar(c, S_TB, &bb));
+    if (rnorm) *rnorm = std::sqrt(rr);
+    if (bnorm) *bnorm = std::sqrt(bb);
+    c->state = ST_IDLE;  // r and p were overwritten
+    return CGX_OK;
+}
+
+}  // extern "C"
