@@ -1,30 +1,6 @@
 // cgx_api.hip -- the C ABI of include/cgx.h: errors and devices, and the
 // kernel-level entry points; the rest of the ABI lives in cgx_setup.hip,
 // cgx_exchange.hip and cgx_iterate.hip (shared types: cgx_ctx.h).
-//
-// Reference mapping:
-//   conjugrad()              serialConjugate.c:180-259 / parallel_cg.c:248-345
-//       -> cgx_solve = cgx_solve_begin (:209-212) + cgx_iterate (:213-245)
-//   MPI_Bcast x0 / MPI_Scatter A,b   parallel_cg.c:109-117 -> cgx_set_rows
-//   MPI_Allgather(local_p -> p)      parallel_cg.c:290-291 -> exchange_allgather
-//   MPI_Allreduce(p.Ap), (r.r)       parallel_cg.c:287,294,313 -> exchange_scalar
-//
-// A context holds one or more shards.  A shard = one contiguous row block of
-// A (rows [row0, row0+nloc), every column, leading dimension lda = n rounded
-// up to 128 with zero padding), its slices of b, x, r, Ap, a full-length p
-// (padded, zero tail) whose own slice doubles as the local p, and a small
-// device scalar block.  Three exchange modes:
-//   SINGLE  one shard, no exchange.
-//   LOCAL   several shards in this process (distinct or repeated devices);
-//           allgather by device-to-device copies, scalars combined as
-//           partials summed in rank order (point-to-point_cg.c allSum order).
-//   RCCL    one shard per process (torchrun / mpirun style), RCCL allgather
-//           of p and allreduce of the scalars over xGMI on the shard stream.
-//
-// Scalar slots (8 bytes each; F32_REF stores a float at the slot start):
-//   RR(j)   = r_j.r_j (global)      PAP(k) = p_k.Ap_k (global)   ring of 4
-//   LRR(j), LPAP(k): this shard's partials when an exchange follows
-//   GATHER+q: the partial of shard q (ordered combine)
 #include "cgx_ctx.h"
 
 namespace cgxh {
