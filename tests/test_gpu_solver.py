@@ -82,9 +82,11 @@ def test_row_block_shards_f32ref(name, P):
 @pytest.mark.parametrize("name", ["kat4", "spd1024", "spd4096"])
 def test_row_block_shards_f64(golden, name, P):
     A, b, x0 = case(name, np.float64)
-    if b.size % P:
-        pytest.skip("n not divisible")
     x = x0.copy()
+    if b.size % P:  # parallel_cg.c:86-90: N must split into P equal row blocks
+        with pytest.raises(cg.CgxError, match="not divisible"):
+            cg.conjugrad(A, b, x, eps=1e-10, shards=[0] * P)
+        return
     st = cg.conjugrad(A, b, x, eps=1e-10, shards=[0] * P)
     xo, so = oracle.cg_f64(A, b, x0, eps=1e-10)
     assert st.iterations == so.iterations
