@@ -356,6 +356,7 @@ def main(argv=None) -> int:
         "n_gpus": world,
         "steps": args.steps,
         "warmup": args.warmup,
+        "settle_s": args.settle,
         "ms_per_step": elapsed / args.steps * 1e3,
         "higher_is_better": True,
         "scaling": "strong",
