@@ -40,6 +40,21 @@ __device__ __forceinline__ void grid_sum_last_block(double v, double *partials, 
     v = wave_sum(v);
     if (lane == 0) red[wid] = v;
     __syncthreads();
+    if (gridDim.x == 1) {
+        // one block (n <= 2048 in the vector kernels): no hand-off through
+        // memory, two dependent round trips fewer (fixed-count iterations
+        // 5-7 % faster at N=512-2048, profiles/r01_ab_one_block_reduce.txt).
+        // The same bits as the hand-off, which adds the block's sum to 0.0
+        // (so a -0 sum comes out +0 there too).
+        if (threadIdx.x == 0) {
+            double t = red[0];
+#pragma unroll
+            for (int w = 1; w < kNT / 64; ++w) t += red[w];
+            t = 0.0 + t;
+            *out = add_to_out ? *out + t : t;
+        }
+        return;
+    }
     if (threadIdx.x == 0) {
         double t = red[0];
 #pragma unroll
