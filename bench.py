@@ -69,6 +69,10 @@ def dist_init():
     import torch.distributed as dist
     if not dist.is_initialized():
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        # one node (every rank local): RCCL's bootstrap over loopback, whatever
+        # interfaces the box has; the data path is xGMI either way
+        if os.environ.get("LOCAL_WORLD_SIZE", "1") == os.environ.get("WORLD_SIZE", "1"):
+            os.environ.setdefault("NCCL_SOCKET_IFNAME", "lo")
         dist.init_process_group("gloo")
     return dist
 
