@@ -56,7 +56,39 @@ using namespace cgx;
 namespace cgxh {
 extern thread_local char g_err[1024];
 int fail(int code, const char *fmt, ...);
+
+// RCCL, loaded on first use (cgx_rccl.hip): rank mode calls it through these
+// pointers (the macros below keep the nccl* names at the call sites).
+struct RcclApi {
+    decltype(&::ncclGetUniqueId) GetUniqueId = nullptr;
+    decltype(&::ncclCommInitRank) CommInitRank = nullptr;
+    decltype(&::ncclCommDestroy) CommDestroy = nullptr;
+    decltype(&::ncclGetErrorString) GetErrorString = nullptr;
+    decltype(&::ncclAllGather) AllGather = nullptr;
+    decltype(&::ncclAllReduce) AllReduce = nullptr;
+    decltype(&::ncclSend) Send = nullptr;
+    decltype(&::ncclRecv) Recv = nullptr;
+    decltype(&::ncclGroupStart) GroupStart = nullptr;
+    decltype(&::ncclGroupEnd) GroupEnd = nullptr;
+};
+extern RcclApi g_rccl;
+// Loads librccl.so.1 once; false (with cgx_last_error set) if it cannot.
+// Every entry point that reaches RCCL first passes through this.
+bool rccl_load();
 }  // namespace cgxh
+
+#ifndef CGX_RCCL_LOADER
+#define ncclGetUniqueId (cgxh::g_rccl.GetUniqueId)
+#define ncclCommInitRank (cgxh::g_rccl.CommInitRank)
+#define ncclCommDestroy (cgxh::g_rccl.CommDestroy)
+#define ncclGetErrorString (cgxh::g_rccl.GetErrorString)
+#define ncclAllGather (cgxh::g_rccl.AllGather)
+#define ncclAllReduce (cgxh::g_rccl.AllReduce)
+#define ncclSend (cgxh::g_rccl.Send)
+#define ncclRecv (cgxh::g_rccl.Recv)
+#define ncclGroupStart (cgxh::g_rccl.GroupStart)
+#define ncclGroupEnd (cgxh::g_rccl.GroupEnd)
+#endif
 
 #define HIPT(expr)                                                                              \
     do {                                                                                        \

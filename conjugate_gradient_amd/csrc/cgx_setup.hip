@@ -345,6 +345,7 @@ static int create_rank(cgx_ctx **ctx, int op, int64_t n, int64_t m, int rank, in
     if (rank < 0 || rank >= nranks) return fail(CGX_ERR_ARG, "rank %d not in [0, %d)", rank, nranks);
     if (nranks > S_TR - S_GATHER) return fail(CGX_ERR_ARG, "at most %d ranks", S_TR - S_GATHER);
     TRY(check_device(device));
+    if (!rccl_load()) return CGX_ERR_RCCL;
     cgx_ctx *c = new_ctx_op(op, n, m, nranks, flags);
     if (!c) return fail(CGX_ERR_NOMEM, "host allocation failed");
     c->mode = M_RCCL;
@@ -379,6 +380,7 @@ int cgx_create_multi(cgx_ctx **ctx, int64_t n, int nshards, const int *devices, 
 int cgx_get_unique_id(cgx_unique_id *id) {
     if (!id) return fail(CGX_ERR_ARG, "id is NULL");
     static_assert(sizeof(ncclUniqueId) == sizeof(cgx_unique_id), "unique id size");
+    if (!rccl_load()) return CGX_ERR_RCCL;
     ncclUniqueId u;
     NCCLT(ncclGetUniqueId(&u));
     std::memcpy(id, &u, sizeof u);

@@ -33,9 +33,24 @@ def test_every_declared_symbol_exported(built):
         assert hasattr(L, f)
 
 
-def test_library_links_hip_and_rccl(built):
+def test_library_links_hip_loads_rccl_on_demand(built):
+    """libcgx links the HIP runtime; RCCL is dlopen'ed by rank mode only
+    (cgx_rccl.hip), so single-GPU processes do not pay for loading it."""
     out = subprocess.run(["readelf", "-d", cg.LIB_PATH], capture_output=True, text=True, check=True).stdout
-    assert "libamdhip64.so" in out and "librccl.so" in out
+    assert "libamdhip64.so" in out and "librccl.so" not in out
+    undef = subprocess.run(["nm", "-D", "--undefined-only", cg.LIB_PATH], capture_output=True, text=True,
+                           check=True).stdout
+    assert " nccl" not in undef
+
+
+def test_rccl_loads_on_first_rank_call(built, monkeypatch):
+    """cgx_get_unique_id loads RCCL: with a GPU it returns an id; without one
+    (this container) RCCL itself reports the error -- never a load failure."""
+    monkeypatch.setenv("NCCL_SOCKET_IFNAME", "lo")
+    try:
+        assert len(cg.get_unique_id()) == 128
+    except cg.CgxError as e:
+        assert "RCCL error" in str(e) and "cannot load RCCL" not in str(e), str(e)
 
 
 def test_gfx950_code_object(built):
