@@ -63,7 +63,10 @@ def lib() -> ctypes.CDLL:
         L.oracle_matvec_f64.argtypes = [i64, i64, vp, vp, vp]
         L.oracle_dot_f64.argtypes = [i64, vp, vp]
         L.oracle_dot_f64.restype = f64
-        L.oracle_cg_f32ref.argtypes = [i64, vp, vp, vp, i64, f64, ctypes.c_int, ctypes.POINTER(OracleStats)]
+        L.oracle_cg_f32ref.argtypes = [i64, vp, vp, vp, i64, f64, ctypes.c_int, ctypes.c_int,
+                                       ctypes.POINTER(OracleStats)]
+        L.oracle_combine_f32.argtypes = [vp, ctypes.c_int, ctypes.c_int]
+        L.oracle_combine_f32.restype = ctypes.c_float
         L.oracle_cg_f32ref.restype = ctypes.c_int
         L.oracle_cg_f64.argtypes = [i64, vp, vp, vp, i64, f64, ctypes.POINTER(OracleStats)]
         L.oracle_cg_f64.restype = ctypes.c_int
@@ -137,13 +140,28 @@ def matvec_f64(A: np.ndarray, v: np.ndarray) -> np.ndarray:
     return out
 
 
-def cg_f32ref(A, b, x0, max_iter: int = -1, eps: float = 1e-6, nparts: int = 1):
-    """serialConjugate.c conjugrad restated; returns (x, OracleStats)."""
+# How P row-block partials of a dot product are combined (cg_oracle.h):
+#   "rank"  -- point-to-point_cg.c allSum (:339-359), sequential in rank order;
+#   "mpich" -- parallel_cg.c's MPI_Allreduce (:287,294,313) as MPICH 3.3 does it
+#              for one float: recursive doubling, a balanced pairwise tree.
+COMBINE = {"rank": 0, "mpich": 1}
+
+
+def combine_f32(parts, combine: str = "rank") -> np.float32:
+    a = np.ascontiguousarray(parts, np.float32)
+    return np.float32(lib().oracle_combine_f32(_p(a), a.size, COMBINE[combine]))
+
+
+def cg_f32ref(A, b, x0, max_iter: int = -1, eps: float = 1e-6, nparts: int = 1, combine: str = "rank"):
+    """serialConjugate.c conjugrad restated (nparts > 1: parallel_cg.c /
+    point-to-point_cg.c on nparts ranks, partials combined in `combine`
+    order); returns (x, OracleStats)."""
     A = np.ascontiguousarray(A, np.float32)
     b = np.ascontiguousarray(b, np.float32)
     x = np.array(x0, dtype=np.float32, copy=True)
     st = OracleStats()
-    rc = lib().oracle_cg_f32ref(b.size, _p(A), _p(b), _p(x), max_iter, eps, nparts, ctypes.byref(st))
+    rc = lib().oracle_cg_f32ref(b.size, _p(A), _p(b), _p(x), max_iter, eps, nparts, COMBINE[combine],
+                                ctypes.byref(st))
     if rc != 0:
         raise RuntimeError(f"oracle_cg_f32ref rc={rc}")
     return x, st

@@ -95,6 +95,14 @@ int oracle_spd_matlab(int64_t n, int as_float, void *A, void *b) {
         for (int64_t i = 0; i < n; ++i) R[(size_t)j * n + i] = mt_res53(&m);
     /* A = 0.5*(R+R') + n*eye(n).  Symmetric, so the row-major reader sees
      * the same values as MATLAB's column-major writer. */
+    /* the text round trip dominates (snprintf + strtof per value); rows are
+     * independent, so it runs on every host core (same values for any count) */
+#ifdef _OPENMP
+    const int gen_threads = omp_get_num_procs() < 16 ? omp_get_num_procs() : 16;
+#else
+    const int gen_threads = 1;
+#endif
+#pragma omp parallel for schedule(dynamic, 16) num_threads(gen_threads)
     for (int64_t i = 0; i < n; ++i) {
         for (int64_t j = 0; j < n; ++j) {
             double v = 0.5 * (R[(size_t)j * n + i] + R[(size_t)i * n + j]);
@@ -186,23 +194,49 @@ float oracle_dot_f32ref(int64_t n, const float *a, const float *b) {
     return s;
 }
 
-/* Dot product as `nparts` row-block partials, each sequential, then summed in
- * part order (point-to-point_cg.c allSum :344-357).  nparts == 1 is vecVec. */
-static float dot_parts_f32(int64_t n, const float *a, const float *b, int nparts) {
-    if (nparts <= 1) return oracle_dot_f32ref(n, a, b);
-    int64_t loc = n / nparts;
-    float total = 0.0f;
-    for (int q = 0; q < nparts; ++q) {
-        float part = oracle_dot_f32ref(loc, a + (size_t)q * loc, b + (size_t)q * loc);
-        total = (q == 0) ? part : total + part;
-    }
+/* MPICH 3.3 MPI_Allreduce, commutative op, short message: recursive doubling
+ * (MPIR_Allreduce_intra_recursive_doubling).  With pof2 the largest power of
+ * two <= cnt and rem = cnt - pof2, ranks 2q and 2q+1 (q < rem) first combine,
+ * leaving pof2 values; then at distance 1, 2, 4, .. every value is combined
+ * with its partner's.  fp32 addition is commutative, so both partners hold
+ * the same bits after each step: the result is the balanced tree below. */
+static float combine_mpich_f32(const float *in, int cnt) {
+    int pof2 = 1;
+    while (pof2 * 2 <= cnt) pof2 *= 2;
+    const int rem = cnt - pof2;
+    float v[64];
+    if (pof2 > 64) return NAN;
+    for (int q = 0; q < pof2; ++q)
+        v[q] = q < rem ? in[2 * q] + in[2 * q + 1] : in[q + rem];
+    for (int d = 1; d < pof2; d *= 2)
+        for (int q = 0; q < pof2; q += 2 * d) v[q] = v[q] + v[q + d];
+    return v[0];
+}
+
+float oracle_combine_f32(const float *in, int cnt, int combine) {
+    if (cnt <= 0) return 0.0f;
+    if (combine == ORACLE_COMBINE_MPICH) return combine_mpich_f32(in, cnt);
+    float total = in[0];                      /* allSum :346-352 */
+    for (int q = 1; q < cnt; ++q) total = total + in[q];
     return total;
 }
 
+/* Dot product as `nparts` row-block partials, each sequential (vecVec
+ * parallel_cg.c:211-221 over local_row), then combined in `combine` order.
+ * nparts == 1 is serialConjugate.c's vecVec. */
+static float dot_parts_f32(int64_t n, const float *a, const float *b, int nparts, int combine) {
+    if (nparts <= 1) return oracle_dot_f32ref(n, a, b);
+    int64_t loc = n / nparts;
+    float part[64];
+    for (int q = 0; q < nparts; ++q)
+        part[q] = oracle_dot_f32ref(loc, a + (size_t)q * loc, b + (size_t)q * loc);
+    return oracle_combine_f32(part, nparts, combine);
+}
+
 int oracle_cg_f32ref(int64_t n, const float *A, const float *b, float *x,
-                     int64_t max_iter, double eps, int nparts, oracle_stats *st) {
+                     int64_t max_iter, double eps, int nparts, int combine, oracle_stats *st) {
     if (nparts < 1) nparts = 1;
-    if (n % nparts != 0) return -2;
+    if (n % nparts != 0 || nparts > 64) return -2;
     if (max_iter < 0) max_iter = n;
     float *Av = (float *)malloc((size_t)n * sizeof(float));
     float *r = (float *)malloc((size_t)n * sizeof(float));
@@ -214,7 +248,7 @@ int oracle_cg_f32ref(int64_t n, const float *A, const float *b, float *x,
     oracle_matvec_f32ref(n, n, A, x, Av);
     for (int64_t i = 0; i < n; ++i) r[i] = b[i] - Av[i];
     for (int64_t i = 0; i < n; ++i) p[i] = b[i] - Av[i];
-    float rsold = dot_parts_f32(n, r, r, nparts);
+    float rsold = dot_parts_f32(n, r, r, nparts, combine);
     double t1 = now_s();
 
     int64_t iters = 0;
@@ -222,7 +256,7 @@ int oracle_cg_f32ref(int64_t n, const float *A, const float *b, float *x,
     float rr = rsold;
     for (int64_t k = 0; k < max_iter; ++k) {
         oracle_matvec_f32ref(n, n, A, p, Av);                 /* :215      */
-        float pAp = dot_parts_f32(n, p, Av, nparts);          /* :219      */
+        float pAp = dot_parts_f32(n, p, Av, nparts, combine);          /* :219      */
         float alpha = rsold / pAp;                            /* :220      */
         for (int64_t i = 0; i < n; ++i) {                     /* :221,225  */
             float t = p[i] * alpha;
@@ -232,7 +266,7 @@ int oracle_cg_f32ref(int64_t n, const float *A, const float *b, float *x,
             float t = Av[i] * alpha;
             r[i] = r[i] - t;
         }
-        rr = dot_parts_f32(n, r, r, nparts);                  /* :234      */
+        rr = dot_parts_f32(n, r, r, nparts, combine);                  /* :234      */
         iters = k + 1;
         if (eps >= 0.0 && sqrt((double)rr) < eps) {           /* :235-238  */
             converged = 1;

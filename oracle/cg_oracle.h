@@ -11,9 +11,15 @@
  *       loops matVec :109-120, residual :124-131, scalarVec :135-142,
  *       vecVec :145-155, vecAdd :159-166, vecSub :170-177, fp32 throughout,
  *       sequential accumulation, no FMA contraction.  With nparts > 1 the dot
- *       products are formed as per-part partials summed sequentially in part
- *       order, which is point-to-point_cg.c's allSum (:339-359) over a
- *       row-block split (parallel_cg.c:83, :283-323).
+ *       products are formed as per-part (row-block, parallel_cg.c:83) partials
+ *       and combined in one of two orders:
+ *         ORACLE_COMBINE_RANK  : sequentially in part order, point-to-point_cg.c's
+ *                                allSum (:339-359);
+ *         ORACLE_COMBINE_MPICH : MPICH 3.3's MPI_Allreduce(MPI_SUM) for a
+ *                                1-element message, recursive doubling: the
+ *                                first 2*rem parts pairwise ((p0+p1), (p2+p3), ..),
+ *                                rem = P - pof2, then a balanced pairwise tree over
+ *                                the pof2 values -- parallel_cg.c:287,294,313.
  *   - oracle_cg_f64    : conjgrad.m:1-18 in IEEE double (sequential sums).
  *   - oracle_spd_matlab: generateSPDmatrix.m:1-45 under MATLAB `rng default`
  *       (MT19937 seed 5489, genrand_res53, column-major fill), passed through
@@ -25,8 +31,11 @@
  *
  * Parity status: pinned.  tests/golden/ holds outputs of the UNMODIFIED
  * serialConjugate.c (built by oracle/Makefile into oracle/_ref/) on the
- * reference's own 2x2/4x4 fixtures and on generateSPDmatrix inputs; the
- * not-gpu suite checks this oracle against them bit for bit.
+ * reference's own 2x2/4x4 fixtures and on generateSPDmatrix inputs, and of the
+ * UNMODIFIED parallel_cg.c / point-to-point_cg.c (mpicc, mpiexec -np 1/2/4/8,
+ * oracle/ref/mpi_harness.c) on the same inputs; the not-gpu suite checks this
+ * oracle against all of them bit for bit (serial, and nparts = P with the
+ * matching combine order).
  */
 #ifndef CG_ORACLE_H
 #define CG_ORACLE_H
@@ -73,10 +82,14 @@ typedef struct {
 
 /* serialConjugate.c conjugrad restated.  x is x0 on entry, solution on exit.
  * max_iter < 0 -> n (the reference's `k < ROWS`); eps < 0 -> never stop.
- * nparts >= 1: dot products as nparts row-block partials summed in order. */
+ * nparts >= 1: dot products as nparts row-block partials, combined in the
+ * `combine` order (ORACLE_COMBINE_*; ignored for nparts == 1). */
+enum { ORACLE_COMBINE_RANK = 0, ORACLE_COMBINE_MPICH = 1 };
 int oracle_cg_f32ref(int64_t n, const float *A, const float *b, float *x,
-                     int64_t max_iter, double eps, int nparts,
+                     int64_t max_iter, double eps, int nparts, int combine,
                      oracle_stats *st);
+/* The combine alone: `cnt` partials in[0..cnt) in the ORACLE_COMBINE_* order. */
+float oracle_combine_f32(const float *in, int cnt, int combine);
 
 /* conjgrad.m restated in double. */
 int oracle_cg_f64(int64_t n, const double *A, const double *b, double *x,

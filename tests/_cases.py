@@ -28,7 +28,7 @@ def numbers(name: str, count: int, dtype=np.float32) -> np.ndarray:
     return np.array([float(t) for t in toks], dtype=dtype)
 
 
-@functools.lru_cache(maxsize=4)
+@functools.lru_cache(maxsize=8)
 def _spd(n: int, dt: str):
     return oracle.spd_matlab(n, np.dtype(dt))
 
@@ -56,3 +56,26 @@ def golden_x(golden: dict, name: str) -> np.ndarray:
 KATS = ["kat2", "kat2_x0", "kat4"]
 SPD_SMALL = ["spd512", "spd1024", "spd2048"]
 SPD_ALL = ["spd512", "spd1024", "spd2048", "spd4096", "spd8192"]
+
+
+# ---- MPI goldens (tests/golden/mpi/, make_golden_mpi.py) -----------------------
+# parallel_cg.c (MPI_Allreduce, MPICH order) and point-to-point_cg.c (allSum,
+# rank order) run unmodified under mpiexec -np P on the cases above.
+COMBINE_OF = {"parallel": "mpich", "p2p": "rank"}
+
+
+@functools.lru_cache(maxsize=1)
+def golden_mpi() -> dict:
+    import json
+    with open(os.path.join(GOLDEN, "mpi", "golden_mpi.json")) as f:
+        return json.load(f)
+
+
+def mpi_runs(min_np: int = 1, cases=None) -> list:
+    """Keys of the MPI golden runs with np >= min_np (optionally of `cases`)."""
+    return sorted(k for k, r in golden_mpi()["runs"].items()
+                  if r["np"] >= min_np and (cases is None or r["case"] in cases))
+
+
+def mpi_golden_x(key: str) -> np.ndarray:
+    return np.load(os.path.join(GOLDEN, golden_mpi()["runs"][key]["x_file"]), allow_pickle=False)

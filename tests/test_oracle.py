@@ -7,7 +7,7 @@ import numpy as np
 import pytest
 
 import oracle
-from _cases import KATS, SPD_ALL, SPD_SMALL, case, golden_x
+from _cases import COMBINE_OF, KATS, SPD_ALL, SPD_SMALL, case, golden_mpi, golden_x, mpi_golden_x, mpi_runs
 
 
 def test_mt19937_matches_numpy():
@@ -96,6 +96,55 @@ def test_hash_generator_properties():
     assert A[3, 5] == 0.5 * (oracle.hash_u01(7, 3, 5) + oracle.hash_u01(7, 5, 3))
     A32, b32 = oracle.spd_hash(n, seed=7, dtype=np.float32)
     assert np.array_equal(A32, A.astype(np.float32)) and np.array_equal(b32, b.astype(np.float32))
+
+
+@pytest.mark.parametrize("key", mpi_runs())
+def test_f32ref_nparts_bit_exact_vs_mpi_reference(key):
+    """oracle_cg_f32ref(nparts=P) == the unmodified parallel_cg.c (combine
+    "mpich") / point-to-point_cg.c (combine "rank") under mpiexec -np P, bit
+    for bit, same loop count (tests/golden/mpi/)."""
+    r = golden_mpi()["runs"][key]
+    A, b, x0 = case(r["case"])
+    assert hashlib.sha256(A.tobytes()).hexdigest() == r["A_sha256"]
+    x, st = oracle.cg_f32ref(A, b, x0, eps=1e-6, nparts=r["np"], combine=COMBINE_OF[r["program"]])
+    assert st.iterations == r["ref_iterations"] and st.converged == 1
+    assert np.array_equal(x.view(np.uint32), mpi_golden_x(key).view(np.uint32))
+
+
+def test_mpi_goldens_discriminate_the_combine_order():
+    """The fixtures pin the order: at np >= 4 the two MPI programs differ, and
+    the wrong order misses the golden on most cases (np <= 2 the orders agree)."""
+    runs = golden_mpi()["runs"]
+    wrong = 0
+    for key in mpi_runs(min_np=4, cases=KATS + SPD_SMALL):
+        r = runs[key]
+        A, b, x0 = case(r["case"])
+        other = "rank" if COMBINE_OF[r["program"]] == "mpich" else "mpich"
+        x, st = oracle.cg_f32ref(A, b, x0, eps=1e-6, nparts=r["np"], combine=other)
+        wrong += not (st.iterations == r["ref_iterations"]
+                      and np.array_equal(x.view(np.uint32), mpi_golden_x(key).view(np.uint32)))
+    assert wrong >= 6
+    # np=1: both programs reduce to serialConjugate.c
+    g = {k: r for k, r in runs.items() if r["np"] == 1}
+    assert len(g) == 16
+    assert all(np.array_equal(mpi_golden_x(k), mpi_golden_x(k.replace("parallel_", "p2p_"))) for k in g
+               if k.startswith("parallel_"))
+
+
+def test_combine_orders():
+    parts = np.array([1e8, 1.0, -1e8, 1.0, 3.0, 0.5, 0.25, 7.0], np.float32)
+    seq = np.float32(0)
+    for q, v in enumerate(parts):
+        seq = v if q == 0 else np.float32(seq + v)
+    assert oracle.combine_f32(parts, "rank") == seq
+    t = lambda a, b: np.float32(a + b)  # noqa: E731
+    tree = t(t(t(parts[0], parts[1]), t(parts[2], parts[3])), t(t(parts[4], parts[5]), t(parts[6], parts[7])))
+    assert oracle.combine_f32(parts, "mpich") == tree
+    # non-power-of-two: first 2*rem pairs, then the tree (MPICH recursive doubling)
+    p6 = parts[:6]
+    assert oracle.combine_f32(p6, "mpich") == t(t(t(p6[0], p6[1]), t(p6[2], p6[3])), t(p6[4], p6[5]))
+    p3 = parts[:3]
+    assert oracle.combine_f32(p3, "mpich") == t(t(p3[0], p3[1]), p3[2])
 
 
 def test_nparts_dot_order():
