@@ -425,5 +425,20 @@ def main(argv=None) -> int:
     return 0
 
 
+def run() -> int:
+    """main(), failing fast: a libcgx error (in rank mode e.g. CGX_ERR_RCCL when
+    a peer died or ranks diverged, after CGX_RCCL_TIMEOUT_S at most) ends this
+    rank with a non-zero status and the message on stderr, so the launcher
+    stops the job instead of the other ranks waiting in a barrier."""
+    import conjugate_gradient_amd as cg
+    try:
+        return main()
+    except cg.CgxError as e:
+        rank = os.environ.get("RANK", "0")
+        print(f"bench.py rank {rank}: {e}", file=sys.stderr, flush=True)
+        sys.stdout.flush()
+        os._exit(3)  # skip interpreter / process-group teardown that could wait on dead peers
+
+
 if __name__ == "__main__":
-    sys.exit(main())
+    sys.exit(run())

@@ -110,6 +110,7 @@ def lib() -> ctypes.CDLL:
         "cgx_create": ([pctx, i64, i32, i32], i32),
         "cgx_create_multi": ([pctx, i64, i32, ctypes.POINTER(i32), i32], i32),
         "cgx_get_unique_id": ([ctypes.POINTER(UniqueId)], i32),
+        "cgx_rccl_available": ([], i32),
         "cgx_create_rank": ([pctx, i64, i32, i32, ctypes.POINTER(UniqueId), i32, i32], i32),
         "cgx_create_poisson": ([pctx, i64, i32, i32], i32),
         "cgx_create_poisson_multi": ([pctx, i64, i32, ctypes.POINTER(i32), i32], i32),
@@ -258,31 +259,62 @@ def _dt_flag(dtype) -> int:
     return CGX_F32_REF if np.dtype(dtype) == np.float32 else CGX_F64
 
 
+def _need(cond: bool, msg: str) -> None:
+    """Explicit size check before a C call (not `assert`: python -O strips it;
+    a short buffer passed on would be read or written past its end)."""
+    if not cond:
+        raise ValueError(msg)
+
+
+def _fits(arrs, n: int, what: str) -> None:
+    for a in arrs:
+        if a is not None:
+            _need(a.count >= n, f"{what}: device array of {a.count} elements, {n} needed")
+
+
 def matVec(A: DeviceArray, v: DeviceArray, out: DeviceArray, rows: int, cols: int, lda: int | None = None) -> None:
     """serialConjugate.c:109-120 / parallel_cg.c:172-184 (rows = local_row)."""
+    lda = lda or cols
+    _need(rows >= 0 and cols >= 0 and lda >= cols, "matVec: need rows, cols >= 0 and lda >= cols")
+    if rows and cols:
+        _fits([A], (rows - 1) * lda + cols, "matVec A")
+        _fits([v], cols, "matVec v")
+        _fits([out], rows, "matVec out")
     _check(lib().cgx_matvec(_dt_flag(A.dtype), A.ptr, lda or cols, rows, cols, v.ptr, out.ptr, None), "cgx_matvec")
 
 
 def vecVec(a: DeviceArray, b: DeviceArray, out: DeviceArray, n: int | None = None) -> None:
     """serialConjugate.c:145-155: out[0] = a . b (device scalar)."""
-    _check(lib().cgx_dot(_dt_flag(a.dtype), n if n is not None else a.count, a.ptr, b.ptr, out.ptr, None), "cgx_dot")
+    n = n if n is not None else a.count
+    _fits([a, b], n, "vecVec")
+    _fits([out], 1, "vecVec out")
+    _check(lib().cgx_dot(_dt_flag(a.dtype), n, a.ptr, b.ptr, out.ptr, None), "cgx_dot")
 
 
 def residual(b, Ax, r, p, rr=None, n=None) -> None:
     """serialConjugate.c:210-212: r = p = b - Ax; rr[0] = r . r."""
-    _check(lib().cgx_residual(_dt_flag(b.dtype), n if n is not None else b.count, b.ptr, Ax.ptr, r.ptr, p.ptr,
+    n = n if n is not None else b.count
+    _fits([b, Ax, r, p], n, "residual")
+    _fits([rr], 1, "residual rr")
+    _check(lib().cgx_residual(_dt_flag(b.dtype), n, b.ptr, Ax.ptr, r.ptr, p.ptr,
                               rr.ptr if rr is not None else None, None), "cgx_residual")
 
 
 def update_xr(x, r, p, Ap, rsold, pAp, rr, n=None) -> None:
     """serialConjugate.c:219-234: alpha = rsold/pAp; x += alpha p; r -= alpha Ap; rr = r.r."""
-    _check(lib().cgx_update_xr(_dt_flag(x.dtype), n if n is not None else x.count, x.ptr, r.ptr, p.ptr, Ap.ptr,
+    n = n if n is not None else x.count
+    _fits([x, r, p, Ap], n, "update_xr")
+    _fits([rsold, pAp, rr], 1, "update_xr scalars")
+    _check(lib().cgx_update_xr(_dt_flag(x.dtype), n, x.ptr, r.ptr, p.ptr, Ap.ptr,
                                rsold.ptr, pAp.ptr, rr.ptr, None), "cgx_update_xr")
 
 
 def update_p(p, r, rr, rsold, n=None) -> None:
     """serialConjugate.c:239-243: p = r + (rr/rsold) p."""
-    _check(lib().cgx_update_p(_dt_flag(p.dtype), n if n is not None else p.count, p.ptr, r.ptr, rr.ptr, rsold.ptr,
+    n = n if n is not None else p.count
+    _fits([p, r], n, "update_p")
+    _fits([rr, rsold], 1, "update_p scalars")
+    _check(lib().cgx_update_p(_dt_flag(p.dtype), n, p.ptr, r.ptr, rr.ptr, rsold.ptr,
                               None), "cgx_update_p")
 
 
@@ -332,15 +364,24 @@ class Solver:
 
     # lifetime
     def close(self) -> None:
+        """cgx_destroy.  In rank mode it first drains the streams with the RCCL
+        deadline; an error there (a peer died) is raised after the free."""
         if getattr(self, "_h", None):
-            lib().cgx_destroy(self._h)
+            rc = lib().cgx_destroy(self._h)
             self._h = None
+            _check(rc, "cgx_destroy")
 
     def __enter__(self):
         return self
 
-    def __exit__(self, *exc):
-        self.close()
+    def __exit__(self, exc_type, *exc):
+        if exc_type is None:
+            self.close()
+        else:  # keep the original error; the free still happens
+            try:
+                self.close()
+            except CgxError:
+                pass
 
     def __del__(self):
         try:
@@ -359,12 +400,23 @@ class Solver:
         A = np.ascontiguousarray(A, self.dtype)
         b = np.ascontiguousarray(b, self.dtype)
         x0 = np.zeros(self.n, self.dtype) if x0 is None else np.ascontiguousarray(x0, self.dtype)
-        assert A.shape == (self.n, self.n) and b.shape == (self.n,) and x0.shape == (self.n,)
+        _need(A.shape == (self.n, self.n), f"set_system: A has shape {A.shape}, ({self.n}, {self.n}) needed")
+        _need(b.shape == (self.n,), f"set_system: b has shape {b.shape}, ({self.n},) needed")
+        _need(x0.shape == (self.n,), f"set_system: x0 has shape {x0.shape}, ({self.n},) needed")
         _check(lib().cgx_set_system(self._h, _ptr(A), _ptr(b), _ptr(x0)), "cgx_set_system")
 
     def set_rows(self, row0: int, A_rows=None, b_rows=None, x_rows=None) -> None:
         arrs = [None if a is None else np.ascontiguousarray(a, self.dtype) for a in (A_rows, b_rows, x_rows)]
+        _need(any(a is not None for a in arrs), "set_rows: nothing to set")
         nrows = next(a.shape[0] for a in arrs if a is not None)
+        if arrs[0] is not None:
+            _need(arrs[0].ndim == 2 and arrs[0].shape[1] >= self.n,
+                  f"set_rows: A_rows has shape {arrs[0].shape}, (nrows, >= {self.n}) needed")
+        for a, name in zip(arrs, ("A_rows", "b_rows", "x_rows")):
+            if a is not None:
+                _need(a.shape[0] == nrows and (a.ndim == 2 if name == "A_rows" else a.ndim == 1),
+                      f"set_rows: {name} has shape {a.shape}; every argument needs the same {nrows} rows")
+        _need(0 <= row0 and row0 + nrows <= self.n, f"set_rows: rows [{row0}, {row0 + nrows}) outside [0, {self.n})")
         lda = arrs[0].shape[1] if arrs[0] is not None else self.n
         _check(lib().cgx_set_rows(self._h, row0, nrows, *(None if a is None else _ptr(a) for a in arrs[:1]), lda,
                                   *(None if a is None else _ptr(a) for a in arrs[1:])), "cgx_set_rows")
@@ -382,6 +434,7 @@ class Solver:
 
     def set_x(self, x: np.ndarray) -> None:
         x = np.ascontiguousarray(x, self.dtype)
+        _need(x.shape == (self.n,), f"set_x: x has shape {x.shape}, ({self.n},) needed")
         _check(lib().cgx_set_x(self._h, _ptr(x)), "cgx_set_x")
 
     # solve
@@ -389,6 +442,7 @@ class Solver:
         st = Stats()
         if x0 is not None:
             x = np.array(x0, dtype=self.dtype, copy=True)
+            _need(x.shape == (self.n,), f"solve: x0 has shape {x.shape}, ({self.n},) needed")
             _check(lib().cgx_solve(self._h, _ptr(x), eps, max_iter, ctypes.byref(st)), "cgx_solve")
         else:
             _check(lib().cgx_solve(self._h, None, eps, max_iter, ctypes.byref(st)), "cgx_solve")

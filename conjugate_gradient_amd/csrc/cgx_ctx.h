@@ -20,10 +20,14 @@
 // device scalar block.  Three exchange modes:
 //   SINGLE  one shard, no exchange.
 //   LOCAL   several shards in this process (distinct or repeated devices);
-//           allgather by device-to-device copies, scalars combined as
-//           partials summed in rank order (point-to-point_cg.c allSum order).
+//           allgather by device-to-device copies, scalars combined from the
+//           gathered partials in a fixed order (fp64: rank order; F32_REF:
+//           MPICH's MPI_Allreduce order, parallel_cg.c).
 //   RCCL    one shard per process (torchrun / mpirun style), RCCL allgather
-//           of p and allreduce of the scalars over xGMI on the shard stream.
+//           of p and allreduce of the scalars over xGMI on the shard stream
+//           (F32_REF: allgather of the partials + the MPICH-order combine).
+// CGX_COMM_P2P (either multi-shard mode) follows point-to-point_cg.c instead:
+// gather to rank 0 and send back, scalars summed in rank order (allSum).
 //
 // Scalar slots (8 bytes each; F32_REF stores a float at the slot start):
 //   RR(j)   = r_j.r_j (global)      PAP(k) = p_k.Ap_k (global)   ring of 4
@@ -70,6 +74,10 @@ struct RcclApi {
     decltype(&::ncclRecv) Recv = nullptr;
     decltype(&::ncclGroupStart) GroupStart = nullptr;
     decltype(&::ncclGroupEnd) GroupEnd = nullptr;
+    // fail-fast: nonblocking init, asynchronous error query, abort
+    decltype(&::ncclCommInitRankConfig) CommInitRankConfig = nullptr;
+    decltype(&::ncclCommGetAsyncError) CommGetAsyncError = nullptr;
+    decltype(&::ncclCommAbort) CommAbort = nullptr;
 };
 extern RcclApi g_rccl;
 // Loads librccl.so.1 once; false (with cgx_last_error set) if it cannot.
@@ -88,6 +96,9 @@ bool rccl_load();
 #define ncclRecv (cgxh::g_rccl.Recv)
 #define ncclGroupStart (cgxh::g_rccl.GroupStart)
 #define ncclGroupEnd (cgxh::g_rccl.GroupEnd)
+#define ncclCommInitRankConfig (cgxh::g_rccl.CommInitRankConfig)
+#define ncclCommGetAsyncError (cgxh::g_rccl.CommGetAsyncError)
+#define ncclCommAbort (cgxh::g_rccl.CommAbort)
 #endif
 
 #define HIPT(expr)                                                                              \
@@ -104,6 +115,17 @@ bool rccl_load();
         if (e_ != ncclSuccess)                                                                    \
             return fail(CGX_ERR_RCCL, "%s: %s (%s:%d)", #expr, ncclGetErrorString(e_), __FILE__, \
                         __LINE__);                                                                \
+    } while (0)
+
+// An RCCL call on the context's communicator (rank mode): `what` names the
+// exchange for the error message; a call that returns ncclInProgress (the
+// communicator is nonblocking) is waited for with the context's deadline; a
+// context whose communicator was aborted refuses further RCCL calls.
+#define NCCLC(c, expr, what)                                                            \
+    do {                                                                                \
+        if ((c)->dead) return dead_error(c);                                            \
+        ncclResult_t e_ = (expr);                                                       \
+        TRY(rccl_after(c, e_, what, #expr, __FILE__, __LINE__));                         \
     } while (0)
 
 #define TRY(expr)                          \
@@ -210,6 +232,17 @@ struct cgx_ctx {
     // iterations captured once, the period of the scalar rings
     hipGraphExec_t graph = nullptr;
     bool graph_failed = false;
+    // rank mode fail-fast (cgx_exchange.hip, rank_wait_*): every host wait
+    // polls with a deadline of rccl_timeout_s seconds (CGX_RCCL_TIMEOUT_S,
+    // default 60, 0 = wait forever) and checks the communicator's asynchronous
+    // error; on either the communicator is aborted (ncclCommAbort, which also
+    // stops RCCL kernels still waiting on a peer) and the call returns
+    // CGX_ERR_RCCL.  `dead` then refuses every later RCCL call.
+    double rccl_timeout_s = 60.0;
+    bool dead = false;
+    char dead_why[400] = "";
+    const char *last_coll = "none";  // the last exchange enqueued, and its iteration
+    int64_t last_coll_k = -1;
 };
 
 namespace cgxh {
@@ -261,6 +294,12 @@ int overlapped_matvec(cgx_ctx *c, int dot_slot, bool gated);
 int exchange_halo_async(cgx_ctx *c);
 int settle_halo(cgx_ctx *c);
 int sync_all(cgx_ctx *c);
+// rank-mode fail-fast (plain blocking waits in the other modes)
+int rccl_after(cgx_ctx *c, ncclResult_t r, const char *what, const char *expr, const char *file, int line);
+int dead_error(const cgx_ctx *c);
+int rank_wait_event(cgx_ctx *c, hipEvent_t ev, const char *what);
+int rank_wait_stream(cgx_ctx *c, hipStream_t st, const char *what);
+double rccl_timeout_from_env();
 // cgx_iterate.hip
 int matvec_rows(cgx_ctx *c, Shard &s, const MatvecPlan &pl, const char *Arows, int64_t r0, int64_t rows,
                 const char *vec, bool fuse_dot, int dot_slot, bool gated = false);

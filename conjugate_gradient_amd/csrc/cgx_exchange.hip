@@ -4,9 +4,21 @@
 //   point-to-point_cg.c:239-256,339-394 (CGX_COMM_P2P) -> p2p_allgather / p2p_scalar
 // in RCCL rank mode, by device copies in multi-shard mode; the overlap of
 // p's exchange with the own-column-block matVec; the Poisson halo rows.
+#include <thread>
+
 #include "cgx_ctx.h"
 
 namespace cgxh {
+
+// Names of the exchanges in rank-mode error messages (NCCLC).
+constexpr const char *kWhatHalo = "the Poisson halo exchange";
+constexpr const char *kWhatP2P = "the p2p gather + send of p (allGather, BcastVector)";
+constexpr const char *kWhatHaloAsync = "the overlapped r halo exchange";
+static const char *scalar_name(int gslot) {
+    if (gslot >= S_PAP && gslot < S_PAP + 4) return "the p.Ap combine";
+    if (gslot >= S_RR && gslot < S_RR + 4) return "the r.r combine";
+    return "the true-residual combine";
+}
 
 // ---- timing -------------------------------------------------------------------
 int timing_resolve(cgx_ctx *c) {
@@ -15,7 +27,7 @@ int timing_resolve(cgx_ctx *c) {
     TRY(set_dev(s));
     for (int i = 0; i < s.ev_used; ++i) {
         float ms = 0.f;
-        HIPT(hipEventSynchronize(s.ev_t[2 * i + 1]));
+        TRY(rank_wait_event(c, s.ev_t[2 * i + 1], "a timed matVec"));
         HIPT(hipEventElapsedTime(&ms, s.ev_t[2 * i], s.ev_t[2 * i + 1]));
         c->matvec_ms += ms;
         c->matvec_count += 1;
@@ -65,16 +77,17 @@ int exchange_halo_of(cgx_ctx *c, char *Shard::*slab) {
         TRY(set_dev(s));
         const int g = s.index;
         char *base = s.*slab, *own = base + row;
-        NCCLT(ncclGroupStart());
+        NCCLC(c, ncclGroupStart(), kWhatHalo);
         if (g > 0) {
-            NCCLT(ncclSend(own, (size_t)c->m, ncclDouble, g - 1, s.comm, s.stream));
-            NCCLT(ncclRecv(base, (size_t)c->m, ncclDouble, g - 1, s.comm, s.stream));
+            NCCLC(c, ncclSend(own, (size_t)c->m, ncclDouble, g - 1, s.comm, s.stream), kWhatHalo);
+            NCCLC(c, ncclRecv(base, (size_t)c->m, ncclDouble, g - 1, s.comm, s.stream), kWhatHalo);
         }
         if (g < c->nranks - 1) {
-            NCCLT(ncclSend(own + (size_t)(mloc - 1) * row, (size_t)c->m, ncclDouble, g + 1, s.comm, s.stream));
-            NCCLT(ncclRecv(own + (size_t)mloc * row, (size_t)c->m, ncclDouble, g + 1, s.comm, s.stream));
+            NCCLC(c, ncclSend(own + (size_t)(mloc - 1) * row, (size_t)c->m, ncclDouble, g + 1, s.comm, s.stream),
+                  kWhatHalo);
+            NCCLC(c, ncclRecv(own + (size_t)mloc * row, (size_t)c->m, ncclDouble, g + 1, s.comm, s.stream), kWhatHalo);
         }
-        NCCLT(ncclGroupEnd());
+        NCCLC(c, ncclGroupEnd(), kWhatHalo);
         return CGX_OK;
     }
     TRY(local_barrier(c));
@@ -107,21 +120,22 @@ int p2p_allgather(cgx_ctx *c, bool from_x) {
         const int P = c->nranks;
         if (s.index == 0 && from_x)
             HIPT(hipMemcpyAsync(s.pown, s.x, s.nloc * es, hipMemcpyDeviceToDevice, s.stream));
-        NCCLT(ncclGroupStart());
+        NCCLC(c, ncclGroupStart(), kWhatP2P);
         if (s.index != 0) {
-            NCCLT(ncclSend(from_x ? (const void *)s.x : (const void *)s.pown, (size_t)s.nloc, t, 0, s.comm, s.stream));
+            const void *src = from_x ? (const void *)s.x : (const void *)s.pown;
+            NCCLC(c, ncclSend(src, (size_t)s.nloc, t, 0, s.comm, s.stream), kWhatP2P);
         } else {
             for (int q = 1; q < P; ++q)
-                NCCLT(ncclRecv(s.pfull + (size_t)q * s.nloc * es, (size_t)s.nloc, t, q, s.comm, s.stream));
+                NCCLC(c, ncclRecv(s.pfull + (size_t)q * s.nloc * es, (size_t)s.nloc, t, q, s.comm, s.stream), kWhatP2P);
         }
-        NCCLT(ncclGroupEnd());
-        NCCLT(ncclGroupStart());
+        NCCLC(c, ncclGroupEnd(), kWhatP2P);
+        NCCLC(c, ncclGroupStart(), kWhatP2P);
         if (s.index == 0) {
-            for (int q = 1; q < P; ++q) NCCLT(ncclSend(s.pfull, (size_t)c->n, t, q, s.comm, s.stream));
+            for (int q = 1; q < P; ++q) NCCLC(c, ncclSend(s.pfull, (size_t)c->n, t, q, s.comm, s.stream), kWhatP2P);
         } else {
-            NCCLT(ncclRecv(s.pfull, (size_t)c->n, t, 0, s.comm, s.stream));
+            NCCLC(c, ncclRecv(s.pfull, (size_t)c->n, t, 0, s.comm, s.stream), kWhatP2P);
         }
-        NCCLT(ncclGroupEnd());
+        NCCLC(c, ncclGroupEnd(), kWhatP2P);
         return CGX_OK;
     }
     TRY(local_barrier(c));
@@ -144,33 +158,35 @@ int p2p_allgather(cgx_ctx *c, bool from_x) {
 // allSum (point-to-point_cg.c:339-359): partials to rank 0, summed there in
 // rank order, the sum sent back to every rank (BcastVector(&s, 1)).
 int p2p_scalar(cgx_ctx *c, int lslot, int gslot) {
+    const char *what = scalar_name(gslot);
     if (c->mode == M_RCCL) {
         Shard &s = c->sh[0];
         TRY(set_dev(s));
         const int P = c->nranks;
         if (s.index == 0) HIPT(hipMemcpyAsync(slot(s, S_GATHER), slot(s, lslot), 8, hipMemcpyDeviceToDevice, s.stream));
-        NCCLT(ncclGroupStart());
+        NCCLC(c, ncclGroupStart(), what);
         if (s.index != 0) {
-            NCCLT(ncclSend(slot(s, lslot), 1, ncclUint64, 0, s.comm, s.stream));
+            NCCLC(c, ncclSend(slot(s, lslot), 1, ncclUint64, 0, s.comm, s.stream), what);
         } else {
-            for (int q = 1; q < P; ++q) NCCLT(ncclRecv(slot(s, S_GATHER + q), 1, ncclUint64, q, s.comm, s.stream));
+            for (int q = 1; q < P; ++q) NCCLC(c, ncclRecv(slot(s, S_GATHER + q), 1, ncclUint64, q, s.comm, s.stream),
+                                              what);
         }
-        NCCLT(ncclGroupEnd());
+        NCCLC(c, ncclGroupEnd(), what);
         if (s.index == 0) {
             if (f32ref(c))
                 HIPT(sum_ordered_f32(reinterpret_cast<const float *>(slot(s, S_GATHER)), P,
-                                     reinterpret_cast<float *>(slot(s, gslot)), s.stream));
+                                     reinterpret_cast<float *>(slot(s, gslot)), s.stream, false));
             else
                 HIPT(sum_ordered_f64(reinterpret_cast<const double *>(slot(s, S_GATHER)), P,
                                      reinterpret_cast<double *>(slot(s, gslot)), s.stream));
         }
-        NCCLT(ncclGroupStart());
+        NCCLC(c, ncclGroupStart(), what);
         if (s.index == 0) {
-            for (int q = 1; q < P; ++q) NCCLT(ncclSend(slot(s, gslot), 1, ncclUint64, q, s.comm, s.stream));
+            for (int q = 1; q < P; ++q) NCCLC(c, ncclSend(slot(s, gslot), 1, ncclUint64, q, s.comm, s.stream), what);
         } else {
-            NCCLT(ncclRecv(slot(s, gslot), 1, ncclUint64, 0, s.comm, s.stream));
+            NCCLC(c, ncclRecv(slot(s, gslot), 1, ncclUint64, 0, s.comm, s.stream), what);
         }
-        NCCLT(ncclGroupEnd());
+        NCCLC(c, ncclGroupEnd(), what);
         return CGX_OK;
     }
     TRY(local_barrier(c));
@@ -181,7 +197,7 @@ int p2p_scalar(cgx_ctx *c, int lslot, int gslot) {
         HIPT(hipMemcpyPeerAsync(slot(r0, S_GATHER + s.index), r0.dev, slot(s, lslot), s.dev, 8, r0.stream));
     if (f32ref(c))
         HIPT(sum_ordered_f32(reinterpret_cast<const float *>(slot(r0, S_GATHER)), S,
-                             reinterpret_cast<float *>(slot(r0, gslot)), r0.stream));
+                             reinterpret_cast<float *>(slot(r0, gslot)), r0.stream, false));
     else
         HIPT(sum_ordered_f64(reinterpret_cast<const double *>(slot(r0, S_GATHER)), S,
                              reinterpret_cast<double *>(slot(r0, gslot)), r0.stream));
@@ -214,7 +230,8 @@ int exchange_allgather(cgx_ctx *c, bool from_x) {
         TRY(set_dev(s));
         const ncclDataType_t t = f32ref(c) ? ncclFloat : ncclDouble;
         const void *send = from_x ? (const void *)s.x : (const void *)s.pown;
-        NCCLT(ncclAllGather(send, s.pfull, (size_t)s.nloc, t, s.comm, s.stream));
+        NCCLC(c, ncclAllGather(send, s.pfull, (size_t)s.nloc, t, s.comm, s.stream),
+              from_x ? "ncclAllGather(x)" : "ncclAllGather(p)");
         return CGX_OK;
     }
     // LOCAL: device-to-device copies after all producers are done.
@@ -236,22 +253,24 @@ int exchange_scalar(cgx_ctx *c, int lslot, int gslot) {
     if (c->mode == M_SINGLE) return CGX_OK;  // kernels wrote the global slot directly
     if (p2p(c)) return p2p_scalar(c, lslot, gslot);
     const int S = (int)c->sh.size();
+    const char *what = scalar_name(gslot);
     if (c->mode == M_RCCL) {
         Shard &s = c->sh[0];
         TRY(set_dev(s));
         if (f32ref(c)) {
-            // point-to-point_cg.c allSum order: gather the partials, sum in rank order
-            NCCLT(ncclAllGather(slot(s, lslot), slot(s, S_GATHER), 1, ncclUint64, s.comm, s.stream));
+            // parallel_cg.c's MPI_Allreduce, bit for bit: gather the partials and
+            // combine them in MPICH's recursive-doubling order on every rank
+            NCCLC(c, ncclAllGather(slot(s, lslot), slot(s, S_GATHER), 1, ncclUint64, s.comm, s.stream), what);
             HIPT(sum_ordered_f32(reinterpret_cast<const float *>(slot(s, S_GATHER)), c->nranks,
-                                 reinterpret_cast<float *>(slot(s, gslot)), s.stream));
+                                 reinterpret_cast<float *>(slot(s, gslot)), s.stream, true));
         } else if (c->flags & CGX_DETERMINISTIC) {
             // fp64, rank-order sum: the same bits as the multi-shard mode with the
             // same partition, whatever algorithm RCCL would pick for an allreduce
-            NCCLT(ncclAllGather(slot(s, lslot), slot(s, S_GATHER), 1, ncclUint64, s.comm, s.stream));
+            NCCLC(c, ncclAllGather(slot(s, lslot), slot(s, S_GATHER), 1, ncclUint64, s.comm, s.stream), what);
             HIPT(sum_ordered_f64(reinterpret_cast<const double *>(slot(s, S_GATHER)), c->nranks,
                                  reinterpret_cast<double *>(slot(s, gslot)), s.stream));
         } else {
-            NCCLT(ncclAllReduce(slot(s, lslot), slot(s, gslot), 1, ncclDouble, ncclSum, s.comm, s.stream));
+            NCCLC(c, ncclAllReduce(slot(s, lslot), slot(s, gslot), 1, ncclDouble, ncclSum, s.comm, s.stream), what);
         }
         return CGX_OK;
     }
@@ -260,9 +279,9 @@ int exchange_scalar(cgx_ctx *c, int lslot, int gslot) {
         TRY(set_dev(d));
         for (auto &s : c->sh)
             HIPT(hipMemcpyPeerAsync(slot(d, S_GATHER + s.index), d.dev, slot(s, lslot), s.dev, 8, d.stream));
-        if (f32ref(c))
+        if (f32ref(c))  // parallel_cg.c's MPI_Allreduce order (MPICH), as in rank mode
             HIPT(sum_ordered_f32(reinterpret_cast<const float *>(slot(d, S_GATHER)), S,
-                                 reinterpret_cast<float *>(slot(d, gslot)), d.stream));
+                                 reinterpret_cast<float *>(slot(d, gslot)), d.stream, true));
         else
             HIPT(sum_ordered_f64(reinterpret_cast<const double *>(slot(d, S_GATHER)), S,
                                  reinterpret_cast<double *>(slot(d, gslot)), d.stream));
@@ -286,7 +305,8 @@ int overlapped_matvec(cgx_ctx *c, int dot_slot, bool gated) {
     if (c->mode == M_RCCL) {
         Shard &s = c->sh[0];
         HIPT(hipStreamWaitEvent(s.cstream, s.ev_pready, 0));
-        NCCLT(ncclAllGather(s.pown, s.pfull, (size_t)s.nloc, ncclDouble, s.comm, s.cstream));
+        NCCLC(c, ncclAllGather(s.pown, s.pfull, (size_t)s.nloc, ncclDouble, s.comm, s.cstream),
+              "ncclAllGather(p), overlapped");
         HIPT(hipEventRecord(s.ev_gathered, s.cstream));
     } else {
         for (auto &d : c->sh) {
@@ -337,16 +357,18 @@ int exchange_halo_async(cgx_ctx *c) {
         const int g = s.index;
         char *base = s.rh, *own = base + row;
         HIPT(hipStreamWaitEvent(s.cstream, s.ev_pready, 0));
-        NCCLT(ncclGroupStart());
+        NCCLC(c, ncclGroupStart(), kWhatHaloAsync);
         if (g > 0) {
-            NCCLT(ncclSend(own, (size_t)c->m, ncclDouble, g - 1, s.comm, s.cstream));
-            NCCLT(ncclRecv(base, (size_t)c->m, ncclDouble, g - 1, s.comm, s.cstream));
+            NCCLC(c, ncclSend(own, (size_t)c->m, ncclDouble, g - 1, s.comm, s.cstream), kWhatHaloAsync);
+            NCCLC(c, ncclRecv(base, (size_t)c->m, ncclDouble, g - 1, s.comm, s.cstream), kWhatHaloAsync);
         }
         if (g < c->nranks - 1) {
-            NCCLT(ncclSend(own + (size_t)(mloc - 1) * row, (size_t)c->m, ncclDouble, g + 1, s.comm, s.cstream));
-            NCCLT(ncclRecv(own + (size_t)mloc * row, (size_t)c->m, ncclDouble, g + 1, s.comm, s.cstream));
+            NCCLC(c, ncclSend(own + (size_t)(mloc - 1) * row, (size_t)c->m, ncclDouble, g + 1, s.comm, s.cstream),
+                  kWhatHaloAsync);
+            NCCLC(c, ncclRecv(own + (size_t)mloc * row, (size_t)c->m, ncclDouble, g + 1, s.comm, s.cstream),
+                  kWhatHaloAsync);
         }
-        NCCLT(ncclGroupEnd());
+        NCCLC(c, ncclGroupEnd(), kWhatHaloAsync);
         HIPT(hipEventRecord(s.ev_gathered, s.cstream));
     } else {
         const int S = (int)c->sh.size();
@@ -384,11 +406,122 @@ int settle_halo(cgx_ctx *c) {
 int sync_all(cgx_ctx *c) {
     for (auto &s : c->sh) {
         TRY(set_dev(s));
-        HIPT(hipStreamSynchronize(s.stream));
+        TRY(rank_wait_stream(c, s.stream, "the compute stream"));
         for (int q = 0; q < s.ncopy; ++q) HIPT(hipStreamSynchronize(s.copy[q]));
-        if (s.cstream) HIPT(hipStreamSynchronize(s.cstream));
+        if (s.cstream) TRY(rank_wait_stream(c, s.cstream, "the exchange stream"));
     }
     return timing_resolve(c);
+}
+
+// ---- rank-mode fail-fast ---------------------------------------------------------
+// The reference stops the whole job on a failure (MPI_Abort, parallel_cg.c:79,
+// 89,94,143).  RCCL has no such global stop: a rank that died or issued a
+// different collective leaves its peers' RCCL kernels waiting forever, and a
+// plain hipStreamSynchronize with them.  So in rank mode every host wait polls
+// with a deadline and watches the communicator's asynchronous error; on either
+// the communicator is aborted (its kernels see the abort flag and exit, the
+// stream drains) and the call returns CGX_ERR_RCCL naming the exchange and the
+// iteration.  The other modes keep plain blocking waits.
+double rccl_timeout_from_env() {
+    const char *e = std::getenv("CGX_RCCL_TIMEOUT_S");
+    if (!e || !*e) return 60.0;
+    const double v = std::atof(e);
+    return v > 0.0 ? v : 0.0;
+}
+
+int dead_error(const cgx_ctx *c) {
+    return fail(CGX_ERR_RCCL, "rank %d of %d: the RCCL communicator was aborted earlier (%s)", c->sh[0].index,
+                c->nranks, c->dead_why);
+}
+
+static int rccl_abort(cgx_ctx *c, const char *fmt, ...) {
+    Shard &s = c->sh[0];
+    char why[320];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(why, sizeof why, fmt, ap);
+    va_end(ap);
+    snprintf(c->dead_why, sizeof c->dead_why, "%s; last exchange enqueued: %s at iteration %lld", why, c->last_coll,
+             (long long)c->last_coll_k);
+    c->dead = true;
+    if (s.comm) {
+        (void)ncclCommAbort(s.comm);  // RCCL kernels still waiting on a peer exit
+        s.comm = nullptr;
+    }
+    return fail(CGX_ERR_RCCL, "rank %d of %d: %s", s.index, c->nranks, c->dead_why);
+}
+
+static double now_s() {
+    return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
+}
+
+// Poll `ready` (a hipEventQuery / hipStreamQuery) until it reports success,
+// checking the communicator and the deadline in between.
+template <typename F>
+static int rank_poll(cgx_ctx *c, F ready, const char *what) {
+    const double t0 = now_s();
+    for (long spins = 0;; ++spins) {
+        const hipError_t e = ready();
+        if (e == hipSuccess) return CGX_OK;
+        if (e != hipErrorNotReady)
+            return fail(CGX_ERR_HIP, "waiting for %s: %s", what, hipGetErrorString(e));
+        if (spins < 2048) continue;  // the common case: done within microseconds
+        ncclResult_t ar = ncclSuccess;
+        if (c->sh[0].comm && ncclCommGetAsyncError(c->sh[0].comm, &ar) == ncclSuccess && ar != ncclSuccess &&
+            ar != ncclInProgress)
+            return rccl_abort(c, "RCCL reported '%s' while waiting for %s", ncclGetErrorString(ar), what);
+        if (c->rccl_timeout_s > 0.0 && now_s() - t0 > c->rccl_timeout_s)
+            return rccl_abort(c, "no progress for %.0f s waiting for %s (a rank died, or ranks issued different "
+                                 "collectives; CGX_RCCL_TIMEOUT_S sets the limit)",
+                              c->rccl_timeout_s, what);
+        std::this_thread::sleep_for(std::chrono::microseconds(spins < 20000 ? 20 : 200));
+    }
+}
+
+int rank_wait_event(cgx_ctx *c, hipEvent_t ev, const char *what) {
+    if (c->mode != M_RCCL || c->rccl_timeout_s <= 0.0) {
+        HIPT(hipEventSynchronize(ev));
+        return CGX_OK;
+    }
+    if (c->dead) return dead_error(c);
+    return rank_poll(c, [ev] { return hipEventQuery(ev); }, what);
+}
+
+int rank_wait_stream(cgx_ctx *c, hipStream_t st, const char *what) {
+    if (c->mode != M_RCCL || c->rccl_timeout_s <= 0.0 || c->dead) {
+        // a dead context's streams drain once the abort has stopped RCCL's kernels
+        HIPT(hipStreamSynchronize(st));
+        return CGX_OK;
+    }
+    return rank_poll(c, [st] { return hipStreamQuery(st); }, what);
+}
+
+// After an RCCL call (NCCLC): ncclInProgress from the nonblocking communicator
+// means the enqueue finishes asynchronously; poll its state with the deadline.
+int rccl_after(cgx_ctx *c, ncclResult_t r, const char *what, const char *expr, const char *file, int line) {
+    c->last_coll = what;
+    c->last_coll_k = c->k;
+    if (r == ncclInProgress) {
+        const double t0 = now_s();
+        Shard &s = c->sh[0];
+        for (;;) {
+            ncclResult_t st = ncclSuccess;
+            const ncclResult_t q = ncclCommGetAsyncError(s.comm, &st);
+            if (q != ncclSuccess) {
+                r = q;
+                break;
+            }
+            if (st != ncclInProgress) {
+                r = st;
+                break;
+            }
+            if (c->rccl_timeout_s > 0.0 && now_s() - t0 > c->rccl_timeout_s)
+                return rccl_abort(c, "%s did not finish enqueueing within %.0f s", what, c->rccl_timeout_s);
+            std::this_thread::yield();
+        }
+    }
+    if (r == ncclSuccess) return CGX_OK;
+    return rccl_abort(c, "%s: %s (%s:%d)", expr, ncclGetErrorString(r), file, line);
 }
 
 }  // namespace cgxh

@@ -139,9 +139,10 @@ int x0_is_zero(cgx_ctx *c, bool *zero) {
     int64_t *pin = reinterpret_cast<int64_t *>(s.h_pin);
     pin[0] = local ? 0 : 1;
     HIPT(hipMemcpyAsync(slot(s, S_XNZ), pin, 8, hipMemcpyHostToDevice, s.stream));
-    NCCLT(ncclAllReduce(slot(s, S_XNZ), slot(s, S_XNZ), 1, ncclInt64, ncclSum, s.comm, s.stream));
+    NCCLC(c, ncclAllReduce(slot(s, S_XNZ), slot(s, S_XNZ), 1, ncclInt64, ncclSum, s.comm, s.stream),
+          "ncclAllReduce(x0 != 0 count)");
     HIPT(hipMemcpyAsync(pin, slot(s, S_XNZ), 8, hipMemcpyDeviceToHost, s.stream));
-    HIPT(hipStreamSynchronize(s.stream));
+    TRY(rank_wait_stream(c, s.stream, "the x0 check"));
     *zero = pin[0] == 0;
     return CGX_OK;
 }
@@ -194,7 +195,7 @@ int read_scalar(cgx_ctx *c, int gslot, double *out) {
     Shard &s = c->sh[0];
     TRY(set_dev(s));
     HIPT(hipMemcpyAsync(s.h_pin, slot(s, gslot), 8, hipMemcpyDeviceToHost, s.stream));
-    HIPT(hipStreamSynchronize(s.stream));
+    TRY(rank_wait_stream(c, s.stream, "a scalar read-back"));
     if (f32ref(c)) {
         float f;
         std::memcpy(&f, s.h_pin, 4);
@@ -436,7 +437,7 @@ static int iterate_gated(cgx_ctx *c, int64_t count, double eps, int64_t *done, i
         const int q = (int)(issued % kLookRing);
         HIPT(hipEventRecord(s0.ev_look[q], s0.stream));
         if (issued >= look) {
-            HIPT(hipEventSynchronize(s0.ev_look[(issued - look) % kLookRing]));
+            TRY(rank_wait_event(c, s0.ev_look[(issued - look) % kLookRing], "an earlier iteration"));
             // Only a record left by an iteration the event covers counts: the
             // host-mapped word may already show a later iteration's decision,
             // and acting on that would make the number of enqueued iterations

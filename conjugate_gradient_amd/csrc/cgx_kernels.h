@@ -12,6 +12,8 @@ struct RedWs {
     unsigned *tickets;     // kTickets counters, zero at rest
 };
 constexpr int kMaxRedBlocks = 8192;
+// Most partials a scalar combine takes (>= kMaxShards, the rank limit).
+constexpr int kMaxCombine = 64;
 constexpr int kTickets = 8;
 enum Ticket { T_MATVEC = 0, T_RESID = 1, T_XR = 2, T_DOT = 3 };
 
@@ -132,7 +134,8 @@ hipError_t update_p_ref_f32(int64_t n, float *p, const float *r, const float *rr
                             const float *rsold, hipStream_t s);
 hipError_t gen_spd_f32(int64_t n, int64_t lda, int64_t row0, int64_t nrows, uint64_t seed,
                        float *A, float *b, hipStream_t s);
-hipError_t sum_ordered_f32(const float *in, int cnt, float *out, hipStream_t s);
+// F32_REF combine: rank order (allSum) or, with mpich, MPICH's MPI_Allreduce order.
+hipError_t sum_ordered_f32(const float *in, int cnt, float *out, hipStream_t s, bool mpich);
 
 // Each kernel file is its own code object, which HIP loads on a device at
 // the first use of one of its kernels.  preload_kernels() loads the ones a

@@ -3,9 +3,12 @@
 // library made every process's HIP start-up ~25-35 ms longer (its device
 // code registers with the runtime; profiles/r01_hip_init_rccl.txt), so
 // single-GPU and multi-shard use, the CLI included, never load it.  If the
-// process already has librccl.so.1 (torch's), dlopen returns that one.
+// process already has librccl.so.1 (torch's), dlopen returns that one.  The
+// load is attempted once per process: a failure is permanent (every later
+// rank-mode call returns CGX_ERR_RCCL with the same reason).
 #include <dlfcn.h>
 
+#include <cstdlib>
 #include <mutex>
 #include <type_traits>
 
@@ -21,8 +24,19 @@ bool rccl_load() {
     static bool ok = false;
     static char why[512] = "";
     std::call_once(once, [] {
-        void *h = dlopen("librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
-        if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_GLOBAL);
+        // soname first (the one torch already mapped, if any), then
+        // $ROCM_PATH/lib, then the image's /opt/rocm.  RTLD_LOCAL: every symbol
+        // is taken through this handle, and a later torch import must not bind
+        // to it by accident.
+        void *h = dlopen("librccl.so.1", RTLD_NOW | RTLD_LOCAL);
+        if (!h) {
+            if (const char *rp = std::getenv("ROCM_PATH")) {
+                char path[1024];
+                snprintf(path, sizeof path, "%s/lib/librccl.so.1", rp);
+                h = dlopen(path, RTLD_NOW | RTLD_LOCAL);
+            }
+        }
+        if (!h) h = dlopen("/opt/rocm/lib/librccl.so.1", RTLD_NOW | RTLD_LOCAL);
         if (!h) {
             const char *e = dlerror();
             snprintf(why, sizeof why, "%s", e ? e : "dlopen failed");
@@ -46,6 +60,9 @@ bool rccl_load() {
         get(g_rccl.Recv, "ncclRecv");
         get(g_rccl.GroupStart, "ncclGroupStart");
         get(g_rccl.GroupEnd, "ncclGroupEnd");
+        get(g_rccl.CommInitRankConfig, "ncclCommInitRankConfig");
+        get(g_rccl.CommGetAsyncError, "ncclCommGetAsyncError");
+        get(g_rccl.CommAbort, "ncclCommAbort");
         ok = all;
     });
     if (!ok) fail(CGX_ERR_RCCL, "cannot load RCCL: %s", why);

@@ -3,6 +3,8 @@
 // device and pinned allocations, and the data in and out of a context
 // (cgx_set_rows / cgx_set_system: parallel_cg.c:109-117's MPI_Bcast and
 // MPI_Scatter; cgx_generate_spd; cgx_get_x).
+#include <thread>
+
 #include "cgx_ctx.h"
 
 namespace cgxh {
@@ -361,8 +363,35 @@ static int create_rank(cgx_ctx **ctx, int op, int64_t n, int64_t m, int rank, in
     }
     ncclUniqueId u;
     std::memcpy(&u, id, sizeof u);
-    ncclResult_t nr = ncclCommInitRank(&s.comm, nranks, u, rank);
+    // Nonblocking initialisation, polled with the deadline: a rank that never
+    // joins fails the others after CGX_RCCL_TIMEOUT_S instead of hanging them
+    // in the bootstrap (CGX_RCCL_BLOCKING=1: plain blocking ncclCommInitRank).
+    c->rccl_timeout_s = rccl_timeout_from_env();
+    const char *bl = std::getenv("CGX_RCCL_BLOCKING");
+    ncclResult_t nr;
+    if ((bl && *bl == '1') || c->rccl_timeout_s <= 0.0) {
+        nr = ncclCommInitRank(&s.comm, nranks, u, rank);
+    } else {
+        ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
+        cfg.blocking = 0;
+        nr = ncclCommInitRankConfig(&s.comm, nranks, u, rank, &cfg);
+        const auto t0 = std::chrono::steady_clock::now();
+        while (nr == ncclInProgress) {
+            ncclResult_t st = ncclInProgress;
+            if (ncclCommGetAsyncError(s.comm, &st) != ncclSuccess) break;
+            nr = st;
+            if (nr != ncclInProgress) break;
+            if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > c->rccl_timeout_s) {
+                (void)ncclCommAbort(s.comm);
+                delete c;
+                return fail(CGX_ERR_RCCL, "ncclCommInitRank(rank %d of %d): not every rank joined within %.0f s",
+                            rank, nranks, rccl_timeout_from_env());
+            }
+            std::this_thread::sleep_for(std::chrono::microseconds(200));
+        }
+    }
     if (nr != ncclSuccess) {
+        if (s.comm) (void)ncclCommAbort(s.comm);
         delete c;
         return fail(CGX_ERR_RCCL, "ncclCommInitRank(rank %d of %d): %s", rank, nranks, ncclGetErrorString(nr));
     }
@@ -386,6 +415,8 @@ int cgx_get_unique_id(cgx_unique_id *id) {
     std::memcpy(id, &u, sizeof u);
     return CGX_OK;
 }
+
+int cgx_rccl_available(void) { return rccl_load() ? CGX_OK : CGX_ERR_RCCL; }
 
 int cgx_create_rank(cgx_ctx **ctx, int64_t n, int rank, int nranks, const cgx_unique_id *id, int device,
                     int flags) {
@@ -433,10 +464,13 @@ int cgx_fill(cgx_ctx *c, double b_value, double x_value) {
 
 int cgx_destroy(cgx_ctx *ctx) {
     if (!ctx) return CGX_OK;
+    // rank mode: drain with the deadline first, so a job whose peer died is
+    // aborted here instead of hanging in the stream syncs below
+    const int rc = (ctx->mode == M_RCCL && !ctx->dead) ? sync_all(ctx) : CGX_OK;
     if (ctx->graph) (void)hipGraphExecDestroy(ctx->graph);
     for (auto &s : ctx->sh) free_shard(s);
     delete ctx;
-    return CGX_OK;
+    return rc;
 }
 
 int cgx_get_info(const cgx_ctx *c, cgx_info *info) {
@@ -526,7 +560,7 @@ int cgx_set_rows(cgx_ctx *c, int64_t row0, int64_t nrows, const void *A_rows, in
             const bool whole = lo == s.row0 && hi == s.row0 + s.nloc;
             s.x_zero = whole ? zeros : (s.x_zero && zeros);
         }
-        HIPT(hipStreamSynchronize(s.stream));
+        TRY(rank_wait_stream(c, s.stream, "the copies of cgx_set_rows"));
     }
     c->state = ST_IDLE;
     return CGX_OK;
@@ -554,7 +588,7 @@ int cgx_generate_spd(cgx_ctx *c, uint64_t seed) {
                                     s.stream));
             }
             HIPT(gen_b_f64(c->n, seed, reinterpret_cast<double *>(s.b), s.stream));
-            HIPT(hipStreamSynchronize(s.stream));
+            TRY(rank_wait_stream(c, s.stream, "the tile generation"));
         } else if (s.A_host) {
             // Generate each tile on the device and move it to the host copy of A;
             // b is generated for the whole block first (rows are independent).
@@ -570,7 +604,7 @@ int cgx_generate_spd(cgx_ctx *c, uint64_t seed) {
                 HIPT(hipMemcpyAsync(s.A_host + (size_t)r0 * row_bytes, s.tile[0], (size_t)rows * row_bytes,
                                     hipMemcpyDeviceToHost, s.stream));
             }
-            HIPT(hipStreamSynchronize(s.stream));
+            TRY(rank_wait_stream(c, s.stream, "the tile generation"));
         } else if (c->flags & CGX_SYMMETRIC) {
             HIPT(gen_spd_sym_f64(c->n, c->lda, seed, reinterpret_cast<double *>(s.A), reinterpret_cast<double *>(s.b),
                                  s.stream));
@@ -601,9 +635,10 @@ int cgx_get_x(cgx_ctx *c, void *x) {
     if (c->mode == M_RCCL && c->nranks > 1) {
         Shard &s = c->sh[0];
         TRY(set_dev(s));
-        NCCLT(ncclAllGather(s.x, s.xfull, (size_t)s.nloc, f32ref(c) ? ncclFloat : ncclDouble, s.comm, s.stream));
+        NCCLC(c, ncclAllGather(s.x, s.xfull, (size_t)s.nloc, f32ref(c) ? ncclFloat : ncclDouble, s.comm, s.stream),
+              "ncclAllGather(x) for cgx_get_x");
         HIPT(hipMemcpyAsync(s.h_x ? s.h_x : x, s.xfull, (size_t)c->n * es, hipMemcpyDeviceToHost, s.stream));
-        HIPT(hipStreamSynchronize(s.stream));
+        TRY(rank_wait_stream(c, s.stream, "the x allgather"));
         if (s.h_x) std::memcpy(x, s.h_x, (size_t)c->n * es);
         return CGX_OK;
     }

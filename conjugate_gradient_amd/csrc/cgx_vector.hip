@@ -265,15 +265,32 @@ __global__ __launch_bounds__(kNT) void k_fill(T *p, int64_t n, T v) {
     for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kNT) p[i] = v;
 }
 
-// Scalars combined in rank order: ((in0 + in1) + in2) + ...  Inputs sit in
-// 8-byte slots (a float at the slot start for F32_REF): element q at in[q*stride].
-
+// Scalars combined in a fixed order.  Inputs sit in 8-byte slots (a float at
+// the slot start for F32_REF): element q at in[q*stride].
+//   rank order  ((in0 + in1) + in2) + ...   point-to-point_cg.c allSum :344-352
+//   MPICH order (mpich != 0): MPI_Allreduce(MPI_SUM) of one value as MPICH 3.3
+//     runs it (recursive doubling, parallel_cg.c:287,294,313): with pof2 the
+//     largest power of two <= cnt and rem = cnt - pof2, pairs (2q, 2q+1), q < rem,
+//     combine first, then a balanced pairwise tree over the pof2 values.
+//     Pinned by tests/golden/mpi/ (mpiexec -np 2/4/8 of the unmodified program).
 template <typename T>
-__global__ void k_sum_ordered(const T *in, int cnt, int stride, T *out) {
+__global__ void k_sum_ordered(const T *in, int cnt, int stride, int mpich, T *out) {
 #pragma clang fp contract(off)
-    T s = in[0];
-    for (int q = 1; q < cnt; ++q) s = s + in[q * stride];
-    *out = s;
+    if (!mpich) {
+        T s = in[0];
+        for (int q = 1; q < cnt; ++q) s = s + in[q * stride];
+        *out = s;
+        return;
+    }
+    int pof2 = 1;
+    while (pof2 * 2 <= cnt) pof2 *= 2;
+    const int rem = cnt - pof2;
+    T v[kMaxCombine];
+    for (int q = 0; q < pof2; ++q)
+        v[q] = q < rem ? in[2 * q * stride] + in[(2 * q + 1) * stride] : in[(q + rem) * stride];
+    for (int d = 1; d < pof2; d *= 2)
+        for (int q = 0; q < pof2; q += 2 * d) v[q] = v[q] + v[q + d];
+    *out = v[0];
 }
 
 }  // namespace
@@ -368,12 +385,13 @@ hipError_t fill_f32(float *p, int64_t n, float v, hipStream_t s) {
 }
 
 hipError_t sum_ordered_f64(const double *in, int cnt, double *out, hipStream_t s) {
-    hipLaunchKernelGGL(k_sum_ordered<double>, dim3(1), dim3(1), 0, s, in, cnt, 1, out);
+    hipLaunchKernelGGL(k_sum_ordered<double>, dim3(1), dim3(1), 0, s, in, cnt, 1, 0, out);
     return hipGetLastError();
 }
 
-hipError_t sum_ordered_f32(const float *in, int cnt, float *out, hipStream_t s) {
-    hipLaunchKernelGGL(k_sum_ordered<float>, dim3(1), dim3(1), 0, s, in, cnt, 2, out);
+hipError_t sum_ordered_f32(const float *in, int cnt, float *out, hipStream_t s, bool mpich) {
+    if (cnt < 1 || cnt > kMaxCombine) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_sum_ordered<float>, dim3(1), dim3(1), 0, s, in, cnt, 2, mpich ? 1 : 0, out);
     return hipGetLastError();
 }
 

@@ -31,7 +31,12 @@
  *                conjgrad.m.  Dots are deterministic fixed-order reductions.
  *   CGX_F32_REF  float data, serialConjugate.c's operation order: sequential
  *                fp32 accumulation per row and per dot, no FMA contraction.
- *                Produces the reference's x bit for bit (single shard).
+ *                Produces the reference's x bit for bit: serialConjugate.c on
+ *                one shard; parallel_cg.c on P row blocks (per-rank partials
+ *                combined in MPICH 3.3's MPI_Allreduce order, recursive
+ *                doubling); point-to-point_cg.c with CGX_COMM_P2P (rank-order
+ *                allSum).  Pinned by mpiexec runs of the unmodified programs
+ *                (tests/golden/mpi/).
  *
  * Multi-GPU: the matrix is split into contiguous row blocks (parallel_cg.c:83,
  * 97-99; n % nranks == 0 as parallel_cg.c:86-90 requires).  Per iteration
@@ -78,7 +83,8 @@ extern "C" {
                                    collectives: gather to rank 0, then rank 0
                                    sends to every rank (ncclSend/Recv; device
                                    copies through shard 0 in multi-shard mode).
-                                   Scalars are summed in rank order.  For the
+                                   Scalars are summed in rank order (allSum,
+                                   point-to-point_cg.c:339-359).  For the
                                    p2p-vs-collective comparison of the report. */
 #define CGX_DETERMINISTIC 0x4000 /* rank mode, fp64: combine the two scalars by
                                     allgathering the per-rank partials and
@@ -148,8 +154,19 @@ int cgx_create_multi(cgx_ctx **ctx, int64_t n, int nshards, const int *devices, 
 /* One process per GPU (parallel_cg.c's one MPI rank per process): this
  * process owns row block `rank` of `nranks`; `id` comes from
  * cgx_get_unique_id() on rank 0 and is broadcast by the caller.  Exchange by
- * RCCL (allgather p, allreduce p.Ap and r.r) on the context's stream. */
+ * RCCL (allgather p, allreduce p.Ap and r.r) on the context's stream.
+ * Fail-fast (the reference stops the job with MPI_Abort, parallel_cg.c:79-94):
+ * the communicator is initialised nonblocking and every host wait polls with a
+ * deadline of CGX_RCCL_TIMEOUT_S seconds (environment, default 60; 0 = wait
+ * forever) while watching RCCL's asynchronous error.  A rank that never joins,
+ * dies, or issues a different collective makes the others' calls return
+ * CGX_ERR_RCCL (naming the exchange and iteration) instead of hanging; the
+ * communicator is then aborted and the context only accepts cgx_destroy. */
 int cgx_get_unique_id(cgx_unique_id *id);
+/* Loads RCCL (done on first rank-mode use anyway) and checks that every entry
+ * point libcgx calls is present: CGX_OK, or CGX_ERR_RCCL with the reason in
+ * cgx_last_error().  Needs no GPU.  A failed load is permanent for the process. */
+int cgx_rccl_available(void);
 int cgx_create_rank(cgx_ctx **ctx, int64_t n, int rank, int nranks,
                     const cgx_unique_id *id, int device, int flags);
 

@@ -19,4 +19,4 @@ os.environ["LOCAL_RANK"] = "0"  # one GPU: every rank drives device 0
 import bench  # noqa: E402
 
 if __name__ == "__main__":
-    sys.exit(bench.main(sys.argv[1:]))
+    sys.exit(bench.run())

@@ -44,6 +44,8 @@ def main():
         with open(uidfile, "rb") as f:
             uid = f.read()
     res = {"rank": rank}
+    if mode in ("peer_dies", "peer_absent"):
+        return fail_fast(mode, n, P, rank, uid, out)
     if mode.startswith("poisson"):
         m = n
         with cg.Solver(None, poisson_m=m, rank=rank, nranks=P, unique_id=uid, device=0) as s:
@@ -76,6 +78,32 @@ def main():
                 res["fixed_iterations"] = st2.iterations
                 res["fixed_relres"] = float(np.divide(*s.residual_norm()))
     np.save(out + f"_x{rank}.npy", x)
+    with open(out + f"_r{rank}.json", "w") as f:
+        json.dump(res, f)
+
+
+def fail_fast(mode, n, P, rank, uid, out):
+    """Rank mode must fail fast, not hang, when a peer is gone (the reference
+    stops the job with MPI_Abort, parallel_cg.c:79,89,94,143).
+      peer_dies:   the last rank exits right after cgx_create_rank; the others
+                   set up and solve, and must get CGX_ERR_RCCL within the deadline.
+      peer_absent: the last rank never creates its context; the others must get
+                   CGX_ERR_RCCL from cgx_create_rank within the deadline."""
+    if rank == P - 1:
+        if mode == "peer_dies":
+            cg.Solver(n, rank=rank, nranks=P, unique_id=uid, device=0)
+        os._exit(0)  # no destroy, no finalisation: as if the process died
+    A, b, x0 = case(f"spd{n}", np.float64)
+    t0 = time.time()
+    res = {"rank": rank, "error": None}
+    try:
+        with cg.Solver(n, rank=rank, nranks=P, unique_id=uid, device=0) as s:
+            res["created_s"] = time.time() - t0
+            s.set_system(A, b, x0)
+            s.solve(None, eps=1e-10)
+    except cg.CgxError as e:
+        res.update(error=str(e), code=e.code)
+    res["elapsed_s"] = time.time() - t0
     with open(out + f"_r{rank}.json", "w") as f:
         json.dump(res, f)
 

@@ -53,6 +53,46 @@ def test_rccl_loads_on_first_rank_call(built, monkeypatch):
         assert "RCCL error" in str(e) and "cannot load RCCL" not in str(e), str(e)
 
 
+def test_rccl_entry_points_resolve(built):
+    """cgx_rccl_available: librccl.so.1 loads (no GPU needed) and every entry
+    point rank mode calls -- the collectives, send/recv, groups, and the
+    fail-fast trio ncclCommInitRankConfig / ncclCommGetAsyncError /
+    ncclCommAbort -- resolves; a missing one fails here, not on the GPU box."""
+    rc = cg.lib().cgx_rccl_available()
+    assert rc == 0, cg.lib().cgx_last_error().decode()
+
+
+def test_python_mirror_checks_sizes_before_the_c_call():
+    """Short or mis-shaped host arrays raise ValueError in the mirror; they
+    never reach cgx_set_rows / cgx_solve (which would read or write n
+    elements).  No context is needed to get there, so this runs without a GPU."""
+    s = cg.Solver.__new__(cg.Solver)
+    s.n, s.dtype, s.flags, s._h = 8, np.dtype(np.float64), cg.CGX_F64, None
+    A, b = np.eye(8), np.ones(8)
+    with pytest.raises(ValueError, match="x0"):
+        s.set_system(A, b, np.zeros(7))
+    with pytest.raises(ValueError, match="A has shape"):
+        s.set_system(np.eye(7), b)
+    with pytest.raises(ValueError, match="b has shape"):
+        s.set_system(A, np.ones(9))
+    with pytest.raises(ValueError, match="x0 has shape"):
+        s.solve(np.zeros(5))
+    with pytest.raises(ValueError, match="x has shape"):
+        s.set_x(np.zeros(3))
+    with pytest.raises(ValueError, match="same 2 rows"):
+        s.set_rows(0, np.ones((2, 8)), np.ones(3))
+    with pytest.raises(ValueError, match="nrows, >= 8"):
+        s.set_rows(0, np.ones((2, 5)))
+    with pytest.raises(ValueError, match="outside"):
+        s.set_rows(6, None, np.ones(3))
+    d = cg.DeviceArray.__new__(cg.DeviceArray)
+    d.count, d.dtype, d.ptr = 4, np.dtype(np.float64), None
+    with pytest.raises(ValueError, match="matVec A"):
+        cg.matVec(d, d, d, rows=4, cols=4)
+    with pytest.raises(ValueError, match="vecVec"):
+        cg.vecVec(d, d, d, n=5)
+
+
 def test_gfx950_code_object(built):
     # the HIP kernels are compiled for gfx950 (offload bundle inside the .so)
     data = open(cg.LIB_PATH, "rb").read()

@@ -11,9 +11,9 @@ exchange and the final x allgather (tests/_rank_worker.py).
 
 Pins: fp64 x vs the fp64 oracle (conjgrad.m order) to 1e-10 with its loop
 count; CGX_DETERMINISTIC bitwise equal to the multi-shard run with the same
-partition; CGX_F32_REF bitwise equal to the oracle's P-part
-(point-to-point_cg.c allSum order) restatement; every rank ends with the
-same x.
+partition; CGX_F32_REF bitwise equal to the unmodified parallel_cg.c
+(collective) / point-to-point_cg.c (p2p) run under mpiexec -np P
+(tests/golden/mpi/); every rank ends with the same x.
 """
 import json
 import os
@@ -25,7 +25,7 @@ import pytest
 
 import conjugate_gradient_amd as cg
 import oracle
-from _cases import case
+from _cases import case, golden_mpi, mpi_golden_x
 
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -110,12 +110,16 @@ def test_rank_mode_f64_sizes(tmp_path, n, P):
 @pytest.mark.timeout(200)
 @pytest.mark.parametrize("mode", ["f32ref", "p2p_f32ref"])
 def test_rank_mode_f32ref_bitwise(tmp_path, mode):
+    """4 RCCL ranks == parallel_cg.c / point-to-point_cg.c on 4 MPI ranks."""
     n, P = 2048, 4
     x, res = run_ranks(tmp_path, mode, n, P)
-    A, b, x0 = case(f"spd{n}")
-    xo, so = oracle.cg_f32ref(A, b, x0, eps=1e-6, nparts=P)
-    assert res[0]["iterations"] == so.iterations
-    assert np.array_equal(x.view(np.uint32), xo.view(np.uint32))
+    _check_mpi_golden(x, res, ("p2p" if mode.startswith("p2p") else "parallel") + f"_spd{n}_np{P}")
+
+
+def _check_mpi_golden(x, res, key):
+    r = golden_mpi()["runs"][key]
+    assert res[0]["iterations"] == r["ref_iterations"]
+    assert np.array_equal(x.view(np.uint32), mpi_golden_x(key).view(np.uint32))
 
 
 @pytest.mark.timeout(200)
@@ -131,7 +135,7 @@ def test_rank_mode_poisson_halo(tmp_path, mode):
 
 
 @pytest.mark.timeout(240)
-@pytest.mark.parametrize("mode", ["collective", "p2p", "deterministic", "f32ref", "poisson_eps"])
+@pytest.mark.parametrize("mode", ["collective", "p2p", "deterministic", "f32ref", "p2p_f32ref", "poisson_eps"])
 def test_rank_mode_world8(tmp_path, mode):
     """The driver's largest placement, 8 ranks (here on one GPU): 8 row
     blocks of 128 / 256 rows, the p2p pattern's 7 sends per exchange, 8
@@ -143,14 +147,11 @@ def test_rank_mode_world8(tmp_path, mode):
         xo, so = oracle.cg_poisson_f64(m, np.ones(m * m), np.zeros(m * m), eps=1e-8, max_iter=-1)
         assert res[0]["iterations"] == so.iterations and rel(x, xo) <= TOL
         return
-    n = 2048 if mode == "f32ref" else 1024
+    n = 2048 if "f32ref" in mode else 1024
     x, res = run_ranks(tmp_path, mode, n, P, timeout=200)
     assert res[0]["nrows"] == n // P
-    if mode == "f32ref":
-        A, b, x0 = case(f"spd{n}")
-        xo, so = oracle.cg_f32ref(A, b, x0, eps=1e-6, nparts=P)
-        assert res[0]["iterations"] == so.iterations
-        assert np.array_equal(x.view(np.uint32), xo.view(np.uint32))
+    if "f32ref" in mode:  # == mpiexec -np 8 of the unmodified program
+        _check_mpi_golden(x, res, ("p2p" if mode.startswith("p2p") else "parallel") + f"_spd{n}_np{P}")
         return
     A, b, x0 = case(f"spd{n}", np.float64)
     xo, so = oracle.cg_f64(A, b, x0, eps=1e-10)
@@ -160,6 +161,41 @@ def test_rank_mode_world8(tmp_path, mode):
         xs = x0.copy()
         cg.conjugrad(A, b, xs, eps=1e-10, shards=[0] * P)
         assert np.array_equal(x, xs)
+
+
+@pytest.mark.timeout(150)
+@pytest.mark.parametrize("mode", ["peer_dies", "peer_absent"])
+def test_rank_mode_fails_fast_when_a_peer_is_gone(tmp_path, mode):
+    """A dead or absent rank must not hang the others (the reference's
+    fail-stop is MPI_Abort, parallel_cg.c:79,89,94,143): with
+    CGX_RCCL_TIMEOUT_S=20, rank 0 gets CGX_ERR_RCCL (-3) naming what it waited
+    for -- from the solve when rank 1 died after cgx_create_rank, from
+    cgx_create_rank when rank 1 never joined -- and exits on its own."""
+    n, P, limit = 1024, 2, 20
+    uidfile, out = str(tmp_path / "uid.bin"), str(tmp_path / mode)
+    procs = []
+    for r in range(P):
+        env = dict(os.environ, NCCL_HOSTID=f"cgx-test-host-{r}", NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1",
+                   HSA_ENABLE_IPC_MODE_LEGACY="0", CGX_RCCL_TIMEOUT_S=str(limit))
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "_rank_worker.py"), mode, str(n), str(P),
+                                       str(r), uidfile, out], env=env, stdout=subprocess.PIPE,
+                                      stderr=subprocess.STDOUT, text=True))
+    try:
+        logs = [p.communicate(timeout=120)[0] for p in procs]
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    assert procs[0].returncode == 0, logs[0][-3000:]
+    with open(out + "_r0.json") as f:
+        res = json.load(f)
+    assert res["error"] is not None and res["code"] == -3, res
+    assert res["elapsed_s"] <= limit + 30, res
+    if mode == "peer_absent":
+        assert "cgx_create" in res["error"] and "created_s" not in res, res
+    else:
+        assert "created_s" in res and "aborted" not in res["error"], res
 
 
 @pytest.mark.timeout(240)

@@ -8,14 +8,17 @@ Pins:
   3. CGX_F64 x vs the reference's fp32 x: ||dx||/||x|| <= 1e-5;
   4. KATs: 2x2 -> [2/3, 1/3], 4x4 -> [-1, 1, -1, 1] to 1e-12.
 Multi-shard runs (several row blocks on this GPU, the parallel_cg.c split)
-must give the oracle's row-block results: bit-exact in F32_REF against the
-point-to-point_cg.c dot order, 1e-10 in F64."""
+must give the reference MPI programs' results: F32_REF bit-exact to the
+unmodified parallel_cg.c (collective exchange, MPICH's MPI_Allreduce order)
+and point-to-point_cg.c (CGX_COMM_P2P, allSum order) run under mpiexec -np P
+(tests/golden/mpi/), and to the oracle's P-part restatement of both beyond
+the fixtures; 1e-10 in F64."""
 import numpy as np
 import pytest
 
 import conjugate_gradient_amd as cg
 import oracle
-from _cases import KATS, SPD_ALL, SPD_SMALL, case, golden_x
+from _cases import COMBINE_OF, KATS, SPD_ALL, SPD_SMALL, case, golden_mpi, golden_x, mpi_golden_x, mpi_runs
 
 pytestmark = pytest.mark.gpu
 TOL = 1e-10
@@ -67,15 +70,31 @@ def test_known_answers():
 @pytest.mark.parametrize("P", [2, 4])
 @pytest.mark.parametrize("name", ["kat4", "spd512", "spd2048"])
 def test_row_block_shards_f32ref(name, P):
-    """P row blocks on this GPU == oracle with P-part dots (point-to-point_cg.c order)."""
+    """P row blocks on this GPU == oracle with P-part dots (parallel_cg.c, MPICH order)."""
     A, b, x0 = case(name)
     if b.size % P:
         pytest.skip("n not divisible")
     x = x0.copy()
     st = cg.conjugrad(A, b, x, eps=1e-6, shards=[0] * P)
-    xo, so = oracle.cg_f32ref(A, b, x0, eps=1e-6, nparts=P)
+    xo, so = oracle.cg_f32ref(A, b, x0, eps=1e-6, nparts=P, combine="mpich")
     assert st.iterations == so.iterations
     assert np.array_equal(x.view(np.uint32), xo.view(np.uint32))
+
+
+@pytest.mark.parametrize("key", mpi_runs(min_np=2))
+def test_f32ref_shards_bit_exact_vs_mpi_reference(key):
+    """P row blocks on this GPU == the unmodified MPI program under
+    mpiexec -np P, bit for bit, same loop count: parallel_cg.c through the
+    collective exchange (MPICH's MPI_Allreduce order), point-to-point_cg.c
+    through CGX_COMM_P2P (allSum, rank order)."""
+    r = golden_mpi()["runs"][key]
+    A, b, x0 = case(r["case"])
+    flags = cg.CGX_F32_REF | (cg.CGX_COMM_P2P if r["program"] == "p2p" else 0)
+    with cg.Solver(b.size, flags=flags, devices=[0] * r["np"]) as s:
+        s.set_system(A, b, x0)
+        x, st = s.solve(None, eps=1e-6)
+    assert st.iterations == r["ref_iterations"] and st.converged == 1
+    assert np.array_equal(x.view(np.uint32), mpi_golden_x(key).view(np.uint32))
 
 
 @pytest.mark.parametrize("P", [2, 4, 8])
@@ -158,7 +177,8 @@ def test_device_generator_matches_oracle(n, shards):
         s.generate_spd(seed=42)
         x32, st32 = s.solve(None, eps=1e-6)
     A32, b32 = oracle.spd_hash(n, seed=42, dtype=np.float32)
-    xo32, _ = oracle.cg_f32ref(A32, b32, np.zeros(n, np.float32), nparts=len(shards) if shards else 1)
+    xo32, _ = oracle.cg_f32ref(A32, b32, np.zeros(n, np.float32), nparts=len(shards) if shards else 1,
+                               combine="mpich")
     assert np.array_equal(x32, xo32)
 
 
@@ -298,7 +318,7 @@ def test_host_streamed_matvec(monkeypatch, shards):
     with cg.Solver(1024, flags=cg.CGX_F32_REF | cg.CGX_HOST_STREAM, devices=shards) as s:
         s.set_system(A32, b32, x032)
         x32, st32 = s.solve(None, eps=1e-6)
-    ref, sr = oracle.cg_f32ref(A32, b32, x032, nparts=len(shards) if shards else 1)
+    ref, sr = oracle.cg_f32ref(A32, b32, x032, nparts=len(shards) if shards else 1, combine="mpich")
     assert st32.iterations == sr.iterations
     assert np.array_equal(x32, ref)
 
@@ -460,7 +480,7 @@ def test_overlapped_exchange_matches(P):
 @pytest.mark.parametrize("P", [2, 4])
 def test_p2p_exchange_mode(P):
     """CGX_COMM_P2P (point-to-point_cg.c's gather-to-root + send-to-all) gives
-    the collective mode's results bit for bit (both sum scalars in rank
+    the collective mode's results bit for bit (fp64: both sum scalars in rank
     order); F32_REF == oracle with P-part dots (point-to-point_cg.c allSum)."""
     A, b, x0 = case("spd1024", np.float64)
     out = {}
@@ -474,7 +494,7 @@ def test_p2p_exchange_mode(P):
     with cg.Solver(b.size, flags=cg.CGX_F32_REF | cg.CGX_COMM_P2P, devices=[0] * P) as s:
         s.set_system(A32, b32, x032)
         x32, st32 = s.solve(None, eps=1e-6)
-    ref, sr = oracle.cg_f32ref(A32, b32, x032, nparts=P)
+    ref, sr = oracle.cg_f32ref(A32, b32, x032, nparts=P, combine="rank")
     assert st32.iterations == sr.iterations and np.array_equal(x32, ref)
     uid = cg.get_unique_id()
     with cg.Solver(b.size, flags=cg.CGX_F64 | cg.CGX_COMM_P2P, rank=0, nranks=1, unique_id=uid) as s:
@@ -488,7 +508,8 @@ def test_p2p_exchange_mode(P):
 def test_ragged_sizes_and_blocks(n, P):
     """Odd n, row blocks of odd length (unaligned vector slices -> scalar
     kernels), blocks not 128-aligned (no overlap): fp64 within 1e-10 of the
-    oracle, F32_REF bit-exact to the P-part oracle."""
+    oracle, F32_REF bit-exact to the P-part oracle (MPICH order, also for P
+    that is not a power of two: pairs first, then the tree)."""
     A, b = oracle.spd_hash(n, seed=n)
     with cg.Solver(n, devices=[0] * P) as s:
         s.set_system(A, b)
@@ -499,7 +520,7 @@ def test_ragged_sizes_and_blocks(n, P):
     with cg.Solver(n, flags=cg.CGX_F32_REF, devices=[0] * P) as s:
         s.set_system(A32, b32)
         x32, st32 = s.solve(None, eps=1e-6)
-    ref, sr = oracle.cg_f32ref(A32, b32, np.zeros(n, np.float32), nparts=P)
+    ref, sr = oracle.cg_f32ref(A32, b32, np.zeros(n, np.float32), nparts=P, combine="mpich")
     assert st32.iterations == sr.iterations and np.array_equal(x32, ref)
 
 
@@ -519,7 +540,7 @@ def test_f32ref_bit_exact_many_iterations(n, P, seed):
     with cg.Solver(n, flags=cg.CGX_F32_REF, devices=[0] * P) as s:
         s.set_system(A, b, x0)
         x, st = s.solve(None, eps=1e-4)
-    ref, sr = oracle.cg_f32ref(A, b, x0, eps=1e-4, nparts=P)
+    ref, sr = oracle.cg_f32ref(A, b, x0, eps=1e-4, nparts=P, combine="mpich")
     assert st.iterations == sr.iterations and st.iterations >= 20
     assert np.array_equal(x.view(np.uint32), ref.view(np.uint32))
 
