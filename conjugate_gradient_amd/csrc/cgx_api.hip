@@ -15,6 +15,21 @@ int fail(int code, const char *fmt, ...) {
     return code;
 }
 
+void debug_log(const char *fmt, ...) {
+    static const bool on = [] {
+        const char *e = std::getenv("CGX_DEBUG");
+        return e && *e == '1';
+    }();
+    if (!on) return;
+    char buf[512];
+    va_list ap;
+    va_start(ap, fmt);
+    vsnprintf(buf, sizeof buf, fmt, ap);
+    va_end(ap);
+    fprintf(stderr, "[cgx] %s\n", buf);
+    fflush(stderr);
+}
+
 // Per-device workspace for the kernel-level entry points.
 std::mutex g_ws_mu;
 RedWs g_ws[64];

@@ -60,6 +60,8 @@ using namespace cgx;
 namespace cgxh {
 extern thread_local char g_err[1024];
 int fail(int code, const char *fmt, ...);
+// CGX_DEBUG=1: one line per rank-mode fail-fast event on stderr.
+void debug_log(const char *fmt, ...);
 
 // RCCL, loaded on first use (cgx_rccl.hip): rank mode calls it through these
 // pointers (the macros below keep the nccl* names at the call sites).
@@ -74,8 +76,7 @@ struct RcclApi {
     decltype(&::ncclRecv) Recv = nullptr;
     decltype(&::ncclGroupStart) GroupStart = nullptr;
     decltype(&::ncclGroupEnd) GroupEnd = nullptr;
-    // fail-fast: nonblocking init, asynchronous error query, abort
-    decltype(&::ncclCommInitRankConfig) CommInitRankConfig = nullptr;
+    // fail-fast: asynchronous error query, abort
     decltype(&::ncclCommGetAsyncError) CommGetAsyncError = nullptr;
     decltype(&::ncclCommAbort) CommAbort = nullptr;
 };
@@ -96,7 +97,6 @@ bool rccl_load();
 #define ncclRecv (cgxh::g_rccl.Recv)
 #define ncclGroupStart (cgxh::g_rccl.GroupStart)
 #define ncclGroupEnd (cgxh::g_rccl.GroupEnd)
-#define ncclCommInitRankConfig (cgxh::g_rccl.CommInitRankConfig)
 #define ncclCommGetAsyncError (cgxh::g_rccl.CommGetAsyncError)
 #define ncclCommAbort (cgxh::g_rccl.CommAbort)
 #endif

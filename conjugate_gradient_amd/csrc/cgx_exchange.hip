@@ -444,10 +444,12 @@ static int rccl_abort(cgx_ctx *c, const char *fmt, ...) {
     snprintf(c->dead_why, sizeof c->dead_why, "%s; last exchange enqueued: %s at iteration %lld", why, c->last_coll,
              (long long)c->last_coll_k);
     c->dead = true;
+    debug_log("rank %d: aborting the communicator: %s", s.index, c->dead_why);
     if (s.comm) {
         (void)ncclCommAbort(s.comm);  // RCCL kernels still waiting on a peer exit
         s.comm = nullptr;
     }
+    debug_log("rank %d: ncclCommAbort returned", s.index);
     return fail(CGX_ERR_RCCL, "rank %d of %d: %s", s.index, c->nranks, c->dead_why);
 }
 
@@ -496,12 +498,14 @@ int rank_wait_stream(cgx_ctx *c, hipStream_t st, const char *what) {
     return rank_poll(c, [st] { return hipStreamQuery(st); }, what);
 }
 
-// After an RCCL call (NCCLC): ncclInProgress from the nonblocking communicator
-// means the enqueue finishes asynchronously; poll its state with the deadline.
+// After an RCCL call (NCCLC): ncclInProgress (a nonblocking communicator's
+// asynchronous enqueue) is waited for with the deadline, and the
+// communicator's asynchronous error state is checked after every call, so a
+// failure the proxy thread saw surfaces at the next exchange.
 int rccl_after(cgx_ctx *c, ncclResult_t r, const char *what, const char *expr, const char *file, int line) {
     c->last_coll = what;
     c->last_coll_k = c->k;
-    if (r == ncclInProgress) {
+    if (r == ncclSuccess || r == ncclInProgress) {
         const double t0 = now_s();
         Shard &s = c->sh[0];
         for (;;) {

@@ -60,7 +60,6 @@ bool rccl_load() {
         get(g_rccl.Recv, "ncclRecv");
         get(g_rccl.GroupStart, "ncclGroupStart");
         get(g_rccl.GroupEnd, "ncclGroupEnd");
-        get(g_rccl.CommInitRankConfig, "ncclCommInitRankConfig");
         get(g_rccl.CommGetAsyncError, "ncclCommGetAsyncError");
         get(g_rccl.CommAbort, "ncclCommAbort");
         ok = all;

@@ -3,6 +3,8 @@
 // device and pinned allocations, and the data in and out of a context
 // (cgx_set_rows / cgx_set_system: parallel_cg.c:109-117's MPI_Bcast and
 // MPI_Scatter; cgx_generate_spd; cgx_get_x).
+#include <condition_variable>
+#include <memory>
 #include <thread>
 
 #include "cgx_ctx.h"
@@ -363,32 +365,53 @@ static int create_rank(cgx_ctx **ctx, int op, int64_t n, int64_t m, int rank, in
     }
     ncclUniqueId u;
     std::memcpy(&u, id, sizeof u);
-    // Nonblocking initialisation, polled with the deadline: a rank that never
-    // joins fails the others after CGX_RCCL_TIMEOUT_S instead of hanging them
-    // in the bootstrap (CGX_RCCL_BLOCKING=1: plain blocking ncclCommInitRank).
+    // The initialisation runs on a helper thread and this one waits for it
+    // with the deadline: ncclCommInitRank blocks in the bootstrap until every
+    // rank has joined (RCCL 2.27 does so inside the call even for a
+    // nonblocking communicator, measured), so a rank that never joins would
+    // hang the others.  On the deadline the call returns CGX_ERR_RCCL and the
+    // helper is left behind, detached; should it still finish, it aborts the
+    // communicator it made.  The process is expected to exit on the error.
     c->rccl_timeout_s = rccl_timeout_from_env();
-    const char *bl = std::getenv("CGX_RCCL_BLOCKING");
-    ncclResult_t nr;
-    if ((bl && *bl == '1') || c->rccl_timeout_s <= 0.0) {
-        nr = ncclCommInitRank(&s.comm, nranks, u, rank);
-    } else {
-        ncclConfig_t cfg = NCCL_CONFIG_INITIALIZER;
-        cfg.blocking = 0;
-        nr = ncclCommInitRankConfig(&s.comm, nranks, u, rank, &cfg);
-        const auto t0 = std::chrono::steady_clock::now();
-        while (nr == ncclInProgress) {
-            ncclResult_t st = ncclInProgress;
-            if (ncclCommGetAsyncError(s.comm, &st) != ncclSuccess) break;
-            nr = st;
-            if (nr != ncclInProgress) break;
-            if (std::chrono::duration<double>(std::chrono::steady_clock::now() - t0).count() > c->rccl_timeout_s) {
-                (void)ncclCommAbort(s.comm);
-                delete c;
-                return fail(CGX_ERR_RCCL, "ncclCommInitRank(rank %d of %d): not every rank joined within %.0f s",
-                            rank, nranks, rccl_timeout_from_env());
-            }
-            std::this_thread::sleep_for(std::chrono::microseconds(200));
+    struct InitJob {
+        std::mutex mu;
+        std::condition_variable cv;
+        bool done = false, abandoned = false;
+        ncclResult_t r = ncclInternalError;
+        ncclComm_t comm = nullptr;
+    };
+    auto job = std::make_shared<InitJob>();
+    std::thread([job, nranks, u, rank, device] {
+        ncclComm_t comm = nullptr;
+        ncclResult_t r = hipSetDevice(device) == hipSuccess ? ncclCommInitRank(&comm, nranks, u, rank)
+                                                            : ncclUnhandledCudaError;
+        std::lock_guard<std::mutex> lk(job->mu);
+        if (job->abandoned) {
+            if (comm) (void)ncclCommAbort(comm);
+            return;
         }
+        job->r = r;
+        job->comm = comm;
+        job->done = true;
+        job->cv.notify_all();
+    }).detach();
+    ncclResult_t nr;
+    {
+        std::unique_lock<std::mutex> lk(job->mu);
+        auto ready = [&job] { return job->done; };
+        if (c->rccl_timeout_s > 0.0)
+            job->cv.wait_for(lk, std::chrono::duration<double>(c->rccl_timeout_s), ready);
+        else
+            job->cv.wait(lk, ready);
+        if (!job->done) {
+            job->abandoned = true;
+            debug_log("rank %d: ncclCommInitRank did not return within %.0f s", rank, c->rccl_timeout_s);
+            delete c;
+            return fail(CGX_ERR_RCCL, "ncclCommInitRank(rank %d of %d): not every rank joined within %.0f s "
+                                      "(CGX_RCCL_TIMEOUT_S)", rank, nranks, rccl_timeout_from_env());
+        }
+        nr = job->r;
+        s.comm = job->comm;
     }
     if (nr != ncclSuccess) {
         if (s.comm) (void)ncclCommAbort(s.comm);

@@ -156,9 +156,9 @@ int cgx_create_multi(cgx_ctx **ctx, int64_t n, int nshards, const int *devices, 
  * cgx_get_unique_id() on rank 0 and is broadcast by the caller.  Exchange by
  * RCCL (allgather p, allreduce p.Ap and r.r) on the context's stream.
  * Fail-fast (the reference stops the job with MPI_Abort, parallel_cg.c:79-94):
- * the communicator is initialised nonblocking and every host wait polls with a
+ * the communicator's initialisation and every host wait are bounded by a
  * deadline of CGX_RCCL_TIMEOUT_S seconds (environment, default 60; 0 = wait
- * forever) while watching RCCL's asynchronous error.  A rank that never joins,
+ * forever), and the waits watch RCCL's asynchronous error.  A rank that never joins,
  * dies, or issues a different collective makes the others' calls return
  * CGX_ERR_RCCL (naming the exchange and iteration) instead of hanging; the
  * communicator is then aborted and the context only accepts cgx_destroy. */

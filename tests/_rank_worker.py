@@ -96,16 +96,32 @@ def fail_fast(mode, n, P, rank, uid, out):
     A, b, x0 = case(f"spd{n}", np.float64)
     t0 = time.time()
     res = {"rank": rank, "error": None}
+
+    def say(msg):
+        print(f"[rank {rank} +{time.time() - t0:.1f}s] {msg}", flush=True)
+
+    s = None
     try:
-        with cg.Solver(n, rank=rank, nranks=P, unique_id=uid, device=0) as s:
-            res["created_s"] = time.time() - t0
-            s.set_system(A, b, x0)
-            s.solve(None, eps=1e-10)
+        say("cgx_create_rank")
+        s = cg.Solver(n, rank=rank, nranks=P, unique_id=uid, device=0)
+        res["created_s"] = time.time() - t0
+        say("set_system + solve")
+        s.set_system(A, b, x0)
+        s.solve(None, eps=1e-10)
     except cg.CgxError as e:
         res.update(error=str(e), code=e.code)
+        say(f"error: {e}")
     res["elapsed_s"] = time.time() - t0
     with open(out + f"_r{rank}.json", "w") as f:
         json.dump(res, f)
+    if s is not None:
+        say("cgx_destroy")
+        try:
+            s.close()
+        except cg.CgxError as e:
+            say(f"destroy: {e}")
+    say("exit")
+    os._exit(0)  # as bench.py does after an error: no teardown that could wait on the dead peer
 
 
 if __name__ == "__main__":

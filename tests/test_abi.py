@@ -55,9 +55,9 @@ def test_rccl_loads_on_first_rank_call(built, monkeypatch):
 
 def test_rccl_entry_points_resolve(built):
     """cgx_rccl_available: librccl.so.1 loads (no GPU needed) and every entry
-    point rank mode calls -- the collectives, send/recv, groups, and the
-    fail-fast trio ncclCommInitRankConfig / ncclCommGetAsyncError /
-    ncclCommAbort -- resolves; a missing one fails here, not on the GPU box."""
+    point rank mode calls -- init, the collectives, send/recv, groups, and the
+    fail-fast pair ncclCommGetAsyncError / ncclCommAbort -- resolves; a
+    missing one fails here, not on the GPU box."""
     rc = cg.lib().cgx_rccl_available()
     assert rc == 0, cg.lib().cgx_last_error().decode()
 

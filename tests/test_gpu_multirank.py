@@ -173,24 +173,30 @@ def test_rank_mode_fails_fast_when_a_peer_is_gone(tmp_path, mode):
     cgx_create_rank when rank 1 never joined -- and exits on its own."""
     n, P, limit = 1024, 2, 20
     uidfile, out = str(tmp_path / "uid.bin"), str(tmp_path / mode)
-    procs = []
+    procs, logs = [], [str(tmp_path / f"rank{r}.log") for r in range(P)]
     for r in range(P):
         env = dict(os.environ, NCCL_HOSTID=f"cgx-test-host-{r}", NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1",
-                   HSA_ENABLE_IPC_MODE_LEGACY="0", CGX_RCCL_TIMEOUT_S=str(limit))
-        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "_rank_worker.py"), mode, str(n), str(P),
-                                       str(r), uidfile, out], env=env, stdout=subprocess.PIPE,
-                                      stderr=subprocess.STDOUT, text=True))
+                   HSA_ENABLE_IPC_MODE_LEGACY="0", CGX_RCCL_TIMEOUT_S=str(limit), CGX_DEBUG="1")
+        with open(logs[r], "w") as lf:
+            procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "_rank_worker.py"), mode, str(n),
+                                           str(P), str(r), uidfile, out], env=env, stdout=lf,
+                                          stderr=subprocess.STDOUT))
+    hung = False
     try:
-        logs = [p.communicate(timeout=120)[0] for p in procs]
+        for p in procs:
+            p.wait(timeout=120)
+    except subprocess.TimeoutExpired:
+        hung = True
     finally:
         for p in procs:
             if p.poll() is None:
                 p.kill()
                 p.wait()
-    assert procs[0].returncode == 0, logs[0][-3000:]
+    tail = "\n".join(f"--- rank {r}:\n" + open(logs[r]).read()[-4000:] for r in range(P))
+    assert not hung and procs[0].returncode == 0, tail
     with open(out + "_r0.json") as f:
         res = json.load(f)
-    assert res["error"] is not None and res["code"] == -3, res
+    assert res["error"] is not None and res["code"] == -3, (res, tail)
     assert res["elapsed_s"] <= limit + 30, res
     if mode == "peer_absent":
         assert "cgx_create" in res["error"] and "created_s" not in res, res
