@@ -71,6 +71,9 @@ def lib() -> ctypes.CDLL:
         L.oracle_cg_f64.argtypes = [i64, vp, vp, vp, i64, f64, ctypes.POINTER(OracleStats)]
         L.oracle_cg_f64.restype = ctypes.c_int
         L.oracle_set_threads.argtypes = [ctypes.c_int]
+        L.oracle_hash_matvec_f64.argtypes = [i64, ctypes.c_uint64, i64, i64, vp, vp]
+        L.oracle_cg_f64_hash.argtypes = [i64, ctypes.c_uint64, vp, i64, f64, ctypes.POINTER(OracleStats)]
+        L.oracle_cg_f64_hash.restype = ctypes.c_int
         L.oracle_poisson_apply.argtypes = [i64, vp, vp]
         L.oracle_cg_poisson_f64.argtypes = [i64, vp, vp, i64, f64, ctypes.POINTER(OracleStats)]
         L.oracle_cg_poisson_f64.restype = ctypes.c_int
@@ -176,6 +179,26 @@ def cg_f64(A, b, x0, max_iter: int = -1, eps: float = 1e-10):
     rc = lib().oracle_cg_f64(b.size, _p(A), _p(b), _p(x), max_iter, eps, ctypes.byref(st))
     if rc != 0:
         raise RuntimeError(f"oracle_cg_f64 rc={rc}")
+    return x, st
+
+
+def hash_matvec_f64(n: int, v: np.ndarray, seed: int = 42, row0: int = 0, nrows: int | None = None) -> np.ndarray:
+    """Rows [row0, row0+nrows) of spd_hash(n, seed)'s A times v, A regenerated on the fly."""
+    nrows = n - row0 if nrows is None else nrows
+    v = np.ascontiguousarray(v, np.float64)
+    out = np.empty(nrows, np.float64)
+    lib().oracle_hash_matvec_f64(n, seed, row0, nrows, _p(v), _p(out))
+    return out
+
+
+def cg_f64_hash(n: int, seed: int = 42, x0=None, max_iter: int = -1, eps: float = 1e-10):
+    """conjgrad.m on spd_hash(n, seed) (A regenerated per matVec, no n*n memory);
+    returns (x, OracleStats).  Same results as cg_f64(*spd_hash(n, seed))."""
+    x = np.zeros(n) if x0 is None else np.array(x0, dtype=np.float64, copy=True)
+    st = OracleStats()
+    rc = lib().oracle_cg_f64_hash(n, seed, _p(x), max_iter, eps, ctypes.byref(st))
+    if rc != 0:
+        raise RuntimeError(f"oracle_cg_f64_hash rc={rc}")
     return x, st
 
 

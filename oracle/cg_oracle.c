@@ -311,15 +311,63 @@ double oracle_dot_f64(int64_t n, const double *a, const double *b) {
     return s;
 }
 
+/* The operator of a conjgrad.m solve: a stored row-major A, or the
+ * counter-hash matrix regenerated row by row (no n*n storage). */
+typedef struct { const double *A; uint64_t seed; int hash; } f64_op;
+
+/* Rows [row0, row0+nrows) of the counter-hash A times v, each row summed in
+ * ascending column order (exactly oracle_matvec_f64 on oracle_spd_hash's A). */
+void oracle_hash_matvec_f64(int64_t n, uint64_t seed, int64_t row0, int64_t nrows, const double *v, double *out) {
+    const uint64_t ms = mix64(seed);  /* oracle_hash_u01's mix64(seed), hoisted */
+#pragma omp parallel for schedule(dynamic, 8) num_threads(g_threads)
+    for (int64_t r = 0; r < nrows; ++r) {
+        const uint64_t i = (uint64_t)(row0 + r);
+        double acc = 0.0;
+        for (int64_t jj = 0; jj < n; ++jj) {
+            const uint64_t j = (uint64_t)jj;
+            const double uij = (double)(mix64(((i << 32) | (j & 0xffffffffull)) ^ ms) >> 11) * (1.0 / 9007199254740992.0);
+            const double uji = (double)(mix64(((j << 32) | (i & 0xffffffffull)) ^ ms) >> 11) * (1.0 / 9007199254740992.0);
+            double a = 0.5 * (uij + uji);
+            if (i == j) a = a + (double)n;
+            acc = acc + a * v[jj];
+        }
+        out[r] = acc;
+    }
+}
+
+static void op_apply(const f64_op *op, int64_t n, const double *v, double *out) {
+    if (op->hash) oracle_hash_matvec_f64(n, op->seed, 0, n, v, out);
+    else oracle_matvec_f64(n, n, op->A, v, out);
+}
+
+static int cg_f64_op(int64_t n, const f64_op *op, const double *b, double *x,
+                     int64_t max_iter, double eps, oracle_stats *st);
+
 int oracle_cg_f64(int64_t n, const double *A, const double *b, double *x,
                   int64_t max_iter, double eps, oracle_stats *st) {
+    const f64_op op = {A, 0, 0};
+    return cg_f64_op(n, &op, b, x, max_iter, eps, st);
+}
+
+int oracle_cg_f64_hash(int64_t n, uint64_t seed, double *x, int64_t max_iter, double eps, oracle_stats *st) {
+    double *b = (double *)malloc((size_t)n * sizeof(double));
+    if (!b) return -1;
+    oracle_spd_hash(n, 0, n, seed, 0, NULL, b);
+    const f64_op op = {NULL, seed, 1};
+    const int rc = cg_f64_op(n, &op, b, x, max_iter, eps, st);
+    free(b);
+    return rc;
+}
+
+static int cg_f64_op(int64_t n, const f64_op *op, const double *b, double *x,
+                     int64_t max_iter, double eps, oracle_stats *st) {
     if (max_iter < 0) max_iter = n;
     double *Av = (double *)malloc((size_t)n * sizeof(double));
     double *r = (double *)malloc((size_t)n * sizeof(double));
     double *p = (double *)malloc((size_t)n * sizeof(double));
     if (!Av || !r || !p) { free(Av); free(r); free(p); return -1; }
     double t0 = now_s();
-    oracle_matvec_f64(n, n, A, x, Av);                 /* conjgrad.m:2  r=b-A*x */
+    op_apply(op, n, x, Av);                            /* conjgrad.m:2  r=b-A*x */
     for (int64_t i = 0; i < n; ++i) { r[i] = b[i] - Av[i]; p[i] = r[i]; } /* :3 */
     double rsold = oracle_dot_f64(n, r, r);            /* :4 */
     double t1 = now_s();
@@ -327,7 +375,7 @@ int oracle_cg_f64(int64_t n, const double *A, const double *b, double *x,
     int converged = 0;
     double rr = rsold;
     for (int64_t k = 0; k < max_iter; ++k) {           /* :6 for i=1:length(b) */
-        oracle_matvec_f64(n, n, A, p, Av);             /* :7 */
+        op_apply(op, n, p, Av);                        /* :7 */
         double alpha = rsold / oracle_dot_f64(n, p, Av); /* :8 */
         for (int64_t i = 0; i < n; ++i) x[i] = x[i] + alpha * p[i];  /* :9  */
         for (int64_t i = 0; i < n; ++i) r[i] = r[i] - alpha * Av[i]; /* :10 */

@@ -94,6 +94,11 @@ float oracle_combine_f32(const float *in, int cnt, int combine);
 /* conjgrad.m restated in double. */
 int oracle_cg_f64(int64_t n, const double *A, const double *b, double *x,
                   int64_t max_iter, double eps, oracle_stats *st);
+/* The same solve of the counter-hash system (oracle_spd_hash, b included)
+ * with A regenerated row by row in every matVec instead of stored: identical
+ * values and sums, no n*n memory (the configs' N = 65536 / 131072 systems). */
+void oracle_hash_matvec_f64(int64_t n, uint64_t seed, int64_t row0, int64_t nrows, const double *v, double *out);
+int oracle_cg_f64_hash(int64_t n, uint64_t seed, double *x, int64_t max_iter, double eps, oracle_stats *st);
 
 /* ---- matrix-free 2D Poisson (configs[4], no reference counterpart) ------ */
 /* out = A p for the 5-point Laplacian on an m x m interior grid, Dirichlet

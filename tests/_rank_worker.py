@@ -60,7 +60,9 @@ def main():
         if not flags & cg.CGX_F32_REF:
             flags |= cg.CGX_F64
         f32 = bool(flags & cg.CGX_F32_REF)
-        if mode == "sized":  # any n: generateSPDmatrix(n) from the oracle's MATLAB-compatible generator
+        if mode == "headline":  # configs[2]: the bench's N=65536 system, generated on the device
+            A = b = x0 = None
+        elif mode == "sized":  # any n: generateSPDmatrix(n) from the oracle's MATLAB-compatible generator
             A, b = oracle.spd_matlab(n, np.float64)
             x0 = np.zeros(n)
         else:
@@ -68,7 +70,10 @@ def main():
         with cg.Solver(n, rank=rank, nranks=P, unique_id=uid, device=0, flags=flags) as s:
             res["overlap"] = bool(s.info.flags & cg.CGX_OVERLAP_ACTIVE)
             res["nrows"] = s.info.nrows
-            s.set_system(A, b, x0)
+            if A is None:
+                s.generate_spd(42)
+            else:
+                s.set_system(A, b, x0)
             x, st = s.solve(None, eps=1e-6 if f32 else 1e-10)
             rn, bn = s.residual_norm()
             res.update(iterations=st.iterations, converged=st.converged, relres=rn / bn)

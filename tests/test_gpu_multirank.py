@@ -163,6 +163,21 @@ def test_rank_mode_world8(tmp_path, mode):
         assert np.array_equal(x, xs)
 
 
+@pytest.mark.timeout(600)
+def test_rank_mode_headline_n65536_world2(tmp_path):
+    """BASELINE configs[2] through the rank path at full size: N=65536 on 2
+    RCCL ranks (17.2 GB of A each, the overlapped allgather, the scalar
+    allreduces), generated on the device; x within 1e-10 of the fp64 oracle
+    with conjgrad.m's loop count, true residual <= 1e-10 ||b||."""
+    n, P = 65536, 2
+    x, res = run_ranks(tmp_path, "headline", n, P, timeout=500)
+    assert res[0]["nrows"] == n // P and res[0]["overlap"]
+    oracle.set_threads(16)
+    xo, so = oracle.cg_f64_hash(n, 42, eps=1e-10)
+    assert res[0]["converged"] and res[0]["iterations"] == so.iterations
+    assert rel(x, xo) <= TOL and res[0]["relres"] <= TOL
+
+
 @pytest.mark.timeout(150)
 @pytest.mark.parametrize("mode", ["peer_dies", "peer_absent"])
 def test_rank_mode_fails_fast_when_a_peer_is_gone(tmp_path, mode):

@@ -160,6 +160,23 @@ def test_nparts_dot_order():
         assert abs(sp.iterations - s1.iterations) <= 1
 
 
+def test_hash_oracle_without_storage_equals_stored():
+    """cg_f64_hash (A regenerated per matVec, for N = 65536 / 131072) == cg_f64
+    on the stored spd_hash system, bit for bit; its matVec rows likewise."""
+    n = 700
+    A, b = oracle.spd_hash(n, seed=9)
+    v = np.random.default_rng(1).random(n)
+    assert np.array_equal(oracle.hash_matvec_f64(n, v, seed=9), oracle.matvec_f64(A, v))
+    assert np.array_equal(oracle.hash_matvec_f64(n, v, seed=9, row0=100, nrows=37), oracle.matvec_f64(A[100:137], v))
+    oracle.set_threads(4)
+    try:
+        x1, s1 = oracle.cg_f64_hash(n, seed=9, eps=1e-10)
+    finally:
+        oracle.set_threads(1)
+    x2, s2 = oracle.cg_f64(A, b, np.zeros(n), eps=1e-10)
+    assert s1.iterations == s2.iterations and np.array_equal(x1, x2)
+
+
 def test_fixed_count_mode():
     A, b, x0 = case("spd512", np.float64)
     _, st = oracle.cg_f64(A, b, x0, eps=-1.0, max_iter=12)
