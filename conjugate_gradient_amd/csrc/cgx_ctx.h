@@ -144,7 +144,6 @@ constexpr int S_XNZ = 134;  // rank mode: count of ranks whose x0 is not all zer
 constexpr int S_KDONE = 132, S_RRFINAL = 133;  // device-side convergence: k+1 at the break, r.r there
 constexpr int kLookRing = 8;                    // pinned slots for the host's lagged convergence checks
 inline int ring(int64_t j) { return (int)(j & 3); }
-constexpr int kGraphIters = 4;  // a multiple of the ring period (and of the Poisson slab alternation)
 
 enum Mode { M_SINGLE = 0, M_LOCAL = 1, M_RCCL = 2 };
 enum Op { OP_DENSE = 0, OP_POISSON = 1 };
@@ -228,10 +227,6 @@ struct cgx_ctx {
     bool fused = false;    // Poisson: two-kernel fused iteration (k_poisson_p + k_poisson_xr)
     bool halo_overlap = false;  // fused Poisson, several slabs: r's halo exchange overlaps k_poisson_p
     bool halo_pending = false;  // an overlapped r halo exchange is in flight on the comm streams
-    // fixed-count iterations replayed from a hipGraph (one GPU): kGraphIters
-    // iterations captured once, the period of the scalar rings
-    hipGraphExec_t graph = nullptr;
-    bool graph_failed = false;
     // rank mode fail-fast (cgx_exchange.hip, rank_wait_*): every host wait
     // polls with a deadline of rccl_timeout_s seconds (CGX_RCCL_TIMEOUT_S,
     // default 60, 0 = wait forever) and checks the communicator's asynchronous

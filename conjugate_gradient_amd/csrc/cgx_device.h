@@ -66,6 +66,11 @@ __device__ __forceinline__ void grid_sum_last_block(double v, double *partials, 
     }
     __syncthreads();
     if (!is_last) return;
+    // Order the partial loads below after the ticket (acquire at agent scope,
+    // once per kernel in this one block).  The sc1 stores and loads already
+    // make the hand-off correct on gfx950; the fence makes it so under the
+    // HIP memory model as well, and keeps the compiler from hoisting the loads.
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     // all of this thread's partials in flight at once (grid <= 8192 = 32 * kNT)
     double s = 0.0;
     for (unsigned i0 = threadIdx.x; i0 < gridDim.x; i0 += 8 * kNT) {

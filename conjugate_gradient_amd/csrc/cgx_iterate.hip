@@ -3,7 +3,7 @@
 //     -> cgx_solve = cgx_solve_begin (:209-212) + cgx_iterate (:213-245)
 // the matVec dispatch (resident, host-streamed, symmetric, Poisson), the
 // iteration with its stopping test on the host or on the device (gating),
-// hipGraph replay, and the true-residual check.
+// and the true-residual check.
 #include "cgx_ctx.h"
 
 namespace cgxh {
@@ -150,11 +150,15 @@ int x0_is_zero(cgx_ctx *c, bool *zero) {
 int do_begin(cgx_ctx *c) {
     // r0 = p0 = b - A x0; rr0 = r0.r0   (serialConjugate.c:209-212, parallel_cg.c:283-287)
     // With x0 = 0 (the reference's usual initialguess, and the bench's) A x0 is
-    // exactly zero, so the exchange and the matVec are skipped: r0 = b - 0 = b
-    // bit for bit, one matVec fewer per solve.
+    // exactly zero for a finite A, so the exchange and the matVec are skipped:
+    // r0 = b - 0 = b bit for bit, one matVec fewer per solve.  (An A holding
+    // Inf or NaN gives NaN in A x0 at serialConjugate.c:209; cgx.h states the
+    // finite-A precondition of the fp64 mode.)  CGX_F32_REF, the mode that
+    // promises the reference's bits for any input, always does the matVec.
     TRY(settle_halo(c));
     bool zero = false;
     TRY(x0_is_zero(c, &zero));
+    if (f32ref(c)) zero = false;
     if (!zero) TRY(exchange_allgather(c, /*from_x=*/true));  // full x0 into pfull
     const int gs = S_RR + ring(0), ls = S_LRR + ring(0);
     const int os = out_slot(c, ls, gs);
@@ -368,56 +372,6 @@ int cgx_solve_begin(cgx_ctx *c) {
     return do_begin(c);
 }
 
-// Fixed-count iterations from a hipGraph: one GPU (no exchange, no host
-// reads inside an iteration), no per-launch timing events.  kGraphIters
-// iterations are captured once per context, from an iteration k >= 1 that
-// is a multiple of kGraphIters: every launch argument then repeats with that
-// period (scalar ring slots, Poisson slab parity; k == 0 alone differs), so
-// the same graph replays at k, k + 4, ...  The kernels and their order are
-// the stream path's, so the results are bitwise the same (tested).  Opt-in
-// (CGX_GRAPH=1): replays measured 1-5 % SLOWER than stream launches at
-// N = 512-16384 and on Poisson grids (profiles/r01_graph_ab.jsonl; the
-// launches are already queued ahead of a GPU-bound loop).  A capture that
-// fails falls back to stream launches.
-static bool graph_ok(const cgx_ctx *c) {
-    const char *e = std::getenv("CGX_GRAPH");
-    if (!(e && *e == '1')) return false;
-    return c->mode == M_SINGLE && !c->graph_failed && !(c->flags & (CGX_TIMING | CGX_HOST_STREAM));
-}
-
-static int graph_block(cgx_ctx *c, bool *ran) {
-    *ran = false;
-    Shard &s = c->sh[0];
-    TRY(set_dev(s));
-    if (!c->graph) {
-        const int64_t k0 = c->k, t0 = c->total_iters;
-        HIPT(hipStreamBeginCapture(s.stream, hipStreamCaptureModeThreadLocal));
-        int rc = CGX_OK;
-        for (int i = 0; i < kGraphIters && rc == CGX_OK; ++i) {
-            int stop = 0;
-            rc = do_iteration(c, -1.0, &stop);
-        }
-        hipGraph_t g = nullptr;
-        const hipError_t ec = hipStreamEndCapture(s.stream, &g);
-        c->k = k0;
-        c->total_iters = t0;
-        if (rc == CGX_OK && ec == hipSuccess && g && hipGraphInstantiate(&c->graph, g, nullptr, nullptr, 0) == hipSuccess) {
-            (void)hipGraphDestroy(g);
-        } else {
-            if (g) (void)hipGraphDestroy(g);
-            (void)hipGetLastError();
-            c->graph = nullptr;
-            c->graph_failed = true;  // stream launches from now on
-            return CGX_OK;
-        }
-    }
-    HIPT(hipGraphLaunch(c->graph, s.stream));
-    c->k += kGraphIters;
-    c->total_iters += kGraphIters;
-    *ran = true;
-    return CGX_OK;
-}
-
 // Convergence-tested iterations without a host round trip per iteration:
 // the update kernel decides sqrt(r.r) < eps on the device and records k+1;
 // queued later iterations skip themselves.  The host keeps `look` iterations
@@ -487,16 +441,7 @@ int cgx_iterate(cgx_ctx *c, int64_t count, double eps, int64_t *done, int *conve
     if (c->state == ST_BEGUN && count > 0 && eps >= 0.0 && !f32ref(c) && !(c->flags & CGX_HOST_STREAM) && gate_ok)
         return iterate_gated(c, count, eps, done, converged);
     int64_t did = 0;
-    const bool use_graph = eps < 0.0 && graph_ok(c);
     while (did < count && c->state == ST_BEGUN) {
-        if (use_graph && c->k >= kGraphIters && c->k % kGraphIters == 0 && count - did >= kGraphIters) {
-            bool ran = false;
-            TRY(graph_block(c, &ran));
-            if (ran) {
-                did += kGraphIters;
-                continue;
-            }
-        }
         int stop = 0;
         TRY(do_iteration(c, eps, &stop));
         ++did;
@@ -566,16 +511,12 @@ int cgx_set_matvec_plan(cgx_ctx *c, int rows_per_wave, int chunks_in_flight, int
     const int R = rows_per_wave, U = chunks_in_flight;
     if (R != 1 && R != 2 && R != 4 && R != 8) return fail(CGX_ERR_ARG, "rows_per_wave must be 1, 2, 4 or 8");
     if (U != 2 && U != 4 && U != 8) return fail(CGX_ERR_ARG, "chunks_in_flight must be 2, 4 or 8");
-    if (nontemporal < 0 || nontemporal > 13 || (nontemporal >= 2 && U == 2))
-        return fail(CGX_ERR_ARG, "load policy must be 0..13 (2..13 need chunks_in_flight 4 or 8)");
+    if (nontemporal != 0 && nontemporal != 1 && nontemporal != 8)
+        return fail(CGX_ERR_ARG, "load policy must be 0 (plain), 1 (non-temporal) or 8 (pipelined non-temporal)");
     for (auto &s : c->sh) {
         TRY(set_dev(s));
         MatvecPlan pl = plan_matvec_f64(s.dev, s.nloc, R, U, nontemporal, blocks_per_cu);
         s.plan = pl;
-    }
-    if (c->graph) {  // the captured launches carry the old plan
-        HIPT(hipGraphExecDestroy(c->graph));
-        c->graph = nullptr;
     }
     return CGX_OK;
 }

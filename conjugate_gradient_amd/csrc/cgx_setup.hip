@@ -490,7 +490,6 @@ int cgx_destroy(cgx_ctx *ctx) {
     // rank mode: drain with the deadline first, so a job whose peer died is
     // aborted here instead of hanging in the stream syncs below
     const int rc = (ctx->mode == M_RCCL && !ctx->dead) ? sync_all(ctx) : CGX_OK;
-    if (ctx->graph) (void)hipGraphExecDestroy(ctx->graph);
     for (auto &s : ctx->sh) free_shard(s);
     delete ctx;
     return rc;

@@ -29,6 +29,8 @@
  * Numerics (flags):
  *   CGX_F64      (default) double data and arithmetic; the fp64 reading of
  *                conjgrad.m.  Dots are deterministic fixed-order reductions.
+ *                Precondition: A is finite (with x0 = 0 the initial A x0 is
+ *                skipped as exactly zero; an Inf/NaN in A would have made it NaN).
  *   CGX_F32_REF  float data, serialConjugate.c's operation order: sequential
  *                fp32 accumulation per row and per dot, no FMA contraction.
  *                Produces the reference's x bit for bit: serialConjugate.c on
@@ -218,13 +220,11 @@ int cgx_synchronize(cgx_ctx *ctx);
 void *cgx_stream(cgx_ctx *ctx);
 /* Tuning of the fp64 matVec (k_matvec_f64): rows per wave (1,2,4,8), 128-column
  * chunks in flight per row (2,4,8), the A load policy (0 plain, 1 non-temporal
- * global loads, 2..6 buffer loads with cache bits nt / nt sc1 / sc0 nt sc1 /
- * sc1 / none, 7 software-pipelined buffer nt, 8 software-pipelined global nt
- * = default, 9 / 10 flattened pipeline global / buffer nt, 11 LDS-staged p,
- * 12 SGPR row bases, 13 SGPR row bases + LDS-staged p; 2..13 need chunks
- * 4 or 8), resident
- * blocks per CU for the grid (<= 0: occupancy query).  Results do not depend
- * on the plan's R/U/nt; the p.Ap partial order depends on the grid size. */
+ * global loads, 8 software-pipelined non-temporal = default; the variants
+ * measured and not adopted are in tools/microbench/matvec_variants.hip),
+ * resident blocks per CU for the grid (<= 0: occupancy query).  Results do not
+ * depend on the plan's R/U/policy; the p.Ap partial order depends on the grid
+ * size. */
 int cgx_set_matvec_plan(cgx_ctx *ctx, int rows_per_wave, int chunks_in_flight, int nontemporal,
                         int blocks_per_cu);
 int cgx_get_matvec_plan(cgx_ctx *ctx, int *rows_per_wave, int *chunks_in_flight, int *nontemporal,

@@ -114,17 +114,21 @@ def test_dot_and_updates_f64(n):
     assert abs(rr_d.to_host()[0] - r_ref @ r_ref) <= F64_TOL * (r_ref @ r_ref)
 
 
-MV_PLANS = [(R, U, nt) for R in (1, 2, 4, 8) for U in (4, 8) for nt in (0, 1, 2, 7, 8, 9, 10, 11, 12, 13)
-            if not (R == 8 and U == 8 and nt >= 7)] + [(R, 2, nt) for R in (1, 4) for nt in (0, 1)]
+# every plan libcgx ships: R rows per wave x U chunks in flight x load policy
+# (0 plain, 1 non-temporal, 8 pipelined non-temporal = default); R=8 U=8
+# pipelined spills and is never planned
+MV_PLANS = [(R, U, nt) for R in (1, 2, 4, 8) for U in (2, 4, 8) for nt in (0, 1, 8)
+            if not (R == 8 and U == 8 and nt == 8)]
 
 
 @pytest.mark.parametrize("rows,cols", [(300, 1000), (1000, 1024), (517, 2176), (2048, 4096), (8192, 3200)])
 def test_matvec_f64_every_plan_bitwise_equal(monkeypatch, rows, cols):
     """Every (rows per wave, chunks in flight, load policy) plan, including the
-    software-pipelined (7, 8) and flattened (9, 10) kernels and their fallback
-    when the chunk count is not a multiple of U, gives the same row sums bit
-    for bit: each lane accumulates its columns in ascending order whatever the
-    plan.  The default plan is checked against the fp64 oracle."""
+    software-pipelined kernel (8) with chunk counts that are not a multiple of
+    U, gives the same row sums bit for bit: each lane accumulates its columns
+    in ascending order whatever the plan.  The default plan is checked against
+    the fp64 oracle.  (The rejected variants are checked the same way by
+    tools/microbench/matvec_variants.hip.)"""
     rng = np.random.default_rng(rows + cols)
     A = rng.random((rows, cols)) - 0.5
     v = rng.random(cols)
