@@ -182,7 +182,8 @@ struct Shard {
     char *sym_prow = nullptr, *sym_pcol = nullptr, *sym_stage = nullptr;
     int64_t sym_stage_rows = 0;
     int sym_grid = 0;
-    hipEvent_t ev_sync = nullptr;  // cross-shard ordering (LOCAL mode)
+    hipEvent_t ev_sync = nullptr;  // cross-shard ordering (LOCAL mode): local_barrier
+    hipEvent_t ev_root = nullptr;  // CGX_COMM_P2P in LOCAL mode: shard 0's result is ready
     std::vector<hipEvent_t> ev_t;  // timing pairs (CGX_TIMING)
     int ev_used = 0;
     // CGX_HOST_STREAM: A stays in pinned host memory; row tiles are copied

@@ -145,14 +145,18 @@ int p2p_allgather(cgx_ctx *c, bool from_x) {
         if (&s == &r0 && !from_x) continue;
         HIPT(hipMemcpyPeerAsync(r0.pfull + s.row0 * es, r0.dev, from_x ? s.x : s.pown, s.dev, s.nloc * es, r0.stream));
     }
-    HIPT(hipEventRecord(r0.ev_sync, r0.stream));
+    HIPT(hipEventRecord(r0.ev_root, r0.stream));
     for (auto &d : c->sh) {
         if (&d == &r0) continue;
         TRY(set_dev(d));
-        HIPT(hipStreamWaitEvent(d.stream, r0.ev_sync, 0));
+        HIPT(hipStreamWaitEvent(d.stream, r0.ev_root, 0));
         HIPT(hipMemcpyPeerAsync(d.pfull, d.dev, r0.pfull, r0.dev, (size_t)c->n * es, d.stream));
     }
-    return CGX_OK;
+    // Shard 0 must not touch its pfull again until every shard has copied it:
+    // with from_x its very next kernels (matVec, then the residual writing p
+    // into pfull) would otherwise race the other streams' copies (seen as
+    // wrong x in about 1 solve in 5 before this barrier).
+    return local_barrier(c);
 }
 
 // allSum (point-to-point_cg.c:339-359): partials to rank 0, summed there in
@@ -201,14 +205,14 @@ int p2p_scalar(cgx_ctx *c, int lslot, int gslot) {
     else
         HIPT(sum_ordered_f64(reinterpret_cast<const double *>(slot(r0, S_GATHER)), S,
                              reinterpret_cast<double *>(slot(r0, gslot)), r0.stream));
-    HIPT(hipEventRecord(r0.ev_sync, r0.stream));
+    HIPT(hipEventRecord(r0.ev_root, r0.stream));
     for (auto &d : c->sh) {
         if (&d == &r0) continue;
         TRY(set_dev(d));
-        HIPT(hipStreamWaitEvent(d.stream, r0.ev_sync, 0));
+        HIPT(hipStreamWaitEvent(d.stream, r0.ev_root, 0));
         HIPT(hipMemcpyPeerAsync(slot(d, gslot), d.dev, slot(r0, gslot), r0.dev, 8, d.stream));
     }
-    return CGX_OK;
+    return local_barrier(c);  // as in p2p_allgather: shard 0's slots stay put until copied
 }
 
 // Every shard's pfull gets every shard's slice of `src(shard)` (its own slice

@@ -29,6 +29,7 @@ int alloc_shard(cgx_ctx *c, Shard &s) {
     const size_t es = (size_t)c->es;
     HIPT(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
     HIPT(hipEventCreateWithFlags(&s.ev_sync, hipEventDisableTiming));
+    HIPT(hipEventCreateWithFlags(&s.ev_root, hipEventDisableTiming));
     const size_t abytes = (size_t)s.nloc * (size_t)c->lda * es;
     auto dmalloc = [&](char **p, size_t bytes) -> int {
         if (bytes == 0) bytes = 16;
@@ -165,6 +166,7 @@ void free_shard(Shard &s) {
     if (s.h_rec) (void)hipHostFree(s.h_rec);
     for (auto e : s.ev_t) (void)hipEventDestroy(e);
     if (s.ev_sync) (void)hipEventDestroy(s.ev_sync);
+    if (s.ev_root) (void)hipEventDestroy(s.ev_root);
     for (int q = 0; q < kMaxCopyStreams; ++q)
         if (s.copy[q]) {
             (void)hipStreamSynchronize(s.copy[q]);

@@ -565,6 +565,22 @@ def test_p2p_exchange_mode(P):
     assert s1.iterations == so.iterations and rel(x1, xo) <= TOL
 
 
+def test_p2p_local_exchange_is_ordered():
+    """Multi-shard CGX_COMM_P2P: shard 0 gathers, then every shard copies from
+    it.  Shard 0's next kernels must wait for those copies (with x0 gathered
+    for A x0 the residual rewrote shard 0's p while the others were still
+    copying it: wrong x in about 1 solve in 5).  Repeated short fixed-count
+    solves, each bit-exact to the P-part oracle (allSum order)."""
+    A, b, x0 = case("kat4")
+    for _ in range(10):
+        for it in (1, 2, 3, 4):
+            with cg.Solver(4, flags=cg.CGX_F32_REF | cg.CGX_COMM_P2P, devices=[0, 0]) as s:
+                s.set_system(A, b, x0)
+                x, _ = s.solve(None, eps=-1.0, max_iter=it)
+            xo, _ = oracle.cg_f32ref(A, b, x0, eps=-1.0, max_iter=it, nparts=2, combine="rank")
+            assert np.array_equal(x.view(np.uint32), xo.view(np.uint32)), it
+
+
 @pytest.mark.parametrize("n,P", [(1, 1), (3, 3), (1001, 7), (1000, 8), (640, 5)])
 def test_ragged_sizes_and_blocks(n, P):
     """Odd n, row blocks of odd length (unaligned vector slices -> scalar

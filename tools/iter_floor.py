@@ -1,6 +1,9 @@
 #!/usr/bin/env python3
 """Per-iteration wall time of fixed-count CG iterations (no stopping test,
-nothing read back) on small systems: the launch-rate floor of the loop.
+nothing read back) on small systems: the launch-rate floor of the loop; the
+host's own enqueue time per iteration beside it (equal to the wall time =>
+the loop is bound by the host's launches), and the wall time of a whole
+convergence-tested solve from x0 = 0.
 
   python tools/iter_floor.py [n ...]    (default 64 512 2048 8192)
 """
@@ -23,10 +26,21 @@ def main():
         iters = 2000
         t0 = time.perf_counter()
         s.iterate(iters, eps=-1.0)
+        t1 = time.perf_counter()  # the host has enqueued every launch
         s.synchronize()
         dt = time.perf_counter() - t0
+        # convergence-tested solves from x0 = 0 (device-gated stop): per-solve wall time
+        reps = 50
+        s.solve(None, eps=1e-10)
+        t2 = time.perf_counter()
+        for _ in range(reps):
+            _, st = s.solve(None, eps=1e-10)
+        solve_ms = 1e3 * (time.perf_counter() - t2) / reps
         s.close()
-        print(json.dumps({"n": n, "iterations": iters, "us_per_iteration": 1e6 * dt / iters}), flush=True)
+        print(json.dumps({"n": n, "iterations": iters, "us_per_iteration": 1e6 * dt / iters,
+                          "host_enqueue_us_per_iteration": 1e6 * (t1 - t0) / iters,
+                          "solve_ms": solve_ms, "solve_iterations": st.iterations,
+                          "env": {k: v for k, v in os.environ.items() if k.startswith("CGX_")}}), flush=True)
 
 
 if __name__ == "__main__":
