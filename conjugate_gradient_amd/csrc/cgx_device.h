@@ -96,6 +96,74 @@ __device__ __forceinline__ void grid_sum_last_block(double v, double *partials, 
     }
 }
 
+// grid_sum_last_block's hand-off, but the last block keeps going: returns
+// true (block-uniform) in the block that summed the partials, with the total
+// in `total` for every thread of it; *out gets the total as well.  The bytes
+// the other blocks wrote in this launch are visible to that block only if
+// they were stored write-through (sc1) and are loaded with sc1 loads
+// (cdna_hip_programming.md Guideline 16, the one-counter row).
+__device__ __forceinline__ bool grid_sum_keep_last(double v, double *partials, unsigned *ticket, double *out,
+                                                   double &total) {
+    __shared__ double red[kNT / 64];
+    __shared__ int is_last;
+    __shared__ double tot;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    v = wave_sum(v);
+    if (lane == 0) red[wid] = v;
+    __syncthreads();
+    if (gridDim.x == 1) {  // the same bits as the hand-off below (which adds to 0.0)
+        if (threadIdx.x == 0) {
+            double t = red[0];
+#pragma unroll
+            for (int w = 1; w < kNT / 64; ++w) t += red[w];
+            tot = 0.0 + t;
+            *out = tot;
+        }
+        __syncthreads();
+        total = tot;
+        return true;
+    }
+    if (threadIdx.x == 0) {
+        double t = red[0];
+#pragma unroll
+        for (int w = 1; w < kNT / 64; ++w) t += red[w];
+        __hip_atomic_store(partials + blockIdx.x, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+        const unsigned prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        is_last = (prev == gridDim.x - 1);
+    }
+    __syncthreads();
+    if (!is_last) return false;
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+    double s = 0.0;
+    for (unsigned i0 = threadIdx.x; i0 < gridDim.x; i0 += 8 * kNT) {
+        double pv[8];
+#pragma unroll
+        for (int u = 0; u < 8; ++u) {
+            const unsigned i = i0 + u * kNT;
+            pv[u] = (i < gridDim.x) ? __hip_atomic_load(partials + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < 8; ++u)
+            if (i0 + u * kNT < gridDim.x) s += pv[u];
+    }
+    s = wave_sum(s);
+    __syncthreads();  // red[] is reused
+    if (lane == 0) red[wid] = s;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        double t = red[0];
+#pragma unroll
+        for (int w = 1; w < kNT / 64; ++w) t += red[w];
+        tot = t;
+        *out = t;
+        __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    }
+    __syncthreads();
+    total = tot;
+    return true;
+}
+
 __device__ __forceinline__ d2 ld2(const double *p) { return *reinterpret_cast<const d2 *>(p); }
 __device__ __forceinline__ void st2(double *p, d2 v) { *reinterpret_cast<d2 *>(p) = v; }
 

@@ -276,8 +276,40 @@ int do_iteration_poisson(cgx_ctx *c, double eps, int *stop, bool gated) {
 // as the reference breaks at :235-238).
 // gated: fp64 device-side convergence (the host does not read r.r here; the
 // update kernel decides sqrt(r.r) < eps and later kernels skip themselves).
+// The two-launch iteration of a small dense fp64 system on one GPU
+// (c->fused_p): the matVec with its fused p.Ap, then k_update_xrp_f64, whose
+// last block decides the stop and forms p for the next iteration.  The same
+// expressions in the same order as the three launches below (bitwise the same
+// x), one kernel boundary and one host launch fewer per iteration.
+static int do_iteration_fused_p(cgx_ctx *c, double eps, int *stop, bool gated) {
+    const int64_t k = c->k;
+    *stop = 0;
+    Shard &s = c->sh[0];
+    const int pg = S_PAP + ring(k), rg = S_RR + ring(k + 1);
+    auto D = [](void *q) { return reinterpret_cast<double *>(q); };
+    TRY(launch_matvec(c, s, s.pfull, true, pg, gated));  // serialConjugate.c:215,219
+    HIPT(update_xrp_f64(s.nloc, D(s.x), D(s.r), D(s.pown), D(s.Ap), D(slot(s, S_RR + ring(k))), D(slot(s, pg)),
+                        D(slot(s, rg)), s.ws, s.stream, gate_of(s, gated), gated ? eps : -1.0, k,
+                        gated ? reinterpret_cast<int64_t *>(slot(s, S_KDONE)) : nullptr,
+                        gated ? D(slot(s, S_RRFINAL)) : nullptr, rec_of(c, s, gated)));  // :221-243
+    c->k = k + 1;
+    c->total_iters += 1;
+    if (!gated && eps >= 0.0) {  // host-checked stop; x is already current
+        double rr = 0.0;
+        TRY(read_scalar(c, rg, &rr));
+        c->last_rr = rr;
+        if (std::sqrt(rr) < eps) {
+            c->converged = 1;
+            c->state = ST_CONVERGED;
+            *stop = 1;
+        }
+    }
+    return CGX_OK;
+}
+
 int do_iteration(cgx_ctx *c, double eps, int *stop, bool gated) {
     if (c->fused) return do_iteration_poisson(c, eps, stop, gated);
+    if (c->fused_p) return do_iteration_fused_p(c, eps, stop, gated);
     const int64_t k = c->k;
     *stop = 0;
     const int pg = S_PAP + ring(k), pl = S_LPAP + ring(k);

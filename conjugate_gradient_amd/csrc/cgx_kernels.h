@@ -62,6 +62,12 @@ hipError_t update_p_f64(int64_t n, double *p, const double *r, const double *rr,
 // once *kdone is in (0, k] both kernels (update_r via gate) do nothing.
 hipError_t update_r_f64(int64_t n, double *r, const double *Ap, const double *rsold, const double *pAp,
                         double *rr_out, const RedWs &ws, hipStream_t s, const int64_t *gate = nullptr);
+// The two-launch iteration's update (one GPU, small n): x += alpha p;
+// r -= alpha Ap; *rr_out = r.r; then (last block) the stopping decision as
+// update_xp's, and unless stopped p = r + (*rr_out / *rsold) p.
+hipError_t update_xrp_f64(int64_t n, double *x, double *r, double *p, const double *Ap, const double *rsold,
+                          const double *pAp, double *rr_out, const RedWs &ws, hipStream_t s, const int64_t *gate,
+                          double eps, int64_t k, int64_t *kdone, double *rrfinal, int64_t *hrec);
 hipError_t update_xp_f64(int64_t n, double *x, double *p, const double *r, const double *rsold, const double *pAp,
                          const double *rr, hipStream_t s, double eps = -1.0, int64_t k = 0,
                          int64_t *kdone = nullptr, double *rrfinal = nullptr, int64_t *hrec = nullptr);

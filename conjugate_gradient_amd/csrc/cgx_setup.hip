@@ -239,8 +239,24 @@ int alloc_overlap(cgx_ctx *c) {
     return CGX_OK;
 }
 
+// The two-launch dense iteration (do_iteration_fused_p): one GPU, fp64,
+// resident row-major A, n up to kFusePMax by default (the p update then runs
+// in one block: n doubles read twice and written once by one CU, a few us at
+// n = 8192); CGX_FUSE_P=0 keeps three launches, =1 uses two at any n.
+constexpr int64_t kFusePMax = 8192;
+static bool can_fuse_p(const cgx_ctx *c) {
+    if (c->mode != M_SINGLE || c->op != OP_DENSE || f32ref(c)) return false;
+    if (c->flags & (CGX_SYMMETRIC | CGX_HOST_STREAM)) return false;
+    if (c->n * 8 > INT32_MAX) return false;
+    const char *e = std::getenv("CGX_FUSE_P");
+    if (e && *e == '0') return false;
+    if (e && *e == '1') return true;
+    return c->n <= kFusePMax;
+}
+
 int finish_create(cgx_ctx *c, cgx_ctx **out) {
     c->overlap = can_overlap(c);
+    c->fused_p = can_fuse_p(c);
     if (c->op == OP_POISSON) {  // CGX_POISSON_FUSED=0: the three-kernel split (stencil, r, x/p)
         const char *e = std::getenv("CGX_POISSON_FUSED");
         c->fused = !(e && *e == '0') && poisson_fusable(c->sh[0].nloc / c->m, c->m);
@@ -507,7 +523,7 @@ int cgx_get_info(const cgx_ctx *c, cgx_info *info) {
     info->row0 = c->sh[0].row0;
     info->nrows = 0;
     for (auto &s : c->sh) info->nrows += s.nloc;
-    info->flags = c->flags | (c->overlap ? CGX_OVERLAP_ACTIVE : 0) | (c->fused ? CGX_FUSED_ACTIVE : 0);
+    info->flags = c->flags | (c->overlap ? CGX_OVERLAP_ACTIVE : 0) | ((c->fused || c->fused_p) ? CGX_FUSED_ACTIVE : 0);
     info->elem_bytes = c->es;
     return CGX_OK;
 }

@@ -119,6 +119,105 @@ __global__ __launch_bounds__(kNT) void k_update_p_f64(int64_t n, double *__restr
     }
 }
 
+// The two-launch iteration (small systems, one GPU; cgx_iterate.hip): after
+// the matVec (with its fused p.Ap) ONE kernel does
+//   x += alpha p; r -= alpha Ap; r.r                 (every block, its rows)
+// and the block that sums the r.r partials then decides the stop
+// (serialConjugate.c:235) and, if the loop goes on, forms
+//   p = r + (r.r / rsold) p                          (the whole vector)
+// -- the update kernel of the three-launch iteration folded into this one's
+// last block.  r crosses blocks inside the launch, so it is stored
+// write-through (sc1) and that block reads it with sc1 loads (Guideline 16's
+// one-counter row).  The expressions are the three-launch kernels' own, so
+// x, r, p and r.r come out bit for bit the same.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t vec_rsrc(const double *p, int64_t n) {
+    return __builtin_amdgcn_make_buffer_rsrc((void *)p, 0, (int)(n * 8), 0x00020000);
+}
+__device__ __forceinline__ void st2_sc1(__amdgpu_buffer_rsrc_t rs, int64_t i, d2 v) {
+    typedef unsigned int u4 __attribute__((ext_vector_type(4)));
+    __builtin_amdgcn_raw_buffer_store_b128(__builtin_bit_cast(u4, v), rs, (int)(i * 8), 0, 16);  // aux 16 = sc1
+}
+__device__ __forceinline__ d2 ld2_sc1(__amdgpu_buffer_rsrc_t rs, int64_t i) {
+    return __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(rs, (int)(i * 8), 0, 16));
+}
+
+template <bool VEC>
+__global__ __launch_bounds__(kNT) void k_update_xrp_f64(int64_t n, double *__restrict__ x, double *__restrict__ r,
+                                                        double *__restrict__ p, const double *__restrict__ Ap,
+                                                        const double *rsold, const double *pAp, double *rr_out,
+                                                        double *partials, unsigned *ticket, const int64_t *gate,
+                                                        ConvArgs cv) {
+    if (gate && *gate) return;
+    const double rs = *rsold;
+    const double alpha = rs / *pAp;
+    const __amdgpu_buffer_rsrc_t rrs = vec_rsrc(r, n);
+    double acc = 0.0;
+    if constexpr (VEC) {
+        CGX_VEC_LOOP_BEGIN
+        d2 xv[kVU], rv[kVU], pv[kVU], av[kVU];
+#pragma unroll
+        for (int u = 0; u < kVU; ++u)
+            if (ok[u]) {
+                const int64_t i = 2 * (base + u * kNT);
+                xv[u] = ld2(x + i); rv[u] = ld2(r + i); pv[u] = ld2(p + i); av[u] = ld2(Ap + i);
+            }
+#pragma unroll
+        for (int u = 0; u < kVU; ++u)
+            if (ok[u]) {
+                const int64_t i = 2 * (base + u * kNT);
+                st2(x + i, xv[u] + alpha * pv[u]);
+                const d2 ri = rv[u] - alpha * av[u];
+                st2_sc1(rrs, i, ri);
+                acc += ri.x * ri.x + ri.y * ri.y;
+            }
+        CGX_VEC_LOOP_END
+        if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+            const int64_t i = n - 1;
+            x[i] = x[i] + alpha * p[i];
+            const double ri = r[i] - alpha * Ap[i];
+            __hip_atomic_store(r + i, ri, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            acc += ri * ri;
+        }
+    } else {
+        for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kNT) {
+            x[i] = x[i] + alpha * p[i];
+            const double ri = r[i] - alpha * Ap[i];
+            __hip_atomic_store(r + i, ri, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+            acc += ri * ri;
+        }
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's r stores land before the ticket
+    double rr;
+    if (!grid_sum_keep_last(acc, partials, ticket, rr_out, rr)) return;
+    // ---- the last block: the stopping test, then p = r + beta p for all of p
+    if (cv.kdone && cv.eps >= 0.0 && sqrt(rr) < cv.eps) {
+        if (threadIdx.x == 0) record_convergence(cv, cv.k + 1, rr);
+        return;
+    }
+    const double beta = rr / rs;
+    if constexpr (VEC) {
+        const int64_t npairs = n >> 1;
+        for (int64_t b0 = threadIdx.x; b0 < npairs; b0 += (int64_t)kNT * kVU) {
+            d2 rv[kVU], pv[kVU];
+#pragma unroll
+            for (int u = 0; u < kVU; ++u)
+                if (b0 + u * kNT < npairs) {
+                    const int64_t i = 2 * (b0 + u * kNT);
+                    rv[u] = ld2_sc1(rrs, i);
+                    pv[u] = ld2(p + i);
+                }
+#pragma unroll
+            for (int u = 0; u < kVU; ++u)
+                if (b0 + u * kNT < npairs) st2(p + 2 * (b0 + u * kNT), rv[u] + beta * pv[u]);
+        }
+        if ((n & 1) && threadIdx.x == 0)
+            p[n - 1] = __hip_atomic_load(r + n - 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + beta * p[n - 1];
+    } else {
+        for (int64_t i = threadIdx.x; i < n; i += kNT)
+            p[i] = __hip_atomic_load(r + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + beta * p[i];
+    }
+}
+
 // The solver's split of the x/r/p updates (fp64): x's update moves into the
 // p update, which reads p anyway -- 24 + 40 B per element instead of 48 + 24.
 // r -= alpha Ap; r.r   (alpha = rsold / pAp)
@@ -330,6 +429,22 @@ hipError_t update_r_f64(int64_t n, double *r, const double *Ap, const double *rs
     const bool vec = al16(r) && al16(Ap);
     hipLaunchKernelGGL(vec ? k_update_r_f64<true> : k_update_r_f64<false>, dim3(grid_vec(n)), dim3(kNT), 0, s, n, r,
                        Ap, rsold, pAp, rr_out, ws.partials, ws.tickets + T_XR, gate);
+    return hipGetLastError();
+}
+
+hipError_t update_xrp_f64(int64_t n, double *x, double *r, double *p, const double *Ap, const double *rsold,
+                          const double *pAp, double *rr_out, const RedWs &ws, hipStream_t s, const int64_t *gate,
+                          double eps, int64_t k, int64_t *kdone, double *rrfinal, int64_t *hrec) {
+    if (n * 8 > INT32_MAX) return hipErrorInvalidValue;  // buffer-resource offsets are 32-bit
+    const bool vec = al16(x) && al16(r) && al16(p) && al16(Ap);
+    ConvArgs cv;
+    cv.eps = eps;
+    cv.k = k;
+    cv.kdone = kdone;
+    cv.rrfinal = rrfinal;
+    cv.hrec = hrec;
+    hipLaunchKernelGGL(vec ? k_update_xrp_f64<true> : k_update_xrp_f64<false>, dim3(grid_vec(n)), dim3(kNT), 0, s,
+                       n, x, r, p, Ap, rsold, pAp, rr_out, ws.partials, ws.tickets + T_XR, gate, cv);
     return hipGetLastError();
 }
 

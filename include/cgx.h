@@ -77,10 +77,15 @@ extern "C" {
                                   (on by default when every row block is a
                                   multiple of 128 rows; env CGX_OVERLAP=0) */
 #define CGX_OVERLAP_ACTIVE 0x800 /* reported in cgx_info.flags when it is on */
-#define CGX_FUSED_ACTIVE 0x2000 /* reported in cgx_info.flags: the Poisson
-                                   operator runs the fused two-kernel iteration
-                                   (even m; env CGX_POISSON_FUSED=0 selects the
-                                   stencil / r / x,p three-kernel split) */
+#define CGX_FUSED_ACTIVE 0x2000 /* reported in cgx_info.flags: a fused
+                                   iteration is on -- the Poisson operator's
+                                   two-kernel iteration (even m; env
+                                   CGX_POISSON_FUSED=0 selects the stencil /
+                                   r / x,p three-kernel split), or a small
+                                   dense fp64 system on one GPU iterating in
+                                   two launches instead of three (n <= 8192;
+                                   env CGX_FUSE_P=0 / 1: never / any n);
+                                   results are the same bits either way */
 #define CGX_COMM_P2P     0x1000 /* point-to-point_cg.c's exchange instead of
                                    collectives: gather to rank 0, then rank 0
                                    sends to every rank (ncclSend/Recv; device

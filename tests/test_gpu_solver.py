@@ -346,6 +346,40 @@ def test_f32ref_nonfinite_A_follows_the_reference():
     assert np.array_equal(np.isnan(x), np.isnan(xo)) and np.isnan(x).any()
 
 
+@pytest.mark.parametrize("n,seed", [(512, 1), (1000, 2), (8192, 3), (8193, 4)])
+def test_two_launch_iteration_bitwise_equals_three(monkeypatch, n, seed):
+    """Small dense fp64 systems on one GPU iterate in two launches (matVec +
+    k_update_xrp_f64, whose last block forms p; CGX_FUSE_P) instead of three.
+    Same expressions, same order: x bit for bit and the same loop count as the
+    three-launch iteration -- device-gated, host-checked and fixed-count; with
+    several blocks (n = 8192: r handed to the last block write-through) and
+    odd n.  Both agree with the fp64 oracle."""
+    A, b = oracle.spd_hash(n, seed=seed)
+    res = {}
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("CGX_FUSE_P", fuse)
+        for gated in ("1", "0"):
+            monkeypatch.setenv("CGX_GATED", gated)
+            with cg.Solver(n) as s:
+                assert bool(s.info.flags & cg.CGX_FUSED_ACTIVE) == (fuse == "1")
+                s.set_system(A, b)
+                x, st = s.solve(np.zeros(n), eps=1e-10)
+                xf, stf = s.solve(np.zeros(n), eps=-1.0, max_iter=9)
+                s.set_x(np.zeros(n))
+                s.begin()
+                d1, _ = s.iterate(3)
+                d2, conv = s.iterate(100, eps=1e-10)
+                xp = s.get_x()
+            res[(fuse, gated)] = (x, st.iterations, xf, stf.iterations, xp, d1 + d2, conv)
+    ref = res[("0", "0")]
+    for key, (x, it, xf, itf, xp, dp, conv) in res.items():
+        assert it == ref[1] and np.array_equal(x, ref[0]), key
+        assert itf == 9 and np.array_equal(xf, ref[2]), key
+        assert conv and dp == it and np.array_equal(xp, ref[0]), key
+    xo, so = oracle.cg_f64(A, b, np.zeros(n), eps=1e-10)
+    assert ref[1] == so.iterations and rel(ref[0], xo) <= TOL
+
+
 def test_errors_are_reported():
     with cg.Solver(8) as s:
         with pytest.raises(cg.CgxError) as ei:

@@ -12,6 +12,8 @@ import os
 import sys
 import time
 
+import numpy as np
+
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import conjugate_gradient_amd as cg  # noqa: E402
 
@@ -31,10 +33,11 @@ def main():
         dt = time.perf_counter() - t0
         # convergence-tested solves from x0 = 0 (device-gated stop): per-solve wall time
         reps = 50
-        s.solve(None, eps=1e-10)
+        x0 = np.zeros(n)
+        s.solve(x0, eps=1e-10)
         t2 = time.perf_counter()
         for _ in range(reps):
-            _, st = s.solve(None, eps=1e-10)
+            _, st = s.solve(x0, eps=1e-10)
         solve_ms = 1e3 * (time.perf_counter() - t2) / reps
         s.close()
         print(json.dumps({"n": n, "iterations": iters, "us_per_iteration": 1e6 * dt / iters,
