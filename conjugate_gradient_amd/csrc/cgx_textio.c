@@ -2,13 +2,23 @@
  * cgx_textio.c -- text reader for dimensions.txt / matrixA.txt / vectorb.txt /
  * initialguess.txt (see cgx_textio.h).  Host C, pthreads.
  *
- * The file is memory-mapped; each thread counts, then parses, one slice cut
- * at a separator.  Each number is converted on its own, exactly as strtof
- * (== fscanf "%f", serialConjugate.c:96) or strtod would (an exact fast path
- * below, those functions otherwise), so the result does not depend on how
- * the file is split among threads.  Separators are whitespace, ',' ';' and any
- * byte >= 0x80 (so a stray UTF-8 BOM, as in the reference's
- * initialguess1.txt, is skipped rather than mis-parsed).
+ * The reference reads with `fscanf(reader, "%f%*c", &v)` once per value
+ * (serialConjugate.c:96, parallel_cg.c:159): skip white space, take the
+ * longest prefix the %f conversion accepts, then consume exactly ONE more
+ * byte whatever it is.  This reader follows that rule byte for byte, so
+ * "1.5-2.0" reads as 1.5 and 2.0 (the '-' is the consumed byte), CRLF and a
+ * trailing byte-order mark after a number are consumed the same way, and
+ * "1.0,,2.0" stops where the reference's conversions start to fail.  Where
+ * the reference would go on with uninitialised values (a failed conversion,
+ * end of file, a missing file) this reader returns an error instead
+ * (INTEGRATION.md lists the divergences; tests/test_abi.py pins both against
+ * the reference's own initialize()).
+ *
+ * The file is memory-mapped and cut into one slice per thread at white space
+ * (where %f skips anyway, so the cut changes nothing); each thread counts,
+ * then parses, its slice.  Each number is converted on its own, exactly as
+ * strtof (what glibc's %f calls on the accepted characters) or strtod would
+ * (an exact fast path below, those functions otherwise).
  */
 #define _GNU_SOURCE
 #include "cgx_textio.h"
@@ -24,16 +34,73 @@
 #include <sys/stat.h>
 #include <unistd.h>
 
-/* Separators: whitespace, ',' ';' NUL and bytes >= 0x80 (a UTF-8 BOM). */
-static unsigned char kSep[256];
-static pthread_once_t kSepOnce = PTHREAD_ONCE_INIT;
-static void init_sep(void) {
-    const char *s = " \n\r\t\v\f,;";
-    for (const char *q = s; *q; ++q) kSep[(unsigned char)*q] = 1;
-    kSep[0] = 1;
-    for (int ch = 0x80; ch < 256; ++ch) kSep[ch] = 1;
+/* White space of the C locale (what %f skips): ' ' \t \n \v \f \r. */
+static unsigned char kSpace[256];
+static pthread_once_t kSpaceOnce = PTHREAD_ONCE_INIT;
+static void init_space(void) {
+    const char *s = " \t\n\v\f\r";
+    for (const char *q = s; *q; ++q) kSpace[(unsigned char)*q] = 1;
 }
-#define IS_SEP(ch) (kSep[(unsigned char)(ch)])
+#define IS_SPACE(ch) (kSpace[(unsigned char)(ch)])
+
+static inline int lower(char ch) { return (ch >= 'A' && ch <= 'Z') ? ch - 'A' + 'a' : ch; }
+static inline int is_digit(char ch) { return (unsigned)(ch - '0') < 10u; }
+static inline int is_xdigit(char ch) { return is_digit(ch) || ((unsigned)(lower(ch) - 'a') < 6u); }
+static inline int match_word(const char *p, const char *end, const char *w) {
+    for (; *w; ++w, ++p)
+        if (p >= end || lower(*p) != *w) return 0;
+    return 1;
+}
+
+/* The characters glibc's scanf %f consumes from p (C locale), probed against
+ * glibc 2.35 fscanf: a sign, then inf / infinity / nan (a '(' after nan is
+ * NOT taken), a hexadecimal float (0x...), or decimal digits with an optional
+ * '.' and an optional exponent -- an exponent marker (and its sign) is taken
+ * even with no digits after it ("1e+" reads as 1).  Returns the end of what
+ * it consumes; *ok = 0 where the conversion fails (a lone sign or '.', "0x"
+ * with nothing after, "infinit", ...): the reference's fscanf stops there. */
+static const char *scan_number(const char *p, const char *end, int *ok) {
+    *ok = 0;
+    if (p < end && (*p == '+' || *p == '-')) ++p;
+    if (p >= end) return p;
+    if (lower(*p) == 'i') {
+        if (!match_word(p, end, "inf")) return p + 1;
+        p += 3;
+        if (p < end && lower(*p) == 'i') {  /* "infinity" or nothing */
+            if (!match_word(p, end, "inity")) return p + 1;
+            p += 5;
+        }
+        *ok = 1;
+        return p;
+    }
+    if (lower(*p) == 'n') {
+        if (!match_word(p, end, "nan")) return p + 1;
+        *ok = 1;
+        return p + 3;
+    }
+    int hex = 0, digits = 0, dot = 0;
+    if (*p == '0' && p + 1 < end && lower(p[1]) == 'x') {
+        hex = 1;
+        p += 2;
+    }
+    while (p < end && (hex ? is_xdigit(*p) : is_digit(*p))) { ++p; ++digits; }
+    if (p < end && *p == '.') {
+        ++p;
+        dot = 1;
+        while (p < end && (hex ? is_xdigit(*p) : is_digit(*p))) { ++p; ++digits; }
+    }
+    if (!digits) {  /* glibc converts "0x." (to 0) and takes no exponent after it */
+        *ok = hex && dot;
+        return p;
+    }
+    if (p < end && lower(*p) == (hex ? 'p' : 'e')) {
+        ++p;
+        if (p < end && (*p == '+' || *p == '-')) ++p;
+        while (p < end && is_digit(*p)) ++p;
+    }
+    *ok = 1;
+    return p;
+}
 
 /* Exact fast path (Clinger): a token [+-]digits[.digits][(e|E)[+-]digits]
  * with at most 19 significant digits m < 2^53 and decimal exponent |e| <= 22
@@ -43,8 +110,8 @@ static void init_sep(void) {
  * on a float rounding midpoint (its 29 bits below float precision are
  * 1000...0), which is sent to strtof, as are subnormal / overflowing floats.
  * Anything else (long mantissas, big exponents, inf/nan, hex) uses
- * strtof/strtod.  Parses from p up to the first separator (or end); returns
- * the token end, or NULL to fall back. */
+ * strtof/strtod.  Converts the number [p, end) (scan_number's span); returns
+ * end, or NULL to fall back. */
 static const double kPow10[23] = {1e0,  1e1,  1e2,  1e3,  1e4,  1e5,  1e6,  1e7,  1e8,  1e9,  1e10, 1e11,
                                   1e12, 1e13, 1e14, 1e15, 1e16, 1e17, 1e18, 1e19, 1e20, 1e21, 1e22};
 
@@ -85,7 +152,7 @@ static inline const char *fast_number(const char *p, const char *end, int as_flo
         if (!edig) return NULL;
         e10 += eneg ? -ev : ev;
     }
-    if (p < end && !IS_SEP(*p)) return NULL; /* trailing garbage: let strto* decide */
+    if (p != end) return NULL; /* hex, inf, nan, ...: strto* */
     double d;
     if (m == 0) {
         d = 0.0;
@@ -111,7 +178,8 @@ static inline const char *fast_number(const char *p, const char *end, int as_flo
 }
 
 /* strtof / strtod on a NUL-terminated copy of [p, tok_end) (the mapping has
- * no terminator).  Returns 0 or -3 if the token is not a whole number. */
+ * no terminator), as glibc's %f does on the characters it took: the value is
+ * what strtof makes of them ("1e+" -> 1); -3 if it converts nothing. */
 static int slow_number(const char *p, const char *tok_end, int as_float, void *out, int64_t idx) {
     char tmp[128];
     size_t n = (size_t)(tok_end - p);
@@ -126,7 +194,7 @@ static int slow_number(const char *p, const char *tok_end, int as_float, void *o
     char *stop = NULL;
     if (as_float) ((float *)out)[idx] = strtof(s, &stop);
     else ((double *)out)[idx] = strtod(s, &stop);
-    const int ok = stop == s + n && n > 0;
+    const int ok = stop > s;
     free(heap);
     return ok ? 0 : -3;
 }
@@ -141,7 +209,7 @@ typedef struct {
 
 static int open_text(const char *path, text_buf *tb) {
     memset(tb, 0, sizeof *tb);
-    pthread_once(&kSepOnce, init_sep);
+    pthread_once(&kSpaceOnce, init_space);
     int fd = open(path, O_RDONLY);
     if (fd < 0) return -1;
     struct stat st;
@@ -185,21 +253,31 @@ static void close_text(text_buf *tb) {
     free(tb->heap);
 }
 
-static int64_t count_tokens(const char *p, const char *end) {
+/* The reference's read loop over [p, end): skip white space, a number, one
+ * more byte.  Counts the numbers; *bad = 1 if it stopped at a place where the
+ * conversion fails (nothing after that is reachable). */
+static int64_t count_tokens(const char *p, const char *end, int *bad) {
     int64_t c = 0;
-    int in = 0;
-    for (; p < end; ++p) {
-        const int sep = IS_SEP(*p);
-        c += (!sep) & (!in);
-        in = !sep;
+    *bad = 0;
+    for (;;) {
+        while (p < end && IS_SPACE(*p)) ++p;
+        if (p >= end) return c;
+        int ok;
+        const char *q = scan_number(p, end, &ok);
+        if (!ok) {
+            *bad = 1;
+            return c;
+        }
+        ++c;
+        p = q < end ? q + 1 : q;  /* %*c */
     }
-    return c;
 }
 
 int64_t cgx_text_count(const char *path) {
     text_buf tb;
     if (open_text(path, &tb) != 0) return -1;
-    int64_t c = count_tokens(tb.data, tb.data + tb.len);
+    int bad;
+    int64_t c = count_tokens(tb.data, tb.data + tb.len, &bad);
     close_text(&tb);
     return c;
 }
@@ -207,7 +285,8 @@ int64_t cgx_text_count(const char *path) {
 typedef struct {
     const char *beg, *end;  /* chunk [beg, end), both at token boundaries */
     int64_t first;          /* index of the chunk's first token            */
-    int64_t ntok;           /* tokens in the chunk                         */
+    int64_t ntok;           /* numbers in the chunk                         */
+    int bad;                /* the chunk stops at a failing conversion      */
     int64_t count;          /* total tokens wanted                         */
     int as_float;
     void *out;
@@ -216,7 +295,7 @@ typedef struct {
 
 static void *count_job(void *arg) {
     chunk_t *c = (chunk_t *)arg;
-    c->ntok = count_tokens(c->beg, c->end);
+    c->ntok = count_tokens(c->beg, c->end, &c->bad);
     return NULL;
 }
 
@@ -226,16 +305,15 @@ static void *parse_job(void *arg) {
     int64_t idx = c->first;
     c->status = 0;
     while (idx < c->count) {
-        while (p < end && IS_SEP(*p)) ++p;
+        while (p < end && IS_SPACE(*p)) ++p;
         if (p >= end) break;
-        const char *q = fast_number(p, end, c->as_float, c->out, idx);
-        if (!q) {
-            q = p;
-            while (q < end && !IS_SEP(*q)) ++q;
-            if (slow_number(p, q, c->as_float, c->out, idx) != 0) { c->status = -3; return NULL; }
-        }
+        int ok;
+        const char *q = scan_number(p, end, &ok);
+        if (!ok) { c->status = -3; return NULL; }
+        if (!fast_number(p, q, c->as_float, c->out, idx) &&
+            slow_number(p, q, c->as_float, c->out, idx) != 0) { c->status = -3; return NULL; }
         ++idx;
-        p = q;
+        p = q < end ? q + 1 : q;  /* %*c */
     }
     return NULL;
 }
@@ -249,12 +327,12 @@ int cgx_text_read(const char *path, int64_t count, int as_float, void *out, int 
     if (threads > 64) threads = 64;
     if (len < (size_t)threads * 4096) threads = 1;
     chunk_t ch[64];
-    /* split at separators so no token straddles two chunks */
+    /* cut at white space: %f skips it, so a cut changes nothing */
     const char *pos = buf, *end = buf + len;
     for (int t = 0; t < threads; ++t) {
         const char *stop = (t == threads - 1) ? end : buf + (len * (size_t)(t + 1)) / (size_t)threads;
         if (stop < pos) stop = pos;
-        while (stop < end && !IS_SEP(*stop)) ++stop;
+        while (stop < end && !IS_SPACE(*stop)) ++stop;
         ch[t].beg = pos;
         ch[t].end = stop;
         ch[t].count = count;
@@ -267,12 +345,15 @@ int cgx_text_read(const char *path, int64_t count, int as_float, void *out, int 
     for (int t = 1; t < threads; ++t) pthread_create(&tid[t], NULL, count_job, &ch[t]);
     count_job(&ch[0]);
     for (int t = 1; t < threads; ++t) pthread_join(tid[t], NULL);
+    /* numbers reachable in file order: up to the first failing conversion */
     int64_t total = 0;
+    int bad = 0;
     for (int t = 0; t < threads; ++t) {
         ch[t].first = total;
-        total += ch[t].ntok;
+        if (!bad) total += ch[t].ntok;
+        bad = bad || ch[t].bad;
     }
-    if (total < count) { close_text(&tb); return -2; }
+    if (total < count) { close_text(&tb); return bad ? -3 : -2; }
     for (int t = 1; t < threads; ++t) pthread_create(&tid[t], NULL, parse_job, &ch[t]);
     parse_job(&ch[0]);
     for (int t = 1; t < threads; ++t) pthread_join(tid[t], NULL);

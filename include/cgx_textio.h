@@ -2,12 +2,14 @@
  * cgx_textio.h -- reader for the reference's text formats (host C).
  *
  * Replaces initialize() (serialConjugate.c:85-105, parallel_cg.c:147-168):
- * one number per line (any single separator after each number is accepted,
- * like fscanf("%f%*c")), A row-major, b and x0 one entry per line, and
- * dimensions.txt ("rows cols" of A then of b).  Differences, by design: a
- * missing file or a short / malformed file is an error instead of silently
- * leaving uninitialised memory (serialConjugate.c:101-104), and N is taken at
- * run time instead of from `#define ROWS`.
+ * reads value after value exactly as the reference's fscanf("%f%*c") loop
+ * does (white space skipped, the longest prefix glibc's %f accepts, then one
+ * more byte consumed whatever it is): A row-major, b and x0 one entry per
+ * line, and dimensions.txt ("rows cols" of A then of b).  Differences, by
+ * design: a missing file, a short file, or a requested
+ * value at or after a failing conversion is an error instead of silently
+ * leaving uninitialised memory (serialConjugate.c:101-104), and N is taken
+ * at run time instead of from `#define ROWS`.
  */
 #ifndef CGX_TEXTIO_H
 #define CGX_TEXTIO_H
@@ -17,13 +19,15 @@
 extern "C" {
 #endif
 
-/* Counts the numbers in a text file.  Returns -1 if it cannot be opened. */
+/* Counts the numbers the reference's loop would convert before its first
+ * failing conversion or end of file.  Returns -1 if it cannot be opened. */
 int64_t cgx_text_count(const char *path);
 
 /* Reads exactly `count` numbers (the first `count` in the file) into out
- * (float if as_float, else double).  0 on success; -1 cannot open; -2 fewer
- * than `count` numbers; -3 malformed token.  `threads` > 1 parses in
- * parallel chunks (same values: every token is converted independently). */
+ * (float if as_float, else double: strtof / strtod of the characters %f
+ * takes).  0 on success; -1 cannot open; -2 fewer than `count` numbers; -3 a
+ * conversion fails before `count` numbers.  `threads` > 1 parses in parallel
+ * slices cut at white space (same values). */
 int cgx_text_read(const char *path, int64_t count, int as_float, void *out, int threads);
 
 /* dimensions.txt: four integers "A_rows A_cols b_rows b_cols".  0 or <0. */

@@ -27,6 +27,7 @@
  * own timing line.
  */
 #define _POSIX_C_SOURCE 200809L
+#include <stdint.h>
 #include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
@@ -61,10 +62,17 @@ static double now_s(void) {
 }
 
 /* serial_ref --initialize <file> <col_num> <out.f32>: time the reference's own
- * text reader (ROWS * col_num values via fscanf "%f%*c", serialConjugate.c:96). */
+ * text reader (ROWS * col_num values via fscanf "%f%*c", serialConjugate.c:96).
+ * The buffer is pre-filled with a signalling-NaN sentinel (0x7FA5A5A5, a
+ * pattern no conversion produces), so the output shows which values the
+ * reader assigned: it stops assigning at its first failing conversion or at
+ * end of file and leaves the rest as they were (uninitialised memory in the
+ * reference's own main). */
 static int time_initialize(char *path, int cols, const char *out) {
     float *v = malloc((size_t)REF_ROWS * cols * sizeof(float));
     if (!v) return 3;
+    const uint32_t sentinel = 0x7FA5A5A5u;
+    for (size_t i = 0; i < (size_t)REF_ROWS * cols; ++i) memcpy(v + i, &sentinel, 4);
     double t0 = now_s();
     initialize(v, path, cols);
     double t1 = now_s();

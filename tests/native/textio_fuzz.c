@@ -6,13 +6,17 @@
  * Each case writes a file of random tokens -- well-formed numbers of every
  * shape the fast path and the strtod/strtof fallback take (long mantissas,
  * big exponents, float midpoints, subnormals, inf/nan, hex), and malformed
- * ones -- separated by random runs of the accepted separators, sometimes
- * with a UTF-8 BOM, sometimes without a trailing separator, sometimes padded
- * so the file ends exactly on a page boundary.  Expected values come from
- * strtof / strtod on each token (what fscanf("%f") does in
- * serialConjugate.c:96); the reader must return them bit for bit, for 1 and
- * several threads, or -3 when a token in the requested range is not a whole
- * number, or -2 when the file holds fewer numbers than requested.
+ * ones -- separated by random runs of white space, ',' and ';', sometimes by
+ * a single other byte ('-', '#', 'x', a byte >= 0x80), sometimes with a
+ * UTF-8 BOM in front, sometimes without a trailing separator, sometimes
+ * padded so the file ends exactly on a page boundary.  The expected values
+ * are what the reference's own loop reads: glibc fscanf(f, "%f%*c") (or
+ * "%lf%*c" for double) once per value (serialConjugate.c:96).  The reader
+ * must return them bit for bit, for 1 and several threads, when all requested
+ * values convert; where fscanf fails first (a failing conversion or end of
+ * file, after which the reference leaves its values uninitialised) it must
+ * return -3 or -2; cgx_text_count must equal the number of values fscanf
+ * converts before its first failure.
  *
  *   textio_fuzz <tmpdir> <cases> <seed>     exit 0 = all cases passed
  */
@@ -74,6 +78,26 @@ static int token(char *o) {
 }
 
 static const char kSeps[] = " \n\r\t,;";
+static const char kOdd[] = "-#x\xEF+|";
+
+/* The reference's loop: fscanf "%f%*c" (float) / "%lf%*c" (double) per value.
+ * Returns how many values it converted before the first failure (<= want),
+ * and in *eof whether that failure was end of file. */
+static int64_t ref_read(const char *path, int64_t want, int as_float, void *out, int *eof) {
+    FILE *f = fopen(path, "rb");
+    *eof = 0;
+    if (!f) return -1;
+    int64_t i = 0;
+    for (; i < want; ++i) {
+        const int r = as_float ? fscanf(f, "%f%*c", (float *)out + i) : fscanf(f, "%lf%*c", (double *)out + i);
+        if (r != 1) {
+            *eof = r == EOF;
+            break;
+        }
+    }
+    fclose(f);
+    return i;
+}
 
 int main(int argc, char **argv) {
     if (argc != 4) return 2;
@@ -83,34 +107,37 @@ int main(int argc, char **argv) {
     char path[4096];
     snprintf(path, sizeof path, "%s/fuzz_%d.txt", dir, (int)getpid());
     enum { kMaxTok = 400 };
-    static char toks[kMaxTok][320];
-    int fails = 0, n_malformed = 0, n_short = 0, n_page = 0, n_slow = 0;
+    static char tok[320];
+    int fails = 0, n_fail = 0, n_short = 0, n_page = 0, n_odd = 0;
     for (int c = 0; c < cases; ++c) {
         const int nt = 1 + rint_(kMaxTok - 1);
         const int clean = rint_(3) != 0; /* mostly files whose tokens are all numbers */
         FILE *f = fopen(path, "wb");
         if (!f) return 2;
         long bytes = 0;
-        if (rint_(10) == 0) bytes += fprintf(f, "\xEF\xBB\xBF");
-        int ntok = 0;
+        if (rint_(20) == 0) bytes += fprintf(f, "\xEF\xBB\xBF");
         for (int i = 0; i < nt; ++i) {
-            char *t = toks[ntok];
             int len;
             for (;;) { /* clean files: only tokens strtod consumes whole */
-                len = token(t);
+                len = token(tok);
                 if (!clean) break;
                 char *stop;
-                (void)strtod(t, &stop);
-                if (stop == t + len) break;
+                (void)strtod(tok, &stop);
+                if (stop == tok + len) break;
             }
-            bytes += fprintf(f, "%s", t);
-            ++ntok;
+            bytes += fprintf(f, "%s", tok);
             const int last = i == nt - 1;
             if (!last || rint_(4)) { /* separators (none after the last token sometimes) */
-                const int ns = 1 + (rint_(4) == 0 ? rint_(3) : 0);
-                for (int q = 0; q < ns; ++q) {
-                    fputc(kSeps[rint_((int)sizeof kSeps - 1)], f);
+                if (rint_(12) == 0) { /* one odd byte: %*c consumes it whatever it is */
+                    fputc(kOdd[rint_((int)sizeof kOdd - 1)], f);
                     ++bytes;
+                    ++n_odd;
+                } else {
+                    const int ns = 1 + (rint_(4) == 0 ? rint_(3) : 0);
+                    for (int q = 0; q < ns; ++q) {
+                        fputc(kSeps[rint_((int)sizeof kSeps - 1)], f);
+                        ++bytes;
+                    }
                 }
             }
         }
@@ -119,60 +146,54 @@ int main(int argc, char **argv) {
             for (long q = 0; q < pad; ++q) fputc(' ', f);
             ++n_page;
             fputc('5', f);
-            snprintf(toks[ntok++], 320, "5");
         }
         fclose(f);
-        if (cgx_text_count(path) != ntok) {
-            fprintf(stderr, "case %d: count %lld != %d\n", c, (long long)cgx_text_count(path), ntok);
+        int eof;
+        static double all[4 * kMaxTok];
+        const int64_t avail = ref_read(path, 4 * kMaxTok, 0, all, &eof);
+        if (cgx_text_count(path) != avail) {
+            fprintf(stderr, "case %d: count %lld != fscanf's %lld\n", c, (long long)cgx_text_count(path),
+                    (long long)avail);
             ++fails;
             continue;
         }
-        const int64_t want = rint_(5) == 0 ? ntok + 1 + rint_(3) : 1 + rint_(ntok);
+        const int64_t want = rint_(5) == 0 ? avail + 1 + rint_(3) : 1 + rint_((int)(avail > 0 ? avail : 1));
         for (int as_float = 0; as_float < 2; ++as_float) {
-            int exp_rc = 0;
-            double *ed = calloc((size_t)want + 1, sizeof(double));
-            float *ef = calloc((size_t)want + 1, sizeof(float));
-            for (int64_t i = 0; i < want && i < ntok; ++i) {
-                char *stop;
-                const size_t len = strlen(toks[i]);
-                if (as_float) ef[i] = strtof(toks[i], &stop);
-                else ed[i] = strtod(toks[i], &stop);
-                if (stop != toks[i] + len && exp_rc == 0) exp_rc = -3;
-            }
-            if (want > ntok && exp_rc == 0) exp_rc = -2;
+            void *exp = calloc((size_t)want + 1, 8);
+            const int64_t got = ref_read(path, want, as_float, exp, &eof);
+            const int ref_ok = got == want;
             if (as_float == 0) {
-                n_malformed += exp_rc == -3;
-                n_short += exp_rc == -2;
-                for (int64_t i = 0; i < want && i < ntok; ++i) n_slow += strlen(toks[i]) > 20;
+                n_fail += !ref_ok && !eof;
+                n_short += !ref_ok && eof;
             }
             for (int threads = 1; threads <= 5; threads += 4) {
                 void *out = calloc((size_t)want + 1, 8);
                 const int rc = cgx_text_read(path, want, as_float, out, threads);
                 int bad = 0;
-                if ((rc == 0) != (exp_rc == 0) || (exp_rc == -2 && rc != -2)) bad = 1;
-                if (rc == 0 && exp_rc == 0)
+                if (ref_ok != (rc == 0) || (!ref_ok && rc != -2 && rc != -3)) bad = 1;
+                if (rc == 0 && ref_ok)
                     for (int64_t i = 0; i < want; ++i) {
-                        const int same = as_float ? !memcmp((float *)out + i, ef + i, 4) : !memcmp((double *)out + i, ed + i, 8);
+                        const int same = as_float ? !memcmp((float *)out + i, (float *)exp + i, 4)
+                                                  : !memcmp((double *)out + i, (double *)exp + i, 8);
                         if (!same) {
-                            fprintf(stderr, "case %d token %lld '%s' (%s, %d threads): value differs\n", c,
-                                    (long long)i, toks[i], as_float ? "float" : "double", threads);
+                            fprintf(stderr, "case %d value %lld (%s, %d threads): differs from fscanf's\n", c,
+                                    (long long)i, as_float ? "float" : "double", threads);
                             bad = 1;
                             break;
                         }
                     }
                 if (bad) {
-                    fprintf(stderr, "case %d: rc %d expected %d (want %lld of %d, %s, %d threads)\n", c, rc, exp_rc,
-                            (long long)want, ntok, as_float ? "float" : "double", threads);
+                    fprintf(stderr, "case %d: rc %d, fscanf converted %lld of %lld (%s, %d threads)\n", c, rc,
+                            (long long)got, (long long)want, as_float ? "float" : "double", threads);
                     ++fails;
                 }
                 free(out);
             }
-            free(ed);
-            free(ef);
+            free(exp);
         }
     }
     unlink(path);
-    printf("cases %d failures %d (malformed %d, short %d, page-end %d, long tokens %d)\n", cases, fails,
-           n_malformed, n_short, n_page, n_slow);
+    printf("cases %d failures %d (fscanf failed first %d, short %d, page-end %d, odd separators %d)\n", cases, fails,
+           n_fail, n_short, n_page, n_odd);
     return fails ? 1 : 0;
 }

@@ -129,10 +129,66 @@ def test_text_reader_reference_fixtures(built):
     assert np.array_equal(A, numbers("matrixA1.txt", 16))
     assert cg.count_text(os.path.join(FIX, "vectorb.txt")) == 2
     assert cg.read_dims(os.path.join(FIX, "dimensions.txt")) == (2, 2, 2, 1)
-    # initialguess1.txt ends in a stray UTF-8 BOM: the two values still read
+    # initialguess1.txt ends in a stray UTF-8 BOM: its first byte is the %*c
+    # after 0.0, so the two values read (and a third conversion would fail)
     x = cg.read_text(os.path.join(FIX, "initialguess1.txt"), 2, np.float64)
     assert np.array_equal(x, [1.0, 0.0])
     assert cg.count_text(os.path.join(FIX, "initialguess1.txt")) == 2
+
+
+_INIT_CASES = {
+    # the reference's own fixtures (copied data)
+    **{name: None for name in ("matrixA.txt", "vectorb.txt", "initialguess.txt", "initialguess1.txt",
+                               "matrixA1.txt", "vectorb1.txt", "X0.txt", "dimensions.txt")},
+    # separators and edge cases of fscanf("%f%*c")
+    "crlf": b"1.5\r\n-2.25\r\n3e2\r\n",
+    "minus_eaten": b"1.5-2.0\n4\n",            # %*c eats the '-': 1.5, 2.0, 4
+    "dot_eaten": b"1.2.3\n",                   # 1.2, then '.' eaten, 3
+    "bom_front": b"\xef\xbb\xbf1.0\n2.0\n",  # the first conversion fails
+    "bom_trailing": b"1.0\n0.0\xef\xbb\xbf\n",  # initialguess1.txt's shape
+    "trailing_junk": b"1\n2\njunk\n",
+    "short": b"7\n",
+    "double_comma": b"1.0,,2.0\n",
+    "exp_no_digits": b"1e+\n2\n",              # glibc takes "1e+" as 1
+    "nan_paren": b"nan(1)\n5\n",               # "nan", '(' eaten, then "1)" -> 1, ')' eaten
+    "tabs_spaces": b"  \t 1.25 \t\n\n -0 \n",
+    "no_final_newline": b"4\n5",
+    "inf_forms": b"inf\nINFINITY\n-Inf\ninfinit\n",
+    "hex": b"0x1p3\n0x.p1\n",
+}
+
+
+@pytest.mark.parametrize("name", sorted(_INIT_CASES))
+def test_text_reader_pinned_to_reference_initialize(built, tmp_path, name):
+    """cgx_text_read against the reference's own initialize()
+    (serialConjugate.c:85-105, fscanf "%f%*c" per value), run through the
+    unmodified reference (oracle/_ref/serial_ref --initialize, its buffer
+    pre-filled with a sentinel so the values it assigned are known).  The
+    values it assigns are read bit for bit; where it stops assigning (a
+    failing conversion, end of file) cgx_text_read returns an error instead
+    of leaving uninitialised values -- the one deliberate divergence."""
+    import oracle
+    exe = oracle.ref_binary()
+    if not exe:
+        pytest.skip("oracle/_ref/serial_ref not built (no /root/reference here)")
+    data = _INIT_CASES[name]
+    path = os.path.join(FIX, name) if data is None else str(tmp_path / f"{name}.txt")
+    if data is not None:
+        with open(path, "wb") as f:
+            f.write(data)
+    out = str(tmp_path / "ref.f32")
+    r = subprocess.run([exe, "--initialize", path, "1", out], capture_output=True, text=True, timeout=60)
+    assert r.returncode == 0, r.stdout + r.stderr
+    ref = np.fromfile(out, dtype=np.uint32)
+    unset = np.flatnonzero(ref == 0x7FA5A5A5)
+    k = int(unset[0]) if unset.size else ref.size
+    assert (ref[k:] == 0x7FA5A5A5).all()  # the reference assigns a prefix, then nothing
+    if k:
+        got = cg.read_text(path, k, np.float32)
+        assert np.array_equal(got.view(np.uint32), ref[:k]), (got, ref[:k].view(np.float32))
+        assert cg.count_text(path) == k
+    with pytest.raises(ValueError):
+        cg.read_text(path, k + 1, np.float32)
 
 
 def test_text_reader_errors(built, tmp_path):

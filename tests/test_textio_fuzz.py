@@ -1,10 +1,11 @@
 """The text reader (cgx_textio.c, the replacement for initialize(),
 serialConjugate.c:85-105) on randomized files under AddressSanitizer and
-UndefinedBehaviorSanitizer: every value bit for bit equal to strtof / strtod
-on its token (fscanf "%f" in the reference), -3 for a malformed token, -2 for
-a short file, with 1 and 5 threads, including files whose last token ends
-exactly at a page boundary of the mapping.  Host-only (tests/native/
-textio_fuzz.c); no GPU."""
+UndefinedBehaviorSanitizer: every value bit for bit equal to what the
+reference's own loop reads, glibc fscanf(f, "%f%*c") per value (odd single
+separators like '-' or a BOM byte consumed by the %*c included); -3 / -2
+where that loop fails first (the reference then reads uninitialised memory);
+1 and 5 threads; files whose last token ends exactly at a page boundary of
+the mapping.  Host-only (tests/native/textio_fuzz.c); no GPU."""
 import os
 import shutil
 import subprocess
