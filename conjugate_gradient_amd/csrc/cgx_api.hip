@@ -128,7 +128,7 @@ int cgx_matvec(int dtype, const void *A, int64_t lda, int64_t rows, int64_t cols
     HIPT(hipGetDevice(&dev));
     RedWs ws;
     TRY(dev_ws(&ws));
-    MatvecPlan pl = plan_matvec_f64(dev, rows);
+    MatvecPlan pl = plan_matvec_f64(dev, rows, 0, 0, -1, 0, cols);
     HIPT(matvec_f64(pl, static_cast<const double *>(A), lda, rows, cols, static_cast<const double *>(v),
                     static_cast<double *>(out), nullptr, nullptr, ws, s));
     return CGX_OK;

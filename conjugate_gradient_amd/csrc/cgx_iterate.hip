@@ -543,11 +543,12 @@ int cgx_set_matvec_plan(cgx_ctx *c, int rows_per_wave, int chunks_in_flight, int
     const int R = rows_per_wave, U = chunks_in_flight;
     if (R != 1 && R != 2 && R != 4 && R != 8) return fail(CGX_ERR_ARG, "rows_per_wave must be 1, 2, 4 or 8");
     if (U != 2 && U != 4 && U != 8) return fail(CGX_ERR_ARG, "chunks_in_flight must be 2, 4 or 8");
-    if (nontemporal != 0 && nontemporal != 1 && nontemporal != 8)
-        return fail(CGX_ERR_ARG, "load policy must be 0 (plain), 1 (non-temporal) or 8 (pipelined non-temporal)");
+    if (nontemporal != 0 && nontemporal != 1 && nontemporal != 2 && nontemporal != 8)
+        return fail(CGX_ERR_ARG, "load policy must be 0 (plain), 1 (non-temporal), 2 (pipelined) or 8 (pipelined "
+                                 "non-temporal)");
     for (auto &s : c->sh) {
         TRY(set_dev(s));
-        MatvecPlan pl = plan_matvec_f64(s.dev, s.nloc, R, U, nontemporal, blocks_per_cu);
+        MatvecPlan pl = plan_matvec_f64(s.dev, s.nloc, R, U, nontemporal, blocks_per_cu, c->lda);
         s.plan = pl;
     }
     return CGX_OK;

@@ -25,8 +25,10 @@ struct MatvecPlan {
     int blocks = 0;   // grid (256-thread blocks), grid-stride over row groups
 };
 // R/U/nt/blocks_per_cu <= 0 pick the defaults (env CGX_MV_* may override).
+// cols > 0 (the row length): fewer than 8 whole 128-column chunks per row
+// take U = 4 or 2, so all of a row's loads are issued at once.
 MatvecPlan plan_matvec_f64(int device, int64_t rows, int R = 0, int U = 0, int nt = -1,
-                           int blocks_per_cu = 0);
+                           int blocks_per_cu = 0, int64_t cols = 0);
 
 // ---- fp64 -------------------------------------------------------------------
 // out[i] = sum_j A[i*lda+j] v[j]; if pown != nullptr also *dot_out = pown . out

@@ -25,8 +25,8 @@ namespace cgx {
 namespace {
 
 // Load policy of the A stream (the only data a matVec reads once):
-//   0 plain global_load, 1 global_load ... nt, 8 software-pipelined
-//   global_load ... nt (the default plan).  The variants measured and not
+//   0 plain global_load, 1 global_load ... nt, 2 / 8 software-pipelined
+//   global_load, default policy / nt (8 = the default plan).  The variants measured and not
 //   adopted (buffer loads with other cache bits, a flattened pipeline,
 //   LDS-staged p, SGPR row bases) live in tools/microbench/matvec_variants.hip.
 //   All give the same row sums bit for bit.
@@ -200,6 +200,7 @@ template <int R, int U>
 MvFn pick_nt(int nt) {
     switch (nt) {
         case 0: return k_matvec_f64<R, U, 0>;
+        case 2: return k_matvec_f64<R, U, 0, true>;  // pipelined, default-policy loads
         case 8: return k_matvec_f64<R, U, 1, true>;  // pipelined, global nt (the default)
         default: return k_matvec_f64<R, U, 1>;
     }
@@ -223,7 +224,7 @@ MvFn pick_mv(int R, int U, int nt) {
 
 }  // namespace
 
-MatvecPlan plan_matvec_f64(int device, int64_t rows, int R, int U, int nt, int blocks_per_cu) {
+MatvecPlan plan_matvec_f64(int device, int64_t rows, int R, int U, int nt, int blocks_per_cu, int64_t cols) {
     MatvecPlan pl;
     const int cus = cu_count(device);
     // Software-pipelined (loads of step c+U issued before the FMAs of step c),
@@ -235,7 +236,11 @@ MatvecPlan plan_matvec_f64(int device, int64_t rows, int R, int U, int nt, int b
     // R=1 when there are fewer than 2 rows per resident wave.
     const int64_t want_waves = (int64_t)cus * 4;
     pl.R = rows >= 2 * want_waves ? 2 : 1;
-    pl.U = 8;
+    // a row of fewer than 8 chunks: with U = 8 its chunks would go through the
+    // one-chunk remainder loop, one dependent memory round trip each (N = 512:
+    // 4 chunks); U = 4 / 2 issues them together
+    const int64_t chunks = cols >> 7;
+    pl.U = (cols <= 0 || chunks >= 8) ? 8 : chunks >= 4 ? 4 : 2;
     pl.nt = 8;
     pl.R = env_int("CGX_MV_R", pl.R);
     pl.U = env_int("CGX_MV_U", pl.U);
@@ -245,7 +250,7 @@ MatvecPlan plan_matvec_f64(int device, int64_t rows, int R, int U, int nt, int b
     if (nt >= 0) pl.nt = nt;
     if (pl.R != 1 && pl.R != 2 && pl.R != 4 && pl.R != 8) pl.R = 4;
     if (pl.U != 2 && pl.U != 4 && pl.U != 8) pl.U = 4;
-    if (pl.nt != 0 && pl.nt != 1 && pl.nt != 8) pl.nt = 8;
+    if (pl.nt != 0 && pl.nt != 1 && pl.nt != 2 && pl.nt != 8) pl.nt = 8;
     int per_cu = 0;
     const void *fn = reinterpret_cast<const void *>(pick_mv(pl.R, pl.U, pl.nt));
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kNT, 0) != hipSuccess || per_cu <= 0)

@@ -81,7 +81,7 @@ int alloc_shard(cgx_ctx *c, Shard &s) {
             for (int q = 0; q < s.ncopy; ++q) HIPT(hipEventCreateWithFlags(&s.ev_loaded[b][q], hipEventDisableTiming));
         }
         for (int q = 0; q < s.ncopy; ++q) HIPT(hipStreamCreateWithFlags(&s.copy[q], hipStreamNonBlocking));
-        if (!f32ref(c)) s.tile_plan = plan_matvec_f64(s.dev, s.tile_rows);
+        if (!f32ref(c)) s.tile_plan = plan_matvec_f64(s.dev, s.tile_rows, 0, 0, -1, 0, c->lda);
     } else if (c->flags & CGX_SYMMETRIC) {
         const int64_t ntiles = sym_tiles(c->lda);
         const size_t tbytes = (size_t)ntiles * 128 * 128 * 8;
@@ -147,7 +147,8 @@ int alloc_shard(cgx_ctx *c, Shard &s) {
         s.ev_t.resize(2 * kEvPairs);
         for (auto &e : s.ev_t) HIPT(hipEventCreate(&e));
     }
-    if (!f32ref(c) && c->op == OP_DENSE && !(c->flags & CGX_SYMMETRIC)) s.plan = plan_matvec_f64(s.dev, s.nloc);
+    if (!f32ref(c) && c->op == OP_DENSE && !(c->flags & CGX_SYMMETRIC))
+        s.plan = plan_matvec_f64(s.dev, s.nloc, 0, 0, -1, 0, c->lda);
     HIPT(hipStreamSynchronize(s.stream));
     return CGX_OK;
 }
