@@ -143,6 +143,78 @@ static void *create_ctx(void *arg) {
     return NULL;
 }
 
+/* A streamed to the GPU row block by row block (parallel_cg.c's MPI_Scatter,
+ * :112-113, one block at a time): the main thread parses block k+1 from the
+ * indexed file while a copy thread sends block k with cgx_set_rows, through
+ * a ring of block buffers, so host memory holds at most CGX_CLI_RING_MB
+ * (default 1024) of A and, once the context is up, the H2D runs under the
+ * parse.  (CGX_CLI_STREAM=0: parse all of A, then one cgx_set_system.) */
+typedef struct {
+    cgx_text *text;
+    int64_t n, block_rows, nblocks;
+    int nslots, as_float, threads;
+    size_t es;
+    big_buf *slot;        /* nslots buffers of block_rows * n values (huge pages) */
+    int *filled;          /* slot holds block filled[s] - 1 (0 = free) */
+    pthread_mutex_t mu;
+    pthread_cond_t cv;
+    int abort_rc;         /* the copy side failed: the parse stops */
+    pthread_t creator;    /* joined by the copy thread */
+    int creator_threaded;
+    create_job *job;
+    int rc;               /* first cgx_set_rows failure */
+    double t_last_h2d;
+} a_stream;
+
+static void *stream_copy(void *arg) {
+    a_stream *st = (a_stream *)arg;
+    if (st->creator_threaded) pthread_join(st->creator, NULL);
+    int rc = st->job->rc;
+    for (int64_t k = 0; k < st->nblocks && rc == CGX_OK; ++k) {
+        const int sl = (int)(k % st->nslots);
+        pthread_mutex_lock(&st->mu);
+        while (st->filled[sl] != k + 1 && !st->abort_rc) pthread_cond_wait(&st->cv, &st->mu);
+        const int stop = st->abort_rc;
+        pthread_mutex_unlock(&st->mu);
+        if (stop) break;
+        const int64_t row0 = k * st->block_rows, rows = row0 + st->block_rows <= st->n ? st->block_rows : st->n - row0;
+        rc = cgx_set_rows(st->job->ctx, row0, rows, st->slot[sl].p, st->n, NULL, NULL);
+        pthread_mutex_lock(&st->mu);
+        st->filled[sl] = 0;
+        pthread_cond_broadcast(&st->cv);
+        pthread_mutex_unlock(&st->mu);
+    }
+    st->t_last_h2d = now_s();
+    pthread_mutex_lock(&st->mu);
+    st->rc = rc;
+    if (rc != CGX_OK && !st->abort_rc) st->abort_rc = 1;
+    pthread_cond_broadcast(&st->cv);
+    pthread_mutex_unlock(&st->mu);
+    return NULL;
+}
+
+/* The parse side (main thread).  Returns 0, or the text reader's error. */
+static int stream_parse(a_stream *st) {
+    for (int64_t k = 0; k < st->nblocks; ++k) {
+        const int sl = (int)(k % st->nslots);
+        pthread_mutex_lock(&st->mu);
+        while (st->filled[sl] != 0 && !st->abort_rc) pthread_cond_wait(&st->cv, &st->mu);
+        const int stop = st->abort_rc;
+        pthread_mutex_unlock(&st->mu);
+        if (stop) return 0; /* the copy side reports its own error */
+        const int64_t row0 = k * st->block_rows, rows = row0 + st->block_rows <= st->n ? st->block_rows : st->n - row0;
+        const int rc = cgx_text_read_range(st->text, row0 * st->n, rows * st->n, st->as_float, st->slot[sl].p,
+                                           st->threads);
+        pthread_mutex_lock(&st->mu);
+        if (rc != 0) st->abort_rc = 1;
+        else st->filled[sl] = (int)(k + 1);
+        pthread_cond_broadcast(&st->cv);
+        pthread_mutex_unlock(&st->mu);
+        if (rc != 0) return rc;
+    }
+    return 0;
+}
+
 /* Whole-string numeric option values: "--eps abc" or "--gpus 2x" is an
  * error (exit 2), not a silent 0. */
 static int opt_ll(const char *name, const char *v, long long *out) {
@@ -244,9 +316,14 @@ int main(int argc, char **argv) {
     big_buf Abuf = {NULL, NULL, 0};
     pthread_t freer;
     int freeing = 0;
+    const char *se = getenv("CGX_CLI_STREAM");
+    const int stream_a = spd_n <= 0 && !(se && !strcmp(se, "0"));
     if (!x) { fprintf(stderr, "can't allocate memory for vector\n"); return 1; }
     if (spd_n > 0) {
         memset(x, 0, (size_t)n * es);
+    } else if (stream_a) {
+        b = malloc((size_t)n * es);
+        if (!b) { fprintf(stderr, "can't allocate memory for vector\n"); return 1; }
     } else {
         /* initialize(A), initialize(b), initialize(x0): serialConjugate.c:65-67 */
         if (big_alloc(&Abuf, (size_t)n * (size_t)n * es) != 0) A = NULL;
@@ -259,11 +336,83 @@ int main(int argc, char **argv) {
     pthread_t creator;
     const int threaded = pthread_create(&creator, NULL, create_ctx, &job) == 0;
     if (!threaded) create_ctx(&job);
-    const int read_rc = spd_n > 0 ? 0
-                        : (read_file(pos[0], n * n, fp32ref, A, threads) ||
-                           read_file(pos[1], n, fp32ref, b, threads) || read_file(pos[2], n, fp32ref, x, 1));
+    int read_rc = 0, stream_rc = CGX_OK;
+    double t_parsed = 0.0, t_h2d = 0.0;
+    if (stream_a) {
+        /* A: indexed once, then parsed and sent row block by row block */
+        a_stream st;
+        memset(&st, 0, sizeof st);
+        const int orc = cgx_text_open(pos[0], threads, &st.text);
+        int stopped = 0;
+        const int64_t have = orc == 0 ? cgx_text_available(st.text, &stopped) : -1;
+        if (orc != 0) {
+            printf("Could not open file\n"); /* serialConjugate.c:103 */
+            fprintf(stderr, "%s: cannot open\n", pos[0]);
+            read_rc = -1;
+        } else if (have < n * n) {
+            fprintf(stderr, stopped ? "%s: malformed number\n" : "%s: fewer than %lld numbers\n", pos[0],
+                    (long long)(n * n));
+            read_rc = stopped ? -3 : -2;
+        }
+        if (!read_rc) {
+            const char *rm = getenv("CGX_CLI_RING_MB");
+            const double ring_mb = (rm && atof(rm) > 0) ? atof(rm) : 1024.0;
+            const size_t row_bytes = (size_t)n * es;
+            const size_t block_bytes = (size_t)32 << 20;
+            st.n = n;
+            st.es = es;
+            st.block_rows = (int64_t)(block_bytes / row_bytes) > 0 ? (int64_t)(block_bytes / row_bytes) : 1;
+            if (st.block_rows > n) st.block_rows = n;
+            st.nblocks = (n + st.block_rows - 1) / st.block_rows;
+            int64_t slots = (int64_t)(ring_mb * 1048576.0 / ((double)st.block_rows * (double)row_bytes));
+            if (slots < 2) slots = 2;
+            if (slots > st.nblocks) slots = st.nblocks;
+            st.nslots = (int)slots;
+            st.as_float = fp32ref;
+            st.threads = threads;
+            st.slot = calloc((size_t)st.nslots, sizeof(big_buf));
+            st.filled = calloc((size_t)st.nslots, sizeof(int));
+            int ok = st.slot && st.filled;
+            for (int q = 0; ok && q < st.nslots; ++q) ok = big_alloc(&st.slot[q], (size_t)st.block_rows * row_bytes) == 0;
+            if (!ok) { fprintf(stderr, "can't allocate memory for vector\n"); return 1; }
+            pthread_mutex_init(&st.mu, NULL);
+            pthread_cond_init(&st.cv, NULL);
+            st.creator = creator;
+            st.creator_threaded = threaded;
+            st.job = &job;
+            pthread_t copier;
+            const int copy_threaded = pthread_create(&copier, NULL, stream_copy, &st) == 0;
+            if (copy_threaded) {
+                const int prc = stream_parse(&st);
+                if (prc) {
+                    fprintf(stderr, prc == -2 ? "%s: fewer than %lld numbers\n" : "%s: malformed number\n", pos[0],
+                            (long long)(n * n));
+                    read_rc = prc;
+                }
+                t_parsed = now_s();
+                pthread_join(copier, NULL); /* also joined the creator */
+                stream_rc = st.rc;
+            } else {
+                read_rc = -1;
+                if (threaded) pthread_join(creator, NULL);
+            }
+            t_h2d = st.t_last_h2d;
+            for (int q = 0; q < st.nslots; ++q) big_free(&st.slot[q]);
+            free(st.slot);
+            free(st.filled);
+        } else if (threaded) {
+            pthread_join(creator, NULL);
+        }
+        cgx_text_close(st.text);
+        if (!read_rc) read_rc = read_file(pos[1], n, fp32ref, b, threads) || read_file(pos[2], n, fp32ref, x, 1);
+    } else {
+        read_rc = spd_n > 0 ? 0
+                            : (read_file(pos[0], n * n, fp32ref, A, threads) ||
+                               read_file(pos[1], n, fp32ref, b, threads) || read_file(pos[2], n, fp32ref, x, 1));
+        t_parsed = now_s();
+        if (threaded) pthread_join(creator, NULL);  /* before any exit: HIP may be starting up on it */
+    }
     const double t_read = now_s();
-    if (threaded) pthread_join(creator, NULL);  /* before any exit: HIP may be starting up on it */
     if (read_rc) {
         if (job.ctx) cgx_destroy(job.ctx);
         return 1;
@@ -271,12 +420,19 @@ int main(int argc, char **argv) {
     cgx_ctx *ctx = job.ctx;
     int rc = job.rc;
     if (rc != CGX_OK) return die_cgx(rc, "cgx_create");
+    if (stream_rc != CGX_OK) return die_cgx(stream_rc, "cgx_set_rows");
 
-    double t_dist0 = now_s(), t_dist1;
+    double t_dist0 = stream_a ? t_parsed : now_s(), t_dist1;
     if (spd_n > 0) {
         rc = cgx_generate_spd(ctx, seed);
         t_dist1 = now_s();
         if (rc != CGX_OK) return die_cgx(rc, "cgx_generate_spd");
+    } else if (stream_a) {
+        /* A is on the device; b and x0 (MPI_Bcast / MPI_Scatter of the vectors) */
+        rc = cgx_set_rows(ctx, 0, n, NULL, n, b, x);
+        t_dist1 = now_s();
+        free(b);
+        if (rc != CGX_OK) return die_cgx(rc, "cgx_set_rows");
     } else {
         /* MPI_Bcast(x0) + MPI_Scatter(A, b): parallel_cg.c:109-117 */
         rc = cgx_set_system(ctx, A, b, x);
@@ -328,9 +484,11 @@ int main(int argc, char **argv) {
         fprintf(stderr,
                 "{\"setup_s\": %.6f, \"read_s\": %.6f, \"hip_runtime_s\": %.6f, \"create_s\": %.6f, \"distribute_s\": %.6f, "
                 "\"solve_s\": %.6f, \"to_x_s\": %.6f, \"printed_s\": %.6f, \"teardown_s\": %.6f, \"fast_exit\": %d, "
-                "\"dist_start_s\": %.6f, \"solve_call_s\": %.6f, \"free_s\": %.6f, \"get_x_s\": %.6f}\n",
+                "\"dist_start_s\": %.6f, \"solve_call_s\": %.6f, \"free_s\": %.6f, \"get_x_s\": %.6f, "
+                "\"streamed\": %d, \"a_parsed_s\": %.6f, \"a_on_device_s\": %.6f}\n",
                 t_start - t_prog0, t_read - t_start, job.t_rt - t_start, job.t_done - t_start, t_dist1 - t_dist0, st.solve_ms / 1e3,
-                t_x - t_prog0, t_printed - t_prog0, now_s() - t_printed, fast_exit, t_dist0 - t_start, t_solve1 - t_solve0, t_freed - t_dist1, t_x - t_solve1);
+                t_x - t_prog0, t_printed - t_prog0, now_s() - t_printed, fast_exit, t_dist0 - t_start, t_solve1 - t_solve0, t_freed - t_dist1, t_x - t_solve1,
+                stream_a, t_parsed > 0 ? t_parsed - t_start : 0.0, t_h2d > 0 ? t_h2d - t_start : 0.0);
     if (fast_exit) {
         /* Every result is written and flushed.  The process ends here without
          * freeing the device/pinned buffers or running the HIP runtime's exit

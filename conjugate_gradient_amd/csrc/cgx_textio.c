@@ -274,93 +274,199 @@ static int64_t count_tokens(const char *p, const char *end, int *bad) {
 }
 
 int64_t cgx_text_count(const char *path) {
-    text_buf tb;
-    if (open_text(path, &tb) != 0) return -1;
-    int bad;
-    int64_t c = count_tokens(tb.data, tb.data + tb.len, &bad);
-    close_text(&tb);
+    cgx_text *t = NULL;
+    if (cgx_text_open(path, 1, &t) != 0) return -1;
+    const int64_t c = cgx_text_available(t, NULL);
+    cgx_text_close(t);
     return c;
 }
 
+/* ---- the indexed file: pieces cut at white space, each with its count ---- */
+/* A piece is ~1 MiB of text (at least 8 per thread); the count pass fills in
+ * how many numbers each holds, so a range of values can be parsed from the
+ * pieces that hold it alone (row blocks streamed by cg_hip). */
+struct cgx_text {
+    text_buf tb;
+    int npieces;
+    const char **beg, **end; /* piece q = [beg[q], end[q])                         */
+    int64_t *first;          /* index of piece q's first number (npieces + 1 entries) */
+    int64_t *ntok;
+    int *bad;                /* piece q stops at a failing conversion                */
+    int64_t avail;           /* numbers reachable: up to the first failing conversion */
+    int stopped;             /* avail ends at a failing conversion (else at end of file) */
+};
+
 typedef struct {
-    const char *beg, *end;  /* chunk [beg, end), both at token boundaries */
-    int64_t first;          /* index of the chunk's first token            */
-    int64_t ntok;           /* numbers in the chunk                         */
-    int bad;                /* the chunk stops at a failing conversion      */
-    int64_t count;          /* total tokens wanted                         */
+    cgx_text *t;
+    int q0, q1;              /* pieces [q0, q1) of this job                          */
+    int64_t lo, hi;          /* values wanted: [lo, hi)                              */
     int as_float;
-    void *out;
+    void *out;               /* out[i - lo]                                          */
     int status;
-} chunk_t;
+} piece_job;
 
 static void *count_job(void *arg) {
-    chunk_t *c = (chunk_t *)arg;
-    c->ntok = count_tokens(c->beg, c->end, &c->bad);
+    piece_job *j = (piece_job *)arg;
+    for (int q = j->q0; q < j->q1; ++q) j->t->ntok[q] = count_tokens(j->t->beg[q], j->t->end[q], &j->t->bad[q]);
     return NULL;
 }
 
 static void *parse_job(void *arg) {
-    chunk_t *c = (chunk_t *)arg;
-    const char *p = c->beg, *end = c->end;
-    int64_t idx = c->first;
-    c->status = 0;
-    while (idx < c->count) {
-        while (p < end && IS_SPACE(*p)) ++p;
-        if (p >= end) break;
-        int ok;
-        const char *q = scan_number(p, end, &ok);
-        if (!ok) { c->status = -3; return NULL; }
-        if (!fast_number(p, q, c->as_float, c->out, idx) &&
-            slow_number(p, q, c->as_float, c->out, idx) != 0) { c->status = -3; return NULL; }
-        ++idx;
-        p = q < end ? q + 1 : q;  /* %*c */
+    piece_job *j = (piece_job *)arg;
+    j->status = 0;
+    for (int qq = j->q0; qq < j->q1; ++qq) {
+        const char *p = j->t->beg[qq], *end = j->t->end[qq];
+        int64_t idx = j->t->first[qq];
+        if (idx >= j->hi || j->t->first[qq + 1] <= j->lo) continue;
+        while (idx < j->hi) {
+            while (p < end && IS_SPACE(*p)) ++p;
+            if (p >= end) break;
+            int ok;
+            const char *q = scan_number(p, end, &ok);
+            if (!ok) { j->status = -3; return NULL; }
+            if (idx >= j->lo) {
+                const int64_t o = idx - j->lo;
+                if (!fast_number(p, q, j->as_float, j->out, o) &&
+                    slow_number(p, q, j->as_float, j->out, o) != 0) { j->status = -3; return NULL; }
+            }
+            ++idx;
+            p = q < end ? q + 1 : q;  /* %*c */
+        }
     }
     return NULL;
 }
 
-int cgx_text_read(const char *path, int64_t count, int as_float, void *out, int threads) {
-    text_buf tb;
-    if (open_text(path, &tb) != 0) return -1;
-    const char *buf = tb.data;
-    const size_t len = tb.len;
+/* Run `fn` over pieces [q0, q1) on up to `threads` threads, contiguous piece
+ * ranges per thread.  Returns the first non-zero job status. */
+static int run_jobs(cgx_text *t, int q0, int q1, int threads, void *(*fn)(void *), int64_t lo, int64_t hi,
+                    int as_float, void *out) {
+    piece_job jobs[64];
+    pthread_t tid[64];
+    const int nq = q1 - q0;
+    if (threads > nq) threads = nq;
     if (threads < 1) threads = 1;
     if (threads > 64) threads = 64;
-    if (len < (size_t)threads * 4096) threads = 1;
-    chunk_t ch[64];
+    for (int k = 0; k < threads; ++k) {
+        jobs[k].t = t;
+        jobs[k].q0 = q0 + (int)((int64_t)nq * k / threads);
+        jobs[k].q1 = q0 + (int)((int64_t)nq * (k + 1) / threads);
+        jobs[k].lo = lo;
+        jobs[k].hi = hi;
+        jobs[k].as_float = as_float;
+        jobs[k].out = out;
+        jobs[k].status = 0;
+    }
+    int started[64] = {0};
+    for (int k = 1; k < threads; ++k) started[k] = pthread_create(&tid[k], NULL, fn, &jobs[k]) == 0;
+    for (int k = 1; k < threads; ++k)
+        if (!started[k]) fn(&jobs[k]);
+    fn(&jobs[0]);
+    for (int k = 1; k < threads; ++k)
+        if (started[k]) pthread_join(tid[k], NULL);
+    for (int k = 0; k < threads; ++k)
+        if (jobs[k].status) return jobs[k].status;
+    return 0;
+}
+
+int cgx_text_open(const char *path, int threads, cgx_text **out) {
+    if (!out) return -1;
+    *out = NULL;
+    cgx_text *t = (cgx_text *)calloc(1, sizeof *t);
+    if (!t) return -1;
+    if (open_text(path, &t->tb) != 0) { free(t); return -1; }
+    if (threads < 1) threads = 1;
+    if (threads > 64) threads = 64;
+    const size_t len = t->tb.len;
+    size_t want = len / ((size_t)1 << 20) + 1;
+    if (want < (size_t)threads * 8) want = (size_t)threads * 8;
+    if (want > len / 64 + 1) want = len / 64 + 1; /* small files: few pieces */
+    const int np = (int)want;
+    t->beg = (const char **)malloc(sizeof(char *) * (size_t)np);
+    t->end = (const char **)malloc(sizeof(char *) * (size_t)np);
+    t->first = (int64_t *)calloc((size_t)np + 1, sizeof(int64_t));
+    t->ntok = (int64_t *)calloc((size_t)np, sizeof(int64_t));
+    t->bad = (int *)calloc((size_t)np, sizeof(int));
+    if (!t->beg || !t->end || !t->first || !t->ntok || !t->bad) { cgx_text_close(t); return -1; }
     /* cut at white space: %f skips it, so a cut changes nothing */
-    const char *pos = buf, *end = buf + len;
-    for (int t = 0; t < threads; ++t) {
-        const char *stop = (t == threads - 1) ? end : buf + (len * (size_t)(t + 1)) / (size_t)threads;
+    const char *buf = t->tb.data, *pos = buf, *end = buf + len;
+    for (int q = 0; q < np; ++q) {
+        const char *stop = (q == np - 1) ? end : buf + (len * (size_t)(q + 1)) / (size_t)np;
         if (stop < pos) stop = pos;
         while (stop < end && !IS_SPACE(*stop)) ++stop;
-        ch[t].beg = pos;
-        ch[t].end = stop;
-        ch[t].count = count;
-        ch[t].as_float = as_float;
-        ch[t].out = out;
-        ch[t].status = 0;
+        t->beg[q] = pos;
+        t->end[q] = stop;
         pos = stop;
     }
-    pthread_t tid[64];
-    for (int t = 1; t < threads; ++t) pthread_create(&tid[t], NULL, count_job, &ch[t]);
-    count_job(&ch[0]);
-    for (int t = 1; t < threads; ++t) pthread_join(tid[t], NULL);
+    t->npieces = np;
+    run_jobs(t, 0, np, threads, count_job, 0, 0, 0, NULL);
     /* numbers reachable in file order: up to the first failing conversion */
     int64_t total = 0;
-    int bad = 0;
-    for (int t = 0; t < threads; ++t) {
-        ch[t].first = total;
-        if (!bad) total += ch[t].ntok;
-        bad = bad || ch[t].bad;
+    for (int q = 0; q < np; ++q) {
+        t->first[q] = total;
+        if (!t->stopped) total += t->ntok[q];
+        t->stopped = t->stopped || t->bad[q];
     }
-    if (total < count) { close_text(&tb); return bad ? -3 : -2; }
-    for (int t = 1; t < threads; ++t) pthread_create(&tid[t], NULL, parse_job, &ch[t]);
-    parse_job(&ch[0]);
-    for (int t = 1; t < threads; ++t) pthread_join(tid[t], NULL);
-    close_text(&tb);
-    for (int t = 0; t < threads; ++t)
-        if (ch[t].status != 0) return ch[t].status;
+    t->first[np] = total;
+    /* pieces after the failing one hold no reachable numbers */
+    for (int q = 0, after = 0; q < np; ++q) {
+        if (after) { t->first[q] = total; t->ntok[q] = 0; }
+        after = after || t->bad[q];
+    }
+    t->avail = total;
+    *out = t;
     return 0;
+}
+
+int64_t cgx_text_available(const cgx_text *t, int *stopped) {
+    if (!t) return -1;
+    if (stopped) *stopped = t->stopped;
+    return t->avail;
+}
+
+int cgx_text_read_range(cgx_text *t, int64_t first, int64_t count, int as_float, void *out, int threads) {
+    if (!t || first < 0 || count < 0) return -3;
+    if (count == 0) return 0;
+    if (first + count > t->avail) return t->stopped ? -3 : -2;
+    /* the pieces holding [first, first + count): first[q] <= first < first[q+1] ... */
+    int q0 = 0, q1 = t->npieces;
+    {
+        int lo = 0, hi = t->npieces - 1;
+        while (lo < hi) {  /* last piece with first[q] <= first */
+            const int mid = (lo + hi + 1) / 2;
+            if (t->first[mid] <= first) lo = mid; else hi = mid - 1;
+        }
+        q0 = lo;
+        while (q0 > 0 && t->ntok[q0] == 0) --q0;
+        lo = q0;
+        hi = t->npieces - 1;
+        const int64_t last = first + count - 1;
+        while (lo < hi) {
+            const int mid = (lo + hi + 1) / 2;
+            if (t->first[mid] <= last) lo = mid; else hi = mid - 1;
+        }
+        q1 = lo + 1;
+    }
+    return run_jobs(t, q0, q1, threads, parse_job, first, first + count, as_float, out);
+}
+
+void cgx_text_close(cgx_text *t) {
+    if (!t) return;
+    close_text(&t->tb);
+    free(t->beg);
+    free((void *)t->end);
+    free(t->first);
+    free(t->ntok);
+    free(t->bad);
+    free(t);
+}
+
+int cgx_text_read(const char *path, int64_t count, int as_float, void *out, int threads) {
+    cgx_text *t = NULL;
+    const int rc = cgx_text_open(path, threads, &t);
+    if (rc != 0) return rc;
+    const int r = cgx_text_read_range(t, 0, count, as_float, out, threads);
+    cgx_text_close(t);
+    return r;
 }
 
 int cgx_text_dims(const char *path, int64_t dims[4]) {

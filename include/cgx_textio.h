@@ -30,6 +30,21 @@ int64_t cgx_text_count(const char *path);
  * slices cut at white space (same values). */
 int cgx_text_read(const char *path, int64_t count, int as_float, void *out, int threads);
 
+/* The same reader on an opened, indexed file, for reading it in ranges
+ * (cg_hip streams A to the GPU row block by row block this way):
+ * cgx_text_open maps the file and counts its numbers in ~1 MiB pieces on
+ * `threads` threads (0, or -1 cannot open); cgx_text_available gives how many
+ * the reference's loop would convert (*stopped = 1 if a failing conversion
+ * ends them, 0 if end of file); cgx_text_read_range parses numbers
+ * [first, first + count) into out[0 .. count) from the pieces that hold them
+ * (0, -2 / -3 as cgx_text_read).  A handle is read-only once open: ranges
+ * may be read from several threads at once. */
+typedef struct cgx_text cgx_text;
+int cgx_text_open(const char *path, int threads, cgx_text **t);
+int64_t cgx_text_available(const cgx_text *t, int *stopped);
+int cgx_text_read_range(cgx_text *t, int64_t first, int64_t count, int as_float, void *out, int threads);
+void cgx_text_close(cgx_text *t);
+
 /* dimensions.txt: four integers "A_rows A_cols b_rows b_cols".  0 or <0. */
 int cgx_text_dims(const char *path, int64_t dims[4]);
 

@@ -72,6 +72,8 @@ def lib() -> ctypes.CDLL:
         L.oracle_cg_f64.restype = ctypes.c_int
         L.oracle_set_threads.argtypes = [ctypes.c_int]
         L.oracle_hash_matvec_f64.argtypes = [i64, ctypes.c_uint64, i64, i64, vp, vp]
+        L.oracle_write_text.argtypes = [ctypes.c_char_p, i64, vp, ctypes.c_int]
+        L.oracle_write_text.restype = ctypes.c_int
         L.oracle_cg_f64_hash.argtypes = [i64, ctypes.c_uint64, vp, i64, f64, ctypes.POINTER(OracleStats)]
         L.oracle_cg_f64_hash.restype = ctypes.c_int
         L.oracle_poisson_apply.argtypes = [i64, vp, vp]
@@ -200,6 +202,13 @@ def cg_f64_hash(n: int, seed: int = 42, x0=None, max_iter: int = -1, eps: float 
     if rc != 0:
         raise RuntimeError(f"oracle_cg_f64_hash rc={rc}")
     return x, st
+
+
+def write_text(path: str, values, decimals: int = 4) -> None:
+    """One "%.<decimals>f" value per line (generateSPDmatrix.m's file format)."""
+    v = np.ascontiguousarray(values, np.float64).ravel()
+    if lib().oracle_write_text(path.encode(), v.size, _p(v), decimals) != 0:
+        raise OSError(f"cannot write {path}")
 
 
 def poisson_apply(m: int, p: np.ndarray) -> np.ndarray:

@@ -455,3 +455,15 @@ int oracle_cg_poisson_f64(int64_t m, const double *b, double *x, int64_t max_ite
     free(Av); free(r); free(p);
     return 0;
 }
+
+/* ======================================================================= */
+/* text files in the reference's format (test / measurement helper)        */
+/* ======================================================================= */
+int oracle_write_text(const char *path, int64_t count, const double *v, int decimals) {
+    FILE *f = fopen(path, "w");
+    if (!f) return -1;
+    static char buf[1 << 20];
+    setvbuf(f, buf, _IOFBF, sizeof buf);
+    for (int64_t i = 0; i < count; ++i) fprintf(f, "%.*f\n", decimals, v[i]);
+    return fclose(f) == 0 ? 0 : -1;
+}

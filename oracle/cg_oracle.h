@@ -109,6 +109,10 @@ void oracle_poisson_apply(int64_t m, const double *p, double *out);
 int oracle_cg_poisson_f64(int64_t m, const double *b, double *x, int64_t max_iter, double eps,
                           oracle_stats *st);
 
+/* v[0..count) as one "%.<decimals>f" value per line, as generateSPDmatrix.m
+ * writes its files (fprintf('%.4f\n')).  0 or -1. */
+int oracle_write_text(const char *path, int64_t count, const double *v, int decimals);
+
 /* threads used by oracle_cg_f64's matVec (rows are independent, so results
  * do not depend on it).  f32ref is always single-threaded, like the reference. */
 void oracle_set_threads(int nthreads);

@@ -157,6 +157,31 @@ int main(int argc, char **argv) {
             ++fails;
             continue;
         }
+        if (avail > 0) { /* random ranges through the indexed handle (cg_hip's row-block reads) */
+            cgx_text *th = NULL;
+            if (cgx_text_open(path, 1 + rint_(6), &th) != 0 || cgx_text_available(th, NULL) != avail) {
+                fprintf(stderr, "case %d: cgx_text_open / available\n", c);
+                ++fails;
+            } else {
+                for (int rr = 0; rr < 4; ++rr) {
+                    const int64_t f0 = rint_((int)avail), cnt = 1 + rint_((int)(avail - f0));
+                    double got[4 * kMaxTok];
+                    const int rc = cgx_text_read_range(th, f0, cnt, 0, got, 1 + rint_(4));
+                    if (rc != 0 || memcmp(got, all + f0, (size_t)cnt * 8) != 0) {
+                        fprintf(stderr, "case %d: range [%lld, +%lld) rc %d or values differ\n", c, (long long)f0,
+                                (long long)cnt, rc);
+                        ++fails;
+                        break;
+                    }
+                }
+                double one;
+                if (cgx_text_read_range(th, avail, 1, 0, &one, 1) == 0) {
+                    fprintf(stderr, "case %d: a range past the last value read\n", c);
+                    ++fails;
+                }
+            }
+            cgx_text_close(th);
+        }
         const int64_t want = rint_(5) == 0 ? avail + 1 + rint_(3) : 1 + rint_((int)(avail > 0 ? avail : 1));
         for (int as_float = 0; as_float < 2; ++as_float) {
             void *exp = calloc((size_t)want + 1, 8);
