@@ -79,8 +79,19 @@ static void big_free(big_buf *bb) {
     memset(bb, 0, sizeof *bb);
 }
 
+/* Buffers released on a helper thread, off the critical path: the matrix
+ * (or the ring A streamed through) and the mapping of A's text file.  Two
+ * munmaps of a GiB or more serialise on the process's mm lock with anything
+ * else that maps memory (the b and x0 reads), so this starts after them. */
+typedef struct {
+    big_buf buf;
+    cgx_text *text;
+} release_job;
+
 static void *release_buf(void *arg) {
-    big_free((big_buf *)arg);
+    release_job *r = (release_job *)arg;
+    cgx_text_close(r->text);
+    big_free(&r->buf);
     return NULL;
 }
 
@@ -148,13 +159,19 @@ static void *create_ctx(void *arg) {
  * indexed file while a copy thread sends block k with cgx_set_rows, through
  * a ring of block buffers, so host memory holds at most CGX_CLI_RING_MB
  * (default 1024) of A and, once the context is up, the H2D runs under the
- * parse.  (CGX_CLI_STREAM=0: parse all of A, then one cgx_set_system.) */
+ * parse.  The ring is one buffer: when the copy thread finds several parsed
+ * blocks waiting (the HIP runtime came up after them) it sends the run of
+ * them that is contiguous in the ring with one cgx_set_rows, since pageable
+ * H2D copies run at ~5 GB/s per 32 MB call and ~20 GB/s per 256 MB call.
+ * Blocks are CGX_CLI_BLOCK_MB (default 128) of A.
+ * (CGX_CLI_STREAM=0: parse all of A, then one cgx_set_system.) */
 typedef struct {
     cgx_text *text;
     int64_t n, block_rows, nblocks;
     int nslots, as_float, threads;
     size_t es;
-    big_buf *slot;        /* nslots buffers of block_rows * n values (huge pages) */
+    big_buf ring;         /* nslots slots of block_rows * n values (huge pages) */
+    size_t slot_bytes;
     int *filled;          /* slot holds block filled[s] - 1 (0 = free) */
     pthread_mutex_t mu;
     pthread_cond_t cv;
@@ -170,19 +187,23 @@ static void *stream_copy(void *arg) {
     a_stream *st = (a_stream *)arg;
     if (st->creator_threaded) pthread_join(st->creator, NULL);
     int rc = st->job->rc;
-    for (int64_t k = 0; k < st->nblocks && rc == CGX_OK; ++k) {
+    for (int64_t k = 0; k < st->nblocks && rc == CGX_OK;) {
         const int sl = (int)(k % st->nslots);
         pthread_mutex_lock(&st->mu);
         while (st->filled[sl] != k + 1 && !st->abort_rc) pthread_cond_wait(&st->cv, &st->mu);
+        int64_t run = 1; /* parsed blocks k, k+1, ... in consecutive slots */
+        while (k + run < st->nblocks && sl + run < st->nslots && st->filled[sl + run] == k + run + 1) ++run;
         const int stop = st->abort_rc;
         pthread_mutex_unlock(&st->mu);
         if (stop) break;
-        const int64_t row0 = k * st->block_rows, rows = row0 + st->block_rows <= st->n ? st->block_rows : st->n - row0;
-        rc = cgx_set_rows(st->job->ctx, row0, rows, st->slot[sl].p, st->n, NULL, NULL);
+        const int64_t row0 = k * st->block_rows, end = (k + run) * st->block_rows < st->n ? (k + run) * st->block_rows : st->n;
+        rc = cgx_set_rows(st->job->ctx, row0, end - row0, (char *)st->ring.p + (size_t)sl * st->slot_bytes, st->n,
+                          NULL, NULL);
         pthread_mutex_lock(&st->mu);
-        st->filled[sl] = 0;
+        for (int64_t q = 0; q < run; ++q) st->filled[sl + q] = 0;
         pthread_cond_broadcast(&st->cv);
         pthread_mutex_unlock(&st->mu);
+        k += run;
     }
     st->t_last_h2d = now_s();
     pthread_mutex_lock(&st->mu);
@@ -203,8 +224,8 @@ static int stream_parse(a_stream *st) {
         pthread_mutex_unlock(&st->mu);
         if (stop) return 0; /* the copy side reports its own error */
         const int64_t row0 = k * st->block_rows, rows = row0 + st->block_rows <= st->n ? st->block_rows : st->n - row0;
-        const int rc = cgx_text_read_range(st->text, row0 * st->n, rows * st->n, st->as_float, st->slot[sl].p,
-                                           st->threads);
+        const int rc = cgx_text_read_range(st->text, row0 * st->n, rows * st->n, st->as_float,
+                                           (char *)st->ring.p + (size_t)sl * st->slot_bytes, st->threads);
         pthread_mutex_lock(&st->mu);
         if (rc != 0) st->abort_rc = 1;
         else st->filled[sl] = (int)(k + 1);
@@ -313,6 +334,9 @@ int main(int argc, char **argv) {
     const size_t es = fp32ref ? 4 : 8;
     void *x = malloc((size_t)n * es);
     void *A = NULL, *b = NULL;
+    /* static: the release thread may still read it while an error path
+     * returns from main */
+    static release_job rel = {{NULL, NULL, 0}, NULL};
     big_buf Abuf = {NULL, NULL, 0};
     pthread_t freer;
     int freeing = 0;
@@ -355,10 +379,10 @@ int main(int argc, char **argv) {
             read_rc = stopped ? -3 : -2;
         }
         if (!read_rc) {
-            const char *rm = getenv("CGX_CLI_RING_MB");
+            const char *rm = getenv("CGX_CLI_RING_MB"), *bm = getenv("CGX_CLI_BLOCK_MB");
             const double ring_mb = (rm && atof(rm) > 0) ? atof(rm) : 1024.0;
             const size_t row_bytes = (size_t)n * es;
-            const size_t block_bytes = (size_t)32 << 20;
+            const size_t block_bytes = (size_t)(((bm && atof(bm) > 0) ? atof(bm) : 128.0) * 1048576.0);
             st.n = n;
             st.es = es;
             st.block_rows = (int64_t)(block_bytes / row_bytes) > 0 ? (int64_t)(block_bytes / row_bytes) : 1;
@@ -370,11 +394,12 @@ int main(int argc, char **argv) {
             st.nslots = (int)slots;
             st.as_float = fp32ref;
             st.threads = threads;
-            st.slot = calloc((size_t)st.nslots, sizeof(big_buf));
+            st.slot_bytes = (size_t)st.block_rows * row_bytes;
             st.filled = calloc((size_t)st.nslots, sizeof(int));
-            int ok = st.slot && st.filled;
-            for (int q = 0; ok && q < st.nslots; ++q) ok = big_alloc(&st.slot[q], (size_t)st.block_rows * row_bytes) == 0;
-            if (!ok) { fprintf(stderr, "can't allocate memory for vector\n"); return 1; }
+            if (!st.filled || big_alloc(&st.ring, (size_t)st.nslots * st.slot_bytes) != 0) {
+                fprintf(stderr, "can't allocate memory for vector\n");
+                return 1;
+            }
             pthread_mutex_init(&st.mu, NULL);
             pthread_cond_init(&st.cv, NULL);
             st.creator = creator;
@@ -397,14 +422,15 @@ int main(int argc, char **argv) {
                 if (threaded) pthread_join(creator, NULL);
             }
             t_h2d = st.t_last_h2d;
-            for (int q = 0; q < st.nslots; ++q) big_free(&st.slot[q]);
-            free(st.slot);
+            rel.buf = st.ring;  /* released after the b and x0 reads */
             free(st.filled);
         } else if (threaded) {
             pthread_join(creator, NULL);
         }
-        cgx_text_close(st.text);
         if (!read_rc) read_rc = read_file(pos[1], n, fp32ref, b, threads) || read_file(pos[2], n, fp32ref, x, 1);
+        rel.text = st.text;
+        if (pthread_create(&freer, NULL, release_buf, &rel) == 0) freeing = 1;
+        else release_buf(&rel);
     } else {
         read_rc = spd_n > 0 ? 0
                             : (read_file(pos[0], n * n, fp32ref, A, threads) ||
@@ -439,8 +465,9 @@ int main(int argc, char **argv) {
         t_dist1 = now_s();
         /* A is no longer needed: release it on a helper thread while the
          * solve runs (unmapping 268 MB took 16-30 ms on the critical path) */
-        if (pthread_create(&freer, NULL, release_buf, &Abuf) == 0) freeing = 1;
-        else big_free(&Abuf);
+        rel.buf = Abuf;
+        if (pthread_create(&freer, NULL, release_buf, &rel) == 0) freeing = 1;
+        else release_buf(&rel);
         free(b);
         if (rc != CGX_OK) return die_cgx(rc, "cgx_set_system");
     }

@@ -282,7 +282,7 @@ int64_t cgx_text_count(const char *path) {
 }
 
 /* ---- the indexed file: pieces cut at white space, each with its count ---- */
-/* A piece is ~1 MiB of text (at least 8 per thread); the count pass fills in
+/* A piece is ~256 KiB of text (at least 8 per thread); the count pass fills in
  * how many numbers each holds, so a range of values can be parsed from the
  * pieces that hold it alone (row blocks streamed by cg_hip). */
 struct cgx_text {
@@ -377,7 +377,7 @@ int cgx_text_open(const char *path, int threads, cgx_text **out) {
     if (threads < 1) threads = 1;
     if (threads > 64) threads = 64;
     const size_t len = t->tb.len;
-    size_t want = len / ((size_t)1 << 20) + 1;
+    size_t want = len / ((size_t)1 << 18) + 1;
     if (want < (size_t)threads * 8) want = (size_t)threads * 8;
     if (want > len / 64 + 1) want = len / 64 + 1; /* small files: few pieces */
     const int np = (int)want;

@@ -9,7 +9,7 @@ import pytest
 
 import conjugate_gradient_amd as cg
 import oracle
-from _cases import FIX, case, golden_x
+from _cases import FIX, case, golden_x, mpi_golden_x
 
 pytestmark = pytest.mark.gpu
 
@@ -80,8 +80,8 @@ def test_cli_generated_text_files_multi_gpu(golden, tmp_path):
     parallel_cg.c-style run (--gpus 2: two row blocks) prints its lines."""
     n = 512
     A, b = oracle.spd_matlab(n, np.float64)
-    for name, arr, fmt in (("A.txt", A.ravel(), "%.4f"), ("b.txt", b, "%.4f"), ("x0.txt", np.zeros(n), "%.1f")):
-        arr.tofile(str(tmp_path / name), sep="\n", format=fmt)
+    for name, arr, dec in (("A.txt", A, 4), ("b.txt", b, 4), ("x0.txt", np.zeros(n), 1)):
+        oracle.write_text(str(tmp_path / name), arr, dec)
     paths = [str(tmp_path / f) for f in ("A.txt", "b.txt", "x0.txt")]
     out = run("--fp32-ref", "--print-x", *paths)
     x = printed_x(out, n, np.float32)
@@ -107,3 +107,55 @@ def test_cli_synthetic_spd():
     assert "Computing cg of matrix size : 16777216" in out
     it = int(out.split("iterations:")[1].split()[0])
     assert 3 <= it <= 20 and "converged: 1" in out
+
+
+def _spd512_files(tmp_path):
+    n = 512
+    A, b = oracle.spd_matlab(n, np.float64)
+    for name, arr, dec in (("A.txt", A, 4), ("b.txt", b, 4), ("x0.txt", np.zeros(n), 1)):
+        oracle.write_text(str(tmp_path / name), arr, dec)
+    return n, [str(tmp_path / f) for f in ("A.txt", "b.txt", "x0.txt")]
+
+
+@pytest.mark.parametrize("args", [("--fp32-ref",), ("--gpus", "2", "--fp32-ref"), ("--eps", "1e-10"),
+                                  ("--gpus", "2", "--eps", "1e-10"), ("--symmetric", "--eps", "1e-10")])
+def test_cli_streamed_a_equals_materialized(golden, tmp_path, args):
+    """A streamed to the device in ragged row blocks (25 rows of 512: 21
+    blocks, the last 12 rows) through a ring of 3 slots, so the parse wraps
+    the ring, waits for free slots and the copy side merges runs of parsed
+    blocks: the same x, bit for bit, as A parsed whole and sent in one copy
+    (CGX_CLI_STREAM=0), and the reference's x for --fp32-ref
+    (serialConjugate.c's on one GPU, parallel_cg.c's at np=2 on two)."""
+    n, paths = _spd512_files(tmp_path)
+    es = 4 if "--fp32-ref" in args else 8
+    block_mb = 25 * n * es / 1048576
+    outs = {}
+    for mode, extra in (("stream", {"CGX_CLI_BLOCK_MB": repr(block_mb), "CGX_CLI_RING_MB": repr(3 * block_mb)}),
+                        ("whole", {"CGX_CLI_STREAM": "0"})):
+        r = subprocess.run([cg.CLI_PATH, *args, "--print-x", "--stats", *paths], capture_output=True, text=True,
+                           timeout=300, env=dict(os.environ, CGX_CLI_TIMES="1", **extra))
+        assert r.returncode == 0, r.stdout + r.stderr
+        assert f'"streamed": {int(mode == "stream")}' in r.stderr
+        outs[mode] = r.stdout
+    dt = np.float32 if es == 4 else np.float64
+    xs, xw = printed_x(outs["stream"], n, dt), printed_x(outs["whole"], n, dt)
+    assert np.array_equal(xs, xw)
+    if es == 4:
+        ref = golden_x(golden, "spd512") if "--gpus" not in args else mpi_golden_x("parallel_spd512_np2")
+        assert np.array_equal(xs.view(np.uint32), ref.view(np.uint32))
+
+
+@pytest.mark.parametrize("cut", ["short", "bad"])
+def test_cli_streamed_a_bad_file_fails(tmp_path, cut):
+    """A truncated A, or one whose last block holds a value fscanf("%f")
+    cannot read, stops the streamed run with the reader's message and exit 1
+    (the index pass over the file finds it before any block is parsed)."""
+    n, paths = _spd512_files(tmp_path)
+    lines = open(paths[0]).read().splitlines()
+    lines = lines[:-7] if cut == "short" else lines[:-7] + ["abc"] + lines[-6:]
+    with open(paths[0], "w") as f:
+        f.write("\n".join(lines) + "\n")
+    r = subprocess.run([cg.CLI_PATH, "--fp32-ref", *paths], capture_output=True, text=True, timeout=300,
+                       env=dict(os.environ, CGX_CLI_BLOCK_MB=repr(25 * n * 4 / 1048576)))
+    assert r.returncode == 1
+    assert ("fewer than" if cut == "short" else "malformed number") in r.stderr

@@ -10,9 +10,11 @@ larger): generateSPDmatrix(n) written as the MATLAB script writes it
     whole program (parse + H2D + GPU solve + print), in three modes: the
     default (A parsed and sent to the GPU row block by row block through a
     ring of up to 1 GiB), A parsed whole and sent in one copy
-    (CGX_CLI_STREAM=0, round 1's path), and the stream through a 64 MiB
-    ring (CGX_CLI_RING_MB=64: host memory for A bounded).
-The x vectors must be identical bit for bit.  oracle/_ref is the reference
+    (CGX_CLI_STREAM=0, round 1's path), the stream through a 64 MiB
+    ring (CGX_CLI_RING_MB=64: host memory for A bounded) and the stream in
+    32 MiB blocks (CGX_CLI_BLOCK_MB=32; the default is 128).
+The x vectors of every mode must be identical bit for bit (to the
+reference's when it runs).  oracle/_ref is the reference
 compiled here from its sources (it travels with the repo snapshot; the
 reference sources do not).
 
@@ -80,10 +82,11 @@ def main():
         if exe:
             t_init, t_solve, xref = run_reference(exe, n, td, paths, res)
         # cg_hip: the whole program, alternating the modes
-        modes = {"fast": {}, "materialize": {"CGX_CLI_STREAM": "0"}, "ring64": {"CGX_CLI_RING_MB": "64"}}
+        modes = {"fast": {}, "materialize": {"CGX_CLI_STREAM": "0"}, "ring64": {"CGX_CLI_RING_MB": "64"},
+                 "block32": {"CGX_CLI_BLOCK_MB": "32"}}
         runs = {k: [] for k in modes}
         phases = {}
-        out = ""
+        xs = {}
         for rep in range(a.reps):
             for mode, extra in modes.items():
                 env = dict(os.environ, CGX_CLI_TIMES="1", **extra)
@@ -98,12 +101,15 @@ def main():
                     rec["process_s"] = runs[mode][-1]
                     rec["after_output_s"] = rec["process_s"] - rec["printed_s"]  # teardown + exit, as seen outside
                     phases.setdefault(mode, []).append(rec)
+                lines = proc.stdout.strip().splitlines()
+                xs.setdefault(mode, []).append(np.array([float(v) for v in lines[-n:]], dtype=np.float32))
                 if mode == "fast":
-                    out = proc.stdout
+                    head = lines[:4]
         med = {k: sorted(v)[len(v) // 2] for k, v in runs.items()}
         res["cg_hip_phases_s"] = phases.get("fast", [])
         res["cg_hip_phases_materialize_s"] = phases.get("materialize", [])
         res["cg_hip_phases_ring64_s"] = phases.get("ring64", [])
+        res["cg_hip_phases_block32_s"] = phases.get("block32", [])
         for mode in modes:
             recs = phases.get(mode, [])
             for r in recs:  # the critical path once HIP is up: context, distribution, solve, x back
@@ -113,19 +119,19 @@ def main():
                 v = sorted(r[key] for r in recs if key in r)
                 if v:
                     res[f"cg_hip_{key[:-2]}_med_s_{mode}"] = v[len(v) // 2]
-        lines = out.strip().splitlines()
-        x = np.array([float(v) for v in lines[-n:]], dtype=np.float32)
-        xr = np.fromfile(xref, dtype=np.float32) if xref else x
+        xr = np.fromfile(xref, dtype=np.float32) if xref else xs["fast"][0]
+        same = all(np.array_equal(x.view(np.uint32), xr.view(np.uint32)) for v in xs.values() for x in v)
         t_cli = med["fast"]
         res.update({"cg_hip_total_s": t_cli, "cg_hip_total_runs_s": runs["fast"],
                     "cg_hip_total_materialize_s": med["materialize"], "cg_hip_total_materialize_runs_s": runs["materialize"],
                     "cg_hip_total_ring64_s": med["ring64"], "cg_hip_total_ring64_runs_s": runs["ring64"],
-                    "cg_hip_stdout_head": lines[:4],
-                    "x_bit_identical": bool(np.array_equal(x.view(np.uint32), xr.view(np.uint32))),
+                    "cg_hip_total_block32_s": med["block32"], "cg_hip_total_block32_runs_s": runs["block32"],
+                    "cg_hip_stdout_head": head,
+                    "x_bit_identical": bool(same),
                     "speedup_total": (t_init + t_solve) / t_cli if exe else None, "threads": a.threads,
                     "note": "reference_conjugrad_process_s includes the harness reading raw float files "
                             "and embedding the system (n <= 8192); the reference itself is single-threaded; "
-                            "cg_hip times are medians of 5 alternating runs per mode"})
+                            f"cg_hip times are medians of {a.reps} alternating runs per mode"})
     print(json.dumps(res, indent=1))
     if a.out:
         with open(a.out, "w") as f:
