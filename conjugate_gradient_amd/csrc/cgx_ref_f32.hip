@@ -213,6 +213,249 @@ __global__ __launch_bounds__(64) void k_matvec_ref_f32_r16(const float *__restri
     if (t < kRef2Rows && row0 + t < rows) out[row0 + t] = acc;
 }
 
+// The same float arithmetic at the HBM rate: loads decoupled from the chains.
+// k_matvec_ref_f32_r16 issues one tile per wave and then waits for it, so
+// every step costs an HBM round trip (62 us at N=8192, ~4.1 TB/s).  Here a
+// 256-thread block owns 32 rows and keeps two 32 x 512 tiles of A in flight
+// (16 nt 16-B buffer loads per lane per tile, two register sets).  Per step
+// (one barrier) wave 0's lanes 0-31 add up tile t from LDS, one row each,
+// while every lane waits for its share of tile t+1 (issued two steps
+// earlier), forms the products A[i][j] * x[j] (rounded to float, as
+// serialConjugate.c:117 forms them) into the other LDS slot and issues its
+// loads of tile t+3.
+//  - Buffer loads: one VGPR offset per lane, the row and tile in the SGPR
+//    offset, so the two register sets fit without copies through AGPRs.
+//    Every step issues the same loads whatever the tile (tiles past the end
+//    read past the buffer's range: zeros, no memory access), and the loads of
+//    a set stay together (sched_barrier), so the wait before the products is
+//    "all but the newer set" (vmcnt 17), not 0.
+//  - FULL: rows % 32 == 0 and cols % 512 == 0 (the reference's sizes).
+//    Otherwise rows past `rows` are out of the buffer's range (zeros) and
+//    columns past `cols` are zeroed: their products are +0.0f, and
+//    acc + 0.0f == acc exactly (acc starts at +0, and a round-to-nearest sum
+//    never makes -0 from it), so the chains still run whole tiles.
+//  - Needs 16-B aligned A and x and lda % 4 == 0.
+constexpr int kRef3Rows = 32, kRef3TC = 512, kRef3Q = kRef3TC / 4, kRef3Ld4 = kRef3Q + 1;
+constexpr int kRef3K = kRef3Rows * kRef3Q / 256;
+static_assert(kRef3K == 16, "lane t: column quad t % 128 of rows t / 128 + 2k");
+template <bool FULL>
+__global__ __launch_bounds__(256) void k_matvec_ref_f32_w4(const float *__restrict__ A, int64_t lda,
+                                                           int64_t rows, int64_t cols,
+                                                           const float *__restrict__ v,
+                                                           float *__restrict__ out) {
+#pragma clang fp contract(off)
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    __shared__ f4 prod[2][kRef3Rows * kRef3Ld4];
+    const int t = threadIdx.x;
+    const int64_t row0 = (int64_t)blockIdx.x * kRef3Rows;
+    const int64_t ntiles = (cols + kRef3TC - 1) / kRef3TC;
+    const int quad = t % kRef3Q, rsub = t / kRef3Q;
+    const int64_t brows = rows - row0 < kRef3Rows ? rows - row0 : kRef3Rows;
+    const __amdgpu_buffer_rsrc_t ars =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(A + row0 * lda), 0, (int)(brows * lda * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc((void *)v, 0, (int)(cols * 4), 0x00020000);
+    const int voff = (int)((rsub * lda + 4 * quad) * 4);
+    const int end_off = (int)(brows * lda * 4);  // a tile past the end: every load out of range
+    f4 a0[kRef3K], a1[kRef3K];
+    f4 p0, p1;
+    auto issue = [&](f4 (&a)[kRef3K], f4 &pv, int64_t tile) {
+        const bool real = tile < ntiles;
+        const int c4 = (int)(tile * kRef3TC * 4);
+#pragma unroll
+        for (int k = 0; k < kRef3K; ++k)
+            a[k] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(
+                                              ars, voff, real ? (int)(2 * k * lda * 4) + c4 : end_off, 2));
+        pv = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(vrs, quad * 16, real ? c4 : (int)(cols * 4), 0));
+    };
+    auto store = [&](f4 (&a)[kRef3K], f4 &pv, int slot, int64_t tile) {
+        if (!FULL) {  // columns past `cols`: +0 products whatever A's padding holds
+            const int64_t cq = tile * kRef3TC + 4 * quad;
+            for (int e = 0; e < 4; ++e)
+                if (cq + e >= cols) {
+                    pv[e] = 0.0f;
+#pragma unroll
+                    for (int k = 0; k < kRef3K; ++k) a[k][e] = 0.0f;
+                }
+        }
+#pragma unroll
+        for (int k = 0; k < kRef3K; ++k) prod[slot][(rsub + 2 * k) * kRef3Ld4 + quad] = a[k] * pv;
+    };
+    float acc = 0.0f;  // matvec[i] = 0.0  (serialConjugate.c:114)
+    auto chain = [&](int slot) {  // matvec[i] += A[i][j] * x[j], j ascending (:117)
+        const f4 *trow = &prod[slot][t * kRef3Ld4];
+        constexpr int G = 8;  // two register sets of G quads: one read from LDS while the other is added
+        f4 q[G], qn[G];
+        auto add = [&](const f4 (&w)[G]) {
+#pragma unroll
+            for (int u = 0; u < G; ++u) {
+                acc = acc + w[u].x;
+                acc = acc + w[u].y;
+                acc = acc + w[u].z;
+                acc = acc + w[u].w;
+            }
+        };
+#pragma unroll
+        for (int u = 0; u < G; ++u) q[u] = trow[u];
+#pragma unroll 1
+        for (int j4 = 0; j4 < kRef3Q; j4 += 2 * G) {
+#pragma unroll
+            for (int u = 0; u < G; ++u) qn[u] = trow[j4 + G + u];
+            add(q);
+            if (j4 + 2 * G < kRef3Q) {
+#pragma unroll
+                for (int u = 0; u < G; ++u) q[u] = trow[j4 + 2 * G + u];
+            }
+            add(qn);
+        }
+    };
+    issue(a0, p0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    issue(a1, p1, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    store(a0, p0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    issue(a0, p0, 2);
+    __builtin_amdgcn_sched_barrier(0);
+    __syncthreads();
+    // step for tile tt (slot tt & 1): wave 0 adds it up; every lane stores
+    // tile tt + 1 (register set (tt + 1) & 1) into the other slot and reuses
+    // that set for tile tt + 3.  Unrolled by two so the sets are static.
+    for (int64_t tt = 0; tt < ntiles; tt += 2) {
+        if (t < kRef3Rows) chain(0);
+        __builtin_amdgcn_sched_barrier(0);
+        store(a1, p1, 1, tt + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        issue(a1, p1, tt + 3);
+        __builtin_amdgcn_sched_barrier(0);
+        __syncthreads();
+        if (t < kRef3Rows && tt + 1 < ntiles) chain(1);
+        __builtin_amdgcn_sched_barrier(0);
+        store(a0, p0, 0, tt + 2);
+        __builtin_amdgcn_sched_barrier(0);
+        issue(a0, p0, tt + 4);
+        __builtin_amdgcn_sched_barrier(0);
+        __syncthreads();
+    }
+    if (t < kRef3Rows && row0 + t < rows) out[row0 + t] = acc;
+}
+
+// The same with a dedicated adding wave: 5 waves, wave 0 only runs the
+// chains and waves 1-4 only load and form products, so a step costs
+// max(chain, loads) rather than chain + wave 0's own share of the loads.
+// Measured at N=8192 (rocprofv3, profiles/r02_kernel_stats_ref_f32_n8192.csv):
+// 49.6 us against 53.9 for k_matvec_ref_f32_w4 and 62.3 for the 16-row
+// kernel; a third register set (192 KiB in flight per CU) measured 51.9.
+template <bool FULL>
+__global__ __launch_bounds__(320) void k_matvec_ref_f32_w5(const float *__restrict__ A, int64_t lda,
+                                                           int64_t rows, int64_t cols,
+                                                           const float *__restrict__ v,
+                                                           float *__restrict__ out) {
+#pragma clang fp contract(off)
+    typedef float f4 __attribute__((ext_vector_type(4)));
+    __shared__ f4 prod[2][kRef3Rows * kRef3Ld4];
+    const int t = threadIdx.x;
+    const int l = t >= 64 ? t - 64 : 0;  // loader lane (waves 1-4); wave 0 only adds
+    const int64_t row0 = (int64_t)blockIdx.x * kRef3Rows;
+    const int64_t ntiles = (cols + kRef3TC - 1) / kRef3TC;
+    const int quad = l % kRef3Q, rsub = l / kRef3Q;
+    const int64_t brows = rows - row0 < kRef3Rows ? rows - row0 : kRef3Rows;
+    const __amdgpu_buffer_rsrc_t ars =
+        __builtin_amdgcn_make_buffer_rsrc((void *)(A + row0 * lda), 0, (int)(brows * lda * 4), 0x00020000);
+    const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc((void *)v, 0, (int)(cols * 4), 0x00020000);
+    const int voff = (int)((rsub * lda + 4 * quad) * 4);
+    const int end_off = (int)(brows * lda * 4);  // a tile past the end: every load out of range
+    f4 a0[kRef3K], a1[kRef3K];
+    f4 p0, p1;
+    auto issue = [&](f4 (&a)[kRef3K], f4 &pv, int64_t tile) {
+        const bool real = tile < ntiles;
+        const int c4 = (int)(tile * kRef3TC * 4);
+#pragma unroll
+        for (int k = 0; k < kRef3K; ++k)
+            a[k] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(
+                                              ars, voff, real ? (int)(2 * k * lda * 4) + c4 : end_off, 2));
+        pv = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(vrs, quad * 16, real ? c4 : (int)(cols * 4), 0));
+    };
+    auto store = [&](f4 (&a)[kRef3K], f4 &pv, int slot, int64_t tile) {
+        if (!FULL) {  // columns past `cols`: +0 products whatever A's padding holds
+            const int64_t cq = tile * kRef3TC + 4 * quad;
+            for (int e = 0; e < 4; ++e)
+                if (cq + e >= cols) {
+                    pv[e] = 0.0f;
+#pragma unroll
+                    for (int k = 0; k < kRef3K; ++k) a[k][e] = 0.0f;
+                }
+        }
+#pragma unroll
+        for (int k = 0; k < kRef3K; ++k) prod[slot][(rsub + 2 * k) * kRef3Ld4 + quad] = a[k] * pv;
+    };
+    float acc = 0.0f;  // matvec[i] = 0.0  (serialConjugate.c:114)
+    auto chain = [&](int slot) {  // matvec[i] += A[i][j] * x[j], j ascending (:117)
+        const f4 *trow = &prod[slot][t * kRef3Ld4];
+        constexpr int G = 8;  // two register sets of G quads: one read from LDS while the other is added
+        f4 q[G], qn[G];
+        auto add = [&](const f4 (&w)[G]) {
+#pragma unroll
+            for (int u = 0; u < G; ++u) {
+                acc = acc + w[u].x;
+                acc = acc + w[u].y;
+                acc = acc + w[u].z;
+                acc = acc + w[u].w;
+            }
+        };
+#pragma unroll
+        for (int u = 0; u < G; ++u) q[u] = trow[u];
+#pragma unroll 1
+        for (int j4 = 0; j4 < kRef3Q; j4 += 2 * G) {
+#pragma unroll
+            for (int u = 0; u < G; ++u) qn[u] = trow[j4 + G + u];
+            add(q);
+            if (j4 + 2 * G < kRef3Q) {
+#pragma unroll
+                for (int u = 0; u < G; ++u) q[u] = trow[j4 + 2 * G + u];
+            }
+            add(qn);
+        }
+    };
+    // Role by wave (a scalar branch: each role's loop is straight-line code,
+    // so the loaders' waits stay "all but the newer set"); both roles pass
+    // the same barriers, one per step.
+    const int64_t nsteps = (ntiles + 1) / 2 * 2;  // the loaders' steps, whole pairs
+    if (__builtin_amdgcn_readfirstlane(t >> 6) == 0) {
+        __syncthreads();
+        for (int64_t tt = 0; tt < nsteps; ++tt) {
+            if (t < kRef3Rows && tt < ntiles) chain((int)(tt & 1));
+            __syncthreads();
+        }
+        if (t < kRef3Rows && row0 + t < rows) out[row0 + t] = acc;
+        return;
+    }
+    // at step tt the loaders store tile tt + 1 into slot (tt + 1) & 1 and
+    // reuse its register set for tile tt + 3 (unrolled by two so the sets
+    // are static; steps past the last tile store zeros into a slot nobody
+    // reads)
+    issue(a0, p0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    issue(a1, p1, 1);
+    __builtin_amdgcn_sched_barrier(0);
+    store(a0, p0, 0, 0);
+    __builtin_amdgcn_sched_barrier(0);
+    issue(a0, p0, 2);
+    __builtin_amdgcn_sched_barrier(0);
+    __syncthreads();
+    for (int64_t tt = 0; tt < nsteps; tt += 2) {
+        store(a1, p1, 1, tt + 1);
+        __builtin_amdgcn_sched_barrier(0);
+        issue(a1, p1, tt + 3);
+        __builtin_amdgcn_sched_barrier(0);
+        __syncthreads();
+        store(a0, p0, 0, tt + 2);
+        __builtin_amdgcn_sched_barrier(0);
+        issue(a0, p0, tt + 4);
+        __builtin_amdgcn_sched_barrier(0);
+        __syncthreads();
+    }
+}
+
 // vecVec: one wave; products in parallel, the sum strictly sequential in
 // index order (s = s + a_i b_i), broadcast lane by lane with v_readlane.
 __global__ __launch_bounds__(64) void k_dot_ref_f32(int64_t n, const float *__restrict__ a,
@@ -295,13 +538,32 @@ __global__ __launch_bounds__(256) void k_dot_ref_f32_blk(int64_t n, const float 
         if (t < 64) {  // wave 0: sum += v1[i] * v2[i], i ascending (:152)
             const int64_t left = n - ch * kDotChunk;
             if (left >= kDotChunk) {
-#pragma unroll 8
-                for (int q = 0; q < kDotChunk / 4; ++q) {
-                    const f4 v = sp[buf][q];
-                    s = s + v.x;
-                    s = s + v.y;
-                    s = s + v.z;
-                    s = s + v.w;
+                // two register sets of G quads: one read from LDS while the
+                // other is added (G = 16: 2.9-3.3 ns per dependent add
+                // against 3.2-3.6 at G = 8, tools/microbench/add_chain.hip)
+                constexpr int G = 16;
+                f4 q[G], qn[G];
+                auto add = [&](const f4 (&w)[G]) {
+#pragma unroll
+                    for (int u = 0; u < G; ++u) {
+                        s = s + w[u].x;
+                        s = s + w[u].y;
+                        s = s + w[u].z;
+                        s = s + w[u].w;
+                    }
+                };
+#pragma unroll
+                for (int u = 0; u < G; ++u) q[u] = sp[buf][u];
+#pragma unroll 1
+                for (int j = 0; j < kDotChunk / 4; j += 2 * G) {
+#pragma unroll
+                    for (int u = 0; u < G; ++u) qn[u] = sp[buf][j + G + u];
+                    add(q);
+                    if (j + 2 * G < kDotChunk / 4) {
+#pragma unroll
+                        for (int u = 0; u < G; ++u) q[u] = sp[buf][j + 2 * G + u];
+                    }
+                    add(qn);
                 }
             } else {
                 const float *spf = reinterpret_cast<const float *>(sp[buf]);
@@ -358,9 +620,23 @@ __global__ __launch_bounds__(kNT) void k_update_p_ref_f32(int64_t n, float *__re
 hipError_t matvec_ref_f32(const float *A, int64_t lda, int64_t rows, int64_t cols, const float *v,
                           float *out, hipStream_t s) {
     if (rows <= 0) return hipSuccess;
-    if (env_int("CGX_REF_MV", 2) == 1)  // the 64-row, 128-column-tile kernel (kept for A/B)
+    const int variant = env_int("CGX_REF_MV", 3);
+    // 16-B aligned rows and x; the buffer offsets (32 rows of lda floats) fit in 31 bits
+    const bool vec_ok = (lda & 3) == 0 && lda < (int64_t(1) << 23) &&
+                        ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(v)) & 15) == 0;
+    if (variant == 1)  // the 64-row, 128-column-tile kernel (kept for A/B)
         hipLaunchKernelGGL(k_matvec_ref_f32, dim3((unsigned)((rows + 63) / 64)), dim3(64), 0, s, A, lda, rows,
                            cols, v, out);
+    else if ((variant == 3 || variant == 4) && vec_ok) {
+        const bool full = rows % kRef3Rows == 0 && cols % kRef3TC == 0;
+        const dim3 grid((unsigned)((rows + kRef3Rows - 1) / kRef3Rows));
+        if (variant == 3)  // a dedicated adding wave (default)
+            hipLaunchKernelGGL(full ? k_matvec_ref_f32_w5<true> : k_matvec_ref_f32_w5<false>, grid, dim3(320), 0, s,
+                               A, lda, rows, cols, v, out);
+        else  // wave 0 adds and loads
+            hipLaunchKernelGGL(full ? k_matvec_ref_f32_w4<true> : k_matvec_ref_f32_w4<false>, grid, dim3(256), 0, s,
+                               A, lda, rows, cols, v, out);
+    }
     else
         hipLaunchKernelGGL(k_matvec_ref_f32_r16, dim3((unsigned)((rows + kRef2Rows - 1) / kRef2Rows)), dim3(64), 0,
                            s, A, lda, rows, cols, v, out);
@@ -396,7 +672,11 @@ hipError_t update_p_ref_f32(int64_t n, float *p, const float *r, const float *rr
 // Load this file's code object on the current device now (see preload_kernels).
 hipError_t preload_ref_f32() {
     hipFuncAttributes a;
-    return hipFuncGetAttributes(&a, reinterpret_cast<const void *>(k_matvec_ref_f32_r16));
+    hipError_t e = hipFuncGetAttributes(&a, reinterpret_cast<const void *>(k_matvec_ref_f32_r16));
+    if (e == hipSuccess) e = hipFuncGetAttributes(&a, reinterpret_cast<const void *>(k_matvec_ref_f32_w4<true>));
+    if (e == hipSuccess) e = hipFuncGetAttributes(&a, reinterpret_cast<const void *>(k_matvec_ref_f32_w4<false>));
+    if (e == hipSuccess) e = hipFuncGetAttributes(&a, reinterpret_cast<const void *>(k_matvec_ref_f32_w5<true>));
+    return e != hipSuccess ? e : hipFuncGetAttributes(&a, reinterpret_cast<const void *>(k_matvec_ref_f32_w5<false>));
 }
 
 }  // namespace cgx

@@ -25,9 +25,28 @@ def _gpu(built):
     assert cg.device_count() >= 1, "no GPU visible: the HIP path must run"
 
 
-@pytest.mark.parametrize("variant", ["1", "2"])  # CGX_REF_MV: 64-row x 128 tiles / 16-row x 512 tiles (default)
+@pytest.mark.parametrize("rows,cols", [(64, 1024), (40, 1000)])
+def test_matvec_ref_f32_nonfinite_bitwise(rows, cols):
+    """Inf, -Inf and NaN entries flow through the chains as in the reference
+    (the zero products the default kernel gives padded columns stay exact)."""
+    rng = np.random.default_rng(11)
+    A = rng.random((rows, cols), dtype=np.float32) - 0.5
+    A[3, 7], A[5, cols - 1], A[rows - 1, 0], A[9, 100] = np.inf, -np.inf, np.nan, 3e38
+    v = rng.random(cols, dtype=np.float32) * 4
+    out = cg.DeviceArray(rows, np.float32)
+    cg.matVec(dev(A), dev(v), out, rows, cols)
+    ref = oracle.matvec_f32ref(A, v)
+    assert np.array_equal(out.to_host().view(np.uint32), ref.view(np.uint32))
+
+
+# CGX_REF_MV: 64-row x 128 tiles / 16-row x 512 tiles / 32-row blocks with two tiles in flight and a
+# dedicated adding wave (default) / the same with wave 0 also loading.  3 and 4 run their FULL form when
+# rows % 32 == 0 and cols % 512 == 0, a bounds-checked form for other multiples of 4, the 16-row kernel when
+# cols % 4 != 0.
+@pytest.mark.parametrize("variant", ["1", "2", "3", "4"])
 @pytest.mark.parametrize("rows,cols", [(1, 1), (2, 2), (5, 3), (64, 64), (300, 257), (1000, 1000), (8192, 96),
-                                       (16, 512), (17, 513), (33, 1536), (48, 1025), (100, 4100)])
+                                       (16, 512), (17, 513), (33, 1536), (48, 1025), (100, 4100), (32, 512),
+                                       (64, 1024), (96, 2560), (31, 4), (33, 516), (1024, 8192), (8192, 8192)])
 def test_matvec_ref_f32_bitwise(monkeypatch, variant, rows, cols):
     monkeypatch.setenv("CGX_REF_MV", variant)
     rng = np.random.default_rng(rows * 7 + cols)
