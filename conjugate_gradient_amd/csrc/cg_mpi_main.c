@@ -1,0 +1,229 @@
+/* cg_mpi: the drop-in for `mpiexec -np P ./parallel_cg A.txt b.txt x0.txt`
+ * (and, with --p2p, for point-to-point_cg), one process per GPU.
+ *
+ * MPI is the launcher and the bootstrap only: rank 0 makes the RCCL unique
+ * id and MPI_Bcast hands it out; every per-iteration
+ * exchange is RCCL inside libcgx (cgx_create_rank).  What parallel_cg.c
+ * does with MPI and what this does instead:
+ *   - rank 0 reads all of A, b, x0 with initialize() (parallel_cg.c:104-107)
+ *     -> every rank indexes the text files and parses only its own rows
+ *        (cgx_text_read_range), so the parse runs on all ranks at once;
+ *   - MPI_Bcast(x0) + MPI_Scatter(A, b) (:109-115) -> cgx_set_rows with the
+ *     rank's rows (the full x0 for the first A x0 is allgathered on the GPUs);
+ *   - conjugrad's MPI_Allgather / MPI_Allreduce (:283-323) -> cgx_solve.
+ * Same output lines from rank 0 (:334, :123-126); with --fp32-ref the x is
+ * parallel_cg.c's (point-to-point_cg.c's with --p2p) bit for bit.
+ *
+ *   mpiexec -np P cg_mpi [--fp32-ref] [--p2p] [--eps E] [--max-iter M]
+ *                        [--dims FILE | --n N] [--threads T] [--print-x]
+ *                        [--stats] matrixA vectorb initialguess
+ * Device: the rank's index among the ranks on its node, modulo the visible
+ * GPUs (CGX_DEVICE overrides). */
+#define _GNU_SOURCE
+#include <errno.h>
+#include <math.h>
+#include <stdint.h>
+#include <stdio.h>
+#include <stdlib.h>
+#include <string.h>
+#include <time.h>
+
+#include <mpi.h>
+
+#include "cgx.h"
+#include "cgx_textio.h"
+
+#define EPSILON_DEFAULT 1.0e-6 /* parallel_cg.c:19 */
+
+static double now_s(void) {
+    struct timespec ts;
+    clock_gettime(CLOCK_MONOTONIC, &ts);
+    return (double)ts.tv_sec + 1e-9 * (double)ts.tv_nsec;
+}
+
+static int opt_ll(const char *v, long long *out) {
+    char *end = NULL;
+    errno = 0;
+    const long long x = strtoll(v, &end, 10);
+    if (!*v || *end || errno) return 0;
+    *out = x;
+    return 1;
+}
+
+static int opt_double(const char *v, double *out) {
+    char *end = NULL;
+    errno = 0;
+    const double x = strtod(v, &end);
+    if (!*v || *end || errno) return 0;
+    *out = x;
+    return 1;
+}
+
+static void usage(void) {
+    fprintf(stderr,
+            "usage: mpiexec -np P cg_mpi [--fp32-ref] [--p2p] [--eps E] [--max-iter M] [--dims FILE | --n N]\n"
+            "                            [--threads T] [--print-x] [--stats] matrixA vectorb initialguess\n");
+}
+
+/* values [first, first + count) of a text file, read as the reference's
+ * fscanf("%f%*c") loop reads it; 0 or the reader's error (-1 open, -2 short,
+ * -3 malformed) */
+static int read_values(const char *path, int64_t first, int64_t count, int as_float, void *out, int threads) {
+    cgx_text *t = NULL;
+    int rc = cgx_text_open(path, threads, &t);
+    if (rc == 0) rc = cgx_text_read_range(t, first, count, as_float, out, threads);
+    cgx_text_close(t);
+    return rc;
+}
+
+int main(int argc, char **argv) {
+    const double t_prog0 = now_s();
+    if (MPI_Init(&argc, &argv) != MPI_SUCCESS) {
+        printf("MPI_Init failed.\n"); /* parallel_cg.c:78 */
+        return 1;
+    }
+    int rank = 0, nranks = 1;
+    MPI_Comm_rank(MPI_COMM_WORLD, &rank);
+    MPI_Comm_size(MPI_COMM_WORLD, &nranks);
+    MPI_Comm node;
+    int local_rank = 0;
+    MPI_Comm_split_type(MPI_COMM_WORLD, MPI_COMM_TYPE_SHARED, rank, MPI_INFO_NULL, &node);
+    MPI_Comm_rank(node, &local_rank);
+    MPI_Comm_free(&node);
+
+    int fp32ref = 0, p2p = 0, print_x = 0, stats = 0, threads = 4, bad = 0;
+    double eps = EPSILON_DEFAULT;
+    long long max_iter = -1, n_opt = -1, v = 0;
+    const char *dims_path = NULL, *pos[3] = {NULL, NULL, NULL};
+    int npos = 0;
+    for (int i = 1; i < argc && !bad; ++i) {
+        const char *a = argv[i];
+        const int has = i + 1 < argc;
+        if (!strcmp(a, "--fp32-ref")) fp32ref = 1;
+        else if (!strcmp(a, "--p2p")) p2p = 1;
+        else if (!strcmp(a, "--print-x")) print_x = 1;
+        else if (!strcmp(a, "--stats")) stats = 1;
+        else if (!strcmp(a, "--eps") && has) bad = !opt_double(argv[++i], &eps);
+        else if (!strcmp(a, "--max-iter") && has) bad = !opt_ll(argv[++i], &max_iter);
+        else if (!strcmp(a, "--n") && has) bad = !opt_ll(argv[++i], &n_opt);
+        else if (!strcmp(a, "--dims") && has) dims_path = argv[++i];
+        else if (!strcmp(a, "--threads") && has) {
+            bad = !opt_ll(argv[++i], &v);
+            threads = v < 1 ? 1 : (v > 64 ? 64 : (int)v);
+        } else if (a[0] == '-' && a[1] == '-') bad = 1;
+        else if (npos < 3) pos[npos++] = a;
+        else bad = 1;
+    }
+    if (bad || npos != 3) {
+        if (rank == 0) usage();
+        MPI_Finalize();
+        return 2;
+    }
+
+    /* N: rank 0 decides (dimensions file, --n, or the count of b's values) */
+    long long n = 0;
+    if (rank == 0) {
+        if (n_opt > 0) n = n_opt;
+        else if (dims_path) {
+            int64_t d[4];
+            if (cgx_text_dims(dims_path, d) != 0) n = -1;
+            else if (d[0] != d[1]) {
+                printf("%lld and %lld must be same size\n", (long long)d[0], (long long)d[1]); /* :93 */
+                n = -1;
+            } else n = d[0];
+        } else {
+            n = cgx_text_count(pos[1]);
+            if (n < 0) printf("Could not open file\n");
+        }
+        if (n == 0) fprintf(stderr, "empty system\n");
+        if (n > 0 && n % nranks != 0) {
+            printf("%lld is not divisible by %d\n", n, nranks); /* parallel_cg.c:88 */
+            n = -1;
+        }
+        if (n > 0) printf("Computing cg of matrix size : %lld\n", n * n); /* :101 */
+        fflush(stdout);
+    }
+    MPI_Bcast(&n, 1, MPI_LONG_LONG, 0, MPI_COMM_WORLD);
+    if (n <= 0) {
+        MPI_Finalize();
+        return 1;
+    }
+    const int64_t nloc = n / nranks, row0 = (int64_t)rank * nloc;
+    const size_t es = fp32ref ? 4 : 8;
+
+    /* every rank parses its own rows of A, b and x0 */
+    void *A = malloc((size_t)nloc * (size_t)n * es), *b = malloc((size_t)nloc * es), *x = malloc((size_t)n * es);
+    int rc = (A && b && x) ? 0 : -4;
+    if (!rc) rc = read_values(pos[0], row0 * n, nloc * n, fp32ref, A, threads);
+    if (!rc) rc = read_values(pos[1], row0, nloc, fp32ref, b, threads);
+    if (!rc) rc = read_values(pos[2], row0, nloc, fp32ref, (char *)x + (size_t)row0 * es, 1);
+    int worst = rc;
+    MPI_Allreduce(&rc, &worst, 1, MPI_INT, MPI_MIN, MPI_COMM_WORLD);
+    if (worst != 0) {
+        if (rc != 0)
+            fprintf(stderr, "rank %d: %s\n", rank,
+                    rc == -1 ? "Could not open file" : rc == -2 ? "a file holds fewer numbers than the system needs"
+                             : rc == -4 ? "can't allocate memory" : "malformed number");
+        MPI_Finalize();
+        return 1;
+    }
+
+    /* RCCL bootstrap over MPI, then the rank's context on its GPU */
+    cgx_unique_id id;
+    memset(&id, 0, sizeof id);
+    int id_rc = CGX_OK;
+    if (rank == 0 && (id_rc = cgx_get_unique_id(&id)) != CGX_OK)
+        fprintf(stderr, "cgx_get_unique_id: %s (%s)\n", cgx_strerror(id_rc), cgx_last_error());
+    MPI_Bcast(&id_rc, 1, MPI_INT, 0, MPI_COMM_WORLD);
+    if (id_rc != CGX_OK) {  /* no RCCL id: nobody can join, every rank stops */
+        MPI_Finalize();
+        return 1;
+    }
+    MPI_Bcast(&id, sizeof id, MPI_BYTE, 0, MPI_COMM_WORLD);
+    int ndev = 0;
+    cgx_device_count(&ndev);
+    const char *de = getenv("CGX_DEVICE");
+    const int dev = de ? atoi(de) : (ndev > 0 ? local_rank % ndev : 0);
+    const int flags = (fp32ref ? CGX_F32_REF : CGX_F64) | (p2p ? CGX_COMM_P2P : 0);
+    cgx_ctx *ctx = NULL;
+    rc = cgx_create_rank(&ctx, n, rank, nranks, &id, dev, flags);
+    if (rc != CGX_OK) {
+        fprintf(stderr, "rank %d: cgx_create_rank: %s (%s)\n", rank, cgx_strerror(rc), cgx_last_error());
+        MPI_Abort(MPI_COMM_WORLD, 1); /* as parallel_cg.c stops the job */
+    }
+
+    /* the scatter of A and b and the broadcast of x0 (parallel_cg.c:109-115) */
+    MPI_Barrier(MPI_COMM_WORLD);
+    const double t_dist0 = MPI_Wtime();
+    rc = cgx_set_rows(ctx, row0, nloc, A, n, b, (char *)x + (size_t)row0 * es);
+    MPI_Barrier(MPI_COMM_WORLD);
+    const double t_dist1 = MPI_Wtime();
+    free(A);
+    free(b);
+    cgx_stats st;
+    memset(&st, 0, sizeof st);
+    if (rc == CGX_OK) rc = cgx_solve(ctx, NULL, eps, max_iter, &st);
+    if (rc == CGX_OK) rc = cgx_get_x(ctx, x); /* the full x on every rank, as the reference leaves it */
+    if (rc != CGX_OK) {
+        fprintf(stderr, "rank %d: %s (%s)\n", rank, cgx_strerror(rc), cgx_last_error());
+        MPI_Abort(MPI_COMM_WORLD, 1);
+    }
+    if (rank == 0) {
+        printf("cg method execution time in seconds: %f\n", st.solve_ms / 1e3);               /* :334 */
+        printf("collective data distribution time in seconds: %f\n", t_dist1 - t_dist0);    /* :123 */
+        printf("clock execution time in seconds: %f\n", now_s() - t_prog0);                  /* :125 */
+        if (stats)
+            printf("iterations: %lld converged: %d residual_norm: %.6e\n", (long long)st.iterations, st.converged,
+                   st.rr >= 0 ? sqrt(st.rr) : -1.0);
+        if (print_x)
+            for (int64_t i = 0; i < n; ++i) {
+                if (fp32ref) printf("%.9g\n", (double)((float *)x)[i]);
+                else printf("%.17g\n", ((double *)x)[i]);
+            }
+        fflush(stdout);
+    }
+    cgx_destroy(ctx);
+    free(x);
+    MPI_Finalize();
+    return 0;
+}

@@ -221,6 +221,28 @@ def run_cli(*args):
     return subprocess.run([cg.CLI_PATH, *args], capture_output=True, text=True, timeout=120)
 
 
+def _cg_mpi():
+    exe = os.path.join(os.path.dirname(cg.CLI_PATH), "cg_mpi")
+    if not (os.path.exists("/opt/conda/bin/mpiexec") and os.path.exists(exe)):
+        pytest.skip("MPICH mpiexec or bin/cg_mpi absent")
+    return exe
+
+
+def test_cg_mpi_rejects_indivisible_n_and_bad_options(built):
+    """cg_mpi's checks before any GPU work, under mpiexec as the reference runs."""
+    exe = _cg_mpi()
+    paths = [os.path.join(FIX, f) for f in ("matrixA1.txt", "vectorb1.txt", "X0.txt")]
+    r = subprocess.run(["/opt/conda/bin/mpiexec", "-np", "3", exe, *paths], capture_output=True, text=True,
+                       timeout=120)
+    assert r.returncode != 0 and "4 is not divisible by 3" in r.stdout  # parallel_cg.c:88
+    r = subprocess.run(["/opt/conda/bin/mpiexec", "-np", "2", exe, "--eps", "x", *paths], capture_output=True,
+                       text=True, timeout=120)
+    assert r.returncode != 0 and "usage: mpiexec -np P cg_mpi" in r.stderr
+    r = subprocess.run(["/opt/conda/bin/mpiexec", "-np", "2", exe, str(FIX) + "/nope.txt", paths[1], paths[2]],
+                       capture_output=True, text=True, timeout=120)
+    assert r.returncode != 0 and "Could not open file" in r.stderr
+
+
 def test_cli_argument_count(built):
     r = run_cli()
     assert r.returncode == 1
