@@ -14,7 +14,8 @@ int matvec_rows(cgx_ctx *c, Shard &s, const MatvecPlan &pl, const char *Arows, i
                 const char *vec, bool fuse_dot, int dot_slot, bool gated) {
     if (f32ref(c)) {
         HIPT(matvec_ref_f32(reinterpret_cast<const float *>(Arows), c->lda, rows, c->n,
-                            reinterpret_cast<const float *>(vec), reinterpret_cast<float *>(s.Ap) + r0, s.stream));
+                            reinterpret_cast<const float *>(vec), reinterpret_cast<float *>(s.Ap) + r0, s.stream,
+                            gate_of(s, gated)));
     } else {
         HIPT(matvec_f64(pl, reinterpret_cast<const double *>(Arows), c->lda, rows, c->lda,
                         reinterpret_cast<const double *>(vec), reinterpret_cast<double *>(s.Ap) + r0,
@@ -116,7 +117,7 @@ int launch_matvec(cgx_ctx *c, Shard &s, const char *vec, bool with_dot, int dot_
         if (f32ref(c))  // vecVec(p, Ap) sequential (serialConjugate.c:219)
             HIPT(dot_ref_f32(s.nloc, reinterpret_cast<const float *>(s.pown),
                              reinterpret_cast<const float *>(s.Ap), reinterpret_cast<float *>(slot(s, dot_slot)),
-                             s.stream));
+                             s.stream, gate_of(s, gated)));
         else
             HIPT(dot_f64(s.nloc, reinterpret_cast<const double *>(s.pown),
                          reinterpret_cast<const double *>(s.Ap), reinterpret_cast<double *>(slot(s, dot_slot)), s.ws,
@@ -332,9 +333,9 @@ int do_iteration(cgx_ctx *c, double eps, int *stop, bool gated) {
                                    reinterpret_cast<const float *>(s.pown),
                                    reinterpret_cast<const float *>(s.Ap),
                                    reinterpret_cast<const float *>(slot(s, S_RR + ring(k))),
-                                   reinterpret_cast<const float *>(slot(s, pg)), s.stream));
+                                   reinterpret_cast<const float *>(slot(s, pg)), s.stream, gate_of(s, gated)));
             HIPT(dot_ref_f32(s.nloc, reinterpret_cast<const float *>(s.r), reinterpret_cast<const float *>(s.r),
-                             reinterpret_cast<float *>(slot(s, ro)), s.stream));
+                             reinterpret_cast<float *>(slot(s, ro)), s.stream, gate_of(s, gated)));
         } else {
             // r -= alpha Ap, r.r; x's update is deferred into the p update
             HIPT(update_r_f64(s.nloc, reinterpret_cast<double *>(s.r), reinterpret_cast<const double *>(s.Ap),
@@ -349,6 +350,14 @@ int do_iteration(cgx_ctx *c, double eps, int *stop, bool gated) {
     if (gated) {  // x (+ p unless converged) on the device, stopping rule decided there
         for (auto &s : c->sh) {
             TRY(set_dev(s));
+            if (f32ref(c)) {  // x is current; the p update decides the stop first
+                HIPT(update_p_ref_f32(s.nloc, reinterpret_cast<float *>(s.pown), reinterpret_cast<const float *>(s.r),
+                                      reinterpret_cast<const float *>(slot(s, rg)),
+                                      reinterpret_cast<const float *>(slot(s, S_RR + ring(k))), s.stream, eps, k,
+                                      reinterpret_cast<int64_t *>(slot(s, S_KDONE)),
+                                      reinterpret_cast<double *>(slot(s, S_RRFINAL)), rec_of(c, s, gated)));
+                continue;
+            }
             HIPT(update_xp_f64(s.nloc, reinterpret_cast<double *>(s.x), reinterpret_cast<double *>(s.pown),
                                reinterpret_cast<const double *>(s.r),
                                reinterpret_cast<const double *>(slot(s, S_RR + ring(k))),
@@ -470,7 +479,7 @@ int cgx_iterate(cgx_ctx *c, int64_t count, double eps, int64_t *done, int *conve
     if (c->state == ST_IDLE) return fail(CGX_ERR_STATE, "cgx_iterate before cgx_solve_begin");
     const char *gv = std::getenv("CGX_GATED");
     const bool gate_ok = !(gv && *gv == '0');
-    if (c->state == ST_BEGUN && count > 0 && eps >= 0.0 && !f32ref(c) && !(c->flags & CGX_HOST_STREAM) && gate_ok)
+    if (c->state == ST_BEGUN && count > 0 && eps >= 0.0 && !(c->flags & CGX_HOST_STREAM) && gate_ok)
         return iterate_gated(c, count, eps, done, converged);
     int64_t did = 0;
     while (did < count && c->state == ST_BEGUN) {

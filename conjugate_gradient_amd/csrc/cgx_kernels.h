@@ -131,15 +131,20 @@ inline int64_t sym_pos_h(int r, int c) {  // kSymNT = 512: (8 tr + rr, 4 tc + 2 
 }
 
 // ---- fp32, serialConjugate.c operation order ---------------------------------
+// gate: the device-side convergence record (kernels of an iteration after the
+// converged one do nothing); update_p_ref_f32 with kdone makes the stopping
+// decision (see k_update_p_ref_f32).
 hipError_t matvec_ref_f32(const float *A, int64_t lda, int64_t rows, int64_t cols,
-                          const float *v, float *out, hipStream_t s);
-hipError_t dot_ref_f32(int64_t n, const float *a, const float *b, float *out, hipStream_t s);
+                          const float *v, float *out, hipStream_t s, const int64_t *gate = nullptr);
+hipError_t dot_ref_f32(int64_t n, const float *a, const float *b, float *out, hipStream_t s,
+                       const int64_t *gate = nullptr);
 hipError_t residual_ref_f32(int64_t n, const float *b, const float *Ax, float *r, float *p,
                             hipStream_t s);
 hipError_t update_xr_ref_f32(int64_t n, float *x, float *r, const float *p, const float *Ap,
-                             const float *rsold, const float *pAp, hipStream_t s);
+                             const float *rsold, const float *pAp, hipStream_t s, const int64_t *gate = nullptr);
 hipError_t update_p_ref_f32(int64_t n, float *p, const float *r, const float *rr,
-                            const float *rsold, hipStream_t s);
+                            const float *rsold, hipStream_t s, double eps = -1.0, int64_t k = 0,
+                            int64_t *kdone = nullptr, double *rrfinal = nullptr, int64_t *hrec = nullptr);
 hipError_t gen_spd_f32(int64_t n, int64_t lda, int64_t row0, int64_t nrows, uint64_t seed,
                        float *A, float *b, hipStream_t s);
 // F32_REF combine: rank order (allSum) or, with mpich, MPICH's MPI_Allreduce order.

@@ -20,8 +20,10 @@ constexpr int kRefTC = 128;  // tile columns
 __global__ __launch_bounds__(64) void k_matvec_ref_f32(const float *__restrict__ A, int64_t lda,
                                                        int64_t rows, int64_t cols,
                                                        const float *__restrict__ v,
-                                                       float *__restrict__ out) {
+                                                       float *__restrict__ out,
+                                                       const int64_t *gate) {
 #pragma clang fp contract(off)
+    if (gate && *gate) return;  // converged in an earlier iteration (device-side gating)
     __shared__ float tile[2][64][kRefTC + 1];
     __shared__ float pv[2][kRefTC];
     typedef float f4 __attribute__((ext_vector_type(4)));
@@ -120,8 +122,10 @@ constexpr int kRef2Rows = 16, kRef2TC = 512, kRef2Ld = kRef2TC + 4;
 __global__ __launch_bounds__(64) void k_matvec_ref_f32_r16(const float *__restrict__ A, int64_t lda,
                                                            int64_t rows, int64_t cols,
                                                            const float *__restrict__ v,
-                                                           float *__restrict__ out) {
+                                                           float *__restrict__ out,
+                                                           const int64_t *gate) {
 #pragma clang fp contract(off)
+    if (gate && *gate) return;  // converged in an earlier iteration (device-side gating)
     typedef float f4 __attribute__((ext_vector_type(4)));
     constexpr int kLd4 = kRef2Ld / 4, kTC4 = kRef2TC / 4;  // f4 per padded row / per tile row
     constexpr int kK = kRef2Rows * kTC4 / 64;              // f4 loads per lane per tile (32)
@@ -242,8 +246,10 @@ template <bool FULL>
 __global__ __launch_bounds__(256) void k_matvec_ref_f32_w4(const float *__restrict__ A, int64_t lda,
                                                            int64_t rows, int64_t cols,
                                                            const float *__restrict__ v,
-                                                           float *__restrict__ out) {
+                                                           float *__restrict__ out,
+                                                           const int64_t *gate) {
 #pragma clang fp contract(off)
+    if (gate && *gate) return;  // converged in an earlier iteration (device-side gating)
     typedef float f4 __attribute__((ext_vector_type(4)));
     __shared__ f4 prod[2][kRef3Rows * kRef3Ld4];
     const int t = threadIdx.x;
@@ -349,8 +355,10 @@ template <bool FULL>
 __global__ __launch_bounds__(320) void k_matvec_ref_f32_w5(const float *__restrict__ A, int64_t lda,
                                                            int64_t rows, int64_t cols,
                                                            const float *__restrict__ v,
-                                                           float *__restrict__ out) {
+                                                           float *__restrict__ out,
+                                                           const int64_t *gate) {
 #pragma clang fp contract(off)
+    if (gate && *gate) return;  // converged in an earlier iteration (device-side gating)
     typedef float f4 __attribute__((ext_vector_type(4)));
     __shared__ f4 prod[2][kRef3Rows * kRef3Ld4];
     const int t = threadIdx.x;
@@ -459,8 +467,10 @@ __global__ __launch_bounds__(320) void k_matvec_ref_f32_w5(const float *__restri
 // vecVec: one wave; products in parallel, the sum strictly sequential in
 // index order (s = s + a_i b_i), broadcast lane by lane with v_readlane.
 __global__ __launch_bounds__(64) void k_dot_ref_f32(int64_t n, const float *__restrict__ a,
-                                                    const float *__restrict__ b, float *out) {
+                                                    const float *__restrict__ b, float *out,
+                                                    const int64_t *gate) {
 #pragma clang fp contract(off)
+    if (gate && *gate) return;  // converged in an earlier iteration (device-side gating)
     // One wave.  The products of 8 chunks of 64 (each rounded to float, as
     // serialConjugate.c:150 forms them) go to LDS; then every lane walks them
     // in index order with 16-B broadcast reads and adds them one by one, the
@@ -505,8 +515,10 @@ __global__ __launch_bounds__(64) void k_dot_ref_f32(int64_t n, const float *__re
 // (rounded to float, serialConjugate.c:150) when the chunk is stored.
 constexpr int kDotChunk = 4096;
 __global__ __launch_bounds__(256) void k_dot_ref_f32_blk(int64_t n, const float *__restrict__ a,
-                                                         const float *__restrict__ b, float *out) {
+                                                         const float *__restrict__ b, float *out,
+                                                         const int64_t *gate) {
 #pragma clang fp contract(off)
+    if (gate && *gate) return;  // converged in an earlier iteration (device-side gating)
     typedef float f4 __attribute__((ext_vector_type(4)));
     constexpr int U = kDotChunk / 256;
     __shared__ f4 sp[2][kDotChunk / 4];
@@ -592,8 +604,10 @@ __global__ __launch_bounds__(kNT) void k_update_xr_ref_f32(int64_t n, float *__r
                                                            float *__restrict__ r,
                                                            const float *__restrict__ p,
                                                            const float *__restrict__ Ap,
-                                                           const float *rsold, const float *pAp) {
+                                                           const float *rsold, const float *pAp,
+                                                           const int64_t *gate) {
 #pragma clang fp contract(off)
+    if (gate && *gate) return;  // converged in an earlier iteration (device-side gating)
     const float alpha = *rsold / *pAp;
     for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kNT) {
         const float tx = p[i] * alpha;
@@ -603,11 +617,24 @@ __global__ __launch_bounds__(kNT) void k_update_xr_ref_f32(int64_t n, float *__r
     }
 }
 
-// p = r + p*(beta/rsold)  (:239,243)
+// p = r + p*(beta/rsold)  (:239,243).  With cv.kdone (device-side gating)
+// the kernel first makes the reference's stopping decision,
+// `if (sqrt(rsnew) < EPSILON) break;` (:235-238: the float r.r widened to
+// double, as C's sqrt takes it): on convergence it records k+1 and r.r and
+// leaves p alone (the loop has ended); in a later iteration it does nothing.
 __global__ __launch_bounds__(kNT) void k_update_p_ref_f32(int64_t n, float *__restrict__ p,
                                                           const float *__restrict__ r,
-                                                          const float *rr, const float *rsold) {
+                                                          const float *rr, const float *rsold, ConvArgs cv) {
 #pragma clang fp contract(off)
+    if (cv.kdone) {
+        const int64_t kd = *cv.kdone;
+        if (kd != 0 && kd <= cv.k) return;
+        const double rrn = (double)*rr;
+        if (cv.eps >= 0.0 && sqrt(rrn) < cv.eps) {
+            if (blockIdx.x == 0 && threadIdx.x == 0) record_convergence(cv, cv.k + 1, rrn);
+            return;
+        }
+    }
     const float ratio = *rr / *rsold;
     for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kNT) {
         const float t = p[i] * ratio;
@@ -618,7 +645,7 @@ __global__ __launch_bounds__(kNT) void k_update_p_ref_f32(int64_t n, float *__re
 }  // namespace
 
 hipError_t matvec_ref_f32(const float *A, int64_t lda, int64_t rows, int64_t cols, const float *v,
-                          float *out, hipStream_t s) {
+                          float *out, hipStream_t s, const int64_t *gate) {
     if (rows <= 0) return hipSuccess;
     const int variant = env_int("CGX_REF_MV", 3);
     // 16-B aligned rows and x; the buffer offsets (32 rows of lda floats) fit in 31 bits
@@ -626,28 +653,28 @@ hipError_t matvec_ref_f32(const float *A, int64_t lda, int64_t rows, int64_t col
                         ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(v)) & 15) == 0;
     if (variant == 1)  // the 64-row, 128-column-tile kernel (kept for A/B)
         hipLaunchKernelGGL(k_matvec_ref_f32, dim3((unsigned)((rows + 63) / 64)), dim3(64), 0, s, A, lda, rows,
-                           cols, v, out);
+                           cols, v, out, gate);
     else if ((variant == 3 || variant == 4) && vec_ok) {
         const bool full = rows % kRef3Rows == 0 && cols % kRef3TC == 0;
         const dim3 grid((unsigned)((rows + kRef3Rows - 1) / kRef3Rows));
         if (variant == 3)  // a dedicated adding wave (default)
             hipLaunchKernelGGL(full ? k_matvec_ref_f32_w5<true> : k_matvec_ref_f32_w5<false>, grid, dim3(320), 0, s,
-                               A, lda, rows, cols, v, out);
+                               A, lda, rows, cols, v, out, gate);
         else  // wave 0 adds and loads
             hipLaunchKernelGGL(full ? k_matvec_ref_f32_w4<true> : k_matvec_ref_f32_w4<false>, grid, dim3(256), 0, s,
-                               A, lda, rows, cols, v, out);
+                               A, lda, rows, cols, v, out, gate);
     }
     else
         hipLaunchKernelGGL(k_matvec_ref_f32_r16, dim3((unsigned)((rows + kRef2Rows - 1) / kRef2Rows)), dim3(64), 0,
-                           s, A, lda, rows, cols, v, out);
+                           s, A, lda, rows, cols, v, out, gate);
     return hipGetLastError();
 }
 
-hipError_t dot_ref_f32(int64_t n, const float *a, const float *b, float *out, hipStream_t s) {
+hipError_t dot_ref_f32(int64_t n, const float *a, const float *b, float *out, hipStream_t s, const int64_t *gate) {
     if (env_int("CGX_REF_DOT", 2) == 1)  // the one-wave kernel (kept for A/B)
-        hipLaunchKernelGGL(k_dot_ref_f32, dim3(1), dim3(64), 0, s, n, a, b, out);
+        hipLaunchKernelGGL(k_dot_ref_f32, dim3(1), dim3(64), 0, s, n, a, b, out, gate);
     else
-        hipLaunchKernelGGL(k_dot_ref_f32_blk, dim3(1), dim3(256), 0, s, n, a, b, out);
+        hipLaunchKernelGGL(k_dot_ref_f32_blk, dim3(1), dim3(256), 0, s, n, a, b, out, gate);
     return hipGetLastError();
 }
 
@@ -658,14 +685,20 @@ hipError_t residual_ref_f32(int64_t n, const float *b, const float *Ax, float *r
 }
 
 hipError_t update_xr_ref_f32(int64_t n, float *x, float *r, const float *p, const float *Ap,
-                             const float *rsold, const float *pAp, hipStream_t s) {
-    hipLaunchKernelGGL(k_update_xr_ref_f32, dim3(grid_vec(n)), dim3(kNT), 0, s, n, x, r, p, Ap, rsold, pAp);
+                             const float *rsold, const float *pAp, hipStream_t s, const int64_t *gate) {
+    hipLaunchKernelGGL(k_update_xr_ref_f32, dim3(grid_vec(n)), dim3(kNT), 0, s, n, x, r, p, Ap, rsold, pAp, gate);
     return hipGetLastError();
 }
 
 hipError_t update_p_ref_f32(int64_t n, float *p, const float *r, const float *rr, const float *rsold,
-                            hipStream_t s) {
-    hipLaunchKernelGGL(k_update_p_ref_f32, dim3(grid_vec(n)), dim3(kNT), 0, s, n, p, r, rr, rsold);
+                            hipStream_t s, double eps, int64_t k, int64_t *kdone, double *rrfinal, int64_t *hrec) {
+    ConvArgs cv;
+    cv.eps = eps;
+    cv.k = k;
+    cv.kdone = kdone;
+    cv.rrfinal = rrfinal;
+    cv.hrec = hrec;
+    hipLaunchKernelGGL(k_update_p_ref_f32, dim3(grid_vec(n)), dim3(kNT), 0, s, n, p, r, rr, rsold, cv);
     return hipGetLastError();
 }
 

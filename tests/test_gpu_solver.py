@@ -693,6 +693,30 @@ def test_device_gated_convergence_matches_host_checked(monkeypatch, shards):
     assert ref[1] == so.iterations and rel(ref[0], xo) <= TOL
 
 
+@pytest.mark.parametrize("case_name,shards", [("spd512", None), ("spd1024", [0, 0]), ("spd2048", [0, 0, 0, 0]),
+                                             ("kat4", None), ("kat2_x0", None)])
+def test_f32ref_device_gated_equals_host_checked_and_reference(monkeypatch, case_name, shards):
+    """CGX_F32_REF with the stopping decision on the device (default) and
+    host-checked (CGX_GATED=0), at every lookahead: the same loop count and
+    x bits as the reference (serial, or the P-part oracle in MPICH order),
+    no extra iteration leaking into x, the converged r.r reported."""
+    A, b, x0 = case(case_name, np.float32)
+    n = A.shape[0]
+    P = len(shards) if shards else 1
+    xr, sr = oracle.cg_f32ref(A, b, x0, eps=1e-6, nparts=P, combine="mpich")
+    for gated in ("1", "0"):
+        monkeypatch.setenv("CGX_GATED", gated)
+        for look in ("1", "2", "5"):
+            monkeypatch.setenv("CGX_LOOKAHEAD", look)
+            with cg.Solver(n, flags=cg.CGX_F32_REF, devices=shards) as s:
+                s.set_system(A, b, x0)
+                x, st = s.solve(x0.copy(), eps=1e-6)
+                assert st.iterations == sr.iterations and st.converged == 1, (gated, look)
+                assert s.stats().total_iterations == st.iterations, (gated, look)
+                assert np.array_equal(x.view(np.uint32), xr.view(np.uint32)), (gated, look)
+                assert np.float32(st.rr) == np.float32(sr.rr) and np.sqrt(st.rr) < 1e-6
+
+
 def test_poisson_fixed_count_is_deterministic():
     """The same fixed-count Poisson solve twice on one context: x bit for bit
     (fixed-order reductions; x0 reset, since begin() starts from the current x)."""
