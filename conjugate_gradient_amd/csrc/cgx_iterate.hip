@@ -171,11 +171,10 @@ int do_begin(cgx_ctx *c) {
             TRY(launch_matvec(c, s, s.pfull, false, 0));
         s.x_zero = false;  // the iterations update x
         if (f32ref(c)) {
-            float *pown = reinterpret_cast<float *>(s.pown);
-            HIPT(residual_ref_f32(s.nloc, reinterpret_cast<const float *>(s.b), reinterpret_cast<const float *>(s.Ap),
-                                  reinterpret_cast<float *>(s.r), pown, s.stream));
-            HIPT(dot_ref_f32(s.nloc, reinterpret_cast<const float *>(s.r), reinterpret_cast<const float *>(s.r),
-                             reinterpret_cast<float *>(slot(s, os)), s.stream));
+            HIPT(residual_dot_ref_f32(s.nloc, reinterpret_cast<const float *>(s.b),
+                                      reinterpret_cast<const float *>(s.Ap), reinterpret_cast<float *>(s.r),
+                                      reinterpret_cast<float *>(s.pown), reinterpret_cast<float *>(slot(s, os)),
+                                      s.stream));
         } else {
             double *pown = reinterpret_cast<double *>(s.pown);
             HIPT(residual_f64(s.nloc, reinterpret_cast<const double *>(s.b), reinterpret_cast<const double *>(s.Ap),
@@ -329,13 +328,12 @@ int do_iteration(cgx_ctx *c, double eps, int *stop, bool gated) {
     for (auto &s : c->sh) {
         TRY(set_dev(s));
         if (f32ref(c)) {
-            HIPT(update_xr_ref_f32(s.nloc, reinterpret_cast<float *>(s.x), reinterpret_cast<float *>(s.r),
-                                   reinterpret_cast<const float *>(s.pown),
-                                   reinterpret_cast<const float *>(s.Ap),
-                                   reinterpret_cast<const float *>(slot(s, S_RR + ring(k))),
-                                   reinterpret_cast<const float *>(slot(s, pg)), s.stream, gate_of(s, gated)));
-            HIPT(dot_ref_f32(s.nloc, reinterpret_cast<const float *>(s.r), reinterpret_cast<const float *>(s.r),
-                             reinterpret_cast<float *>(slot(s, ro)), s.stream, gate_of(s, gated)));
+            // x += alpha p; r -= alpha Ap; r.r in one launch  (serialConjugate.c:219-234)
+            HIPT(update_xr_dot_ref_f32(s.nloc, reinterpret_cast<float *>(s.x), reinterpret_cast<float *>(s.r),
+                                       reinterpret_cast<const float *>(s.pown), reinterpret_cast<const float *>(s.Ap),
+                                       reinterpret_cast<const float *>(slot(s, S_RR + ring(k))),
+                                       reinterpret_cast<const float *>(slot(s, pg)),
+                                       reinterpret_cast<float *>(slot(s, ro)), s.stream, gate_of(s, gated)));
         } else {
             // r -= alpha Ap, r.r; x's update is deferred into the p update
             HIPT(update_r_f64(s.nloc, reinterpret_cast<double *>(s.r), reinterpret_cast<const double *>(s.Ap),

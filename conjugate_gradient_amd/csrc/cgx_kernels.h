@@ -142,6 +142,12 @@ hipError_t residual_ref_f32(int64_t n, const float *b, const float *Ax, float *r
                             hipStream_t s);
 hipError_t update_xr_ref_f32(int64_t n, float *x, float *r, const float *p, const float *Ap,
                              const float *rsold, const float *pAp, hipStream_t s, const int64_t *gate = nullptr);
+// one launch each: x += p alpha, r -= Ap alpha, *rr = r.r (serialConjugate.c:219-234) /
+// r = p = b - Ax, *rr = r.r (:209-212); the same float operations as the separate kernels
+hipError_t update_xr_dot_ref_f32(int64_t n, float *x, float *r, const float *p, const float *Ap, const float *rsold,
+                                 const float *pAp, float *rr, hipStream_t s, const int64_t *gate = nullptr);
+hipError_t residual_dot_ref_f32(int64_t n, const float *b, const float *Ax, float *r, float *p, float *rr,
+                                hipStream_t s);
 hipError_t update_p_ref_f32(int64_t n, float *p, const float *r, const float *rr,
                             const float *rsold, hipStream_t s, double eps = -1.0, int64_t k = 0,
                             int64_t *kdone = nullptr, double *rrfinal = nullptr, int64_t *hrec = nullptr);

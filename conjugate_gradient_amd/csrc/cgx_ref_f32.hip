@@ -510,38 +510,78 @@ __global__ __launch_bounds__(64) void k_dot_ref_f32(int64_t n, const float *__re
 }
 
 // The same single sequential sum with its loads off the chain: 4 waves load
-// the next 4096-element chunk (raw a and b, 16 of each per thread) while wave
-// 0 adds up the current chunk's products from LDS; the products are formed
-// (rounded to float, serialConjugate.c:150) when the chunk is stored.
+// the next 4096-element chunk while wave 0 adds up the current chunk's
+// products from LDS; the products are formed (rounded to float,
+// serialConjugate.c:150) when the chunk is stored.  The element-wise step
+// that produces the summed vector can ride along (one launch instead of two,
+// the same float operations in the same order):
+//   kDotPlain  sum a_i b_i                                 (vecVec, :145-155)
+//   kDotXR     x += p alpha; r -= Ap alpha; sum r_i r_i    (:219-234)
+//   kDotResid  r = p = b - Ax; sum r_i r_i                 (:209-212)
 constexpr int kDotChunk = 4096;
-__global__ __launch_bounds__(256) void k_dot_ref_f32_blk(int64_t n, const float *__restrict__ a,
-                                                         const float *__restrict__ b, float *out,
-                                                         const int64_t *gate) {
+enum { kDotPlain = 0, kDotXR = 1, kDotResid = 2 };
+struct DotArgs {
+    const float *a = nullptr, *b = nullptr;  // plain: the two vectors; resid: b, Ax
+    float *x = nullptr, *r = nullptr, *p = nullptr;
+    const float *Ap = nullptr, *rsold = nullptr, *pAp = nullptr;
+};
+template <int MODE>
+__global__ __launch_bounds__(256) void k_dot_ref_f32_blk(int64_t n, DotArgs d, float *out, const int64_t *gate) {
 #pragma clang fp contract(off)
     if (gate && *gate) return;  // converged in an earlier iteration (device-side gating)
     typedef float f4 __attribute__((ext_vector_type(4)));
     constexpr int U = kDotChunk / 256;
     __shared__ f4 sp[2][kDotChunk / 4];
     const int t = threadIdx.x;
-    float av[U], bv[U];
+    float av[U], bv[U], cv[U], dv[U];
+    const float alpha = MODE == kDotXR ? *d.rsold / *d.pAp : 0.0f;  // alpha = rsold / pAp  (:220)
     auto load = [&](int64_t c0) {
 #pragma unroll
         for (int u = 0; u < U; ++u) {
             const int64_t i = c0 + u * 256 + t;
-            av[u] = i < n ? a[i] : 0.0f;
-            bv[u] = i < n ? b[i] : 0.0f;
+            if (MODE == kDotXR) {
+                av[u] = i < n ? d.x[i] : 0.0f;
+                bv[u] = i < n ? d.p[i] : 0.0f;
+                cv[u] = i < n ? d.r[i] : 0.0f;
+                dv[u] = i < n ? d.Ap[i] : 0.0f;
+            } else {
+                av[u] = i < n ? d.a[i] : 0.0f;
+                bv[u] = i < n ? d.b[i] : 0.0f;
+            }
         }
     };
-    auto store = [&](int buf) {
+    auto store = [&](int buf, int64_t c0) {
         float *spf = reinterpret_cast<float *>(sp[buf]);
 #pragma unroll
-        for (int u = 0; u < U; ++u) spf[u * 256 + t] = av[u] * bv[u];
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = c0 + u * 256 + t;
+            if (MODE == kDotPlain) {
+                spf[u * 256 + t] = av[u] * bv[u];
+            } else if (MODE == kDotXR) {
+                const float tx = bv[u] * alpha;  // x = x + p*alpha  (:221,225)
+                const float xn = av[u] + tx;
+                const float tr = dv[u] * alpha;  // r = r - Ap*alpha  (:226,230)
+                const float rn = cv[u] - tr;
+                if (i < n) {
+                    d.x[i] = xn;
+                    d.r[i] = rn;
+                }
+                spf[u * 256 + t] = i < n ? rn * rn : 0.0f;
+            } else {
+                const float rn = av[u] - bv[u];  // r = b - Ax; p = b - Ax  (:210-211)
+                if (i < n) {
+                    d.r[i] = rn;
+                    d.p[i] = rn;
+                }
+                spf[u * 256 + t] = i < n ? rn * rn : 0.0f;
+            }
+        }
     };
     const int64_t nch = (n + kDotChunk - 1) / kDotChunk;
     float s = 0.0f;  // sum = 0.0  (:149)
     if (nch > 0) {
         load(0);
-        store(0);
+        store(0, 0);
         __syncthreads();
     }
     for (int64_t ch = 0; ch < nch; ++ch) {
@@ -582,7 +622,7 @@ __global__ __launch_bounds__(256) void k_dot_ref_f32_blk(int64_t n, const float 
                 for (int i = 0; i < (int)left; ++i) s = s + spf[i];
             }
         }
-        if (ch + 1 < nch) store(buf ^ 1);
+        if (ch + 1 < nch) store(buf ^ 1, (ch + 1) * kDotChunk);
         __syncthreads();
     }
     if (t == 0) *out = s;
@@ -674,7 +714,36 @@ hipError_t dot_ref_f32(int64_t n, const float *a, const float *b, float *out, hi
     if (env_int("CGX_REF_DOT", 2) == 1)  // the one-wave kernel (kept for A/B)
         hipLaunchKernelGGL(k_dot_ref_f32, dim3(1), dim3(64), 0, s, n, a, b, out, gate);
     else
-        hipLaunchKernelGGL(k_dot_ref_f32_blk, dim3(1), dim3(256), 0, s, n, a, b, out, gate);
+    {
+        DotArgs d;
+        d.a = a;
+        d.b = b;
+        hipLaunchKernelGGL(k_dot_ref_f32_blk<kDotPlain>, dim3(1), dim3(256), 0, s, n, d, out, gate);
+    }
+    return hipGetLastError();
+}
+
+hipError_t update_xr_dot_ref_f32(int64_t n, float *x, float *r, const float *p, const float *Ap, const float *rsold,
+                                 const float *pAp, float *rr, hipStream_t s, const int64_t *gate) {
+    DotArgs d;
+    d.x = x;
+    d.r = r;
+    d.p = const_cast<float *>(p);
+    d.Ap = Ap;
+    d.rsold = rsold;
+    d.pAp = pAp;
+    hipLaunchKernelGGL(k_dot_ref_f32_blk<kDotXR>, dim3(1), dim3(256), 0, s, n, d, rr, gate);
+    return hipGetLastError();
+}
+
+hipError_t residual_dot_ref_f32(int64_t n, const float *b, const float *Ax, float *r, float *p, float *rr,
+                                hipStream_t s) {
+    DotArgs d;
+    d.a = b;
+    d.b = Ax;
+    d.r = r;
+    d.p = p;
+    hipLaunchKernelGGL(k_dot_ref_f32_blk<kDotResid>, dim3(1), dim3(256), 0, s, n, d, rr, nullptr);
     return hipGetLastError();
 }
 
@@ -706,6 +775,7 @@ hipError_t update_p_ref_f32(int64_t n, float *p, const float *r, const float *rr
 hipError_t preload_ref_f32() {
     hipFuncAttributes a;
     hipError_t e = hipFuncGetAttributes(&a, reinterpret_cast<const void *>(k_matvec_ref_f32_r16));
+    if (e == hipSuccess) e = hipFuncGetAttributes(&a, reinterpret_cast<const void *>(k_dot_ref_f32_blk<kDotXR>));
     if (e == hipSuccess) e = hipFuncGetAttributes(&a, reinterpret_cast<const void *>(k_matvec_ref_f32_w4<true>));
     if (e == hipSuccess) e = hipFuncGetAttributes(&a, reinterpret_cast<const void *>(k_matvec_ref_f32_w4<false>));
     if (e == hipSuccess) e = hipFuncGetAttributes(&a, reinterpret_cast<const void *>(k_matvec_ref_f32_w5<true>));
