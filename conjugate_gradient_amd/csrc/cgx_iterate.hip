@@ -423,7 +423,14 @@ static int iterate_gated(cgx_ctx *c, int64_t count, double eps, int64_t *done, i
     const int64_t k0 = c->k;
     int64_t issued = 0, kd = 0;
     volatile int64_t *rec = s0.h_rec;  // {kdone, r.r bits}, stored by the deciding kernel
+    // One process (single GPU or row blocks on several): the record may also
+    // be read as soon as it appears, without an event, so a GPU that runs
+    // ahead of the host's launches (small N) stops the enqueueing after the
+    // deciding iteration.  Never in rank mode, where every rank must enqueue
+    // the same iterations (their collectives pair up).
+    const bool early = c->mode != M_RCCL;
     for (; issued < count && kd == 0; ++issued) {
+        if (early && rec[0] != 0) break;
         int stop = 0;
         TRY(do_iteration(c, eps, &stop, /*gated=*/true));
         TRY(set_dev(s0));

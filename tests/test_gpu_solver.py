@@ -311,10 +311,13 @@ def test_timing_events_count():
 
 
 @pytest.mark.parametrize("shards", [None, [0, 0]])
-def test_zero_x0_skips_initial_matvec_same_result(shards):
+def test_zero_x0_skips_initial_matvec_same_result(monkeypatch, shards):
     """Skipping A x0 for x0 = 0 changes nothing: the same x, bit for bit, as a
     solve from x0 = [0, ..., 0, 0] with the last entry first set nonzero and
-    then zeroed (partial set_rows), which keeps the initial matVec."""
+    then zeroed (partial set_rows), which keeps the initial matVec.  (The
+    host-checked loop: with device-side gating a single process may stop
+    enqueueing at a timing-dependent point, so the launch count varies.)"""
+    monkeypatch.setenv("CGX_GATED", "0")
     A, b, x0 = case("spd1024", np.float64)
     n = b.size
     res = []
