@@ -234,8 +234,13 @@ MatvecPlan plan_matvec_f64(int device, int64_t rows, int R, int U, int nt, int b
     // 7.24 TB/s at 65536^2 (unpipelined best R=8,U=8,buffer-nt: 7.09),
     // 7.21 TB/s on an 8192 x 65536 row block (7.05), 6.81 TB/s at 16384^2 (6.60).
     // R=1 when there are fewer than 2 rows per resident wave.
+    // Rows of 4096-8192 columns keep R = 1, one row per wave and twice the
+    // waves: 81.0-82.5 vs 82.6 us at 8192^2, 20.9 vs 21.7 at 4096^2, but
+    // 5.3 vs 5.2 at 2048^2 (profiles/r02_sweep_square_n*.jsonl); per CG
+    // iteration at N=8192 93.1-94.1 vs 94.2-95.7 us, at N=2048 16.5 vs 14.0
+    // (profiles/r02_floor_plan_r1_vs_r2.jsonl).
     const int64_t want_waves = (int64_t)cus * 4;
-    pl.R = rows >= 2 * want_waves ? 2 : 1;
+    pl.R = (rows >= 2 * want_waves && !(cols >= 4096 && cols <= 8192)) ? 2 : 1;
     // a row of fewer than 8 chunks: with U = 8 its chunks would go through the
     // one-chunk remainder loop, one dependent memory round trip each (N = 512:
     // 4 chunks); U = 4 / 2 issues them together
