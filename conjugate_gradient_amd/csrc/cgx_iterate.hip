@@ -108,12 +108,17 @@ int launch_matvec(cgx_ctx *c, Shard &s, const char *vec, bool with_dot, int dot_
                       with_dot ? reinterpret_cast<const double *>(s.pown) : nullptr,
                       with_dot ? reinterpret_cast<double *>(slot(s, dot_slot)) : nullptr, s.ws, s.stream,
                       gate_of(s, gated)));
+    else if (with_dot && c->ref_fused)  // matVec + vecVec(p, Ap) in one launch (serialConjugate.c:215,219)
+        HIPT(matvec_dot_ref_f32(reinterpret_cast<const float *>(s.A), c->lda, s.nloc, c->n,
+                                reinterpret_cast<const float *>(vec), reinterpret_cast<float *>(s.Ap),
+                                reinterpret_cast<const float *>(s.pown), reinterpret_cast<float *>(slot(s, dot_slot)),
+                                s.ws.tickets + T_REF_MV, s.stream, gate_of(s, gated)));
     else TRY(matvec_rows(c, s, s.plan, s.A, 0, s.nloc, vec, with_dot && !f32ref(c), dot_slot, gated));
     if (timing) {
         HIPT(hipEventRecord(s.ev_t[2 * s.ev_used + 1], s.stream));
         s.ev_used++;
     }
-    if (with_dot && (f32ref(c) || (streamed && !(c->flags & CGX_SYMMETRIC)))) {
+    if (with_dot && ((f32ref(c) && !c->ref_fused) || (streamed && !(c->flags & CGX_SYMMETRIC)))) {
         if (f32ref(c))  // vecVec(p, Ap) sequential (serialConjugate.c:219)
             HIPT(dot_ref_f32(s.nloc, reinterpret_cast<const float *>(s.pown),
                              reinterpret_cast<const float *>(s.Ap), reinterpret_cast<float *>(slot(s, dot_slot)),
@@ -307,9 +312,41 @@ static int do_iteration_fused_p(cgx_ctx *c, double eps, int *stop, bool gated) {
     return CGX_OK;
 }
 
+// The same for CGX_F32_REF (c->ref_fused): the matVec whose last block runs
+// vecVec(p, Ap), then one single-block launch for x += p alpha, r -= Ap alpha,
+// r.r, the stopping test and p = r + p (rr/rsold) -- four launches' float
+// operations in their order (bitwise the same x and loop count).
+static int do_iteration_ref_fused(cgx_ctx *c, double eps, int *stop, bool gated) {
+    const int64_t k = c->k;
+    *stop = 0;
+    Shard &s = c->sh[0];
+    const int pg = S_PAP + ring(k), rg = S_RR + ring(k + 1);
+    auto F = [](void *q) { return reinterpret_cast<float *>(q); };
+    TRY(launch_matvec(c, s, s.pfull, true, pg, gated));  // serialConjugate.c:215,219
+    HIPT(update_xrp_dot_ref_f32(s.nloc, F(s.x), F(s.r), F(s.pown), F(s.Ap), F(slot(s, S_RR + ring(k))),
+                                F(slot(s, pg)), F(slot(s, rg)), s.stream, gate_of(s, gated), gated ? eps : -1.0, k,
+                                gated ? reinterpret_cast<int64_t *>(slot(s, S_KDONE)) : nullptr,
+                                gated ? reinterpret_cast<double *>(slot(s, S_RRFINAL)) : nullptr,
+                                rec_of(c, s, gated)));  // :220-243
+    c->k = k + 1;
+    c->total_iters += 1;
+    if (!gated && eps >= 0.0) {  // host-checked stop; x is already current
+        double rr = 0.0;
+        TRY(read_scalar(c, rg, &rr));
+        c->last_rr = rr;
+        if (std::sqrt(rr) < eps) {
+            c->converged = 1;
+            c->state = ST_CONVERGED;
+            *stop = 1;
+        }
+    }
+    return CGX_OK;
+}
+
 int do_iteration(cgx_ctx *c, double eps, int *stop, bool gated) {
     if (c->fused) return do_iteration_poisson(c, eps, stop, gated);
     if (c->fused_p) return do_iteration_fused_p(c, eps, stop, gated);
+    if (c->ref_fused) return do_iteration_ref_fused(c, eps, stop, gated);
     const int64_t k = c->k;
     *stop = 0;
     const int pg = S_PAP + ring(k), pl = S_LPAP + ring(k);

@@ -15,7 +15,7 @@ constexpr int kMaxRedBlocks = 8192;
 // Most partials a scalar combine takes (>= kMaxShards, the rank limit).
 constexpr int kMaxCombine = 64;
 constexpr int kTickets = 8;
-enum Ticket { T_MATVEC = 0, T_RESID = 1, T_XR = 2, T_DOT = 3 };
+enum Ticket { T_MATVEC = 0, T_RESID = 1, T_XR = 2, T_DOT = 3, T_REF_MV = 4 };
 
 // Geometry of the fp64 row-streaming matVec, chosen once per (device, rows).
 struct MatvecPlan {
@@ -148,6 +148,18 @@ hipError_t update_xr_dot_ref_f32(int64_t n, float *x, float *r, const float *p, 
                                  const float *pAp, float *rr, hipStream_t s, const int64_t *gate = nullptr);
 hipError_t residual_dot_ref_f32(int64_t n, const float *b, const float *Ax, float *r, float *p, float *rr,
                                 hipStream_t s);
+// The single-GPU two-launch F32_REF iteration (the same float operations as
+// matvec_ref_f32 + dot_ref_f32 + update_xr_dot_ref_f32 + update_p_ref_f32):
+// out = A v with *dot_out = pown . out from the matVec's last block (ticket:
+// a zeroed counter), then x, r, *rr = r.r, the stopping decision and (unless
+// stopped) p = r + p (*rr / *rsold) in one single-block launch.
+bool matvec_dot_ref_f32_fusable(const float *A, int64_t lda, const float *v);
+hipError_t matvec_dot_ref_f32(const float *A, int64_t lda, int64_t rows, int64_t cols, const float *v, float *out,
+                              const float *pown, float *dot_out, unsigned *ticket, hipStream_t s,
+                              const int64_t *gate = nullptr);
+hipError_t update_xrp_dot_ref_f32(int64_t n, float *x, float *r, float *p, const float *Ap, const float *rsold,
+                                  const float *pAp, float *rr, hipStream_t s, const int64_t *gate, double eps,
+                                  int64_t k, int64_t *kdone, double *rrfinal, int64_t *hrec);
 hipError_t update_p_ref_f32(int64_t n, float *p, const float *r, const float *rr,
                             const float *rsold, hipStream_t s, double eps = -1.0, int64_t k = 0,
                             int64_t *kdone = nullptr, double *rrfinal = nullptr, int64_t *hrec = nullptr);

@@ -217,6 +217,136 @@ __global__ __launch_bounds__(64) void k_matvec_ref_f32_r16(const float *__restri
     if (t < kRef2Rows && row0 + t < rows) out[row0 + t] = acc;
 }
 
+// The same single sequential sum with its loads off the chain: 4 waves load
+// the next 4096-element chunk while wave 0 adds up the current chunk's
+// products from LDS; the products are formed (rounded to float,
+// serialConjugate.c:150) when the chunk is stored.  The element-wise step
+// that produces the summed vector can ride along (one launch instead of two,
+// the same float operations in the same order):
+//   kDotPlain  sum a_i b_i                                 (vecVec, :145-155)
+//   kDotXR     x += p alpha; r -= Ap alpha; sum r_i r_i    (:219-234)
+//   kDotResid  r = p = b - Ax; sum r_i r_i                 (:209-212)
+//   kDotXRP    kDotXR, then the stopping test (:235-238) and, unless the
+//              loop ends, p = r + p (rr / rsold)            (:239,243)
+// dot_ref_body is the one block's work, shared by k_dot_ref_f32_blk and the
+// last block of k_matvec_ref_f32_w5<.., true>: threads t < 256 load and
+// store (a 320-thread block's fifth wave only passes the barriers), wave 0
+// holds the sum.  SC1B: b was stored write-through by other blocks of the
+// same launch and is read with sc1 loads (the one-counter hand-off).
+constexpr int kDotChunk = 4096;
+enum { kDotPlain = 0, kDotXR = 1, kDotResid = 2, kDotXRP = 3 };
+typedef float f4v __attribute__((ext_vector_type(4)));
+struct DotArgs {
+    const float *a = nullptr, *b = nullptr;  // plain: the two vectors; resid: b, Ax
+    float *x = nullptr, *r = nullptr, *p = nullptr;
+    const float *Ap = nullptr, *rsold = nullptr, *pAp = nullptr;
+};
+template <int MODE, bool SC1B>
+__device__ __forceinline__ float dot_ref_body(int64_t n, const DotArgs &d, f4v (*sp)[kDotChunk / 4], int t) {
+#pragma clang fp contract(off)
+    typedef f4v f4;
+    constexpr int U = kDotChunk / 256;
+    const bool act = t < 256;
+    float av[U], bv[U], cv[U], dv[U];
+    const float alpha = MODE == kDotXR ? *d.rsold / *d.pAp : 0.0f;  // alpha = rsold / pAp  (:220)
+    auto load = [&](int64_t c0) {
+        if (!act) return;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = c0 + u * 256 + t;
+            if (MODE == kDotXR) {
+                av[u] = i < n ? d.x[i] : 0.0f;
+                bv[u] = i < n ? d.p[i] : 0.0f;
+                cv[u] = i < n ? d.r[i] : 0.0f;
+                dv[u] = i < n ? d.Ap[i] : 0.0f;
+            } else {
+                av[u] = i < n ? d.a[i] : 0.0f;
+                if (SC1B)
+                    bv[u] = i < n ? __hip_atomic_load(d.b + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0f;
+                else
+                    bv[u] = i < n ? d.b[i] : 0.0f;
+            }
+        }
+    };
+    auto store = [&](int buf, int64_t c0) {
+        if (!act) return;
+        float *spf = reinterpret_cast<float *>(sp[buf]);
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const int64_t i = c0 + u * 256 + t;
+            if (MODE == kDotPlain) {
+                spf[u * 256 + t] = av[u] * bv[u];
+            } else if (MODE == kDotXR) {
+                const float tx = bv[u] * alpha;  // x = x + p*alpha  (:221,225)
+                const float xn = av[u] + tx;
+                const float tr = dv[u] * alpha;  // r = r - Ap*alpha  (:226,230)
+                const float rn = cv[u] - tr;
+                if (i < n) {
+                    d.x[i] = xn;
+                    d.r[i] = rn;
+                }
+                spf[u * 256 + t] = i < n ? rn * rn : 0.0f;
+            } else {
+                const float rn = av[u] - bv[u];  // r = b - Ax; p = b - Ax  (:210-211)
+                if (i < n) {
+                    d.r[i] = rn;
+                    d.p[i] = rn;
+                }
+                spf[u * 256 + t] = i < n ? rn * rn : 0.0f;
+            }
+        }
+    };
+    const int64_t nch = (n + kDotChunk - 1) / kDotChunk;
+    float s = 0.0f;  // sum = 0.0  (:149)
+    if (nch > 0) {
+        load(0);
+        store(0, 0);
+        __syncthreads();
+    }
+    for (int64_t ch = 0; ch < nch; ++ch) {
+        const int buf = (int)(ch & 1);
+        if (ch + 1 < nch) load((ch + 1) * kDotChunk);
+        if (t < 64) {  // wave 0: sum += v1[i] * v2[i], i ascending (:152)
+            const int64_t left = n - ch * kDotChunk;
+            if (left >= kDotChunk) {
+                // two register sets of G quads: one read from LDS while the
+                // other is added (G = 16: 2.9-3.3 ns per dependent add
+                // against 3.2-3.6 at G = 8, tools/microbench/add_chain.hip)
+                constexpr int G = 16;
+                f4 q[G], qn[G];
+                auto add = [&](const f4 (&w)[G]) {
+#pragma unroll
+                    for (int u = 0; u < G; ++u) {
+                        s = s + w[u].x;
+                        s = s + w[u].y;
+                        s = s + w[u].z;
+                        s = s + w[u].w;
+                    }
+                };
+#pragma unroll
+                for (int u = 0; u < G; ++u) q[u] = sp[buf][u];
+#pragma unroll 1
+                for (int j = 0; j < kDotChunk / 4; j += 2 * G) {
+#pragma unroll
+                    for (int u = 0; u < G; ++u) qn[u] = sp[buf][j + G + u];
+                    add(q);
+                    if (j + 2 * G < kDotChunk / 4) {
+#pragma unroll
+                        for (int u = 0; u < G; ++u) q[u] = sp[buf][j + 2 * G + u];
+                    }
+                    add(qn);
+                }
+            } else {
+                const float *spf = reinterpret_cast<const float *>(sp[buf]);
+                for (int i = 0; i < (int)left; ++i) s = s + spf[i];
+            }
+        }
+        if (ch + 1 < nch) store(buf ^ 1, (ch + 1) * kDotChunk);
+        __syncthreads();
+    }
+    return s;
+}
+
 // The same float arithmetic at the HBM rate: loads decoupled from the chains.
 // k_matvec_ref_f32_r16 issues one tile per wave and then waits for it, so
 // every step costs an HBM round trip (62 us at N=8192, ~4.1 TB/s).  Here a
@@ -351,12 +481,18 @@ __global__ __launch_bounds__(256) void k_matvec_ref_f32_w4(const float *__restri
 // Measured at N=8192 (rocprofv3, profiles/r02_kernel_stats_ref_f32_n8192.csv):
 // 49.6 us against 53.9 for k_matvec_ref_f32_w4 and 62.3 for the 16-row
 // kernel; a third register set (192 KiB in flight per CU) measured 51.9.
-template <bool FULL>
+//
+// DOT (the single-GPU two-launch iteration): the rows go out write-through
+// (sc1) and the last block to arrive (ticket) runs vecVec(p, Ap) over all
+// `rows` -- dot_ref_body, the separate dot kernel's code -- so the matVec and
+// p.Ap are one launch (serialConjugate.c:215,219), the same bits.
+template <bool FULL, bool DOT>
 __global__ __launch_bounds__(320) void k_matvec_ref_f32_w5(const float *__restrict__ A, int64_t lda,
                                                            int64_t rows, int64_t cols,
                                                            const float *__restrict__ v,
                                                            float *__restrict__ out,
-                                                           const int64_t *gate) {
+                                                           const int64_t *gate, const float *pown,
+                                                           float *dot_out, unsigned *ticket) {
 #pragma clang fp contract(off)
     if (gate && *gate) return;  // converged in an earlier iteration (device-side gating)
     typedef float f4 __attribute__((ext_vector_type(4)));
@@ -424,6 +560,25 @@ __global__ __launch_bounds__(320) void k_matvec_ref_f32_w5(const float *__restri
             add(qn);
         }
     };
+    // DOT: every wave (both roles) arrives here after the last barrier.
+    __shared__ int is_last;
+    auto dot_epilogue = [&](int64_t n, const float *Ap, const float *pv, float *dst, unsigned *tk, int tid) {
+        asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // wave 0's Ap stores have landed
+        __syncthreads();
+        if (tid == 0)
+            is_last = __hip_atomic_fetch_add(tk, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == gridDim.x - 1;
+        __syncthreads();
+        if (!is_last) return;
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
+        DotArgs d;
+        d.a = pv;
+        d.b = Ap;
+        const float sum = dot_ref_body<kDotPlain, true>(n, d, reinterpret_cast<f4v (*)[kDotChunk / 4]>(&prod[0][0]), tid);
+        if (tid == 0) {
+            *dst = sum;
+            __hip_atomic_store(tk, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+        }
+    };
     // Role by wave (a scalar branch: each role's loop is straight-line code,
     // so the loaders' waits stay "all but the newer set"); both roles pass
     // the same barriers, one per step.
@@ -434,7 +589,13 @@ __global__ __launch_bounds__(320) void k_matvec_ref_f32_w5(const float *__restri
             if (t < kRef3Rows && tt < ntiles) chain((int)(tt & 1));
             __syncthreads();
         }
-        if (t < kRef3Rows && row0 + t < rows) out[row0 + t] = acc;
+        if (t < kRef3Rows && row0 + t < rows) {
+            if (DOT)
+                __hip_atomic_store(out + row0 + t, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1
+            else
+                out[row0 + t] = acc;
+        }
+        if (DOT) dot_epilogue(rows, out, pown, dot_out, ticket, t);
         return;
     }
     // at step tt the loaders store tile tt + 1 into slot (tt + 1) & 1 and
@@ -462,6 +623,7 @@ __global__ __launch_bounds__(320) void k_matvec_ref_f32_w5(const float *__restri
         __builtin_amdgcn_sched_barrier(0);
         __syncthreads();
     }
+    if (DOT) dot_epilogue(rows, out, pown, dot_out, ticket, t);
 }
 
 // vecVec: one wave; products in parallel, the sum strictly sequential in
@@ -509,123 +671,36 @@ __global__ __launch_bounds__(64) void k_dot_ref_f32(int64_t n, const float *__re
     if (lane == 0) *out = s;
 }
 
-// The same single sequential sum with its loads off the chain: 4 waves load
-// the next 4096-element chunk while wave 0 adds up the current chunk's
-// products from LDS; the products are formed (rounded to float,
-// serialConjugate.c:150) when the chunk is stored.  The element-wise step
-// that produces the summed vector can ride along (one launch instead of two,
-// the same float operations in the same order):
-//   kDotPlain  sum a_i b_i                                 (vecVec, :145-155)
-//   kDotXR     x += p alpha; r -= Ap alpha; sum r_i r_i    (:219-234)
-//   kDotResid  r = p = b - Ax; sum r_i r_i                 (:209-212)
-constexpr int kDotChunk = 4096;
-enum { kDotPlain = 0, kDotXR = 1, kDotResid = 2 };
-struct DotArgs {
-    const float *a = nullptr, *b = nullptr;  // plain: the two vectors; resid: b, Ax
-    float *x = nullptr, *r = nullptr, *p = nullptr;
-    const float *Ap = nullptr, *rsold = nullptr, *pAp = nullptr;
-};
 template <int MODE>
-__global__ __launch_bounds__(256) void k_dot_ref_f32_blk(int64_t n, DotArgs d, float *out, const int64_t *gate) {
+__global__ __launch_bounds__(256) void k_dot_ref_f32_blk(int64_t n, DotArgs d, float *out, const int64_t *gate,
+                                                         ConvArgs cv) {
 #pragma clang fp contract(off)
     if (gate && *gate) return;  // converged in an earlier iteration (device-side gating)
-    typedef float f4 __attribute__((ext_vector_type(4)));
-    constexpr int U = kDotChunk / 256;
-    __shared__ f4 sp[2][kDotChunk / 4];
+    __shared__ f4v sp[2][kDotChunk / 4];
+    __shared__ float rr_b;
     const int t = threadIdx.x;
-    float av[U], bv[U], cv[U], dv[U];
-    const float alpha = MODE == kDotXR ? *d.rsold / *d.pAp : 0.0f;  // alpha = rsold / pAp  (:220)
-    auto load = [&](int64_t c0) {
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int64_t i = c0 + u * 256 + t;
-            if (MODE == kDotXR) {
-                av[u] = i < n ? d.x[i] : 0.0f;
-                bv[u] = i < n ? d.p[i] : 0.0f;
-                cv[u] = i < n ? d.r[i] : 0.0f;
-                dv[u] = i < n ? d.Ap[i] : 0.0f;
-            } else {
-                av[u] = i < n ? d.a[i] : 0.0f;
-                bv[u] = i < n ? d.b[i] : 0.0f;
-            }
-        }
-    };
-    auto store = [&](int buf, int64_t c0) {
-        float *spf = reinterpret_cast<float *>(sp[buf]);
-#pragma unroll
-        for (int u = 0; u < U; ++u) {
-            const int64_t i = c0 + u * 256 + t;
-            if (MODE == kDotPlain) {
-                spf[u * 256 + t] = av[u] * bv[u];
-            } else if (MODE == kDotXR) {
-                const float tx = bv[u] * alpha;  // x = x + p*alpha  (:221,225)
-                const float xn = av[u] + tx;
-                const float tr = dv[u] * alpha;  // r = r - Ap*alpha  (:226,230)
-                const float rn = cv[u] - tr;
-                if (i < n) {
-                    d.x[i] = xn;
-                    d.r[i] = rn;
-                }
-                spf[u * 256 + t] = i < n ? rn * rn : 0.0f;
-            } else {
-                const float rn = av[u] - bv[u];  // r = b - Ax; p = b - Ax  (:210-211)
-                if (i < n) {
-                    d.r[i] = rn;
-                    d.p[i] = rn;
-                }
-                spf[u * 256 + t] = i < n ? rn * rn : 0.0f;
-            }
-        }
-    };
-    const int64_t nch = (n + kDotChunk - 1) / kDotChunk;
-    float s = 0.0f;  // sum = 0.0  (:149)
-    if (nch > 0) {
-        load(0);
-        store(0, 0);
-        __syncthreads();
-    }
-    for (int64_t ch = 0; ch < nch; ++ch) {
-        const int buf = (int)(ch & 1);
-        if (ch + 1 < nch) load((ch + 1) * kDotChunk);
-        if (t < 64) {  // wave 0: sum += v1[i] * v2[i], i ascending (:152)
-            const int64_t left = n - ch * kDotChunk;
-            if (left >= kDotChunk) {
-                // two register sets of G quads: one read from LDS while the
-                // other is added (G = 16: 2.9-3.3 ns per dependent add
-                // against 3.2-3.6 at G = 8, tools/microbench/add_chain.hip)
-                constexpr int G = 16;
-                f4 q[G], qn[G];
-                auto add = [&](const f4 (&w)[G]) {
-#pragma unroll
-                    for (int u = 0; u < G; ++u) {
-                        s = s + w[u].x;
-                        s = s + w[u].y;
-                        s = s + w[u].z;
-                        s = s + w[u].w;
-                    }
-                };
-#pragma unroll
-                for (int u = 0; u < G; ++u) q[u] = sp[buf][u];
-#pragma unroll 1
-                for (int j = 0; j < kDotChunk / 4; j += 2 * G) {
-#pragma unroll
-                    for (int u = 0; u < G; ++u) qn[u] = sp[buf][j + G + u];
-                    add(q);
-                    if (j + 2 * G < kDotChunk / 4) {
-#pragma unroll
-                        for (int u = 0; u < G; ++u) q[u] = sp[buf][j + 2 * G + u];
-                    }
-                    add(qn);
-                }
-            } else {
-                const float *spf = reinterpret_cast<const float *>(sp[buf]);
-                for (int i = 0; i < (int)left; ++i) s = s + spf[i];
-            }
-        }
-        if (ch + 1 < nch) store(buf ^ 1, (ch + 1) * kDotChunk);
-        __syncthreads();
-    }
+    const float s = dot_ref_body<MODE == kDotXRP ? (int)kDotXR : MODE, false>(n, d, sp, t);
     if (t == 0) *out = s;
+    if constexpr (MODE == kDotXRP) {
+        // The single-GPU two-launch iteration's update: this block also makes
+        // the stopping decision (:235-238, the float r.r widened to double as
+        // C's sqrt takes it) and, unless the loop ends there, forms
+        // p = r + p*(rr/rsold) (:239,243) -- k_update_p_ref_f32's arithmetic.
+        // Element i is stored by thread i % 256 in the body and read back by
+        // the same thread here.
+        if (t == 0) rr_b = s;
+        __syncthreads();
+        const float rr = rr_b;
+        if (cv.kdone && cv.eps >= 0.0 && sqrt((double)rr) < cv.eps) {
+            if (t == 0) record_convergence(cv, cv.k + 1, (double)rr);
+            return;
+        }
+        const float ratio = rr / *d.rsold;
+        for (int64_t i = t; i < n; i += 256) {
+            const float tp = d.p[i] * ratio;
+            d.p[i] = d.r[i] + tp;
+        }
+    }
 }
 
 // residual(r) and residual(p): r = b - Ax; p = b - Ax  (serialConjugate.c:210-211)
@@ -698,8 +773,8 @@ hipError_t matvec_ref_f32(const float *A, int64_t lda, int64_t rows, int64_t col
         const bool full = rows % kRef3Rows == 0 && cols % kRef3TC == 0;
         const dim3 grid((unsigned)((rows + kRef3Rows - 1) / kRef3Rows));
         if (variant == 3)  // a dedicated adding wave (default)
-            hipLaunchKernelGGL(full ? k_matvec_ref_f32_w5<true> : k_matvec_ref_f32_w5<false>, grid, dim3(320), 0, s,
-                               A, lda, rows, cols, v, out, gate);
+            hipLaunchKernelGGL((full ? k_matvec_ref_f32_w5<true, false> : k_matvec_ref_f32_w5<false, false>), grid,
+                               dim3(320), 0, s, A, lda, rows, cols, v, out, gate, nullptr, nullptr, nullptr);
         else  // wave 0 adds and loads
             hipLaunchKernelGGL(full ? k_matvec_ref_f32_w4<true> : k_matvec_ref_f32_w4<false>, grid, dim3(256), 0, s,
                                A, lda, rows, cols, v, out, gate);
@@ -718,8 +793,48 @@ hipError_t dot_ref_f32(int64_t n, const float *a, const float *b, float *out, hi
         DotArgs d;
         d.a = a;
         d.b = b;
-        hipLaunchKernelGGL(k_dot_ref_f32_blk<kDotPlain>, dim3(1), dim3(256), 0, s, n, d, out, gate);
+        hipLaunchKernelGGL(k_dot_ref_f32_blk<kDotPlain>, dim3(1), dim3(256), 0, s, n, d, out, gate, ConvArgs{});
     }
+    return hipGetLastError();
+}
+
+bool matvec_dot_ref_f32_fusable(const float *A, int64_t lda, const float *v) {
+    return env_int("CGX_REF_MV", 3) == 3 && env_int("CGX_REF_DOT", 2) == 2 && (lda & 3) == 0 &&
+           lda < (int64_t(1) << 23) && ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(v)) & 15) == 0;
+}
+
+hipError_t matvec_dot_ref_f32(const float *A, int64_t lda, int64_t rows, int64_t cols, const float *v, float *out,
+                              const float *pown, float *dot_out, unsigned *ticket, hipStream_t s,
+                              const int64_t *gate) {
+    if (rows <= 0) return hipSuccess;
+    if (!matvec_dot_ref_f32_fusable(A, lda, v)) {  // two launches, the same bits
+        const hipError_t e = matvec_ref_f32(A, lda, rows, cols, v, out, s, gate);
+        return e != hipSuccess ? e : dot_ref_f32(rows, pown, out, dot_out, s, gate);
+    }
+    const bool full = rows % kRef3Rows == 0 && cols % kRef3TC == 0;
+    hipLaunchKernelGGL((full ? k_matvec_ref_f32_w5<true, true> : k_matvec_ref_f32_w5<false, true>),
+                       dim3((unsigned)((rows + kRef3Rows - 1) / kRef3Rows)), dim3(320), 0, s, A, lda, rows, cols, v,
+                       out, gate, pown, dot_out, ticket);
+    return hipGetLastError();
+}
+
+hipError_t update_xrp_dot_ref_f32(int64_t n, float *x, float *r, float *p, const float *Ap, const float *rsold,
+                                  const float *pAp, float *rr, hipStream_t s, const int64_t *gate, double eps,
+                                  int64_t k, int64_t *kdone, double *rrfinal, int64_t *hrec) {
+    DotArgs d;
+    d.x = x;
+    d.r = r;
+    d.p = p;
+    d.Ap = Ap;
+    d.rsold = rsold;
+    d.pAp = pAp;
+    ConvArgs cv;
+    cv.eps = eps;
+    cv.k = k;
+    cv.kdone = kdone;
+    cv.rrfinal = rrfinal;
+    cv.hrec = hrec;
+    hipLaunchKernelGGL(k_dot_ref_f32_blk<kDotXRP>, dim3(1), dim3(256), 0, s, n, d, rr, gate, cv);
     return hipGetLastError();
 }
 
@@ -732,7 +847,7 @@ hipError_t update_xr_dot_ref_f32(int64_t n, float *x, float *r, const float *p, 
     d.Ap = Ap;
     d.rsold = rsold;
     d.pAp = pAp;
-    hipLaunchKernelGGL(k_dot_ref_f32_blk<kDotXR>, dim3(1), dim3(256), 0, s, n, d, rr, gate);
+    hipLaunchKernelGGL(k_dot_ref_f32_blk<kDotXR>, dim3(1), dim3(256), 0, s, n, d, rr, gate, ConvArgs{});
     return hipGetLastError();
 }
 
@@ -743,7 +858,7 @@ hipError_t residual_dot_ref_f32(int64_t n, const float *b, const float *Ax, floa
     d.b = Ax;
     d.r = r;
     d.p = p;
-    hipLaunchKernelGGL(k_dot_ref_f32_blk<kDotResid>, dim3(1), dim3(256), 0, s, n, d, rr, nullptr);
+    hipLaunchKernelGGL(k_dot_ref_f32_blk<kDotResid>, dim3(1), dim3(256), 0, s, n, d, rr, nullptr, ConvArgs{});
     return hipGetLastError();
 }
 
@@ -778,8 +893,10 @@ hipError_t preload_ref_f32() {
     if (e == hipSuccess) e = hipFuncGetAttributes(&a, reinterpret_cast<const void *>(k_dot_ref_f32_blk<kDotXR>));
     if (e == hipSuccess) e = hipFuncGetAttributes(&a, reinterpret_cast<const void *>(k_matvec_ref_f32_w4<true>));
     if (e == hipSuccess) e = hipFuncGetAttributes(&a, reinterpret_cast<const void *>(k_matvec_ref_f32_w4<false>));
-    if (e == hipSuccess) e = hipFuncGetAttributes(&a, reinterpret_cast<const void *>(k_matvec_ref_f32_w5<true>));
-    return e != hipSuccess ? e : hipFuncGetAttributes(&a, reinterpret_cast<const void *>(k_matvec_ref_f32_w5<false>));
+    if (e == hipSuccess) e = hipFuncGetAttributes(&a, reinterpret_cast<const void *>(k_matvec_ref_f32_w5<true, false>));
+    if (e == hipSuccess) e = hipFuncGetAttributes(&a, reinterpret_cast<const void *>(k_matvec_ref_f32_w5<true, true>));
+    if (e == hipSuccess) e = hipFuncGetAttributes(&a, reinterpret_cast<const void *>(k_dot_ref_f32_blk<kDotXRP>));
+    return e != hipSuccess ? e : hipFuncGetAttributes(&a, reinterpret_cast<const void *>(k_matvec_ref_f32_w5<false, false>));
 }
 
 }  // namespace cgx

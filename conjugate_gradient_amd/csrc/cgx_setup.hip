@@ -255,9 +255,20 @@ static bool can_fuse_p(const cgx_ctx *c) {
     return c->n <= kFusePMax;
 }
 
+// The F32_REF counterpart (do_iteration_ref_fused): one GPU, resident
+// row-major A; CGX_REF_FUSE=0 keeps four launches (matVec, p.Ap, x/r + r.r,
+// p).  The same float operations in the same order either way.
+static bool can_fuse_ref(const cgx_ctx *c) {
+    if (c->mode != M_SINGLE || c->op != OP_DENSE || !f32ref(c)) return false;
+    if (c->flags & (CGX_SYMMETRIC | CGX_HOST_STREAM)) return false;
+    const char *e = std::getenv("CGX_REF_FUSE");
+    return !(e && *e == '0');
+}
+
 int finish_create(cgx_ctx *c, cgx_ctx **out) {
     c->overlap = can_overlap(c);
     c->fused_p = can_fuse_p(c);
+    c->ref_fused = can_fuse_ref(c);
     if (c->op == OP_POISSON) {  // CGX_POISSON_FUSED=0: the three-kernel split (stencil, r, x/p)
         const char *e = std::getenv("CGX_POISSON_FUSED");
         c->fused = !(e && *e == '0') && poisson_fusable(c->sh[0].nloc / c->m, c->m);
@@ -524,7 +535,8 @@ int cgx_get_info(const cgx_ctx *c, cgx_info *info) {
     info->row0 = c->sh[0].row0;
     info->nrows = 0;
     for (auto &s : c->sh) info->nrows += s.nloc;
-    info->flags = c->flags | (c->overlap ? CGX_OVERLAP_ACTIVE : 0) | ((c->fused || c->fused_p) ? CGX_FUSED_ACTIVE : 0);
+    info->flags = c->flags | (c->overlap ? CGX_OVERLAP_ACTIVE : 0) |
+                  ((c->fused || c->fused_p || c->ref_fused) ? CGX_FUSED_ACTIVE : 0);
     info->elem_bytes = c->es;
     return CGX_OK;
 }

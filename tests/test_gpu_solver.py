@@ -383,6 +383,48 @@ def test_two_launch_iteration_bitwise_equals_three(monkeypatch, n, seed):
     assert ref[1] == so.iterations and rel(ref[0], xo) <= TOL
 
 
+def _f32_system(name):
+    if name.startswith("hash"):  # ragged sizes: rows not a multiple of 32, columns not of 512, 2 dot chunks
+        n = int(name[4:])
+        A, b = oracle.spd_hash(n, seed=11)
+        return A.astype(np.float32), b.astype(np.float32), np.zeros(n, np.float32)
+    return case(name, np.float32)
+
+
+@pytest.mark.parametrize("name", ["kat2_x0", "kat4", "spd512", "spd2048", "spd8192", "hash1000", "hash4100"])
+def test_f32ref_two_launch_iteration_bitwise_equals_four(monkeypatch, name):
+    """CGX_F32_REF on one GPU iterates in two launches (CGX_REF_FUSE): the
+    matVec whose last block runs vecVec(p, Ap), then one block for x/r, r.r,
+    the stopping test and p -- instead of four (matVec, vecVec, x/r + r.r,
+    p).  The same float operations in the same order: x bit for bit and the
+    same loop count as the four-launch iteration and as serialConjugate.c's
+    restatement, device-gated, host-checked, fixed-count and in pieces."""
+    A, b, x0 = _f32_system(name)
+    n = A.shape[0]
+    xr, sr = oracle.cg_f32ref(A, b, x0, eps=1e-6)
+    res = {}
+    for fuse in ("1", "0"):
+        monkeypatch.setenv("CGX_REF_FUSE", fuse)
+        for gated in ("1", "0"):
+            monkeypatch.setenv("CGX_GATED", gated)
+            with cg.Solver(n, flags=cg.CGX_F32_REF) as s:
+                assert bool(s.info.flags & cg.CGX_FUSED_ACTIVE) == (fuse == "1")
+                s.set_system(A, b, x0)
+                x, st = s.solve(x0.copy(), eps=1e-6)
+                xf, _ = s.solve(x0.copy(), eps=-1.0, max_iter=3)
+                s.set_x(x0)
+                s.begin()
+                d1, _ = s.iterate(1, eps=1e-6)
+                d2, conv = s.iterate(100, eps=1e-6)
+                xp = s.get_x()
+            res[(fuse, gated)] = (x, st.iterations, xf, xp, d1 + d2, conv)
+    bits = lambda v: v.view(np.uint32)
+    for key, (x, it, xf, xp, dp, conv) in res.items():
+        assert it == sr.iterations and np.array_equal(bits(x), bits(xr)), key
+        assert np.array_equal(bits(xf), bits(res[("0", "0")][2])), key
+        assert conv and dp == it and np.array_equal(bits(xp), bits(xr)), key
+
+
 def test_errors_are_reported():
     with cg.Solver(8) as s:
         with pytest.raises(cg.CgxError) as ei:
