@@ -696,9 +696,21 @@ __global__ __launch_bounds__(256) void k_dot_ref_f32_blk(int64_t n, DotArgs d, f
             return;
         }
         const float ratio = rr / *d.rsold;
-        for (int64_t i = t; i < n; i += 256) {
-            const float tp = d.p[i] * ratio;
-            d.p[i] = d.r[i] + tp;
+        constexpr int U = 16;  // every load of a step issued before its stores: one round trip per 4096
+        for (int64_t c0 = 0; c0 < n; c0 += 256 * U) {
+            float pv[U], rv[U];
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t i = c0 + u * 256 + t;
+                pv[u] = i < n ? d.p[i] : 0.0f;
+                rv[u] = i < n ? d.r[i] : 0.0f;
+            }
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t i = c0 + u * 256 + t;
+                const float tp = pv[u] * ratio;
+                if (i < n) d.p[i] = rv[u] + tp;
+            }
         }
     }
 }

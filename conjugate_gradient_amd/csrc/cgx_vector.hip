@@ -196,18 +196,23 @@ __global__ __launch_bounds__(kNT) void k_update_xrp_f64(int64_t n, double *__res
     }
     const double beta = rr / rs;
     if constexpr (VEC) {
+        // One CU does all of p: every load of a thread's share (up to kPU
+        // pairs, n <= 8192 in one step) is issued before the first store, so
+        // the pass costs one round trip to memory instead of one per kVU pairs
+        // (n = 8192: 4 dependent steps before).
+        constexpr int kPU = 16;
         const int64_t npairs = n >> 1;
-        for (int64_t b0 = threadIdx.x; b0 < npairs; b0 += (int64_t)kNT * kVU) {
-            d2 rv[kVU], pv[kVU];
+        for (int64_t b0 = threadIdx.x; b0 < npairs; b0 += (int64_t)kNT * kPU) {
+            d2 rv[kPU], pv[kPU];
 #pragma unroll
-            for (int u = 0; u < kVU; ++u)
+            for (int u = 0; u < kPU; ++u)
                 if (b0 + u * kNT < npairs) {
                     const int64_t i = 2 * (b0 + u * kNT);
                     rv[u] = ld2_sc1(rrs, i);
                     pv[u] = ld2(p + i);
                 }
 #pragma unroll
-            for (int u = 0; u < kVU; ++u)
+            for (int u = 0; u < kPU; ++u)
                 if (b0 + u * kNT < npairs) st2(p + 2 * (b0 + u * kNT), rv[u] + beta * pv[u]);
         }
         if ((n & 1) && threadIdx.x == 0)
