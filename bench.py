@@ -253,6 +253,10 @@ def main(argv=None) -> int:
                          "without overlap, or the scalars combined in rank order (deterministic)")
     ap.add_argument("--n", "--size", dest="n", type=int, default=None,
                     help="system size (default 65536 dense, 131072 stream)")
+    ap.add_argument("--resident-gb", type=float, default=0.0,
+                    help="stream workload: keep this many GB of each GPU's rows of A in HBM and stream only the "
+                         "rest (CGX_STREAM_RESIDENT_MB; an out-of-core matrix keeps what fits). Default 0: all "
+                         "of A streams every matVec, as configs[3] states")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-n", type=int, default=None, help="N for the CPU baseline (default: --n)")
     args = ap.parse_args(argv)
@@ -276,6 +280,8 @@ def main(argv=None) -> int:
     flags = cg.CGX_F64 | cg.CGX_TIMING | (cg.CGX_HOST_STREAM if stream else 0) | (cg.CGX_SYMMETRIC if symmetric else 0)
     flags |= {"collective": 0, "p2p": cg.CGX_COMM_P2P, "nooverlap": cg.CGX_NO_OVERLAP,
               "deterministic": cg.CGX_DETERMINISTIC}[args.comm]
+    if stream and args.resident_gb > 0 and not symmetric:
+        os.environ["CGX_STREAM_RESIDENT_MB"] = str(int(args.resident_gb * 1024))
     if use_dist:
         uid = bcast_bytes(dist, cg.get_unique_id() if rank == 0 else None)
         # one GPU per process: LOCAL_RANK indexes the visible devices; if the
@@ -349,7 +355,13 @@ def main(argv=None) -> int:
         bytes_launch = 8 * (lda // 128) * (lda // 128 + 1) // 2 * 128 * 128 + 8 * n + 8 * n
     else:
         bytes_launch = matvec_bytes(n, nloc)
-    achieved = bytes_launch / (mv_ms * 1e-3) / 1e9
+    lda = (n + 127) // 128 * 128
+    res_rows = 0
+    if stream and not symmetric and args.resident_gb > 0:  # the rows kept in HBM (setup's rounding)
+        res_rows = min(nloc, int(args.resident_gb * 1024) * (1 << 20) // (lda * 8))
+    # a streamed workload's roofline is the host link: the bytes that cross it
+    link_bytes = bytes_launch - 8 * res_rows * n if stream else bytes_launch
+    achieved = link_bytes / (mv_ms * 1e-3) / 1e9
     traffic = None if (stream or poisson) else pmc_traffic(n, world, "_symmetric" if symmetric else "")
     peak = H2D_PEAK_GBS if stream else HBM_PEAK_GBS
     iters_per_s = args.steps / elapsed
@@ -372,6 +384,8 @@ def main(argv=None) -> int:
         "config": {
             "workload": (f"configs[3]: N={n} dense SPD fp64 CG, A streamed from pinned host memory every matVec"
                          + (" as its upper-triangle tiles (CGX_SYMMETRIC)" if symmetric else "")
+                         + (f" except the first {res_rows} rows per GPU, kept in HBM ({args.resident_gb:g} GB "
+                            f"budget)" if res_rows else "")
                          + f", row-block over {world} GPU(s), fixed-count iterations") if stream else
                         (f"configs[4]: matrix-free 5-point Poisson CG, m={m} (N={n}), b=1, x0=0, slabs over {world} "
                          f"GPU(s), halo exchange, fixed-count iterations") if poisson else
@@ -390,7 +404,7 @@ def main(argv=None) -> int:
                          "RCCL allgather(p) overlapped with own-block matVec + 2x allreduce"
                          if overlap_on else "RCCL allgather(p) + 2x allreduce"),
         },
-        "matvec_gbps": achieved,
+        "matvec_gbps": bytes_launch / (mv_ms * 1e-3) / 1e9,
         "matvec_ms": mv_ms,
         "matvec_ms_max_rank": mv_ms_max,
         "roofline": {
@@ -405,6 +419,7 @@ def main(argv=None) -> int:
                        "k_symv_f64 + k_symv_reduce_f64" if symmetric else "k_matvec_f64"),
             "plan": plan,
             "algorithmic_bytes_per_launch": bytes_launch,
+            "link_bytes_per_launch": link_bytes if stream else None,
         },
         "check": {"relres": rnorm / bnorm},
         # algorithmic bytes of a whole iteration: 64 B/point fused (r, p_{k-1} -> p_k;

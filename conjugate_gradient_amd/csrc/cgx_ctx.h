@@ -199,6 +199,12 @@ struct Shard {
     bool buf_used[kStreamBufs] = {};
     int next_buf = 0;
     MatvecPlan tile_plan;
+    // CGX_STREAM_RESIDENT_MB: the first res_rows rows also live in HBM (A),
+    // copied from A_host when res_dirty; only the rest streams per matVec,
+    // and the resident rows are multiplied while the first tiles copy.
+    int64_t res_rows = 0;
+    bool res_dirty = false;
+    MatvecPlan res_plan;
     hipEvent_t ev_look[8] = {};  // lagged convergence checks (kLookRing)
     // overlap of the p exchange with the own-column-block matVec
     hipStream_t cstream = nullptr;

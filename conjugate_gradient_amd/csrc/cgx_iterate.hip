@@ -30,9 +30,19 @@ int matvec_rows(cgx_ctx *c, Shard &s, const MatvecPlan &pl, const char *Arows, i
 // its copy waits until the kernel that last read that buffer is done (A is
 // read-only, so copies of the next iteration's first tiles overlap this
 // iteration's vector work); its kernel waits for the copy.
+// With resident rows (CGX_STREAM_RESIDENT_MB) their kernel goes first on the
+// compute stream, so it runs while the copy streams bring in the first tiles
+// of the rest (same row sums: every plan adds a row in the same order).
 int matvec_streamed(cgx_ctx *c, Shard &s, const char *vec) {
     const int64_t row_bytes = c->lda * (int64_t)c->es;
-    for (int64_t r0 = 0; r0 < s.nloc; r0 += s.tile_rows) {
+    if (s.res_rows > 0) {
+        if (s.res_dirty) {  // A changed on the host since the last copy (pinned: async)
+            HIPT(hipMemcpyAsync(s.A, s.A_host, (size_t)s.res_rows * row_bytes, hipMemcpyHostToDevice, s.stream));
+            s.res_dirty = false;
+        }
+        TRY(matvec_rows(c, s, s.res_plan, s.A, 0, s.res_rows, vec, false, 0));
+    }
+    for (int64_t r0 = s.res_rows; r0 < s.nloc; r0 += s.tile_rows) {
         const int64_t rows = std::min(s.tile_rows, s.nloc - r0);
         const int b = s.next_buf;
         s.next_buf = (s.next_buf + 1) % kStreamBufs;

@@ -82,6 +82,15 @@ int alloc_shard(cgx_ctx *c, Shard &s) {
         }
         for (int q = 0; q < s.ncopy; ++q) HIPT(hipStreamCreateWithFlags(&s.copy[q], hipStreamNonBlocking));
         if (!f32ref(c)) s.tile_plan = plan_matvec_f64(s.dev, s.tile_rows, 0, 0, -1, 0, c->lda);
+        // an HBM budget for A (out-of-core sizes: keep what fits, stream the rest)
+        const char *rmb = std::getenv("CGX_STREAM_RESIDENT_MB");
+        const int64_t res_bytes = (int64_t)((rmb && *rmb) ? std::atoll(rmb) : 0) << 20;
+        s.res_rows = std::max<int64_t>(0, std::min<int64_t>(s.nloc, res_bytes / row_bytes));
+        if (s.res_rows > 0) {
+            TRY(dmalloc(&s.A, (size_t)s.res_rows * row_bytes));
+            HIPT(hipMemsetAsync(s.A, 0, (size_t)s.res_rows * row_bytes, s.stream));
+            if (!f32ref(c)) s.res_plan = plan_matvec_f64(s.dev, s.res_rows, 0, 0, -1, 0, c->lda);
+        }
     } else if (c->flags & CGX_SYMMETRIC) {
         const int64_t ntiles = sym_tiles(c->lda);
         const size_t tbytes = (size_t)ntiles * 128 * 128 * 8;
@@ -573,6 +582,7 @@ int cgx_set_rows(cgx_ctx *c, int64_t row0, int64_t nrows, const void *A_rows, in
                 std::memcpy(dst, static_cast<const char *>(A_rows) + (size_t)(i - row0) * lda_host * es, (size_t)c->n * es);
                 if (c->lda > c->n) std::memset(dst + (size_t)c->n * es, 0, (size_t)(c->lda - c->n) * es);
             }
+            if (lo - s.row0 < s.res_rows) s.res_dirty = true;
         } else if (A_rows && (c->flags & CGX_SYMMETRIC)) {
             // rows through a staging buffer, then packed into the tiles
             if (!s.sym_stage) {
@@ -657,6 +667,7 @@ int cgx_generate_spd(cgx_ctx *c, uint64_t seed) {
                 HIPT(hipMemcpyAsync(s.A_host + (size_t)r0 * row_bytes, s.tile[0], (size_t)rows * row_bytes,
                                     hipMemcpyDeviceToHost, s.stream));
             }
+            s.res_dirty = s.res_rows > 0;
             TRY(rank_wait_stream(c, s.stream, "the tile generation"));
         } else if (c->flags & CGX_SYMMETRIC) {
             HIPT(gen_spd_sym_f64(c->n, c->lda, seed, reinterpret_cast<double *>(s.A), reinterpret_cast<double *>(s.b),

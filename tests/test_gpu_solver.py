@@ -463,6 +463,41 @@ def test_host_streamed_matvec(monkeypatch, shards):
     assert np.array_equal(x32, ref)
 
 
+@pytest.mark.parametrize("resident_mb,shards", [("5", None), ("5", [0, 0]), ("1000", None)])
+def test_host_streamed_with_resident_rows(monkeypatch, resident_mb, shards):
+    """CGX_STREAM_RESIDENT_MB: the first rows of each shard's block stay in
+    HBM and only the rest streams (an out-of-core matrix keeps what fits).
+    The row sums are the same whichever plan adds them, so x is bit for bit
+    the fully streamed solve's -- rows set on the host, generated on the
+    device, an A replaced between solves (the resident copy follows), all
+    rows resident (1000 MB) -- and F32_REF stays the reference's."""
+    monkeypatch.setenv("CGX_STREAM_TILE_MB", "1")
+    n = 2048  # 16 KiB rows: 5 MB keeps 320 of them
+    A, b = oracle.spd_hash(n, seed=5)
+    A2, b2 = oracle.spd_hash(n, seed=6)
+    out = {}
+    for res in ("0", resident_mb):
+        monkeypatch.setenv("CGX_STREAM_RESIDENT_MB", res)
+        with cg.Solver(n, flags=cg.CGX_F64 | cg.CGX_HOST_STREAM, devices=shards) as s:
+            s.set_system(A, b)
+            x1, st1 = s.solve(None, eps=1e-10)
+            s.set_system(A2, b2)
+            x2, st2 = s.solve(None, eps=1e-10)
+            s.generate_spd(seed=5)
+            x3, st3 = s.solve(None, eps=1e-10)
+        A32, b32, x032 = case("spd1024")
+        with cg.Solver(1024, flags=cg.CGX_F32_REF | cg.CGX_HOST_STREAM, devices=shards) as s:
+            s.set_system(A32, b32, x032)
+            x4, st4 = s.solve(None, eps=1e-6)
+        out[res] = [(x1, st1.iterations), (x2, st2.iterations), (x3, st3.iterations), (x4, st4.iterations)]
+    for (xa, ia), (xb, ib) in zip(out["0"], out[resident_mb]):
+        assert ia == ib and np.array_equal(xa.view(np.uint8), xb.view(np.uint8))
+    xo, so = oracle.cg_f64(A2, b2, np.zeros(n), eps=1e-10)
+    assert out["0"][1][1] == so.iterations and rel(out["0"][1][0], xo) <= TOL
+    ref, sr = oracle.cg_f32ref(A32, b32, x032, nparts=len(shards) if shards else 1, combine="mpich")
+    assert np.array_equal(out[resident_mb][3][0], ref)
+
+
 # ---------------------------------------------------------------------------
 # matrix-free 5-point Poisson (configs[4]); oracle: oracle_cg_poisson_f64
 # ---------------------------------------------------------------------------
