@@ -280,7 +280,7 @@ def main(argv=None) -> int:
     flags = cg.CGX_F64 | cg.CGX_TIMING | (cg.CGX_HOST_STREAM if stream else 0) | (cg.CGX_SYMMETRIC if symmetric else 0)
     flags |= {"collective": 0, "p2p": cg.CGX_COMM_P2P, "nooverlap": cg.CGX_NO_OVERLAP,
               "deterministic": cg.CGX_DETERMINISTIC}[args.comm]
-    if stream and args.resident_gb > 0 and not symmetric:
+    if stream and args.resident_gb > 0:
         os.environ["CGX_STREAM_RESIDENT_MB"] = str(int(args.resident_gb * 1024))
     if use_dist:
         uid = bcast_bytes(dist, cg.get_unique_id() if rank == 0 else None)
@@ -356,14 +356,19 @@ def main(argv=None) -> int:
     else:
         bytes_launch = matvec_bytes(n, nloc)
     lda = (n + 127) // 128 * 128
-    res_rows = 0
-    if stream and not symmetric and args.resident_gb > 0:  # the rows kept in HBM (setup's rounding)
-        res_rows = min(nloc, int(args.resident_gb * 1024) * (1 << 20) // (lda * 8))
+    res_rows = res_bytes = 0  # the rows (symmetric: 128x128 tiles) kept in HBM, setup's rounding
+    if stream and args.resident_gb > 0:
+        unit = 128 * 128 * 8 if symmetric else lda * 8
+        units = (lda // 128) * (lda // 128 + 1) // 2 if symmetric else nloc
+        res_rows = min(units, int(args.resident_gb * 1024) * (1 << 20) // unit)
+        res_bytes = res_rows * unit if symmetric else 8 * res_rows * n
     # a streamed workload's roofline is the host link: the bytes that cross it
-    link_bytes = bytes_launch - 8 * res_rows * n if stream else bytes_launch
-    achieved = link_bytes / (mv_ms * 1e-3) / 1e9
+    link_bytes = bytes_launch - res_bytes if stream else bytes_launch
+    # ... unless so much of A is resident that HBM, not the link, bounds the matVec
+    link_bound = stream and link_bytes / H2D_PEAK_GBS >= bytes_launch / HBM_PEAK_GBS
+    achieved = (link_bytes if link_bound else bytes_launch) / (mv_ms * 1e-3) / 1e9
     traffic = None if (stream or poisson) else pmc_traffic(n, world, "_symmetric" if symmetric else "")
-    peak = H2D_PEAK_GBS if stream else HBM_PEAK_GBS
+    peak = H2D_PEAK_GBS if link_bound else HBM_PEAK_GBS
     iters_per_s = args.steps / elapsed
     out = {
         "metric": METRIC,
@@ -384,8 +389,8 @@ def main(argv=None) -> int:
         "config": {
             "workload": (f"configs[3]: N={n} dense SPD fp64 CG, A streamed from pinned host memory every matVec"
                          + (" as its upper-triangle tiles (CGX_SYMMETRIC)" if symmetric else "")
-                         + (f" except the first {res_rows} rows per GPU, kept in HBM ({args.resident_gb:g} GB "
-                            f"budget)" if res_rows else "")
+                         + (f" except the first {res_rows} {'tiles' if symmetric else 'rows per GPU'}, kept in HBM "
+                            f"({args.resident_gb:g} GB budget)" if res_rows else "")
                          + f", row-block over {world} GPU(s), fixed-count iterations") if stream else
                         (f"configs[4]: matrix-free 5-point Poisson CG, m={m} (N={n}), b=1, x0=0, slabs over {world} "
                          f"GPU(s), halo exchange, fixed-count iterations") if poisson else
@@ -408,7 +413,7 @@ def main(argv=None) -> int:
         "matvec_ms": mv_ms,
         "matvec_ms_max_rank": mv_ms_max,
         "roofline": {
-            "bound": "h2d" if stream else "hbm",
+            "bound": "h2d" if link_bound else "hbm",
             "achieved": achieved,
             "peak": peak,
             "unit": "GB/s",

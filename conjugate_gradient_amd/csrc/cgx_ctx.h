@@ -199,7 +199,7 @@ struct Shard {
     bool buf_used[kStreamBufs] = {};
     int next_buf = 0;
     MatvecPlan tile_plan;
-    // CGX_STREAM_RESIDENT_MB: the first res_rows rows also live in HBM (A),
+    // CGX_STREAM_RESIDENT_MB: the first res_rows rows (CGX_SYMMETRIC: tiles) also live in HBM (A),
     // copied from A_host when res_dirty; only the rest streams per matVec,
     // and the resident rows are multiplied while the first tiles copy.
     int64_t res_rows = 0;

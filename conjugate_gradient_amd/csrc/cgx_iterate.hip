@@ -70,7 +70,16 @@ int matvec_streamed(cgx_ctx *c, Shard &s, const char *vec) {
 int matvec_sym_streamed(cgx_ctx *c, Shard &s, const char *vec, bool with_dot, int dot_slot, const int64_t *gate) {
     const int64_t ntiles = sym_tiles(c->lda), tb = 128 * 128 * 8;
     const double *p = reinterpret_cast<const double *>(vec);
-    for (int64_t q0 = 0; q0 < ntiles; q0 += s.tile_rows) {
+    if (s.res_rows > 0) {  // the resident tiles first, under the copies of the rest (as matvec_streamed)
+        if (s.res_dirty) {
+            HIPT(hipMemcpyAsync(s.A, s.A_host, (size_t)s.res_rows * tb, hipMemcpyHostToDevice, s.stream));
+            s.res_dirty = false;
+        }
+        HIPT(symv_tiles_f64(reinterpret_cast<const double *>(s.A), 0, s.res_rows, c->lda, s.sym_grid, true, p,
+                            reinterpret_cast<double *>(s.sym_prow), reinterpret_cast<double *>(s.sym_pcol), s.stream,
+                            gate));
+    }
+    for (int64_t q0 = s.res_rows; q0 < ntiles; q0 += s.tile_rows) {
         const int64_t cnt = std::min(s.tile_rows, ntiles - q0);
         const int b = s.next_buf;
         s.next_buf = (s.next_buf + 1) % kStreamBufs;

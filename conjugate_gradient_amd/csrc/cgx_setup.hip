@@ -63,6 +63,11 @@ int alloc_shard(cgx_ctx *c, Shard &s) {
         TRY(dmalloc(&s.sym_prow, (size_t)ntiles * 128 * 8));
         TRY(dmalloc(&s.sym_pcol, (size_t)ntiles * 128 * 8));
         s.sym_grid = sym_grid(s.dev);
+        // CGX_STREAM_RESIDENT_MB: the first tiles (res_rows counts tiles here) stay in HBM
+        const char *rmb = std::getenv("CGX_STREAM_RESIDENT_MB");
+        const int64_t res_bytes = (int64_t)((rmb && *rmb) ? std::atoll(rmb) : 0) << 20;
+        s.res_rows = std::max<int64_t>(0, std::min<int64_t>(ntiles, res_bytes / tb));
+        if (s.res_rows > 0) TRY(dmalloc(&s.A, (size_t)s.res_rows * tb));
     } else if (c->flags & CGX_HOST_STREAM) {
         // A in pinned host memory, kStreamBufs device tiles of ~CGX_STREAM_TILE_MB.
         hipError_t e = hipHostMalloc(reinterpret_cast<void **>(&s.A_host), abytes ? abytes : 16, hipHostMallocDefault);
@@ -576,6 +581,7 @@ int cgx_set_rows(cgx_ctx *c, int64_t row0, int64_t nrows, const void *A_rows, in
                     At[(sym_off_h(I, nt) + j / 128 - I) * 128 * 128 + sym_pos_h(r, (int)(j % 128))] =
                         j < c->n ? row[j] : 0.0;
             }
+            if (sym_off_h(lo / 128, nt) < s.res_rows) s.res_dirty = true;
         } else if (A_rows && s.A_host) {
             for (int64_t i = lo; i < hi; ++i) {
                 char *dst = s.A_host + (size_t)(i - s.row0) * c->lda * es;
@@ -652,6 +658,7 @@ int cgx_generate_spd(cgx_ctx *c, uint64_t seed) {
             }
             HIPT(gen_b_f64(c->n, seed, reinterpret_cast<double *>(s.b), s.stream));
             TRY(rank_wait_stream(c, s.stream, "the tile generation"));
+            s.res_dirty = s.res_rows > 0;
         } else if (s.A_host) {
             // Generate each tile on the device and move it to the host copy of A;
             // b is generated for the whole block first (rows are independent).

@@ -131,3 +131,31 @@ def test_symmetric_host_streamed_generator_matches_resident(monkeypatch):
         xd, sd = d.solve(None, eps=1e-10)
     assert ss.iterations == sd.iterations
     assert rel(xs, xd) <= 1e-12
+
+
+@pytest.mark.parametrize("resident_mb", ["3", "1000"])
+def test_symmetric_host_streamed_with_resident_tiles(monkeypatch, resident_mb):
+    """CGX_STREAM_RESIDENT_MB with the tile stream: the first tiles stay in
+    HBM (3 MB = 24 tiles: a resident part that ends inside a tile row; 1000
+    MB: all of them) and only the rest streams.  Every chunking writes the
+    same per-tile partials, so x is bit for bit the fully streamed solve's --
+    rows set on the host, generated on the device, A replaced between solves."""
+    monkeypatch.setenv("CGX_STREAM_TILE_MB", "1")
+    n = 2000
+    A, b = oracle.spd_hash(n, seed=3)
+    A2, b2 = oracle.spd_hash(n, seed=4)
+    out = {}
+    for res in ("0", resident_mb):
+        monkeypatch.setenv("CGX_STREAM_RESIDENT_MB", res)
+        with cg.Solver(n, flags=SYM | cg.CGX_HOST_STREAM) as s:
+            s.set_system(A, b)
+            r1 = s.solve(None, eps=1e-10)
+            s.set_system(A2, b2)
+            r2 = s.solve(None, eps=1e-10)
+            s.generate_spd(42)
+            r3 = s.solve(None, eps=1e-10)
+        out[res] = [(x, st.iterations) for x, st in (r1, r2, r3)]
+    for (xa, ia), (xb, ib) in zip(out["0"], out[resident_mb]):
+        assert ia == ib and np.array_equal(xa.view(np.uint8), xb.view(np.uint8))
+    xo, so = oracle.cg_f64(A2, b2, np.zeros(n), eps=1e-10)
+    assert out[resident_mb][1][1] == so.iterations and rel(out[resident_mb][1][0], xo) <= TOL
