@@ -233,7 +233,8 @@ struct cgx_ctx {
     bool overlap = false;  // own-column-block matVec while p is exchanged
     bool fused = false;    // Poisson: two-kernel fused iteration (k_poisson_p + k_poisson_xr)
     bool fused_p = false;  // dense, one GPU, small n: two launches per iteration (matVec, k_update_xrp_f64)
-    bool ref_fused = false;  // CGX_F32_REF, dense, one GPU: two launches per iteration (matVec + p.Ap, x/r/r.r/p)
+    bool ref_mv_dot = false;  // CGX_F32_REF, resident dense: the matVec's last block runs vecVec(p, Ap) (any mode)
+    bool ref_fused = false;   // ... and on one GPU: two launches per iteration (matVec + p.Ap, x/r/r.r/p)
     bool halo_overlap = false;  // fused Poisson, several slabs: r's halo exchange overlaps k_poisson_p
     bool halo_pending = false;  // an overlapped r halo exchange is in flight on the comm streams
     // rank mode fail-fast (cgx_exchange.hip, rank_wait_*): every host wait

@@ -127,7 +127,7 @@ int launch_matvec(cgx_ctx *c, Shard &s, const char *vec, bool with_dot, int dot_
                       with_dot ? reinterpret_cast<const double *>(s.pown) : nullptr,
                       with_dot ? reinterpret_cast<double *>(slot(s, dot_slot)) : nullptr, s.ws, s.stream,
                       gate_of(s, gated)));
-    else if (with_dot && c->ref_fused)  // matVec + vecVec(p, Ap) in one launch (serialConjugate.c:215,219)
+    else if (with_dot && c->ref_mv_dot)  // matVec + vecVec(p, Ap) in one launch (serialConjugate.c:215,219)
         HIPT(matvec_dot_ref_f32(reinterpret_cast<const float *>(s.A), c->lda, s.nloc, c->n,
                                 reinterpret_cast<const float *>(vec), reinterpret_cast<float *>(s.Ap),
                                 reinterpret_cast<const float *>(s.pown), reinterpret_cast<float *>(slot(s, dot_slot)),
@@ -137,7 +137,7 @@ int launch_matvec(cgx_ctx *c, Shard &s, const char *vec, bool with_dot, int dot_
         HIPT(hipEventRecord(s.ev_t[2 * s.ev_used + 1], s.stream));
         s.ev_used++;
     }
-    if (with_dot && ((f32ref(c) && !c->ref_fused) || (streamed && !(c->flags & CGX_SYMMETRIC)))) {
+    if (with_dot && ((f32ref(c) && !c->ref_mv_dot) || (streamed && !(c->flags & CGX_SYMMETRIC)))) {
         if (f32ref(c))  // vecVec(p, Ap) sequential (serialConjugate.c:219)
             HIPT(dot_ref_f32(s.nloc, reinterpret_cast<const float *>(s.pown),
                              reinterpret_cast<const float *>(s.Ap), reinterpret_cast<float *>(slot(s, dot_slot)),

@@ -269,11 +269,14 @@ static bool can_fuse_p(const cgx_ctx *c) {
     return c->n <= kFusePMax;
 }
 
-// The F32_REF counterpart (do_iteration_ref_fused): one GPU, resident
-// row-major A; CGX_REF_FUSE=0 keeps four launches (matVec, p.Ap, x/r + r.r,
-// p).  The same float operations in the same order either way.
-static bool can_fuse_ref(const cgx_ctx *c) {
-    if (c->mode != M_SINGLE || c->op != OP_DENSE || !f32ref(c)) return false;
+// The F32_REF counterparts: with resident row-major A the matVec's last
+// block runs vecVec(p, Ap) over the shard's rows (the shard's partial in
+// row-block modes), and on one GPU the iteration is two launches
+// (do_iteration_ref_fused).  CGX_REF_FUSE=0 keeps the separate launches
+// (matVec, p.Ap, x/r + r.r, p).  The same float operations in the same order
+// either way.
+static bool can_fuse_ref_dot(const cgx_ctx *c) {
+    if (c->op != OP_DENSE || !f32ref(c)) return false;
     if (c->flags & (CGX_SYMMETRIC | CGX_HOST_STREAM)) return false;
     const char *e = std::getenv("CGX_REF_FUSE");
     return !(e && *e == '0');
@@ -282,7 +285,8 @@ static bool can_fuse_ref(const cgx_ctx *c) {
 int finish_create(cgx_ctx *c, cgx_ctx **out) {
     c->overlap = can_overlap(c);
     c->fused_p = can_fuse_p(c);
-    c->ref_fused = can_fuse_ref(c);
+    c->ref_mv_dot = can_fuse_ref_dot(c);
+    c->ref_fused = c->ref_mv_dot && c->mode == M_SINGLE;
     if (c->op == OP_POISSON) {  // CGX_POISSON_FUSED=0: the three-kernel split (stencil, r, x/p)
         const char *e = std::getenv("CGX_POISSON_FUSED");
         c->fused = !(e && *e == '0') && poisson_fusable(c->sh[0].nloc / c->m, c->m);

@@ -9,6 +9,9 @@ per-iteration time; every solve's x must be serialConjugate.c's (the
 oracle's) bit for bit.
 
   python tools/ref_fuse_ab.py [n ...]        (default 512 1024 2048 4096 8192)
+  CGX_AB_SHARDS=4 python tools/ref_fuse_ab.py 8192   (P row blocks on this GPU:
+      the matVec + partial vecVec launch against two launches; x checked
+      against parallel_cg.c's MPICH combine order)
 """
 import json
 import os
@@ -28,12 +31,13 @@ def main():
     for n in sizes:
         A, b = oracle.spd_matlab(n, np.float32)
         x0 = np.zeros(n, np.float32)
-        xr, sr = oracle.cg_f32ref(A, b, x0, eps=1e-6)
+        P = int(os.environ.get("CGX_AB_SHARDS", "1"))
+        xr, sr = oracle.cg_f32ref(A, b, x0, eps=1e-6, nparts=P, combine="mpich")
         solvers = {}
         for fuse in ("1", "0"):
             os.environ["CGX_REF_FUSE"] = fuse
-            s = cg.Solver(n, flags=cg.CGX_F32_REF)
-            assert bool(s.info.flags & cg.CGX_FUSED_ACTIVE) == (fuse == "1")
+            s = cg.Solver(n, flags=cg.CGX_F32_REF, devices=[0] * P if P > 1 else None)
+            assert P > 1 or bool(s.info.flags & cg.CGX_FUSED_ACTIVE) == (fuse == "1")
             s.set_system(A, b, x0)
             solvers["two_launch" if fuse == "1" else "four_launch"] = s
         solve_ms = {k: [] for k in solvers}
@@ -56,7 +60,7 @@ def main():
                     iter_us[name].append((t1 - t0) / 200 * 1e6)
         for s in solvers.values():
             s.close()
-        row = {"n": n, "iterations": int(sr.iterations), "x_bit_identical_to_reference": True}
+        row = {"n": n, "shards": P, "iterations": int(sr.iterations), "x_bit_identical_to_reference": True}
         for name in solvers:
             row[name + "_solve_ms_med"] = statistics.median(solve_ms[name])
             row[name + "_solve_ms_min"] = min(solve_ms[name])
