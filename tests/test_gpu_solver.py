@@ -391,7 +391,8 @@ def _f32_system(name):
     return case(name, np.float32)
 
 
-@pytest.mark.parametrize("name", ["kat2_x0", "kat4", "spd512", "spd2048", "spd8192", "hash1000", "hash4100"])
+@pytest.mark.parametrize("name", ["kat2_x0", "kat4", "spd512", "spd2048", "spd8192", "hash1000", "hash4100",
+                                  "hash1", "hash3", "hash33", "hash513", "hash4097"])
 def test_f32ref_two_launch_iteration_bitwise_equals_four(monkeypatch, name):
     """CGX_F32_REF on one GPU iterates in two launches (CGX_REF_FUSE): the
     matVec whose last block runs vecVec(p, Ap), then one block for x/r, r.r,
