@@ -103,15 +103,22 @@ def matvec_bytes(n: int, nloc: int) -> int:
     return 8 * nloc * n + 8 * n + 8 * nloc
 
 
-def pmc_traffic(n: int, nranks: int, suffix: str = "") -> float | None:
+def pmc_traffic(n: int, nranks: int, suffix: str = "") -> tuple[float | None, str | None]:
+    """HBM bytes per matVec launch from the committed PMC passes (rocprofv3
+    cannot run inside this process), and where that figure came from."""
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     try:
         with open(path) as f:
             s = json.load(f)
         key = f"n{n}_g{nranks}{suffix}"
-        return float(s[key]["hbm_bytes_per_matvec"]) if key in s else None
+        if key not in s:
+            return None, None
+        e = s[key]
+        src = (f"profiles/pmc_summary.json[{key}]: 2*FETCH_SIZE + WRITE_SIZE from separate rocprofv3 --pmc passes "
+               f"of this workload (tag {e.get('tag', '?')}), not counted in this run")
+        return float(e["hbm_bytes_per_matvec"]), src
     except (OSError, ValueError, KeyError):
-        return None
+        return None, None
 
 
 def cpu_baseline(n: int, iters: int = 5, threads_gen: int = 16) -> dict:
@@ -367,7 +374,8 @@ def main(argv=None) -> int:
     # ... unless so much of A is resident that HBM, not the link, bounds the matVec
     link_bound = stream and link_bytes / H2D_PEAK_GBS >= bytes_launch / HBM_PEAK_GBS
     achieved = (link_bytes if link_bound else bytes_launch) / (mv_ms * 1e-3) / 1e9
-    traffic = None if (stream or poisson) else pmc_traffic(n, world, "_symmetric" if symmetric else "")
+    traffic, traffic_src = (None, None) if (stream or poisson) else pmc_traffic(n, world,
+                                                                               "_symmetric" if symmetric else "")
     peak = H2D_PEAK_GBS if link_bound else HBM_PEAK_GBS
     iters_per_s = args.steps / elapsed
     out = {
@@ -419,6 +427,7 @@ def main(argv=None) -> int:
             "unit": "GB/s",
             "frac": achieved / peak,
             "traffic": traffic,
+            "traffic_source": traffic_src,
             "kernel": (("k_poisson_xr_f64" if fused else "k_stencil5_f64") if poisson else
                        "H2D copies + k_symv_f64 per chunk + k_symv_reduce_f64" if (symmetric and stream) else
                        "k_symv_f64 + k_symv_reduce_f64" if symmetric else "k_matvec_f64"),
