@@ -62,3 +62,16 @@ def test_matvec_bytes_formula():
     # 34.36 GB on 1 GPU, 4.295 GB per GPU on 8 at N = 65536
     assert abs(bench.matvec_bytes(65536, 65536) / 1e9 - 34.36) < 0.01
     assert abs(bench.matvec_bytes(65536, 8192) / 1e9 - 4.295) < 0.001
+
+
+def test_traffic_lookup_names_its_source():
+    """roofline.traffic is the committed PMC figure for the same workload
+    (rocprofv3 cannot run inside the bench process): the bench reports where
+    it came from, and null where no pass exists (e.g. N=4096)."""
+    t, src = bench.pmc_traffic(65536, 1)
+    assert t is not None and 1.0 <= t / bench.matvec_bytes(65536, 65536) < 1.01
+    assert "pmc_summary.json[n65536_g1]" in src and "FETCH_SIZE" in src
+    for g in (2, 4, 8):
+        t, src = bench.pmc_traffic(65536, g)
+        assert t is not None and 1.0 <= t / bench.matvec_bytes(65536, 65536 // g) < 1.01, g
+    assert bench.pmc_traffic(4096, 1) == (None, None)
