@@ -569,6 +569,9 @@ int cgx_set_rows(cgx_ctx *c, int64_t row0, int64_t nrows, const void *A_rows, in
     if (A_rows && c->op == OP_POISSON) return fail(CGX_ERR_ARG, "the Poisson operator is matrix-free: A must be NULL");
     if (A_rows && lda_host < c->n) return fail(CGX_ERR_ARG, "lda_host (%lld) < n", (long long)lda_host);
     const size_t es = (size_t)c->es;
+    // A host-streamed A is rewritten in place on the host: first let every
+    // copy (and kernel) still reading it from enqueued iterations finish.
+    if (A_rows && (c->flags & CGX_HOST_STREAM)) TRY(sync_all(c));
     for (auto &s : c->sh) {
         const int64_t lo = std::max(row0, s.row0), hi = std::min(row0 + nrows, s.row0 + s.nloc);
         if (hi <= lo) continue;
@@ -648,6 +651,7 @@ int cgx_generate_spd(cgx_ctx *c, uint64_t seed) {
     const Range range_("cgx_generate_spd");
     if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
     if (c->op == OP_POISSON) return fail(CGX_ERR_ARG, "the Poisson operator has no matrix to generate (use cgx_fill)");
+    if (c->flags & CGX_HOST_STREAM) TRY(sync_all(c));  // copies of enqueued iterations still read A_host
     for (auto &s : c->sh) {
         TRY(set_dev(s));
         if (s.A_host && (c->flags & CGX_SYMMETRIC)) {

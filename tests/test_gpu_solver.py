@@ -482,8 +482,10 @@ def test_host_streamed_with_resident_rows(monkeypatch, resident_mb, shards):
         with cg.Solver(n, flags=cg.CGX_F64 | cg.CGX_HOST_STREAM, devices=shards) as s:
             s.set_system(A, b)
             x1, st1 = s.solve(None, eps=1e-10)
+            s.begin()
+            s.iterate(4, eps=-1.0)  # left in flight: set_system must wait for its copies of A
             s.set_system(A2, b2)
-            x2, st2 = s.solve(None, eps=1e-10)
+            x2, st2 = s.solve(np.zeros(n), eps=1e-10)
             s.generate_spd(seed=5)
             x3, st3 = s.solve(None, eps=1e-10)
         A32, b32, x032 = case("spd1024")
