@@ -46,7 +46,7 @@ def counters(path, name):
     return vals
 
 
-def summarise(n, shards, fetch_csv, write_csv):
+def summarise(n, shards, fetch_csv, write_csv, tag):
     fe, wr = counters(fetch_csv, "FETCH_SIZE"), counters(write_csv, "WRITE_SIZE")
     assert len(fe) % 2 == 0 and len(fe) == len(wr), (len(fe), len(wr))
     pairs_f = [fe[i] + fe[i + 1] for i in range(0, len(fe), 2)]
@@ -57,7 +57,7 @@ def summarise(n, shards, fetch_csv, write_csv):
     hbm = 2 * f_kib * 1024 + w_kib * 1024
     entry = {
         "kernel": KERNEL,
-        "tag": "r01",
+        "tag": tag,
         "measured_as": f"{shards} row blocks of {nloc} rows on one MI355X (multi-shard mode): per rank, the "
                        f"own-column-block and remaining-columns launches of one matVec, summed",
         "fetch_size_kib_median": f_kib,
@@ -87,11 +87,12 @@ def main():
     ap.add_argument("--iters", type=int, default=3)
     ap.add_argument("--fetch")
     ap.add_argument("--write")
+    ap.add_argument("--tag", default="r02", help="round the counters were collected in")
     a = ap.parse_args()
     if a.mode == "run":
         run(a.n, a.shards, a.iters)
     else:
-        summarise(a.n, a.shards, a.fetch, a.write)
+        summarise(a.n, a.shards, a.fetch, a.write, a.tag)
 
 
 if __name__ == "__main__":
