@@ -15,6 +15,15 @@ typedef double d2 __attribute__((ext_vector_type(2)));
 
 constexpr int kNT = 256;  // threads per block for the fp64 kernels
 
+// CG's alpha = r.r / p.Ap and beta = r.r_new / r.r_old, fp64.  A zero
+// denominator means the iteration has converged exactly (r = 0, or r.r has
+// underflowed: fixed-count runs go on long past convergence): that is CG's
+// "lucky breakdown", and the ratio is 0, so x stays at the solution and r, p
+// stay 0 instead of turning into 0/0 = NaN.  Any other denominator gives the
+// plain quotient, bit for bit.  (CGX_F32_REF keeps the reference's float
+// division as it is, NaN included: serialConjugate.c:220,239.)
+__device__ __forceinline__ double cg_ratio(double num, double den) { return den != 0.0 ? num / den : 0.0; }
+
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, 64);

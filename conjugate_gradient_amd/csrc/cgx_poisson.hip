@@ -281,7 +281,7 @@ __global__ __launch_bounds__(kNT) void k_poisson_p_f64(const double *__restrict_
     // p_0 = r_0 (first) has its own instantiation: no p_{k-1} loads
     const double acc = first ? poisson_p_body<RB, NT, true, HT>(rh, poh, pnh, mloc, m, nstrips, rpi, ir, 0.0, edge)
                              : poisson_p_body<RB, NT, false, HT>(rh, poh, pnh, mloc, m, nstrips, rpi, ir,
-                                                                 *rr / *rsold, edge);
+                                                                 cg_ratio(*rr, *rsold), edge);
     grid_sum_last_block(acc, partials, ticket, dot_out, add_to_out != 0);
 }
 
@@ -349,7 +349,7 @@ __global__ __launch_bounds__(kNT) void k_poisson_xr_f64(const double *__restrict
     static_assert(RB <= kEdgeRB, "edge buffer");
     __shared__ double edge[2 * kWaves * 2 * kEdgeRB];
     if (gate && *gate) return;
-    const double alpha = *rsold / *pAp;
+    const double alpha = cg_ratio(*rsold, *pAp);
     double acc = 0.0;
     int par = 0;
     for (int64_t v = blockIdx.x; v < nitems; v += gridDim.x) {

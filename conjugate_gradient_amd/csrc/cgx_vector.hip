@@ -57,7 +57,7 @@ __global__ __launch_bounds__(kNT) void k_update_xr_f64(int64_t n, double *__rest
                                                        const double *rsold, const double *pAp,
                                                        double *rr_out, double *partials,
                                                        unsigned *ticket) {
-    const double alpha = *rsold / *pAp;
+    const double alpha = cg_ratio(*rsold, *pAp);
     double acc = 0.0;
     if constexpr (VEC) {
         CGX_VEC_LOOP_BEGIN
@@ -101,7 +101,7 @@ template <bool VEC, int VP = 0>
 __global__ __launch_bounds__(kNT) void k_update_p_f64(int64_t n, double *__restrict__ p,
                                                       const double *__restrict__ r,
                                                       const double *rr, const double *rsold) {
-    const double beta = *rr / *rsold;
+    const double beta = cg_ratio(*rr, *rsold);
     if constexpr (VEC) {
         CGX_VEC_LOOP_BEGIN
         d2 pv[kVU], rv[kVU];
@@ -149,7 +149,7 @@ __global__ __launch_bounds__(kNT) void k_update_xrp_f64(int64_t n, double *__res
                                                         ConvArgs cv) {
     if (gate && *gate) return;
     const double rs = *rsold;
-    const double alpha = rs / *pAp;
+    const double alpha = cg_ratio(rs, *pAp);
     const __amdgpu_buffer_rsrc_t rrs = vec_rsrc(r, n);
     double acc = 0.0;
     if constexpr (VEC) {
@@ -194,7 +194,7 @@ __global__ __launch_bounds__(kNT) void k_update_xrp_f64(int64_t n, double *__res
         if (threadIdx.x == 0) record_convergence(cv, cv.k + 1, rr);
         return;
     }
-    const double beta = rr / rs;
+    const double beta = cg_ratio(rr, rs);
     if constexpr (VEC) {
         // One CU does all of p: every load of a thread's share (up to kPU
         // pairs, n <= 8192 in one step) is issued before the first store, so
@@ -231,7 +231,7 @@ __global__ __launch_bounds__(kNT) void k_update_r_f64(int64_t n, double *__restr
                                                       const double *rsold, const double *pAp, double *rr_out,
                                                       double *partials, unsigned *ticket, const int64_t *gate) {
     if (gate && *gate) return;
-    const double alpha = *rsold / *pAp;
+    const double alpha = cg_ratio(*rsold, *pAp);
     double acc = 0.0;
     if constexpr (VEC) {
         CGX_VEC_LOOP_BEGIN
@@ -282,8 +282,8 @@ __global__ __launch_bounds__(kNT) void k_update_xp_f64(int64_t n, double *__rest
             if (blockIdx.x == 0 && threadIdx.x == 0) record_convergence(cv, cv.k + 1, rrn);
         }
     }
-    const double alpha = *rsold / *pAp;
-    const double beta = upd_p ? *rr / *rsold : 0.0;
+    const double alpha = cg_ratio(*rsold, *pAp);
+    const double beta = upd_p ? cg_ratio(*rr, *rsold) : 0.0;
     if constexpr (VEC) {
         CGX_VEC_LOOP_BEGIN
         d2 xv[kVU], pv[kVU], rv[kVU];

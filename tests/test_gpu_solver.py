@@ -295,6 +295,41 @@ def test_solve_in_pieces_and_fixed_count():
         assert st2.iterations == 9 and st2.converged == 0
 
 
+@pytest.mark.parametrize("kind,fuse_p", [("dense", None), ("dense", "0"), ("shards", None), ("symmetric", None),
+                                         ("poisson", None)])
+def test_fixed_count_past_convergence_stays_finite(monkeypatch, kind, fuse_p):
+    """bench.py's fixed-count mode runs on long after CG has converged: r.r
+    shrinks until it underflows to 0, and alpha / beta would then be 0/0.
+    The fp64 kernels treat a zero denominator as the exact convergence it is
+    (alpha = beta = 0, cg_ratio in cgx_device.h): x stays at the solution, no
+    NaN (bench.py at N=16384, 300 steps, reported relres NaN before)."""
+    if fuse_p is not None:
+        monkeypatch.setenv("CGX_FUSE_P", fuse_p)
+    if kind == "poisson":
+        kw, n, steps = {"poisson_m": 8}, None, 3000
+    else:
+        kw = {"flags": cg.CGX_F64 | (cg.CGX_SYMMETRIC if kind == "symmetric" else 0)}
+        if kind == "shards":
+            kw["devices"] = [0, 0]
+        n, steps = 1024, 600
+    with cg.Solver(n, **kw) as s:
+        if kind == "poisson":
+            s.fill(1.0, 0.0)
+        else:
+            s.generate_spd(3)
+        x_conv, st = s.solve(None, eps=1e-12)
+        assert st.converged
+        rn_conv, bn = s.residual_norm()
+        s.set_x(np.zeros(s.n))
+        _, st2 = s.solve(None, eps=-1.0, max_iter=steps)
+        assert st2.iterations == steps
+        x = s.get_x()
+        rn, bn2 = s.residual_norm()
+    assert np.all(np.isfinite(x)), kind
+    assert rn / bn2 <= max(1e-12, 10 * rn_conv / bn), (rn / bn2, rn_conv / bn)
+    assert rel(x, x_conv) <= 1e-10
+
+
 def test_timing_events_count():
     """CGX_TIMING times every matVec launch.  With x0 = 0 the initial A x0 is
     skipped (exactly zero); with any other x0 it runs."""
