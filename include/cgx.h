@@ -213,7 +213,10 @@ int cgx_set_x(cgx_ctx *ctx, const void *x);
 
 /* ---- the solve (conjugrad) -------------------------------------------------- */
 /* x_inout may be NULL (use / leave the device-resident x).  eps < 0: never
- * stop early; max_iter < 0: n (the reference's `k < ROWS`). */
+ * stop early; max_iter < 0: n (the reference's `k < ROWS`).  Iterations past
+ * exact convergence (p.Ap or the old r.r exactly 0, e.g. after r.r underflows
+ * in a long fixed-count run) take alpha = beta = 0 in fp64, so x stays at the
+ * solution; CGX_F32_REF divides as serialConjugate.c does (0/0 = NaN). */
 int cgx_solve(cgx_ctx *ctx, void *x_inout, double eps, int64_t max_iter, cgx_stats *st);
 /* The same solve in pieces: r0 = p0 = b - A x, then `count` iterations. */
 int cgx_solve_begin(cgx_ctx *ctx);
