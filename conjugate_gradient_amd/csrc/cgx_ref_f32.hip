@@ -486,7 +486,7 @@ __global__ __launch_bounds__(256) void k_matvec_ref_f32_w4(const float *__restri
 // (sc1) and the last block to arrive (ticket) runs vecVec(p, Ap) over all
 // `rows` -- dot_ref_body, the separate dot kernel's code -- so the matVec and
 // p.Ap are one launch (serialConjugate.c:215,219), the same bits.
-template <int ROWS, bool FULL, bool DOT>
+template <bool FULL, bool DOT>
 __global__ __launch_bounds__(320) void k_matvec_ref_f32_w5(const float *__restrict__ A, int64_t lda,
                                                            int64_t rows, int64_t cols,
                                                            const float *__restrict__ v,
@@ -496,42 +496,41 @@ __global__ __launch_bounds__(320) void k_matvec_ref_f32_w5(const float *__restri
 #pragma clang fp contract(off)
     if (gate && *gate) return;  // converged in an earlier iteration (device-side gating)
     typedef float f4 __attribute__((ext_vector_type(4)));
-    constexpr int K = ROWS * kRef3Q / 256;  // quads per loader lane per tile: rows rsub + 2k
-    __shared__ f4 prod[2][ROWS * kRef3Ld4];
+    __shared__ f4 prod[2][kRef3Rows * kRef3Ld4];
     const int t = threadIdx.x;
     const int l = t >= 64 ? t - 64 : 0;  // loader lane (waves 1-4); wave 0 only adds
-    const int64_t row0 = (int64_t)blockIdx.x * ROWS;
+    const int64_t row0 = (int64_t)blockIdx.x * kRef3Rows;
     const int64_t ntiles = (cols + kRef3TC - 1) / kRef3TC;
     const int quad = l % kRef3Q, rsub = l / kRef3Q;
-    const int64_t brows = rows - row0 < ROWS ? rows - row0 : ROWS;
+    const int64_t brows = rows - row0 < kRef3Rows ? rows - row0 : kRef3Rows;
     const __amdgpu_buffer_rsrc_t ars =
         __builtin_amdgcn_make_buffer_rsrc((void *)(A + row0 * lda), 0, (int)(brows * lda * 4), 0x00020000);
     const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc((void *)v, 0, (int)(cols * 4), 0x00020000);
     const int voff = (int)((rsub * lda + 4 * quad) * 4);
     const int end_off = (int)(brows * lda * 4);  // a tile past the end: every load out of range
-    f4 a0[K], a1[K];
+    f4 a0[kRef3K], a1[kRef3K];
     f4 p0, p1;
-    auto issue = [&](f4 (&a)[K], f4 &pv, int64_t tile) {
+    auto issue = [&](f4 (&a)[kRef3K], f4 &pv, int64_t tile) {
         const bool real = tile < ntiles;
         const int c4 = (int)(tile * kRef3TC * 4);
 #pragma unroll
-        for (int k = 0; k < K; ++k)
+        for (int k = 0; k < kRef3K; ++k)
             a[k] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(
                                               ars, voff, real ? (int)(2 * k * lda * 4) + c4 : end_off, 2));
         pv = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(vrs, quad * 16, real ? c4 : (int)(cols * 4), 0));
     };
-    auto store = [&](f4 (&a)[K], f4 &pv, int slot, int64_t tile) {
+    auto store = [&](f4 (&a)[kRef3K], f4 &pv, int slot, int64_t tile) {
         if (!FULL) {  // columns past `cols`: +0 products whatever A's padding holds
             const int64_t cq = tile * kRef3TC + 4 * quad;
             for (int e = 0; e < 4; ++e)
                 if (cq + e >= cols) {
                     pv[e] = 0.0f;
 #pragma unroll
-                    for (int k = 0; k < K; ++k) a[k][e] = 0.0f;
+                    for (int k = 0; k < kRef3K; ++k) a[k][e] = 0.0f;
                 }
         }
 #pragma unroll
-        for (int k = 0; k < K; ++k) prod[slot][(rsub + 2 * k) * kRef3Ld4 + quad] = a[k] * pv;
+        for (int k = 0; k < kRef3K; ++k) prod[slot][(rsub + 2 * k) * kRef3Ld4 + quad] = a[k] * pv;
     };
     float acc = 0.0f;  // matvec[i] = 0.0  (serialConjugate.c:114)
     auto chain = [&](int slot) {  // matvec[i] += A[i][j] * x[j], j ascending (:117)
@@ -587,10 +586,10 @@ __global__ __launch_bounds__(320) void k_matvec_ref_f32_w5(const float *__restri
     if (__builtin_amdgcn_readfirstlane(t >> 6) == 0) {
         __syncthreads();
         for (int64_t tt = 0; tt < nsteps; ++tt) {
-            if (t < ROWS && tt < ntiles) chain((int)(tt & 1));
+            if (t < kRef3Rows && tt < ntiles) chain((int)(tt & 1));
             __syncthreads();
         }
-        if (t < ROWS && row0 + t < rows) {
+        if (t < kRef3Rows && row0 + t < rows) {
             if (DOT)
                 __hip_atomic_store(out + row0 + t, acc, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);  // sc1
             else
@@ -772,10 +771,6 @@ __global__ __launch_bounds__(kNT) void k_update_p_ref_f32(int64_t n, float *__re
 
 }  // namespace
 
-// rows per block of k_matvec_ref_f32_w5: 32 (one block per CU, 132 KiB of
-// LDS) or, with CGX_REF_ROWS=16, 16 (66 KiB: two blocks per CU)
-static int w5_rows() { return env_int("CGX_REF_ROWS", 32) == 16 ? 16 : 32; }
-
 hipError_t matvec_ref_f32(const float *A, int64_t lda, int64_t rows, int64_t cols, const float *v,
                           float *out, hipStream_t s, const int64_t *gate) {
     if (rows <= 0) return hipSuccess;
@@ -787,16 +782,11 @@ hipError_t matvec_ref_f32(const float *A, int64_t lda, int64_t rows, int64_t col
         hipLaunchKernelGGL(k_matvec_ref_f32, dim3((unsigned)((rows + 63) / 64)), dim3(64), 0, s, A, lda, rows,
                            cols, v, out, gate);
     else if ((variant == 3 || variant == 4) && vec_ok) {
-        const int wr = w5_rows();
-        const bool full = rows % (variant == 3 ? wr : kRef3Rows) == 0 && cols % kRef3TC == 0;
+        const bool full = rows % kRef3Rows == 0 && cols % kRef3TC == 0;
         const dim3 grid((unsigned)((rows + kRef3Rows - 1) / kRef3Rows));
-        if (variant == 3 && wr == 16)  // a dedicated adding wave, 16 rows per block (two blocks per CU)
-            hipLaunchKernelGGL((full ? k_matvec_ref_f32_w5<16, true, false> : k_matvec_ref_f32_w5<16, false, false>),
-                               dim3((unsigned)((rows + 15) / 16)), dim3(320), 0, s, A, lda, rows, cols, v, out, gate,
-                               nullptr, nullptr, nullptr);
-        else if (variant == 3)  // a dedicated adding wave (default)
-            hipLaunchKernelGGL((full ? k_matvec_ref_f32_w5<32, true, false> : k_matvec_ref_f32_w5<32, false, false>),
-                               grid, dim3(320), 0, s, A, lda, rows, cols, v, out, gate, nullptr, nullptr, nullptr);
+        if (variant == 3)  // a dedicated adding wave (default)
+            hipLaunchKernelGGL((full ? k_matvec_ref_f32_w5<true, false> : k_matvec_ref_f32_w5<false, false>), grid,
+                               dim3(320), 0, s, A, lda, rows, cols, v, out, gate, nullptr, nullptr, nullptr);
         else  // wave 0 adds and loads
             hipLaunchKernelGGL(full ? k_matvec_ref_f32_w4<true> : k_matvec_ref_f32_w4<false>, grid, dim3(256), 0, s,
                                A, lda, rows, cols, v, out, gate);
@@ -833,16 +823,10 @@ hipError_t matvec_dot_ref_f32(const float *A, int64_t lda, int64_t rows, int64_t
         const hipError_t e = matvec_ref_f32(A, lda, rows, cols, v, out, s, gate);
         return e != hipSuccess ? e : dot_ref_f32(rows, pown, out, dot_out, s, gate);
     }
-    const int wr = w5_rows();
-    const bool full = rows % wr == 0 && cols % kRef3TC == 0;
-    if (wr == 16)
-        hipLaunchKernelGGL((full ? k_matvec_ref_f32_w5<16, true, true> : k_matvec_ref_f32_w5<16, false, true>),
-                           dim3((unsigned)((rows + 15) / 16)), dim3(320), 0, s, A, lda, rows, cols, v, out, gate, pown,
-                           dot_out, ticket);
-    else
-        hipLaunchKernelGGL((full ? k_matvec_ref_f32_w5<32, true, true> : k_matvec_ref_f32_w5<32, false, true>),
-                           dim3((unsigned)((rows + kRef3Rows - 1) / kRef3Rows)), dim3(320), 0, s, A, lda, rows, cols,
-                           v, out, gate, pown, dot_out, ticket);
+    const bool full = rows % kRef3Rows == 0 && cols % kRef3TC == 0;
+    hipLaunchKernelGGL((full ? k_matvec_ref_f32_w5<true, true> : k_matvec_ref_f32_w5<false, true>),
+                       dim3((unsigned)((rows + kRef3Rows - 1) / kRef3Rows)), dim3(320), 0, s, A, lda, rows, cols, v,
+                       out, gate, pown, dot_out, ticket);
     return hipGetLastError();
 }
 
@@ -921,10 +905,10 @@ hipError_t preload_ref_f32() {
     if (e == hipSuccess) e = hipFuncGetAttributes(&a, reinterpret_cast<const void *>(k_dot_ref_f32_blk<kDotXR>));
     if (e == hipSuccess) e = hipFuncGetAttributes(&a, reinterpret_cast<const void *>(k_matvec_ref_f32_w4<true>));
     if (e == hipSuccess) e = hipFuncGetAttributes(&a, reinterpret_cast<const void *>(k_matvec_ref_f32_w4<false>));
-    if (e == hipSuccess) e = hipFuncGetAttributes(&a, reinterpret_cast<const void *>(k_matvec_ref_f32_w5<32, true, false>));
-    if (e == hipSuccess) e = hipFuncGetAttributes(&a, reinterpret_cast<const void *>(k_matvec_ref_f32_w5<32, true, true>));
+    if (e == hipSuccess) e = hipFuncGetAttributes(&a, reinterpret_cast<const void *>(k_matvec_ref_f32_w5<true, false>));
+    if (e == hipSuccess) e = hipFuncGetAttributes(&a, reinterpret_cast<const void *>(k_matvec_ref_f32_w5<true, true>));
     if (e == hipSuccess) e = hipFuncGetAttributes(&a, reinterpret_cast<const void *>(k_dot_ref_f32_blk<kDotXRP>));
-    return e != hipSuccess ? e : hipFuncGetAttributes(&a, reinterpret_cast<const void *>(k_matvec_ref_f32_w5<32, false, false>));
+    return e != hipSuccess ? e : hipFuncGetAttributes(&a, reinterpret_cast<const void *>(k_matvec_ref_f32_w5<false, false>));
 }
 
 }  // namespace cgx
