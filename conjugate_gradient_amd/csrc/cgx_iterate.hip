@@ -189,9 +189,7 @@ int do_begin(cgx_ctx *c) {
     const int os = out_slot(c, ls, gs);
     for (auto &s : c->sh) {
         TRY(set_dev(s));
-        if (zero)
-            HIPT(hipMemsetAsync(s.Ap, 0, (size_t)s.nloc * c->es, s.stream));
-        else
+        if (!zero)
             TRY(launch_matvec(c, s, s.pfull, false, 0));
         s.x_zero = false;  // the iterations update x
         if (f32ref(c)) {
@@ -200,17 +198,20 @@ int do_begin(cgx_ctx *c) {
                                       reinterpret_cast<float *>(s.pown), reinterpret_cast<float *>(slot(s, os)),
                                       s.stream));
         } else {
+            // x0 = 0: Ax = nullptr (r = b - 0.0, no Ap buffer to clear); the
+            // kernel also resets the convergence record (no memset launch)
             double *pown = reinterpret_cast<double *>(s.pown);
-            HIPT(residual_f64(s.nloc, reinterpret_cast<const double *>(s.b), reinterpret_cast<const double *>(s.Ap),
+            HIPT(residual_f64(s.nloc, reinterpret_cast<const double *>(s.b),
+                              zero ? nullptr : reinterpret_cast<const double *>(s.Ap),
                               reinterpret_cast<double *>(s.r), pown, reinterpret_cast<double *>(slot(s, os)), s.ws,
-                              s.stream));
+                              s.stream, reinterpret_cast<int64_t *>(slot(s, S_KDONE))));
         }
     }
     TRY(exchange_scalar(c, ls, gs));
     if (c->fused) TRY(exchange_halo_of(c, &Shard::rh));  // r0's halo rows for k_poisson_p
-    for (auto &s : c->sh) {  // device-side convergence record: not converged
+    for (auto &s : c->sh) {  // device-side convergence record: not converged (fp64: reset by k_residual_f64)
         TRY(set_dev(s));
-        HIPT(hipMemsetAsync(slot(s, S_KDONE), 0, 16, s.stream));
+        if (f32ref(c)) HIPT(hipMemsetAsync(slot(s, S_KDONE), 0, 16, s.stream));
         s.h_rec[0] = s.h_rec[1] = 0;  // no kernel of this solve has run yet (do_begin follows a sync)
     }
     c->k = 0;

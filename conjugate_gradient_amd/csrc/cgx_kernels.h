@@ -46,9 +46,10 @@ hipError_t matvec_f64_cols(const MatvecPlan &pl, const double *A, int64_t lda, i
                            int64_t col_first, int64_t col_count, bool accumulate, const double *v, double *out,
                            const double *pown, double *dot_out, const RedWs &ws, hipStream_t s,
                            const int64_t *gate = nullptr);
-// r = b - Ax; p = r (if p); *rr_out = r.r (if rr_out)
+// r = b - Ax; p = r (if p); *rr_out = r.r (if rr_out).  Ax == nullptr: Ax = 0
+// (r = b - 0.0).  clear2: two int64 the kernel zeroes (the convergence record).
 hipError_t residual_f64(int64_t n, const double *b, const double *Ax, double *r, double *p,
-                        double *rr_out, const RedWs &ws, hipStream_t s);
+                        double *rr_out, const RedWs &ws, hipStream_t s, int64_t *clear2 = nullptr);
 // alpha = *rsold / *pAp; x += alpha p; r -= alpha Ap; *rr_out = r.r
 hipError_t update_xr_f64(int64_t n, double *x, double *r, const double *p, const double *Ap,
                          const double *rsold, const double *pAp, double *rr_out,

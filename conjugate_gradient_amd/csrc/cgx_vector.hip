@@ -7,20 +7,26 @@
 namespace cgx {
 namespace {
 
-// residual x2 + vecVec (serialConjugate.c:210-212)
+// residual x2 + vecVec (serialConjugate.c:210-212).  Ax == nullptr: A x0 is
+// exactly zero (x0 = 0), so r = b - 0.0 without reading an Ap buffer (the same
+// operation, the same bits).  clear2 != nullptr: the solve's device-side
+// convergence record {kdone, r.r} is reset here, by block 0, instead of by a
+// separate memset launch (every gated kernel of the solve follows in stream
+// order).
 template <bool VEC>
 __global__ __launch_bounds__(kNT) void k_residual_f64(int64_t n, const double *__restrict__ b,
                                                       const double *__restrict__ Ax,
                                                       double *__restrict__ r, double *__restrict__ p,
                                                       double *rr_out, double *partials,
-                                                      unsigned *ticket) {
+                                                      unsigned *ticket, int64_t *clear2) {
+    if (clear2 && blockIdx.x == 0 && threadIdx.x < 2) clear2[threadIdx.x] = 0;
     double acc = 0.0;
     if constexpr (VEC) {
         CGX_VEC_LOOP_BEGIN
         d2 bv[kVU], av[kVU];
 #pragma unroll
         for (int u = 0; u < kVU; ++u)
-            if (ok[u]) { const int64_t i = 2 * (base + u * kNT); bv[u] = ld2(b + i); av[u] = ld2(Ax + i); }
+            if (ok[u]) { const int64_t i = 2 * (base + u * kNT); bv[u] = ld2(b + i); av[u] = Ax ? ld2(Ax + i) : (d2)(0.0); }
 #pragma unroll
         for (int u = 0; u < kVU; ++u)
             if (ok[u]) {
@@ -32,14 +38,14 @@ __global__ __launch_bounds__(kNT) void k_residual_f64(int64_t n, const double *_
             }
         CGX_VEC_LOOP_END
         if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
-            const double ri = b[n - 1] - Ax[n - 1];
+            const double ri = b[n - 1] - (Ax ? Ax[n - 1] : 0.0);
             r[n - 1] = ri;
             if (p) p[n - 1] = ri;
             acc += ri * ri;
         }
     } else {
         for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kNT) {
-            const double ri = b[i] - Ax[i];
+            const double ri = b[i] - (Ax ? Ax[i] : 0.0);
             r[i] = ri;
             if (p) p[i] = ri;
             acc += ri * ri;
@@ -400,10 +406,10 @@ __global__ void k_sum_ordered(const T *in, int cnt, int stride, int mpich, T *ou
 }  // namespace
 
 hipError_t residual_f64(int64_t n, const double *b, const double *Ax, double *r, double *p,
-                        double *rr_out, const RedWs &ws, hipStream_t s) {
+                        double *rr_out, const RedWs &ws, hipStream_t s, int64_t *clear2) {
     const bool vec = al16(b) && al16(Ax) && al16(r) && al16(p);
     hipLaunchKernelGGL(vec ? k_residual_f64<true> : k_residual_f64<false>, dim3(grid_vec(n)), dim3(kNT), 0, s, n, b,
-                       Ax, r, p, rr_out, ws.partials, ws.tickets + T_RESID);
+                       Ax, r, p, rr_out, ws.partials, ws.tickets + T_RESID, clear2);
     return hipGetLastError();
 }
 
