@@ -196,7 +196,7 @@ int do_begin(cgx_ctx *c) {
             HIPT(residual_dot_ref_f32(s.nloc, reinterpret_cast<const float *>(s.b),
                                       reinterpret_cast<const float *>(s.Ap), reinterpret_cast<float *>(s.r),
                                       reinterpret_cast<float *>(s.pown), reinterpret_cast<float *>(slot(s, os)),
-                                      s.stream));
+                                      s.stream, reinterpret_cast<int64_t *>(slot(s, S_KDONE))));
         } else {
             // x0 = 0: Ax = nullptr (r = b - 0.0, no Ap buffer to clear); the
             // kernel also resets the convergence record (no memset launch)
@@ -209,11 +209,9 @@ int do_begin(cgx_ctx *c) {
     }
     TRY(exchange_scalar(c, ls, gs));
     if (c->fused) TRY(exchange_halo_of(c, &Shard::rh));  // r0's halo rows for k_poisson_p
-    for (auto &s : c->sh) {  // device-side convergence record: not converged (fp64: reset by k_residual_f64)
-        TRY(set_dev(s));
-        if (f32ref(c)) HIPT(hipMemsetAsync(slot(s, S_KDONE), 0, 16, s.stream));
-        s.h_rec[0] = s.h_rec[1] = 0;  // no kernel of this solve has run yet (do_begin follows a sync)
-    }
+    // The device-side convergence record {kdone, r.r} was reset by the residual
+    // kernel above (k_residual_f64 / k_dot_ref_f32_blk<kDotResid>); the host copy here.
+    for (auto &s : c->sh) s.h_rec[0] = s.h_rec[1] = 0;  // no kernel of this solve has run yet (do_begin follows a sync)
     c->k = 0;
     c->converged = 0;
     c->state = ST_BEGUN;

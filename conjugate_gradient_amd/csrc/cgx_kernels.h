@@ -148,7 +148,7 @@ hipError_t update_xr_ref_f32(int64_t n, float *x, float *r, const float *p, cons
 hipError_t update_xr_dot_ref_f32(int64_t n, float *x, float *r, const float *p, const float *Ap, const float *rsold,
                                  const float *pAp, float *rr, hipStream_t s, const int64_t *gate = nullptr);
 hipError_t residual_dot_ref_f32(int64_t n, const float *b, const float *Ax, float *r, float *p, float *rr,
-                                hipStream_t s);
+                                hipStream_t s, int64_t *clear2 = nullptr);  // clear2: as residual_f64
 // The single-GPU two-launch F32_REF iteration (the same float operations as
 // matvec_ref_f32 + dot_ref_f32 + update_xr_dot_ref_f32 + update_p_ref_f32):
 // out = A v with *dot_out = pown . out from the matVec's last block (ticket:

@@ -679,6 +679,12 @@ __global__ __launch_bounds__(256) void k_dot_ref_f32_blk(int64_t n, DotArgs d, f
     __shared__ f4v sp[2][kDotChunk / 4];
     __shared__ float rr_b;
     const int t = threadIdx.x;
+    if constexpr (MODE == kDotResid) {  // the solve's start: reset the convergence record (no memset launch)
+        if (cv.kdone && t == 0) {
+            *cv.kdone = 0;
+            *cv.rrfinal = 0.0;
+        }
+    }
     const float s = dot_ref_body<MODE == kDotXRP ? (int)kDotXR : MODE, false>(n, d, sp, t);
     if (t == 0) *out = s;
     if constexpr (MODE == kDotXRP) {
@@ -864,13 +870,16 @@ hipError_t update_xr_dot_ref_f32(int64_t n, float *x, float *r, const float *p, 
 }
 
 hipError_t residual_dot_ref_f32(int64_t n, const float *b, const float *Ax, float *r, float *p, float *rr,
-                                hipStream_t s) {
+                                hipStream_t s, int64_t *clear2) {
     DotArgs d;
     d.a = b;
     d.b = Ax;
     d.r = r;
     d.p = p;
-    hipLaunchKernelGGL(k_dot_ref_f32_blk<kDotResid>, dim3(1), dim3(256), 0, s, n, d, rr, nullptr, ConvArgs{});
+    ConvArgs cv;
+    cv.kdone = clear2;
+    cv.rrfinal = clear2 ? reinterpret_cast<double *>(clear2 + 1) : nullptr;
+    hipLaunchKernelGGL(k_dot_ref_f32_blk<kDotResid>, dim3(1), dim3(256), 0, s, n, d, rr, nullptr, cv);
     return hipGetLastError();
 }
 
