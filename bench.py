@@ -90,6 +90,13 @@ def max_over_ranks(dist, value: float) -> float:
     return float(t.item())
 
 
+def gather_objects(dist, obj) -> list:
+    """Every rank's `obj` on every rank (gloo, CPU), in rank order."""
+    out = [None] * dist.get_world_size()
+    dist.all_gather_object(out, obj)
+    return out
+
+
 def sum_over_ranks(dist, value: float) -> float:
     import torch
     t = torch.tensor([value], dtype=torch.float64)
@@ -236,6 +243,63 @@ def cpu_baseline_poisson(m: int, iters: int = 3) -> dict:
     }
 
 
+# The phases that tile an iteration on the compute stream (cgx.h CGX_PH_*):
+# their medians add up to about the iteration time.
+TILING_PHASES = ("matvec_own", "gather_exposed", "matvec", "combine_pap", "update_r", "combine_rr", "update_xp", "gap")
+
+
+def phase_summary(all_ph: list, ms_per_step: float) -> dict:
+    """Per-rank medians (us) of each phase over the timed iterations, the max
+    over ranks, and how the tiling phases add up against ms_per_step."""
+    per_rank = [{k: round(v["median_us"], 2) for k, v in ph.items()} for ph in all_ph]
+    sums = [sum(r[k] for k in TILING_PHASES) for r in per_rank]
+    # means tile exactly (the phases are consecutive intervals), medians nearly
+    mean_sums = [sum(ph[k]["mean_us"] for k in TILING_PHASES) for ph in all_ph]
+    return {
+        "what": "median over the timed iterations, per rank, of each phase of the rank's compute stream, from "
+                "start / end stamps its kernels take on the device clock (CGX_PHASES: nothing inserted between "
+                "kernels): a kernel's own span, or the span between two consecutive kernels (the exchange "
+                "enqueued there, or a launch gap); matvec_own + gather_exposed + matvec + combine_pap + update_r "
+                "+ combine_rr + update_xp + gap tile an iteration (parallel_cg.c:288-323)",
+        "iterations_sampled": int(all_ph[0]["iteration"]["samples"]),
+        "per_rank": per_rank,
+        "max_over_ranks": {k: max(r[k] for r in per_rank) for k in per_rank[0]},
+        "tiling_sum_ms_per_rank": [round(x / 1e3, 4) for x in sums],
+        "tiling_sum_over_ms_per_step": max(sums) / 1e3 / ms_per_step,
+        "tiling_mean_sum_over_ms_per_step": max(mean_sums) / 1e3 / ms_per_step,
+    }
+
+
+def rccl_summary(all_comm: list, solver_device: int) -> dict:
+    """Did RCCL see N ranks on N devices, and what links join them: every
+    rank's communicator view and PCI bus id, and the HIP link type / hops /
+    peer access from rank 0's device to each other rank's device."""
+    import conjugate_gradient_amd as cg
+    visible = {}
+    for d in range(cg.device_count()):
+        try:
+            visible[cg.device_pci_bus_id(d).lower()] = d
+        except cg.CgxError:
+            pass
+    links = []
+    for r, ci in enumerate(all_comm[1:], start=1):
+        d = visible.get(ci["pci_bus_id"].lower())
+        if d is None:
+            links.append({"to_rank": r, "link": "device not visible to rank 0"})
+        elif d == solver_device:
+            links.append({"to_rank": r, "link": "same device"})
+        else:
+            links.append({"to_rank": r, **cg.device_link(solver_device, d)})
+    return {
+        "nranks": all_comm[0]["rccl_nranks"],
+        "distinct_devices": len({ci["pci_bus_id"].lower() for ci in all_comm}),
+        "pci_bus_ids": [ci["pci_bus_id"] for ci in all_comm],
+        "ranks": all_comm,
+        "links_from_rank0": links,
+        "nccl_env": {k: v for k, v in sorted(os.environ.items()) if k.startswith(("NCCL_", "RCCL_"))},
+    }
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
@@ -264,6 +328,11 @@ def main(argv=None) -> int:
                     help="stream workload: keep this many GB of each GPU's rows of A in HBM and stream only the "
                          "rest (CGX_STREAM_RESIDENT_MB; an out-of-core matrix keeps what fits). Default 0: all "
                          "of A streams every matVec, as configs[3] states")
+    ap.add_argument("--phases", choices=["auto", "on", "off"], default="auto",
+                    help="the iteration's kernels stamp their start / end on the device clock (CGX_PHASES; "
+                         "nothing is inserted between kernels, overhead within run-to-run noise, "
+                         "profiles/r03_phases_ab.jsonl) and the line reports per-phase medians per rank; "
+                         "auto: on for the dense resident workloads")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-n", type=int, default=None, help="N for the CPU baseline (default: --n)")
     args = ap.parse_args(argv)
@@ -287,6 +356,9 @@ def main(argv=None) -> int:
     flags = cg.CGX_F64 | cg.CGX_TIMING | (cg.CGX_HOST_STREAM if stream else 0) | (cg.CGX_SYMMETRIC if symmetric else 0)
     flags |= {"collective": 0, "p2p": cg.CGX_COMM_P2P, "nooverlap": cg.CGX_NO_OVERLAP,
               "deterministic": cg.CGX_DETERMINISTIC}[args.comm]
+    phases = args.phases != "off" and not (poisson or stream or symmetric)
+    if phases:
+        flags |= cg.CGX_PHASES
     if stream and args.resident_gb > 0:
         os.environ["CGX_STREAM_RESIDENT_MB"] = str(int(args.resident_gb * 1024))
     if use_dist:
@@ -341,6 +413,13 @@ def main(argv=None) -> int:
         mv_ms_max = max_over_ranks(dist, mv_ms)
     else:
         mv_ms_max = mv_ms
+
+    # after the timed region: what each phase of an iteration cost (the
+    # events recorded inside it are resolved only now), and what RCCL ran on
+    ph = solver.phase_times() if phases else None
+    comm = solver.comm_info() if (use_dist and world > 1) else None
+    all_ph = gather_objects(dist, ph) if (dist and phases) else ([ph] if phases else None)
+    all_comm = gather_objects(dist, comm) if comm is not None else None
 
     # correctness after the timed region (not timed): true residual of x
     rnorm, bnorm = solver.residual_norm()
@@ -440,6 +519,10 @@ def main(argv=None) -> int:
         # p_k, x, r -> x, r), 80 B/point for the stencil / r / x,p split
         "iteration_gbps": ((64.0 if fused else 80.0) * n / (elapsed / args.steps) / 1e9) if poisson else None,
     }
+    if all_ph is not None:
+        out["phases_us"] = phase_summary(all_ph, elapsed / args.steps * 1e3)
+    if all_comm is not None:
+        out["rccl"] = rccl_summary(all_comm, solver_device=local_rank % max(1, cg.device_count()))
     if world == 1 and not args.no_cpu and poisson:
         out["cpu_baseline"] = cpu_baseline_poisson(m)
     elif world == 1 and not args.no_cpu and not stream and not symmetric:

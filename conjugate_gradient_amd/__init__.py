@@ -31,7 +31,9 @@ import subprocess
 import numpy as np
 
 __all__ = [
-    "CGX_F64", "CGX_F32_REF", "CGX_TIMING", "CGX_HOST_STREAM", "CGX_NO_OVERLAP", "CGX_COMM_P2P", "CGX_SYMMETRIC", "CgxError", "Stats", "Solver", "lib", "build",
+    "CGX_F64", "CGX_F32_REF", "CGX_TIMING", "CGX_HOST_STREAM", "CGX_NO_OVERLAP", "CGX_COMM_P2P", "CGX_SYMMETRIC",
+    "CGX_PHASES", "CGX_PEER_ACTIVE", "PHASE_NAMES", "CgxError", "Stats", "Solver", "lib", "build",
+    "device_pci_bus_id", "device_link",
     "conjugrad", "matVec", "vecVec", "residual", "update_xr", "update_p", "read_text",
     "count_text", "read_dims", "device_count", "get_unique_id", "DeviceArray",
 ]
@@ -46,6 +48,12 @@ CGX_FUSED_ACTIVE = 0x2000
 CGX_DETERMINISTIC = 0x4000
 CGX_COMM_P2P = 0x1000
 CGX_SYMMETRIC = 0x8000
+CGX_PHASES = 0x10000
+CGX_PEER_ACTIVE = 0x20000
+
+# cgx_phase_times indices (include/cgx.h), in the order the phases tile an iteration
+PHASE_NAMES = ("matvec_own", "gather_exposed", "matvec", "combine_pap", "update_r", "combine_rr", "update_xp",
+               "gap", "iteration")
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libcgx.so")
@@ -82,6 +90,16 @@ class Info(ctypes.Structure):
     ]
 
 
+class PhaseTimes(ctypes.Structure):
+    _fields_ = [("samples", ctypes.c_int64 * 9), ("median_us", ctypes.c_double * 9),
+                ("mean_us", ctypes.c_double * 9)]
+
+
+class CommInfo(ctypes.Structure):
+    _fields_ = [("rccl_nranks", ctypes.c_int), ("rccl_device", ctypes.c_int), ("rccl_rank", ctypes.c_int),
+                ("device", ctypes.c_int), ("pci_bus_id", ctypes.c_char * 32)]
+
+
 class UniqueId(ctypes.Structure):
     _fields_ = [("bytes", ctypes.c_char * 128)]
 
@@ -107,6 +125,11 @@ def lib() -> ctypes.CDLL:
         "cgx_last_error": ([], ctypes.c_char_p),
         "cgx_version": ([], i32),
         "cgx_device_count": ([ctypes.POINTER(i32)], i32),
+        "cgx_hip_last_error": ([], i32),
+        "cgx_device_pci_bus_id": ([i32, ctypes.c_char_p, i32], i32),
+        "cgx_device_link": ([i32, i32, ctypes.POINTER(i32), ctypes.POINTER(i32), ctypes.POINTER(i32)], i32),
+        "cgx_get_comm_info": ([vp, ctypes.POINTER(CommInfo)], i32),
+        "cgx_get_phase_times": ([vp, ctypes.POINTER(PhaseTimes)], i32),
         "cgx_create": ([pctx, i64, i32, i32], i32),
         "cgx_create_multi": ([pctx, i64, i32, ctypes.POINTER(i32), i32], i32),
         "cgx_get_unique_id": ([ctypes.POINTER(UniqueId)], i32),
@@ -175,6 +198,22 @@ def device_count() -> int:
     n = ctypes.c_int(0)
     _check(lib().cgx_device_count(ctypes.byref(n)), "cgx_device_count")
     return n.value
+
+
+def device_pci_bus_id(device: int) -> str:
+    buf = ctypes.create_string_buffer(32)
+    _check(lib().cgx_device_pci_bus_id(device, buf, 32), "cgx_device_pci_bus_id")
+    return buf.value.decode()
+
+
+def device_link(a: int, b: int) -> dict:
+    """The link between two visible devices: HSA link type (4 = xGMI, 2 = PCIe,
+    -1 unknown), hop count, and whether a can access b's memory directly."""
+    lt, hops, peer = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    _check(lib().cgx_device_link(a, b, ctypes.byref(lt), ctypes.byref(hops), ctypes.byref(peer)), "cgx_device_link")
+    names = {0: "hypertransport", 1: "qpi", 2: "pcie", 3: "infiniband", 4: "xgmi"}
+    return {"link": names.get(lt.value, "unknown" if lt.value < 0 else str(lt.value)), "hops": hops.value,
+            "peer_access": bool(peer.value)}
 
 
 def get_unique_id() -> bytes:
@@ -478,6 +517,20 @@ class Solver:
         v = [ctypes.c_int() for _ in range(4)]
         _check(lib().cgx_get_matvec_plan(self._h, *(ctypes.byref(x) for x in v)), "cgx_get_matvec_plan")
         return dict(zip(("R", "U", "nt", "blocks"), (x.value for x in v)))
+
+    def phase_times(self) -> dict:
+        """CGX_PHASES: {phase: {"median_us", "mean_us", "samples"}} since the last reset_timing()."""
+        t = PhaseTimes()
+        _check(lib().cgx_get_phase_times(self._h, ctypes.byref(t)), "cgx_get_phase_times")
+        return {name: {"median_us": t.median_us[i], "mean_us": t.mean_us[i], "samples": int(t.samples[i])}
+                for i, name in enumerate(PHASE_NAMES)}
+
+    def comm_info(self) -> dict:
+        """What the exchange runs on: RCCL's rank count / device / rank (rank mode) and the PCI bus id."""
+        ci = CommInfo()
+        _check(lib().cgx_get_comm_info(self._h, ctypes.byref(ci)), "cgx_get_comm_info")
+        return {"rccl_nranks": ci.rccl_nranks, "rccl_device": ci.rccl_device, "rccl_rank": ci.rccl_rank,
+                "device": ci.device, "pci_bus_id": ci.pci_bus_id.decode()}
 
     def reset_timing(self) -> None:
         _check(lib().cgx_reset_timing(self._h), "cgx_reset_timing")

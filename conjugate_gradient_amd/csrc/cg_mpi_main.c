@@ -11,7 +11,11 @@
  *   - MPI_Bcast(x0) + MPI_Scatter(A, b) (:109-115) -> cgx_set_rows with the
  *     rank's rows (the full x0 for the first A x0 is allgathered on the GPUs);
  *   - conjugrad's MPI_Allgather / MPI_Allreduce (:283-323) -> cgx_solve.
- * Same output lines from rank 0 (:334, :123-126); with --fp32-ref the x is
+ * Same output lines from rank 0 (:334, :123-126), the CG time bracketed by
+ * barriers on every rank as conjugrad does (:278-279, :328-329); with --p2p
+ * point-to-point_cg.c's contract instead: its lines (:493, :133-135, the
+ * distribution bracket taking in the reads of A and b as scatterRow's does,
+ * :119-127) and its error texts (:101, :226).  With --fp32-ref the x is
  * parallel_cg.c's (point-to-point_cg.c's with --p2p) bit for bit.
  *
  *   mpiexec -np P cg_mpi [--fp32-ref] [--p2p] [--eps E] [--max-iter M]
@@ -76,6 +80,33 @@ static int read_values(const char *path, int64_t first, int64_t count, int as_fl
     return rc;
 }
 
+/* A read failure on any rank stops every rank (the reference reads on rank
+ * 0 only and, on a missing file, prints and goes on with whatever memory
+ * holds; here every rank exits non-zero).  Rank 0 prints the reference's
+ * message for the first file that failed: initialize()'s "Could not open
+ * file" (parallel_cg.c:166, and x0 in point-to-point_cg.c:176), scatterRow's
+ * "Could not open %s file. " for A and b in point-to-point_cg.c (:226). */
+static int input_failed(int rank, int p2p, const char *const *pos, const int rc[3]) {
+    int worst[3] = {0, 0, 0};
+    MPI_Allreduce((void *)rc, worst, 3, MPI_INT, MPI_MIN, MPI_COMM_WORLD);
+    int f = -1;
+    for (int q = 0; q < 3 && f < 0; ++q) {
+        const int order = q == 0 ? 2 : q - 1; /* x0 is read first, then A, then b */
+        if (worst[order] != 0) f = order;
+    }
+    if (f < 0) return 0;
+    if (rc[f] != 0 && rc[f] != -1)
+        fprintf(stderr, "rank %d: %s: %s\n", rank, pos[f],
+                rc[f] == -2 ? "holds fewer numbers than the system needs"
+                            : rc[f] == -4 ? "can't allocate memory" : "malformed number");
+    if (rank == 0 && worst[f] == -1) {
+        if (p2p && f < 2) printf("Could not open %s file. \n", pos[f]);
+        else printf("Could not open file\n");
+        fflush(stdout);
+    }
+    return 1;
+}
+
 int main(int argc, char **argv) {
     const double t_prog0 = now_s();
     if (MPI_Init(&argc, &argv) != MPI_SUCCESS) {
@@ -137,7 +168,8 @@ int main(int argc, char **argv) {
         }
         if (n == 0) fprintf(stderr, "empty system\n");
         if (n > 0 && n % nranks != 0) {
-            printf("%lld is not divisible by %d\n", n, nranks); /* parallel_cg.c:88 */
+            if (p2p) printf("%lld must be divisible by %d\n", n, nranks); /* point-to-point_cg.c:101 */
+            else printf("%lld is not divisible by %d\n", n, nranks);      /* parallel_cg.c:88 */
             n = -1;
         }
         if (n > 0) printf("Computing cg of matrix size : %lld\n", n * n); /* :101 */
@@ -149,21 +181,27 @@ int main(int argc, char **argv) {
         return 1;
     }
     const int64_t nloc = n / nranks, row0 = (int64_t)rank * nloc;
+    double t_dist0 = 0.0;
     const size_t es = fp32ref ? 4 : 8;
 
-    /* every rank parses its own rows of A, b and x0 */
+    /* every rank parses its own rows of A, b and x0: x0 first (rank 0's
+     * initialize() before the distribution, both programs), A and b where the
+     * program reads them -- before the distribution bracket in parallel_cg.c
+     * (:104-106), inside it in point-to-point_cg.c (scatterRow reads the file
+     * while it sends, :119-127, :183-235) */
     void *A = malloc((size_t)nloc * (size_t)n * es), *b = malloc((size_t)nloc * es), *x = malloc((size_t)n * es);
-    int rc = (A && b && x) ? 0 : -4;
-    if (!rc) rc = read_values(pos[0], row0 * n, nloc * n, fp32ref, A, threads);
-    if (!rc) rc = read_values(pos[1], row0, nloc, fp32ref, b, threads);
-    if (!rc) rc = read_values(pos[2], row0, nloc, fp32ref, (char *)x + (size_t)row0 * es, 1);
-    int worst = rc;
-    MPI_Allreduce(&rc, &worst, 1, MPI_INT, MPI_MIN, MPI_COMM_WORLD);
-    if (worst != 0) {
-        if (rc != 0)
-            fprintf(stderr, "rank %d: %s\n", rank,
-                    rc == -1 ? "Could not open file" : rc == -2 ? "a file holds fewer numbers than the system needs"
-                             : rc == -4 ? "can't allocate memory" : "malformed number");
+    int rc[3] = {0, 0, 0};
+    if (!(A && b && x)) rc[0] = rc[1] = rc[2] = -4;
+    if (!rc[2]) rc[2] = read_values(pos[2], row0, nloc, fp32ref, (char *)x + (size_t)row0 * es, 1);
+    if (!p2p && !rc[0]) rc[0] = read_values(pos[0], row0 * n, nloc * n, fp32ref, A, threads);
+    if (!p2p && !rc[1]) rc[1] = read_values(pos[1], row0, nloc, fp32ref, b, threads);
+    if (p2p) {
+        MPI_Barrier(MPI_COMM_WORLD); /* point-to-point_cg.c:119-120: the bracket opens before the reads */
+        t_dist0 = MPI_Wtime();
+        if (!rc[0]) rc[0] = read_values(pos[0], row0 * n, nloc * n, fp32ref, A, threads);
+        if (!rc[1]) rc[1] = read_values(pos[1], row0, nloc, fp32ref, b, threads);
+    }
+    if (input_failed(rank, p2p, pos, rc)) {
         MPI_Finalize();
         return 1;
     }
@@ -186,32 +224,48 @@ int main(int argc, char **argv) {
     const int dev = de ? atoi(de) : (ndev > 0 ? local_rank % ndev : 0);
     const int flags = (fp32ref ? CGX_F32_REF : CGX_F64) | (p2p ? CGX_COMM_P2P : 0);
     cgx_ctx *ctx = NULL;
-    rc = cgx_create_rank(&ctx, n, rank, nranks, &id, dev, flags);
-    if (rc != CGX_OK) {
-        fprintf(stderr, "rank %d: cgx_create_rank: %s (%s)\n", rank, cgx_strerror(rc), cgx_last_error());
+    const int crc = cgx_create_rank(&ctx, n, rank, nranks, &id, dev, flags);
+    if (crc != CGX_OK) {
+        fprintf(stderr, "rank %d: cgx_create_rank: %s (%s)\n", rank, cgx_strerror(crc), cgx_last_error());
         MPI_Abort(MPI_COMM_WORLD, 1); /* as parallel_cg.c stops the job */
     }
 
-    /* the scatter of A and b and the broadcast of x0 (parallel_cg.c:109-115) */
-    MPI_Barrier(MPI_COMM_WORLD);
-    const double t_dist0 = MPI_Wtime();
-    rc = cgx_set_rows(ctx, row0, nloc, A, n, b, (char *)x + (size_t)row0 * es);
+    /* the scatter of A and b and the broadcast of x0: parallel_cg.c:109-117
+     * (MPI_Bcast + MPI_Scatter between two barriers), point-to-point_cg.c:119-127
+     * (BcastVector + scatterRow, the reads above included) */
+    if (!p2p) {
+        MPI_Barrier(MPI_COMM_WORLD);
+        t_dist0 = MPI_Wtime();
+    }
+    int src = cgx_set_rows(ctx, row0, nloc, A, n, b, (char *)x + (size_t)row0 * es);
     MPI_Barrier(MPI_COMM_WORLD);
     const double t_dist1 = MPI_Wtime();
     free(A);
     free(b);
     cgx_stats st;
     memset(&st, 0, sizeof st);
-    if (rc == CGX_OK) rc = cgx_solve(ctx, NULL, eps, max_iter, &st);
-    if (rc == CGX_OK) rc = cgx_get_x(ctx, x); /* the full x on every rank, as the reference leaves it */
-    if (rc != CGX_OK) {
-        fprintf(stderr, "rank %d: %s (%s)\n", rank, cgx_strerror(rc), cgx_last_error());
+    /* conjugrad's own bracket: MPI_Barrier + MPI_Wtime on every rank before
+     * and after the loop (parallel_cg.c:278-279,328-329; point-to-point_cg.c
+     * :435-436,488-489), rank 0 prints the difference */
+    MPI_Barrier(MPI_COMM_WORLD);
+    const double t_cg0 = MPI_Wtime();
+    if (src == CGX_OK) src = cgx_solve(ctx, NULL, eps, max_iter, &st);
+    if (src != CGX_OK) {
+        fprintf(stderr, "rank %d: %s (%s)\n", rank, cgx_strerror(src), cgx_last_error());
+        MPI_Abort(MPI_COMM_WORLD, 1);
+    }
+    MPI_Barrier(MPI_COMM_WORLD);
+    const double t_cg1 = MPI_Wtime();
+    src = cgx_get_x(ctx, x); /* the full x on every rank, as the reference leaves it */
+    if (src != CGX_OK) {
+        fprintf(stderr, "rank %d: %s (%s)\n", rank, cgx_strerror(src), cgx_last_error());
         MPI_Abort(MPI_COMM_WORLD, 1);
     }
     if (rank == 0) {
-        printf("cg method execution time in seconds: %f\n", st.solve_ms / 1e3);               /* :334 */
-        printf("collective data distribution time in seconds: %f\n", t_dist1 - t_dist0);    /* :123 */
-        printf("clock execution time in seconds: %f\n", now_s() - t_prog0);                  /* :125 */
+        printf("cg method execution time in seconds: %f\n", t_cg1 - t_cg0); /* parallel_cg.c:334, p2p :493 */
+        if (p2p) printf("p2p data distribution time in seconds: %f\n", t_dist1 - t_dist0);   /* p2p :133-134 */
+        else printf("collective data distribution time in seconds: %f\n", t_dist1 - t_dist0); /* :123-124 */
+        printf("clock execution time in seconds: %f\n", now_s() - t_prog0);    /* parallel_cg.c:125, p2p :135 */
         if (stats)
             printf("iterations: %lld converged: %d residual_norm: %.6e\n", (long long)st.iterations, st.converged,
                    st.rr >= 0 ? sqrt(st.rr) : -1.0);

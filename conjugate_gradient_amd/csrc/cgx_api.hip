@@ -89,6 +89,35 @@ int cgx_device_count(int *count) {
     return CGX_OK;
 }
 
+int cgx_hip_last_error(void) { return (int)hipPeekAtLastError(); }
+
+int cgx_device_pci_bus_id(int device, char *buf, int len) {
+    if (!buf || len < 13) return fail(CGX_ERR_ARG, "buf is NULL or shorter than 13 bytes");
+    HIPT(hipDeviceGetPCIBusId(buf, len, device));
+    return CGX_OK;
+}
+
+int cgx_device_link(int device_a, int device_b, int *link_type, int *hops, int *peer) {
+    int n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n <= 0) return fail(CGX_ERR_NODEV, "no HIP device visible");
+    if (device_a < 0 || device_a >= n || device_b < 0 || device_b >= n)
+        return fail(CGX_ERR_ARG, "devices %d, %d: %d visible", device_a, device_b, n);
+    if (link_type) *link_type = -1;
+    if (hops) *hops = -1;
+    if (peer) *peer = 0;
+    if (device_a == device_b) return CGX_OK;
+    uint32_t lt = 0, hc = 0;
+    if (hipExtGetLinkTypeAndHopCount(device_a, device_b, &lt, &hc) == hipSuccess) {
+        if (link_type) *link_type = (int)lt;
+        if (hops) *hops = (int)hc;
+    }
+    (void)hipGetLastError();  // a device pair HIP cannot describe is not an error of the caller's next call
+    int can = 0;
+    HIPT(hipDeviceCanAccessPeer(&can, device_a, device_b));
+    if (peer) *peer = can;
+    return CGX_OK;
+}
+
 // ---- kernel-level entry points ---------------------------------------------------------
 int cgx_dev_malloc(void **ptr, size_t bytes) {
     if (!ptr) return fail(CGX_ERR_ARG, "ptr is NULL");

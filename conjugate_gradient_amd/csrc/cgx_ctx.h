@@ -79,6 +79,10 @@ struct RcclApi {
     // fail-fast: asynchronous error query, abort
     decltype(&::ncclCommGetAsyncError) CommGetAsyncError = nullptr;
     decltype(&::ncclCommAbort) CommAbort = nullptr;
+    // what the communicator reports about itself (cgx_get_comm_info)
+    decltype(&::ncclCommCount) CommCount = nullptr;
+    decltype(&::ncclCommCuDevice) CommCuDevice = nullptr;
+    decltype(&::ncclCommUserRank) CommUserRank = nullptr;
 };
 extern RcclApi g_rccl;
 // Loads librccl.so.1 once; false (with cgx_last_error set) if it cannot.
@@ -99,6 +103,9 @@ bool rccl_load();
 #define ncclGroupEnd (cgxh::g_rccl.GroupEnd)
 #define ncclCommGetAsyncError (cgxh::g_rccl.CommGetAsyncError)
 #define ncclCommAbort (cgxh::g_rccl.CommAbort)
+#define ncclCommCount (cgxh::g_rccl.CommCount)
+#define ncclCommCuDevice (cgxh::g_rccl.CommCuDevice)
+#define ncclCommUserRank (cgxh::g_rccl.CommUserRank)
 #endif
 
 #define HIPT(expr)                                                                              \
@@ -150,6 +157,10 @@ enum Op { OP_DENSE = 0, OP_POISSON = 1 };
 enum State { ST_IDLE = 0, ST_BEGUN = 1, ST_CONVERGED = 2 };
 
 constexpr int kEvPairs = 256;
+// CGX_PHASES: the kernels of an iteration that stamp their start / end
+// (cgx_kernels.h kTsSlot), in the order they run on the first shard's stream.
+enum TsKernel { TK_OWN = 0, TK_MV = 1, TK_UR = 2, TK_UXP = 3, kTsKern = 4 };
+constexpr int kTsIters = 256;  // iterations stamped before a resolve (256 x 4 x 16 KiB)
 constexpr size_t kXStageMax = 64u << 20;
 constexpr int kStreamBufs = 3;
 constexpr int kMaxCopyStreams = 4;
@@ -206,6 +217,13 @@ struct Shard {
     bool res_dirty = false;
     MatvecPlan res_plan;
     hipEvent_t ev_look[8] = {};  // lagged convergence checks (kLookRing)
+    hipEvent_t ev_prog[8] = {};  // rank mode, host-checked iterations: one per iteration (fail-fast progress)
+    int prog_next = 0;
+    // CGX_PHASES (shard 0): kTsIters x kTsKern timestamp slots on the device,
+    // zero where no kernel stamped; ts_cur = the ring row of the iteration
+    // being enqueued (-1 between iterations), ts_used = rows since the resolve
+    int64_t *ts_dev = nullptr;
+    int ts_used = 0, ts_cur = -1;
     // overlap of the p exchange with the own-column-block matVec
     hipStream_t cstream = nullptr;
     hipEvent_t ev_pready = nullptr, ev_gathered = nullptr;
@@ -248,6 +266,13 @@ struct cgx_ctx {
     char dead_why[400] = "";
     const char *last_coll = "none";  // the last exchange enqueued, and its iteration
     int64_t last_coll_k = -1;
+    bool peer = false;  // multi-shard over distinct devices: peer access enabled between every pair
+    // CGX_PHASES: resolved per-iteration phase durations (us), cgx_phase_times' order;
+    // the wall clock's rate, and the previous stamped iteration's first start /
+    // last end (ticks; 0 = none) so the gap across a resolve is still measured
+    std::vector<float> ph_samples[CGX_PH_COUNT];
+    double ts_khz = 100000.0;
+    int64_t ts_prev_start = 0, ts_prev_end = 0;
 };
 
 namespace cgxh {
@@ -288,6 +313,11 @@ int alloc_overlap(cgx_ctx *c);
 int finish_create(cgx_ctx *c, cgx_ctx **out);
 // cgx_exchange.hip
 int timing_resolve(cgx_ctx *c);
+int phase_iter_begin(cgx_ctx *c);
+int64_t *ts_of(cgx_ctx *c, const Shard &s, int kern);
+void phase_iter_end(cgx_ctx *c);
+int phase_resolve(cgx_ctx *c);
+int progress_mark(cgx_ctx *c);
 int local_barrier(cgx_ctx *c);
 int exchange_halo(cgx_ctx *c, bool from_x);
 int exchange_halo_of(cgx_ctx *c, char *Shard::*slab);
@@ -307,7 +337,7 @@ int rank_wait_stream(cgx_ctx *c, hipStream_t st, const char *what);
 double rccl_timeout_from_env();
 // cgx_iterate.hip
 int matvec_rows(cgx_ctx *c, Shard &s, const MatvecPlan &pl, const char *Arows, int64_t r0, int64_t rows,
-                const char *vec, bool fuse_dot, int dot_slot, bool gated = false);
+                const char *vec, bool fuse_dot, int dot_slot, bool gated = false, int64_t *ts = nullptr);
 int matvec_streamed(cgx_ctx *c, Shard &s, const char *vec);
 int matvec_sym_streamed(cgx_ctx *c, Shard &s, const char *vec, bool with_dot, int dot_slot, const int64_t *gate);
 int launch_matvec(cgx_ctx *c, Shard &s, const char *vec, bool with_dot, int dot_slot, bool gated = false);

@@ -16,13 +16,22 @@ typedef double d2 __attribute__((ext_vector_type(2)));
 constexpr int kNT = 256;  // threads per block for the fp64 kernels
 
 // CG's alpha = r.r / p.Ap and beta = r.r_new / r.r_old, fp64.  A zero
-// denominator means the iteration has converged exactly (r = 0, or r.r has
-// underflowed: fixed-count runs go on long past convergence): that is CG's
-// "lucky breakdown", and the ratio is 0, so x stays at the solution and r, p
-// stay 0 instead of turning into 0/0 = NaN.  Any other denominator gives the
-// plain quotient, bit for bit.  (CGX_F32_REF keeps the reference's float
-// division as it is, NaN included: serialConjugate.c:220,239.)
-__device__ __forceinline__ double cg_ratio(double num, double den) { return den != 0.0 ? num / den : 0.0; }
+// denominator under a numerator that has underflowed too (|num| below the
+// smallest normal double, 0 included) means the iteration has converged
+// exactly -- r = 0, or, in a fixed-count run that goes on long past
+// convergence, r.r and p.Ap have sunk into the subnormals, where their
+// rounding is noise: that is CG's "lucky breakdown", and the ratio is 0, so x
+// stays at the solution and r, p stay 0 instead of turning into NaN.  Every
+// other pair gives the plain quotient, bit for bit -- in particular a normal
+// r.r over p.Ap = 0 (an A that is not positive definite), which is a real
+// breakdown and shows up as Inf / NaN exactly as the reference's division
+// would (test_indefinite_breakdown_is_not_hidden).  (An SPD A keeps p.Ap >=
+// lambda_min |p|^2 ~ lambda_min r.r, nonzero while r.r is normal.)
+// CGX_F32_REF keeps the reference's float division as it is
+// (serialConjugate.c:220,239).
+__device__ __forceinline__ double cg_ratio(double num, double den) {
+    return (den != 0.0 || !(__builtin_fabs(num) < 0x1p-1022)) ? num / den : 0.0;
+}
 
 __device__ __forceinline__ double wave_sum(double v) {
 #pragma unroll
@@ -34,13 +43,26 @@ __device__ __forceinline__ double wave_sum(double v) {
 // partials[blockIdx.x]; the last block to arrive sums the partials in index
 // order and writes *out.  Deterministic for a fixed grid.
 //
-// Hand-off (cdna_hip_programming.md Guideline 16, the write-through form):
-// the partial is stored write-through (8-B agent-scope atomic store = sc1),
-// the storing lane drains it (s_waitcnt vmcnt(0)) before its relaxed
-// agent-scope ticket add, and the block whose add returns gridDim-1 reads
-// every partial with sc1 loads (agent-scope atomic loads) -- no release /
-// acquire fence, so no per-block write-back of the L2's dirty lines (which
-// cost the r-update ~35 % of its time with a buffer_wbl2 per block).
+// Hand-off (kHandoffNote; cdna_hip_programming.md Guideline 16, Recipe R1,
+// the write-through form): the partial is stored write-through (8-B
+// agent-scope atomic store = sc1), the storing lane drains it (s_waitcnt
+// vmcnt(0)) before its relaxed agent-scope ticket add, and the block whose
+// add returns gridDim-1 reads every partial with sc1 loads (agent-scope
+// atomic loads).
+//
+// kHandoffNote -- why the producer has no release.  In the C++/HIP memory
+// model a relaxed store followed by a relaxed RMW publishes nothing; what
+// makes this hand-off correct is gfx950's implementation, which the guide's
+// Recipe R1 states as the rule: a payload stored write-through (sc1: past
+// this XCD's L2 to the coherence point) and drained by EVERY storing wave
+// before the signal "needs no release fence", and a consumer whose every load
+// of the payload is an sc1 load needs no L1 invalidate.  Here the payload is
+// the partial (an agent-scope atomic store) or, in k_update_xrp_f64 and the
+// F32_REF matVec + vecVec, r / Ap stored with 16-B sc1 buffer stores by every
+// wave, each wave draining (vmcnt(0)) before the block barrier that precedes
+// the ticket.  An agent-scope release on the ticket would add a buffer_wbl2
+// (write-back of the whole L2's dirty lines) per block: measured 378 vs 283 us
+// on a 537 MB k_update_r (round 1), for no change in what the consumer reads.
 __device__ __forceinline__ void grid_sum_last_block(double v, double *partials, unsigned *ticket,
                                                     double *out, bool add_to_out = false) {
     __shared__ double red[kNT / 64];
@@ -76,9 +98,10 @@ __device__ __forceinline__ void grid_sum_last_block(double v, double *partials, 
     __syncthreads();
     if (!is_last) return;
     // Order the partial loads below after the ticket (acquire at agent scope,
-    // once per kernel in this one block).  The sc1 stores and loads already
-    // make the hand-off correct on gfx950; the fence makes it so under the
-    // HIP memory model as well, and keeps the compiler from hoisting the loads.
+    // once per kernel in this one block; it also keeps the compiler from
+    // hoisting the loads).  The producer side has no release: see
+    // kHandoffNote below for why the hand-off is correct on gfx950 and what a
+    // release would cost.
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
     // all of this thread's partials in flight at once (grid <= 8192 = 32 * kNT)
     double s = 0.0;
@@ -171,6 +194,18 @@ __device__ __forceinline__ bool grid_sum_keep_last(double v, double *partials, u
     __syncthreads();
     total = tot;
     return true;
+}
+
+// CGX_PHASES timestamps (cgx_kernels.h kTsSlot): ts_start after a kernel's
+// gate, ts_end at every block-uniform exit reached by all of the block's
+// threads (one extra barrier, then lane 0 of the block stores its exit time).
+__device__ __forceinline__ void ts_start(int64_t *ts) {
+    if (ts && blockIdx.x == 0 && threadIdx.x == 0) ts[0] = wall_clock64();
+}
+__device__ __forceinline__ void ts_end(int64_t *ts) {
+    if (!ts) return;
+    __syncthreads();
+    if (threadIdx.x == 0 && blockIdx.x < (unsigned)kTsMaxBlocks) ts[1 + blockIdx.x] = wall_clock64();
 }
 
 __device__ __forceinline__ d2 ld2(const double *p) { return *reinterpret_cast<const d2 *>(p); }

@@ -36,6 +36,98 @@ int timing_resolve(cgx_ctx *c) {
     return CGX_OK;
 }
 
+// ---- CGX_PHASES ------------------------------------------------------------------
+// The iteration's kernels on the first shard stamp their start and end on the
+// device's constant wall clock (cgx_kernels.h kTsSlot); nothing is inserted
+// between them, so what is measured is the timeline that runs without
+// CGX_PHASES.  (HIP events were tried first: each one put 3.3 us onto the
+// stream, 4.4 us with its default system-scope release -- 5-7 % of an 8-GPU
+// iteration.)  The stamps are turned into phase durations after the fact
+// (phase_resolve): a kernel's own time, and the time between consecutive
+// kernels, which is the exchange enqueued between them (RCCL's allgather /
+// allreduce kernels, or the device copies) or the launch gap.
+int phase_iter_begin(cgx_ctx *c) {
+    if (!(c->flags & CGX_PHASES)) return CGX_OK;
+    Shard &s = c->sh[0];
+    if (s.ts_used >= kTsIters) TRY(phase_resolve(c));
+    s.ts_cur = s.ts_used;
+    return CGX_OK;
+}
+
+int64_t *ts_of(cgx_ctx *c, const Shard &s, int kern) {
+    if (!(c->flags & CGX_PHASES) || &s != &c->sh[0] || s.ts_cur < 0) return nullptr;
+    return s.ts_dev + ((size_t)s.ts_cur * kTsKern + kern) * kTsSlot;
+}
+
+void phase_iter_end(cgx_ctx *c) {
+    if (!(c->flags & CGX_PHASES)) return;
+    Shard &s = c->sh[0];
+    if (s.ts_cur >= 0) s.ts_used = s.ts_cur + 1;
+    s.ts_cur = -1;
+}
+
+int phase_resolve(cgx_ctx *c) {
+    if (c->sh.empty() || !(c->flags & CGX_PHASES)) return CGX_OK;
+    Shard &s = c->sh[0];
+    if (s.ts_used == 0) return CGX_OK;
+    TRY(set_dev(s));
+    const size_t words = (size_t)s.ts_used * kTsKern * kTsSlot;
+    std::vector<int64_t> h(words);
+    HIPT(hipMemcpyAsync(h.data(), s.ts_dev, words * 8, hipMemcpyDeviceToHost, s.stream));
+    TRY(rank_wait_stream(c, s.stream, "the phase timestamps"));
+    HIPT(hipMemsetAsync(s.ts_dev, 0, words * 8, s.stream));
+    s.ts_used = 0;
+    const double us_per_tick = 1e3 / c->ts_khz;
+    auto add = [&](int seg, int64_t t0, int64_t t1) { c->ph_samples[seg].push_back((float)((t1 - t0) * us_per_tick)); };
+    // the phase between two consecutive kernels of an iteration (by slot)
+    auto between = [](int a, int b) {
+        if (a == TK_OWN) return CGX_PH_GATHER_EXPOSED;  // own block done, waiting for p
+        if (a == TK_MV) return CGX_PH_COMBINE_PAP;      // (two-launch form: the kernel boundary)
+        return CGX_PH_COMBINE_RR;
+    };
+    const int kern_seg[kTsKern] = {CGX_PH_MATVEC_OWN, CGX_PH_MATVEC, CGX_PH_UPDATE_R, CGX_PH_UPDATE_XP};
+    for (int i = 0; i < (int)(words / ((size_t)kTsKern * kTsSlot)); ++i) {
+        int64_t st[kTsKern], en[kTsKern];
+        int first = -1, last = -1;
+        for (int k = 0; k < kTsKern; ++k) {
+            const int64_t *q = h.data() + ((size_t)i * kTsKern + k) * kTsSlot;
+            st[k] = q[0];
+            en[k] = 0;
+            for (int b = 1; b < kTsSlot; ++b) en[k] = std::max(en[k], q[b]);
+            if (st[k] == 0 || en[k] == 0) continue;  // not launched, or skipped itself (gated)
+            if (first < 0) first = k;
+            if (last >= 0) add(between(last, k), en[last], st[k]);
+            add(kern_seg[k], st[k], en[k]);
+            last = k;
+        }
+        if (first < 0) {  // an iteration that did nothing (after a device-side stop)
+            c->ts_prev_start = c->ts_prev_end = 0;
+            continue;
+        }
+        if (c->ts_prev_end) {
+            // before the first kernel: p's allgather when it is not overlapped
+            // (a non-overlapped exchange between iterations), else the launch gap
+            add((first == TK_MV && c->mode != M_SINGLE) ? CGX_PH_GATHER_EXPOSED : CGX_PH_GAP, c->ts_prev_end, st[first]);
+            add(CGX_PH_ITERATION, c->ts_prev_start, st[first]);
+        }
+        c->ts_prev_start = st[first];
+        c->ts_prev_end = en[last];
+    }
+    return CGX_OK;
+}
+
+// Rank mode, host-checked iterations: one event per iteration, so a host
+// wait can tell a healthy long queue (events completing) from a stall.
+int progress_mark(cgx_ctx *c) {
+    if (c->mode != M_RCCL) return CGX_OK;
+    Shard &s = c->sh[0];
+    if (!s.ev_prog[0]) return CGX_OK;
+    TRY(set_dev(s));
+    HIPT(hipEventRecord(s.ev_prog[s.prog_next], s.stream));
+    s.prog_next = (s.prog_next + 1) % 8;
+    return CGX_OK;
+}
+
 // ---- exchange ---------------------------------------------------------------------
 // Make every shard's stream wait for the work already queued on all shards.
 int local_barrier(cgx_ctx *c) {
@@ -331,11 +423,12 @@ int overlapped_matvec(cgx_ctx *c, int dot_slot, bool gated) {
         const double *v = reinterpret_cast<const double *>(s.pfull);
         double *Ap = reinterpret_cast<double *>(s.Ap);
         HIPT(matvec_f64_cols(s.plan, A, c->lda, s.nloc, c->lda, s.row0, s.nloc, false, v, Ap, nullptr, nullptr,
-                             s.ws, s.stream, gate_of(s, gated)));
+                             s.ws, s.stream, gate_of(s, gated), ts_of(c, s, TK_OWN)));
         HIPT(hipStreamWaitEvent(s.stream, s.ev_gathered, 0));
         HIPT(matvec_f64_cols(s.plan, A, c->lda, s.nloc, c->lda, (s.row0 + s.nloc) % c->lda, c->lda - s.nloc, true,
                              v, Ap, reinterpret_cast<const double *>(s.pown),
-                             reinterpret_cast<double *>(slot(s, dot_slot)), s.ws, s.stream, gate_of(s, gated)));
+                             reinterpret_cast<double *>(slot(s, dot_slot)), s.ws, s.stream, gate_of(s, gated),
+                             ts_of(c, s, TK_MV)));
         if (timing) {
             HIPT(hipEventRecord(s.ev_t[2 * s.ev_used + 1], s.stream));
             s.ev_used++;
@@ -414,7 +507,10 @@ int sync_all(cgx_ctx *c) {
         for (int q = 0; q < s.ncopy; ++q) HIPT(hipStreamSynchronize(s.copy[q]));
         if (s.cstream) TRY(rank_wait_stream(c, s.cstream, "the exchange stream"));
     }
-    return timing_resolve(c);
+    // The timing and phase events are resolved on request (cgx_get_stats,
+    // cgx_get_phase_times, cgx_reset_timing), not here: a caller's own timed
+    // region ending in a synchronize pays no event queries.
+    return CGX_OK;
 }
 
 // ---- rank-mode fail-fast ---------------------------------------------------------
@@ -461,11 +557,36 @@ static double now_s() {
     return std::chrono::duration<double>(std::chrono::steady_clock::now().time_since_epoch()).count();
 }
 
+// Which of the shard's per-iteration events (the lookahead ring, the progress
+// ring, the newest timing event) have completed, as a bit pattern: when
+// it changes the GPU has finished more of the enqueued work, i.e. the job is
+// making progress.
+static uint64_t progress_sig(const cgx_ctx *c) {
+    const Shard &s = c->sh[0];
+    uint64_t sig = 0;
+    int bit = 0;
+    auto probe = [&](hipEvent_t e) {
+        if (e && bit < 64 && hipEventQuery(e) == hipSuccess) sig |= uint64_t(1) << bit;
+        ++bit;
+    };
+    for (auto e : s.ev_look) probe(e);
+    for (auto e : s.ev_prog) probe(e);
+    const int nt = s.ev_used;  // the newest timed matVec's end
+    if (nt > 0) probe(s.ev_t[2 * nt - 1]);
+    return sig;
+}
+
 // Poll `ready` (a hipEventQuery / hipStreamQuery) until it reports success,
-// checking the communicator and the deadline in between.
+// checking the communicator and the deadline in between.  The deadline
+// counts time WITHOUT PROGRESS: it restarts whenever one more of the shard's
+// per-iteration events completes (progress_sig), so a long healthy wait (a
+// fixed-count run of many iterations, ranks reaching their first collective
+// at different times while the others still compute) never trips it; only a
+// stall does -- a peer that died or issued a different collective.
 template <typename F>
 static int rank_poll(cgx_ctx *c, F ready, const char *what) {
-    const double t0 = now_s();
+    double t0 = now_s();
+    uint64_t sig = progress_sig(c);
     for (long spins = 0;; ++spins) {
         const hipError_t e = ready();
         if (e == hipSuccess) return CGX_OK;
@@ -476,6 +597,13 @@ static int rank_poll(cgx_ctx *c, F ready, const char *what) {
         if (c->sh[0].comm && ncclCommGetAsyncError(c->sh[0].comm, &ar) == ncclSuccess && ar != ncclSuccess &&
             ar != ncclInProgress)
             return rccl_abort(c, "RCCL reported '%s' while waiting for %s", ncclGetErrorString(ar), what);
+        if ((spins & 63) == 0) {
+            const uint64_t now_sig = progress_sig(c);
+            if (now_sig != sig) {
+                sig = now_sig;
+                t0 = now_s();
+            }
+        }
         if (c->rccl_timeout_s > 0.0 && now_s() - t0 > c->rccl_timeout_s)
             return rccl_abort(c, "no progress for %.0f s waiting for %s (a rank died, or ranks issued different "
                                  "collectives; CGX_RCCL_TIMEOUT_S sets the limit)",

@@ -11,7 +11,7 @@ namespace cgxh {
 // ---- the iteration pieces ----------------------------------------------------------
 // One tile of the matVec: rows [r0, r0+rows) of this shard, A rows at `Arows`.
 int matvec_rows(cgx_ctx *c, Shard &s, const MatvecPlan &pl, const char *Arows, int64_t r0, int64_t rows,
-                const char *vec, bool fuse_dot, int dot_slot, bool gated) {
+                const char *vec, bool fuse_dot, int dot_slot, bool gated, int64_t *ts) {
     if (f32ref(c)) {
         HIPT(matvec_ref_f32(reinterpret_cast<const float *>(Arows), c->lda, rows, c->n,
                             reinterpret_cast<const float *>(vec), reinterpret_cast<float *>(s.Ap) + r0, s.stream,
@@ -21,7 +21,7 @@ int matvec_rows(cgx_ctx *c, Shard &s, const MatvecPlan &pl, const char *Arows, i
                         reinterpret_cast<const double *>(vec), reinterpret_cast<double *>(s.Ap) + r0,
                         fuse_dot ? reinterpret_cast<const double *>(s.pown) + r0 : nullptr,
                         fuse_dot ? reinterpret_cast<double *>(slot(s, dot_slot)) : nullptr, s.ws, s.stream,
-                        gated ? reinterpret_cast<const int64_t *>(slot(s, S_KDONE)) : nullptr));
+                        gated ? reinterpret_cast<const int64_t *>(slot(s, S_KDONE)) : nullptr, ts));
     }
     return CGX_OK;
 }
@@ -132,7 +132,8 @@ int launch_matvec(cgx_ctx *c, Shard &s, const char *vec, bool with_dot, int dot_
                                 reinterpret_cast<const float *>(vec), reinterpret_cast<float *>(s.Ap),
                                 reinterpret_cast<const float *>(s.pown), reinterpret_cast<float *>(slot(s, dot_slot)),
                                 s.ws.tickets + T_REF_MV, s.stream, gate_of(s, gated)));
-    else TRY(matvec_rows(c, s, s.plan, s.A, 0, s.nloc, vec, with_dot && !f32ref(c), dot_slot, gated));
+    else TRY(matvec_rows(c, s, s.plan, s.A, 0, s.nloc, vec, with_dot && !f32ref(c), dot_slot, gated,
+                         f32ref(c) ? nullptr : ts_of(c, s, TK_MV)));
     if (timing) {
         HIPT(hipEventRecord(s.ev_t[2 * s.ev_used + 1], s.stream));
         s.ev_used++;
@@ -181,9 +182,8 @@ int do_begin(cgx_ctx *c) {
     // finite-A precondition of the fp64 mode.)  CGX_F32_REF, the mode that
     // promises the reference's bits for any input, always does the matVec.
     TRY(settle_halo(c));
-    bool zero = false;
-    TRY(x0_is_zero(c, &zero));
-    if (f32ref(c)) zero = false;
+    bool zero = false;  // CGX_F32_REF always does the matVec: no need to ask (in rank mode: a collective)
+    if (!f32ref(c)) TRY(x0_is_zero(c, &zero));
     if (!zero) TRY(exchange_allgather(c, /*from_x=*/true));  // full x0 into pfull
     const int gs = S_RR + ring(0), ls = S_LRR + ring(0);
     const int os = out_slot(c, ls, gs);
@@ -310,11 +310,13 @@ static int do_iteration_fused_p(cgx_ctx *c, double eps, int *stop, bool gated) {
     Shard &s = c->sh[0];
     const int pg = S_PAP + ring(k), rg = S_RR + ring(k + 1);
     auto D = [](void *q) { return reinterpret_cast<double *>(q); };
+    TRY(phase_iter_begin(c));
     TRY(launch_matvec(c, s, s.pfull, true, pg, gated));  // serialConjugate.c:215,219
     HIPT(update_xrp_f64(s.nloc, D(s.x), D(s.r), D(s.pown), D(s.Ap), D(slot(s, S_RR + ring(k))), D(slot(s, pg)),
                         D(slot(s, rg)), s.ws, s.stream, gate_of(s, gated), gated ? eps : -1.0, k,
                         gated ? reinterpret_cast<int64_t *>(slot(s, S_KDONE)) : nullptr,
-                        gated ? D(slot(s, S_RRFINAL)) : nullptr, rec_of(c, s, gated)));  // :221-243
+                        gated ? D(slot(s, S_RRFINAL)) : nullptr, rec_of(c, s, gated), ts_of(c, s, TK_UXP)));  // :221-243
+    phase_iter_end(c);
     c->k = k + 1;
     c->total_iters += 1;
     if (!gated && eps >= 0.0) {  // host-checked stop; x is already current
@@ -368,6 +370,7 @@ int do_iteration(cgx_ctx *c, double eps, int *stop, bool gated) {
     const int64_t k = c->k;
     *stop = 0;
     const int pg = S_PAP + ring(k), pl = S_LPAP + ring(k);
+    TRY(phase_iter_begin(c));
     if (c->overlap) {
         TRY(overlapped_matvec(c, out_slot(c, pl, pg), gated));  // parallel_cg.c:290-293, overlapped
     } else {
@@ -394,7 +397,7 @@ int do_iteration(cgx_ctx *c, double eps, int *stop, bool gated) {
             HIPT(update_r_f64(s.nloc, reinterpret_cast<double *>(s.r), reinterpret_cast<const double *>(s.Ap),
                               reinterpret_cast<const double *>(slot(s, S_RR + ring(k))),
                               reinterpret_cast<const double *>(slot(s, pg)), reinterpret_cast<double *>(slot(s, ro)),
-                              s.ws, s.stream, gate_of(s, gated)));
+                              s.ws, s.stream, gate_of(s, gated), ts_of(c, s, TK_UR)));
         }
     }
     TRY(exchange_scalar(c, rl, rg));  // MPI_Allreduce(r.r)  parallel_cg.c:313
@@ -417,8 +420,10 @@ int do_iteration(cgx_ctx *c, double eps, int *stop, bool gated) {
                                reinterpret_cast<const double *>(slot(s, pg)),
                                reinterpret_cast<const double *>(slot(s, rg)), s.stream, eps, k,
                                reinterpret_cast<int64_t *>(slot(s, S_KDONE)),
-                               reinterpret_cast<double *>(slot(s, S_RRFINAL)), rec_of(c, s, gated)));
+                               reinterpret_cast<double *>(slot(s, S_RRFINAL)), rec_of(c, s, gated),
+                               ts_of(c, s, TK_UXP)));
         }
+        phase_iter_end(c);
         return CGX_OK;
     }
     if (eps >= 0.0) {  // if (sqrt(beta) < EPSILON) break;  serialConjugate.c:235-238
@@ -435,8 +440,10 @@ int do_iteration(cgx_ctx *c, double eps, int *stop, bool gated) {
                     HIPT(update_xp_f64(s.nloc, reinterpret_cast<double *>(s.x), reinterpret_cast<double *>(s.pown),
                                        reinterpret_cast<const double *>(s.r),
                                        reinterpret_cast<const double *>(slot(s, S_RR + ring(k))),
-                                       reinterpret_cast<const double *>(slot(s, pg)), nullptr, s.stream));
+                                       reinterpret_cast<const double *>(slot(s, pg)), nullptr, s.stream, -1.0, 0,
+                                       nullptr, nullptr, nullptr, ts_of(c, s, TK_UXP)));
                 }
+            phase_iter_end(c);
             return CGX_OK;
         }
     }
@@ -451,8 +458,10 @@ int do_iteration(cgx_ctx *c, double eps, int *stop, bool gated) {
                                reinterpret_cast<const double *>(s.r),
                                reinterpret_cast<const double *>(slot(s, S_RR + ring(k))),
                                reinterpret_cast<const double *>(slot(s, pg)),
-                               reinterpret_cast<const double *>(slot(s, rg)), s.stream));
+                               reinterpret_cast<const double *>(slot(s, rg)), s.stream, -1.0, 0, nullptr, nullptr,
+                               nullptr, ts_of(c, s, TK_UXP)));
     }
+    phase_iter_end(c);
     return CGX_OK;
 }
 
@@ -545,6 +554,7 @@ int cgx_iterate(cgx_ctx *c, int64_t count, double eps, int64_t *done, int *conve
     while (did < count && c->state == ST_BEGUN) {
         int stop = 0;
         TRY(do_iteration(c, eps, &stop));
+        TRY(progress_mark(c));
         ++did;
         if (stop) break;
     }
@@ -580,6 +590,7 @@ int cgx_solve(cgx_ctx *c, void *x_inout, double eps, int64_t max_iter, cgx_stats
 int cgx_get_stats(cgx_ctx *c, cgx_stats *st) {
     if (!c || !st) return fail(CGX_ERR_ARG, "NULL argument");
     TRY(sync_all(c));
+    TRY(timing_resolve(c));
     st->iterations = c->k;
     st->converged = c->converged;
     st->rr = c->last_rr;
@@ -593,8 +604,36 @@ int cgx_get_stats(cgx_ctx *c, cgx_stats *st) {
 int cgx_reset_timing(cgx_ctx *c) {
     if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
     TRY(sync_all(c));
+    c->sh[0].ev_used = 0;
+    if (c->sh[0].ts_used > 0) {  // drop the stamps recorded so far (warmup)
+        TRY(set_dev(c->sh[0]));
+        HIPT(hipMemsetAsync(c->sh[0].ts_dev, 0, (size_t)c->sh[0].ts_used * kTsKern * kTsSlot * 8, c->sh[0].stream));
+        c->sh[0].ts_used = 0;
+    }
+    c->ts_prev_start = c->ts_prev_end = 0;
+    for (auto &v : c->ph_samples) v.clear();
     c->matvec_ms = 0.0;
     c->matvec_count = 0;
+    return CGX_OK;
+}
+
+int cgx_get_phase_times(cgx_ctx *c, cgx_phase_times *out) {
+    if (!c || !out) return fail(CGX_ERR_ARG, "NULL argument");
+    if (!(c->flags & CGX_PHASES)) return fail(CGX_ERR_STATE, "the context was created without CGX_PHASES");
+    TRY(sync_all(c));
+    TRY(phase_resolve(c));
+    for (int q = 0; q < CGX_PH_COUNT; ++q) {
+        std::vector<float> v = c->ph_samples[q];
+        out->samples[q] = (int64_t)v.size();
+        out->median_us[q] = out->mean_us[q] = 0.0;
+        if (v.empty()) continue;
+        double sum = 0.0;
+        for (float t : v) sum += t;
+        out->mean_us[q] = sum / (double)v.size();
+        std::sort(v.begin(), v.end());
+        const size_t h = v.size() / 2;
+        out->median_us[q] = (v.size() & 1) ? v[h] : 0.5 * ((double)v[h - 1] + (double)v[h]);
+    }
     return CGX_OK;
 }
 

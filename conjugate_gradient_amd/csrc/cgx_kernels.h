@@ -17,6 +17,14 @@ constexpr int kMaxCombine = 64;
 constexpr int kTickets = 8;
 enum Ticket { T_MATVEC = 0, T_RESID = 1, T_XR = 2, T_DOT = 3, T_REF_MV = 4 };
 
+// CGX_PHASES in-kernel timestamps: a kernel given `ts` stores block 0's entry
+// time in ts[0] and block b's exit time in ts[1 + b] (b < kTsMaxBlocks), on
+// the device's constant wall clock (hipDeviceAttributeWallClockRate).  No
+// event packets between the kernels, so the timeline being measured is the
+// one that runs without CGX_PHASES.
+constexpr int kTsMaxBlocks = 2047;
+constexpr int kTsSlot = kTsMaxBlocks + 1;  // int64 per kernel slot
+
 // Geometry of the fp64 row-streaming matVec, chosen once per (device, rows).
 struct MatvecPlan {
     int R = 4;        // rows per wave
@@ -37,7 +45,8 @@ MatvecPlan plan_matvec_f64(int device, int64_t rows, int R = 0, int U = 0, int n
 // (device-side convergence gating of queued iterations).
 hipError_t matvec_f64(const MatvecPlan &pl, const double *A, int64_t lda, int64_t rows,
                       int64_t cols, const double *v, double *out, const double *pown,
-                      double *dot_out, const RedWs &ws, hipStream_t s, const int64_t *gate = nullptr);
+                      double *dot_out, const RedWs &ws, hipStream_t s, const int64_t *gate = nullptr,
+                      int64_t *ts = nullptr);
 // Columns [col_first, col_first+col_count) mod cols (all multiples of 128,
 // cols = the padded width): out[i] = (accumulate ? out[i] : 0) + partial row
 // sum; optional fused dot as above.  Used to overlap the p exchange with the
@@ -45,7 +54,7 @@ hipError_t matvec_f64(const MatvecPlan &pl, const double *A, int64_t lda, int64_
 hipError_t matvec_f64_cols(const MatvecPlan &pl, const double *A, int64_t lda, int64_t rows, int64_t cols,
                            int64_t col_first, int64_t col_count, bool accumulate, const double *v, double *out,
                            const double *pown, double *dot_out, const RedWs &ws, hipStream_t s,
-                           const int64_t *gate = nullptr);
+                           const int64_t *gate = nullptr, int64_t *ts = nullptr);
 // r = b - Ax; p = r (if p); *rr_out = r.r (if rr_out).  Ax == nullptr: Ax = 0
 // (r = b - 0.0).  clear2: two int64 the kernel zeroes (the convergence record).
 hipError_t residual_f64(int64_t n, const double *b, const double *Ax, double *r, double *p,
@@ -64,16 +73,19 @@ hipError_t update_p_f64(int64_t n, double *p, const double *r, const double *rr,
 // (and the same pair into hrec[0..1], host-mapped memory, when hrec != nullptr);
 // once *kdone is in (0, k] both kernels (update_r via gate) do nothing.
 hipError_t update_r_f64(int64_t n, double *r, const double *Ap, const double *rsold, const double *pAp,
-                        double *rr_out, const RedWs &ws, hipStream_t s, const int64_t *gate = nullptr);
+                        double *rr_out, const RedWs &ws, hipStream_t s, const int64_t *gate = nullptr,
+                        int64_t *ts = nullptr);
 // The two-launch iteration's update (one GPU, small n): x += alpha p;
 // r -= alpha Ap; *rr_out = r.r; then (last block) the stopping decision as
 // update_xp's, and unless stopped p = r + (*rr_out / *rsold) p.
 hipError_t update_xrp_f64(int64_t n, double *x, double *r, double *p, const double *Ap, const double *rsold,
                           const double *pAp, double *rr_out, const RedWs &ws, hipStream_t s, const int64_t *gate,
-                          double eps, int64_t k, int64_t *kdone, double *rrfinal, int64_t *hrec);
+                          double eps, int64_t k, int64_t *kdone, double *rrfinal, int64_t *hrec,
+                          int64_t *ts = nullptr);
 hipError_t update_xp_f64(int64_t n, double *x, double *p, const double *r, const double *rsold, const double *pAp,
                          const double *rr, hipStream_t s, double eps = -1.0, int64_t k = 0,
-                         int64_t *kdone = nullptr, double *rrfinal = nullptr, int64_t *hrec = nullptr);
+                         int64_t *kdone = nullptr, double *rrfinal = nullptr, int64_t *hrec = nullptr,
+                         int64_t *ts = nullptr);
 hipError_t dot_f64(int64_t n, const double *a, const double *b, double *out,
                    const RedWs &ws, hipStream_t s);
 // Rows [row0, row0+nrows) of the counter-hash SPD system; pad columns zeroed.

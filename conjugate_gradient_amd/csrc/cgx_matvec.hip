@@ -141,8 +141,10 @@ template <int R, int U, int NT, bool PIPE = false>
 __global__ __launch_bounds__(kNT) void k_matvec_f64(
     const double *__restrict__ A, int64_t lda, int64_t rows, int64_t cols, int64_t vec_cols, int64_t cfirst,
     int64_t ccount, int tail, int accumulate, const double *__restrict__ v, double *__restrict__ out,
-    const double *__restrict__ pown, double *dot_out, double *partials, unsigned *ticket, const int64_t *gate) {
+    const double *__restrict__ pown, double *dot_out, double *partials, unsigned *ticket, const int64_t *gate,
+    int64_t *ts) {
     if (gate && *gate) return;  // the solve converged in an earlier iteration (device-side gating)
+    ts_start(ts);
     const int lane = threadIdx.x & 63;
     const int wid = threadIdx.x >> 6;
     const int64_t ngroups = (rows + R - 1) / R;
@@ -191,10 +193,12 @@ __global__ __launch_bounds__(kNT) void k_matvec_f64(
         }
     }
     if (pown) grid_sum_last_block(dacc, partials, ticket, dot_out);
+    ts_end(ts);
 }
 
 using MvFn = void (*)(const double *, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, int, int,
-                      const double *, double *, const double *, double *, double *, unsigned *, const int64_t *);
+                      const double *, double *, const double *, double *, double *, unsigned *, const int64_t *,
+                      int64_t *);
 
 template <int R, int U>
 MvFn pick_nt(int nt) {
@@ -272,7 +276,7 @@ MatvecPlan plan_matvec_f64(int device, int64_t rows, int R, int U, int nt, int b
 
 hipError_t matvec_f64(const MatvecPlan &pl, const double *A, int64_t lda, int64_t rows, int64_t cols,
                       const double *v, double *out, const double *pown, double *dot_out,
-                      const RedWs &ws, hipStream_t s, const int64_t *gate) {
+                      const RedWs &ws, hipStream_t s, const int64_t *gate, int64_t *ts) {
     if (rows <= 0) return hipSuccess;
     // The vector path needs 16-B-aligned rows and p; otherwise every column
     // goes through the scalar tail loop.
@@ -281,14 +285,14 @@ hipError_t matvec_f64(const MatvecPlan &pl, const double *A, int64_t lda, int64_
     const int64_t vec_cols = aligned ? (cols & ~int64_t(127)) : 0;
     MvFn fn = pick_mv(pl.R, pl.U, pl.nt);
     hipLaunchKernelGGL(fn, dim3(pl.blocks), dim3(kNT), 0, s, A, lda, rows, cols, vec_cols, int64_t(0),
-                       vec_cols >> 7, 1, 0, v, out, pown, dot_out, ws.partials, ws.tickets + T_MATVEC, gate);
+                       vec_cols >> 7, 1, 0, v, out, pown, dot_out, ws.partials, ws.tickets + T_MATVEC, gate, ts);
     return hipGetLastError();
 }
 
 hipError_t matvec_f64_cols(const MatvecPlan &pl, const double *A, int64_t lda, int64_t rows, int64_t cols,
                            int64_t col_first, int64_t col_count, bool accumulate, const double *v, double *out,
                            const double *pown, double *dot_out, const RedWs &ws, hipStream_t s,
-                           const int64_t *gate) {
+                           const int64_t *gate, int64_t *ts) {
     if (rows <= 0) return hipSuccess;
     if ((cols & 127) || (col_first & 127) || (col_count & 127) || (lda & 1) ||
         ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(v)) & 15))
@@ -296,7 +300,7 @@ hipError_t matvec_f64_cols(const MatvecPlan &pl, const double *A, int64_t lda, i
     MvFn fn = pick_mv(pl.R, pl.U, pl.nt);
     hipLaunchKernelGGL(fn, dim3(pl.blocks), dim3(kNT), 0, s, A, lda, rows, cols, cols, col_first >> 7,
                        col_count >> 7, 0, accumulate ? 1 : 0, v, out, pown, dot_out, ws.partials,
-                       ws.tickets + T_MATVEC, gate);
+                       ws.tickets + T_MATVEC, gate, ts);
     return hipGetLastError();
 }
 

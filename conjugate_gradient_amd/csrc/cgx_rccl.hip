@@ -62,6 +62,9 @@ bool rccl_load() {
         get(g_rccl.GroupEnd, "ncclGroupEnd");
         get(g_rccl.CommGetAsyncError, "ncclCommGetAsyncError");
         get(g_rccl.CommAbort, "ncclCommAbort");
+        get(g_rccl.CommCount, "ncclCommCount");
+        get(g_rccl.CommCuDevice, "ncclCommCuDevice");
+        get(g_rccl.CommUserRank, "ncclCommUserRank");
         ok = all;
     });
     if (!ok) fail(CGX_ERR_RCCL, "cannot load RCCL: %s", why);

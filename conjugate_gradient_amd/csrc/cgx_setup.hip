@@ -157,10 +157,28 @@ int alloc_shard(cgx_ctx *c, Shard &s) {
     HIPT(hipHostGetDevicePointer(reinterpret_cast<void **>(&s.d_rec), s.h_rec, 0));
     s.h_rec[0] = s.h_rec[1] = 0;
     for (int q = 0; q < kLookRing; ++q) HIPT(hipEventCreateWithFlags(&s.ev_look[q], hipEventDisableTiming));
+    // Timing-only events (the matVec brackets) skip the system-scope release
+    // an event does by default when it completes: that fence writes back and
+    // invalidates the caches; an event costs 3.3 us on the stream without it,
+    // 4.4 us with it (profiles/r03_event_fence_ab.jsonl).  Nothing reads memory
+    // through these events; they only time.  CGX_EVENT_FENCE=1 restores the
+    // default events.
+    const char *ef = std::getenv("CGX_EVENT_FENCE");
+    const unsigned tflags = (ef && *ef == '1') ? hipEventDefault : hipEventDisableSystemFence;
     if (c->flags & CGX_TIMING) {
         s.ev_t.resize(2 * kEvPairs);
-        for (auto &e : s.ev_t) HIPT(hipEventCreate(&e));
+        for (auto &e : s.ev_t) HIPT(hipEventCreateWithFlags(&e, tflags));
     }
+    if ((c->flags & CGX_PHASES) && &s == &c->sh[0]) {
+        const size_t tsb = (size_t)kTsIters * kTsKern * kTsSlot * 8;
+        TRY(dmalloc(reinterpret_cast<char **>(&s.ts_dev), tsb));
+        HIPT(hipMemsetAsync(s.ts_dev, 0, tsb, s.stream));
+        int khz = 0;
+        if (hipDeviceGetAttribute(&khz, hipDeviceAttributeWallClockRate, s.dev) == hipSuccess && khz > 0)
+            c->ts_khz = khz;
+    }
+    if (c->mode == M_RCCL)
+        for (auto &e : s.ev_prog) HIPT(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     if (!f32ref(c) && c->op == OP_DENSE && !(c->flags & CGX_SYMMETRIC))
         s.plan = plan_matvec_f64(s.dev, s.nloc, 0, 0, -1, 0, c->lda);
     HIPT(hipStreamSynchronize(s.stream));
@@ -180,6 +198,9 @@ void free_shard(Shard &s) {
     if (s.h_x) (void)hipHostFree(s.h_x);
     if (s.h_rec) (void)hipHostFree(s.h_rec);
     for (auto e : s.ev_t) (void)hipEventDestroy(e);
+    if (s.ts_dev) (void)hipFree(s.ts_dev);
+    for (auto e : s.ev_prog)
+        if (e) (void)hipEventDestroy(e);
     if (s.ev_sync) (void)hipEventDestroy(s.ev_sync);
     if (s.ev_root) (void)hipEventDestroy(s.ev_root);
     for (int q = 0; q < kMaxCopyStreams; ++q)
@@ -324,6 +345,8 @@ static int check_device(int device) {
 // Operator-generic constructors.  Dense: n unknowns, row blocks of n/P rows.
 // Poisson: n = m*m unknowns, slabs of m/P grid rows (n/P unknowns).
 static int check_op(int op, int64_t n, int64_t m, int parts, int flags) {
+    if ((flags & CGX_PHASES) && (op != OP_DENSE || (flags & (CGX_F32_REF | CGX_HOST_STREAM | CGX_SYMMETRIC))))
+        return fail(CGX_ERR_ARG, "CGX_PHASES: the dense fp64 operator with A resident (row-major) only");
     if (op == OP_POISSON) {
         if (m < 1) return fail(CGX_ERR_ARG, "m must be >= 1");
         if (m % parts != 0) return fail(CGX_ERR_SHAPE, "%lld is not divisible by %d", (long long)m, parts);
@@ -378,14 +401,42 @@ static int create_multi(cgx_ctx **ctx, int op, int64_t n, int64_t m, int nshards
         c->sh[i].row0 = (int64_t)i * loc;
         c->sh[i].nloc = loc;
     }
-    // Peer access between distinct devices (xGMI); repeated devices need none.
+    // Peer access between distinct devices (xGMI), which parallel_cg.c's
+    // MPI_Scatter / MPI_Allgather (:109-117, :290) become here: every ordered
+    // pair must be able to reach the other's memory (hipDeviceCanAccessPeer),
+    // and access is enabled once per pair.  A pair that cannot is an error
+    // naming it -- the copies would otherwise be staged through host memory
+    // without a word.  Every failed HIP call's error is consumed here, so the
+    // thread's last HIP error is clean when the context is handed out
+    // (test_create_multi_leaves_no_hip_error).  Repeated devices need nothing.
+    bool distinct = false;
     for (int i = 0; i < nshards; ++i)
-        for (int j = 0; j < nshards; ++j)
-            if (devices[i] != devices[j]) {
-                (void)hipSetDevice(devices[i]);
-                hipError_t e = hipDeviceEnablePeerAccess(devices[j], 0);
-                if (e == hipErrorPeerAccessAlreadyEnabled) (void)hipGetLastError();
+        for (int j = 0; j < nshards; ++j) {
+            if (devices[i] == devices[j]) continue;
+            distinct = true;
+            int can = 0;
+            hipError_t e = hipDeviceCanAccessPeer(&can, devices[i], devices[j]);
+            if (e != hipSuccess || !can) {
+                (void)hipGetLastError();
+                delete c;
+                return fail(CGX_ERR_HIP, "device %d cannot access device %d's memory (hipDeviceCanAccessPeer: %s, "
+                                         "%d): the row blocks need peer access",
+                            devices[i], devices[j], hipGetErrorString(e), can);
             }
+            if (hipSetDevice(devices[i]) != hipSuccess) {
+                (void)hipGetLastError();
+                delete c;
+                return fail(CGX_ERR_HIP, "hipSetDevice(%d) failed", devices[i]);
+            }
+            e = hipDeviceEnablePeerAccess(devices[j], 0);
+            (void)hipGetLastError();  // hipErrorPeerAccessAlreadyEnabled (an earlier context) is fine
+            if (e != hipSuccess && e != hipErrorPeerAccessAlreadyEnabled) {
+                delete c;
+                return fail(CGX_ERR_HIP, "hipDeviceEnablePeerAccess(%d -> %d): %s", devices[i], devices[j],
+                            hipGetErrorString(e));
+            }
+        }
+    c->peer = distinct;
     return finish_create(c, ctx);
 }
 
@@ -554,8 +605,26 @@ int cgx_get_info(const cgx_ctx *c, cgx_info *info) {
     info->nrows = 0;
     for (auto &s : c->sh) info->nrows += s.nloc;
     info->flags = c->flags | (c->overlap ? CGX_OVERLAP_ACTIVE : 0) |
-                  ((c->fused || c->fused_p || c->ref_fused) ? CGX_FUSED_ACTIVE : 0);
+                  ((c->fused || c->fused_p || c->ref_fused) ? CGX_FUSED_ACTIVE : 0) | (c->peer ? CGX_PEER_ACTIVE : 0);
     info->elem_bytes = c->es;
+    return CGX_OK;
+}
+
+int cgx_get_comm_info(cgx_ctx *c, cgx_comm_info *info) {
+    if (!c || !info) return fail(CGX_ERR_ARG, "NULL argument");
+    std::memset(info, 0, sizeof *info);
+    const Shard &s = c->sh[0];
+    info->device = s.dev;
+    info->rccl_nranks = c->nranks;
+    info->rccl_device = -1;
+    info->rccl_rank = s.index;
+    HIPT(hipDeviceGetPCIBusId(info->pci_bus_id, (int)sizeof info->pci_bus_id, s.dev));
+    if (c->mode == M_RCCL) {
+        if (c->dead || !s.comm) return dead_error(c);
+        NCCLT(ncclCommCount(s.comm, &info->rccl_nranks));
+        NCCLT(ncclCommCuDevice(s.comm, &info->rccl_device));
+        NCCLT(ncclCommUserRank(s.comm, &info->rccl_rank));
+    }
     return CGX_OK;
 }
 

@@ -152,8 +152,9 @@ __global__ __launch_bounds__(kNT) void k_update_xrp_f64(int64_t n, double *__res
                                                         double *__restrict__ p, const double *__restrict__ Ap,
                                                         const double *rsold, const double *pAp, double *rr_out,
                                                         double *partials, unsigned *ticket, const int64_t *gate,
-                                                        ConvArgs cv) {
+                                                        ConvArgs cv, int64_t *ts) {
     if (gate && *gate) return;
+    ts_start(ts);
     const double rs = *rsold;
     const double alpha = cg_ratio(rs, *pAp);
     const __amdgpu_buffer_rsrc_t rrs = vec_rsrc(r, n);
@@ -194,10 +195,14 @@ __global__ __launch_bounds__(kNT) void k_update_xrp_f64(int64_t n, double *__res
     }
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");  // every wave's r stores land before the ticket
     double rr;
-    if (!grid_sum_keep_last(acc, partials, ticket, rr_out, rr)) return;
+    if (!grid_sum_keep_last(acc, partials, ticket, rr_out, rr)) {
+        ts_end(ts);
+        return;
+    }
     // ---- the last block: the stopping test, then p = r + beta p for all of p
     if (cv.kdone && cv.eps >= 0.0 && sqrt(rr) < cv.eps) {
         if (threadIdx.x == 0) record_convergence(cv, cv.k + 1, rr);
+        ts_end(ts);
         return;
     }
     const double beta = cg_ratio(rr, rs);
@@ -227,6 +232,7 @@ __global__ __launch_bounds__(kNT) void k_update_xrp_f64(int64_t n, double *__res
         for (int64_t i = threadIdx.x; i < n; i += kNT)
             p[i] = __hip_atomic_load(r + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) + beta * p[i];
     }
+    ts_end(ts);
 }
 
 // The solver's split of the x/r/p updates (fp64): x's update moves into the
@@ -235,8 +241,10 @@ __global__ __launch_bounds__(kNT) void k_update_xrp_f64(int64_t n, double *__res
 template <bool VEC, int VP = 2>
 __global__ __launch_bounds__(kNT) void k_update_r_f64(int64_t n, double *__restrict__ r, const double *__restrict__ Ap,
                                                       const double *rsold, const double *pAp, double *rr_out,
-                                                      double *partials, unsigned *ticket, const int64_t *gate) {
+                                                      double *partials, unsigned *ticket, const int64_t *gate,
+                                                      int64_t *ts) {
     if (gate && *gate) return;
+    ts_start(ts);
     const double alpha = cg_ratio(*rsold, *pAp);
     double acc = 0.0;
     if constexpr (VEC) {
@@ -266,6 +274,7 @@ __global__ __launch_bounds__(kNT) void k_update_r_f64(int64_t n, double *__restr
         }
     }
     grid_sum_last_block(acc, partials, ticket, rr_out);
+    ts_end(ts);
 }
 
 // x += alpha p (alpha = rsold / pAp); then, if rr != nullptr, p = r + (rr / rsold) p.
@@ -277,7 +286,8 @@ __global__ __launch_bounds__(kNT) void k_update_r_f64(int64_t n, double *__restr
 template <bool VEC, int VP = 2>
 __global__ __launch_bounds__(kNT) void k_update_xp_f64(int64_t n, double *__restrict__ x, double *__restrict__ p,
                                                        const double *__restrict__ r, const double *rsold,
-                                                       const double *pAp, const double *rr, ConvArgs cv) {
+                                                       const double *pAp, const double *rr, ConvArgs cv,
+                                                       int64_t *ts) {
     bool upd_p = rr != nullptr;
     if (cv.kdone) {
         const int64_t kd = *cv.kdone;
@@ -288,6 +298,7 @@ __global__ __launch_bounds__(kNT) void k_update_xp_f64(int64_t n, double *__rest
             if (blockIdx.x == 0 && threadIdx.x == 0) record_convergence(cv, cv.k + 1, rrn);
         }
     }
+    ts_start(ts);
     const double alpha = cg_ratio(*rsold, *pAp);
     const double beta = upd_p ? cg_ratio(*rr, *rsold) : 0.0;
     if constexpr (VEC) {
@@ -319,6 +330,7 @@ __global__ __launch_bounds__(kNT) void k_update_xp_f64(int64_t n, double *__rest
             if (upd_p) p[i] = r[i] + beta * p[i];
         }
     }
+    ts_end(ts);
 }
 
 template <bool VEC>
@@ -436,16 +448,16 @@ hipError_t update_p_f64(int64_t n, double *p, const double *r, const double *rr,
 }
 
 hipError_t update_r_f64(int64_t n, double *r, const double *Ap, const double *rsold, const double *pAp,
-                        double *rr_out, const RedWs &ws, hipStream_t s, const int64_t *gate) {
+                        double *rr_out, const RedWs &ws, hipStream_t s, const int64_t *gate, int64_t *ts) {
     const bool vec = al16(r) && al16(Ap);
     hipLaunchKernelGGL(vec ? k_update_r_f64<true> : k_update_r_f64<false>, dim3(grid_vec(n)), dim3(kNT), 0, s, n, r,
-                       Ap, rsold, pAp, rr_out, ws.partials, ws.tickets + T_XR, gate);
+                       Ap, rsold, pAp, rr_out, ws.partials, ws.tickets + T_XR, gate, ts);
     return hipGetLastError();
 }
 
 hipError_t update_xrp_f64(int64_t n, double *x, double *r, double *p, const double *Ap, const double *rsold,
                           const double *pAp, double *rr_out, const RedWs &ws, hipStream_t s, const int64_t *gate,
-                          double eps, int64_t k, int64_t *kdone, double *rrfinal, int64_t *hrec) {
+                          double eps, int64_t k, int64_t *kdone, double *rrfinal, int64_t *hrec, int64_t *ts) {
     if (n * 8 > INT32_MAX) return hipErrorInvalidValue;  // buffer-resource offsets are 32-bit
     const bool vec = al16(x) && al16(r) && al16(p) && al16(Ap);
     ConvArgs cv;
@@ -455,13 +467,13 @@ hipError_t update_xrp_f64(int64_t n, double *x, double *r, double *p, const doub
     cv.rrfinal = rrfinal;
     cv.hrec = hrec;
     hipLaunchKernelGGL(vec ? k_update_xrp_f64<true> : k_update_xrp_f64<false>, dim3(grid_vec(n)), dim3(kNT), 0, s,
-                       n, x, r, p, Ap, rsold, pAp, rr_out, ws.partials, ws.tickets + T_XR, gate, cv);
+                       n, x, r, p, Ap, rsold, pAp, rr_out, ws.partials, ws.tickets + T_XR, gate, cv, ts);
     return hipGetLastError();
 }
 
 hipError_t update_xp_f64(int64_t n, double *x, double *p, const double *r, const double *rsold, const double *pAp,
                          const double *rr, hipStream_t s, double eps, int64_t k, int64_t *kdone, double *rrfinal,
-                         int64_t *hrec) {
+                         int64_t *hrec, int64_t *ts) {
     const bool vec = al16(x) && al16(p) && al16(r);
     ConvArgs cv;
     cv.eps = eps;
@@ -470,7 +482,7 @@ hipError_t update_xp_f64(int64_t n, double *x, double *p, const double *r, const
     cv.rrfinal = rrfinal;
     cv.hrec = hrec;
     hipLaunchKernelGGL(vec ? k_update_xp_f64<true> : k_update_xp_f64<false>, dim3(grid_vec(n)), dim3(kNT), 0, s, n, x,
-                       p, r, rsold, pAp, rr, cv);
+                       p, r, rsold, pAp, rr, cv, ts);
     return hipGetLastError();
 }
 

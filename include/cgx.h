@@ -115,6 +115,17 @@ extern "C" {
                                   tiles through the GPU every matVec (out-of-HBM
                                   systems; tile size CGX_STREAM_TILE_MB, default
                                   256, copy streams CGX_STREAM_COPIES, default 2) */
+#define CGX_PHASES       0x10000 /* dense fp64 (row-major, resident A): the
+                                    kernels of every iteration on the first
+                                    shard stamp their start and end on the
+                                    device's constant clock -- nothing is
+                                    inserted between them -- and
+                                    cgx_get_phase_times() turns the stamps into
+                                    phase durations after the fact */
+#define CGX_PEER_ACTIVE  0x20000 /* reported in cgx_info.flags: a multi-shard
+                                    context spans distinct devices and peer
+                                    access is enabled between every pair of
+                                    them (device copies then go over xGMI) */
 
 typedef struct cgx_ctx cgx_ctx;
 
@@ -143,12 +154,62 @@ typedef struct {
     int64_t total_iterations; /* iterations since the context was created     */
 } cgx_stats;
 
+/* Per-phase times of the iterations since the last cgx_reset_timing (or since
+ * creation), CGX_PHASES contexts: for each phase the median and the mean over
+ * the iterations, in microseconds, and the number of samples.  Phases follow
+ * parallel_cg.c's loop (:288-323) on the first shard's stream: a kernel's own
+ * span (first block's start to last block's end), or the span between two
+ * consecutive kernels -- the exchange enqueued between them, or a launch gap.
+ * Consecutive phases tile the iteration: MATVEC_OWN + GATHER_EXPOSED + MATVEC
+ * + COMBINE_PAP + UPDATE_R + COMBINE_RR + UPDATE_XP + GAP = ITERATION. */
+#define CGX_PH_MATVEC_OWN     0 /* overlap: own-column-block matVec (p local)   */
+#define CGX_PH_GATHER_EXPOSED 1 /* the compute stream waiting for p's allgather
+                                   (overlap: after its own block; otherwise the
+                                   whole allgather, launch gap included)
+                                   parallel_cg.c:290-291                        */
+#define CGX_PH_MATVEC         2 /* the (rest of the) matVec with p.Ap   :292-293 */
+#define CGX_PH_COMBINE_PAP    3 /* MPI_Allreduce(p.Ap) counterpart        :294   */
+#define CGX_PH_UPDATE_R       4 /* r -= alpha Ap, r.r                     :304-309 */
+#define CGX_PH_COMBINE_RR     5 /* MPI_Allreduce(r.r) counterpart         :313   */
+#define CGX_PH_UPDATE_XP      6 /* x += alpha p, p = r + beta p  :299-303,318-322 */
+#define CGX_PH_GAP            7 /* end of an iteration to the start of the next
+                                   (host launch rate, lookahead waits)          */
+#define CGX_PH_ITERATION      8 /* start of an iteration to the start of the next */
+#define CGX_PH_COUNT          9
+typedef struct {
+    int64_t samples[CGX_PH_COUNT];
+    double  median_us[CGX_PH_COUNT];
+    double  mean_us[CGX_PH_COUNT];
+} cgx_phase_times;
+
+/* What the exchange runs on (rank mode): the communicator's rank count,
+ * device and rank as RCCL reports them (ncclCommCount / ncclCommCuDevice /
+ * ncclCommUserRank), and the PCI bus id of the context's device.  Other
+ * modes: nranks = row blocks, rccl_device = -1. */
+typedef struct {
+    int  rccl_nranks;
+    int  rccl_device;
+    int  rccl_rank;
+    int  device;
+    char pci_bus_id[32];
+} cgx_comm_info;
+
 /* ---- errors / info ------------------------------------------------------- */
 const char *cgx_strerror(int code);
 /* Detail message of the last failure on this thread ("" if none). */
 const char *cgx_last_error(void);
 int cgx_version(void);
 int cgx_device_count(int *count);
+/* The calling thread's pending HIP error (hipPeekAtLastError; 0 = none).
+ * libcgx consumes the errors of the HIP calls it makes and reports them
+ * through its own return codes, so this stays 0 across its entry points. */
+int cgx_hip_last_error(void);
+/* PCI bus id of a visible device ("0000:xx:yy.z"). */
+int cgx_device_pci_bus_id(int device, char *buf, int len);
+/* The link between two visible devices: *link_type as HSA reports it (4 =
+ * xGMI, 2 = PCIe; -1 when HIP cannot tell), *hops, and *peer = 1 when
+ * device_a can access device_b's memory directly (hipDeviceCanAccessPeer). */
+int cgx_device_link(int device_a, int device_b, int *link_type, int *hops, int *peer);
 
 /* ---- context lifetime ------------------------------------------------------ */
 /* One GPU (device `device`).  Replaces serialConjugate.c's single process. */
@@ -191,6 +252,7 @@ int cgx_create_poisson_rank(cgx_ctx **ctx, int64_t m, int rank, int nranks,
 
 int cgx_destroy(cgx_ctx *ctx);
 int cgx_get_info(const cgx_ctx *ctx, cgx_info *info);
+int cgx_get_comm_info(cgx_ctx *ctx, cgx_comm_info *info);
 
 /* ---- data in / out (host arrays; element type per flags) ----------------- */
 /* Rows [row0, row0+nrows) of A (row-major, host leading dimension lda_host),
@@ -222,14 +284,21 @@ int cgx_solve(cgx_ctx *ctx, void *x_inout, double eps, int64_t max_iter, cgx_sta
 int cgx_solve_begin(cgx_ctx *ctx);
 int cgx_iterate(cgx_ctx *ctx, int64_t count, double eps, int64_t *done, int *converged);
 int cgx_get_stats(cgx_ctx *ctx, cgx_stats *st);
+/* CGX_PHASES: the per-phase times (resolves the recorded events; waits for
+ * the work they mark). */
+int cgx_get_phase_times(cgx_ctx *ctx, cgx_phase_times *out);
 int cgx_reset_timing(cgx_ctx *ctx);
 int cgx_synchronize(cgx_ctx *ctx);
 /* The context's HIP stream of its first shard (hipStream_t as void*). */
 void *cgx_stream(cgx_ctx *ctx);
 /* Tuning of the fp64 matVec (k_matvec_f64): rows per wave (1,2,4,8), 128-column
  * chunks in flight per row (2,4,8), the A load policy (0 plain, 1 non-temporal
- * global loads, 8 software-pipelined non-temporal = default; the variants
- * measured and not adopted are in tools/microbench/matvec_variants.hip),
+ * global loads, 2 software-pipelined default-policy loads, 8 software-
+ * pipelined non-temporal = default; every R and U goes with each policy --
+ * R=8 U=8 pipelined is accepted but spills to scratch, so the default plan
+ * never picks it; all give the same row sums bit for bit,
+ * test_matvec_f64_every_plan_bitwise_equal; the variants measured and not adopted are
+ * in tools/microbench/matvec_variants.hip),
  * resident blocks per CU for the grid (<= 0: occupancy query).  Results do not
  * depend on the plan's R/U/policy; the p.Ap partial order depends on the grid
  * size. */

@@ -55,12 +55,12 @@ def main():
             res.update(iterations=st.iterations, converged=st.converged)
     else:
         flags = {"f32ref": cg.CGX_F32_REF, "p2p": cg.CGX_COMM_P2P, "nooverlap": cg.CGX_NO_OVERLAP,
-                 "deterministic": cg.CGX_DETERMINISTIC, "p2p_f32ref": cg.CGX_F32_REF | cg.CGX_COMM_P2P}.get(
-            mode, cg.CGX_F64)
+                 "deterministic": cg.CGX_DETERMINISTIC, "headline_det": cg.CGX_DETERMINISTIC,
+                 "p2p_f32ref": cg.CGX_F32_REF | cg.CGX_COMM_P2P}.get(mode, cg.CGX_F64)
         if not flags & cg.CGX_F32_REF:
             flags |= cg.CGX_F64
         f32 = bool(flags & cg.CGX_F32_REF)
-        if mode == "headline":  # configs[2]: the bench's N=65536 system, generated on the device
+        if mode.startswith("headline"):  # configs[2]: the bench's N=65536 system, generated on the device
             A = b = x0 = None
         elif mode == "sized":  # any n: generateSPDmatrix(n) from the oracle's MATLAB-compatible generator
             A, b = oracle.spd_matlab(n, np.float64)

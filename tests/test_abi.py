@@ -240,7 +240,24 @@ def test_cg_mpi_rejects_indivisible_n_and_bad_options(built):
     assert r.returncode != 0 and "usage: mpiexec -np P cg_mpi" in r.stderr
     r = subprocess.run(["/opt/conda/bin/mpiexec", "-np", "2", exe, str(FIX) + "/nope.txt", paths[1], paths[2]],
                        capture_output=True, text=True, timeout=120)
-    assert r.returncode != 0 and "Could not open file" in r.stderr
+    assert r.returncode != 0 and "Could not open file\n" in r.stdout  # initialize(), parallel_cg.c:166
+
+
+def test_cg_mpi_p2p_keeps_point_to_point_cg_texts(built):
+    """--p2p speaks point-to-point_cg.c's error texts, not parallel_cg.c's:
+    "%d must be divisible by %d" (:101) and scatterRow's "Could not open %s
+    file. " for A and b (:226); x0 goes through initialize() (:177)."""
+    exe = _cg_mpi()
+    paths = [os.path.join(FIX, f) for f in ("matrixA1.txt", "vectorb1.txt", "X0.txt")]
+    run = lambda np_, *a: subprocess.run(["/opt/conda/bin/mpiexec", "-np", str(np_), exe, "--p2p", *a],
+                                         capture_output=True, text=True, timeout=120)
+    r = run(3, *paths)
+    assert r.returncode != 0 and "4 must be divisible by 3\n" in r.stdout and "is not divisible" not in r.stdout
+    nope = str(FIX) + "/nope.txt"
+    r = run(2, nope, paths[1], paths[2])
+    assert r.returncode != 0 and f"Could not open {nope} file. \n" in r.stdout
+    r = run(2, paths[0], paths[1], nope)
+    assert r.returncode != 0 and "Could not open file\n" in r.stdout and "nope.txt file" not in r.stdout
 
 
 def test_cli_argument_count(built):
@@ -332,3 +349,28 @@ def test_flag_constants_match_header():
     assert names
     for k in names:
         assert k in hdr and getattr(cg, k) == hdr[k], k
+
+
+def test_phase_indices_match_header():
+    """cgx_phase_times' index order (CGX_PH_*) is the mirror's PHASE_NAMES order,
+    and the mirror's structs have the header's sizes."""
+    import ctypes
+    with open(os.path.join(ROOT, "include", "cgx.h")) as f:
+        src = f.read()
+    idx = {m.group(1).lower(): int(m.group(2)) for m in re.finditer(r"#define\s+CGX_PH_([A-Z_]+)\s+(\d+)", src)}
+    count = idx.pop("count")
+    assert count == len(cg.PHASE_NAMES) == len(idx)
+    assert [n for n, _ in sorted(idx.items(), key=lambda kv: kv[1])] == list(cg.PHASE_NAMES)
+    assert ctypes.sizeof(cg.PhaseTimes) == 8 * 3 * count
+    assert ctypes.sizeof(cg.CommInfo) == 4 * 4 + 32
+
+
+def test_device_queries_without_a_gpu_fail_cleanly(built):
+    """cgx_device_link / cgx_device_pci_bus_id return an error code (no
+    abort) when the device does not exist."""
+    if cg.device_count() > 0:
+        pytest.skip("a GPU is visible")
+    with pytest.raises(cg.CgxError):
+        cg.device_link(0, 1)
+    with pytest.raises(cg.CgxError):
+        cg.device_pci_bus_id(0)

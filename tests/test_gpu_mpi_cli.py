@@ -63,10 +63,16 @@ def test_cg_mpi_fp32ref_equals_mpi_programs(spd512_files, program, nranks):
     key = f"{program}_spd512_np{nranks}"
     args = ["--fp32-ref", "--print-x", "--stats"] + (["--p2p"] if program == "p2p" else []) + spd512_files
     out = run_mpi(nranks, *args)
-    assert "Computing cg of matrix size : 262144" in out                       # parallel_cg.c:101
-    for line in ("cg method execution time in seconds:", "collective data distribution time in seconds:",
-                 "clock execution time in seconds:"):
-        assert line in out                                                     # :334, :123-126
+    assert "Computing cg of matrix size : 262144" in out      # parallel_cg.c:101, point-to-point_cg.c:116
+    # each program's own lines, in its order: cg time (printed by conjugrad),
+    # then the distribution time, then the clock time
+    dist = "p2p" if program == "p2p" else "collective"  # point-to-point_cg.c:133 / parallel_cg.c:123
+    lines = [ln for ln in out.splitlines() if "time in seconds:" in ln]
+    assert [ln.split(":")[0] for ln in lines] == ["cg method execution time in seconds",
+                                                 f"{dist} data distribution time in seconds",
+                                                 "clock execution time in seconds"], lines
+    assert ("collective" if program == "p2p" else "p2p") + " data distribution" not in out
+    assert all(float(ln.split(":")[1]) >= 0 for ln in lines)
     assert f"iterations: {golden_mpi()['runs'][key]['ref_iterations']} converged: 1" in out
     x = printed_x(out, 512, np.float32)
     assert np.array_equal(x.view(np.uint32), mpi_golden_x(key).view(np.uint32))

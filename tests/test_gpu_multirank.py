@@ -163,6 +163,18 @@ def test_rank_mode_world8(tmp_path, mode):
         assert np.array_equal(x, xs)
 
 
+_HASH_ORACLE = {}
+
+
+def hash_oracle(n):
+    """conjgrad.m in fp64 on the bench's counter-hash system (seed 42), A
+    regenerated row by row (oracle_cg_f64_hash); computed once per session."""
+    if n not in _HASH_ORACLE:
+        oracle.set_threads(16)
+        _HASH_ORACLE[n] = oracle.cg_f64_hash(n, 42, eps=1e-10)
+    return _HASH_ORACLE[n]
+
+
 @pytest.mark.timeout(600)
 def test_rank_mode_headline_n65536_world2(tmp_path):
     """BASELINE configs[2] through the rank path at full size: N=65536 on 2
@@ -172,10 +184,34 @@ def test_rank_mode_headline_n65536_world2(tmp_path):
     n, P = 65536, 2
     x, res = run_ranks(tmp_path, "headline", n, P, timeout=500)
     assert res[0]["nrows"] == n // P and res[0]["overlap"]
-    oracle.set_threads(16)
-    xo, so = oracle.cg_f64_hash(n, 42, eps=1e-10)
+    xo, so = hash_oracle(n)
     assert res[0]["converged"] and res[0]["iterations"] == so.iterations
     assert rel(x, xo) <= TOL and res[0]["relres"] <= TOL
+
+
+@pytest.mark.timeout(900)
+@pytest.mark.parametrize("mode", ["headline", "headline_det"])
+def test_rank_mode_headline_n65536_world8(tmp_path, mode):
+    """configs[2] in the driver's placement: N=65536 over 8 RCCL rank
+    processes (parallel_cg.c:83's row blocks: 8192 rows x 65536 = 4.3 GB of A
+    each; the loop :283-323 with the overlapped allgather and the two scalar
+    exchanges), generated on the device, converged at eps 1e-10.  Every rank
+    ends with the same x; the loop count is conjgrad.m's; x within 1e-10 of
+    the fp64 oracle; true residual <= 1e-10 ||b||.  CGX_DETERMINISTIC
+    (headline_det) must also equal, bit for bit, the 8-shard multi-shard
+    solve of the same system in one process."""
+    n, P = 65536, 8
+    x, res = run_ranks(tmp_path, mode, n, P, timeout=780)
+    assert res[0]["nrows"] == n // P and res[0]["overlap"]
+    xo, so = hash_oracle(n)
+    assert res[0]["converged"] and res[0]["iterations"] == so.iterations
+    assert rel(x, xo) <= TOL and res[0]["relres"] <= TOL
+    if mode == "headline_det":  # the rank-ordered combine == the LOCAL mode's combine of the same partition
+        with cg.Solver(n, devices=[0] * P) as s:
+            s.generate_spd(42)
+            xs, st = s.solve(None, eps=1e-10)
+        assert st.iterations == res[0]["iterations"]
+        assert np.array_equal(x, xs)
 
 
 @pytest.mark.timeout(150)
@@ -229,7 +265,8 @@ def test_bench_under_torchrun_world2(workload):
     s.bind(("127.0.0.1", 0))
     port = s.getsockname()[1]
     s.close()
-    args = ["--gpus", "2", "--steps", "4", "--warmup", "1", "--no-cpu"]
+    steps = 30 if workload == "dense" else 4
+    args = ["--gpus", "2", "--steps", str(steps), "--warmup", "1", "--no-cpu"]
     args += ["--size", "4096"] if workload == "dense" else ["--workload", "poisson", "--grid", "512"]
     cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", "--nproc-per-node", "2",
            "--master-addr", "127.0.0.1", "--master-port", str(port),
@@ -240,11 +277,23 @@ def test_bench_under_torchrun_world2(workload):
     lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
     assert len(lines) == 1, p.stdout[-2000:]  # rank 0 only
     out = json.loads(lines[0])
-    assert out["n_gpus"] == 2 and out["steps"] == 4 and out["value"] > 0
+    assert out["n_gpus"] == 2 and out["steps"] == steps and out["value"] > 0
     assert out["config"]["rows_per_gpu"] == (2048 if workload == "dense" else 512 * 512 // 2)
+    # what RCCL ran on: 2 ranks; here both on this box's one GPU (per-rank host ids)
+    rc = out["rccl"]
+    assert rc["nranks"] == 2 and len(rc["pci_bus_ids"]) == 2 and rc["distinct_devices"] == 1
+    assert [r["rccl_rank"] for r in rc["ranks"]] == [0, 1] and rc["links_from_rank0"][0]["link"] == "same device"
     if workload == "dense":
         assert "allgather" in out["config"]["exchange"]
         assert out["check"]["relres"] < 1e-6
+        # the per-phase breakdown: every rank, every phase, and the phases tile the iteration
+        ph = out["phases_us"]
+        assert ph["iterations_sampled"] == steps - 1 and len(ph["per_rank"]) == 2
+        for r in ph["per_rank"]:
+            assert set(r) == set(cg.PHASE_NAMES)
+            assert r["matvec_own"] > 0 and r["matvec"] > 0 and r["combine_pap"] > 0 and r["iteration"] > 0
+        assert abs(ph["tiling_mean_sum_over_ms_per_step"] - 1) <= 0.05, ph
+        assert abs(ph["tiling_sum_over_ms_per_step"] - 1) <= 0.25, ph  # medians of a noisy socket transport
     else:  # 1 warmup + 4 timed iterations from x0 = 0: the oracle's true residual after 5
         m = 512
         xo, _ = oracle.cg_poisson_f64(m, np.ones(m * m), np.zeros(m * m), max_iter=5, eps=-1.0)

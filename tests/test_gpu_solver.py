@@ -330,6 +330,102 @@ def test_fixed_count_past_convergence_stays_finite(monkeypatch, kind, fuse_p):
     assert rel(x, x_conv) <= 1e-10
 
 
+@pytest.mark.parametrize("shards", [None, [0, 0]])
+def test_indefinite_breakdown_is_not_hidden(shards):
+    """An A that is not positive definite can give p.Ap = 0 with r.r != 0: a
+    real breakdown.  alpha = r.r / p.Ap is then Inf, as in the reference's
+    division (serialConjugate.c:220), and x stops being finite -- not a quiet
+    alpha = 0 that would stall the solve at x0 until max_iter (cg_ratio keeps
+    0 only for an underflowed numerator, the exact-convergence case)."""
+    A = np.diag([1.0, -1.0])
+    b = np.ones(2)
+    with cg.Solver(2, devices=shards) as s:
+        s.set_system(A, b, np.zeros(2))
+        x, st = s.solve(None, eps=1e-10)
+    assert not st.converged and st.iterations == 2  # the reference's k < ROWS cap
+    assert not np.all(np.isfinite(x)), x
+
+
+def test_create_multi_leaves_no_hip_error():
+    """cgx_create_multi enables peer access only between distinct devices,
+    after hipDeviceCanAccessPeer, and consumes every HIP error it meets: the
+    thread's pending HIP error is clean afterwards (a stale one would surface
+    as a spurious CGX_ERR_HIP at the first kernel launch).  CGX_PEER_ACTIVE
+    reports whether the blocks span several devices with peer access on."""
+    L = cg.lib()
+    with cg.Solver(1024, devices=[0, 0]) as s:
+        assert L.cgx_hip_last_error() == 0
+        assert not s.info.flags & cg.CGX_PEER_ACTIVE  # one device: nothing to enable
+        s.generate_spd(1)
+        _, st = s.solve(None, eps=1e-10)
+        assert st.converged
+    if cg.device_count() >= 2:
+        link = cg.device_link(0, 1)
+        if link["peer_access"]:
+            with cg.Solver(1024, devices=[0, 1]) as s:
+                assert L.cgx_hip_last_error() == 0 and s.info.flags & cg.CGX_PEER_ACTIVE
+        else:  # named in the error, not a silent host-staged copy
+            with pytest.raises(cg.CgxError, match="cannot access"):
+                cg.Solver(1024, devices=[0, 1])
+    assert cg.device_link(0, 0)["link"] == "unknown" and len(cg.device_pci_bus_id(0)) >= 12
+
+
+@pytest.mark.parametrize("kind", ["single", "small_fused", "shards_overlap", "shards_plain", "gated"])
+def test_phase_times_tile_the_iteration(kind):
+    """CGX_PHASES: the iteration's kernels stamp their start and end on the
+    device clock; the phases are resolved after the fact.  Every kernel phase
+    gets one sample per iteration (the gap and the iteration one fewer), more
+    iterations than one stamp ring holds (256) are carried across resolves,
+    and the consecutive phases tile the iteration: their means add up to the
+    mean iteration.  A converged, device-gated solve stops sampling where the
+    kernels stop running."""
+    n, steps = {"small_fused": 2048, "single": 16384}.get(kind, 4096), 600
+    devices = {"shards_overlap": [0, 0], "shards_plain": [0, 0, 0]}.get(kind)  # 4095/3 rows: no overlap
+    if kind == "shards_plain":
+        n = 4095
+    with cg.Solver(n, flags=cg.CGX_PHASES | cg.CGX_TIMING, devices=devices) as s:
+        s.generate_spd(5)
+        if kind == "gated":
+            _, st = s.solve(None, eps=1e-10)
+            ph = s.phase_times()
+            assert ph["matvec"]["samples"] == st.iterations and ph["iteration"]["samples"] == st.iterations - 1
+            return
+        s.begin()
+        s.iterate(3, eps=-1.0)
+        s.reset_timing()
+        s.iterate(steps, eps=-1.0)
+        ph = s.phase_times()
+    assert ph["iteration"]["samples"] == steps - 1, ph["iteration"]
+    # samples per phase: one per iteration for a kernel and for the span between
+    # two kernels of an iteration; one fewer for the span before an
+    # iteration's first kernel (the gap; p's allgather when not overlapped)
+    S, F = steps, steps - 1
+    want = {"single": {"matvec": S, "combine_pap": S, "update_r": S, "combine_rr": S, "update_xp": S, "gap": F},
+            "small_fused": {"matvec": S, "combine_pap": S, "update_xp": S, "gap": F},
+            "shards_overlap": {"matvec_own": S, "gather_exposed": S, "matvec": S, "combine_pap": S, "update_r": S,
+                               "combine_rr": S, "update_xp": S, "gap": F},
+            "shards_plain": {"gather_exposed": F, "matvec": S, "combine_pap": S, "update_r": S, "combine_rr": S,
+                             "update_xp": S}}[kind]
+    for name in cg.PHASE_NAMES[:8]:
+        assert ph[name]["samples"] == want.get(name, 0), (name, ph[name])
+        if name in want:
+            assert ph[name]["mean_us"] > 0, (name, ph[name])
+    tiles = sum(ph[k]["mean_us"] * ph[k]["samples"] for k in cg.PHASE_NAMES[:8]) / (steps - 1)
+    assert abs(tiles / ph["iteration"]["mean_us"] - 1) <= 0.02, (tiles, ph["iteration"])
+
+
+@pytest.mark.parametrize("flags,kw", [(cg.CGX_F32_REF, {}), (cg.CGX_HOST_STREAM, {}), (cg.CGX_SYMMETRIC, {}),
+                                      (0, {"poisson_m": 8})])
+def test_phase_times_refused_where_not_stamped(flags, kw):
+    """CGX_PHASES covers the dense fp64 kernels with A resident; the other
+    operators are refused at creation, and a context without the flag
+    refuses cgx_get_phase_times."""
+    with pytest.raises(cg.CgxError, match="CGX_PHASES"):
+        cg.Solver(64, flags=flags | cg.CGX_PHASES, **kw)
+    with cg.Solver(64) as s, pytest.raises(cg.CgxError):
+        s.phase_times()
+
+
 def test_timing_events_count():
     """CGX_TIMING times every matVec launch.  With x0 = 0 the initial A x0 is
     skipped (exactly zero); with any other x0 it runs."""
