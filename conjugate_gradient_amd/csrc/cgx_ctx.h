@@ -177,6 +177,7 @@ struct Shard {
     // fused Poisson iteration: r with halo rows (r = rh + one row) and a
     // second p slab; p_k lives in pfull for even k, in p2 for odd k
     char *rh = nullptr, *p2 = nullptr;
+    char *p_alt = nullptr;  // the folded two-launch iteration: p_k for odd k (pfull holds even k)
     bool x_zero = true;  // x is known to be all zeros (x0 = 0: the first A x is skipped)
     RedWs ws{nullptr, nullptr};
     double *h_pin = nullptr;
@@ -188,6 +189,7 @@ struct Shard {
     // memory: the deciding kernel stores it, the host reads it after an event
     int64_t *h_rec = nullptr, *d_rec = nullptr;
     MatvecPlan plan;
+    MatvecPlan fold_plan;  // k_matvec_fold_f64's (c->fold_p)
     // CGX_SYMMETRIC: A = the upper-triangle tiles; per-tile row / column
     // partials of a matVec; a staging buffer for rows copied from the host
     char *sym_prow = nullptr, *sym_pcol = nullptr, *sym_stage = nullptr;
@@ -251,6 +253,7 @@ struct cgx_ctx {
     bool overlap = false;  // own-column-block matVec while p is exchanged
     bool fused = false;    // Poisson: two-kernel fused iteration (k_poisson_p + k_poisson_xr)
     bool fused_p = false;  // dense, one GPU, small n: two launches per iteration (matVec, k_update_xrp_f64)
+    bool fold_p = false;   // ... with the p update folded into the matVec (k_matvec_fold_f64, k_update_xr_stop_f64)
     bool ref_mv_dot = false;  // CGX_F32_REF, resident dense: the matVec's last block runs vecVec(p, Ap) (any mode)
     bool ref_fused = false;   // ... and on one GPU: two launches per iteration (matVec + p.Ap, x/r/r.r/p)
     bool halo_overlap = false;  // fused Poisson, several slabs: r's halo exchange overlaps k_poisson_p

@@ -332,6 +332,58 @@ static int do_iteration_fused_p(cgx_ctx *c, double eps, int *stop, bool gated) {
     return CGX_OK;
 }
 
+// The two-launch iteration with the p update folded into the matVec
+// (c->fold_p): k_matvec_fold_f64 forms p_k = r_k + beta p_{k-1} as it
+// multiplies it (its row owners store p_k into the other p buffer and fuse
+// p_k . A p_k), then k_update_xr_stop_f64 does x, r, r.r and the stopping
+// decision on every block -- no single-block pass over p.  Iteration 0 uses
+// p_0 = r_0 as the residual left it.  p_k lives in pfull for even k, in
+// p_alt for odd k.  The expressions are the three-launch kernels' (bitwise
+// the same x, test_two_launch_iteration_bitwise_equals_three).
+static int do_iteration_fold_p(cgx_ctx *c, double eps, int *stop, bool gated) {
+    const int64_t k = c->k;
+    *stop = 0;
+    Shard &s = c->sh[0];
+    const int pg = S_PAP + ring(k), rg = S_RR + ring(k + 1);
+    auto D = [](void *q) { return reinterpret_cast<double *>(q); };
+    char *pk = (k & 1) ? s.p_alt : s.pfull, *pkm1 = (k & 1) ? s.pfull : s.p_alt;
+    TRY(phase_iter_begin(c));
+    if (k == 0) {
+        TRY(launch_matvec(c, s, s.pfull, true, pg, gated));  // serialConjugate.c:215,219 with p_0 = r_0
+    } else {
+        const bool timing = (c->flags & CGX_TIMING) != 0;
+        if (timing && s.ev_used >= kEvPairs) TRY(timing_resolve(c));
+        if (timing) HIPT(hipEventRecord(s.ev_t[2 * s.ev_used], s.stream));
+        // every column up to lda, as the plain matVec runs them (A, r and both p
+        // buffers are zero there), so the row sums add in the same order
+        HIPT(matvec_fold_f64(s.fold_plan, D(s.A), c->lda, s.nloc, c->lda, D(s.r), D(pkm1), D(pk), D(slot(s, S_RR + ring(k))),
+                             D(slot(s, S_RR + ring(k + 3))), D(s.Ap), D(slot(s, pg)), s.ws, s.stream,
+                             gate_of(s, gated), ts_of(c, s, TK_MV)));  // :239-243 of k-1, then :215,219
+        if (timing) {
+            HIPT(hipEventRecord(s.ev_t[2 * s.ev_used + 1], s.stream));
+            s.ev_used++;
+        }
+    }
+    HIPT(update_xr_stop_f64(s.nloc, D(s.x), D(s.r), D(pk), D(s.Ap), D(slot(s, S_RR + ring(k))), D(slot(s, pg)),
+                            D(slot(s, rg)), s.ws, s.stream, gate_of(s, gated), gated ? eps : -1.0, k,
+                            gated ? reinterpret_cast<int64_t *>(slot(s, S_KDONE)) : nullptr,
+                            gated ? D(slot(s, S_RRFINAL)) : nullptr, rec_of(c, s, gated), ts_of(c, s, TK_UXP)));
+    phase_iter_end(c);
+    c->k = k + 1;
+    c->total_iters += 1;
+    if (!gated && eps >= 0.0) {  // host-checked stop; x is already current
+        double rr = 0.0;
+        TRY(read_scalar(c, rg, &rr));
+        c->last_rr = rr;
+        if (std::sqrt(rr) < eps) {
+            c->converged = 1;
+            c->state = ST_CONVERGED;
+            *stop = 1;
+        }
+    }
+    return CGX_OK;
+}
+
 // The same for CGX_F32_REF (c->ref_fused): the matVec whose last block runs
 // vecVec(p, Ap), then one single-block launch for x += p alpha, r -= Ap alpha,
 // r.r, the stopping test and p = r + p (rr/rsold) -- four launches' float
@@ -365,6 +417,7 @@ static int do_iteration_ref_fused(cgx_ctx *c, double eps, int *stop, bool gated)
 
 int do_iteration(cgx_ctx *c, double eps, int *stop, bool gated) {
     if (c->fused) return do_iteration_poisson(c, eps, stop, gated);
+    if (c->fold_p) return do_iteration_fold_p(c, eps, stop, gated);
     if (c->fused_p) return do_iteration_fused_p(c, eps, stop, gated);
     if (c->ref_fused) return do_iteration_ref_fused(c, eps, stop, gated);
     const int64_t k = c->k;

@@ -82,6 +82,18 @@ hipError_t update_xrp_f64(int64_t n, double *x, double *r, double *p, const doub
                           const double *pAp, double *rr_out, const RedWs &ws, hipStream_t s, const int64_t *gate,
                           double eps, int64_t k, int64_t *kdone, double *rrfinal, int64_t *hrec,
                           int64_t *ts = nullptr);
+// The folded two-launch iteration (one GPU, small n): the matVec forms
+// p_k = r + (*rr_new / *rr_old) p_{k-1} for the chunks it multiplies, stores
+// p_k's own rows into pnew and fuses *dot_out = p_k . out; then update_xr_stop
+// does x += alpha p_k, r -= alpha Ap, *rr_out = r.r and the stopping decision.
+hipError_t matvec_fold_f64(const MatvecPlan &pl, const double *A, int64_t lda, int64_t rows, int64_t cols,
+                           const double *r, const double *pold, double *pnew, const double *rr_new,
+                           const double *rr_old, double *out, double *dot_out, const RedWs &ws, hipStream_t s,
+                           const int64_t *gate = nullptr, int64_t *ts = nullptr);
+hipError_t update_xr_stop_f64(int64_t n, double *x, double *r, const double *p, const double *Ap,
+                              const double *rsold, const double *pAp, double *rr_out, const RedWs &ws, hipStream_t s,
+                              const int64_t *gate, double eps, int64_t k, int64_t *kdone, double *rrfinal,
+                              int64_t *hrec, int64_t *ts = nullptr);
 hipError_t update_xp_f64(int64_t n, double *x, double *p, const double *r, const double *rsold, const double *pAp,
                          const double *rr, hipStream_t s, double eps = -1.0, int64_t k = 0,
                          int64_t *kdone = nullptr, double *rrfinal = nullptr, int64_t *hrec = nullptr,
@@ -113,7 +125,8 @@ hipError_t fill_f32(float *p, int64_t n, float v, hipStream_t s);
 
 // ---- CGX_SYMMETRIC: A as the upper triangle of 128 x 128 tiles ---------------
 // (layout: cgx_symv.hip).  lda is a multiple of 128; At holds sym_tiles(lda)
-// tiles of 128*128 doubles; prow/pcol sym_tiles(lda)*128 doubles each.
+// tiles of 128*128 doubles; prow 2*sym_tiles(lda)*128 doubles (one row
+// partial per unit = half tile, at most), pcol sym_tiles(lda)*128.
 int64_t sym_tiles(int64_t lda);
 int sym_grid(int device);
 // y = A p (rows [0, n)), *dot_out = pown . y when pown != nullptr
@@ -138,9 +151,10 @@ hipError_t symv_reduce_f64(int64_t n, int64_t lda, int64_t per, const double *pr
                            const int64_t *gate = nullptr);
 // host copies of the layout helpers (tile index, element offset in a tile)
 inline int64_t sym_off_h(int64_t I, int64_t nt) { return I * nt - I * (I - 1) / 2; }
-inline int64_t sym_pos_h(int r, int c) {  // kSymNT = 512: (8 tr + rr, 4 tc + 2 cc + e)
-    const int t = (r / 8) * 32 + (c >> 2), k = (r % 8) * 2 + ((c >> 1) & 1);
-    return ((int64_t)k * 512 + t) * 2 + (c & 1);
+inline int64_t sym_pos_h(int r, int c) {  // kSymNT = 256: unit c / 64, (8 tr + rr, 4 tc + 2 cc + e)
+    const int h = c / 64, cc = c % 64;
+    const int t = (r / 8) * 16 + (cc >> 2), k = (r % 8) * 2 + ((cc >> 1) & 1);
+    return (int64_t)h * 128 * 64 + ((int64_t)k * 256 + t) * 2 + (c & 1);
 }
 
 // ---- fp32, serialConjugate.c operation order ---------------------------------

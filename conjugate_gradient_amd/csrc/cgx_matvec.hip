@@ -196,6 +196,130 @@ __global__ __launch_bounds__(kNT) void k_matvec_f64(
     ts_end(ts);
 }
 
+// ---------------------------------------------------------------------------
+// The matVec of a small system's two-launch iteration with the previous
+// iteration's p update folded in (one GPU, n <= kFusePMax): p_k is never
+// formed by a pass of its own -- every wave forms the chunks it multiplies,
+//   p_k[j] = r_k[j] + beta p_{k-1}[j],   beta = r.r_k / r.r_{k-1}
+// (serialConjugate.c:239-243, the expression k_update_xp_f64 evaluates, so
+// the same bits), multiplies them, and the wave that owns row i also stores
+// p_k[i] into the other p buffer (p_{k-1} and p_k never share one: no
+// write-after-read race) and adds p_k[i] * (A p_k)[i] to the fused p.Ap.
+// The next kernel (k_update_xr_stop_f64) is then fully parallel: no
+// single-block pass over p at the end of the iteration.
+// Loads of r and p_{k-1} for step c + U go out before the FMAs of step c,
+// like k_matvec_f64's pipeline; the combine waits until the FMA step.
+template <int R, int U>
+__device__ __forceinline__ void fold_load_step(const d2 *const (&arow)[R], const d2 *r2, const d2 *q2, int64_t c,
+                                               d2 (&rv)[U], d2 (&qv)[U], d2 (&av)[R][U]) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        rv[u] = r2[(c + u) * 64];
+        qv[u] = q2[(c + u) * 64];
+    }
+#pragma unroll
+    for (int r = 0; r < R; ++r)
+#pragma unroll
+        for (int u = 0; u < U; ++u) av[r][u] = load_a<1>(arow[r] + (c + u) * 64);
+}
+
+template <int R, int U>
+__device__ __forceinline__ void fold_fma_step(const d2 (&rv)[U], const d2 (&qv)[U], const d2 (&av)[R][U], double beta,
+                                              d2 (&acc)[R]) {
+#pragma unroll
+    for (int u = 0; u < U; ++u) {
+        const d2 pv = rv[u] + beta * qv[u];  // p = r + beta p (k_update_xp_f64's expression)
+#pragma unroll
+        for (int r = 0; r < R; ++r) {
+            acc[r].x = __builtin_fma(av[r][u].x, pv.x, acc[r].x);
+            acc[r].y = __builtin_fma(av[r][u].y, pv.y, acc[r].y);
+        }
+    }
+}
+
+template <int R, int U>
+__global__ __launch_bounds__(kNT) void k_matvec_fold_f64(
+    const double *__restrict__ A, int64_t lda, int64_t rows, int64_t cols, int64_t vec_cols,
+    const double *__restrict__ r, const double *__restrict__ pold, double *__restrict__ pnew, const double *rr_new,
+    const double *rr_old, double *__restrict__ out, double *dot_out, double *partials, unsigned *ticket,
+    const int64_t *gate, int64_t *ts) {
+    if (gate && *gate) return;
+    ts_start(ts);
+    const double beta = cg_ratio(*rr_new, *rr_old);
+    const int lane = threadIdx.x & 63;
+    const int wid = threadIdx.x >> 6;
+    const int64_t ngroups = (rows + R - 1) / R;
+    const int64_t wstride = (int64_t)gridDim.x * (kNT / 64);
+    const int64_t nchunk = vec_cols >> 7;
+    const d2 *r2 = reinterpret_cast<const d2 *>(r) + lane;
+    const d2 *q2 = reinterpret_cast<const d2 *>(pold) + lane;
+    double dacc = 0.0;
+    for (int64_t g = (int64_t)blockIdx.x * (kNT / 64) + wid; g < ngroups; g += wstride) {
+        const int64_t r0 = g * R;
+        int64_t ridx[R];
+        const d2 *arow[R];
+        d2 acc[R];
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            ridx[q] = (r0 + q < rows) ? (r0 + q) : (rows - 1);
+            arow[q] = reinterpret_cast<const d2 *>(A + ridx[q] * lda) + lane;
+            acc[q] = (d2)(0.0);
+        }
+        {
+            d2 ra[U], qa[U], aa[R][U], rb[U], qb[U], ab[R][U];
+            int64_t c = 0;
+            if (c + U <= nchunk) fold_load_step<R, U>(arow, r2, q2, c, ra, qa, aa);
+            while (c + U <= nchunk) {
+                const bool more = c + 2 * U <= nchunk;
+                if (more) fold_load_step<R, U>(arow, r2, q2, c + U, rb, qb, ab);
+                fold_fma_step<R, U>(ra, qa, aa, beta, acc);
+                c += U;
+                if (!more) break;
+                const bool more2 = c + 2 * U <= nchunk;
+                if (more2) fold_load_step<R, U>(arow, r2, q2, c + U, ra, qa, aa);
+                fold_fma_step<R, U>(rb, qb, ab, beta, acc);
+                c += U;
+                if (!more2) break;
+            }
+            for (; c < nchunk; ++c) {
+                const d2 pv = r2[c * 64] + beta * q2[c * 64];
+#pragma unroll
+                for (int q = 0; q < R; ++q) {
+                    const d2 a = load_a<1>(arow[q] + c * 64);
+                    acc[q].x = __builtin_fma(a.x, pv.x, acc[q].x);
+                    acc[q].y = __builtin_fma(a.y, pv.y, acc[q].y);
+                }
+            }
+        }
+        for (int64_t j = (nchunk << 7) + lane; j < cols; j += 64) {  // columns past the last whole chunk
+            const double pj = r[j] + beta * pold[j];
+#pragma unroll
+            for (int q = 0; q < R; ++q) acc[q].x = __builtin_fma(A[ridx[q] * lda + j], pj, acc[q].x);
+        }
+        double mine = 0.0;
+#pragma unroll
+        for (int q = 0; q < R; ++q) {
+            const double sum = wave_sum(acc[q].x + acc[q].y);
+            if (lane == q) mine = sum;
+        }
+        if (lane < R && r0 + lane < rows) {
+            const int64_t i = r0 + lane;
+            const double pi = r[i] + beta * pold[i];
+            pnew[i] = pi;
+            out[i] = mine;
+            dacc += pi * mine;
+        }
+    }
+    grid_sum_last_block(dacc, partials, ticket, dot_out);
+    ts_end(ts);
+}
+
+using FoldFn = decltype(&k_matvec_fold_f64<1, 8>);
+FoldFn pick_fold(int R, int U) {
+    if (R == 1) return U == 2 ? k_matvec_fold_f64<1, 2> : U == 4 ? k_matvec_fold_f64<1, 4> : k_matvec_fold_f64<1, 8>;
+    return U == 2 ? k_matvec_fold_f64<2, 2> : U == 4 ? k_matvec_fold_f64<2, 4> : k_matvec_fold_f64<2, 8>;
+}
+
 using MvFn = void (*)(const double *, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, int, int,
                       const double *, double *, const double *, double *, double *, unsigned *, const int64_t *,
                       int64_t *);
@@ -300,6 +424,20 @@ hipError_t matvec_f64_cols(const MatvecPlan &pl, const double *A, int64_t lda, i
     MvFn fn = pick_mv(pl.R, pl.U, pl.nt);
     hipLaunchKernelGGL(fn, dim3(pl.blocks), dim3(kNT), 0, s, A, lda, rows, cols, cols, col_first >> 7,
                        col_count >> 7, 0, accumulate ? 1 : 0, v, out, pown, dot_out, ws.partials,
+                       ws.tickets + T_MATVEC, gate, ts);
+    return hipGetLastError();
+}
+
+hipError_t matvec_fold_f64(const MatvecPlan &pl, const double *A, int64_t lda, int64_t rows, int64_t cols,
+                           const double *r, const double *pold, double *pnew, const double *rr_new,
+                           const double *rr_old, double *out, double *dot_out, const RedWs &ws, hipStream_t s,
+                           const int64_t *gate, int64_t *ts) {
+    if (rows <= 0) return hipSuccess;
+    if (((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(r) | reinterpret_cast<uintptr_t>(pold)) & 15) ||
+        (lda & 1))
+        return hipErrorInvalidValue;
+    hipLaunchKernelGGL(pick_fold(pl.R == 1 ? 1 : 2, pl.U), dim3(pl.blocks), dim3(kNT), 0, s, A, lda, rows, cols,
+                       cols & ~int64_t(127), r, pold, pnew, rr_new, rr_old, out, dot_out, ws.partials,
                        ws.tickets + T_MATVEC, gate, ts);
     return hipGetLastError();
 }

@@ -231,6 +231,27 @@ __device__ __forceinline__ void poisson_p_step(const double *__restrict__ rh, co
     }
 }
 
+// XCD bands (CGX_POISSON_BANDS=1, one item range of whole runs): the
+// blocks of XCD x (blockIdx % 8, the dispatcher's round-robin) take the
+// items of the x-th eighth of the runs, strip-fastest, so an item's left and
+// right neighbours (whose edge columns it loads as side points) and the item
+// below (whose first two rows are its last two) are fetched through the same
+// L2 at about the same time.  Without bands those neighbours are taken by
+// blocks of other XCDs.  The v-th item of this block within its band, or -1.
+struct Band {
+    int64_t first, count, stride, start;
+};
+__device__ __forceinline__ Band band_of(int64_t w0, int64_t nitems, int64_t nstrips) {
+    Band b;
+    const int64_t nruns = nitems / nstrips, x = blockIdx.x % 8;
+    const int64_t r0 = nruns * x / 8, r1 = nruns * (x + 1) / 8;
+    b.first = w0 + r0 * nstrips;
+    b.count = (r1 - r0) * nstrips;
+    b.stride = gridDim.x / 8;
+    b.start = blockIdx.x / 8;
+    return b;
+}
+
 // Work items [w0, w0+cnt1) then [w2, w2+cnt2) (the whole slab, or, when
 // the r halo exchange overlaps the kernel, the slab's interior runs first
 // and its two edge runs after the exchange).
@@ -241,11 +262,13 @@ struct ItemRanges {
 template <int RB, bool NT, bool FIRST, bool HT>
 __device__ __forceinline__ double poisson_p_body(const double *__restrict__ rh, const double *__restrict__ poh,
                                                  double *__restrict__ pnh, int64_t mloc, int64_t m, int64_t nstrips,
-                                                 int64_t rpi, ItemRanges ir, double beta, double *edge) {
+                                                 int64_t rpi, ItemRanges ir, double beta, double *edge, int bands) {
     double acc = 0.0;
     int par = 0;
-    for (int64_t v = blockIdx.x; v < ir.cnt1 + ir.cnt2; v += gridDim.x) {
-        const int64_t w = v < ir.cnt1 ? ir.w0 + v : ir.w2 + (v - ir.cnt1);
+    const Band bd = bands ? band_of(ir.w0, ir.cnt1, nstrips) : Band{0, 0, 0, 0};
+    const int64_t vend = bands ? bd.count : ir.cnt1 + ir.cnt2;
+    for (int64_t v = bands ? bd.start : blockIdx.x; v < vend; v += bands ? bd.stride : gridDim.x) {
+        const int64_t w = bands ? bd.first + v : v < ir.cnt1 ? ir.w0 + v : ir.w2 + (v - ir.cnt1);
         const StripLane L = strip_lane(w, nstrips, m);
         const int64_t i0 = (w / nstrips) * rpi;
         const int64_t i1 = (i0 + rpi < mloc) ? i0 + rpi : mloc;
@@ -268,7 +291,7 @@ __global__ __launch_bounds__(kNT) void k_poisson_p_f64(const double *__restrict_
                                                        double *__restrict__ pnh, int64_t mloc, int64_t m,
                                                        int64_t nstrips, int64_t rpi, ItemRanges ir, const double *rr,
                                                        const double *rsold, int first, ConvArgs cv, double *dot_out,
-                                                       int add_to_out, double *partials, unsigned *ticket) {
+                                                       int add_to_out, double *partials, unsigned *ticket, int bands) {
     static_assert(RB <= kEdgeRB, "edge buffer");
     __shared__ double edge[2 * kWaves * 2 * kEdgeRB];
     if (cv.kdone) {
@@ -279,9 +302,10 @@ __global__ __launch_bounds__(kNT) void k_poisson_p_f64(const double *__restrict_
         }
     }
     // p_0 = r_0 (first) has its own instantiation: no p_{k-1} loads
-    const double acc = first ? poisson_p_body<RB, NT, true, HT>(rh, poh, pnh, mloc, m, nstrips, rpi, ir, 0.0, edge)
+    const double acc = first ? poisson_p_body<RB, NT, true, HT>(rh, poh, pnh, mloc, m, nstrips, rpi, ir, 0.0, edge,
+                                                                bands)
                              : poisson_p_body<RB, NT, false, HT>(rh, poh, pnh, mloc, m, nstrips, rpi, ir,
-                                                                 cg_ratio(*rr, *rsold), edge);
+                                                                 cg_ratio(*rr, *rsold), edge, bands);
     grid_sum_last_block(acc, partials, ticket, dot_out, add_to_out != 0);
 }
 
@@ -345,18 +369,20 @@ __global__ __launch_bounds__(kNT) void k_poisson_xr_f64(const double *__restrict
                                                         double *__restrict__ r, int64_t mloc, int64_t m,
                                                         int64_t nstrips, int64_t rpi, int64_t nitems, int reverse,
                                                         const double *rsold, const double *pAp, double *rr_out,
-                                                        double *partials, unsigned *ticket, const int64_t *gate) {
+                                                        double *partials, unsigned *ticket, const int64_t *gate,
+                                                        int bands) {
     static_assert(RB <= kEdgeRB, "edge buffer");
     __shared__ double edge[2 * kWaves * 2 * kEdgeRB];
     if (gate && *gate) return;
     const double alpha = cg_ratio(*rsold, *pAp);
     double acc = 0.0;
     int par = 0;
-    for (int64_t v = blockIdx.x; v < nitems; v += gridDim.x) {
-        // reverse: walk the slab from its end, where the previous kernel
-        // (k_poisson_p, forward) last wrote p_k, so the first bytes read may
-        // still sit in the 256 MB MALL
-        const int64_t w = reverse ? nitems - 1 - v : v;
+    const Band bd = bands ? band_of(0, nitems, nstrips) : Band{0, nitems, (int64_t)gridDim.x, (int64_t)blockIdx.x};
+    for (int64_t v = bd.start; v < bd.count; v += bd.stride) {
+        // reverse: walk the slab (each band) from its end, where the previous
+        // kernel (k_poisson_p, forward) last wrote p_k, so the first bytes read
+        // may still sit in the 256 MB MALL
+        const int64_t w = bd.first + (reverse ? bd.count - 1 - v : v);
         const StripLane L = strip_lane(w, nstrips, m);
         const int64_t i0 = (w / nstrips) * rpi;
         const int64_t i1 = (i0 + rpi < mloc) ? i0 + rpi : mloc;
@@ -423,7 +449,7 @@ hipError_t stencil5_f64(const double *ph, int64_t mloc, int64_t m, double *Ap, d
 // short items keep the rows in flight in a narrow band (64- and 128-row items
 // are 7-20 % slower).
 struct PoissonPlan {
-    int rb, nt, ht;
+    int rb, nt, ht, bands;
     int64_t nstrips, rpi, nitems, grid;
 };
 static PoissonPlan poisson_plan(int64_t mloc, int64_t m) {
@@ -431,6 +457,7 @@ static PoissonPlan poisson_plan(int64_t mloc, int64_t m) {
     p.rb = env_int("CGX_STENCIL_RB", 8);
     p.nt = env_int("CGX_STENCIL_NT", 1);
     p.ht = env_int("CGX_STENCIL_HALO_T", 1);
+    p.bands = env_int("CGX_POISSON_BANDS", 0);
     p.nstrips = (m + 2 * kNT - 1) / (2 * kNT);
     p.rpi = std::max(1, env_int("CGX_STENCIL_ROWS", 8));
     p.nitems = p.nstrips * ((mloc + p.rpi - 1) / p.rpi);
@@ -468,9 +495,11 @@ static void launch_poisson_p(const PoissonPlan &pl, hipStream_t s, const double 
                              double *pap_out, const RedWs &ws, ItemRanges ir, int add_to_out) {
     auto fn = pl.nt ? (pl.ht ? k_poisson_p_f64<RB, true, true> : k_poisson_p_f64<RB, true, false>)
                     : k_poisson_p_f64<RB, false, false>;
-    const int64_t grid = resident_grid(reinterpret_cast<const void *>(fn), ir.cnt1 + ir.cnt2);
+    int64_t grid = resident_grid(reinterpret_cast<const void *>(fn), ir.cnt1 + ir.cnt2);
+    const int bands = pl.bands && ir.cnt2 == 0 && ir.cnt1 % pl.nstrips == 0 && grid >= 8;
+    if (bands) grid &= ~int64_t(7);
     hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(kNT), 0, s, rh, poh, pnh, mloc, m, pl.nstrips, pl.rpi, ir, rr,
-                       rsold, first, cv, pap_out, add_to_out, ws.partials, ws.tickets + T_MATVEC);
+                       rsold, first, cv, pap_out, add_to_out, ws.partials, ws.tickets + T_MATVEC, bands);
 }
 template <int RB>
 static void launch_poisson_xr(const PoissonPlan &pl, hipStream_t s, const double *pnh, double *x, double *r,
@@ -478,10 +507,12 @@ static void launch_poisson_xr(const PoissonPlan &pl, hipStream_t s, const double
                               const RedWs &ws, const int64_t *gate) {
     auto fn = pl.nt ? (pl.ht ? k_poisson_xr_f64<RB, true, true> : k_poisson_xr_f64<RB, true, false>)
                     : k_poisson_xr_f64<RB, false, false>;
-    const int64_t grid = resident_grid(reinterpret_cast<const void *>(fn), pl.nitems);
+    int64_t grid = resident_grid(reinterpret_cast<const void *>(fn), pl.nitems);
+    const int bands = pl.bands && grid >= 8;
+    if (bands) grid &= ~int64_t(7);
     hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(kNT), 0, s, pnh, x, r, mloc, m, pl.nstrips, pl.rpi,
                        pl.nitems, env_int("CGX_STENCIL_REVERSE", 1), rsold, pAp, rr_out, ws.partials,
-                       ws.tickets + T_XR, gate);
+                       ws.tickets + T_XR, gate, bands);
 }
 
 hipError_t poisson_p_f64(const double *rh, const double *poh, double *pnh, int64_t mloc, int64_t m, const double *rr,

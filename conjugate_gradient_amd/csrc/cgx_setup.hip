@@ -60,7 +60,7 @@ int alloc_shard(cgx_ctx *c, Shard &s) {
             for (int q = 0; q < s.ncopy; ++q) HIPT(hipEventCreateWithFlags(&s.ev_loaded[b][q], hipEventDisableTiming));
         }
         for (int q = 0; q < s.ncopy; ++q) HIPT(hipStreamCreateWithFlags(&s.copy[q], hipStreamNonBlocking));
-        TRY(dmalloc(&s.sym_prow, (size_t)ntiles * 128 * 8));
+        TRY(dmalloc(&s.sym_prow, (size_t)ntiles * 2 * 128 * 8));  // a row partial per unit (half tile), at most
         TRY(dmalloc(&s.sym_pcol, (size_t)ntiles * 128 * 8));
         s.sym_grid = sym_grid(s.dev);
         // CGX_STREAM_RESIDENT_MB: the first tiles (res_rows counts tiles here) stay in HBM
@@ -101,7 +101,7 @@ int alloc_shard(cgx_ctx *c, Shard &s) {
         const size_t tbytes = (size_t)ntiles * 128 * 128 * 8;
         TRY(dmalloc(&s.A, tbytes));
         HIPT(hipMemsetAsync(s.A, 0, tbytes, s.stream));  // padding rows / columns stay zero
-        TRY(dmalloc(&s.sym_prow, (size_t)ntiles * 128 * 8));
+        TRY(dmalloc(&s.sym_prow, (size_t)ntiles * 2 * 128 * 8));  // a row partial per unit (half tile), at most
         TRY(dmalloc(&s.sym_pcol, (size_t)ntiles * 128 * 8));
         s.sym_grid = sym_grid(s.dev);
     } else {
@@ -116,6 +116,9 @@ int alloc_shard(cgx_ctx *c, Shard &s) {
         s.r = s.rh + c->m * es;
         TRY(dmalloc(&s.p2, (s.nloc + 2 * c->m) * es));
         HIPT(hipMemsetAsync(s.p2, 0, (s.nloc + 2 * c->m) * es, s.stream));
+    } else if (c->fold_p) {  // the folded matVec reads r over all lda columns: zero past n
+        TRY(dmalloc(&s.r, c->lda * es));
+        HIPT(hipMemsetAsync(s.r, 0, c->lda * es, s.stream));
     } else {
         TRY(dmalloc(&s.r, s.nloc * es));
     }
@@ -124,6 +127,10 @@ int alloc_shard(cgx_ctx *c, Shard &s) {
     const int64_t plen = (c->op == OP_POISSON) ? s.nloc + 2 * c->m : c->lda;
     const int64_t xlen = (c->op == OP_POISSON) ? c->n : c->lda;
     TRY(dmalloc(&s.pfull, plen * es));
+    if (c->fold_p) {
+        TRY(dmalloc(&s.p_alt, plen * es));
+        HIPT(hipMemsetAsync(s.p_alt, 0, plen * es, s.stream));
+    }
     s.pown = (c->op == OP_POISSON) ? s.pfull + c->m * es : s.pfull + s.row0 * es;
     TRY(dmalloc(&s.scal, kScalSlots * 8));
     if (c->mode == M_RCCL && c->nranks > 1) TRY(dmalloc(&s.xfull, xlen * es));
@@ -181,6 +188,13 @@ int alloc_shard(cgx_ctx *c, Shard &s) {
         for (auto &e : s.ev_prog) HIPT(hipEventCreateWithFlags(&e, hipEventDisableTiming));
     if (!f32ref(c) && c->op == OP_DENSE && !(c->flags & CGX_SYMMETRIC))
         s.plan = plan_matvec_f64(s.dev, s.nloc, 0, 0, -1, 0, c->lda);
+    if (c->fold_p) {
+        // the folded matVec reads r and p_{k-1} per chunk of A: two rows per
+        // wave halve those reads per byte of A (R = 1: 30.8 vs 22.8 us at n =
+        // 4096), and at n = 2048 four chunks in flight beat eight
+        const int R = c->n >= 2048 ? 2 : 0, U = c->n >= 2048 ? (c->n <= 2048 ? 4 : 8) : 0;
+        s.fold_plan = plan_matvec_f64(s.dev, s.nloc, R, U, -1, 0, c->lda);
+    }
     HIPT(hipStreamSynchronize(s.stream));
     return CGX_OK;
 }
@@ -189,8 +203,8 @@ void free_shard(Shard &s) {
     (void)hipSetDevice(s.dev);
     if (s.stream) (void)hipStreamSynchronize(s.stream);
     if (s.comm) ncclCommDestroy(s.comm);
-    for (char *p : {s.A, s.b, s.x, s.rh ? s.rh : s.r, s.p2, s.Ap, s.pfull, s.xfull, s.scal, s.sym_prow, s.sym_pcol,
-                    s.sym_stage})
+    for (char *p : {s.A, s.b, s.x, s.rh ? s.rh : s.r, s.p2, s.Ap, s.pfull, s.p_alt, s.xfull, s.scal, s.sym_prow,
+                    s.sym_pcol, s.sym_stage})
         if (p) (void)hipFree(p);
     if (s.ws.partials) (void)hipFree(s.ws.partials);
     if (s.ws.tickets) (void)hipFree(s.ws.tickets);
@@ -280,6 +294,13 @@ int alloc_overlap(cgx_ctx *c) {
 // in one block: n doubles read twice and written once by one CU, a few us at
 // n = 8192); CGX_FUSE_P=0 keeps three launches, =1 uses two at any n.
 constexpr int64_t kFusePMax = 8192;
+// ... and up to kFoldPMax the p update is folded into the next matVec
+// (do_iteration_fold_p): measured per iteration (profiles/r03_iteration_floor.jsonl,
+// device clock) 9.6 vs 10.2 us at n = 512, 11.8 vs 12.0 at 1024, 14.0-14.1 vs
+// 14.3 at 2048, 30.5-30.6 vs 30.8 at 4096; at 8192 the matVec's extra reads
+// of r and p_{k-1} cost more than the single-block pass they replace (95.0
+// vs 91.6), so it keeps k_update_xrp_f64.
+constexpr int64_t kFoldPMax = 4096;
 static bool can_fuse_p(const cgx_ctx *c) {
     if (c->mode != M_SINGLE || c->op != OP_DENSE || f32ref(c)) return false;
     if (c->flags & (CGX_SYMMETRIC | CGX_HOST_STREAM)) return false;
@@ -306,6 +327,10 @@ static bool can_fuse_ref_dot(const cgx_ctx *c) {
 int finish_create(cgx_ctx *c, cgx_ctx **out) {
     c->overlap = can_overlap(c);
     c->fused_p = can_fuse_p(c);
+    {  // the folded form of the two-launch iteration (CGX_FOLD_P=0 / 1: never / at any fused n)
+        const char *e = std::getenv("CGX_FOLD_P");
+        c->fold_p = c->fused_p && (e && *e ? *e == '1' : c->n <= kFoldPMax);
+    }
     c->ref_mv_dot = can_fuse_ref_dot(c);
     c->ref_fused = c->ref_mv_dot && c->mode == M_SINGLE;
     if (c->op == OP_POISSON) {  // CGX_POISSON_FUSED=0: the three-kernel split (stencil, r, x/p)

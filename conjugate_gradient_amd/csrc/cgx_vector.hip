@@ -235,6 +235,61 @@ __global__ __launch_bounds__(kNT) void k_update_xrp_f64(int64_t n, double *__res
     ts_end(ts);
 }
 
+// The update of the folded two-launch iteration (k_matvec_fold_f64 formed
+// p_k): x += alpha p_k; r -= alpha Ap; r.r, and the block that sums the r.r
+// partials decides the stop (serialConjugate.c:235).  Fully parallel: the
+// p update is the next matVec's.  The expressions are k_update_xrp_f64's.
+template <bool VEC>
+__global__ __launch_bounds__(kNT) void k_update_xr_stop_f64(int64_t n, double *__restrict__ x, double *__restrict__ r,
+                                                            const double *__restrict__ p, const double *__restrict__ Ap,
+                                                            const double *rsold, const double *pAp, double *rr_out,
+                                                            double *partials, unsigned *ticket, const int64_t *gate,
+                                                            ConvArgs cv, int64_t *ts) {
+    if (gate && *gate) return;
+    ts_start(ts);
+    const double alpha = cg_ratio(*rsold, *pAp);
+    double acc = 0.0;
+    if constexpr (VEC) {
+        CGX_VEC_LOOP_BEGIN
+        d2 xv[kVU], rv[kVU], pv[kVU], av[kVU];
+#pragma unroll
+        for (int u = 0; u < kVU; ++u)
+            if (ok[u]) {
+                const int64_t i = 2 * (base + u * kNT);
+                xv[u] = ld2(x + i); rv[u] = ld2(r + i); pv[u] = ld2(p + i); av[u] = ld2(Ap + i);
+            }
+#pragma unroll
+        for (int u = 0; u < kVU; ++u)
+            if (ok[u]) {
+                const int64_t i = 2 * (base + u * kNT);
+                st2(x + i, xv[u] + alpha * pv[u]);
+                const d2 ri = rv[u] - alpha * av[u];
+                st2(r + i, ri);
+                acc += ri.x * ri.x + ri.y * ri.y;
+            }
+        CGX_VEC_LOOP_END
+        if ((n & 1) && blockIdx.x == 0 && threadIdx.x == 0) {
+            const int64_t i = n - 1;
+            x[i] = x[i] + alpha * p[i];
+            const double ri = r[i] - alpha * Ap[i];
+            r[i] = ri;
+            acc += ri * ri;
+        }
+    } else {
+        for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kNT) {
+            x[i] = x[i] + alpha * p[i];
+            const double ri = r[i] - alpha * Ap[i];
+            r[i] = ri;
+            acc += ri * ri;
+        }
+    }
+    double rr;
+    if (grid_sum_keep_last(acc, partials, ticket, rr_out, rr) && cv.kdone && cv.eps >= 0.0 && sqrt(rr) < cv.eps &&
+        threadIdx.x == 0)
+        record_convergence(cv, cv.k + 1, rr);
+    ts_end(ts);
+}
+
 // The solver's split of the x/r/p updates (fp64): x's update moves into the
 // p update, which reads p anyway -- 24 + 40 B per element instead of 48 + 24.
 // r -= alpha Ap; r.r   (alpha = rsold / pAp)
@@ -468,6 +523,22 @@ hipError_t update_xrp_f64(int64_t n, double *x, double *r, double *p, const doub
     cv.hrec = hrec;
     hipLaunchKernelGGL(vec ? k_update_xrp_f64<true> : k_update_xrp_f64<false>, dim3(grid_vec(n)), dim3(kNT), 0, s,
                        n, x, r, p, Ap, rsold, pAp, rr_out, ws.partials, ws.tickets + T_XR, gate, cv, ts);
+    return hipGetLastError();
+}
+
+hipError_t update_xr_stop_f64(int64_t n, double *x, double *r, const double *p, const double *Ap,
+                              const double *rsold, const double *pAp, double *rr_out, const RedWs &ws, hipStream_t s,
+                              const int64_t *gate, double eps, int64_t k, int64_t *kdone, double *rrfinal,
+                              int64_t *hrec, int64_t *ts) {
+    const bool vec = al16(x) && al16(r) && al16(p) && al16(Ap);
+    ConvArgs cv;
+    cv.eps = eps;
+    cv.k = k;
+    cv.kdone = kdone;
+    cv.rrfinal = rrfinal;
+    cv.hrec = hrec;
+    hipLaunchKernelGGL(vec ? k_update_xr_stop_f64<true> : k_update_xr_stop_f64<false>, dim3(grid_vec(n)), dim3(kNT),
+                       0, s, n, x, r, p, Ap, rsold, pAp, rr_out, ws.partials, ws.tickets + T_XR, gate, cv, ts);
     return hipGetLastError();
 }
 

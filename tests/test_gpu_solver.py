@@ -480,18 +480,23 @@ def test_f32ref_nonfinite_A_follows_the_reference():
     assert np.array_equal(np.isnan(x), np.isnan(xo)) and np.isnan(x).any()
 
 
-@pytest.mark.parametrize("n,seed", [(512, 1), (1000, 2), (8192, 3), (8193, 4)])
+@pytest.mark.parametrize("n,seed", [(130, 5), (512, 1), (1000, 2), (2048, 6), (4096, 7), (8192, 3), (8193, 4)])
 def test_two_launch_iteration_bitwise_equals_three(monkeypatch, n, seed):
-    """Small dense fp64 systems on one GPU iterate in two launches (matVec +
-    k_update_xrp_f64, whose last block forms p; CGX_FUSE_P) instead of three.
-    Same expressions, same order: x bit for bit and the same loop count as the
-    three-launch iteration -- device-gated, host-checked and fixed-count; with
-    several blocks (n = 8192: r handed to the last block write-through) and
-    odd n.  Both agree with the fp64 oracle."""
+    """Small dense fp64 systems on one GPU iterate in two launches instead of
+    three (CGX_FUSE_P): matVec + k_update_xrp_f64, whose last block forms p;
+    or, folded (CGX_FOLD_P=1), k_matvec_fold_f64 forming p_k as it multiplies
+    it + the fully parallel k_update_xr_stop_f64.  Same expressions, same
+    order: x bit for bit and the same loop count as the three-launch iteration
+    -- device-gated, host-checked, fixed-count and in pieces; with several
+    blocks (n = 8192: r handed to the last block write-through), odd n, rows
+    not a whole number of 128-column chunks (the fold's tail columns) and both
+    row plans (R = 2 at n = 2048, R = 1 at 4096-8192).  All agree with the
+    fp64 oracle."""
     A, b = oracle.spd_hash(n, seed=seed)
     res = {}
-    for fuse in ("1", "0"):
+    for form, fuse, fold in (("three", "0", "0"), ("two", "1", "0"), ("fold", "1", "1")):
         monkeypatch.setenv("CGX_FUSE_P", fuse)
+        monkeypatch.setenv("CGX_FOLD_P", fold)
         for gated in ("1", "0"):
             monkeypatch.setenv("CGX_GATED", gated)
             with cg.Solver(n) as s:
@@ -504,8 +509,8 @@ def test_two_launch_iteration_bitwise_equals_three(monkeypatch, n, seed):
                 d1, _ = s.iterate(3)
                 d2, conv = s.iterate(100, eps=1e-10)
                 xp = s.get_x()
-            res[(fuse, gated)] = (x, st.iterations, xf, stf.iterations, xp, d1 + d2, conv)
-    ref = res[("0", "0")]
+            res[(form, gated)] = (x, st.iterations, xf, stf.iterations, xp, d1 + d2, conv)
+    ref = res[("three", "0")]
     for key, (x, it, xf, itf, xp, dp, conv) in res.items():
         assert it == ref[1] and np.array_equal(x, ref[0]), key
         assert itf == 9 and np.array_equal(xf, ref[2]), key
