@@ -457,7 +457,9 @@ static PoissonPlan poisson_plan(int64_t mloc, int64_t m) {
     p.rb = env_int("CGX_STENCIL_RB", 8);
     p.nt = env_int("CGX_STENCIL_NT", 1);
     p.ht = env_int("CGX_STENCIL_HALO_T", 1);
-    p.bands = env_int("CGX_POISSON_BANDS", 0);
+    // XCD bands: 1341 vs 1288 it/s at m = 8192, two interleaved rounds
+    // (profiles/r03_poisson_bands_ab.jsonl); CGX_POISSON_BANDS=0 turns them off
+    p.bands = env_int("CGX_POISSON_BANDS", 1);
     p.nstrips = (m + 2 * kNT - 1) / (2 * kNT);
     p.rpi = std::max(1, env_int("CGX_STENCIL_ROWS", 8));
     p.nitems = p.nstrips * ((mloc + p.rpi - 1) / p.rpi);
