@@ -711,7 +711,9 @@ int cgx_set_matvec_plan(cgx_ctx *c, int rows_per_wave, int chunks_in_flight, int
         TRY(set_dev(s));
         MatvecPlan pl = plan_matvec_f64(s.dev, s.nloc, R, U, nontemporal, blocks_per_cu, c->lda);
         s.plan = pl;
+        s.fold_plan = pl;  // the folded matVec follows the same rows per wave and grid (same p.Ap order)
     }
+    if (R > 2) c->fold_p = false;  // the folded matVec has one or two rows per wave
     return CGX_OK;
 }
 

@@ -189,11 +189,11 @@ int alloc_shard(cgx_ctx *c, Shard &s) {
     if (!f32ref(c) && c->op == OP_DENSE && !(c->flags & CGX_SYMMETRIC))
         s.plan = plan_matvec_f64(s.dev, s.nloc, 0, 0, -1, 0, c->lda);
     if (c->fold_p) {
-        // the folded matVec reads r and p_{k-1} per chunk of A: two rows per
-        // wave halve those reads per byte of A (R = 1: 30.8 vs 22.8 us at n =
-        // 4096), and at n = 2048 four chunks in flight beat eight
-        const int R = c->n >= 2048 ? 2 : 0, U = c->n >= 2048 ? (c->n <= 2048 ? 4 : 8) : 0;
-        s.fold_plan = plan_matvec_f64(s.dev, s.nloc, R, U, -1, 0, c->lda);
+        // The folded matVec keeps the plain plan's rows per wave and grid: the
+        // fused p.Ap partials then add in the same order (x bit for bit the
+        // other forms').  At n = 2048 (R = 2) four chunks in flight beat eight.
+        s.fold_plan = plan_matvec_f64(s.dev, s.nloc, s.plan.R, c->n == 2048 ? 4 : s.plan.U, -1, 0, c->lda);
+        if (s.fold_plan.blocks != s.plan.blocks) s.fold_plan = s.plan;
     }
     HIPT(hipStreamSynchronize(s.stream));
     return CGX_OK;
@@ -296,11 +296,13 @@ int alloc_overlap(cgx_ctx *c) {
 constexpr int64_t kFusePMax = 8192;
 // ... and up to kFoldPMax the p update is folded into the next matVec
 // (do_iteration_fold_p): measured per iteration (profiles/r03_iteration_floor.jsonl,
-// device clock) 9.6 vs 10.2 us at n = 512, 11.8 vs 12.0 at 1024, 14.0-14.1 vs
-// 14.3 at 2048, 30.5-30.6 vs 30.8 at 4096; at 8192 the matVec's extra reads
-// of r and p_{k-1} cost more than the single-block pass they replace (95.0
-// vs 91.6), so it keeps k_update_xrp_f64.
-constexpr int64_t kFoldPMax = 4096;
+// device clock) 9.6 vs 10.2 us at n = 512, 11.8 vs 12.0 at 1024, 13.9-14.0 vs
+// 14.2 at 2048.  Above, the matVec's plan has one row per wave, and the
+// fold's extra reads of r and p_{k-1} per chunk of A cost about what the
+// single-block pass saves (n = 4096: 31.1 either way with two rows per wave,
+// whose p.Ap partials would add in another order; 37.4 with one), so
+// k_update_xrp_f64 stays.
+constexpr int64_t kFoldPMax = 2048;
 static bool can_fuse_p(const cgx_ctx *c) {
     if (c->mode != M_SINGLE || c->op != OP_DENSE || f32ref(c)) return false;
     if (c->flags & (CGX_SYMMETRIC | CGX_HOST_STREAM)) return false;
