@@ -160,7 +160,9 @@ constexpr int kEvPairs = 256;
 // CGX_PHASES: the kernels of an iteration that stamp their start / end
 // (cgx_kernels.h kTsSlot), in the order they run on the first shard's stream.
 enum TsKernel { TK_OWN = 0, TK_MV = 1, TK_UR = 2, TK_UXP = 3, kTsKern = 4 };
-constexpr int kTsIters = 256;  // iterations stamped before a resolve (256 x 4 x 16 KiB)
+// iterations stamped before a resolve (1024 x 4 x 16 KiB = 64 MiB of HBM):
+// a timed run of up to 1024 iterations never resolves (copies, waits) inside
+constexpr int kTsIters = 1024;
 constexpr size_t kXStageMax = 64u << 20;
 constexpr int kStreamBufs = 3;
 constexpr int kMaxCopyStreams = 4;
@@ -225,6 +227,7 @@ struct Shard {
     // zero where no kernel stamped; ts_cur = the ring row of the iteration
     // being enqueued (-1 between iterations), ts_used = rows since the resolve
     int64_t *ts_dev = nullptr;
+    int64_t *ts_host = nullptr;  // pinned copy for the resolve, allocated at the first one
     int ts_used = 0, ts_cur = -1;
     // overlap of the p exchange with the own-column-block matVec
     hipStream_t cstream = nullptr;

@@ -72,8 +72,11 @@ int phase_resolve(cgx_ctx *c) {
     if (s.ts_used == 0) return CGX_OK;
     TRY(set_dev(s));
     const size_t words = (size_t)s.ts_used * kTsKern * kTsSlot;
-    std::vector<int64_t> h(words);
-    HIPT(hipMemcpyAsync(h.data(), s.ts_dev, words * 8, hipMemcpyDeviceToHost, s.stream));
+    if (!s.ts_host)
+        HIPT(hipHostMalloc(reinterpret_cast<void **>(&s.ts_host), (size_t)kTsIters * kTsKern * kTsSlot * 8,
+                           hipHostMallocDefault));
+    const int64_t *h = s.ts_host;
+    HIPT(hipMemcpyAsync(s.ts_host, s.ts_dev, words * 8, hipMemcpyDeviceToHost, s.stream));
     TRY(rank_wait_stream(c, s.stream, "the phase timestamps"));
     HIPT(hipMemsetAsync(s.ts_dev, 0, words * 8, s.stream));
     s.ts_used = 0;
@@ -90,7 +93,7 @@ int phase_resolve(cgx_ctx *c) {
         int64_t st[kTsKern], en[kTsKern];
         int first = -1, last = -1;
         for (int k = 0; k < kTsKern; ++k) {
-            const int64_t *q = h.data() + ((size_t)i * kTsKern + k) * kTsSlot;
+            const int64_t *q = h + ((size_t)i * kTsKern + k) * kTsSlot;
             st[k] = q[0];
             en[k] = 0;
             for (int b = 1; b < kTsSlot; ++b) en[k] = std::max(en[k], q[b]);

@@ -213,6 +213,7 @@ void free_shard(Shard &s) {
     if (s.h_rec) (void)hipHostFree(s.h_rec);
     for (auto e : s.ev_t) (void)hipEventDestroy(e);
     if (s.ts_dev) (void)hipFree(s.ts_dev);
+    if (s.ts_host) (void)hipHostFree(s.ts_host);
     for (auto e : s.ev_prog)
         if (e) (void)hipEventDestroy(e);
     if (s.ev_sync) (void)hipEventDestroy(s.ev_sync);

@@ -375,11 +375,11 @@ def test_phase_times_tile_the_iteration(kind):
     """CGX_PHASES: the iteration's kernels stamp their start and end on the
     device clock; the phases are resolved after the fact.  Every kernel phase
     gets one sample per iteration (the gap and the iteration one fewer), more
-    iterations than one stamp ring holds (256) are carried across resolves,
+    iterations than one stamp ring holds (1024) are carried across resolves,
     and the consecutive phases tile the iteration: their means add up to the
     mean iteration.  A converged, device-gated solve stops sampling where the
     kernels stop running."""
-    n, steps = {"small_fused": 2048, "single": 16384}.get(kind, 4096), 600
+    n, steps = {"small_fused": 2048, "single": 16384}.get(kind, 4096), 1100  # > the 1024-iteration stamp ring
     devices = {"shards_overlap": [0, 0], "shards_plain": [0, 0, 0]}.get(kind)  # 4095/3 rows: no overlap
     if kind == "shards_plain":
         n = 4095
