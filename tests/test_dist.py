@@ -32,6 +32,8 @@ def _worker(rank, world, port, q):
         sm = bench.sum_over_ranks(dist, 1.0)
         n = 65536
         nloc = n // w
+        objs = bench.gather_objects(dist, {"rank": r, "pci_bus_id": f"0000:{r:02x}:00.0"})
+        assert [o["rank"] for o in objs] == list(range(w)), objs  # every rank's, in rank order
         q.put((r, got == bytes(range(128)), mx, sm, bench.matvec_bytes(n, nloc)))
         dist.barrier()
         dist.destroy_process_group()
@@ -75,3 +77,31 @@ def test_traffic_lookup_names_its_source():
         t, src = bench.pmc_traffic(65536, g)
         assert t is not None and 1.0 <= t / bench.matvec_bytes(65536, 65536 // g) < 1.01, g
     assert bench.pmc_traffic(4096, 1) == (None, None)
+
+
+def _phases(scale):
+    import conjugate_gradient_amd as cg
+    base = dict(zip(cg.PHASE_NAMES, (80.0, 2.0, 550.0, 15.0, 4.5, 15.0, 4.5, 3.0, 674.0)))
+    return {k: {"median_us": v * scale, "mean_us": v * scale, "samples": 19} for k, v in base.items()}
+
+
+def test_phase_summary_tiles_the_step():
+    """The N>1 line's breakdown: per-rank medians, the max over ranks, and the
+    tiling phases (all but `iteration`) added up against ms_per_step."""
+    out = bench.phase_summary([_phases(1.0), _phases(1.02)], ms_per_step=0.6885)
+    assert out["iterations_sampled"] == 19 and len(out["per_rank"]) == 2
+    assert out["max_over_ranks"]["matvec"] == 561.0
+    tiles = (80 + 2 + 550 + 15 + 4.5 + 15 + 4.5 + 3) * 1.02
+    assert abs(out["tiling_sum_ms_per_rank"][1] - tiles / 1e3) < 1e-4
+    assert abs(out["tiling_sum_over_ms_per_step"] - tiles / 1e3 / 0.6885) < 1e-9
+    assert abs(out["tiling_mean_sum_over_ms_per_step"] - tiles / 1e3 / 0.6885) < 1e-9
+
+
+def test_rccl_summary_counts_devices():
+    """`rccl`: the ranks' own view, distinct devices by PCI bus id; a device
+    rank 0 cannot see is named as such (no GPU here: none visible)."""
+    ranks = [{"rccl_nranks": 2, "rccl_device": d, "rccl_rank": r, "device": d, "pci_bus_id": f"0000:{0x11 + d:02x}:00.0"}
+             for r, d in ((0, 0), (1, 1))]
+    out = bench.rccl_summary(ranks, solver_device=0)
+    assert out["nranks"] == 2 and out["distinct_devices"] == 2 and len(out["pci_bus_ids"]) == 2
+    assert out["links_from_rank0"][0]["to_rank"] == 1 and "link" in out["links_from_rank0"][0]
