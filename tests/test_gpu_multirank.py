@@ -301,3 +301,27 @@ def test_bench_under_torchrun_world2(workload):
         xo, _ = oracle.cg_poisson_f64(m, np.ones(m * m), np.zeros(m * m), max_iter=5, eps=-1.0)
         ro = np.linalg.norm(np.ones(m * m) - oracle.poisson_apply(m, xo)) / m
         assert abs(out["check"]["relres"] - ro) <= 1e-9 * ro
+
+
+@pytest.mark.timeout(200)
+def test_bench_single_gpu_line():
+    """The driver's N=1 command shape at a small size: one JSON line with the
+    contract's keys, the roofline and the per-phase breakdown whose tiling
+    phases add up to ms_per_step."""
+    cmd = [sys.executable, os.path.join(os.path.dirname(HERE), "bench.py"), "--size", "8192", "--steps", "40",
+           "--warmup", "2", "--settle", "0", "--no-cpu"]
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=150)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    out = json.loads(lines[0])
+    for key in ("metric", "value", "unit", "n_gpus", "steps", "warmup", "ms_per_step", "higher_is_better", "scaling",
+                "vs_baseline", "dtype", "data", "config", "roofline"):
+        assert key in out, key
+    assert out["n_gpus"] == 1 and out["steps"] == 40 and out["dtype"] == "f64" and out["value"] > 0
+    rf = out["roofline"]
+    assert rf["bound"] == "hbm" and 0 < rf["frac"] < 1 and rf["achieved"] == pytest.approx(rf["frac"] * rf["peak"])
+    ph = out["phases_us"]
+    assert ph["iterations_sampled"] == 39 and ph["per_rank"][0]["matvec"] > 0
+    assert abs(ph["tiling_mean_sum_over_ms_per_step"] - 1) <= 0.05, ph
+    assert out["check"]["relres"] < 1e-10
