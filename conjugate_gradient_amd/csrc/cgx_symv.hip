@@ -350,12 +350,15 @@ int sym_grid(int device) {
                                                      0) != hipSuccess ||
         per_cu <= 0)
         per_cu = 1;
-    // Two 256-thread blocks per CU, each streaming its own range of units (the
-    // read pattern measured fastest); never more than are resident at once --
-    // each block owns a fixed range, so a block that has to wait for a free
-    // CU would run its whole range after the others.  (The occupancy query
-    // can over-report by a block for 256-thread kernels: cdna_hip_programming.md.)
-    per_cu = std::min(per_cu, env_int("CGX_SYM_BLOCKS_PER_CU", 2));
+    // One 256-thread block per CU, streaming its own range of units: 388.1
+    // it/s at N=65536 against 384.8-386.4 with two per CU (and 367-377 for
+    // round 2's one 512-thread block per CU), interleaved on one box
+    // (profiles/r03_symmetric_blocks_ab.jsonl).  Never more than are resident
+    // at once -- each block owns a fixed range, so a block that had to wait
+    // for a free CU would run its whole range after the others.  (The
+    // occupancy query can over-report by a block for 256-thread kernels:
+    // cdna_hip_programming.md.)
+    per_cu = std::min(per_cu, env_int("CGX_SYM_BLOCKS_PER_CU", 1));
     return cus * per_cu;
 }
 
