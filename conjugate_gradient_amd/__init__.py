@@ -32,7 +32,8 @@ import numpy as np
 
 __all__ = [
     "CGX_F64", "CGX_F32_REF", "CGX_TIMING", "CGX_HOST_STREAM", "CGX_NO_OVERLAP", "CGX_COMM_P2P", "CGX_SYMMETRIC",
-    "CGX_PHASES", "CGX_PEER_ACTIVE", "PHASE_NAMES", "CgxError", "Stats", "Solver", "lib", "build",
+    "CGX_PHASES", "CGX_PEER_ACTIVE", "CGX_SMALL_ACTIVE", "CGX_FOLD_ACTIVE", "PHASE_NAMES", "CgxError", "Stats",
+    "Solver", "lib", "build",
     "device_pci_bus_id", "device_link",
     "conjugrad", "matVec", "vecVec", "residual", "update_xr", "update_p", "read_text",
     "count_text", "read_dims", "device_count", "get_unique_id", "DeviceArray",
@@ -50,6 +51,8 @@ CGX_COMM_P2P = 0x1000
 CGX_SYMMETRIC = 0x8000
 CGX_PHASES = 0x10000
 CGX_PEER_ACTIVE = 0x20000
+CGX_SMALL_ACTIVE = 0x40000
+CGX_FOLD_ACTIVE = 0x80000
 
 # cgx_phase_times indices (include/cgx.h), in the order the phases tile an iteration
 PHASE_NAMES = ("matvec_own", "gather_exposed", "matvec", "combine_pap", "update_r", "combine_rr", "update_xp",

@@ -311,6 +311,7 @@ inline int64_t round_up(int64_t v, int64_t m) { return (v + m - 1) / m * m; }
 // cgx_setup.hip
 int set_dev(const Shard &s);
 int alloc_shard(cgx_ctx *c, Shard &s);
+bool small_matvec(const cgx_ctx *c);  // k_matvec_small_f64 applies (cgx_setup.hip)
 void free_shard(Shard &s);
 int check_n(int64_t n, int nranks);
 cgx_ctx *new_ctx(int64_t n, int nranks, int flags);

@@ -63,9 +63,10 @@ __device__ __forceinline__ double wave_sum(double v) {
 // the ticket.  An agent-scope release on the ticket would add a buffer_wbl2
 // (write-back of the whole L2's dirty lines) per block: measured 378 vs 283 us
 // on a 537 MB k_update_r (round 1), for no change in what the consumer reads.
+template <int NT = kNT>
 __device__ __forceinline__ void grid_sum_last_block(double v, double *partials, unsigned *ticket,
                                                     double *out, bool add_to_out = false) {
-    __shared__ double red[kNT / 64];
+    __shared__ double red[NT / 64];
     __shared__ int is_last;
     const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
     v = wave_sum(v);
@@ -80,7 +81,7 @@ __device__ __forceinline__ void grid_sum_last_block(double v, double *partials, 
         if (threadIdx.x == 0) {
             double t = red[0];
 #pragma unroll
-            for (int w = 1; w < kNT / 64; ++w) t += red[w];
+            for (int w = 1; w < NT / 64; ++w) t += red[w];
             t = 0.0 + t;
             *out = add_to_out ? *out + t : t;
         }
@@ -89,7 +90,7 @@ __device__ __forceinline__ void grid_sum_last_block(double v, double *partials, 
     if (threadIdx.x == 0) {
         double t = red[0];
 #pragma unroll
-        for (int w = 1; w < kNT / 64; ++w) t += red[w];
+        for (int w = 1; w < NT / 64; ++w) t += red[w];
         __hip_atomic_store(partials + blockIdx.x, t, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
         const unsigned prev = __hip_atomic_fetch_add(ticket, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
@@ -103,18 +104,18 @@ __device__ __forceinline__ void grid_sum_last_block(double v, double *partials, 
     // kHandoffNote below for why the hand-off is correct on gfx950 and what a
     // release would cost.
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-    // all of this thread's partials in flight at once (grid <= 8192 = 32 * kNT)
+    // all of this thread's partials in flight at once (grid <= 8192 = 32 * NT)
     double s = 0.0;
-    for (unsigned i0 = threadIdx.x; i0 < gridDim.x; i0 += 8 * kNT) {
+    for (unsigned i0 = threadIdx.x; i0 < gridDim.x; i0 += 8 * NT) {
         double pv[8];
 #pragma unroll
         for (int u = 0; u < 8; ++u) {
-            const unsigned i = i0 + u * kNT;
+            const unsigned i = i0 + u * NT;
             pv[u] = (i < gridDim.x) ? __hip_atomic_load(partials + i, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) : 0.0;
         }
 #pragma unroll
         for (int u = 0; u < 8; ++u)
-            if (i0 + u * kNT < gridDim.x) s += pv[u];
+            if (i0 + u * NT < gridDim.x) s += pv[u];
     }
     s = wave_sum(s);
     if (lane == 0) red[wid] = s;
@@ -122,7 +123,7 @@ __device__ __forceinline__ void grid_sum_last_block(double v, double *partials, 
     if (threadIdx.x == 0) {
         double t = red[0];
 #pragma unroll
-        for (int w = 1; w < kNT / 64; ++w) t += red[w];
+        for (int w = 1; w < NT / 64; ++w) t += red[w];
         *out = add_to_out ? *out + t : t;
         __hip_atomic_store(ticket, 0u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     }

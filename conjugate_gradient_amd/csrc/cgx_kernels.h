@@ -31,12 +31,18 @@ struct MatvecPlan {
     int U = 4;        // 128-column chunks in flight per row
     int nt = 1;       // non-temporal loads of A
     int blocks = 0;   // grid (256-thread blocks), grid-stride over row groups
+    int small = 0;    // > 0: k_matvec_small_f64 with this many threads per block (vector in LDS)
 };
 // R/U/nt/blocks_per_cu <= 0 pick the defaults (env CGX_MV_* may override).
 // cols > 0 (the row length): fewer than 8 whole 128-column chunks per row
 // take U = 4 or 2, so all of a row's loads are issued at once.
 MatvecPlan plan_matvec_f64(int device, int64_t rows, int R = 0, int U = 0, int nt = -1,
                            int blocks_per_cu = 0, int64_t cols = 0);
+// The LDS-staged matVec of small systems (cgx_matvec.hip k_matvec_small_f64):
+// rows of lda columns, 2048 <= lda <= 8192; small = 0 (not applicable)
+// otherwise.  CGX_MV_SMALL=0 turns it off; CGX_SMALL_NT / CGX_SMALL_U pick
+// the block size (512, 1024) and chunks per step (4, 8).
+MatvecPlan plan_matvec_small_f64(int device, int64_t rows, int64_t lda);
 
 // ---- fp64 -------------------------------------------------------------------
 // out[i] = sum_j A[i*lda+j] v[j]; if pown != nullptr also *dot_out = pown . out

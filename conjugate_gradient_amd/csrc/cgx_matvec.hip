@@ -314,6 +314,134 @@ __global__ __launch_bounds__(kNT) void k_matvec_fold_f64(
     ts_end(ts);
 }
 
+// ---------------------------------------------------------------------------
+// Small systems on one GPU (2048 <= lda <= 8192, the reference's published
+// sizes): the vector staged in LDS, one block per CU.
+// k_matvec_f64 reads the p chunks a wave multiplies through L1/L2: with one
+// row per wave (the plan for rows of 4096-8192 columns) that is as many
+// bytes as A itself (n waves x 8n bytes), and the folded form above reads r
+// and p_{k-1} instead, twice that.  Here each block first loads the whole
+// vector into LDS -- p, or (FOLD) r and p_{k-1} combined into
+// p_k = r + beta p_{k-1} (k_update_xp_f64's expression, so the same bits) --
+// and its waves multiply their rows against it: the vector crosses L2 once
+// per CU.  The first two steps of A loads are issued before the staging, so
+// the stream starts at once.
+// Wave w of the grid owns rows w, w + W, ... (W waves in all) and walks
+// them as one stream of steps (U chunks of a row each; the next step's
+// loads, possibly the next row's, go out before this step's FMAs).  A row
+// is summed exactly as k_matvec_f64<1, U> sums it (per lane, chunks in
+// order, then the wave sum), so Ap is bit for bit the same; the owner lane
+// stores Ap[i] (FOLD: and p_k[i] into the other p buffer) and adds
+// p[i] Ap[i] to the fused p.Ap, which therefore adds in this kernel's own
+// order -- every form of the iteration at these sizes uses this kernel.
+// The LDS array is static (cdna_hip_programming.md Guideline 17: a dynamic
+// region behind grid_sum's statics would start misaligned for ds_read_b128).
+constexpr int kSmallMaxCols = 8192;
+template <bool FOLD, int NTB, int U>
+__global__ __launch_bounds__(NTB) void k_matvec_small_f64(
+    const double *__restrict__ A, int64_t lda, int64_t rows, const double *__restrict__ v,
+    const double *__restrict__ pold, double *__restrict__ pnew, const double *rr_new, const double *rr_old,
+    const double *__restrict__ pown, double *__restrict__ out, double *dot_out, double *partials,
+    unsigned *ticket, const int64_t *gate, int64_t *ts) {
+    __shared__ __attribute__((aligned(16))) d2 sp[kSmallMaxCols / 2];
+    if (gate && *gate) return;
+    ts_start(ts);
+    constexpr int WPB = NTB / 64;
+    const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+    const double beta = FOLD ? cg_ratio(*rr_new, *rr_old) : 0.0;
+    const int64_t W = (int64_t)gridDim.x * WPB;
+    const int64_t i0 = (int64_t)blockIdx.x * WPB + wid;
+    const int64_t spr = (lda >> 7) / U;                               // steps per row
+    const int64_t nrw = i0 < rows ? (rows - i0 + W - 1) / W : 0;      // this wave's rows
+    const int64_t nsteps = nrw * spr;
+    const d2 *A2 = reinterpret_cast<const d2 *>(A) + lane;
+    const int64_t ld2 = lda >> 1;
+    // load state: row k_l, step c_l of it
+    int64_t kl = 0, cl = 0;
+    auto load = [&](d2 (&av)[U]) {
+        const d2 *ar = A2 + (i0 + kl * W) * ld2 + cl * (U * 64);
+#pragma unroll
+        for (int u = 0; u < U; ++u) av[u] = __builtin_nontemporal_load(ar + u * 64);
+        if (++cl == spr) {
+            cl = 0;
+            ++kl;
+        }
+    };
+    d2 aa[U], ab[U];
+    if (nsteps > 0) load(aa);
+    if (nsteps > 1) load(ab);
+    {  // stage the vector (FOLD: form p_k) while the first two steps of A are in flight
+        constexpr int KS = 4;
+        const d2 *v2 = reinterpret_cast<const d2 *>(v);
+        const d2 *q2 = reinterpret_cast<const d2 *>(pold);
+        for (int64_t k0 = threadIdx.x; k0 < ld2; k0 += KS * NTB) {
+            d2 rv[KS], qv[KS];
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+                const int64_t k = k0 + s * NTB;
+                rv[s] = k < ld2 ? v2[k] : (d2)(0.0);
+                if constexpr (FOLD) qv[s] = k < ld2 ? q2[k] : (d2)(0.0);
+            }
+#pragma unroll
+            for (int s = 0; s < KS; ++s) {
+                const int64_t k = k0 + s * NTB;
+                if (k < ld2) {
+                    if constexpr (FOLD) sp[k] = rv[s] + beta * qv[s];  // p = r + beta p
+                    else sp[k] = rv[s];
+                }
+            }
+        }
+    }
+    __syncthreads();
+    const double *spd = reinterpret_cast<const double *>(sp);
+    double dacc = 0.0;
+    d2 acc = (d2)(0.0);
+    int64_t kf = 0, cf = 0;  // FMA state
+    auto fma_step = [&](const d2 (&av)[U]) {
+        const d2 *pr = sp + cf * (U * 64) + lane;
+#pragma unroll
+        for (int u = 0; u < U; ++u) {
+            const d2 pv = pr[u * 64];
+            acc.x = __builtin_fma(av[u].x, pv.x, acc.x);
+            acc.y = __builtin_fma(av[u].y, pv.y, acc.y);
+        }
+        if (++cf == spr) {  // the row is complete
+            const double y = wave_sum(acc.x + acc.y);
+            const int64_t i = i0 + kf * W;
+            if (lane == 0) {
+                out[i] = y;
+                if constexpr (FOLD) {
+                    const double pi = spd[i];
+                    pnew[i] = pi;
+                    dacc += pi * y;
+                } else if (pown) {
+                    dacc += pown[i] * y;
+                }
+            }
+            acc = (d2)(0.0);
+            cf = 0;
+            ++kf;
+        }
+    };
+    for (int64_t s = 0; s < nsteps; s += 2) {  // one step's loads in flight behind each step's FMAs
+        fma_step(aa);
+        if (s + 2 < nsteps) load(aa);
+        if (s + 1 >= nsteps) break;
+        fma_step(ab);
+        if (s + 3 < nsteps) load(ab);
+    }
+    if (dot_out) grid_sum_last_block<NTB>(dacc, partials, ticket, dot_out);
+    ts_end(ts);
+}
+
+template <bool FOLD>
+using SmallFn = decltype(&k_matvec_small_f64<FOLD, 1024, 4>);
+template <bool FOLD>
+SmallFn<FOLD> pick_small(int ntb, int U) {
+    if (ntb == 512) return U == 8 ? k_matvec_small_f64<FOLD, 512, 8> : k_matvec_small_f64<FOLD, 512, 4>;
+    return U == 8 ? k_matvec_small_f64<FOLD, 1024, 8> : k_matvec_small_f64<FOLD, 1024, 4>;
+}
+
 using FoldFn = decltype(&k_matvec_fold_f64<1, 8>);
 FoldFn pick_fold(int R, int U) {
     if (R == 1) return U == 2 ? k_matvec_fold_f64<1, 2> : U == 4 ? k_matvec_fold_f64<1, 4> : k_matvec_fold_f64<1, 8>;
@@ -398,10 +526,44 @@ MatvecPlan plan_matvec_f64(int device, int64_t rows, int R, int U, int nt, int b
     return pl;
 }
 
+MatvecPlan plan_matvec_small_f64(int device, int64_t rows, int64_t lda) {
+    MatvecPlan pl;
+    if (env_int("CGX_MV_SMALL", 1) == 0 || rows <= 0 || lda < 2048 || lda > kSmallMaxCols || (lda & 127))
+        return pl;
+    const int cus = cu_count(device);
+    const int64_t chunks = lda >> 7;
+    // One 512-thread block per CU, 8 chunks per step (64 KiB of A in flight
+    // per CU), the first two steps issued before the staging.  Per iteration
+    // (folded, device clock) at n = 2048 / 4096 / 8192: 13.8 / 30.0-30.1 /
+    // 91.0 us against 14.3 / 30.8 / 92.1 for round 2's two-launch form on
+    // the same box; 1024 threads x 4 chunks: 14.6-14.8 / 30.9-33.3 / 92.2-92.4,
+    // x 8: 15.2 / 31.0 / 91.1-91.4 (profiles/r03_iteration_floor_small*.jsonl).
+    pl.small = env_int("CGX_SMALL_NT", 512);
+    pl.U = env_int("CGX_SMALL_U", chunks % 8 ? 4 : 8);
+    if ((pl.small != 512 && pl.small != 1024) || (pl.U != 4 && pl.U != 8) || chunks % pl.U) {
+        pl.small = 0;
+        return pl;
+    }
+    pl.R = 1;
+    pl.nt = 8;
+    const int64_t need = (rows + pl.small / 64 - 1) / (pl.small / 64);
+    pl.blocks = (int)std::max<int64_t>(1, std::min<int64_t>(need, std::min<int64_t>(cus, kMaxRedBlocks)));
+    return pl;
+}
+
 hipError_t matvec_f64(const MatvecPlan &pl, const double *A, int64_t lda, int64_t rows, int64_t cols,
                       const double *v, double *out, const double *pown, double *dot_out,
                       const RedWs &ws, hipStream_t s, const int64_t *gate, int64_t *ts) {
     if (rows <= 0) return hipSuccess;
+    if (pl.small) {  // every column to lda (A and v zero past n), vector in LDS
+        if (cols != lda || (lda & 127) || lda > kSmallMaxCols ||
+            ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(v)) & 15))
+            return hipErrorInvalidValue;
+        hipLaunchKernelGGL(pick_small<false>(pl.small, pl.U), dim3(pl.blocks), dim3(pl.small), 0, s, A, lda, rows, v,
+                           nullptr, nullptr, nullptr, nullptr, pown, out, dot_out, ws.partials,
+                           ws.tickets + T_MATVEC, gate, ts);
+        return hipGetLastError();
+    }
     // The vector path needs 16-B-aligned rows and p; otherwise every column
     // goes through the scalar tail loop.
     const bool aligned = ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(v)) & 15) == 0 &&
@@ -436,6 +598,13 @@ hipError_t matvec_fold_f64(const MatvecPlan &pl, const double *A, int64_t lda, i
     if (((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(r) | reinterpret_cast<uintptr_t>(pold)) & 15) ||
         (lda & 1))
         return hipErrorInvalidValue;
+    if (pl.small) {
+        if (cols != lda || (lda & 127) || lda > kSmallMaxCols) return hipErrorInvalidValue;
+        hipLaunchKernelGGL(pick_small<true>(pl.small, pl.U), dim3(pl.blocks), dim3(pl.small), 0, s, A, lda, rows, r,
+                           pold, pnew, rr_new, rr_old, nullptr, out, dot_out, ws.partials, ws.tickets + T_MATVEC,
+                           gate, ts);
+        return hipGetLastError();
+    }
     hipLaunchKernelGGL(pick_fold(pl.R == 1 ? 1 : 2, pl.U), dim3(pl.blocks), dim3(kNT), 0, s, A, lda, rows, cols,
                        cols & ~int64_t(127), r, pold, pnew, rr_new, rr_old, out, dot_out, ws.partials,
                        ws.tickets + T_MATVEC, gate, ts);

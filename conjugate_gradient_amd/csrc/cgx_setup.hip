@@ -186,14 +186,16 @@ int alloc_shard(cgx_ctx *c, Shard &s) {
     }
     if (c->mode == M_RCCL)
         for (auto &e : s.ev_prog) HIPT(hipEventCreateWithFlags(&e, hipEventDisableTiming));
-    if (!f32ref(c) && c->op == OP_DENSE && !(c->flags & CGX_SYMMETRIC))
+    if (!f32ref(c) && c->op == OP_DENSE && !(c->flags & CGX_SYMMETRIC)) {
         s.plan = plan_matvec_f64(s.dev, s.nloc, 0, 0, -1, 0, c->lda);
+        if (small_matvec(c)) s.plan = plan_matvec_small_f64(s.dev, s.nloc, c->lda);
+    }
     if (c->fold_p) {
         // The folded matVec keeps the plain plan's rows per wave and grid: the
         // fused p.Ap partials then add in the same order (x bit for bit the
         // other forms').  At n = 2048 (R = 2) four chunks in flight beat eight.
         s.fold_plan = plan_matvec_f64(s.dev, s.nloc, s.plan.R, c->n == 2048 ? 4 : s.plan.U, -1, 0, c->lda);
-        if (s.fold_plan.blocks != s.plan.blocks) s.fold_plan = s.plan;
+        if (s.fold_plan.blocks != s.plan.blocks || s.plan.small) s.fold_plan = s.plan;
     }
     HIPT(hipStreamSynchronize(s.stream));
     return CGX_OK;
@@ -295,15 +297,26 @@ int alloc_overlap(cgx_ctx *c) {
 // in one block: n doubles read twice and written once by one CU, a few us at
 // n = 8192); CGX_FUSE_P=0 keeps three launches, =1 uses two at any n.
 constexpr int64_t kFusePMax = 8192;
-// ... and up to kFoldPMax the p update is folded into the next matVec
-// (do_iteration_fold_p): measured per iteration (profiles/r03_iteration_floor.jsonl,
-// device clock) 9.6 vs 10.2 us at n = 512, 11.8 vs 12.0 at 1024, 13.9-14.0 vs
-// 14.2 at 2048.  Above, the matVec's plan has one row per wave, and the
-// fold's extra reads of r and p_{k-1} per chunk of A cost about what the
-// single-block pass saves (n = 4096: 31.1 either way with two rows per wave,
-// whose p.Ap partials would add in another order; 37.4 with one), so
-// k_update_xrp_f64 stays.
+// ... and the p update is folded into the next matVec (do_iteration_fold_p)
+// up to kFoldPMax with k_matvec_fold_f64 -- measured per iteration
+// (profiles/r03_iteration_floor.jsonl, device clock) 9.6 vs 10.2 us at
+// n = 512, 11.8 vs 12.0 at 1024, 13.9-14.0 vs 14.2 at 2048 -- and wherever
+// the LDS-staged matVec applies (small_matvec: 2048 <= lda <= 8192), which
+// forms p_k once per CU instead of once per wave: 13.8 / 30.0-30.1 / 91.0 us
+// at 2048 / 4096 / 8192 against 14.3 / 30.8 / 92.1 for the two-launch form
+// with round 2's matVec (profiles/r03_iteration_floor_small_prefetch2.jsonl).
+// With k_matvec_fold_f64 above 2048 the fold's extra reads of r and p_{k-1}
+// per chunk of A cost more than the single-block pass saves (37.4 vs 31.1 us
+// at 4096), so without the LDS-staged matVec k_update_xrp_f64 stays.
 constexpr int64_t kFoldPMax = 2048;
+// One GPU, one resident row-major shard of 2048 <= lda <= 8192 columns: the
+// matVec stages p in LDS (k_matvec_small_f64, every form of the iteration).
+bool small_matvec(const cgx_ctx *c) {
+    if (c->mode != M_SINGLE || c->sh.size() != 1 || c->op != OP_DENSE || f32ref(c)) return false;
+    if (c->flags & (CGX_SYMMETRIC | CGX_HOST_STREAM)) return false;
+    return plan_matvec_small_f64(c->sh[0].dev, c->sh[0].nloc, c->lda).small > 0;
+}
+
 static bool can_fuse_p(const cgx_ctx *c) {
     if (c->mode != M_SINGLE || c->op != OP_DENSE || f32ref(c)) return false;
     if (c->flags & (CGX_SYMMETRIC | CGX_HOST_STREAM)) return false;
@@ -332,7 +345,7 @@ int finish_create(cgx_ctx *c, cgx_ctx **out) {
     c->fused_p = can_fuse_p(c);
     {  // the folded form of the two-launch iteration (CGX_FOLD_P=0 / 1: never / at any fused n)
         const char *e = std::getenv("CGX_FOLD_P");
-        c->fold_p = c->fused_p && (e && *e ? *e == '1' : c->n <= kFoldPMax);
+        c->fold_p = c->fused_p && (e && *e ? *e == '1' : c->n <= kFoldPMax || small_matvec(c));
     }
     c->ref_mv_dot = can_fuse_ref_dot(c);
     c->ref_fused = c->ref_mv_dot && c->mode == M_SINGLE;
@@ -633,7 +646,8 @@ int cgx_get_info(const cgx_ctx *c, cgx_info *info) {
     info->nrows = 0;
     for (auto &s : c->sh) info->nrows += s.nloc;
     info->flags = c->flags | (c->overlap ? CGX_OVERLAP_ACTIVE : 0) |
-                  ((c->fused || c->fused_p || c->ref_fused) ? CGX_FUSED_ACTIVE : 0) | (c->peer ? CGX_PEER_ACTIVE : 0);
+                  ((c->fused || c->fused_p || c->ref_fused) ? CGX_FUSED_ACTIVE : 0) | (c->peer ? CGX_PEER_ACTIVE : 0) |
+                  (c->sh[0].plan.small ? CGX_SMALL_ACTIVE : 0) | (c->fold_p ? CGX_FOLD_ACTIVE : 0);
     info->elem_bytes = c->es;
     return CGX_OK;
 }

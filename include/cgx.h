@@ -126,6 +126,14 @@ extern "C" {
                                     context spans distinct devices and peer
                                     access is enabled between every pair of
                                     them (device copies then go over xGMI) */
+#define CGX_SMALL_ACTIVE 0x40000 /* reported in cgx_info.flags: one GPU, one
+                                    resident fp64 row block of 2048..8192
+                                    columns -- the matVec stages the vector in
+                                    LDS, one block per CU (k_matvec_small_f64;
+                                    CGX_MV_SMALL=0 turns it off) */
+#define CGX_FOLD_ACTIVE  0x80000 /* reported in cgx_info.flags: the two-launch
+                                    iteration folds p = r + beta p into the
+                                    next matVec (CGX_FOLD_P) */
 
 typedef struct cgx_ctx cgx_ctx;
 

@@ -490,8 +490,9 @@ def test_two_launch_iteration_bitwise_equals_three(monkeypatch, n, seed):
     -- device-gated, host-checked, fixed-count and in pieces; with several
     blocks (n = 8192: r handed to the last block write-through), odd n, rows
     not a whole number of 128-column chunks (the fold's tail columns) and both
-    row plans (R = 2 at n = 2048, R = 1 at 4096-8192).  All agree with the
-    fp64 oracle."""
+    row plans (R = 2 at n = 2048, R = 1 at 4096-8192).  At n = 2048-8192 every
+    form's matVec is k_matvec_small_f64 (p staged in LDS; the fold forms
+    p_k into LDS).  All agree with the fp64 oracle."""
     A, b = oracle.spd_hash(n, seed=seed)
     res = {}
     for form, fuse, fold in (("three", "0", "0"), ("two", "1", "0"), ("fold", "1", "1")):
@@ -501,6 +502,8 @@ def test_two_launch_iteration_bitwise_equals_three(monkeypatch, n, seed):
             monkeypatch.setenv("CGX_GATED", gated)
             with cg.Solver(n) as s:
                 assert bool(s.info.flags & cg.CGX_FUSED_ACTIVE) == (fuse == "1")
+                assert bool(s.info.flags & cg.CGX_FOLD_ACTIVE) == (fold == "1")
+                assert bool(s.info.flags & cg.CGX_SMALL_ACTIVE) == (2048 <= n <= 8192)
                 s.set_system(A, b)
                 x, st = s.solve(np.zeros(n), eps=1e-10)
                 xf, stf = s.solve(np.zeros(n), eps=-1.0, max_iter=9)
@@ -517,6 +520,32 @@ def test_two_launch_iteration_bitwise_equals_three(monkeypatch, n, seed):
         assert conv and dp == it and np.array_equal(xp, ref[0]), key
     xo, so = oracle.cg_f64(A, b, np.zeros(n), eps=1e-10)
     assert ref[1] == so.iterations and rel(ref[0], xo) <= TOL
+
+
+@pytest.mark.parametrize("n,seed", [(2048, 6), (2100, 8), (4096, 7), (5000, 9), (8192, 3)])
+def test_small_matvec_lds_agrees_with_l2_kernel(monkeypatch, n, seed):
+    """k_matvec_small_f64 (one GPU, 2048 <= lda <= 8192: the vector staged in
+    LDS once per CU, one block per CU) sums each row as k_matvec_f64 does;
+    only the fused p.Ap adds in another order.  Default and folded forms
+    converge in the oracle's loop count, agree with the oracle and, to fp64
+    rounding, with round 2's kernel (CGX_MV_SMALL=0).  lda = 2176 (17 chunks,
+    not a whole number of steps) keeps k_matvec_f64."""
+    A, b = oracle.spd_hash(n, seed=seed)
+    xo, so = oracle.cg_f64(A, b, np.zeros(n), eps=1e-10)
+    res = {}
+    for small in ("1", "0"):
+        for fold in ("1", "0"):
+            monkeypatch.setenv("CGX_MV_SMALL", small)
+            monkeypatch.setenv("CGX_FOLD_P", fold)
+            with cg.Solver(n) as s:
+                assert bool(s.info.flags & cg.CGX_SMALL_ACTIVE) == (small == "1" and n != 2100)
+                s.set_system(A, b)
+                x, st = s.solve(np.zeros(n), eps=1e-10)
+            assert st.converged and st.iterations == so.iterations and rel(x, xo) <= TOL, (small, fold)
+            res[(small, fold)] = x
+    for key, x in res.items():
+        assert rel(x, res[("0", "0")]) <= 1e-12, key
+    assert np.array_equal(res[("1", "1")], res[("1", "0")])  # the fold: same kernel, same bits
 
 
 def _f32_system(name):

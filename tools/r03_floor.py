@@ -1,7 +1,8 @@
 """Per-iteration time of small dense fp64 systems on one GPU, the launch forms
 interleaved in one process: three launches (CGX_FUSE_P=0), two launches with
 the single-block p pass (k_update_xrp_f64), two launches with the p update
-folded into the matVec (CGX_FOLD_P=1).  Fixed-count iterations, timed by
+folded into the matVec (CGX_FOLD_P=1); "_l2p": the same with round 2's
+matVec (p read through L2, CGX_MV_SMALL=0) instead of k_matvec_small_f64.  Fixed-count iterations, timed by
 the host around a synchronize, with the CGX_PHASES stamps alongside.
   python tools/r03_floor.py [rounds] > profiles/r03_iteration_floor.jsonl"""
 import json
@@ -12,14 +13,27 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import conjugate_gradient_amd as cg  # noqa: E402
 
-# (CGX_FUSE_P, CGX_FOLD_P, CGX_MV_R, CGX_MV_U); "" = the library's default
-FORMS = {"three": ("0", "0", "", ""), "two": ("1", "0", "", ""), "fold": ("1", "1", "", ""), "default": ("", "", "", "")}
+KNOBS = ("CGX_FUSE_P", "CGX_FOLD_P", "CGX_MV_R", "CGX_MV_U", "CGX_MV_SMALL", "CGX_SMALL_NT", "CGX_SMALL_U")
+# form -> the knobs it sets (the rest: the library's default)
+FORMS = {"three": {"CGX_FUSE_P": "0", "CGX_FOLD_P": "0"}, "two": {"CGX_FUSE_P": "1", "CGX_FOLD_P": "0"},
+         "fold": {"CGX_FUSE_P": "1", "CGX_FOLD_P": "1"}, "default": {},
+         # round 2's kernels: k_matvec_f64 reading p through L2 (no LDS staging)
+         "two_l2p": {"CGX_FUSE_P": "1", "CGX_FOLD_P": "0", "CGX_MV_SMALL": "0"},
+         "fold_l2p": {"CGX_FUSE_P": "1", "CGX_FOLD_P": "1", "CGX_MV_SMALL": "0"}}
 if os.environ.get("R03_FOLD_VARIANTS"):  # the plans tried for the fold (CGX_MV_* also sets the k = 0 matVec's)
-    FORMS.update({"fold_r2u4": ("1", "1", "2", "4"), "fold_r2u8": ("1", "1", "2", "8")})
+    FORMS.update({"fold_r2u4": {"CGX_FUSE_P": "1", "CGX_FOLD_P": "1", "CGX_MV_R": "2", "CGX_MV_U": "4",
+                                "CGX_MV_SMALL": "0"},
+                  "fold_r2u8": {"CGX_FUSE_P": "1", "CGX_FOLD_P": "1", "CGX_MV_R": "2", "CGX_MV_U": "8",
+                                "CGX_MV_SMALL": "0"}})
+if os.environ.get("R03_SMALL_VARIANTS"):  # k_matvec_small_f64's block size and chunks per step
+    for nt in ("512", "1024"):
+        for u in ("4", "8"):
+            FORMS[f"fold_nt{nt}u{u}"] = {"CGX_FUSE_P": "1", "CGX_FOLD_P": "1", "CGX_SMALL_NT": nt, "CGX_SMALL_U": u}
 
 
 def run(n, form, steps=400, warm=50):
-    os.environ["CGX_FUSE_P"], os.environ["CGX_FOLD_P"], os.environ["CGX_MV_R"], os.environ["CGX_MV_U"] = FORMS[form]
+    for k in KNOBS:
+        os.environ[k] = FORMS[form].get(k, "")
     with cg.Solver(n, flags=cg.CGX_PHASES) as s:
         s.generate_spd(42)
         s.begin()
