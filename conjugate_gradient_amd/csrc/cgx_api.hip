@@ -158,6 +158,11 @@ int cgx_matvec(int dtype, const void *A, int64_t lda, int64_t rows, int64_t cols
     RedWs ws;
     TRY(dev_ws(&ws));
     MatvecPlan pl = plan_matvec_f64(dev, rows, 0, 0, -1, 0, cols);
+    const char *sm = std::getenv("CGX_MV_SMALL");
+    if (cols == lda && sm && *sm == '2') {  // the solver's LDS-staged kernel here too (tests)
+        const MatvecPlan sp = plan_matvec_small_f64(dev, rows, lda);
+        if (sp.small) pl = sp;
+    }
     HIPT(matvec_f64(pl, static_cast<const double *>(A), lda, rows, cols, static_cast<const double *>(v),
                     static_cast<double *>(out), nullptr, nullptr, ws, s));
     return CGX_OK;

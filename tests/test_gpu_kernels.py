@@ -140,6 +140,32 @@ MV_PLANS = [(R, U, nt) for R in (1, 2, 4, 8) for U in (2, 4, 8) for nt in (0, 1,
             if not (R == 8 and U == 8 and nt in (2, 8))]
 
 
+@pytest.mark.parametrize("rows,cols", [(300, 2048), (2048, 4096), (5000, 5120), (8192, 8192), (77, 2560)])
+def test_matvec_small_lds_bitwise_equals_l2_kernel(monkeypatch, rows, cols):
+    """k_matvec_small_f64 (the vector staged in LDS, one block per CU; the
+    solver's matVec on one GPU at 2048 <= lda <= 8192) sums every row as
+    k_matvec_f64 does -- per lane, chunks in ascending order, then the wave
+    sum -- so Ap is bit for bit the L2 kernel's: rows fewer than the grid's
+    waves (77, 300), several rows per wave (5000, 8192), 4 chunks per step
+    (2560 = 20 chunks).  CGX_MV_SMALL=2 routes the kernel-level cgx_matvec
+    through it."""
+    rng = np.random.default_rng(rows * 7 + cols)
+    A = rng.random((rows, cols)) - 0.5
+    v = rng.random(cols)
+    A_d, v_d = dev(A), dev(v)
+    out = cg.DeviceArray(rows)
+    cg.matVec(A_d, v_d, out, rows, cols)
+    base = out.to_host()
+    assert np.all(np.abs(base - oracle.matvec_f64(A, v)) <= F64_TOL * (np.abs(A) @ np.abs(v)))
+    monkeypatch.setenv("CGX_MV_SMALL", "2")
+    for nt, u in (("512", "8"), ("512", "4"), ("1024", "4"), ("1024", "8")):
+        monkeypatch.setenv("CGX_SMALL_NT", nt)
+        monkeypatch.setenv("CGX_SMALL_U", u)
+        out = cg.DeviceArray(rows)
+        cg.matVec(A_d, v_d, out, rows, cols)
+        assert np.array_equal(out.to_host(), base), (nt, u)
+
+
 @pytest.mark.parametrize("rows,cols", [(300, 1000), (1000, 1024), (517, 2176), (2048, 4096), (8192, 3200)])
 def test_matvec_f64_every_plan_bitwise_equal(monkeypatch, rows, cols):
     """Every (rows per wave, chunks in flight, load policy) plan, including the
