@@ -337,7 +337,7 @@ __global__ __launch_bounds__(kNT) void k_matvec_fold_f64(
 // The LDS array is static (cdna_hip_programming.md Guideline 17: a dynamic
 // region behind grid_sum's statics would start misaligned for ds_read_b128).
 constexpr int kSmallMaxCols = 8192;
-template <bool FOLD, int NTB, int U>
+template <bool FOLD, int NTB, int U, int NTA = 1>
 __global__ __launch_bounds__(NTB) void k_matvec_small_f64(
     const double *__restrict__ A, int64_t lda, int64_t rows, const double *__restrict__ v,
     const double *__restrict__ pold, double *__restrict__ pnew, const double *rr_new, const double *rr_old,
@@ -361,7 +361,7 @@ __global__ __launch_bounds__(NTB) void k_matvec_small_f64(
     auto load = [&](d2 (&av)[U]) {
         const d2 *ar = A2 + (i0 + kl * W) * ld2 + cl * (U * 64);
 #pragma unroll
-        for (int u = 0; u < U; ++u) av[u] = __builtin_nontemporal_load(ar + u * 64);
+        for (int u = 0; u < U; ++u) av[u] = load_a<NTA>(ar + u * 64);
         if (++cl == spr) {
             cl = 0;
             ++kl;
@@ -436,10 +436,16 @@ __global__ __launch_bounds__(NTB) void k_matvec_small_f64(
 
 template <bool FOLD>
 using SmallFn = decltype(&k_matvec_small_f64<FOLD, 1024, 4>);
+template <bool FOLD, int NTA>
+SmallFn<FOLD> pick_small_u(int ntb, int U) {
+    if (ntb == 512) return U == 8 ? k_matvec_small_f64<FOLD, 512, 8, NTA> : k_matvec_small_f64<FOLD, 512, 4, NTA>;
+    return U == 8 ? k_matvec_small_f64<FOLD, 1024, 8, NTA> : k_matvec_small_f64<FOLD, 1024, 4, NTA>;
+}
+// nt: the plan's A load policy (0: default policy, A may stay in the 256 MB
+// MALL between iterations; otherwise non-temporal)
 template <bool FOLD>
-SmallFn<FOLD> pick_small(int ntb, int U) {
-    if (ntb == 512) return U == 8 ? k_matvec_small_f64<FOLD, 512, 8> : k_matvec_small_f64<FOLD, 512, 4>;
-    return U == 8 ? k_matvec_small_f64<FOLD, 1024, 8> : k_matvec_small_f64<FOLD, 1024, 4>;
+SmallFn<FOLD> pick_small(int ntb, int U, int nt) {
+    return nt == 0 ? pick_small_u<FOLD, 0>(ntb, U) : pick_small_u<FOLD, 1>(ntb, U);
 }
 
 using FoldFn = decltype(&k_matvec_fold_f64<1, 8>);
@@ -545,7 +551,11 @@ MatvecPlan plan_matvec_small_f64(int device, int64_t rows, int64_t lda) {
         return pl;
     }
     pl.R = 1;
-    pl.nt = 8;
+    // A of up to 64 MiB read with default-policy loads stays in the 256 MB
+    // MALL between iterations: 13.4 vs 13.9 us per iteration at n = 2048 (33.5
+    // MB); at 4096 (134 MB) 30.6 vs 30.2, at 8192 (537 MB) 103 vs 90
+    // (profiles/r03_iteration_floor_small_mall.jsonl)
+    pl.nt = env_int("CGX_SMALL_ANT", rows * lda * 8 <= (int64_t(64) << 20) ? 0 : 1) ? 8 : 0;
     const int64_t need = (rows + pl.small / 64 - 1) / (pl.small / 64);
     pl.blocks = (int)std::max<int64_t>(1, std::min<int64_t>(need, std::min<int64_t>(cus, kMaxRedBlocks)));
     return pl;
@@ -559,7 +569,7 @@ hipError_t matvec_f64(const MatvecPlan &pl, const double *A, int64_t lda, int64_
         if (cols != lda || (lda & 127) || lda > kSmallMaxCols ||
             ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(v)) & 15))
             return hipErrorInvalidValue;
-        hipLaunchKernelGGL(pick_small<false>(pl.small, pl.U), dim3(pl.blocks), dim3(pl.small), 0, s, A, lda, rows, v,
+        hipLaunchKernelGGL(pick_small<false>(pl.small, pl.U, pl.nt), dim3(pl.blocks), dim3(pl.small), 0, s, A, lda, rows, v,
                            nullptr, nullptr, nullptr, nullptr, pown, out, dot_out, ws.partials,
                            ws.tickets + T_MATVEC, gate, ts);
         return hipGetLastError();
@@ -600,7 +610,7 @@ hipError_t matvec_fold_f64(const MatvecPlan &pl, const double *A, int64_t lda, i
         return hipErrorInvalidValue;
     if (pl.small) {
         if (cols != lda || (lda & 127) || lda > kSmallMaxCols) return hipErrorInvalidValue;
-        hipLaunchKernelGGL(pick_small<true>(pl.small, pl.U), dim3(pl.blocks), dim3(pl.small), 0, s, A, lda, rows, r,
+        hipLaunchKernelGGL(pick_small<true>(pl.small, pl.U, pl.nt), dim3(pl.blocks), dim3(pl.small), 0, s, A, lda, rows, r,
                            pold, pnew, rr_new, rr_old, nullptr, out, dot_out, ws.partials, ws.tickets + T_MATVEC,
                            gate, ts);
         return hipGetLastError();
