@@ -209,7 +209,7 @@ __global__ __launch_bounds__(kNT) void k_matvec_f64(
 // single-block pass over p at the end of the iteration.
 // Loads of r and p_{k-1} for step c + U go out before the FMAs of step c,
 // like k_matvec_f64's pipeline; the combine waits until the FMA step.
-template <int R, int U>
+template <int R, int U, int NTA>
 __device__ __forceinline__ void fold_load_step(const d2 *const (&arow)[R], const d2 *r2, const d2 *q2, int64_t c,
                                                d2 (&rv)[U], d2 (&qv)[U], d2 (&av)[R][U]) {
 #pragma unroll
@@ -220,7 +220,7 @@ __device__ __forceinline__ void fold_load_step(const d2 *const (&arow)[R], const
 #pragma unroll
     for (int r = 0; r < R; ++r)
 #pragma unroll
-        for (int u = 0; u < U; ++u) av[r][u] = load_a<1>(arow[r] + (c + u) * 64);
+        for (int u = 0; u < U; ++u) av[r][u] = load_a<NTA>(arow[r] + (c + u) * 64);
 }
 
 template <int R, int U>
@@ -237,7 +237,7 @@ __device__ __forceinline__ void fold_fma_step(const d2 (&rv)[U], const d2 (&qv)[
     }
 }
 
-template <int R, int U>
+template <int R, int U, int NTA = 1>
 __global__ __launch_bounds__(kNT) void k_matvec_fold_f64(
     const double *__restrict__ A, int64_t lda, int64_t rows, int64_t cols, int64_t vec_cols,
     const double *__restrict__ r, const double *__restrict__ pold, double *__restrict__ pnew, const double *rr_new,
@@ -268,15 +268,15 @@ __global__ __launch_bounds__(kNT) void k_matvec_fold_f64(
         {
             d2 ra[U], qa[U], aa[R][U], rb[U], qb[U], ab[R][U];
             int64_t c = 0;
-            if (c + U <= nchunk) fold_load_step<R, U>(arow, r2, q2, c, ra, qa, aa);
+            if (c + U <= nchunk) fold_load_step<R, U, NTA>(arow, r2, q2, c, ra, qa, aa);
             while (c + U <= nchunk) {
                 const bool more = c + 2 * U <= nchunk;
-                if (more) fold_load_step<R, U>(arow, r2, q2, c + U, rb, qb, ab);
+                if (more) fold_load_step<R, U, NTA>(arow, r2, q2, c + U, rb, qb, ab);
                 fold_fma_step<R, U>(ra, qa, aa, beta, acc);
                 c += U;
                 if (!more) break;
                 const bool more2 = c + 2 * U <= nchunk;
-                if (more2) fold_load_step<R, U>(arow, r2, q2, c + U, ra, qa, aa);
+                if (more2) fold_load_step<R, U, NTA>(arow, r2, q2, c + U, ra, qa, aa);
                 fold_fma_step<R, U>(rb, qb, ab, beta, acc);
                 c += U;
                 if (!more2) break;
@@ -285,7 +285,7 @@ __global__ __launch_bounds__(kNT) void k_matvec_fold_f64(
                 const d2 pv = r2[c * 64] + beta * q2[c * 64];
 #pragma unroll
                 for (int q = 0; q < R; ++q) {
-                    const d2 a = load_a<1>(arow[q] + c * 64);
+                    const d2 a = load_a<NTA>(arow[q] + c * 64);
                     acc[q].x = __builtin_fma(a.x, pv.x, acc[q].x);
                     acc[q].y = __builtin_fma(a.y, pv.y, acc[q].y);
                 }
@@ -449,9 +449,15 @@ SmallFn<FOLD> pick_small(int ntb, int U, int nt) {
 }
 
 using FoldFn = decltype(&k_matvec_fold_f64<1, 8>);
-FoldFn pick_fold(int R, int U) {
-    if (R == 1) return U == 2 ? k_matvec_fold_f64<1, 2> : U == 4 ? k_matvec_fold_f64<1, 4> : k_matvec_fold_f64<1, 8>;
-    return U == 2 ? k_matvec_fold_f64<2, 2> : U == 4 ? k_matvec_fold_f64<2, 4> : k_matvec_fold_f64<2, 8>;
+template <int NTA>
+FoldFn pick_fold_u(int R, int U) {
+    if (R == 1)
+        return U == 2 ? k_matvec_fold_f64<1, 2, NTA> : U == 4 ? k_matvec_fold_f64<1, 4, NTA> : k_matvec_fold_f64<1, 8, NTA>;
+    return U == 2 ? k_matvec_fold_f64<2, 2, NTA> : U == 4 ? k_matvec_fold_f64<2, 4, NTA> : k_matvec_fold_f64<2, 8, NTA>;
+}
+// the plan's A policy: 0 / 2 default-policy loads, otherwise non-temporal
+FoldFn pick_fold(int R, int U, int nt) {
+    return (nt == 0 || nt == 2) ? pick_fold_u<0>(R, U) : pick_fold_u<1>(R, U);
 }
 
 using MvFn = void (*)(const double *, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, int, int,
@@ -508,7 +514,9 @@ MatvecPlan plan_matvec_f64(int device, int64_t rows, int R, int U, int nt, int b
     // 4 chunks); U = 4 / 2 issues them together
     const int64_t chunks = cols >> 7;
     pl.U = (cols <= 0 || chunks >= 8) ? 8 : chunks >= 4 ? 4 : 2;
-    pl.nt = 8;
+    // an A of up to 64 MiB with default-policy loads (2), so it stays in the
+    // 256 MB MALL between iterations (profiles/r03_iteration_floor_mall_l2.jsonl)
+    pl.nt = (cols > 0 && rows * cols * 8 <= (int64_t(64) << 20)) ? 2 : 8;
     pl.R = env_int("CGX_MV_R", pl.R);
     pl.U = env_int("CGX_MV_U", pl.U);
     pl.nt = env_int("CGX_MV_NT", pl.nt);
@@ -615,7 +623,7 @@ hipError_t matvec_fold_f64(const MatvecPlan &pl, const double *A, int64_t lda, i
                            gate, ts);
         return hipGetLastError();
     }
-    hipLaunchKernelGGL(pick_fold(pl.R == 1 ? 1 : 2, pl.U), dim3(pl.blocks), dim3(kNT), 0, s, A, lda, rows, cols,
+    hipLaunchKernelGGL(pick_fold(pl.R == 1 ? 1 : 2, pl.U, pl.nt), dim3(pl.blocks), dim3(kNT), 0, s, A, lda, rows, cols,
                        cols & ~int64_t(127), r, pold, pnew, rr_new, rr_old, out, dot_out, ws.partials,
                        ws.tickets + T_MATVEC, gate, ts);
     return hipGetLastError();

@@ -14,7 +14,7 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import conjugate_gradient_amd as cg  # noqa: E402
 
 KNOBS = ("CGX_FUSE_P", "CGX_FOLD_P", "CGX_MV_R", "CGX_MV_U", "CGX_MV_SMALL", "CGX_SMALL_NT", "CGX_SMALL_U",
-         "CGX_SMALL_ANT")
+         "CGX_SMALL_ANT", "CGX_MV_NT")
 # form -> the knobs it sets (the rest: the library's default)
 FORMS = {"three": {"CGX_FUSE_P": "0", "CGX_FOLD_P": "0"}, "two": {"CGX_FUSE_P": "1", "CGX_FOLD_P": "0"},
          "fold": {"CGX_FUSE_P": "1", "CGX_FOLD_P": "1"}, "default": {},
@@ -32,6 +32,8 @@ if os.environ.get("R03_SMALL_VARIANTS"):  # k_matvec_small_f64's block size and 
             FORMS[f"fold_nt{nt}u{u}"] = {"CGX_FUSE_P": "1", "CGX_FOLD_P": "1", "CGX_SMALL_NT": nt, "CGX_SMALL_U": u}
 if os.environ.get("R03_SMALL_MALL"):  # default-policy A loads: A (<= 537 MB) may stay in the 256 MB MALL
     FORMS["fold_mall"] = {"CGX_FUSE_P": "1", "CGX_FOLD_P": "1", "CGX_SMALL_ANT": "0"}
+    FORMS["fold_nt"] = {"CGX_FUSE_P": "1", "CGX_FOLD_P": "1", "CGX_SMALL_ANT": "1", "CGX_MV_NT": "8"}
+    FORMS["two_nt"] = {"CGX_FUSE_P": "1", "CGX_FOLD_P": "0", "CGX_SMALL_ANT": "1", "CGX_MV_NT": "8"}
 
 
 def run(n, form, steps=400, warm=50):
