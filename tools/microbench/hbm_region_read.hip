@@ -69,6 +69,67 @@ __global__ __launch_bounds__(NT) void k_region(const d2 *__restrict__ a, int64_t
     out[(int64_t)blockIdx.x * NT + threadIdx.x] = acc.x + acc.y;
 }
 
+// k_symv_f64's exact load form: one contiguous region per block, each step
+// NT * K * 16 bytes read with raw buffer loads (a wave-uniform descriptor per
+// step, the lane offset t * 16, the load index in soffset), two slots.
+template <int NT, int K>
+__global__ __launch_bounds__(NT) void k_region_buf(const d2 *__restrict__ a, int64_t steps, double *out) {
+    const int t = threadIdx.x;
+    const int64_t step_d2 = (int64_t)NT * K;
+    const d2 *base = a + (int64_t)blockIdx.x * steps * step_d2;
+    d2 s0[K], s1[K], acc = (d2)(0.0);
+    auto load = [&](d2 *s, int64_t st) {
+        st = st < steps ? st : steps - 1;
+        const __amdgpu_buffer_rsrc_t rs =
+            __builtin_amdgcn_make_buffer_rsrc((void *)(base + st * step_d2), 0, (int)(step_d2 * 16), 0x00020000);
+#pragma unroll
+        for (int k = 0; k < K; ++k)
+            s[k] = __builtin_bit_cast(d2, __builtin_amdgcn_raw_buffer_load_b128(rs, t * 16, k * NT * 16, 2));
+    };
+    load(s0, 0);
+    for (int64_t st = 0; st < steps; st += 2) {
+        load(s1, st + 1);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int k = 0; k < K; ++k) acc += s0[k];
+        load(s0, st + 2);
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int k = 0; k < K; ++k) acc += s1[k];
+    }
+    out[(int64_t)blockIdx.x * NT + threadIdx.x] = acc.x + acc.y;
+}
+template <int NT, int K>
+void run_buf(const d2 *a, int64_t total_d2, double *out, int blocks, int reps, bool &first) {
+    const int64_t step_d2 = (int64_t)NT * K;
+    int64_t steps = total_d2 / ((int64_t)blocks * step_d2);
+    steps &= ~int64_t(1);
+    const double bytes = (double)steps * blocks * step_d2 * 16.0;
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    hipLaunchKernelGGL((k_region_buf<NT, K>), dim3(blocks), dim3(NT), 0, 0, a, steps, out);
+    CK(hipDeviceSynchronize());
+    std::vector<float> ms;
+    for (int r = 0; r < reps; ++r) {
+        CK(hipEventRecord(e0));
+        hipLaunchKernelGGL((k_region_buf<NT, K>), dim3(blocks), dim3(NT), 0, 0, a, steps, out);
+        CK(hipEventRecord(e1));
+        CK(hipEventSynchronize(e1));
+        float tm = 0;
+        CK(hipEventElapsedTime(&tm, e0, e1));
+        ms.push_back(tm);
+    }
+    std::sort(ms.begin(), ms.end());
+    CK(hipEventDestroy(e0));
+    CK(hipEventDestroy(e1));
+    const double gbps = bytes / (ms[ms.size() / 2] * 1e-3) / 1e9;
+    std::printf("%s\n  {\"threads\": %d, \"streams_per_block\": 1, \"buffer_loads\": 1, \"K\": %d, \"blocks\": %d, "
+                "\"step_bytes\": %lld, \"GBps\": %.1f}",
+                first ? "" : ",", NT, K, blocks, (long long)(step_d2 * 16), gbps);
+    first = false;
+}
+
 template <int NT, int S, int K, bool ALT = false>
 void run(const d2 *a, int64_t total_d2, double *out, int blocks, int reps, bool &first) {
     const int64_t step_d2 = (int64_t)(NT / S) * K;
@@ -125,6 +186,11 @@ int main(int argc, char **argv) {
         run<256, 1, 16>(a, n, out, 2 * cus, 5, first);
         run<256, 4, 16>(a, n, out, 2 * cus, 5, first);
         run<256, 4, 16>(a, n, out, cus, 5, first);
+        // round 3: k_symv_f64's shape (256 threads, one region per block, one
+        // block per CU) with global loads and with its buffer loads
+        run<256, 1, 16>(a, n, out, cus, 5, first);
+        run_buf<256, 16>(a, n, out, cus, 5, first);
+        run_buf<256, 16>(a, n, out, 2 * cus, 5, first);
     }
     std::printf("\n]}\n");
     CK(hipFree(a));
