@@ -537,6 +537,8 @@ static int iterate_gated(cgx_ctx *c, int64_t count, double eps, int64_t *done, i
     Shard &s0 = c->sh[0];
     const char *la = std::getenv("CGX_LOOKAHEAD");
     const int look = std::max(1, std::min(kLookRing - 1, (la && *la) ? std::atoi(la) : 2));
+    const char *le = std::getenv("CGX_LOOK_EVERY");  // an event after every E-th iteration
+    const int64_t every = std::max(1, (le && *le) ? std::atoi(le) : 1);
     const int64_t k0 = c->k;
     int64_t issued = 0, kd = 0;
     volatile int64_t *rec = s0.h_rec;  // {kdone, r.r bits}, stored by the deciding kernel
@@ -551,10 +553,12 @@ static int iterate_gated(cgx_ctx *c, int64_t count, double eps, int64_t *done, i
         int stop = 0;
         TRY(do_iteration(c, eps, &stop, /*gated=*/true));
         TRY(set_dev(s0));
-        const int q = (int)(issued % kLookRing);
-        HIPT(hipEventRecord(s0.ev_look[q], s0.stream));
-        if (issued >= look) {
-            TRY(rank_wait_event(c, s0.ev_look[(issued - look) % kLookRing], "an earlier iteration"));
+        if ((issued + 1) % every) continue;
+        const int64_t ev = (issued + 1) / every - 1;  // this event's index
+        HIPT(hipEventRecord(s0.ev_look[ev % kLookRing], s0.stream));
+        if (ev >= look) {
+            TRY(rank_wait_event(c, s0.ev_look[(ev - look) % kLookRing], "an earlier iteration"));
+            const int64_t synced = (ev - look + 1) * every - 1;  // the last iteration that event covers
             // Only a record left by an iteration the event covers counts: the
             // host-mapped word may already show a later iteration's decision,
             // and acting on that would make the number of enqueued iterations
@@ -563,7 +567,7 @@ static int iterate_gated(cgx_ctx *c, int64_t count, double eps, int64_t *done, i
             // converged iteration + 1, Poisson: the next iteration), so
             // k <= the synced iteration means that launch is covered.
             const int64_t r = rec[0];
-            if (r != 0 && r <= k0 + (issued - look)) kd = r;
+            if (r != 0 && r <= k0 + synced) kd = r;
         }
     }
     TRY(sync_all(c));
