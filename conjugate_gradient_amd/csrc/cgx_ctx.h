@@ -148,6 +148,7 @@ constexpr int kMaxShards = 32;
 constexpr int S_RR = 0, S_PAP = 4, S_LRR = 8, S_LPAP = 12, S_GATHER = 16;
 constexpr int S_TR = 128, S_TB = 129, S_LTR = 130, S_LTB = 131;  // true-residual check
 constexpr int S_XNZ = 134;  // rank mode: count of ranks whose x0 is not all zeros
+constexpr int S_XALPHA = 135;  // fused Poisson, x every other iteration: the alpha of the x update left out
 constexpr int S_KDONE = 132, S_RRFINAL = 133;  // device-side convergence: k+1 at the break, r.r there
 constexpr int kLookRing = 8;                    // pinned slots for the host's lagged convergence checks
 inline int ring(int64_t j) { return (int)(j & 3); }
@@ -261,6 +262,12 @@ struct cgx_ctx {
     bool ref_fused = false;   // ... and on one GPU: two launches per iteration (matVec + p.Ap, x/r/r.r/p)
     bool halo_overlap = false;  // fused Poisson, several slabs: r's halo exchange overlaps k_poisson_p
     bool halo_pending = false;  // an overlapped r halo exchange is in flight on the comm streams
+    // fused Poisson: x updated every other iteration (k_poisson_xr_f64's XM;
+    // CGX_POISSON_XDEFER=0: every iteration).  Within one cgx_iterate call the
+    // iterations k0, k0+2, ... leave x out and k0+1, k0+3, ... catch up; a call
+    // that ends after a left-out update finishes x (poisson_x_finish).
+    bool xdefer = false;
+    int64_t xd_k0 = 0;
     // rank mode fail-fast (cgx_exchange.hip, rank_wait_*): every host wait
     // polls with a deadline of rccl_timeout_s seconds (CGX_RCCL_TIMEOUT_S,
     // default 60, 0 = wait forever) and checks the communicator's asynchronous
@@ -352,6 +359,7 @@ int x0_is_zero(cgx_ctx *c, bool *zero);
 int do_begin(cgx_ctx *c);
 int read_scalar(cgx_ctx *c, int gslot, double *out);
 int do_iteration_poisson(cgx_ctx *c, double eps, int *stop, bool gated);
+int poisson_x_finish(cgx_ctx *c);
 int do_iteration(cgx_ctx *c, double eps, int *stop, bool gated = false);
 // cgx_api.hip
 int dev_ws(RedWs *out);

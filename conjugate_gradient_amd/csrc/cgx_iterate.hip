@@ -240,7 +240,10 @@ int read_scalar(cgx_ctx *c, int gslot, double *out) {
 //   allreduce(p.Ap)
 //   x += alpha p_k, r -= alpha A p_k, r.r
 //   allreduce(r.r); host-checked stop; r's halo rows for the next iteration.
-// x is current after every iteration, so a converged solve needs no extra pass.
+// x is updated every other iteration (c->xdefer: the left-out iteration's
+// alpha is kept in S_XALPHA and p_k stays in its slab until the next
+// iteration's xr kernel has read it); poisson_x_finish completes it at the end
+// of a cgx_iterate call.
 int do_iteration_poisson(cgx_ctx *c, double eps, int *stop, bool gated) {
     const int64_t k = c->k;
     *stop = 0;
@@ -249,6 +252,8 @@ int do_iteration_poisson(cgx_ctx *c, double eps, int *stop, bool gated) {
     const int rk = S_RR + ring(k), rkm1 = S_RR + ring(k + 3);  // r.r of iterations k, k-1
     auto D = [](void *p) { return reinterpret_cast<double *>(p); };
     const bool split = c->halo_pending;  // interior runs while the r halo exchange is in flight
+    // x every other iteration: leave it out at k0, k0+2, ..., catch up at k0+1, ...
+    const int xmode = !c->xdefer ? 1 : ((k - c->xd_k0) & 1) ? 2 : 0;
     for (auto &s : c->sh) {
         TRY(set_dev(s));
         char *pold = (k & 1) ? s.pfull : s.p2, *pnew = (k & 1) ? s.p2 : s.pfull;
@@ -269,9 +274,9 @@ int do_iteration_poisson(cgx_ctx *c, double eps, int *stop, bool gated) {
         const bool timing = (c->flags & CGX_TIMING) && (&s == &c->sh[0]);
         if (timing && s.ev_used >= kEvPairs) TRY(timing_resolve(c));
         if (timing) HIPT(hipEventRecord(s.ev_t[2 * s.ev_used], s.stream));
-        char *pnew = (k & 1) ? s.p2 : s.pfull;
-        HIPT(poisson_xr_f64(D(pnew), D(s.x), D(s.r), s.nloc / m, m, D(slot(s, rk)), D(slot(s, pg)), D(slot(s, ro)),
-                            s.ws, s.stream, gate_of(s, gated)));
+        char *pnew = (k & 1) ? s.p2 : s.pfull, *pold = (k & 1) ? s.pfull : s.p2;
+        HIPT(poisson_xr_f64(D(pnew), D(pold), D(s.x), D(s.r), s.nloc / m, m, D(slot(s, rk)), D(slot(s, pg)),
+                            D(slot(s, ro)), xmode, D(slot(s, S_XALPHA)), s.ws, s.stream, gate_of(s, gated)));
         if (timing) {
             HIPT(hipEventRecord(s.ev_t[2 * s.ev_used + 1], s.stream));
             s.ev_used++;
@@ -292,6 +297,26 @@ int do_iteration_poisson(cgx_ctx *c, double eps, int *stop, bool gated) {
         }
     }
     return c->halo_overlap ? exchange_halo_async(c) : exchange_halo_of(c, &Shard::rh);
+}
+
+// The end of a cgx_iterate call (the device's loop count known: c->k): when
+// the last iteration run left x's update out (xmode 0), x += alpha_K p_K.
+// Gated solves enqueue iterations past the stop that skip themselves, so this
+// is decided from c->k, never from what was enqueued.
+int poisson_x_finish(cgx_ctx *c) {
+    if (!c->fused || !c->xdefer) return CGX_OK;
+    const int64_t last = c->k - 1;
+    if (last >= c->xd_k0 && ((last - c->xd_k0) & 1) == 0) {
+        for (auto &s : c->sh) {
+            TRY(set_dev(s));
+            char *pk = (last & 1) ? s.p2 : s.pfull;
+            HIPT(poisson_xflush_f64(reinterpret_cast<const double *>(pk), reinterpret_cast<double *>(s.x),
+                                    s.nloc / c->m, c->m, reinterpret_cast<const double *>(slot(s, S_XALPHA)),
+                                    s.stream));
+        }
+    }
+    c->xd_k0 = c->k;
+    return CGX_OK;
 }
 
 // One loop iteration k (serialConjugate.c:215-244 / parallel_cg.c:290-323).
@@ -594,6 +619,7 @@ static int iterate_gated(cgx_ctx *c, int64_t count, double eps, int64_t *done, i
             c->state = ST_CONVERGED;
         }
     }
+    TRY(poisson_x_finish(c));
     if (done) *done = did;
     if (converged) *converged = c->converged;
     return CGX_OK;
@@ -605,6 +631,7 @@ int cgx_iterate(cgx_ctx *c, int64_t count, double eps, int64_t *done, int *conve
     if (c->state == ST_IDLE) return fail(CGX_ERR_STATE, "cgx_iterate before cgx_solve_begin");
     const char *gv = std::getenv("CGX_GATED");
     const bool gate_ok = !(gv && *gv == '0');
+    c->xd_k0 = c->k;
     if (c->state == ST_BEGUN && count > 0 && eps >= 0.0 && !(c->flags & CGX_HOST_STREAM) && gate_ok)
         return iterate_gated(c, count, eps, done, converged);
     int64_t did = 0;
@@ -615,6 +642,7 @@ int cgx_iterate(cgx_ctx *c, int64_t count, double eps, int64_t *done, int *conve
         ++did;
         if (stop) break;
     }
+    TRY(poisson_x_finish(c));
     if (done) *done = did;
     if (converged) *converged = c->converged;
     return CGX_OK;

@@ -312,18 +312,31 @@ __global__ __launch_bounds__(kNT) void k_poisson_p_f64(const double *__restrict_
 // k_poisson_xr_f64 (iteration k): alpha = *rsold / *pAp; x += alpha p_k and
 // r -= alpha A p_k with A p_k recomputed from p_k (halo included);
 // *rr_out = r.r.  Skipped once *gate != 0.
-template <int RBn, bool NT, bool HT>
-__device__ __forceinline__ void poisson_xr_step(const double *__restrict__ pnh, double *__restrict__ x,
-                                                double *__restrict__ r, int64_t m, int64_t i, const StripLane &L,
-                                                double alpha, d2 &pm, d2 &pc, double &acc, double *eb) {
+//
+// x's update every other iteration (XM, the solver's CGX_POISSON_XDEFER):
+//   XM = 1: x += alpha_k p_k (every iteration: 40 B per point);
+//   XM = 0: x is not touched; alpha_k goes to *xalpha (24 B per point);
+//   XM = 2: x += alpha_{k-1} p_{k-1} (p_{k-1} = the other slab, which the next
+//           k_poisson_p overwrites only after this kernel; alpha_{k-1} from
+//           *xalpha), then x += alpha_k p_k (48 B per point).
+// The two FMAs are XM = 1's two iterations' own, in the same order, so x is
+// bit for bit the every-iteration update's; a solve that ends after an XM = 0
+// iteration finishes x with k_poisson_xflush_f64.  60 instead of 64 B per
+// point per iteration over a pair of iterations.
+template <int RBn, bool NT, bool HT, int XM>
+__device__ __forceinline__ void poisson_xr_step(const double *__restrict__ pnh, const double *__restrict__ poh,
+                                                double *__restrict__ x, double *__restrict__ r, int64_t m, int64_t i,
+                                                const StripLane &L, double alpha, double alpha_prev, d2 &pm, d2 &pc,
+                                                double &acc, double *eb) {
     const int lane = threadIdx.x & 63;
-    d2 pr[RBn], xv[RBn], rv[RBn], ce[RBn];
+    d2 pr[RBn], xv[RBn], rv[RBn], ce[RBn], po[RBn];
     double el[RBn], er[RBn];
 #pragma unroll
     for (int t = 0; t < RBn; ++t) {
         const int64_t hc = (i + t + 1) * m, ic = (i + t) * m;
         pr[t] = keep(L.valid, (HT && t >= RBn - 2) ? lds2<false>(pnh + hc + m, L.off) : lds2<NT>(pnh + hc + m, L.off));
-        xv[t] = lds2<NT>(x + ic, L.off);
+        if constexpr (XM != 0) xv[t] = lds2<NT>(x + ic, L.off);
+        if constexpr (XM == 2) po[t] = lds2<NT>(poh + hc, L.off);
         rv[t] = lds2<NT>(r + ic, L.off);
         el[t] = L.has_l ? pnh[hc + L.jw - 1] : 0.0;
         er[t] = L.has_r ? pnh[hc + L.jw + 128] : 0.0;
@@ -345,13 +358,20 @@ __device__ __forceinline__ void poisson_xr_step(const double *__restrict__ pnh, 
         o.x = 4.0 * ce[t].x - up.x - dn.x - l - ce[t].y;
         o.y = 4.0 * ce[t].y - up.y - dn.y - ce[t].x - rt;
         d2 xn, rn;
-        xn.x = __builtin_fma(alpha, ce[t].x, xv[t].x);
-        xn.y = __builtin_fma(alpha, ce[t].y, xv[t].y);
+        if constexpr (XM == 2) {
+            xn.x = __builtin_fma(alpha_prev, po[t].x, xv[t].x);
+            xn.y = __builtin_fma(alpha_prev, po[t].y, xv[t].y);
+            xn.x = __builtin_fma(alpha, ce[t].x, xn.x);
+            xn.y = __builtin_fma(alpha, ce[t].y, xn.y);
+        } else if constexpr (XM == 1) {
+            xn.x = __builtin_fma(alpha, ce[t].x, xv[t].x);
+            xn.y = __builtin_fma(alpha, ce[t].y, xv[t].y);
+        }
         rn.x = __builtin_fma(-alpha, o.x, rv[t].x);
         rn.y = __builtin_fma(-alpha, o.y, rv[t].y);
         acc += L.valid ? rn.x * rn.x + rn.y * rn.y : 0.0;
         if (L.valid) {
-            sts2<NT>(x + (i + t) * m, L.off, xn);
+            if constexpr (XM != 0) sts2<NT>(x + (i + t) * m, L.off, xn);
             sts2<NT>(r + (i + t) * m, L.off, rn);
         }
     }
@@ -364,17 +384,22 @@ __device__ __forceinline__ void poisson_xr_step(const double *__restrict__ pnh, 
     }
 }
 
-template <int RB, bool NT, bool HT>
-__global__ __launch_bounds__(kNT) void k_poisson_xr_f64(const double *__restrict__ pnh, double *__restrict__ x,
-                                                        double *__restrict__ r, int64_t mloc, int64_t m,
-                                                        int64_t nstrips, int64_t rpi, int64_t nitems, int reverse,
-                                                        const double *rsold, const double *pAp, double *rr_out,
-                                                        double *partials, unsigned *ticket, const int64_t *gate,
-                                                        int bands) {
+// Every x mode runs on XM = 1's grid (launch_poisson_xr), so the r.r
+// partials add in the same order whichever variant runs (a thread adds its
+// rows in row order whatever RB is): x is the same bits with and without the
+// deferral.
+template <int RB, bool NT, bool HT, int XM>
+__global__ __launch_bounds__(kNT) void k_poisson_xr_f64(const double *__restrict__ pnh, const double *__restrict__ poh,
+                                                        double *__restrict__ x, double *__restrict__ r, int64_t mloc,
+                                                        int64_t m, int64_t nstrips, int64_t rpi, int64_t nitems,
+                                                        int reverse, const double *rsold, const double *pAp,
+                                                        double *rr_out, double *xalpha, double *partials,
+                                                        unsigned *ticket, const int64_t *gate, int bands) {
     static_assert(RB <= kEdgeRB, "edge buffer");
     __shared__ double edge[2 * kWaves * 2 * kEdgeRB];
     if (gate && *gate) return;
     const double alpha = cg_ratio(*rsold, *pAp);
+    const double alpha_prev = XM == 2 ? *xalpha : 0.0;
     double acc = 0.0;
     int par = 0;
     const Band bd = bands ? band_of(0, nitems, nstrips) : Band{0, nitems, (int64_t)gridDim.x, (int64_t)blockIdx.x};
@@ -390,11 +415,34 @@ __global__ __launch_bounds__(kNT) void k_poisson_xr_f64(const double *__restrict
         d2 pc = keep(L.valid, lds2<NT && !HT>(pnh + (i0 + 1) * m, L.off));
         int64_t i = i0;
         for (; i + RB <= i1; i += RB, par ^= 1)
-            poisson_xr_step<RB, NT, HT>(pnh, x, r, m, i, L, alpha, pm, pc, acc, edge + par * (kWaves * 2 * kEdgeRB));
+            poisson_xr_step<RB, NT, HT, XM>(pnh, poh, x, r, m, i, L, alpha, alpha_prev, pm, pc, acc,
+                                            edge + par * (kWaves * 2 * kEdgeRB));
         for (; i < i1; ++i, par ^= 1)
-            poisson_xr_step<1, NT, HT>(pnh, x, r, m, i, L, alpha, pm, pc, acc, edge + par * (kWaves * 2 * kEdgeRB));
+            poisson_xr_step<1, NT, HT, XM>(pnh, poh, x, r, m, i, L, alpha, alpha_prev, pm, pc, acc,
+                                           edge + par * (kWaves * 2 * kEdgeRB));
     }
+    // XM = 0: alpha_k for the next iteration's (or the flush's) x update.  Read
+    // by a later kernel on this stream only (kernel boundary = ordering).
+    if (XM == 0 && blockIdx.x == 0 && threadIdx.x == 0) *xalpha = alpha;
     grid_sum_last_block(acc, partials, ticket, rr_out);
+}
+
+// The x update an XM = 0 iteration left out: x += alpha p_k over the slab's
+// interior (p_k's slab pnh, alpha from *xalpha).  The same FMA as the xr
+// kernel's, so x is bit for bit the every-iteration update's.
+// Even m: npts is even and both slabs 16-B aligned, so it runs on pairs.
+__global__ __launch_bounds__(kNT) void k_poisson_xflush_f64(const double *__restrict__ pnh, double *__restrict__ x,
+                                                            int64_t npts, const double *xalpha) {
+    const double alpha = *xalpha;
+    const d2 *p = reinterpret_cast<const d2 *>(pnh);
+    d2 *xv = reinterpret_cast<d2 *>(x);
+    for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < npts / 2; i += (int64_t)gridDim.x * kNT) {
+        const d2 pv = __builtin_nontemporal_load(p + i), xo = __builtin_nontemporal_load(xv + i);
+        d2 o;
+        o.x = __builtin_fma(alpha, pv.x, xo.x);
+        o.y = __builtin_fma(alpha, pv.y, xo.y);
+        __builtin_nontemporal_store(o, xv + i);
+    }
 }
 
 __global__ __launch_bounds__(kNT) void k_stencil5_rows_f64(const double *__restrict__ ph, int64_t mloc, int64_t m,
@@ -503,17 +551,39 @@ static void launch_poisson_p(const PoissonPlan &pl, hipStream_t s, const double 
     hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(kNT), 0, s, rh, poh, pnh, mloc, m, pl.nstrips, pl.rpi, ir, rr,
                        rsold, first, cv, pap_out, add_to_out, ws.partials, ws.tickets + T_MATVEC, bands);
 }
-template <int RB>
-static void launch_poisson_xr(const PoissonPlan &pl, hipStream_t s, const double *pnh, double *x, double *r,
-                              int64_t mloc, int64_t m, const double *rsold, const double *pAp, double *rr_out,
-                              const RedWs &ws, const int64_t *gate) {
-    auto fn = pl.nt ? (pl.ht ? k_poisson_xr_f64<RB, true, true> : k_poisson_xr_f64<RB, true, false>)
-                    : k_poisson_xr_f64<RB, false, false>;
-    int64_t grid = resident_grid(reinterpret_cast<const void *>(fn), pl.nitems);
+using XrFn = void (*)(const double *, const double *, double *, double *, int64_t, int64_t, int64_t, int64_t, int64_t,
+                     int, const double *, const double *, double *, double *, double *, unsigned *, const int64_t *,
+                     int);
+template <int RB, int XM>
+static XrFn xr_fn(const PoissonPlan &pl) {
+    return pl.nt ? (pl.ht ? k_poisson_xr_f64<RB, true, true, XM> : k_poisson_xr_f64<RB, true, false, XM>)
+                 : k_poisson_xr_f64<RB, false, false, XM>;
+}
+template <int XM>
+static XrFn xr_fn_rb(const PoissonPlan &pl, int rb) {
+    switch (rb) {
+        case 1: return xr_fn<1, XM>(pl);
+        case 2: return xr_fn<2, XM>(pl);
+        case 8: return xr_fn<8, XM>(pl);
+        default: return xr_fn<4, XM>(pl);
+    }
+}
+// Every x mode runs on the grid of the every-iteration kernel at the plan's
+// RB (its occupancy), so the r.r partials add in the same order whichever
+// variant runs.  XM = 2 steps RB / 2 rows at a time (RB = 8: 193 VGPRs, 2
+// waves per SIMD, fewer than that grid; held to 3 waves it spilled).
+template <int XM>
+static void launch_poisson_xr(const PoissonPlan &pl, hipStream_t s, const double *pnh, const double *poh, double *x,
+                              double *r, int64_t mloc, int64_t m, const double *rsold, const double *pAp,
+                              double *rr_out, double *xalpha, const RedWs &ws, const int64_t *gate) {
+    const int rb = XM == 2 && pl.rb > 1 && !env_int("CGX_XR2_FULL_RB", 0) ? pl.rb / 2 : pl.rb;
+    const XrFn fn = xr_fn_rb<XM>(pl, rb);
+    const XrFn fg = env_int("CGX_XR_OWN_GRID", 0) ? fn : xr_fn_rb<1>(pl, pl.rb);
+    int64_t grid = resident_grid(reinterpret_cast<const void *>(fg), pl.nitems);
     const int bands = pl.bands && grid >= 8;
     if (bands) grid &= ~int64_t(7);
-    hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(kNT), 0, s, pnh, x, r, mloc, m, pl.nstrips, pl.rpi,
-                       pl.nitems, env_int("CGX_STENCIL_REVERSE", 1), rsold, pAp, rr_out, ws.partials,
+    hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(kNT), 0, s, pnh, poh, x, r, mloc, m, pl.nstrips, pl.rpi,
+                       pl.nitems, env_int("CGX_STENCIL_REVERSE", 1), rsold, pAp, rr_out, xalpha, ws.partials,
                        ws.tickets + T_XR, gate, bands);
 }
 
@@ -549,16 +619,28 @@ hipError_t poisson_p_f64(const double *rh, const double *poh, double *pnh, int64
     return hipGetLastError();
 }
 
-hipError_t poisson_xr_f64(const double *pnh, double *x, double *r, int64_t mloc, int64_t m, const double *rsold,
-                          const double *pAp, double *rr_out, const RedWs &ws, hipStream_t s, const int64_t *gate) {
+hipError_t poisson_xr_f64(const double *pnh, const double *poh, double *x, double *r, int64_t mloc, int64_t m,
+                          const double *rsold, const double *pAp, double *rr_out, int xmode, double *xalpha,
+                          const RedWs &ws, hipStream_t s, const int64_t *gate) {
     if (!poisson_fusable(mloc, m) || !al16(pnh) || !al16(x) || !al16(r)) return hipErrorInvalidValue;
+    if ((xmode != 1 && !xalpha) || (xmode == 2 && !al16(poh)) || xmode < 0 || xmode > 2) return hipErrorInvalidValue;
     const PoissonPlan pl = poisson_plan(mloc, m);
-    switch (pl.rb) {
-        case 1: launch_poisson_xr<1>(pl, s, pnh, x, r, mloc, m, rsold, pAp, rr_out, ws, gate); break;
-        case 2: launch_poisson_xr<2>(pl, s, pnh, x, r, mloc, m, rsold, pAp, rr_out, ws, gate); break;
-        case 8: launch_poisson_xr<8>(pl, s, pnh, x, r, mloc, m, rsold, pAp, rr_out, ws, gate); break;
-        default: launch_poisson_xr<4>(pl, s, pnh, x, r, mloc, m, rsold, pAp, rr_out, ws, gate); break;
-    }
+    if (xmode == 0)
+        launch_poisson_xr<0>(pl, s, pnh, poh, x, r, mloc, m, rsold, pAp, rr_out, xalpha, ws, gate);
+    else if (xmode == 2)
+        launch_poisson_xr<2>(pl, s, pnh, poh, x, r, mloc, m, rsold, pAp, rr_out, xalpha, ws, gate);
+    else
+        launch_poisson_xr<1>(pl, s, pnh, poh, x, r, mloc, m, rsold, pAp, rr_out, xalpha, ws, gate);
+    return hipGetLastError();
+}
+
+hipError_t poisson_xflush_f64(const double *pnh, double *x, int64_t mloc, int64_t m, const double *xalpha,
+                              hipStream_t s) {
+    const int64_t npts = mloc * m;
+    if (npts <= 0) return hipSuccess;
+    if (!poisson_fusable(mloc, m) || !al16(pnh) || !al16(x)) return hipErrorInvalidValue;
+    const unsigned grid = (unsigned)std::min<int64_t>((npts / 2 + kNT - 1) / kNT, 8192);
+    hipLaunchKernelGGL(k_poisson_xflush_f64, dim3(grid), dim3(kNT), 0, s, pnh + m, x, npts, xalpha);
     return hipGetLastError();
 }
 

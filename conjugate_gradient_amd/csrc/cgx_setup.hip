@@ -365,6 +365,8 @@ int finish_create(cgx_ctx *c, cgx_ctx **out) {
         const bool force = h && std::strcmp(h, "force") == 0;  // also at world size 1 in rank mode
         c->halo_overlap = c->fused && !(h && *h == '0') && c->mode != M_SINGLE &&
                           !(c->mode == M_RCCL && c->nranks == 1 && !force);
+        const char *xd = std::getenv("CGX_POISSON_XDEFER");
+        c->xdefer = c->fused && !(xd && *xd == '0');
     }
     for (auto &s : c->sh) {
         int rc = alloc_shard(c, s);
@@ -656,7 +658,8 @@ int cgx_get_info(const cgx_ctx *c, cgx_info *info) {
     for (auto &s : c->sh) info->nrows += s.nloc;
     info->flags = c->flags | (c->overlap ? CGX_OVERLAP_ACTIVE : 0) |
                   ((c->fused || c->fused_p || c->ref_fused) ? CGX_FUSED_ACTIVE : 0) | (c->peer ? CGX_PEER_ACTIVE : 0) |
-                  (c->sh[0].plan.small ? CGX_SMALL_ACTIVE : 0) | (c->fold_p ? CGX_FOLD_ACTIVE : 0);
+                  (c->sh[0].plan.small ? CGX_SMALL_ACTIVE : 0) | (c->fold_p ? CGX_FOLD_ACTIVE : 0) |
+                  (c->xdefer ? CGX_XDEFER_ACTIVE : 0);
     info->elem_bytes = c->es;
     return CGX_OK;
 }

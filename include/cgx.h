@@ -134,6 +134,12 @@ extern "C" {
 #define CGX_FOLD_ACTIVE  0x80000 /* reported in cgx_info.flags: the two-launch
                                     iteration folds p = r + beta p into the
                                     next matVec (CGX_FOLD_P) */
+#define CGX_XDEFER_ACTIVE 0x100000 /* reported in cgx_info.flags: the fused
+                                    Poisson iteration updates x every other
+                                    iteration (60 instead of 64 B per grid
+                                    point; x the same bits after every
+                                    cgx_iterate call; CGX_POISSON_XDEFER=0:
+                                    every iteration) */
 
 typedef struct cgx_ctx cgx_ctx;
 

@@ -735,6 +735,56 @@ def test_poisson_halo_overlap_matches(monkeypatch, m, P, eps):
         assert rel(x1, x0) <= 1e-12 and rel(x1, xo) <= TOL
 
 
+def _poisson_x_runs(m, shards, xdefer, monkeypatch):
+    """x after each way of driving a fused Poisson solve (x updated every other
+    iteration, or every iteration with CGX_POISSON_XDEFER=0)."""
+    monkeypatch.setenv("CGX_POISSON_XDEFER", xdefer)
+    out = {}
+    with cg.Solver(None, poisson_m=m, devices=shards) as s:
+        assert s.info.flags & cg.CGX_FUSED_ACTIVE
+        assert bool(s.info.flags & cg.CGX_XDEFER_ACTIVE) == (xdefer == "1")
+        for gated in ("1", "0"):
+            monkeypatch.setenv("CGX_GATED", gated)
+            s.fill(1.0, 0.0)
+            x, st = s.solve(None, eps=1e-10)
+            out["solve" + gated] = (x, st.iterations)
+        for count in (1, 2, 7, 8):  # fixed count, odd and even
+            s.fill(1.0, 0.0)
+            s.begin()
+            d, _ = s.iterate(count, eps=-1.0)
+            out[f"fixed{count}"] = (s.get_x(), d)
+        s.fill(1.0, 0.0)  # pieces of odd length, then convergence-tested
+        s.begin()
+        s.iterate(3, eps=-1.0)
+        s.iterate(5, eps=-1.0)
+        d, c = s.iterate(10 ** 6, eps=1e-10)
+        out["pieces"] = (s.get_x(), d, c)
+    return out
+
+
+@pytest.mark.parametrize("m,shards", [(64, None), (96, [0] * 4), (130, [0, 0]), (1040, None)])
+def test_poisson_x_every_other_iteration_is_bitwise(monkeypatch, m, shards):
+    """k_poisson_xr_f64 updates x every other iteration (the left-out iteration's
+    alpha kept, p_{k-1} read from the other slab; 60 instead of 64 B per point)
+    with the every-iteration update's two FMAs in the same order: x is bit for
+    bit CGX_POISSON_XDEFER=0's after every way a solve can end (gated and
+    host-checked convergence at either parity, fixed counts 1/2/7/8, odd pieces),
+    with the same loop counts."""
+    monkeypatch.setenv("CGX_POISSON_FUSED", "1")
+    a = _poisson_x_runs(m, shards, "1", monkeypatch)
+    b = _poisson_x_runs(m, shards, "0", monkeypatch)
+    assert a.keys() == b.keys()
+    for key in a:
+        assert np.array_equal(a[key][0], b[key][0]), key
+        assert a[key][1:] == b[key][1:], key
+    if m >= 520:  # eps = 1e-10 is below the attainable residual there (test_poisson_matches_oracle)
+        return
+    n = m * m
+    xo, so = oracle.cg_poisson_f64(m, np.ones(n), np.zeros(n), eps=1e-10)
+    assert a["solve1"][1] == a["solve0"][1] == so.iterations
+    assert rel(a["solve1"][0], xo) <= TOL
+
+
 def test_poisson_fused_in_pieces_and_iteration_cap():
     """Iterations issued in several cgx_iterate calls (fixed count, then
     convergence-tested) give the one-call solve; a cap that stops exactly at
