@@ -16,7 +16,12 @@ import re
 
 def short(name):
     m = re.search(r"(k_\w+)(<[^>]*>)?", name)
-    return m.group(1) if m else name
+    if not m:
+        return name
+    if m.group(1) == "k_poisson_xr_f64" and m.group(2) and m.group(2).count(",") == 3:
+        # x every other iteration: the variants move different bytes (XM = last argument)
+        return f"k_poisson_xr_f64<XM={m.group(2).strip('<>').split(',')[-1].strip()}>"
+    return m.group(1)
 
 
 def algorithmic(w, kernel, n, m):
@@ -28,8 +33,14 @@ def algorithmic(w, kernel, n, m):
         return 8 * 128 * 128 * t * (t + 1) // 2 + 16 * n  # tiles + p + y (partials are overhead)
     if w == "poisson" and kernel == "k_poisson_p_f64":
         return 24 * m * m
-    if w == "poisson" and kernel == "k_poisson_xr_f64":
+    if w == "poisson" and kernel in ("k_poisson_xr_f64", "k_poisson_xr_f64<XM=1>"):
         return 40 * m * m + 16 * m
+    if w == "poisson" and kernel == "k_poisson_xr_f64<XM=0>":  # p_k (+ halo rows), r -> r
+        return 24 * m * m + 16 * m
+    if w == "poisson" and kernel == "k_poisson_xr_f64<XM=2>":  # p_{k-1}, p_k (+ halo), x, r -> x, r
+        return 48 * m * m + 16 * m
+    if w == "poisson" and kernel == "k_poisson_xflush_f64":
+        return 24 * m * m
     return None
 
 
