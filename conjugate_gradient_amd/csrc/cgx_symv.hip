@@ -182,146 +182,6 @@ __device__ __forceinline__ void sym_unit(const SymSlot &S, int64_t u, double (*c
     }
 }
 
-// The paired form (CGX_SYM_PAIR=1): the same arithmetic as sym_unit, but a
-// unit's column partials go to its own LDS half (slot) and the block crosses
-// one barrier per PAIR of units; sym_pair_cols then stores both units'
-// column sums (threads 0-63 the first unit's, 64-127 the second's).  The
-// same bits: every column sum adds the 16 thread rows in the same order.
-__device__ __forceinline__ void sym_unit_rows(const SymSlot &S, int64_t u, double *__restrict__ prow, int tr, int tc,
-                                              double &racc, int64_t &urun, bool end_of_run) {
-    double rs[kSymRPT];
-#pragma unroll
-    for (int rr = 0; rr < kSymRPT; ++rr) {
-        double v = S.a[2 * rr].x * S.pj[0].x;
-        v = __builtin_fma(S.a[2 * rr].y, S.pj[0].y, v);
-        v = __builtin_fma(S.a[2 * rr + 1].x, S.pj[1].x, v);
-        rs[rr] = __builtin_fma(S.a[2 * rr + 1].y, S.pj[1].y, v);
-    }
-    int row = 0;
-    double k1;
-    {
-        const bool h1 = tc & 8;
-        double k[4];
-#pragma unroll
-        for (int q = 0; q < 4; ++q) k[q] = (h1 ? rs[q + 4] : rs[q]) + __shfl_xor(h1 ? rs[q] : rs[q + 4], 8, 64);
-        row += h1 ? 4 : 0;
-        const bool h2 = tc & 4;
-        double m[2];
-#pragma unroll
-        for (int q = 0; q < 2; ++q) m[q] = (h2 ? k[q + 2] : k[q]) + __shfl_xor(h2 ? k[q] : k[q + 2], 4, 64);
-        row += h2 ? 2 : 0;
-        const bool h3 = tc & 2;
-        k1 = (h3 ? m[1] : m[0]) + __shfl_xor(h3 ? m[0] : m[1], 2, 64);
-        row += h3 ? 1 : 0;
-    }
-    k1 += __shfl_xor(k1, 1, 64);
-    racc += k1;
-    if (end_of_run) {
-        if ((tc & 1) == 0) prow[urun * kSymT + tr * kSymRPT + row] = racc;
-        racc = 0.0;
-        urun = u + 1;
-    }
-}
-__device__ __forceinline__ void sym_unit_cols_lds(const SymSlot &S, double (*cs)[kSymH], int tr, int tc) {
-    if (S.J > S.I) {
-        double c[4] = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-        for (int rr = 0; rr < kSymRPT; ++rr) {
-            const double pr = (rr & 1) ? S.pi[rr >> 1].y : S.pi[rr >> 1].x;
-            c[0] = __builtin_fma(S.a[2 * rr].x, pr, c[0]);
-            c[1] = __builtin_fma(S.a[2 * rr].y, pr, c[1]);
-            c[2] = __builtin_fma(S.a[2 * rr + 1].x, pr, c[2]);
-            c[3] = __builtin_fma(S.a[2 * rr + 1].y, pr, c[3]);
-        }
-        *reinterpret_cast<d2 *>(&cs[tr][tc * 4]) = d2{c[0], c[1]};
-        *reinterpret_cast<d2 *>(&cs[tr][tc * 4 + 2]) = d2{c[2], c[3]};
-    }
-}
-// after the barrier: unit (uq, Iq, Jq, hq)'s column sums from LDS half cs, by 64 threads
-__device__ __forceinline__ void sym_cols_store(double (*cs)[kSymH], int64_t uq, int64_t Iq, int64_t Jq, int hq, int c,
-                                               double *__restrict__ pcol) {
-    if (Jq > Iq) {
-        double sum = cs[0][c];
-#pragma unroll
-        for (int g = 1; g < kSymTR; ++g) sum += cs[g][c];
-        pcol[(uq >> 1) * kSymT + hq * kSymH + c] = sum;
-    }
-}
-
-template <int NTL>
-__global__ __launch_bounds__(kSymNT) void k_symv_pair_f64(const double *__restrict__ At, int64_t nt, int64_t q_base,
-                                                          int64_t count, int64_t per, int tile_runs,
-                                                          const double *__restrict__ p, double *__restrict__ prow,
-                                                          double *__restrict__ pcol, const int64_t *gate) {
-    if (gate && *gate) return;
-    __shared__ double cs[2][2][kSymTR][kSymH];  // [buffer][unit of the pair]
-    const int t = threadIdx.x, tr = t / kSymTC, tc = t % kSymTC;
-    const int64_t u_base = 2 * q_base, u_end = 2 * (q_base + count);
-    const int64_t u0 = u_base + (int64_t)blockIdx.x * per;
-    const int64_t u1 = (u0 + per < u_end) ? u0 + per : u_end;
-    if (u0 >= u1) return;
-    int64_t Ic, Jc;
-    sym_tile_ij(u0 >> 1, nt, Ic, Jc);
-    int hc = (int)(u0 & 1);
-    const __amdgpu_buffer_rsrc_t prs =
-        __builtin_amdgcn_make_buffer_rsrc((void *)p, 0, (int)(nt * kSymT * 8), 0x00020000);
-    int buf = 0;
-    double racc = 0.0;
-    int64_t urun = u0;
-    SymSlot S0, S1;
-    sym_load<NTL>(S0, At, prs, u0 - u_base, Ic, Jc, hc, t, tr, tc);
-    // 32-bit loop counter (a 64-bit compare of SGPR pairs takes a VGPR, and the
-    // compiler picked one a load in flight writes: vmcnt(6) at every latch)
-    const int cnt = (int)(u1 - u0);
-    for (int e = 0; e < cnt; e += 2) {
-        const int64_t u = u0 + e;
-        int64_t I1 = Ic, J1 = Jc;
-        int h1 = hc;
-        sym_next(I1, J1, h1, nt);
-        const bool va = e + 1 < cnt;
-        sym_load<NTL>(S1, At, prs, (va ? u + 1 : u) - u_base, va ? I1 : Ic, va ? J1 : Jc, va ? h1 : hc, t, tr, tc);
-        __builtin_amdgcn_sched_barrier(0);
-        if (tile_runs) urun = u;
-        sym_unit_rows(S0, u, prow, tr, tc, racc, urun, tile_runs || !va || I1 != Ic);
-        sym_unit_cols_lds(S0, cs[buf][0], tr, tc);
-        const int64_t uA = u, IA = S0.I, JA = S0.J;
-        const int hA = S0.h;
-        if (!va) {
-            asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-            if (t < kSymH) sym_cols_store(cs[buf][0], uA, IA, JA, hA, t, pcol);
-            break;
-        }
-        int64_t I2 = I1, J2 = J1;
-        int h2 = h1;
-        sym_next(I2, J2, h2, nt);
-        const bool vb = e + 2 < cnt;
-        sym_load<NTL>(S0, At, prs, (vb ? u + 2 : u + 1) - u_base, vb ? I2 : I1, vb ? J2 : J1, vb ? h2 : h1, t, tr,
-                      tc);
-        __builtin_amdgcn_sched_barrier(0);
-        if (tile_runs) urun = u + 1;
-        sym_unit_rows(S1, u + 1, prow, tr, tc, racc, urun, tile_runs || !vb || I2 != I1);
-        sym_unit_cols_lds(S1, cs[buf][1], tr, tc);
-        // LDS-only barrier (see sym_unit): the next units' loads stay in flight
-        asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
-        {  // threads 0-63: unit u's column sums, 64-127: unit u+1's (wave-uniform choice)
-            const int wq = t >> 6, c = t & (kSymH - 1);
-            const bool second = wq == 1;
-            const int64_t uq = second ? u + 1 : uA, Iq = second ? S1.I : IA, Jq = second ? S1.J : JA;
-            const int hq = second ? S1.h : hA;
-            if (wq < 2 && Jq > Iq) {
-                double sum = cs[buf][wq][0][c];
-#pragma unroll
-                for (int g = 1; g < kSymTR; ++g) sum += cs[buf][wq][g][c];
-                pcol[(uq >> 1) * kSymT + hq * kSymH + c] = sum;
-            }
-        }
-        buf ^= 1;
-        Ic = I2;
-        Jc = J2;
-        hc = h2;
-    }
-}
-
 // Two slots alternate: the loads of unit u+1 go out before unit u's
 // arithmetic.
 // Tiles [q_base, q_base + count) of the triangle, At holding exactly those
@@ -519,15 +379,7 @@ hipError_t symv_tiles_f64(const double *At, int64_t q_base, int64_t count, int64
         ((reinterpret_cast<uintptr_t>(At) | reinterpret_cast<uintptr_t>(p)) & 15))
         return hipErrorInvalidValue;
     const int64_t per = (2 * count + grid - 1) / grid;  // units per block
-    // One column-partial barrier per pair of units when each block streams a
-    // long range: N=65536 (1026 units per block) 388.6-389.6 vs 361.9-362.2 it/s,
-    // N=32768 (257) 1383-1385 vs 1401-1402, N=16384 (65) 5176-5189 vs
-    // 5240-5262, interleaved on two boxes (profiles/r03_symmetric_pair_ab.jsonl);
-    // the same bits either way.  CGX_SYM_PAIR=0 / 1 forces one form.
-    const int pe = env_int("CGX_SYM_PAIR", -1);
-    const bool pair = pe >= 0 ? pe != 0 : per >= 512;
-    auto fn = pair ? (env_int("CGX_SYM_NT", 1) ? k_symv_pair_f64<1> : k_symv_pair_f64<0>)
-                   : (env_int("CGX_SYM_NT", 1) ? k_symv_f64<1> : k_symv_f64<0>);
+    auto fn = env_int("CGX_SYM_NT", 1) ? k_symv_f64<1> : k_symv_f64<0>;
     hipLaunchKernelGGL(fn, dim3(grid), dim3(kSymNT), 0, s, At, lda / kSymT, q_base, count, per, tile_runs ? 1 : 0, p,
                        prow, pcol, gate);
     return hipGetLastError();

@@ -159,24 +159,3 @@ def test_symmetric_host_streamed_with_resident_tiles(monkeypatch, resident_mb):
         assert ia == ib and np.array_equal(xa.view(np.uint8), xb.view(np.uint8))
     xo, so = oracle.cg_f64(A2, b2, np.zeros(n), eps=1e-10)
     assert out[resident_mb][1][1] == so.iterations and rel(out[resident_mb][1][0], xo) <= TOL
-
-
-@pytest.mark.parametrize("n,stream", [(2304, False), (5000, False), (16384, False), (4096, True)])
-def test_symmetric_pair_kernel_is_bitwise(monkeypatch, n, stream):
-    """k_symv_pair_f64 (one column-partial barrier per pair of units, the
-    default when a block streams >= 512 units) adds every row and column
-    partial in k_symv_f64's order: x and the loop count are the same bits, on
-    the resident tiles (odd unit ranges per block: 2304, 5000) and streamed in
-    chunks of whole tiles (every unit its own run)."""
-    if stream:
-        monkeypatch.setenv("CGX_STREAM_TILE_MB", "1")
-    flags = SYM | (cg.CGX_HOST_STREAM if stream else 0)
-    res = {}
-    for pair in ("0", "1"):
-        monkeypatch.setenv("CGX_SYM_PAIR", pair)
-        with cg.Solver(n, flags=flags) as s:
-            s.generate_spd(7)
-            x, st = s.solve(None, eps=1e-10)
-            res[pair] = (x, st.iterations)
-    assert res["0"][1] == res["1"][1]
-    assert np.array_equal(res["0"][0], res["1"][0])
