@@ -362,12 +362,25 @@ int sym_grid(int device) {
     return cus * per_cu;
 }
 
+// Units per block (each block streams one contiguous range), rounded up to an
+// odd count: the 256 ranges then start at 32 different offsets modulo 2 MiB
+// (64-KiB units) instead of all at one offset modulo 128 KiB (N=65536: 1026
+// units per block), so the streams spread over the HBM channels however the
+// pages land.  N=65536: 399.5-399.7 it/s (6.91 TB/s on the stored bytes)
+// against 387.6-388.6 with 1026, four processes each, alternating
+// (profiles/r03_symmetric_per_odd_ab.jsonl).  CGX_SYM_PER_ODD=0: the plain count.
+static int64_t sym_units_per_block(int64_t units, int grid) {
+    int64_t per = (units + grid - 1) / grid;
+    if (env_int("CGX_SYM_PER_ODD", 1) && per > 1) per |= 1;
+    return per;
+}
+
 hipError_t symv_f64(const double *At, int64_t n, int64_t lda, int grid, const double *p, double *prow, double *pcol,
                     double *y, const double *pown, double *dot_out, const RedWs &ws, hipStream_t s,
                     const int64_t *gate) {
     const int64_t ntiles = sym_tiles(lda);
     if (grid <= 0) return hipErrorInvalidValue;
-    const int64_t per = (2 * ntiles + grid - 1) / grid;  // units per block
+    const int64_t per = sym_units_per_block(2 * ntiles, grid);
     hipError_t e = symv_tiles_f64(At, 0, ntiles, lda, grid, false, p, prow, pcol, s, gate);
     if (e != hipSuccess) return e;
     return symv_reduce_f64(n, lda, per, prow, pcol, y, pown, dot_out, ws, s, gate);
@@ -378,7 +391,7 @@ hipError_t symv_tiles_f64(const double *At, int64_t q_base, int64_t count, int64
     if (lda % kSymT || grid <= 0 || count <= 0 ||
         ((reinterpret_cast<uintptr_t>(At) | reinterpret_cast<uintptr_t>(p)) & 15))
         return hipErrorInvalidValue;
-    const int64_t per = (2 * count + grid - 1) / grid;  // units per block
+    const int64_t per = sym_units_per_block(2 * count, grid);
     auto fn = env_int("CGX_SYM_NT", 1) ? k_symv_f64<1> : k_symv_f64<0>;
     hipLaunchKernelGGL(fn, dim3(grid), dim3(kSymNT), 0, s, At, lda / kSymT, q_base, count, per, tile_runs ? 1 : 0, p,
                        prow, pcol, gate);
