@@ -238,10 +238,13 @@ __device__ __forceinline__ void poisson_p_step(const double *__restrict__ rh, co
 // below (whose first two rows are its last two) are fetched through the same
 // L2 at about the same time.  Without bands those neighbours are taken by
 // blocks of other XCDs.  The v-th item of this block within its band, or -1.
+// bands = 1 + rot: band x walks its items starting rot * x items in (mod its
+// count), so the eight XCDs' streams (bands 64 MiB apart at m = 8192) sit at
+// different offsets (CGX_POISSON_BAND_ROT; an experiment, as for k_symv_f64).
 struct Band {
-    int64_t first, count, stride, start;
+    int64_t first, count, stride, start, rot;
 };
-__device__ __forceinline__ Band band_of(int64_t w0, int64_t nitems, int64_t nstrips) {
+__device__ __forceinline__ Band band_of(int64_t w0, int64_t nitems, int64_t nstrips, int bands) {
     Band b;
     const int64_t nruns = nitems / nstrips, x = blockIdx.x % 8;
     const int64_t r0 = nruns * x / 8, r1 = nruns * (x + 1) / 8;
@@ -249,7 +252,12 @@ __device__ __forceinline__ Band band_of(int64_t w0, int64_t nitems, int64_t nstr
     b.count = (r1 - r0) * nstrips;
     b.stride = gridDim.x / 8;
     b.start = blockIdx.x / 8;
+    b.rot = b.count > 0 ? (int64_t)(bands - 1) * x % b.count : 0;
     return b;
+}
+__device__ __forceinline__ int64_t band_item(const Band &b, int64_t v) {
+    const int64_t q = v + b.rot;
+    return b.first + (q >= b.count ? q - b.count : q);
 }
 
 // Work items [w0, w0+cnt1) then [w2, w2+cnt2) (the whole slab, or, when
@@ -265,10 +273,10 @@ __device__ __forceinline__ double poisson_p_body(const double *__restrict__ rh, 
                                                  int64_t rpi, ItemRanges ir, double beta, double *edge, int bands) {
     double acc = 0.0;
     int par = 0;
-    const Band bd = bands ? band_of(ir.w0, ir.cnt1, nstrips) : Band{0, 0, 0, 0};
+    const Band bd = bands ? band_of(ir.w0, ir.cnt1, nstrips, bands) : Band{0, 0, 0, 0, 0};
     const int64_t vend = bands ? bd.count : ir.cnt1 + ir.cnt2;
     for (int64_t v = bands ? bd.start : blockIdx.x; v < vend; v += bands ? bd.stride : gridDim.x) {
-        const int64_t w = bands ? bd.first + v : v < ir.cnt1 ? ir.w0 + v : ir.w2 + (v - ir.cnt1);
+        const int64_t w = bands ? band_item(bd, v) : v < ir.cnt1 ? ir.w0 + v : ir.w2 + (v - ir.cnt1);
         const StripLane L = strip_lane(w, nstrips, m);
         const int64_t i0 = (w / nstrips) * rpi;
         const int64_t i1 = (i0 + rpi < mloc) ? i0 + rpi : mloc;
@@ -402,12 +410,13 @@ __global__ __launch_bounds__(kNT) void k_poisson_xr_f64(const double *__restrict
     const double alpha_prev = XM == 2 ? *xalpha : 0.0;
     double acc = 0.0;
     int par = 0;
-    const Band bd = bands ? band_of(0, nitems, nstrips) : Band{0, nitems, (int64_t)gridDim.x, (int64_t)blockIdx.x};
+    const Band bd = bands ? band_of(0, nitems, nstrips, bands)
+                          : Band{0, nitems, (int64_t)gridDim.x, (int64_t)blockIdx.x, 0};
     for (int64_t v = bd.start; v < bd.count; v += bd.stride) {
         // reverse: walk the slab (each band) from its end, where the previous
         // kernel (k_poisson_p, forward) last wrote p_k, so the first bytes read
         // may still sit in the 256 MB MALL
-        const int64_t w = bd.first + (reverse ? bd.count - 1 - v : v);
+        const int64_t w = band_item(bd, reverse ? bd.count - 1 - v : v);
         const StripLane L = strip_lane(w, nstrips, m);
         const int64_t i0 = (w / nstrips) * rpi;
         const int64_t i1 = (i0 + rpi < mloc) ? i0 + rpi : mloc;
@@ -497,7 +506,7 @@ hipError_t stencil5_f64(const double *ph, int64_t mloc, int64_t m, double *Ap, d
 // short items keep the rows in flight in a narrow band (64- and 128-row items
 // are 7-20 % slower).
 struct PoissonPlan {
-    int rb, nt, ht, bands;
+    int rb, nt, ht, bands, band_rot;
     int64_t nstrips, rpi, nitems, grid;
 };
 static PoissonPlan poisson_plan(int64_t mloc, int64_t m) {
@@ -508,6 +517,7 @@ static PoissonPlan poisson_plan(int64_t mloc, int64_t m) {
     // XCD bands: 1341 vs 1288 it/s at m = 8192, two interleaved rounds
     // (profiles/r03_poisson_bands_ab.jsonl); CGX_POISSON_BANDS=0 turns them off
     p.bands = env_int("CGX_POISSON_BANDS", 1);
+    p.band_rot = std::max(0, env_int("CGX_POISSON_BAND_ROT", 0));
     p.nstrips = (m + 2 * kNT - 1) / (2 * kNT);
     p.rpi = std::max(1, env_int("CGX_STENCIL_ROWS", 8));
     p.nitems = p.nstrips * ((mloc + p.rpi - 1) / p.rpi);
@@ -546,7 +556,7 @@ static void launch_poisson_p(const PoissonPlan &pl, hipStream_t s, const double 
     auto fn = pl.nt ? (pl.ht ? k_poisson_p_f64<RB, true, true> : k_poisson_p_f64<RB, true, false>)
                     : k_poisson_p_f64<RB, false, false>;
     int64_t grid = resident_grid(reinterpret_cast<const void *>(fn), ir.cnt1 + ir.cnt2);
-    const int bands = pl.bands && ir.cnt2 == 0 && ir.cnt1 % pl.nstrips == 0 && grid >= 8;
+    const int bands = pl.bands && ir.cnt2 == 0 && ir.cnt1 % pl.nstrips == 0 && grid >= 8 ? 1 + pl.band_rot : 0;
     if (bands) grid &= ~int64_t(7);
     hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(kNT), 0, s, rh, poh, pnh, mloc, m, pl.nstrips, pl.rpi, ir, rr,
                        rsold, first, cv, pap_out, add_to_out, ws.partials, ws.tickets + T_MATVEC, bands);
@@ -580,7 +590,7 @@ static void launch_poisson_xr(const PoissonPlan &pl, hipStream_t s, const double
     const XrFn fn = xr_fn_rb<XM>(pl, rb);
     const XrFn fg = env_int("CGX_XR_OWN_GRID", 0) ? fn : xr_fn_rb<1>(pl, pl.rb);
     int64_t grid = resident_grid(reinterpret_cast<const void *>(fg), pl.nitems);
-    const int bands = pl.bands && grid >= 8;
+    const int bands = pl.bands && grid >= 8 ? 1 + pl.band_rot : 0;
     if (bands) grid &= ~int64_t(7);
     hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(kNT), 0, s, pnh, poh, x, r, mloc, m, pl.nstrips, pl.rpi,
                        pl.nitems, env_int("CGX_STENCIL_REVERSE", 1), rsold, pAp, rr_out, xalpha, ws.partials,
