@@ -374,7 +374,8 @@ def main(argv=None) -> int:
     nloc = solver.info.nrows
     overlap_on = bool(solver.info.flags & cg.CGX_OVERLAP_ACTIVE)
     fused = bool(solver.info.flags & cg.CGX_FUSED_ACTIVE)
-    xdefer = bool(solver.info.flags & cg.CGX_XDEFER_ACTIVE)  # fused Poisson: x every other iteration
+    # fused Poisson: x every other (or third) iteration
+    xperiod = (3 if solver.info.flags & cg.CGX_XDEFER3_ACTIVE else 2) if solver.info.flags & cg.CGX_XDEFER_ACTIVE else 1
     plan = None if (poisson or symmetric) else solver.matvec_plan()
 
     if poisson:
@@ -436,9 +437,11 @@ def main(argv=None) -> int:
     # halo rows, x and r; writes x and r); unfused: the stencil (p -> Ap).
     # dense: SURVEY.md s8(d)
     # With x updated every other iteration the xr launches alternate between
-    # 24 B/point (p_k, r -> r) and 48 (p_{k-1}, p_k, x, r -> x, r): 36 on average.
+    # 24 B/point (p_k, r -> r) and 48 (p_{k-1}, p_k, x, r -> x, r): 36 on average;
+    # every third: 24, 24, 56 (p_{k-2} too): 34.67.
+    xr_bpp = {1: 40.0, 2: 36.0, 3: 104.0 / 3}[xperiod]
     if poisson:
-        bytes_launch = ((36 if xdefer else 40) * nloc + 16 * m) if fused else (16 * nloc + 16 * m)
+        bytes_launch = (xr_bpp * nloc + 16 * m) if fused else (16 * nloc + 16 * m)
     elif symmetric:  # the stored tiles + p + y (the per-tile partials are extra traffic, not algorithmic)
         lda = (n + 127) // 128 * 128
         bytes_launch = 8 * (lda // 128) * (lda // 128 + 1) // 2 * 128 * 128 + 8 * n + 8 * n
@@ -531,9 +534,9 @@ def main(argv=None) -> int:
         },
         "check": {"relres": rnorm / bnorm},
         # algorithmic bytes of a whole iteration: 64 B/point fused (r, p_{k-1} -> p_k;
-        # p_k, x, r -> x, r), 60 with x updated every other iteration, 80 B/point
-        # for the stencil / r / x,p split
-        "iteration_gbps": (((60.0 if xdefer else 64.0) if fused else 80.0) * n / (elapsed / args.steps) / 1e9)
+        # p_k, x, r -> x, r), 60 with x updated every other iteration (58.67 every
+        # third), 80 B/point for the stencil / r / x,p split
+        "iteration_gbps": (((24.0 + xr_bpp) if fused else 80.0) * n / (elapsed / args.steps) / 1e9)
         if poisson else None,
     }
     if all_ph is not None:

@@ -32,7 +32,7 @@ import numpy as np
 
 __all__ = [
     "CGX_F64", "CGX_F32_REF", "CGX_TIMING", "CGX_HOST_STREAM", "CGX_NO_OVERLAP", "CGX_COMM_P2P", "CGX_SYMMETRIC",
-    "CGX_PHASES", "CGX_PEER_ACTIVE", "CGX_SMALL_ACTIVE", "CGX_FOLD_ACTIVE", "CGX_XDEFER_ACTIVE", "PHASE_NAMES", "CgxError", "Stats",
+    "CGX_PHASES", "CGX_PEER_ACTIVE", "CGX_SMALL_ACTIVE", "CGX_FOLD_ACTIVE", "CGX_XDEFER_ACTIVE", "CGX_XDEFER3_ACTIVE", "PHASE_NAMES", "CgxError", "Stats",
     "Solver", "lib", "build",
     "device_pci_bus_id", "device_link",
     "conjugrad", "matVec", "vecVec", "residual", "update_xr", "update_p", "read_text",
@@ -54,6 +54,7 @@ CGX_PEER_ACTIVE = 0x20000
 CGX_SMALL_ACTIVE = 0x40000
 CGX_FOLD_ACTIVE = 0x80000
 CGX_XDEFER_ACTIVE = 0x100000
+CGX_XDEFER3_ACTIVE = 0x200000
 
 # cgx_phase_times indices (include/cgx.h), in the order the phases tile an iteration
 PHASE_NAMES = ("matvec_own", "gather_exposed", "matvec", "combine_pap", "update_r", "combine_rr", "update_xp",

@@ -143,12 +143,12 @@ bool rccl_load();
 
 namespace cgxh {
 
-constexpr int kScalSlots = 136;  // 16 ring slots, up to 112 gathered partials, 4 aux
+constexpr int kScalSlots = 138;  // 16 ring slots, up to 112 gathered partials, 10 aux
 constexpr int kMaxShards = 32;
 constexpr int S_RR = 0, S_PAP = 4, S_LRR = 8, S_LPAP = 12, S_GATHER = 16;
 constexpr int S_TR = 128, S_TB = 129, S_LTR = 130, S_LTB = 131;  // true-residual check
 constexpr int S_XNZ = 134;  // rank mode: count of ranks whose x0 is not all zeros
-constexpr int S_XALPHA = 135;  // fused Poisson, x every other iteration: the alpha of the x update left out
+constexpr int S_XALPHA = 135;  // fused Poisson, x every D-th iteration: the alphas of the x updates left out (135, 136)
 constexpr int S_KDONE = 132, S_RRFINAL = 133;  // device-side convergence: k+1 at the break, r.r there
 constexpr int kLookRing = 8;                    // pinned slots for the host's lagged convergence checks
 inline int ring(int64_t j) { return (int)(j & 3); }
@@ -180,6 +180,7 @@ struct Shard {
     // fused Poisson iteration: r with halo rows (r = rh + one row) and a
     // second p slab; p_k lives in pfull for even k, in p2 for odd k
     char *rh = nullptr, *p2 = nullptr;
+    char *p3 = nullptr;  // fused Poisson, x every third iteration: p_k in {pfull, p2, p3}[k % 3]
     char *p_alt = nullptr;  // the folded two-launch iteration: p_k for odd k (pfull holds even k)
     bool x_zero = true;  // x is known to be all zeros (x0 = 0: the first A x is skipped)
     RedWs ws{nullptr, nullptr};
@@ -267,6 +268,7 @@ struct cgx_ctx {
     // iterations k0, k0+2, ... leave x out and k0+1, k0+3, ... catch up; a call
     // that ends after a left-out update finishes x (poisson_x_finish).
     bool xdefer = false;
+    int xd = 1;  // the period: 2 (default) or 3 (CGX_POISSON_XDEFER=3, a third p slab)
     int64_t xd_k0 = 0;
     // rank mode fail-fast (cgx_exchange.hip, rank_wait_*): every host wait
     // polls with a deadline of rccl_timeout_s seconds (CGX_RCCL_TIMEOUT_S,

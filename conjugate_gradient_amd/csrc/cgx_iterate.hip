@@ -244,6 +244,15 @@ int read_scalar(cgx_ctx *c, int gslot, double *out) {
 // alpha is kept in S_XALPHA and p_k stays in its slab until the next
 // iteration's xr kernel has read it); poisson_x_finish completes it at the end
 // of a cgx_iterate call.
+// Where p_k lives: two slabs alternate (pfull for even k), three rotate with x every third iteration.
+static char *poisson_slab(const cgx_ctx *c, const Shard &s, int64_t k) {
+    if (c->xd == 3) {
+        const int64_t q = ((k % 3) + 3) % 3;
+        return q == 0 ? s.pfull : q == 1 ? s.p2 : s.p3;
+    }
+    return (k & 1) ? s.p2 : s.pfull;
+}
+
 int do_iteration_poisson(cgx_ctx *c, double eps, int *stop, bool gated) {
     const int64_t k = c->k;
     *stop = 0;
@@ -252,11 +261,14 @@ int do_iteration_poisson(cgx_ctx *c, double eps, int *stop, bool gated) {
     const int rk = S_RR + ring(k), rkm1 = S_RR + ring(k + 3);  // r.r of iterations k, k-1
     auto D = [](void *p) { return reinterpret_cast<double *>(p); };
     const bool split = c->halo_pending;  // interior runs while the r halo exchange is in flight
-    // x every other iteration: leave it out at k0, k0+2, ..., catch up at k0+1, ...
-    const int xmode = !c->xdefer ? 1 : ((k - c->xd_k0) & 1) ? 2 : 0;
+    // x every D-th iteration (D = c->xd): leave it out at the first D-1 of every
+    // D iterations from k0 (alpha_k to slot S_XALPHA + j), catch up at the D-th
+    const int64_t jx = (k - c->xd_k0) % c->xd;
+    const int xmode = c->xd == 1 ? 1 : jx == c->xd - 1 ? c->xd : 0;
+    const int xslot = S_XALPHA + (xmode == 0 ? (int)jx : 0);
     for (auto &s : c->sh) {
         TRY(set_dev(s));
-        char *pold = (k & 1) ? s.pfull : s.p2, *pnew = (k & 1) ? s.p2 : s.pfull;
+        char *pold = poisson_slab(c, s, k - 1), *pnew = poisson_slab(c, s, k);
         for (int part : split ? std::initializer_list<int>{1, 2} : std::initializer_list<int>{0}) {
             if (part == 2) HIPT(hipStreamWaitEvent(s.stream, s.ev_gathered, 0));
             HIPT(poisson_p_f64(D(s.rh), D(pold), D(pnew), s.nloc / m, m, D(slot(s, rk)), D(slot(s, rkm1)), k == 0,
@@ -274,9 +286,10 @@ int do_iteration_poisson(cgx_ctx *c, double eps, int *stop, bool gated) {
         const bool timing = (c->flags & CGX_TIMING) && (&s == &c->sh[0]);
         if (timing && s.ev_used >= kEvPairs) TRY(timing_resolve(c));
         if (timing) HIPT(hipEventRecord(s.ev_t[2 * s.ev_used], s.stream));
-        char *pnew = (k & 1) ? s.p2 : s.pfull, *pold = (k & 1) ? s.pfull : s.p2;
-        HIPT(poisson_xr_f64(D(pnew), D(pold), D(s.x), D(s.r), s.nloc / m, m, D(slot(s, rk)), D(slot(s, pg)),
-                            D(slot(s, ro)), xmode, D(slot(s, S_XALPHA)), s.ws, s.stream, gate_of(s, gated)));
+        char *pnew = poisson_slab(c, s, k), *pold = poisson_slab(c, s, k - 1),
+             *pq = c->xd == 3 ? poisson_slab(c, s, k - 2) : nullptr;
+        HIPT(poisson_xr_f64(D(pnew), D(pold), D(pq), D(s.x), D(s.r), s.nloc / m, m, D(slot(s, rk)), D(slot(s, pg)),
+                            D(slot(s, ro)), xmode, D(slot(s, xslot)), s.ws, s.stream, gate_of(s, gated)));
         if (timing) {
             HIPT(hipEventRecord(s.ev_t[2 * s.ev_used + 1], s.stream));
             s.ev_used++;
@@ -304,15 +317,16 @@ int do_iteration_poisson(cgx_ctx *c, double eps, int *stop, bool gated) {
 // Gated solves enqueue iterations past the stop that skip themselves, so this
 // is decided from c->k, never from what was enqueued.
 int poisson_x_finish(cgx_ctx *c) {
-    if (!c->fused || !c->xdefer) return CGX_OK;
+    if (!c->fused || c->xd == 1) return CGX_OK;
     const int64_t last = c->k - 1;
-    if (last >= c->xd_k0 && ((last - c->xd_k0) & 1) == 0) {
+    const int64_t jx = last >= c->xd_k0 ? (last - c->xd_k0) % c->xd : c->xd - 1;
+    if (jx != c->xd - 1) {  // jx + 1 updates left out: iterations last - jx .. last
         for (auto &s : c->sh) {
             TRY(set_dev(s));
-            char *pk = (last & 1) ? s.p2 : s.pfull;
-            HIPT(poisson_xflush_f64(reinterpret_cast<const double *>(pk), reinterpret_cast<double *>(s.x),
-                                    s.nloc / c->m, c->m, reinterpret_cast<const double *>(slot(s, S_XALPHA)),
-                                    s.stream));
+            char *pa = poisson_slab(c, s, last - jx), *pb = jx == 1 ? poisson_slab(c, s, last) : nullptr;
+            HIPT(poisson_xflush_f64(reinterpret_cast<const double *>(pa), reinterpret_cast<const double *>(pb),
+                                    reinterpret_cast<double *>(s.x), s.nloc / c->m, c->m,
+                                    reinterpret_cast<const double *>(slot(s, S_XALPHA)), s.stream));
         }
     }
     c->xd_k0 = c->k;

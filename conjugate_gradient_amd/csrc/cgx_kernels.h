@@ -124,14 +124,16 @@ hipError_t poisson_p_f64(const double *rh, const double *poh, double *pnh, int64
                          double eps = -1.0, int64_t k = 0, int64_t *kdone = nullptr, double *rrfinal = nullptr,
                          int part = 0, int64_t *hrec = nullptr);  // part: 0 all rows; 1 interior runs; 2 the two edge runs (+= part 1's p.Ap)
 // xmode: 1 x += alpha p_k; 0 x untouched, alpha_k to *xalpha; 2 x += alpha_{k-1}
-// p_{k-1} (poh, *xalpha) then += alpha_k p_k (x updated every other iteration).
-hipError_t poisson_xr_f64(const double *pnh, const double *poh, double *x, double *r, int64_t mloc, int64_t m,
-                          const double *rsold, const double *pAp, double *rr_out, int xmode, double *xalpha,
-                          const RedWs &ws, hipStream_t s, const int64_t *gate = nullptr);
-// x += (*xalpha) p over the slab interior (pnh with halo rows): the x update an
-// xmode-0 iteration left out.
-hipError_t poisson_xflush_f64(const double *pnh, double *x, int64_t mloc, int64_t m, const double *xalpha,
-                              hipStream_t s);
+// p_{k-1} (poh, xalpha[0]) then += alpha_k p_k (x every other iteration);
+// 3 x += alpha_{k-2} p_{k-2} (pqh, xalpha[0]), alpha_{k-1} p_{k-1} (poh,
+// xalpha[1]), alpha_k p_k (x every third iteration).
+hipError_t poisson_xr_f64(const double *pnh, const double *poh, const double *pqh, double *x, double *r,
+                          int64_t mloc, int64_t m, const double *rsold, const double *pAp, double *rr_out, int xmode,
+                          double *xalpha, const RedWs &ws, hipStream_t s, const int64_t *gate = nullptr);
+// x += xalpha[0] p (pnh) [then += xalpha[1] p (pbh) when pbh != nullptr] over the
+// slab interior: the x updates the last iterations left out.
+hipError_t poisson_xflush_f64(const double *pnh, const double *pbh, double *x, int64_t mloc, int64_t m,
+                              const double *xalpha, hipStream_t s);
 hipError_t fill_f64(double *p, int64_t n, double v, hipStream_t s);
 hipError_t fill_f32(float *p, int64_t n, float v, hipStream_t s);
 

@@ -333,18 +333,20 @@ __global__ __launch_bounds__(kNT) void k_poisson_p_f64(const double *__restrict_
 // point per iteration over a pair of iterations.
 template <int RBn, bool NT, bool HT, int XM>
 __device__ __forceinline__ void poisson_xr_step(const double *__restrict__ pnh, const double *__restrict__ poh,
-                                                double *__restrict__ x, double *__restrict__ r, int64_t m, int64_t i,
-                                                const StripLane &L, double alpha, double alpha_prev, d2 &pm, d2 &pc,
+                                                const double *__restrict__ pqh, double *__restrict__ x,
+                                                double *__restrict__ r, int64_t m, int64_t i, const StripLane &L,
+                                                double alpha, double alpha_prev, double alpha_prev2, d2 &pm, d2 &pc,
                                                 double &acc, double *eb) {
     const int lane = threadIdx.x & 63;
-    d2 pr[RBn], xv[RBn], rv[RBn], ce[RBn], po[RBn];
+    d2 pr[RBn], xv[RBn], rv[RBn], ce[RBn], po[RBn], pq[RBn];
     double el[RBn], er[RBn];
 #pragma unroll
     for (int t = 0; t < RBn; ++t) {
         const int64_t hc = (i + t + 1) * m, ic = (i + t) * m;
         pr[t] = keep(L.valid, (HT && t >= RBn - 2) ? lds2<false>(pnh + hc + m, L.off) : lds2<NT>(pnh + hc + m, L.off));
         if constexpr (XM != 0) xv[t] = lds2<NT>(x + ic, L.off);
-        if constexpr (XM == 2) po[t] = lds2<NT>(poh + hc, L.off);
+        if constexpr (XM >= 2) po[t] = lds2<NT>(poh + hc, L.off);
+        if constexpr (XM == 3) pq[t] = lds2<NT>(pqh + hc, L.off);
         rv[t] = lds2<NT>(r + ic, L.off);
         el[t] = L.has_l ? pnh[hc + L.jw - 1] : 0.0;
         er[t] = L.has_r ? pnh[hc + L.jw + 128] : 0.0;
@@ -366,7 +368,14 @@ __device__ __forceinline__ void poisson_xr_step(const double *__restrict__ pnh, 
         o.x = 4.0 * ce[t].x - up.x - dn.x - l - ce[t].y;
         o.y = 4.0 * ce[t].y - up.y - dn.y - ce[t].x - rt;
         d2 xn, rn;
-        if constexpr (XM == 2) {
+        if constexpr (XM == 3) {  // alpha_{k-2} p_{k-2}, alpha_{k-1} p_{k-1}, alpha_k p_k: their order
+            xn.x = __builtin_fma(alpha_prev2, pq[t].x, xv[t].x);
+            xn.y = __builtin_fma(alpha_prev2, pq[t].y, xv[t].y);
+            xn.x = __builtin_fma(alpha_prev, po[t].x, xn.x);
+            xn.y = __builtin_fma(alpha_prev, po[t].y, xn.y);
+            xn.x = __builtin_fma(alpha, ce[t].x, xn.x);
+            xn.y = __builtin_fma(alpha, ce[t].y, xn.y);
+        } else if constexpr (XM == 2) {
             xn.x = __builtin_fma(alpha_prev, po[t].x, xv[t].x);
             xn.y = __builtin_fma(alpha_prev, po[t].y, xv[t].y);
             xn.x = __builtin_fma(alpha, ce[t].x, xn.x);
@@ -398,7 +407,8 @@ __device__ __forceinline__ void poisson_xr_step(const double *__restrict__ pnh, 
 // deferral.
 template <int RB, bool NT, bool HT, int XM>
 __global__ __launch_bounds__(kNT) void k_poisson_xr_f64(const double *__restrict__ pnh, const double *__restrict__ poh,
-                                                        double *__restrict__ x, double *__restrict__ r, int64_t mloc,
+                                                        const double *__restrict__ pqh, double *__restrict__ x,
+                                                        double *__restrict__ r, int64_t mloc,
                                                         int64_t m, int64_t nstrips, int64_t rpi, int64_t nitems,
                                                         int reverse, const double *rsold, const double *pAp,
                                                         double *rr_out, double *xalpha, double *partials,
@@ -407,7 +417,9 @@ __global__ __launch_bounds__(kNT) void k_poisson_xr_f64(const double *__restrict
     __shared__ double edge[2 * kWaves * 2 * kEdgeRB];
     if (gate && *gate) return;
     const double alpha = cg_ratio(*rsold, *pAp);
-    const double alpha_prev = XM == 2 ? *xalpha : 0.0;
+    // XM = 2: alpha_{k-1} = xalpha[0]; XM = 3: alpha_{k-2} = xalpha[0], alpha_{k-1} = xalpha[1]
+    const double alpha_prev = XM == 2 ? xalpha[0] : XM == 3 ? xalpha[1] : 0.0;
+    const double alpha_prev2 = XM == 3 ? xalpha[0] : 0.0;
     double acc = 0.0;
     int par = 0;
     const Band bd = bands ? band_of(0, nitems, nstrips, bands)
@@ -424,10 +436,10 @@ __global__ __launch_bounds__(kNT) void k_poisson_xr_f64(const double *__restrict
         d2 pc = keep(L.valid, lds2<NT && !HT>(pnh + (i0 + 1) * m, L.off));
         int64_t i = i0;
         for (; i + RB <= i1; i += RB, par ^= 1)
-            poisson_xr_step<RB, NT, HT, XM>(pnh, poh, x, r, m, i, L, alpha, alpha_prev, pm, pc, acc,
+            poisson_xr_step<RB, NT, HT, XM>(pnh, poh, pqh, x, r, m, i, L, alpha, alpha_prev, alpha_prev2, pm, pc, acc,
                                             edge + par * (kWaves * 2 * kEdgeRB));
         for (; i < i1; ++i, par ^= 1)
-            poisson_xr_step<1, NT, HT, XM>(pnh, poh, x, r, m, i, L, alpha, alpha_prev, pm, pc, acc,
+            poisson_xr_step<1, NT, HT, XM>(pnh, poh, pqh, x, r, m, i, L, alpha, alpha_prev, alpha_prev2, pm, pc, acc,
                                            edge + par * (kWaves * 2 * kEdgeRB));
     }
     // XM = 0: alpha_k for the next iteration's (or the flush's) x update.  Read
@@ -440,16 +452,24 @@ __global__ __launch_bounds__(kNT) void k_poisson_xr_f64(const double *__restrict
 // interior (p_k's slab pnh, alpha from *xalpha).  The same FMA as the xr
 // kernel's, so x is bit for bit the every-iteration update's.
 // Even m: npts is even and both slabs 16-B aligned, so it runs on pairs.
-__global__ __launch_bounds__(kNT) void k_poisson_xflush_f64(const double *__restrict__ pnh, double *__restrict__ x,
+// With a second slab pbh (x every third iteration, two updates left out):
+// x += xalpha[0] pnh, then += xalpha[1] pbh, in that order.
+__global__ __launch_bounds__(kNT) void k_poisson_xflush_f64(const double *__restrict__ pnh,
+                                                            const double *__restrict__ pbh, double *__restrict__ x,
                                                             int64_t npts, const double *xalpha) {
-    const double alpha = *xalpha;
-    const d2 *p = reinterpret_cast<const d2 *>(pnh);
+    const double alpha = xalpha[0], alpha_b = pbh ? xalpha[1] : 0.0;
+    const d2 *p = reinterpret_cast<const d2 *>(pnh), *pb = reinterpret_cast<const d2 *>(pbh);
     d2 *xv = reinterpret_cast<d2 *>(x);
     for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < npts / 2; i += (int64_t)gridDim.x * kNT) {
         const d2 pv = __builtin_nontemporal_load(p + i), xo = __builtin_nontemporal_load(xv + i);
         d2 o;
         o.x = __builtin_fma(alpha, pv.x, xo.x);
         o.y = __builtin_fma(alpha, pv.y, xo.y);
+        if (pbh) {
+            const d2 qv = __builtin_nontemporal_load(pb + i);
+            o.x = __builtin_fma(alpha_b, qv.x, o.x);
+            o.y = __builtin_fma(alpha_b, qv.y, o.y);
+        }
         __builtin_nontemporal_store(o, xv + i);
     }
 }
@@ -561,9 +581,9 @@ static void launch_poisson_p(const PoissonPlan &pl, hipStream_t s, const double 
     hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(kNT), 0, s, rh, poh, pnh, mloc, m, pl.nstrips, pl.rpi, ir, rr,
                        rsold, first, cv, pap_out, add_to_out, ws.partials, ws.tickets + T_MATVEC, bands);
 }
-using XrFn = void (*)(const double *, const double *, double *, double *, int64_t, int64_t, int64_t, int64_t, int64_t,
-                     int, const double *, const double *, double *, double *, double *, unsigned *, const int64_t *,
-                     int);
+using XrFn = void (*)(const double *, const double *, const double *, double *, double *, int64_t, int64_t, int64_t,
+                     int64_t, int64_t, int, const double *, const double *, double *, double *, double *, unsigned *,
+                     const int64_t *, int);
 template <int RB, int XM>
 static XrFn xr_fn(const PoissonPlan &pl) {
     return pl.nt ? (pl.ht ? k_poisson_xr_f64<RB, true, true, XM> : k_poisson_xr_f64<RB, true, false, XM>)
@@ -583,16 +603,20 @@ static XrFn xr_fn_rb(const PoissonPlan &pl, int rb) {
 // variant runs.  XM = 2 steps RB / 2 rows at a time (RB = 8: 193 VGPRs, 2
 // waves per SIMD, fewer than that grid; held to 3 waves it spilled).
 template <int XM>
-static void launch_poisson_xr(const PoissonPlan &pl, hipStream_t s, const double *pnh, const double *poh, double *x,
-                              double *r, int64_t mloc, int64_t m, const double *rsold, const double *pAp,
-                              double *rr_out, double *xalpha, const RedWs &ws, const int64_t *gate) {
-    const int rb = XM == 2 && pl.rb > 1 && !env_int("CGX_XR2_FULL_RB", 0) ? pl.rb / 2 : pl.rb;
+static void launch_poisson_xr(const PoissonPlan &pl, hipStream_t s, const double *pnh, const double *poh,
+                              const double *pqh, double *x, double *r, int64_t mloc, int64_t m, const double *rsold,
+                              const double *pAp, double *rr_out, double *xalpha, const RedWs &ws,
+                              const int64_t *gate) {
+    // XM = 2 / 3 carry p_{k-1} (and p_{k-2}): RB / 2 rows per step (XM = 3 at RB = 8:
+    // 130 VGPRs; CGX_XR3_QUARTER=1: RB / 4, 82)
+    const int rb = XM == 3 && env_int("CGX_XR3_QUARTER", 0) ? std::max(1, pl.rb / 4)
+                   : XM >= 2 && pl.rb > 1 && !env_int("CGX_XR2_FULL_RB", 0) ? pl.rb / 2 : pl.rb;
     const XrFn fn = xr_fn_rb<XM>(pl, rb);
     const XrFn fg = env_int("CGX_XR_OWN_GRID", 0) ? fn : xr_fn_rb<1>(pl, pl.rb);
     int64_t grid = resident_grid(reinterpret_cast<const void *>(fg), pl.nitems);
     const int bands = pl.bands && grid >= 8 ? 1 + pl.band_rot : 0;
     if (bands) grid &= ~int64_t(7);
-    hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(kNT), 0, s, pnh, poh, x, r, mloc, m, pl.nstrips, pl.rpi,
+    hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(kNT), 0, s, pnh, poh, pqh, x, r, mloc, m, pl.nstrips, pl.rpi,
                        pl.nitems, env_int("CGX_STENCIL_REVERSE", 1), rsold, pAp, rr_out, xalpha, ws.partials,
                        ws.tickets + T_XR, gate, bands);
 }
@@ -629,28 +653,31 @@ hipError_t poisson_p_f64(const double *rh, const double *poh, double *pnh, int64
     return hipGetLastError();
 }
 
-hipError_t poisson_xr_f64(const double *pnh, const double *poh, double *x, double *r, int64_t mloc, int64_t m,
-                          const double *rsold, const double *pAp, double *rr_out, int xmode, double *xalpha,
-                          const RedWs &ws, hipStream_t s, const int64_t *gate) {
+hipError_t poisson_xr_f64(const double *pnh, const double *poh, const double *pqh, double *x, double *r,
+                          int64_t mloc, int64_t m, const double *rsold, const double *pAp, double *rr_out, int xmode,
+                          double *xalpha, const RedWs &ws, hipStream_t s, const int64_t *gate) {
     if (!poisson_fusable(mloc, m) || !al16(pnh) || !al16(x) || !al16(r)) return hipErrorInvalidValue;
-    if ((xmode != 1 && !xalpha) || (xmode == 2 && !al16(poh)) || xmode < 0 || xmode > 2) return hipErrorInvalidValue;
+    if (xmode < 0 || xmode > 3 || (xmode != 1 && !xalpha) || (xmode >= 2 && !al16(poh)) ||
+        (xmode == 3 && !al16(pqh)))
+        return hipErrorInvalidValue;
     const PoissonPlan pl = poisson_plan(mloc, m);
-    if (xmode == 0)
-        launch_poisson_xr<0>(pl, s, pnh, poh, x, r, mloc, m, rsold, pAp, rr_out, xalpha, ws, gate);
-    else if (xmode == 2)
-        launch_poisson_xr<2>(pl, s, pnh, poh, x, r, mloc, m, rsold, pAp, rr_out, xalpha, ws, gate);
-    else
-        launch_poisson_xr<1>(pl, s, pnh, poh, x, r, mloc, m, rsold, pAp, rr_out, xalpha, ws, gate);
+    switch (xmode) {
+        case 0: launch_poisson_xr<0>(pl, s, pnh, poh, pqh, x, r, mloc, m, rsold, pAp, rr_out, xalpha, ws, gate); break;
+        case 2: launch_poisson_xr<2>(pl, s, pnh, poh, pqh, x, r, mloc, m, rsold, pAp, rr_out, xalpha, ws, gate); break;
+        case 3: launch_poisson_xr<3>(pl, s, pnh, poh, pqh, x, r, mloc, m, rsold, pAp, rr_out, xalpha, ws, gate); break;
+        default: launch_poisson_xr<1>(pl, s, pnh, poh, pqh, x, r, mloc, m, rsold, pAp, rr_out, xalpha, ws, gate); break;
+    }
     return hipGetLastError();
 }
 
-hipError_t poisson_xflush_f64(const double *pnh, double *x, int64_t mloc, int64_t m, const double *xalpha,
-                              hipStream_t s) {
+hipError_t poisson_xflush_f64(const double *pnh, const double *pbh, double *x, int64_t mloc, int64_t m,
+                              const double *xalpha, hipStream_t s) {
     const int64_t npts = mloc * m;
     if (npts <= 0) return hipSuccess;
-    if (!poisson_fusable(mloc, m) || !al16(pnh) || !al16(x)) return hipErrorInvalidValue;
+    if (!poisson_fusable(mloc, m) || !al16(pnh) || !al16(x) || (pbh && !al16(pbh))) return hipErrorInvalidValue;
     const unsigned grid = (unsigned)std::min<int64_t>((npts / 2 + kNT - 1) / kNT, 8192);
-    hipLaunchKernelGGL(k_poisson_xflush_f64, dim3(grid), dim3(kNT), 0, s, pnh + m, x, npts, xalpha);
+    hipLaunchKernelGGL(k_poisson_xflush_f64, dim3(grid), dim3(kNT), 0, s, pnh + m, pbh ? pbh + m : nullptr, x, npts,
+                       xalpha);
     return hipGetLastError();
 }
 

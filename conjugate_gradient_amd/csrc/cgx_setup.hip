@@ -116,6 +116,10 @@ int alloc_shard(cgx_ctx *c, Shard &s) {
         s.r = s.rh + c->m * es;
         TRY(dmalloc(&s.p2, (s.nloc + 2 * c->m) * es));
         HIPT(hipMemsetAsync(s.p2, 0, (s.nloc + 2 * c->m) * es, s.stream));
+        if (c->xd == 3) {
+            TRY(dmalloc(&s.p3, (s.nloc + 2 * c->m) * es));
+            HIPT(hipMemsetAsync(s.p3, 0, (s.nloc + 2 * c->m) * es, s.stream));
+        }
     } else if (c->fold_p) {  // the folded matVec reads r over all lda columns: zero past n
         TRY(dmalloc(&s.r, c->lda * es));
         HIPT(hipMemsetAsync(s.r, 0, c->lda * es, s.stream));
@@ -214,7 +218,7 @@ void free_shard(Shard &s) {
     (void)hipSetDevice(s.dev);
     if (s.stream) (void)hipStreamSynchronize(s.stream);
     if (s.comm) ncclCommDestroy(s.comm);
-    for (char *p : {s.A, s.b, s.x, s.rh ? s.rh : s.r, s.p2, s.Ap, s.pfull, s.p_alt, s.xfull, s.scal, s.sym_prow,
+    for (char *p : {s.A, s.b, s.x, s.rh ? s.rh : s.r, s.p2, s.p3, s.Ap, s.pfull, s.p_alt, s.xfull, s.scal, s.sym_prow,
                     s.sym_pcol, s.sym_stage})
         if (p) (void)hipFree(p);
     if (s.ws.partials) (void)hipFree(s.ws.partials);
@@ -367,6 +371,10 @@ int finish_create(cgx_ctx *c, cgx_ctx **out) {
                           !(c->mode == M_RCCL && c->nranks == 1 && !force);
         const char *xd = std::getenv("CGX_POISSON_XDEFER");
         c->xdefer = c->fused && !(xd && *xd == '0');
+        // x every third iteration by default (1478-1479 vs 1447-1457 it/s every
+        // other, 1330-1344 every iteration at m = 8192, interleaved:
+        // profiles/r03_poisson_xdefer3_ab.jsonl); CGX_POISSON_XDEFER=2: every other
+        c->xd = !c->xdefer ? 1 : (xd && *xd == '2') ? 2 : 3;
     }
     for (auto &s : c->sh) {
         int rc = alloc_shard(c, s);
@@ -659,7 +667,8 @@ int cgx_get_info(const cgx_ctx *c, cgx_info *info) {
     info->flags = c->flags | (c->overlap ? CGX_OVERLAP_ACTIVE : 0) |
                   ((c->fused || c->fused_p || c->ref_fused) ? CGX_FUSED_ACTIVE : 0) | (c->peer ? CGX_PEER_ACTIVE : 0) |
                   (c->sh[0].plan.small ? CGX_SMALL_ACTIVE : 0) | (c->fold_p ? CGX_FOLD_ACTIVE : 0) |
-                  (c->xdefer ? CGX_XDEFER_ACTIVE : 0);
+                  (c->xdefer ? CGX_XDEFER_ACTIVE : 0) |
+                  (c->xd == 3 ? CGX_XDEFER3_ACTIVE : 0);
     info->elem_bytes = c->es;
     return CGX_OK;
 }

@@ -135,11 +135,15 @@ extern "C" {
                                     iteration folds p = r + beta p into the
                                     next matVec (CGX_FOLD_P) */
 #define CGX_XDEFER_ACTIVE 0x100000 /* reported in cgx_info.flags: the fused
-                                    Poisson iteration updates x every other
-                                    iteration (60 instead of 64 B per grid
-                                    point; x the same bits after every
-                                    cgx_iterate call; CGX_POISSON_XDEFER=0:
-                                    every iteration) */
+                                    Poisson iteration updates x only every
+                                    other or every third iteration (60 / 58.7
+                                    instead of 64 B per grid point; x the same
+                                    bits after every cgx_iterate call;
+                                    CGX_POISSON_XDEFER=0: every iteration) */
+#define CGX_XDEFER3_ACTIVE 0x200000 /* reported in cgx_info.flags with
+                                    CGX_XDEFER_ACTIVE: every third iteration
+                                    (the default, a third p slab;
+                                    CGX_POISSON_XDEFER=2: every other) */
 
 typedef struct cgx_ctx cgx_ctx;
 

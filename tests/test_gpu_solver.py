@@ -742,13 +742,14 @@ def _poisson_x_runs(m, shards, xdefer, monkeypatch):
     out = {}
     with cg.Solver(None, poisson_m=m, devices=shards) as s:
         assert s.info.flags & cg.CGX_FUSED_ACTIVE
-        assert bool(s.info.flags & cg.CGX_XDEFER_ACTIVE) == (xdefer == "1")
+        assert bool(s.info.flags & cg.CGX_XDEFER_ACTIVE) == (xdefer != "0")
+        assert bool(s.info.flags & cg.CGX_XDEFER3_ACTIVE) == (xdefer == "3")
         for gated in ("1", "0"):
             monkeypatch.setenv("CGX_GATED", gated)
             s.fill(1.0, 0.0)
             x, st = s.solve(None, eps=1e-10)
             out["solve" + gated] = (x, st.iterations)
-        for count in (1, 2, 7, 8):  # fixed count, odd and even
+        for count in (1, 2, 3, 7, 8, 9):  # fixed count, every residue of 2 and 3
             s.fill(1.0, 0.0)
             s.begin()
             d, _ = s.iterate(count, eps=-1.0)
@@ -762,16 +763,18 @@ def _poisson_x_runs(m, shards, xdefer, monkeypatch):
     return out
 
 
+@pytest.mark.parametrize("period", ["2", "3"])
 @pytest.mark.parametrize("m,shards", [(64, None), (96, [0] * 4), (130, [0, 0]), (1040, None)])
-def test_poisson_x_every_other_iteration_is_bitwise(monkeypatch, m, shards):
-    """k_poisson_xr_f64 updates x every other iteration (the left-out iteration's
-    alpha kept, p_{k-1} read from the other slab; 60 instead of 64 B per point)
-    with the every-iteration update's two FMAs in the same order: x is bit for
-    bit CGX_POISSON_XDEFER=0's after every way a solve can end (gated and
-    host-checked convergence at either parity, fixed counts 1/2/7/8, odd pieces),
-    with the same loop counts."""
+def test_poisson_x_every_other_iteration_is_bitwise(monkeypatch, m, shards, period):
+    """k_poisson_xr_f64 updates x every other (every third: the default) iteration
+    (the left-out iterations' alphas kept, p_{k-1} (and p_{k-2}) read from the
+    other slabs; 60 (58.7) instead of 64 B per point) with the every-iteration
+    update's FMAs in the same order: x is bit for bit CGX_POISSON_XDEFER=0's
+    after every way a solve can end (gated and host-checked convergence at every
+    residue, fixed counts 1/2/3/7/8/9, pieces of 3 and 5), with the same loop
+    counts."""
     monkeypatch.setenv("CGX_POISSON_FUSED", "1")
-    a = _poisson_x_runs(m, shards, "1", monkeypatch)
+    a = _poisson_x_runs(m, shards, period, monkeypatch)  # x every 2nd / 3rd iteration (3: a third p slab)
     b = _poisson_x_runs(m, shards, "0", monkeypatch)
     assert a.keys() == b.keys()
     for key in a:
