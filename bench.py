@@ -17,7 +17,12 @@ work; the true residual ||b - A x|| / ||b|| is checked after the timed region.
 Under torchrun each process drives one GPU (cgx_create_rank): RCCL carries the
 per-iteration exchange inside libcgx; torch.distributed (gloo, CPU) is only the
 control plane (RCCL id broadcast, barriers, max-over-ranks of the timings).
-Run without torchrun, the N=1 case uses a single-GPU context and no torch.
+Run without torchrun, N=1 uses a single-GPU context and no torch; N>1 drives
+devices 0..N-1 from this one process (cgx_create_multi: row blocks on N GPUs,
+p gathered and the scalars combined by pull kernels over peer access), and
+exits non-zero when fewer than N devices are visible -- never a 1-GPU line
+for an N-GPU request.  --devices lists them explicitly (repeats allowed: row
+blocks sharing a GPU, reported as such).
 
 Output: ONE JSON line on rank 0 (see the keys below).  `roofline.achieved`
 is ALGORITHMIC matVec bytes per launch (8*N_loc*N + 8*N + 8*N_loc, SURVEY.md
@@ -300,6 +305,23 @@ def rccl_summary(all_comm: list, solver_device: int) -> dict:
     }
 
 
+def local_summary(devices: list, peer_active: bool) -> dict:
+    """The single-process multi-GPU run (cgx_create_multi): which devices hold
+    the row blocks, their PCI bus ids, and the link / peer access from the
+    first block's device to each other device."""
+    import conjugate_gradient_amd as cg
+    d0 = devices[0]
+    return {
+        "mode": "one process, cgx_create_multi",
+        "devices": devices,
+        "distinct_devices": len(set(devices)),
+        "pci_bus_ids": [cg.device_pci_bus_id(d) for d in devices],
+        "peer_active": peer_active,
+        "links_from_block0": [{"to_block": q, "link": "same device"} if d == d0 else
+                              {"to_block": q, **cg.device_link(d0, d)} for q, d in enumerate(devices) if q],
+    }
+
+
 def main(argv=None) -> int:
     ap = argparse.ArgumentParser(description=__doc__, formatter_class=argparse.RawDescriptionHelpFormatter)
     ap.add_argument("--gpus", type=int, default=1)
@@ -333,6 +355,9 @@ def main(argv=None) -> int:
                          "nothing is inserted between kernels, overhead within run-to-run noise, "
                          "profiles/r03_phases_ab.jsonl) and the line reports per-phase medians per rank; "
                          "auto: on for the dense resident workloads")
+    ap.add_argument("--devices", default=None,
+                    help="without a launcher: the devices of the row blocks, comma-separated (default 0..N-1 for "
+                         "--gpus N); repeats put several row blocks on one GPU")
     ap.add_argument("--no-cpu", action="store_true", help="skip the CPU baseline leg")
     ap.add_argument("--cpu-n", type=int, default=None, help="N for the CPU baseline (default: --n)")
     args = ap.parse_args(argv)
@@ -344,6 +369,22 @@ def main(argv=None) -> int:
         print(f"warning: --gpus {args.gpus} but WORLD_SIZE={world}; using WORLD_SIZE", file=sys.stderr)
 
     import conjugate_gradient_amd as cg
+    # Without a launcher, --gpus N > 1 (or --devices) runs the N row blocks from
+    # this process (cgx_create_multi); world is then the number of row blocks.
+    devices = None
+    if not use_dist and (args.gpus > 1 or args.devices):
+        devices = ([int(v) for v in args.devices.split(",")] if args.devices else list(range(args.gpus)))
+        if args.devices and args.gpus not in (1, len(devices)):
+            raise SystemExit(f"bench.py: --gpus {args.gpus} but --devices lists {len(devices)} row blocks")
+        ndev = cg.device_count()
+        missing = sorted({d for d in devices if not 0 <= d < ndev})
+        if missing:
+            raise SystemExit(f"bench.py: --gpus {len(devices)} asks for device(s) {missing}, but {ndev} "
+                             f"device(s) are visible; run on a node with {len(devices)} GPUs, or under "
+                             f"torch.distributed.run with one process per GPU")
+        world = len(devices)
+    n_gpus = len(set(devices)) if devices else world
+    span = f"{world} GPU(s)" if n_gpus == world else f"{world} row blocks on {n_gpus} GPU(s)"
     stream = args.workload in ("stream", "stream_symmetric")
     poisson = args.workload == "poisson"
     symmetric = args.workload in ("symmetric", "stream_symmetric")
@@ -369,9 +410,11 @@ def main(argv=None) -> int:
         ndev = max(1, cg.device_count())
         solver = cg.Solver(n, rank=rank, nranks=world, unique_id=uid, device=local_rank % ndev, flags=flags,
                            poisson_m=m)
+    elif devices is not None:
+        solver = cg.Solver(n, devices=devices, flags=flags, poisson_m=m)
     else:
         solver = cg.Solver(n, device=0, flags=flags, poisson_m=m)
-    nloc = solver.info.nrows
+    nloc = solver.info.nrows // len(devices or [0])
     overlap_on = bool(solver.info.flags & cg.CGX_OVERLAP_ACTIVE)
     fused = bool(solver.info.flags & cg.CGX_FUSED_ACTIVE)
     # fused Poisson: x every other (or third) iteration
@@ -420,6 +463,7 @@ def main(argv=None) -> int:
     # events recorded inside it are resolved only now), and what RCCL ran on
     ph = solver.phase_times() if phases else None
     comm = solver.comm_info() if (use_dist and world > 1) else None
+    peer_flag = bool(solver.info.flags & cg.CGX_PEER_ACTIVE) if devices else False
     all_ph = gather_objects(dist, ph) if (dist and phases) else ([ph] if phases else None)
     all_comm = gather_objects(dist, comm) if comm is not None else None
 
@@ -464,9 +508,11 @@ def main(argv=None) -> int:
     # The kernels' own spans come from the CGX_PHASES stamps (device clock,
     # first block's start to last block's end): their sum is the matVec's
     # duration on rank 0's GPU.
+    # The roofline takes the slowest rank's kernel spans (max over ranks);
+    # matvec_ms stays the CGX_TIMING event figure of earlier rounds.
     mv_kernel_ms = None
     if all_ph is not None and world > 1 and all_ph[0]["matvec_own"]["samples"] > 0:
-        mv_kernel_ms = (all_ph[0]["matvec_own"]["median_us"] + all_ph[0]["matvec"]["median_us"]) / 1e3
+        mv_kernel_ms = max(ph["matvec_own"]["median_us"] + ph["matvec"]["median_us"] for ph in all_ph) / 1e3
     achieved = (link_bytes if link_bound else bytes_launch) / ((mv_kernel_ms or mv_ms) * 1e-3) / 1e9
     traffic, traffic_src = (None, None) if (stream or poisson) else pmc_traffic(n, world,
                                                                                "_symmetric" if symmetric else "")
@@ -476,7 +522,7 @@ def main(argv=None) -> int:
         "metric": METRIC,
         "value": iters_per_s,
         "unit": "iterations/s",
-        "n_gpus": world,
+        "n_gpus": n_gpus,
         "steps": args.steps,
         "warmup": args.warmup,
         "settle_s": args.settle,
@@ -493,17 +539,25 @@ def main(argv=None) -> int:
                          + (" as its upper-triangle tiles (CGX_SYMMETRIC)" if symmetric else "")
                          + (f" except the first {res_rows} {'tiles' if symmetric else 'rows per GPU'}, kept in HBM "
                             f"({args.resident_gb:g} GB budget)" if res_rows else "")
-                         + f", row-block over {world} GPU(s), fixed-count iterations") if stream else
-                        (f"configs[4]: matrix-free 5-point Poisson CG, m={m} (N={n}), b=1, x0=0, slabs over {world} "
-                         f"GPU(s), halo exchange, fixed-count iterations") if poisson else
+                         + f", row-block over {span}, fixed-count iterations") if stream else
+                        (f"configs[4]: matrix-free 5-point Poisson CG, m={m} (N={n}), b=1, x0=0, slabs over {span}, "
+                         f"halo exchange, fixed-count iterations") if poisson else
                         (f"configs[{1 if n == 16384 else 2}] system, A stored as its upper triangle (128x128 tiles, "
                          f"CGX_SYMMETRIC), N={n} dense SPD fp64 CG on 1 GPU, fixed-count iterations") if symmetric else
-                        (f"configs[{1 if n == 16384 else 2}]: N={n} dense SPD fp64 CG, row-block over {world} GPU(s), "
+                        (f"configs[{1 if n == 16384 else 2}]: N={n} dense SPD fp64 CG, row-block over {span}, "
                          f"fixed-count iterations"),
             "n": n,
             "rows_per_gpu": nloc,
             "parallelism": f"rowblock{world}",
-            "exchange": ("none (single GPU)" if not use_dist or world == 1 else
+            "exchange": ("none (single GPU)" if world == 1 else
+                         ("one process, row blocks on devices " + ",".join(map(str, devices)) +
+                          ": halo rows by peer copies + scalars combined by a pull kernel per block"
+                          if poisson else
+                          "one process, row blocks on devices " + ",".join(map(str, devices)) +
+                          ": p gathered by a pull kernel per block over peer access"
+                          + (" (overlapped with the own-block matVec)" if overlap_on else "")
+                          + " + scalars combined in rank order by a pull kernel per block")
+                         if devices else
                          "RCCL halo ncclSend/Recv + 2x allreduce" if poisson else
                          "point-to-point_cg.c pattern: ncclSend/Recv via rank 0" if args.comm == "p2p" else
                          "RCCL allgather(p) overlapped + rank-ordered scalar combine (allgather of partials)"
@@ -511,12 +565,15 @@ def main(argv=None) -> int:
                          "RCCL allgather(p) overlapped with own-block matVec + 2x allreduce"
                          if overlap_on else "RCCL allgather(p) + 2x allreduce"),
         },
-        "matvec_gbps": bytes_launch / ((mv_kernel_ms or mv_ms) * 1e-3) / 1e9,
-        "matvec_ms": mv_kernel_ms or mv_ms,
-        "matvec_ms_source": ("rank 0's own-block + rest matVec kernel spans (CGX_PHASES medians, device clock)"
-                             if mv_kernel_ms else "HIP events around the matVec launch on its stream (CGX_TIMING)"),
-        "matvec_ms_events": mv_ms,
+        "matvec_gbps": bytes_launch / (mv_ms * 1e-3) / 1e9,
+        "matvec_ms": mv_ms,
+        "matvec_ms_source": ("HIP events around the matVec launch(es) on rank 0's / block 0's stream (CGX_TIMING); "
+                             "with several row blocks and the overlap they bracket both launches and the wait for "
+                             "p's allgather between them"),
         "matvec_ms_max_rank": mv_ms_max,
+        # the kernels alone: own-block + rest spans on the device clock, the slowest rank's (roofline.achieved)
+        "matvec_kernel_ms": mv_kernel_ms,
+        "matvec_kernel_gbps": bytes_launch / (mv_kernel_ms * 1e-3) / 1e9 if mv_kernel_ms else None,
         "roofline": {
             "bound": "h2d" if link_bound else "hbm",
             "achieved": achieved,
@@ -543,6 +600,9 @@ def main(argv=None) -> int:
         out["phases_us"] = phase_summary(all_ph, elapsed / args.steps * 1e3)
     if all_comm is not None:
         out["rccl"] = rccl_summary(all_comm, solver_device=local_rank % max(1, cg.device_count()))
+    if devices:
+        out["config"]["row_blocks"] = len(devices)
+        out["multi_device"] = local_summary(devices, peer_flag)
     if world == 1 and not args.no_cpu and poisson:
         out["cpu_baseline"] = cpu_baseline_poisson(m)
     elif world == 1 and not args.no_cpu and not stream and not symmetric:

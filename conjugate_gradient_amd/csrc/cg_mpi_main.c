@@ -195,18 +195,20 @@ int main(int argc, char **argv) {
     if (!rc[2]) rc[2] = read_values(pos[2], row0, nloc, fp32ref, (char *)x + (size_t)row0 * es, 1);
     if (!p2p && !rc[0]) rc[0] = read_values(pos[0], row0 * n, nloc * n, fp32ref, A, threads);
     if (!p2p && !rc[1]) rc[1] = read_values(pos[1], row0, nloc, fp32ref, b, threads);
-    if (p2p) {
-        MPI_Barrier(MPI_COMM_WORLD); /* point-to-point_cg.c:119-120: the bracket opens before the reads */
-        t_dist0 = MPI_Wtime();
-        if (!rc[0]) rc[0] = read_values(pos[0], row0 * n, nloc * n, fp32ref, A, threads);
-        if (!rc[1]) rc[1] = read_values(pos[1], row0, nloc, fp32ref, b, threads);
-    }
+    if (p2p) /* the files are parsed inside the bracket; whether they open is known before the GPU set-up */
+        for (int f = 0; f < 2; ++f) {
+            cgx_text *t = NULL;
+            if (!rc[f]) rc[f] = cgx_text_open(pos[f], 1, &t);
+            cgx_text_close(t);
+        }
+    cgx_ctx *ctx = NULL;
     if (input_failed(rank, p2p, pos, rc)) {
         MPI_Finalize();
         return 1;
     }
-
-    /* RCCL bootstrap over MPI, then the rank's context on its GPU */
+    /* RCCL bootstrap over MPI, then the rank's context on its GPU -- before
+     * the p2p distribution bracket opens, so that bracket holds only what
+     * point-to-point_cg.c:119-127 times (the reads and the distribution) */
     cgx_unique_id id;
     memset(&id, 0, sizeof id);
     int id_rc = CGX_OK;
@@ -223,11 +225,22 @@ int main(int argc, char **argv) {
     const char *de = getenv("CGX_DEVICE");
     const int dev = de ? atoi(de) : (ndev > 0 ? local_rank % ndev : 0);
     const int flags = (fp32ref ? CGX_F32_REF : CGX_F64) | (p2p ? CGX_COMM_P2P : 0);
-    cgx_ctx *ctx = NULL;
     const int crc = cgx_create_rank(&ctx, n, rank, nranks, &id, dev, flags);
     if (crc != CGX_OK) {
         fprintf(stderr, "rank %d: cgx_create_rank: %s (%s)\n", rank, cgx_strerror(crc), cgx_last_error());
         MPI_Abort(MPI_COMM_WORLD, 1); /* as parallel_cg.c stops the job */
+    }
+
+    if (p2p) {
+        MPI_Barrier(MPI_COMM_WORLD); /* point-to-point_cg.c:119-120: the bracket opens before the reads */
+        t_dist0 = MPI_Wtime();
+        if (!rc[0]) rc[0] = read_values(pos[0], row0 * n, nloc * n, fp32ref, A, threads);
+        if (!rc[1]) rc[1] = read_values(pos[1], row0, nloc, fp32ref, b, threads);
+    }
+    if (p2p && input_failed(rank, p2p, pos, rc)) {
+        cgx_destroy(ctx);
+        MPI_Finalize();
+        return 1;
     }
 
     /* the scatter of A and b and the broadcast of x0: parallel_cg.c:109-117

@@ -270,6 +270,10 @@ struct cgx_ctx {
     bool xdefer = false;
     int xd = 1;  // the period: 2 (default) or 3 (CGX_POISSON_XDEFER=3, a third p slab)
     int64_t xd_k0 = 0;
+    // a cgx_iterate call failed with x updates still deferred (xd > 1): the
+    // alphas left out cannot be placed, so x is incomplete until the next
+    // cgx_solve_begin; cgx_get_x / cgx_iterate / cgx_residual_norm refuse it
+    bool x_incomplete = false;
     // rank mode fail-fast (cgx_exchange.hip, rank_wait_*): every host wait
     // polls with a deadline of rccl_timeout_s seconds (CGX_RCCL_TIMEOUT_S,
     // default 60, 0 = wait forever) and checks the communicator's asynchronous
@@ -282,6 +286,11 @@ struct cgx_ctx {
     const char *last_coll = "none";  // the last exchange enqueued, and its iteration
     int64_t last_coll_k = -1;
     bool peer = false;  // multi-shard over distinct devices: peer access enabled between every pair
+    // LOCAL mode: the allgather and the scalar combines as one pull kernel per
+    // consuming shard (gather_slices / combine_peers_*), the default; false
+    // (CGX_LOCAL_XCHG=copy): one hipMemcpyPeerAsync per (consumer, producer)
+    // pair, round 3's form, kept for A/B runs
+    bool xchg_kernels = true;
     // CGX_PHASES: resolved per-iteration phase durations (us), cgx_phase_times' order;
     // the wall clock's rate, and the previous stamped iteration's first start /
     // last end (ticks; 0 = none) so the gap across a resolve is still measured
@@ -362,6 +371,7 @@ int do_begin(cgx_ctx *c);
 int read_scalar(cgx_ctx *c, int gslot, double *out);
 int do_iteration_poisson(cgx_ctx *c, double eps, int *stop, bool gated);
 int poisson_x_finish(cgx_ctx *c);
+int check_x_complete(const cgx_ctx *c);
 int do_iteration(cgx_ctx *c, double eps, int *stop, bool gated = false);
 // cgx_api.hip
 int dev_ws(RedWs *out);

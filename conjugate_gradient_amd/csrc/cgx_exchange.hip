@@ -146,6 +146,15 @@ int local_barrier(cgx_ctx *c) {
     return CGX_OK;
 }
 
+// The table of every shard's copy of a buffer at byte offset `off` (+ the
+// shard's own row offset when `own_rows`), in shard order, for the pull
+// kernels of the LOCAL exchange.
+static PeerTable peer_table(const cgx_ctx *c, char *Shard::*buf, int64_t off) {
+    PeerTable t{};
+    for (const auto &s : c->sh) t.p[s.index] = s.*buf + off;
+    return t;
+}
+
 // Poisson: refresh the two halo rows of every slab from its neighbours
 // (ncclSend/Recv of one grid row each way in rank mode, device copies in
 // LOCAL mode); from_x first copies x into the slab interior (for A x0).
@@ -333,8 +342,19 @@ int exchange_allgather(cgx_ctx *c, bool from_x) {
               from_x ? "ncclAllGather(x)" : "ncclAllGather(p)");
         return CGX_OK;
     }
-    // LOCAL: device-to-device copies after all producers are done.
+    // LOCAL: after all producers are done, every shard pulls the other
+    // slices: one gather kernel per shard (or, CGX_LOCAL_XCHG=copy, a peer
+    // copy per pair).
     TRY(local_barrier(c));
+    if (c->xchg_kernels) {
+        const PeerTable src = peer_table(c, from_x ? &Shard::x : &Shard::pown, 0);
+        for (auto &d : c->sh) {
+            TRY(set_dev(d));
+            HIPT(gather_slices(src, (int)c->sh.size(), from_x ? -1 : d.index, d.nloc * (int64_t)es, d.pfull,
+                               d.stream));
+        }
+        return CGX_OK;
+    }
     for (auto &d : c->sh) {
         TRY(set_dev(d));
         for (auto &s : c->sh) {
@@ -374,6 +394,17 @@ int exchange_scalar(cgx_ctx *c, int lslot, int gslot) {
         return CGX_OK;
     }
     TRY(local_barrier(c));
+    if (c->xchg_kernels) {  // every shard reads the S partials from their slots: the same sums, no copies
+        const PeerTable src = peer_table(c, &Shard::scal, 8 * (int64_t)lslot);
+        for (auto &d : c->sh) {
+            TRY(set_dev(d));
+            if (f32ref(c))  // parallel_cg.c's MPI_Allreduce order (MPICH), as in rank mode
+                HIPT(combine_peers_f32(src, S, reinterpret_cast<float *>(slot(d, gslot)), d.stream, true));
+            else
+                HIPT(combine_peers_f64(src, S, reinterpret_cast<double *>(slot(d, gslot)), d.stream));
+        }
+        return CGX_OK;
+    }
     for (auto &d : c->sh) {
         TRY(set_dev(d));
         for (auto &s : c->sh)
@@ -408,12 +439,16 @@ int overlapped_matvec(cgx_ctx *c, int dot_slot, bool gated) {
               "ncclAllGather(p), overlapped");
         HIPT(hipEventRecord(s.ev_gathered, s.cstream));
     } else {
+        const PeerTable src = peer_table(c, &Shard::pown, 0);
         for (auto &d : c->sh) {
             TRY(set_dev(d));
             for (auto &s : c->sh) HIPT(hipStreamWaitEvent(d.cstream, s.ev_pready, 0));
-            for (auto &s : c->sh)
-                if (&s != &d)
-                    HIPT(hipMemcpyPeerAsync(d.pfull + s.row0 * es, d.dev, s.pown, s.dev, s.nloc * es, d.cstream));
+            if (c->xchg_kernels)
+                HIPT(gather_slices(src, (int)c->sh.size(), d.index, d.nloc * (int64_t)es, d.pfull, d.cstream));
+            else
+                for (auto &s : c->sh)
+                    if (&s != &d)
+                        HIPT(hipMemcpyPeerAsync(d.pfull + s.row0 * es, d.dev, s.pown, s.dev, s.nloc * es, d.cstream));
             HIPT(hipEventRecord(d.ev_gathered, d.cstream));
         }
     }

@@ -215,6 +215,7 @@ int do_begin(cgx_ctx *c) {
     c->k = 0;
     c->converged = 0;
     c->state = ST_BEGUN;
+    c->x_incomplete = false;
     return CGX_OK;
 }
 
@@ -331,6 +332,12 @@ int poisson_x_finish(cgx_ctx *c) {
     }
     c->xd_k0 = c->k;
     return CGX_OK;
+}
+
+int check_x_complete(const cgx_ctx *c) {
+    if (!c->x_incomplete) return CGX_OK;
+    return fail(CGX_ERR_STATE, "an earlier cgx_iterate failed with x updates still deferred (Poisson, x every "
+                               "%d-th iteration): x is incomplete until the next cgx_solve_begin", c->xd);
 }
 
 // One loop iteration k (serialConjugate.c:215-244 / parallel_cg.c:290-323).
@@ -639,10 +646,22 @@ static int iterate_gated(cgx_ctx *c, int64_t count, double eps, int64_t *done, i
     return CGX_OK;
 }
 
+static int iterate_calls(cgx_ctx *c, int64_t count, double eps, int64_t *done, int *converged);
+
 int cgx_iterate(cgx_ctx *c, int64_t count, double eps, int64_t *done, int *converged) {
     const Range range_("cgx_iterate");
     if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
     if (c->state == ST_IDLE) return fail(CGX_ERR_STATE, "cgx_iterate before cgx_solve_begin");
+    TRY(check_x_complete(c));
+    const int rc = iterate_calls(c, count, eps, done, converged);
+    // A failure inside the call (a HIP error, an RCCL deadline) may leave x
+    // updates deferred (poisson_x_finish not reached): say so at the next use
+    // of x instead of handing out an x with terms silently missing.
+    if (rc != CGX_OK && c->fused && c->xd > 1) c->x_incomplete = true;
+    return rc;
+}
+
+static int iterate_calls(cgx_ctx *c, int64_t count, double eps, int64_t *done, int *converged) {
     const char *gv = std::getenv("CGX_GATED");
     const bool gate_ok = !(gv && *gv == '0');
     c->xd_k0 = c->k;
@@ -753,6 +772,13 @@ int cgx_set_matvec_plan(cgx_ctx *c, int rows_per_wave, int chunks_in_flight, int
     if (nontemporal != 0 && nontemporal != 1 && nontemporal != 2 && nontemporal != 8)
         return fail(CGX_ERR_ARG, "load policy must be 0 (plain), 1 (non-temporal), 2 (pipelined) or 8 (pipelined "
                                  "non-temporal)");
+    // The folded iteration keeps p_k in pfull / p_alt by the parity of k, and
+    // the other forms keep it in pfull: switching forms inside a solve would
+    // multiply a stale p.  A plan that turns the fold off waits for the next
+    // cgx_solve_begin.
+    if (R > 2 && c->fold_p && c->state == ST_BEGUN)
+        return fail(CGX_ERR_STATE, "rows_per_wave %d turns the folded iteration off: not inside a solve "
+                                   "(set the plan before cgx_solve_begin)", R);
     for (auto &s : c->sh) {
         TRY(set_dev(s));
         MatvecPlan pl = plan_matvec_f64(s.dev, s.nloc, R, U, nontemporal, blocks_per_cu, c->lda);
@@ -776,6 +802,7 @@ int cgx_get_matvec_plan(cgx_ctx *c, int *rows_per_wave, int *chunks_in_flight, i
 int cgx_residual_norm(cgx_ctx *c, double *rnorm, double *bnorm) {
     const Range range_("cgx_residual_norm");
     if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
+    TRY(check_x_complete(c));
     // ||b - A x|| with the current x: allgather x, matVec, residual, two dots.
     TRY(settle_halo(c));
     TRY(exchange_allgather(c, /*from_x=*/true));

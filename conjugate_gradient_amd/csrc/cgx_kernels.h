@@ -112,6 +112,28 @@ hipError_t gen_spd_f64(int64_t n, int64_t lda, int64_t row0, int64_t nrows, uint
 // out = sum_{q<cnt} (8-byte slot q of in), in q order (one thread): rank-ordered combine.
 hipError_t sum_ordered_f64(const double *in, int cnt, double *out, hipStream_t s);
 
+// ---- the multi-shard exchange in one process (several row blocks, LOCAL) ---
+// Pointers to every shard's copy of something (its p slice, its scalar slot),
+// in shard order; passed by value.  On distinct devices they are peer
+// pointers (access enabled at context creation): the kernels below run on the
+// CONSUMING shard's stream and only read peers' memory -- the same pull a
+// hipMemcpyPeerAsync on that stream does -- after the stream has waited for
+// the producers' events.
+constexpr int kMaxPeers = 32;
+struct PeerTable {
+    const char *p[kMaxPeers];
+};
+// dst[q * slice_bytes ...] = src.p[q][0 .. slice_bytes) for every q < cnt
+// except q == skip (the consumer's own slice, already in place; skip < 0
+// copies every slice): the allgather of p (or of x) in one launch instead of
+// cnt - 1 peer copies.
+hipError_t gather_slices(const PeerTable &src, int cnt, int skip, int64_t slice_bytes, char *dst, hipStream_t s);
+// *out = the cnt partials src.p[q] (fp64), summed in q order: the rank-order
+// combine of exchange_scalar read straight from each shard's slot.
+hipError_t combine_peers_f64(const PeerTable &src, int cnt, double *out, hipStream_t s);
+// F32_REF: the float partials in rank order or (mpich) MPICH's MPI_Allreduce order.
+hipError_t combine_peers_f32(const PeerTable &src, int cnt, float *out, hipStream_t s, bool mpich);
+
 // 5-point Poisson A.p on a slab of mloc grid rows of width m; ph has one halo
 // row above and below.  *dot_out = ph[m..] . Ap when dot_out != nullptr.
 hipError_t stencil5_f64(const double *ph, int64_t mloc, int64_t m, double *Ap, double *dot_out, const RedWs &ws,

@@ -354,6 +354,10 @@ static bool can_fuse_ref_dot(const cgx_ctx *c) {
 }
 
 int finish_create(cgx_ctx *c, cgx_ctx **out) {
+    {
+        const char *e = std::getenv("CGX_LOCAL_XCHG");
+        c->xchg_kernels = !(e && !std::strcmp(e, "copy"));
+    }
     c->overlap = can_overlap(c);
     c->fused_p = can_fuse_p(c);
     {  // the folded form of the two-launch iteration (CGX_FOLD_P=0 / 1: never / at any fused n)
@@ -842,6 +846,7 @@ int cgx_set_x(cgx_ctx *c, const void *x) {
 int cgx_get_x(cgx_ctx *c, void *x) {
     const Range range_("cgx_get_x");
     if (!c || !x) return fail(CGX_ERR_ARG, "NULL argument");
+    TRY(check_x_complete(c));
     const size_t es = (size_t)c->es;
     if (c->mode == M_RCCL && c->nranks > 1) {
         Shard &s = c->sh[0];

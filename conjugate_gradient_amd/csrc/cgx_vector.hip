@@ -470,7 +470,82 @@ __global__ void k_sum_ordered(const T *in, int cnt, int stride, int mpich, T *ou
     *out = v[0];
 }
 
+// The same combines over a table of peer pointers (one partial per shard).
+template <typename T>
+__global__ void k_combine_peers(PeerTable src, int cnt, int mpich, T *out) {
+#pragma clang fp contract(off)
+    T in[kMaxPeers];
+    for (int q = 0; q < cnt; ++q) in[q] = *reinterpret_cast<const T *>(src.p[q]);
+    if (!mpich) {
+        T s = in[0];
+        for (int q = 1; q < cnt; ++q) s = s + in[q];
+        *out = s;
+        return;
+    }
+    int pof2 = 1;
+    while (pof2 * 2 <= cnt) pof2 *= 2;
+    const int rem = cnt - pof2;
+    T v[kMaxPeers];
+    for (int q = 0; q < pof2; ++q) v[q] = q < rem ? in[2 * q] + in[2 * q + 1] : in[q + rem];
+    for (int d = 1; d < pof2; d *= 2)
+        for (int q = 0; q < pof2; q += 2 * d) v[q] = v[q] + v[q + d];
+    *out = v[0];
+}
+
+// blockIdx.y = the source slice; each thread moves kGU words of W bytes per
+// pass with all its loads issued before the stores (remote reads over xGMI
+// are latency-bound: keep many in flight).
+constexpr int kGU = 4;
+template <typename W>
+__global__ __launch_bounds__(kNT) void k_gather_slices(PeerTable src, int skip, int64_t words, char *dst) {
+    const int q = blockIdx.y;
+    if (q == skip) return;
+    const W *__restrict__ in = reinterpret_cast<const W *>(src.p[q]);
+    W *__restrict__ out = reinterpret_cast<W *>(dst) + (int64_t)q * words;
+    const int64_t stride = (int64_t)gridDim.x * kNT * kGU;
+    for (int64_t base = (int64_t)blockIdx.x * kNT * kGU + threadIdx.x; base < words; base += stride) {
+        W v[kGU];
+#pragma unroll
+        for (int u = 0; u < kGU; ++u)
+            if (base + u * kNT < words) v[u] = in[base + u * kNT];
+#pragma unroll
+        for (int u = 0; u < kGU; ++u)
+            if (base + u * kNT < words) out[base + u * kNT] = v[u];
+    }
+}
+
 }  // namespace
+
+hipError_t gather_slices(const PeerTable &src, int cnt, int skip, int64_t slice_bytes, char *dst, hipStream_t s) {
+    if (cnt < 1 || cnt > kMaxPeers || slice_bytes < 0 || (slice_bytes & 3)) return hipErrorInvalidValue;
+    if (slice_bytes == 0) return hipSuccess;
+    bool a16 = (slice_bytes % 16) == 0 && (reinterpret_cast<uintptr_t>(dst) % 16) == 0;
+    bool a8 = (slice_bytes % 8) == 0 && (reinterpret_cast<uintptr_t>(dst) % 8) == 0;
+    for (int q = 0; q < cnt; ++q) {
+        a16 = a16 && (reinterpret_cast<uintptr_t>(src.p[q]) % 16) == 0;
+        a8 = a8 && (reinterpret_cast<uintptr_t>(src.p[q]) % 8) == 0;
+    }
+    const int64_t wb = a16 ? 16 : a8 ? 8 : 4, words = slice_bytes / wb;
+    const int64_t per_block = (int64_t)kNT * kGU;
+    const unsigned gx = (unsigned)std::min<int64_t>((words + per_block - 1) / per_block, 64);
+    const dim3 grid(gx, (unsigned)cnt);
+    if (a16) hipLaunchKernelGGL(k_gather_slices<uint4>, grid, dim3(kNT), 0, s, src, skip, words, dst);
+    else if (a8) hipLaunchKernelGGL(k_gather_slices<uint2>, grid, dim3(kNT), 0, s, src, skip, words, dst);
+    else hipLaunchKernelGGL(k_gather_slices<unsigned>, grid, dim3(kNT), 0, s, src, skip, words, dst);
+    return hipGetLastError();
+}
+
+hipError_t combine_peers_f64(const PeerTable &src, int cnt, double *out, hipStream_t s) {
+    if (cnt < 1 || cnt > kMaxPeers) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_combine_peers<double>, dim3(1), dim3(1), 0, s, src, cnt, 0, out);
+    return hipGetLastError();
+}
+
+hipError_t combine_peers_f32(const PeerTable &src, int cnt, float *out, hipStream_t s, bool mpich) {
+    if (cnt < 1 || cnt > kMaxPeers) return hipErrorInvalidValue;
+    hipLaunchKernelGGL(k_combine_peers<float>, dim3(1), dim3(1), 0, s, src, cnt, mpich ? 1 : 0, out);
+    return hipGetLastError();
+}
 
 hipError_t residual_f64(int64_t n, const double *b, const double *Ax, double *r, double *p,
                         double *rr_out, const RedWs &ws, hipStream_t s, int64_t *clear2) {

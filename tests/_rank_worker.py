@@ -44,7 +44,7 @@ def main():
         with open(uidfile, "rb") as f:
             uid = f.read()
     res = {"rank": rank}
-    if mode in ("peer_dies", "peer_absent"):
+    if mode in ("peer_dies", "peer_absent", "poisson_peer_dies"):
         return fail_fast(mode, n, P, rank, uid, out)
     if mode.startswith("poisson"):
         m = n
@@ -93,11 +93,22 @@ def fail_fast(mode, n, P, rank, uid, out):
       peer_dies:   the last rank exits right after cgx_create_rank; the others
                    set up and solve, and must get CGX_ERR_RCCL within the deadline.
       peer_absent: the last rank never creates its context; the others must get
-                   CGX_ERR_RCCL from cgx_create_rank within the deadline."""
+                   CGX_ERR_RCCL from cgx_create_rank within the deadline.
+      poisson_peer_dies: peer_dies on an m = n Poisson grid, x deferred over
+                   iterations (the default): after the failed iterate, x is
+                   refused (CGX_ERR_STATE) instead of handed out incomplete."""
+    poisson = mode == "poisson_peer_dies"
     if rank == P - 1:
         if mode == "peer_dies":
             cg.Solver(n, rank=rank, nranks=P, unique_id=uid, device=0)
+        if poisson:  # joins the solve's start (its collectives), then dies before the iterations
+            s = cg.Solver(None, poisson_m=n, rank=rank, nranks=P, unique_id=uid, device=0)
+            s.fill(1.0, 0.0)
+            s.begin()
+            s.synchronize()
         os._exit(0)  # no destroy, no finalisation: as if the process died
+    if poisson:
+        return fail_fast_poisson(n, P, rank, uid, out)
     A, b, x0 = case(f"spd{n}", np.float64)
     t0 = time.time()
     res = {"rank": rank, "error": None}
@@ -127,6 +138,29 @@ def fail_fast(mode, n, P, rank, uid, out):
             say(f"destroy: {e}")
     say("exit")
     os._exit(0)  # as bench.py does after an error: no teardown that could wait on the dead peer
+
+
+def fail_fast_poisson(m, P, rank, uid, out):
+    t0 = time.time()
+    res = {"rank": rank, "error": None}
+    s = cg.Solver(None, poisson_m=m, rank=rank, nranks=P, unique_id=uid, device=0)
+    res["created_s"] = time.time() - t0
+    res["xdefer"] = bool(s.info.flags & cg.CGX_XDEFER_ACTIVE)
+    s.fill(1.0, 0.0)
+    try:
+        s.begin()
+        s.iterate(200, eps=1e-12)
+    except cg.CgxError as e:
+        res.update(error=str(e), code=e.code)
+    try:
+        s.get_x()
+        res["get_x"] = "ok"
+    except cg.CgxError as e:
+        res.update(get_x=str(e), get_x_code=e.code)
+    res["elapsed_s"] = time.time() - t0
+    with open(out + f"_r{rank}.json", "w") as f:
+        json.dump(res, f)
+    os._exit(0)
 
 
 if __name__ == "__main__":

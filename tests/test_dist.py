@@ -105,3 +105,25 @@ def test_rccl_summary_counts_devices():
     out = bench.rccl_summary(ranks, solver_device=0)
     assert out["nranks"] == 2 and out["distinct_devices"] == 2 and len(out["pci_bus_ids"]) == 2
     assert out["links_from_rank0"][0]["to_rank"] == 1 and "link" in out["links_from_rank0"][0]
+
+
+@pytest.mark.timeout(120)
+def test_bench_gpus_without_launcher_fails_loudly_when_devices_are_missing():
+    """`bench.py --gpus 2` outside torchrun drives devices 0 and 1 from one
+    process; with fewer GPUs visible (none here) it exits non-zero and says
+    so, and prints no JSON line -- never a 1-GPU line for a 2-GPU request."""
+    import subprocess
+    import sys
+
+    import conjugate_gradient_amd as cg
+    if cg.device_count() >= 2:
+        pytest.skip("two GPUs are visible: the run would proceed")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2", "--no-cpu"],
+                       capture_output=True, text=True, timeout=100)
+    assert p.returncode != 0
+    assert not [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert "--gpus 2" in p.stderr and "device(s) are visible" in p.stderr
+    p = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "3", "--devices", "0,0",
+                        "--no-cpu"], capture_output=True, text=True, timeout=100)
+    assert p.returncode != 0 and "--devices lists 2" in p.stderr

@@ -97,6 +97,43 @@ def test_f32ref_shards_bit_exact_vs_mpi_reference(key):
     assert np.array_equal(x.view(np.uint32), mpi_golden_x(key).view(np.uint32))
 
 
+@pytest.mark.parametrize("P", [2, 3, 8])
+@pytest.mark.parametrize("kind", ["f64", "f64_nooverlap", "f32ref"])
+def test_local_exchange_kernels_bitwise_equal_peer_copies(monkeypatch, kind, P):
+    """The multi-shard exchange in one process: the pull kernels (one gather
+    kernel and one combine kernel per consuming shard, the default) move the
+    same bytes and add the same partials in the same order as round 3's
+    per-pair peer copies (CGX_LOCAL_XCHG=copy): x bit for bit, the same loop
+    count -- with the overlapped gather, the plain one (3 shards: 2048/3 is no
+    multiple of 128 rows; CGX_NO_OVERLAP), the x0 allgather of a nonzero x0,
+    and F32_REF's MPICH-order combine."""
+    n = 2048 if P != 3 else 2049
+    f32 = kind == "f32ref"
+    dt = np.float32 if f32 else np.float64
+    A, b = oracle.spd_hash(n, seed=11, dtype=dt)
+    x0 = np.full(n, 0.125, dt)
+    flags = cg.CGX_F32_REF if f32 else cg.CGX_F64 | (cg.CGX_NO_OVERLAP if kind == "f64_nooverlap" else 0)
+    res = {}
+    for form in ("kernel", "copy"):
+        monkeypatch.setenv("CGX_LOCAL_XCHG", form)
+        with cg.Solver(n, flags=flags, devices=[0] * P) as s:
+            if kind == "f64" and P in (2, 8):
+                assert s.info.flags & cg.CGX_OVERLAP_ACTIVE
+            s.set_system(A, b, x0)
+            x, st = s.solve(None, eps=1e-6 if f32 else 1e-10)
+            xf, stf = s.solve(x0, eps=-1.0, max_iter=7)
+            rn, bn = s.residual_norm()
+        res[form] = (x, st.iterations, xf, rn)
+    (xk, itk, xfk, rnk), (xc, itc, xfc, rnc) = res["kernel"], res["copy"]
+    assert itk == itc and np.array_equal(xk, xc) and np.array_equal(xfk, xfc) and rnk == rnc
+    if f32:
+        xo, so = oracle.cg_f32ref(A, b, x0, eps=1e-6, nparts=P, combine="mpich")
+        assert itk == so.iterations and np.array_equal(xk.view(np.uint32), xo.view(np.uint32))
+    else:
+        xo, so = oracle.cg_f64(A, b, x0, eps=1e-10)
+        assert itk == so.iterations and rel(xk, xo) <= TOL
+
+
 @pytest.mark.parametrize("P", [2, 4, 8])
 @pytest.mark.parametrize("name", ["kat4", "spd1024", "spd4096"])
 def test_row_block_shards_f64(golden, name, P):
@@ -520,6 +557,42 @@ def test_two_launch_iteration_bitwise_equals_three(monkeypatch, n, seed):
         assert conv and dp == it and np.array_equal(xp, ref[0]), key
     xo, so = oracle.cg_f64(A, b, np.zeros(n), eps=1e-10)
     assert ref[1] == so.iterations and rel(ref[0], xo) <= TOL
+
+
+@pytest.mark.parametrize("n", [1024, 2048])
+def test_plan_change_inside_a_folded_solve_is_refused(n):
+    """A matVec plan with more than 2 rows per wave turns the folded iteration
+    off.  Inside a solve that would multiply a stale p (p_k lives in pfull or
+    p_alt by the parity of k), so cgx_set_matvec_plan refuses it there
+    (CGX_ERR_STATE) and the solve goes on bit for bit.  A plan that keeps the
+    fold may change between cgx_iterate calls (x agrees with the oracle), and
+    the R = 4 plan is taken between solves (the next solve runs unfolded)."""
+    A, b = oracle.spd_hash(n, seed=6)
+    xo, so = oracle.cg_f64(A, b, np.zeros(n), eps=1e-10)
+    with cg.Solver(n) as s:
+        assert s.info.flags & cg.CGX_FOLD_ACTIVE
+        s.set_system(A, b)
+        x_ref, st = s.solve(np.zeros(n), eps=1e-10)
+        s.set_x(np.zeros(n))
+        s.begin()
+        d1, _ = s.iterate(3)
+        with pytest.raises(cg.CgxError) as e:
+            s.set_matvec_plan(4, 8)
+        assert e.value.code == -6  # CGX_ERR_STATE
+        assert s.info.flags & cg.CGX_FOLD_ACTIVE
+        d2, conv = s.iterate(100, eps=1e-10)
+        assert conv and d1 + d2 == st.iterations and np.array_equal(s.get_x(), x_ref)
+        s.set_x(np.zeros(n))
+        s.begin()
+        s.iterate(3)
+        s.set_matvec_plan(2, 4)
+        assert s.info.flags & cg.CGX_FOLD_ACTIVE
+        _, conv = s.iterate(100, eps=1e-10)
+        assert conv and rel(s.get_x(), xo) <= TOL
+        s.set_matvec_plan(4, 8)
+        assert not s.info.flags & cg.CGX_FOLD_ACTIVE
+        x4, st4 = s.solve(np.zeros(n), eps=1e-10)
+    assert st4.iterations == so.iterations and rel(x4, xo) <= TOL
 
 
 @pytest.mark.parametrize("n,seed", [(2048, 6), (2100, 8), (4096, 7), (5000, 9), (8192, 3)])

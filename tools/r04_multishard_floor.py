@@ -1,0 +1,64 @@
+"""Per-iteration cost of the single-process multi-shard path (cgx_create_multi,
+`cg_hip --gpus P`) at S = 1/2/4/8 row blocks, every shard on device 0
+(devices=[0]*S): fixed-count iterations (dense fp64, the overlapped exchange),
+timed three ways:
+  enqueue_us  host time inside cgx_iterate per iteration (it returns without
+              a sync for eps < 0, so this is the host's enqueue cost alone);
+  wall_us     host time from the call to the end of cgx_synchronize;
+  phases      the CGX_PHASES device-clock medians on shard 0.
+On one GPU the shards' kernels share the device, so wall_us is the sum of all
+shards' work; the host side (enqueue_us) is what a distinct-device run pays
+too.  Exchange forms (CGX_LOCAL_XCHG, read at context creation): "kernel"
+(one pull kernel per consuming shard for the gather and each combine, the
+default) and "copy" (round 3's hipMemcpyPeerAsync per pair), interleaved.
+Usage:  python tools/r04_multishard_floor.py [rounds] [n,...] [S,...] [forms]
+  > profiles/r04_multishard_floor.jsonl"""
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
+import conjugate_gradient_amd as cg  # noqa: E402
+
+
+def run(n, shards, steps=200, warm=30):
+    flags = cg.CGX_PHASES
+    with cg.Solver(n, flags=flags, devices=[0] * shards) as s:
+        s.generate_spd(42)
+        info = s.info
+        s.begin()
+        s.iterate(warm, eps=-1.0)
+        s.synchronize()
+        s.reset_timing()
+        t0 = time.perf_counter()
+        s.iterate(steps, eps=-1.0)
+        t1 = time.perf_counter()
+        s.synchronize()
+        t2 = time.perf_counter()
+        ph = s.phase_times()
+        rn, bn = s.residual_norm()
+    return {"n": n, "shards": shards, "steps": steps, "exchange": os.environ.get("CGX_LOCAL_XCHG", "default"),
+            "flags": int(info.flags),
+            "enqueue_us": round((t1 - t0) / steps * 1e6, 2), "wall_us": round((t2 - t0) / steps * 1e6, 2),
+            "relres": rn / bn,
+            "phases_median_us": {k: round(v["median_us"], 2) for k, v in ph.items() if v["samples"]}}
+
+
+def main():
+    rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 2
+    sizes = tuple(int(v) for v in sys.argv[2].split(",")) if len(sys.argv) > 2 else (4096,)
+    counts = tuple(int(v) for v in sys.argv[3].split(",")) if len(sys.argv) > 3 else (1, 2, 4, 8)
+    forms = tuple(sys.argv[4].split(",")) if len(sys.argv) > 4 else ("kernel", "copy")
+    for r in range(rounds):
+        for n in sizes:
+            for S in counts:
+                for form in forms if S > 1 else forms[:1]:
+                    os.environ["CGX_LOCAL_XCHG"] = form
+                    out = run(n, S)
+                    out["round"] = r
+                    print(json.dumps(out), flush=True)
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,5 @@
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+timeout -k 10 600 python -u -m pytest tests/test_gpu_solver.py -m gpu -x -q --timeout 300 --timeout-method thread > gpurun_out/r04_step1_tests.log 2>&1 || { tail -30 gpurun_out/r04_step1_tests.log; exit 1; }
+tail -3 gpurun_out/r04_step1_tests.log
+timeout -k 10 400 python -u tools/r04_multishard_floor.py 2 4096,65536 1,2,4,8 > gpurun_out/r04_floor_ab.jsonl
