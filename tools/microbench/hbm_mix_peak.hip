@@ -1,8 +1,10 @@
 // Empirical HBM ceiling for read/write stream mixes on one MI355X: NR input
 // and NW output vectors of `n` doubles, one contiguous grid-stride pass with
 // 16-B non-temporal loads and stores, 4 elements pairs per thread in flight.
-// The mixes are the Poisson kernels' (k_poisson_p: 2 reads + 1 write;
-// k_poisson_xr: 3 reads + 2 writes) and a plain copy (1 + 1).
+// The mixes are the Poisson kernels' (k_poisson_p and k_poisson_xr without
+// the x update: 2 reads + 1 write; k_poisson_xr with x every iteration: 3 + 2;
+// x every other iteration's catch-up: 4 + 2; every third's: 5 + 2) and a
+// plain copy (1 + 1).
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -o /tmp/hbm_mix_peak tools/microbench/hbm_mix_peak.hip
 //   /tmp/hbm_mix_peak [n = 67108864]
 #include <hip/hip_runtime.h>
@@ -24,7 +26,7 @@ typedef double d2 __attribute__((ext_vector_type(2)));
     } while (0)
 
 struct Bufs {
-    const d2 *in[3];
+    const d2 *in[5];
     d2 *out[2];
 };
 
@@ -83,7 +85,7 @@ int main(int argc, char **argv) {
     int cus = 0;
     CK(hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, 0));
     Bufs b;
-    for (int i = 0; i < 3; ++i) {
+    for (int i = 0; i < 5; ++i) {
         d2 *p = nullptr;
         CK(hipMalloc(&p, npairs * 16));
         CK(hipMemset(p, 0, npairs * 16));
@@ -95,10 +97,11 @@ int main(int argc, char **argv) {
     for (int bpc : {2, 4, 8}) {
         const int blocks = bpc * cus;
         const double c11 = run<1, 1>(b, npairs, blocks), c21 = run<2, 1>(b, npairs, blocks);
-        const double c32 = run<3, 2>(b, npairs, blocks);
+        const double c32 = run<3, 2>(b, npairs, blocks), c42 = run<4, 2>(b, npairs, blocks);
+        const double c52 = run<5, 2>(b, npairs, blocks);
         std::printf("%s{\"blocks_per_cu\": %d, \"read1_write1_GBps\": %.1f, \"read2_write1_GBps\": %.1f, "
-                    "\"read3_write2_GBps\": %.1f}",
-                    first ? "" : ", ", bpc, c11, c21, c32);
+                    "\"read3_write2_GBps\": %.1f, \"read4_write2_GBps\": %.1f, \"read5_write2_GBps\": %.1f}",
+                    first ? "" : ", ", bpc, c11, c21, c32, c42, c52);
         first = false;
     }
     std::printf("]}\n");
