@@ -4,7 +4,7 @@ the single-block p pass (k_update_xrp_f64), two launches with the p update
 folded into the matVec (CGX_FOLD_P=1); "_l2p": the same with round 2's
 matVec (p read through L2, CGX_MV_SMALL=0) instead of k_matvec_small_f64.  Fixed-count iterations, timed by
 the host around a synchronize, with the CGX_PHASES stamps alongside.
-  python tools/r03_floor.py [rounds] > profiles/r03_iteration_floor.jsonl"""
+  python tools/floor_small_n.py [rounds] > profiles/r03_iteration_floor.jsonl"""
 import json
 import os
 import sys

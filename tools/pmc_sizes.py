@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Summarise tools/r03_pmc_sizes.sh: per workload and kernel, the mean of
+"""Summarise tools/pmc_dram_bytes.sh: per workload and kernel, the mean of
 every counter over its launches and the bytes they imply, next to the
 kernel's algorithmic bytes per launch (where this file knows them).
 

@@ -4,7 +4,7 @@ eps 1e-10, device-gated) at the reference's sizes, round 3's default
 (folded iteration, LDS-staged matVec at 2048-8192 columns) against round 2's
 form (CGX_FOLD_P=0 CGX_MV_SMALL=0), interleaved in one process: median of 9
 solves each, the solve's own clock (cgx_stats.solve_ms).
-  python tools/r03_solve_latency.py [sizes...] > profiles/r03_solve_latency.jsonl"""
+  python tools/solve_latency_published.py [sizes...] > profiles/r03_solve_latency.jsonl"""
 import json
 import os
 import statistics
