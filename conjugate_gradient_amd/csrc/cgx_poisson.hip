@@ -474,6 +474,160 @@ __global__ __launch_bounds__(kNT) void k_poisson_xflush_f64(const double *__rest
     }
 }
 
+// ---- k_poisson_xr_f64, software-pipelined (CGX_XR_PIPE) ----------------------
+// The same arithmetic, row by row and item by item in the same order as
+// k_poisson_xr_f64 (so r, x and every r.r partial are the same bits), with
+// the loads of the next step -- or, at an item's last step, of the next
+// item's first step and its two prefix rows -- issued before this step's
+// arithmetic and stores.  In the plain kernel a step's loads go out only
+// after the previous step's stores, and the wait for its own last loads then
+// also waits for those stores (loads and stores share vmcnt on gfx9-class
+// parts): one store round trip per step.  Here every load and store is
+// unconditional, so the compiler's counts stay exact and no wait covers a
+// store.  For full strips only (m a multiple of 2 * kNT: every lane valid),
+// items of exactly NS * RBn rows (mloc a multiple of that), NT and HT on (the
+// defaults); the launcher falls back to k_poisson_xr_f64 otherwise.
+// Side points are loaded by every wave (wave-uniform addresses, clamped to
+// the grid): lanes 0 / 63 of waves 1-2 read them from LDS as before, so the
+// values used are unchanged; the extra loads hit lines the neighbouring wave
+// fetches anyway.
+template <int RBn, int XM>
+struct XrSet {
+    d2 pr[RBn], xv[RBn], po[RBn], pq[RBn], rv[RBn];
+    double el[RBn], er[RBn];
+};
+template <int RBn, int XM>
+__device__ __forceinline__ void xr_pipe_load(XrSet<RBn, XM> &S, const double *__restrict__ pnh,
+                                             const double *__restrict__ poh, const double *__restrict__ pqh,
+                                             const double *__restrict__ x, const double *__restrict__ r, int64_t m,
+                                             int64_t i, const StripLane &L, bool last) {
+    const int64_t cl = L.jw > 0 ? L.jw - 1 : 0, cr = L.jw + 128 < m ? L.jw + 128 : m - 1;
+#pragma unroll
+    for (int t = 0; t < RBn; ++t) {
+        const int64_t hc = (i + t + 1) * m, ic = (i + t) * m;
+        // the item's last two rows are the next item's first two (HT): default policy, kept in L2
+        S.pr[t] = (last && t >= RBn - 2) ? lds2<false>(pnh + hc + m, L.off) : lds2<true>(pnh + hc + m, L.off);
+        if constexpr (XM != 0) S.xv[t] = lds2<true>(x + ic, L.off);
+        if constexpr (XM >= 2) S.po[t] = lds2<true>(poh + hc, L.off);
+        if constexpr (XM == 3) S.pq[t] = lds2<true>(pqh + hc, L.off);
+        S.rv[t] = lds2<true>(r + ic, L.off);
+        S.el[t] = pnh[hc + cl];
+        S.er[t] = pnh[hc + cr];
+    }
+}
+template <int RBn, int XM>
+__device__ __forceinline__ void xr_pipe_step(const XrSet<RBn, XM> &S, double *__restrict__ x,
+                                             double *__restrict__ r, int64_t m, int64_t i, const StripLane &L,
+                                             double alpha, double alpha_prev, double alpha_prev2, d2 &pm, d2 &pc,
+                                             double &acc, double *eb) {
+    const int lane = threadIdx.x & 63;
+    d2 ce[RBn];
+#pragma unroll
+    for (int t = 0; t < RBn; ++t) ce[t] = t == 0 ? pc : S.pr[t - 1];
+    edges_put<RBn>(eb, L, ce);
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < RBn; ++t) {
+        const d2 up = t == 0 ? pm : (t == 1 ? pc : S.pr[t - 2]);
+        const d2 dn = S.pr[t];
+        const double lw = edge_l(eb, L, t, L.has_l ? S.el[t] : 0.0), rw = edge_r(eb, L, t, L.has_r ? S.er[t] : 0.0);
+        double l = __shfl_up(ce[t].y, 1, 64);
+        double rt = __shfl_down(ce[t].x, 1, 64);
+        l = lane == 0 ? lw : l;
+        rt = lane == 63 ? rw : rt;
+        d2 o;
+        o.x = 4.0 * ce[t].x - up.x - dn.x - l - ce[t].y;
+        o.y = 4.0 * ce[t].y - up.y - dn.y - ce[t].x - rt;
+        d2 xn, rn;
+        if constexpr (XM == 3) {
+            xn.x = __builtin_fma(alpha_prev2, S.pq[t].x, S.xv[t].x);
+            xn.y = __builtin_fma(alpha_prev2, S.pq[t].y, S.xv[t].y);
+            xn.x = __builtin_fma(alpha_prev, S.po[t].x, xn.x);
+            xn.y = __builtin_fma(alpha_prev, S.po[t].y, xn.y);
+            xn.x = __builtin_fma(alpha, ce[t].x, xn.x);
+            xn.y = __builtin_fma(alpha, ce[t].y, xn.y);
+        } else if constexpr (XM == 2) {
+            xn.x = __builtin_fma(alpha_prev, S.po[t].x, S.xv[t].x);
+            xn.y = __builtin_fma(alpha_prev, S.po[t].y, S.xv[t].y);
+            xn.x = __builtin_fma(alpha, ce[t].x, xn.x);
+            xn.y = __builtin_fma(alpha, ce[t].y, xn.y);
+        } else if constexpr (XM == 1) {
+            xn.x = __builtin_fma(alpha, ce[t].x, S.xv[t].x);
+            xn.y = __builtin_fma(alpha, ce[t].y, S.xv[t].y);
+        }
+        rn.x = __builtin_fma(-alpha, o.x, S.rv[t].x);
+        rn.y = __builtin_fma(-alpha, o.y, S.rv[t].y);
+        acc += rn.x * rn.x + rn.y * rn.y;
+        if constexpr (XM != 0) sts2<true>(x + (i + t) * m, L.off, xn);
+        sts2<true>(r + (i + t) * m, L.off, rn);
+    }
+    if constexpr (RBn >= 2) {
+        pm = S.pr[RBn - 2];
+        pc = S.pr[RBn - 1];
+    } else {
+        pm = pc;
+        pc = S.pr[0];
+    }
+}
+template <int RBn, int NS, int XM>
+__global__ __launch_bounds__(kNT) void k_poisson_xr_pipe_f64(const double *__restrict__ pnh,
+                                                             const double *__restrict__ poh,
+                                                             const double *__restrict__ pqh, double *__restrict__ x,
+                                                             double *__restrict__ r, int64_t m, int64_t nstrips,
+                                                             int64_t nitems, int reverse, const double *rsold,
+                                                             const double *pAp, double *rr_out, double *xalpha,
+                                                             double *partials, unsigned *ticket, const int64_t *gate,
+                                                             int bands) {
+    static_assert(RBn <= kEdgeRB && NS % 2 == 0, "edge buffer / set parity");
+    constexpr int64_t kRpi = RBn * NS;
+    __shared__ double edge[2 * kWaves * 2 * kEdgeRB];
+    if (gate && *gate) return;
+    const double alpha = cg_ratio(*rsold, *pAp);
+    const double alpha_prev = XM == 2 ? xalpha[0] : XM == 3 ? xalpha[1] : 0.0;
+    const double alpha_prev2 = XM == 3 ? xalpha[0] : 0.0;
+    double acc = 0.0;
+    const Band bd = bands ? band_of(0, nitems, nstrips, bands)
+                          : Band{0, nitems, (int64_t)gridDim.x, (int64_t)blockIdx.x, 0};
+    if (bd.start < bd.count) {
+        auto item_of = [&](int64_t v) { return band_item(bd, reverse ? bd.count - 1 - v : v); };
+        int64_t v = bd.start, w = item_of(v);
+        StripLane L = strip_lane(w, nstrips, m);
+        int64_t i0 = (w / nstrips) * kRpi;
+        d2 pm = lds2<false>(pnh + i0 * m, L.off), pc = lds2<false>(pnh + (i0 + 1) * m, L.off);
+        XrSet<RBn, XM> S[2];
+        xr_pipe_load<RBn, XM>(S[0], pnh, poh, pqh, x, r, m, i0, L, NS == 1);
+        for (;;) {
+            // the next item (the last one again when there is none: loaded, never used)
+            const int64_t vn = v + bd.stride < bd.count ? v + bd.stride : v;
+            const int64_t wn = item_of(vn);
+            const StripLane Ln = strip_lane(wn, nstrips, m);
+            const int64_t i0n = (wn / nstrips) * kRpi;
+            d2 pmn, pcn;
+#pragma unroll
+            for (int s = 0; s < NS; ++s) {
+                if (s + 1 < NS) {
+                    xr_pipe_load<RBn, XM>(S[(s + 1) & 1], pnh, poh, pqh, x, r, m, i0 + (s + 1) * RBn, L,
+                                          s + 2 == NS);
+                } else {
+                    pmn = lds2<false>(pnh + i0n * m, Ln.off);
+                    pcn = lds2<false>(pnh + (i0n + 1) * m, Ln.off);
+                    xr_pipe_load<RBn, XM>(S[(s + 1) & 1], pnh, poh, pqh, x, r, m, i0n, Ln, NS == 1);
+                }
+                xr_pipe_step<RBn, XM>(S[s & 1], x, r, m, i0 + s * RBn, L, alpha, alpha_prev, alpha_prev2, pm, pc, acc,
+                                      edge + (s & 1) * (kWaves * 2 * kEdgeRB));
+            }
+            if (vn == v) break;
+            v = vn;
+            L = Ln;
+            i0 = i0n;
+            pm = pmn;
+            pc = pcn;
+        }
+    }
+    if (XM == 0 && blockIdx.x == 0 && threadIdx.x == 0) *xalpha = alpha;
+    grid_sum_last_block(acc, partials, ticket, rr_out);
+}
+
 __global__ __launch_bounds__(kNT) void k_stencil5_rows_f64(const double *__restrict__ ph, int64_t mloc, int64_t m,
                                                            double *__restrict__ Ap, double *dot_out, double *partials,
                                                            unsigned *ticket, const int64_t *gate) {
@@ -616,9 +770,17 @@ static void launch_poisson_xr(const PoissonPlan &pl, hipStream_t s, const double
     int64_t grid = resident_grid(reinterpret_cast<const void *>(fg), pl.nitems);
     const int bands = pl.bands && grid >= 8 ? 1 + pl.band_rot : 0;
     if (bands) grid &= ~int64_t(7);
+    const int reverse = env_int("CGX_STENCIL_REVERSE", 1);
+    // the software-pipelined kernel: full strips, 8-row items, NT + HT (same bits, same grid)
+    const int pipe_rb = env_int("CGX_XR_PIPE", 0);
+    if ((pipe_rb == 2 || pipe_rb == 4) && m % (2 * kNT) == 0 && pl.rpi == 8 && mloc % 8 == 0 && pl.nt && pl.ht) {
+        auto fp = pipe_rb == 2 ? k_poisson_xr_pipe_f64<2, 4, XM> : k_poisson_xr_pipe_f64<4, 2, XM>;
+        hipLaunchKernelGGL(fp, dim3((unsigned)grid), dim3(kNT), 0, s, pnh, poh, pqh, x, r, m, pl.nstrips, pl.nitems,
+                           reverse, rsold, pAp, rr_out, xalpha, ws.partials, ws.tickets + T_XR, gate, bands);
+        return;
+    }
     hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(kNT), 0, s, pnh, poh, pqh, x, r, mloc, m, pl.nstrips, pl.rpi,
-                       pl.nitems, env_int("CGX_STENCIL_REVERSE", 1), rsold, pAp, rr_out, xalpha, ws.partials,
-                       ws.tickets + T_XR, gate, bands);
+                       pl.nitems, reverse, rsold, pAp, rr_out, xalpha, ws.partials, ws.tickets + T_XR, gate, bands);
 }
 
 hipError_t poisson_p_f64(const double *rh, const double *poh, double *pnh, int64_t mloc, int64_t m, const double *rr,

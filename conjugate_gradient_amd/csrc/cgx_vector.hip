@@ -470,12 +470,24 @@ __global__ void k_sum_ordered(const T *in, int cnt, int stride, int mpich, T *ou
     *out = v[0];
 }
 
+// The pull kernels of the one-process multi-shard exchange read other
+// shards' memory -- on distinct devices, peer memory over xGMI, which this
+// device's L2 may hold from an earlier iteration's read of the same address.
+// So every such read is a system-scope load (sc0 sc1: served coherently, not
+// from a stale L2 line); the producers' event records carry the system-scope
+// release that wrote their data back.  On one device these are plain loads'
+// worth of traffic (512 KB of p per iteration at N = 65536).
+template <typename T>
+__device__ __forceinline__ T load_sys(const T *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
 // The same combines over a table of peer pointers (one partial per shard).
 template <typename T>
 __global__ void k_combine_peers(PeerTable src, int cnt, int mpich, T *out) {
 #pragma clang fp contract(off)
     T in[kMaxPeers];
-    for (int q = 0; q < cnt; ++q) in[q] = *reinterpret_cast<const T *>(src.p[q]);
+    for (int q = 0; q < cnt; ++q) in[q] = load_sys(reinterpret_cast<const T *>(src.p[q]));
     if (!mpich) {
         T s = in[0];
         for (int q = 1; q < cnt; ++q) s = s + in[q];
@@ -492,10 +504,10 @@ __global__ void k_combine_peers(PeerTable src, int cnt, int mpich, T *out) {
     *out = v[0];
 }
 
-// blockIdx.y = the source slice; each thread moves kGU words of W bytes per
-// pass with all its loads issued before the stores (remote reads over xGMI
-// are latency-bound: keep many in flight).
-constexpr int kGU = 4;
+// blockIdx.y = the source slice; each thread moves kGU words of W (8 or 4)
+// bytes per pass with all its loads issued before the stores (remote reads
+// over xGMI are latency-bound: keep many in flight).
+constexpr int kGU = 8;
 template <typename W>
 __global__ __launch_bounds__(kNT) void k_gather_slices(PeerTable src, int skip, int64_t words, char *dst) {
     const int q = blockIdx.y;
@@ -507,7 +519,7 @@ __global__ __launch_bounds__(kNT) void k_gather_slices(PeerTable src, int skip, 
         W v[kGU];
 #pragma unroll
         for (int u = 0; u < kGU; ++u)
-            if (base + u * kNT < words) v[u] = in[base + u * kNT];
+            if (base + u * kNT < words) v[u] = load_sys(in + base + u * kNT);
 #pragma unroll
         for (int u = 0; u < kGU; ++u)
             if (base + u * kNT < words) out[base + u * kNT] = v[u];
@@ -519,19 +531,14 @@ __global__ __launch_bounds__(kNT) void k_gather_slices(PeerTable src, int skip, 
 hipError_t gather_slices(const PeerTable &src, int cnt, int skip, int64_t slice_bytes, char *dst, hipStream_t s) {
     if (cnt < 1 || cnt > kMaxPeers || slice_bytes < 0 || (slice_bytes & 3)) return hipErrorInvalidValue;
     if (slice_bytes == 0) return hipSuccess;
-    bool a16 = (slice_bytes % 16) == 0 && (reinterpret_cast<uintptr_t>(dst) % 16) == 0;
     bool a8 = (slice_bytes % 8) == 0 && (reinterpret_cast<uintptr_t>(dst) % 8) == 0;
-    for (int q = 0; q < cnt; ++q) {
-        a16 = a16 && (reinterpret_cast<uintptr_t>(src.p[q]) % 16) == 0;
-        a8 = a8 && (reinterpret_cast<uintptr_t>(src.p[q]) % 8) == 0;
-    }
-    const int64_t wb = a16 ? 16 : a8 ? 8 : 4, words = slice_bytes / wb;
+    for (int q = 0; q < cnt; ++q) a8 = a8 && (reinterpret_cast<uintptr_t>(src.p[q]) % 8) == 0;
+    const int64_t wb = a8 ? 8 : 4, words = slice_bytes / wb;
     const int64_t per_block = (int64_t)kNT * kGU;
     const unsigned gx = (unsigned)std::min<int64_t>((words + per_block - 1) / per_block, 64);
     const dim3 grid(gx, (unsigned)cnt);
-    if (a16) hipLaunchKernelGGL(k_gather_slices<uint4>, grid, dim3(kNT), 0, s, src, skip, words, dst);
-    else if (a8) hipLaunchKernelGGL(k_gather_slices<uint2>, grid, dim3(kNT), 0, s, src, skip, words, dst);
-    else hipLaunchKernelGGL(k_gather_slices<unsigned>, grid, dim3(kNT), 0, s, src, skip, words, dst);
+    if (a8) hipLaunchKernelGGL(k_gather_slices<uint64_t>, grid, dim3(kNT), 0, s, src, skip, words, dst);
+    else hipLaunchKernelGGL(k_gather_slices<uint32_t>, grid, dim3(kNT), 0, s, src, skip, words, dst);
     return hipGetLastError();
 }
 

@@ -861,6 +861,26 @@ def test_poisson_x_every_other_iteration_is_bitwise(monkeypatch, m, shards, peri
     assert rel(a["solve1"][0], xo) <= TOL
 
 
+@pytest.mark.parametrize("rb", ["2", "4"])
+@pytest.mark.parametrize("period", ["0", "3"])
+@pytest.mark.parametrize("m,shards", [(1024, None), (1024, [0, 0]), (512, [0] * 4)])
+def test_poisson_xr_pipelined_kernel_is_bitwise(monkeypatch, m, shards, period, rb):
+    """The software-pipelined k_poisson_xr_pipe_f64 (CGX_XR_PIPE = rows per
+    step; full 512-column strips, 8-row items) does k_poisson_xr_f64's
+    arithmetic row by row and item by item in the same order on the same grid:
+    x and the loop counts are bit for bit the plain kernel's after every way a
+    solve can end, with x every iteration and every third iteration."""
+    monkeypatch.setenv("CGX_POISSON_FUSED", "1")
+    monkeypatch.setenv("CGX_XR_PIPE", rb)
+    a = _poisson_x_runs(m, shards, period, monkeypatch)
+    monkeypatch.setenv("CGX_XR_PIPE", "0")
+    b = _poisson_x_runs(m, shards, period, monkeypatch)
+    assert a.keys() == b.keys()
+    for key in a:
+        assert np.array_equal(a[key][0], b[key][0]), key
+        assert a[key][1:] == b[key][1:], key
+
+
 def test_poisson_fused_in_pieces_and_iteration_cap():
     """Iterations issued in several cgx_iterate calls (fixed count, then
     convergence-tested) give the one-call solve; a cap that stops exactly at
