@@ -43,8 +43,9 @@
  * Multi-GPU: the matrix is split into contiguous row blocks (parallel_cg.c:83,
  * 97-99; n % nranks == 0 as parallel_cg.c:86-90 requires).  Per iteration
  * the p vector is allgathered and the two scalars p.Ap and r.r are
- * allreduced (RCCL over xGMI in rank mode; intra-process device copies for
- * the multi-shard mode).  x stays distributed and is gathered on demand.
+ * allreduced (RCCL over xGMI in rank mode; in the multi-shard mode one pull
+ * kernel per consuming row block reads the other blocks' slices / partials
+ * through peer pointers).  x stays distributed and is gathered on demand.
  */
 #ifndef CGX_H
 #define CGX_H
@@ -125,7 +126,8 @@ extern "C" {
 #define CGX_PEER_ACTIVE  0x20000 /* reported in cgx_info.flags: a multi-shard
                                     context spans distinct devices and peer
                                     access is enabled between every pair of
-                                    them (device copies then go over xGMI) */
+                                    them (the exchange kernels then read
+                                    peers' memory over xGMI) */
 #define CGX_SMALL_ACTIVE 0x40000 /* reported in cgx_info.flags: one GPU, one
                                     resident fp64 row block of 2048..8192
                                     columns -- the matVec stages the vector in
@@ -234,7 +236,10 @@ int cgx_device_link(int device_a, int device_b, int *link_type, int *hops, int *
 int cgx_create(cgx_ctx **ctx, int64_t n, int device, int flags);
 
 /* One process driving `nshards` row blocks on devices[0..nshards-1] (a device
- * may repeat: several row blocks on one GPU).  Exchange by device copies. */
+ * may repeat: several row blocks on one GPU).  Exchange by pull kernels on
+ * each consuming block's stream: one gather of p (k_gather_slices), one
+ * rank-order combine per scalar (k_combine_peers); CGX_LOCAL_XCHG=copy:
+ * one hipMemcpyPeerAsync per block pair instead (the same bits). */
 int cgx_create_multi(cgx_ctx **ctx, int64_t n, int nshards, const int *devices, int flags);
 
 /* One process per GPU (parallel_cg.c's one MPI rank per process): this
