@@ -291,6 +291,11 @@ struct cgx_ctx {
     // (CGX_LOCAL_XCHG=copy): one hipMemcpyPeerAsync per (consumer, producer)
     // pair, round 3's form, kept for A/B runs
     bool xchg_kernels = true;
+    // ... and, for the dense fp64 iteration, the two scalar combines folded
+    // into the kernels that consume them (k_update_r_f64 sums the p.Ap
+    // partials, k_update_xp_f64 the r.r partials: PeerSum), so an iteration
+    // launches no combine kernel (CGX_LOCAL_FUSE=0: separate combine kernels)
+    bool fuse_combine = false;
     // CGX_PHASES: resolved per-iteration phase durations (us), cgx_phase_times' order;
     // the wall clock's rate, and the previous stamped iteration's first start /
     // last end (ticks; 0 = none) so the gap across a resolve is still measured
@@ -350,6 +355,7 @@ int p2p_allgather(cgx_ctx *c, bool from_x);
 int p2p_scalar(cgx_ctx *c, int lslot, int gslot);
 int exchange_allgather(cgx_ctx *c, bool from_x);
 int exchange_scalar(cgx_ctx *c, int lslot, int gslot);
+PeerSum peer_sum(const cgx_ctx *c, const Shard &d, int lslot, int gslot);
 int overlapped_matvec(cgx_ctx *c, int dot_slot, bool gated);
 int exchange_halo_async(cgx_ctx *c);
 int settle_halo(cgx_ctx *c);

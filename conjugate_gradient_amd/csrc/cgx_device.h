@@ -29,6 +29,32 @@ constexpr int kNT = 256;  // threads per block for the fp64 kernels
 // lambda_min |p|^2 ~ lambda_min r.r, nonzero while r.r is normal.)
 // CGX_F32_REF keeps the reference's float division as it is
 // (serialConjugate.c:220,239).
+// A system-scope load (sc0 sc1): coherent with another device's writes made
+// visible by its system-scope release (the one-process multi-shard exchange
+// reads peers' memory this way; cgx_kernels.h PeerTable).
+template <typename T>
+__device__ __forceinline__ T load_sys(const T *p) {
+    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
+}
+
+// PeerSum (cgx_kernels.h): the cnt partials in rank order, computed by thread
+// 0 of every block and shared through LDS; block 0 stores it for later use.
+// Every thread of the block must call it (it has a barrier).
+__device__ __forceinline__ double peer_sum_block(const PeerSum &c) {
+#pragma clang fp contract(off)
+    __shared__ double sh;
+    if (threadIdx.x == 0) {
+        double in[kMaxPeers];
+        for (int q = 0; q < c.cnt; ++q) in[q] = load_sys(reinterpret_cast<const double *>(c.src.p[q]));
+        double v = in[0];
+        for (int q = 1; q < c.cnt; ++q) v = v + in[q];
+        sh = v;
+        if (blockIdx.x == 0) *c.out = v;
+    }
+    __syncthreads();
+    return sh;
+}
+
 __device__ __forceinline__ double cg_ratio(double num, double den) {
     return (den != 0.0 || !(__builtin_fabs(num) < 0x1p-1022)) ? num / den : 0.0;
 }

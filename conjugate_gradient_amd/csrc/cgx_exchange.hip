@@ -367,6 +367,17 @@ int exchange_allgather(cgx_ctx *c, bool from_x) {
     return CGX_OK;
 }
 
+// The combine folded into the consuming kernel (c->fuse_combine): the table
+// of every shard's partial in `lslot`, summed into shard d's `gslot`.  The
+// caller has ordered d's stream after every producer (local_barrier).
+PeerSum peer_sum(const cgx_ctx *c, const Shard &d, int lslot, int gslot) {
+    PeerSum ps{};
+    ps.src = peer_table(c, &Shard::scal, 8 * (int64_t)lslot);
+    ps.cnt = (int)c->sh.size();
+    ps.out = reinterpret_cast<double *>(slot(d, gslot));
+    return ps;
+}
+
 // Combine the per-shard partials in slot `lslot` into the global slot `gslot`.
 int exchange_scalar(cgx_ctx *c, int lslot, int gslot) {
     if (c->mode == M_SINGLE) return CGX_OK;  // kernels wrote the global slot directly

@@ -479,9 +479,15 @@ int do_iteration(cgx_ctx *c, double eps, int *stop, bool gated) {
             TRY(launch_matvec(c, s, s.pfull, true, out_slot(c, pl, pg), gated));  // :215 / :292-293
         }
     }
-    TRY(exchange_scalar(c, pl, pg));  // MPI_Allreduce(p.Ap)  parallel_cg.c:294
+    // MPI_Allreduce(p.Ap)  parallel_cg.c:294 -- multi-shard fp64: summed by
+    // k_update_r_f64 itself after the barrier (fuse_combine)
+    if (c->fuse_combine) TRY(local_barrier(c));
+    else TRY(exchange_scalar(c, pl, pg));
     const int rg = S_RR + ring(k + 1), rl = S_LRR + ring(k + 1);
     const int ro = out_slot(c, rl, rg);
+    // the r.r combine folds into k_update_xp_f64 unless the host reads r.r
+    // first (host-checked convergence)
+    const bool fuse_rr = c->fuse_combine && (gated || eps < 0.0);
     for (auto &s : c->sh) {
         TRY(set_dev(s));
         if (f32ref(c)) {
@@ -493,13 +499,15 @@ int do_iteration(cgx_ctx *c, double eps, int *stop, bool gated) {
                                        reinterpret_cast<float *>(slot(s, ro)), s.stream, gate_of(s, gated)));
         } else {
             // r -= alpha Ap, r.r; x's update is deferred into the p update
+            const PeerSum ps = c->fuse_combine ? peer_sum(c, s, pl, pg) : PeerSum{};
             HIPT(update_r_f64(s.nloc, reinterpret_cast<double *>(s.r), reinterpret_cast<const double *>(s.Ap),
                               reinterpret_cast<const double *>(slot(s, S_RR + ring(k))),
                               reinterpret_cast<const double *>(slot(s, pg)), reinterpret_cast<double *>(slot(s, ro)),
-                              s.ws, s.stream, gate_of(s, gated), ts_of(c, s, TK_UR)));
+                              s.ws, s.stream, gate_of(s, gated), ts_of(c, s, TK_UR), c->fuse_combine ? &ps : nullptr));
         }
     }
-    TRY(exchange_scalar(c, rl, rg));  // MPI_Allreduce(r.r)  parallel_cg.c:313
+    if (fuse_rr) TRY(local_barrier(c));  // MPI_Allreduce(r.r)  parallel_cg.c:313, summed by k_update_xp_f64
+    else TRY(exchange_scalar(c, rl, rg));
     c->k = k + 1;
     c->total_iters += 1;
     if (gated) {  // x (+ p unless converged) on the device, stopping rule decided there
@@ -513,6 +521,7 @@ int do_iteration(cgx_ctx *c, double eps, int *stop, bool gated) {
                                       reinterpret_cast<double *>(slot(s, S_RRFINAL)), rec_of(c, s, gated)));
                 continue;
             }
+            const PeerSum ps = fuse_rr ? peer_sum(c, s, rl, rg) : PeerSum{};
             HIPT(update_xp_f64(s.nloc, reinterpret_cast<double *>(s.x), reinterpret_cast<double *>(s.pown),
                                reinterpret_cast<const double *>(s.r),
                                reinterpret_cast<const double *>(slot(s, S_RR + ring(k))),
@@ -520,7 +529,7 @@ int do_iteration(cgx_ctx *c, double eps, int *stop, bool gated) {
                                reinterpret_cast<const double *>(slot(s, rg)), s.stream, eps, k,
                                reinterpret_cast<int64_t *>(slot(s, S_KDONE)),
                                reinterpret_cast<double *>(slot(s, S_RRFINAL)), rec_of(c, s, gated),
-                               ts_of(c, s, TK_UXP)));
+                               ts_of(c, s, TK_UXP), fuse_rr ? &ps : nullptr));
         }
         phase_iter_end(c);
         return CGX_OK;
@@ -552,13 +561,15 @@ int do_iteration(cgx_ctx *c, double eps, int *stop, bool gated) {
             HIPT(update_p_ref_f32(s.nloc, reinterpret_cast<float *>(s.pown),
                                   reinterpret_cast<const float *>(s.r), reinterpret_cast<const float *>(slot(s, rg)),
                                   reinterpret_cast<const float *>(slot(s, S_RR + ring(k))), s.stream));
-        else  // x += alpha p (deferred from the r update), then p = r + beta p
+        else {  // x += alpha p (deferred from the r update), then p = r + beta p
+            const PeerSum ps = fuse_rr ? peer_sum(c, s, rl, rg) : PeerSum{};
             HIPT(update_xp_f64(s.nloc, reinterpret_cast<double *>(s.x), reinterpret_cast<double *>(s.pown),
                                reinterpret_cast<const double *>(s.r),
                                reinterpret_cast<const double *>(slot(s, S_RR + ring(k))),
                                reinterpret_cast<const double *>(slot(s, pg)),
                                reinterpret_cast<const double *>(slot(s, rg)), s.stream, -1.0, 0, nullptr, nullptr,
-                               nullptr, ts_of(c, s, TK_UXP)));
+                               nullptr, ts_of(c, s, TK_UXP), fuse_rr ? &ps : nullptr));
+        }
     }
     phase_iter_end(c);
     return CGX_OK;

@@ -17,6 +17,38 @@ constexpr int kMaxCombine = 64;
 constexpr int kTickets = 8;
 enum Ticket { T_MATVEC = 0, T_RESID = 1, T_XR = 2, T_DOT = 3, T_REF_MV = 4 };
 
+// ---- the multi-shard exchange in one process (several row blocks, LOCAL) ---
+// Pointers to every shard's copy of something (its p slice, its scalar slot),
+// in shard order; passed by value.  On distinct devices they are peer
+// pointers (access enabled at context creation): the kernels below run on the
+// CONSUMING shard's stream and only read peers' memory -- the same pull a
+// hipMemcpyPeerAsync on that stream does -- after the stream has waited for
+// the producers' events.
+constexpr int kMaxPeers = 32;
+struct PeerTable {
+    const char *p[kMaxPeers];
+};
+// dst[q * slice_bytes ...] = src.p[q][0 .. slice_bytes) for every q < cnt
+// except q == skip (the consumer's own slice, already in place; skip < 0
+// copies every slice): the allgather of p (or of x) in one launch instead of
+// cnt - 1 peer copies.
+hipError_t gather_slices(const PeerTable &src, int cnt, int skip, int64_t slice_bytes, char *dst, hipStream_t s);
+// *out = the cnt partials src.p[q] (fp64), summed in q order: the rank-order
+// combine of exchange_scalar read straight from each shard's slot.
+hipError_t combine_peers_f64(const PeerTable &src, int cnt, double *out, hipStream_t s);
+// F32_REF: the float partials in rank order or (mpich) MPICH's MPI_Allreduce order.
+hipError_t combine_peers_f32(const PeerTable &src, int cnt, float *out, hipStream_t s, bool mpich);
+// The fp64 combine folded into the kernel that consumes the scalar (no
+// launch of its own): every block sums the cnt partials src.p[q] in q order
+// (k_combine_peers' sum, so the same bits) and uses it in place of the
+// global slot; block 0 also stores it to *out (the global slot) for later
+// kernels and the host.  cnt = 0: none (the kernel reads the slot).
+struct PeerSum {
+    PeerTable src;
+    int cnt;
+    double *out;
+};
+
 // CGX_PHASES in-kernel timestamps: a kernel given `ts` stores block 0's entry
 // time in ts[0] and block b's exit time in ts[1 + b] (b < kTsMaxBlocks), on
 // the device's constant wall clock (hipDeviceAttributeWallClockRate).  No
@@ -80,7 +112,7 @@ hipError_t update_p_f64(int64_t n, double *p, const double *r, const double *rr,
 // once *kdone is in (0, k] both kernels (update_r via gate) do nothing.
 hipError_t update_r_f64(int64_t n, double *r, const double *Ap, const double *rsold, const double *pAp,
                         double *rr_out, const RedWs &ws, hipStream_t s, const int64_t *gate = nullptr,
-                        int64_t *ts = nullptr);
+                        int64_t *ts = nullptr, const PeerSum *pap_sum = nullptr);
 // The two-launch iteration's update (one GPU, small n): x += alpha p;
 // r -= alpha Ap; *rr_out = r.r; then (last block) the stopping decision as
 // update_xp's, and unless stopped p = r + (*rr_out / *rsold) p.
@@ -103,7 +135,7 @@ hipError_t update_xr_stop_f64(int64_t n, double *x, double *r, const double *p, 
 hipError_t update_xp_f64(int64_t n, double *x, double *p, const double *r, const double *rsold, const double *pAp,
                          const double *rr, hipStream_t s, double eps = -1.0, int64_t k = 0,
                          int64_t *kdone = nullptr, double *rrfinal = nullptr, int64_t *hrec = nullptr,
-                         int64_t *ts = nullptr);
+                         int64_t *ts = nullptr, const PeerSum *rr_sum = nullptr);
 hipError_t dot_f64(int64_t n, const double *a, const double *b, double *out,
                    const RedWs &ws, hipStream_t s);
 // Rows [row0, row0+nrows) of the counter-hash SPD system; pad columns zeroed.
@@ -112,27 +144,6 @@ hipError_t gen_spd_f64(int64_t n, int64_t lda, int64_t row0, int64_t nrows, uint
 // out = sum_{q<cnt} (8-byte slot q of in), in q order (one thread): rank-ordered combine.
 hipError_t sum_ordered_f64(const double *in, int cnt, double *out, hipStream_t s);
 
-// ---- the multi-shard exchange in one process (several row blocks, LOCAL) ---
-// Pointers to every shard's copy of something (its p slice, its scalar slot),
-// in shard order; passed by value.  On distinct devices they are peer
-// pointers (access enabled at context creation): the kernels below run on the
-// CONSUMING shard's stream and only read peers' memory -- the same pull a
-// hipMemcpyPeerAsync on that stream does -- after the stream has waited for
-// the producers' events.
-constexpr int kMaxPeers = 32;
-struct PeerTable {
-    const char *p[kMaxPeers];
-};
-// dst[q * slice_bytes ...] = src.p[q][0 .. slice_bytes) for every q < cnt
-// except q == skip (the consumer's own slice, already in place; skip < 0
-// copies every slice): the allgather of p (or of x) in one launch instead of
-// cnt - 1 peer copies.
-hipError_t gather_slices(const PeerTable &src, int cnt, int skip, int64_t slice_bytes, char *dst, hipStream_t s);
-// *out = the cnt partials src.p[q] (fp64), summed in q order: the rank-order
-// combine of exchange_scalar read straight from each shard's slot.
-hipError_t combine_peers_f64(const PeerTable &src, int cnt, double *out, hipStream_t s);
-// F32_REF: the float partials in rank order or (mpich) MPICH's MPI_Allreduce order.
-hipError_t combine_peers_f32(const PeerTable &src, int cnt, float *out, hipStream_t s, bool mpich);
 
 // 5-point Poisson A.p on a slab of mloc grid rows of width m; ph has one halo
 // row above and below.  *dot_out = ph[m..] . Ap when dot_out != nullptr.

@@ -357,6 +357,9 @@ int finish_create(cgx_ctx *c, cgx_ctx **out) {
     {
         const char *e = std::getenv("CGX_LOCAL_XCHG");
         c->xchg_kernels = !(e && !std::strcmp(e, "copy"));
+        const char *f = std::getenv("CGX_LOCAL_FUSE");
+        c->fuse_combine = c->mode == M_LOCAL && c->xchg_kernels && !(f && *f == '0') && !(c->flags & CGX_F32_REF) &&
+                          !(c->flags & CGX_COMM_P2P) && c->op == OP_DENSE && (int)c->sh.size() <= kMaxPeers;
     }
     c->overlap = can_overlap(c);
     c->fused_p = can_fuse_p(c);

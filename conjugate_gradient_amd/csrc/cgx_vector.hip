@@ -297,10 +297,10 @@ template <bool VEC, int VP = 2>
 __global__ __launch_bounds__(kNT) void k_update_r_f64(int64_t n, double *__restrict__ r, const double *__restrict__ Ap,
                                                       const double *rsold, const double *pAp, double *rr_out,
                                                       double *partials, unsigned *ticket, const int64_t *gate,
-                                                      int64_t *ts) {
+                                                      int64_t *ts, PeerSum pap_sum) {
     if (gate && *gate) return;
     ts_start(ts);
-    const double alpha = cg_ratio(*rsold, *pAp);
+    const double alpha = cg_ratio(*rsold, pap_sum.cnt ? peer_sum_block(pap_sum) : *pAp);
     double acc = 0.0;
     if constexpr (VEC) {
         CGX_VEC_LOOP_BEGIN
@@ -342,12 +342,13 @@ template <bool VEC, int VP = 2>
 __global__ __launch_bounds__(kNT) void k_update_xp_f64(int64_t n, double *__restrict__ x, double *__restrict__ p,
                                                        const double *__restrict__ r, const double *rsold,
                                                        const double *pAp, const double *rr, ConvArgs cv,
-                                                       int64_t *ts) {
+                                                       int64_t *ts, PeerSum rr_sum) {
     bool upd_p = rr != nullptr;
+    if (cv.kdone && *cv.kdone != 0 && *cv.kdone <= cv.k) return;
+    // the r.r combine folded in (multi-shard): every block sums the partials
+    const double rrv = rr_sum.cnt ? peer_sum_block(rr_sum) : rr ? *rr : 0.0;
     if (cv.kdone) {
-        const int64_t kd = *cv.kdone;
-        if (kd != 0 && kd <= cv.k) return;
-        const double rrn = *rr;
+        const double rrn = rrv;
         if (cv.eps >= 0.0 && sqrt(rrn) < cv.eps) {
             upd_p = false;
             if (blockIdx.x == 0 && threadIdx.x == 0) record_convergence(cv, cv.k + 1, rrn);
@@ -355,7 +356,7 @@ __global__ __launch_bounds__(kNT) void k_update_xp_f64(int64_t n, double *__rest
     }
     ts_start(ts);
     const double alpha = cg_ratio(*rsold, *pAp);
-    const double beta = upd_p ? cg_ratio(*rr, *rsold) : 0.0;
+    const double beta = upd_p ? cg_ratio(rrv, *rsold) : 0.0;
     if constexpr (VEC) {
         CGX_VEC_LOOP_BEGIN
         d2 xv[kVU], pv[kVU], rv[kVU];
@@ -476,11 +477,8 @@ __global__ void k_sum_ordered(const T *in, int cnt, int stride, int mpich, T *ou
 // So every such read is a system-scope load (sc0 sc1: served coherently, not
 // from a stale L2 line); the producers' event records carry the system-scope
 // release that wrote their data back.  On one device these are plain loads'
-// worth of traffic (512 KB of p per iteration at N = 65536).
-template <typename T>
-__device__ __forceinline__ T load_sys(const T *p) {
-    return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
-}
+// worth of traffic (512 KB of p per iteration at N = 65536).  (load_sys:
+// cgx_device.h.)
 
 // The same combines over a table of peer pointers (one partial per shard).
 template <typename T>
@@ -585,10 +583,13 @@ hipError_t update_p_f64(int64_t n, double *p, const double *r, const double *rr,
 }
 
 hipError_t update_r_f64(int64_t n, double *r, const double *Ap, const double *rsold, const double *pAp,
-                        double *rr_out, const RedWs &ws, hipStream_t s, const int64_t *gate, int64_t *ts) {
+                        double *rr_out, const RedWs &ws, hipStream_t s, const int64_t *gate, int64_t *ts,
+                        const PeerSum *pap_sum) {
     const bool vec = al16(r) && al16(Ap);
+    PeerSum ps{};
+    if (pap_sum) ps = *pap_sum;
     hipLaunchKernelGGL(vec ? k_update_r_f64<true> : k_update_r_f64<false>, dim3(grid_vec(n)), dim3(kNT), 0, s, n, r,
-                       Ap, rsold, pAp, rr_out, ws.partials, ws.tickets + T_XR, gate, ts);
+                       Ap, rsold, pAp, rr_out, ws.partials, ws.tickets + T_XR, gate, ts, ps);
     return hipGetLastError();
 }
 
@@ -626,8 +627,10 @@ hipError_t update_xr_stop_f64(int64_t n, double *x, double *r, const double *p, 
 
 hipError_t update_xp_f64(int64_t n, double *x, double *p, const double *r, const double *rsold, const double *pAp,
                          const double *rr, hipStream_t s, double eps, int64_t k, int64_t *kdone, double *rrfinal,
-                         int64_t *hrec, int64_t *ts) {
+                         int64_t *hrec, int64_t *ts, const PeerSum *rr_sum) {
     const bool vec = al16(x) && al16(p) && al16(r);
+    PeerSum ps{};
+    if (rr_sum) ps = *rr_sum;
     ConvArgs cv;
     cv.eps = eps;
     cv.k = k;
@@ -635,7 +638,7 @@ hipError_t update_xp_f64(int64_t n, double *x, double *p, const double *r, const
     cv.rrfinal = rrfinal;
     cv.hrec = hrec;
     hipLaunchKernelGGL(vec ? k_update_xp_f64<true> : k_update_xp_f64<false>, dim3(grid_vec(n)), dim3(kNT), 0, s, n, x,
-                       p, r, rsold, pAp, rr, cv, ts);
+                       p, r, rsold, pAp, rr, cv, ts, ps);
     return hipGetLastError();
 }
 

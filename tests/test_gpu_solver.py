@@ -101,12 +101,13 @@ def test_f32ref_shards_bit_exact_vs_mpi_reference(key):
 @pytest.mark.parametrize("kind", ["f64", "f64_nooverlap", "f32ref"])
 def test_local_exchange_kernels_bitwise_equal_peer_copies(monkeypatch, kind, P):
     """The multi-shard exchange in one process: the pull kernels (one gather
-    kernel and one combine kernel per consuming shard, the default) move the
-    same bytes and add the same partials in the same order as round 3's
+    kernel per consuming shard; the scalar combines folded into the update
+    kernels, the default, or one combine kernel each, CGX_LOCAL_FUSE=0) move
+    the same bytes and add the same partials in the same order as round 3's
     per-pair peer copies (CGX_LOCAL_XCHG=copy): x bit for bit, the same loop
-    count -- with the overlapped gather, the plain one (3 shards: 2048/3 is no
-    multiple of 128 rows; CGX_NO_OVERLAP), the x0 allgather of a nonzero x0,
-    and F32_REF's MPICH-order combine."""
+    count -- gated and fixed-count, with the overlapped gather, the plain one
+    (3 shards: 2049/3 rows; CGX_NO_OVERLAP), the x0 allgather of a nonzero x0,
+    and F32_REF's MPICH-order combine (never folded)."""
     n = 2048 if P != 3 else 2049
     f32 = kind == "f32ref"
     dt = np.float32 if f32 else np.float64
@@ -114,8 +115,9 @@ def test_local_exchange_kernels_bitwise_equal_peer_copies(monkeypatch, kind, P):
     x0 = np.full(n, 0.125, dt)
     flags = cg.CGX_F32_REF if f32 else cg.CGX_F64 | (cg.CGX_NO_OVERLAP if kind == "f64_nooverlap" else 0)
     res = {}
-    for form in ("kernel", "copy"):
-        monkeypatch.setenv("CGX_LOCAL_XCHG", form)
+    for form in ("kernel", "nofuse", "copy"):  # nofuse: a combine kernel per scalar instead of the folded sums
+        monkeypatch.setenv("CGX_LOCAL_XCHG", "copy" if form == "copy" else "kernel")
+        monkeypatch.setenv("CGX_LOCAL_FUSE", "0" if form == "nofuse" else "1")
         with cg.Solver(n, flags=flags, devices=[0] * P) as s:
             if kind == "f64" and P in (2, 8):
                 assert s.info.flags & cg.CGX_OVERLAP_ACTIVE
@@ -123,9 +125,17 @@ def test_local_exchange_kernels_bitwise_equal_peer_copies(monkeypatch, kind, P):
             x, st = s.solve(None, eps=1e-6 if f32 else 1e-10)
             xf, stf = s.solve(x0, eps=-1.0, max_iter=7)
             rn, bn = s.residual_norm()
-        res[form] = (x, st.iterations, xf, rn)
-    (xk, itk, xfk, rnk), (xc, itc, xfc, rnc) = res["kernel"], res["copy"]
-    assert itk == itc and np.array_equal(xk, xc) and np.array_equal(xfk, xfc) and rnk == rnc
+            monkeypatch.setenv("CGX_GATED", "0")  # host-checked: r.r read before the p update
+            xh, sth = s.solve(x0, eps=1e-6 if f32 else 1e-10)
+            monkeypatch.delenv("CGX_GATED")
+        res[form] = (x, st.iterations, xf, rn, xh, sth.iterations)
+    c = res["copy"]
+    for form in ("kernel", "nofuse"):
+        r = res[form]
+        assert r[1] == c[1] and r[5] == c[5] == c[1], form
+        assert np.array_equal(r[0], c[0]) and np.array_equal(r[2], c[2]) and r[3] == c[3], form
+        assert np.array_equal(r[4], c[0]), form
+    xk, itk = res["kernel"][0], res["kernel"][1]
     if f32:
         xo, so = oracle.cg_f32ref(A, b, x0, eps=1e-6, nparts=P, combine="mpich")
         assert itk == so.iterations and np.array_equal(xk.view(np.uint32), xo.view(np.uint32))

@@ -8,9 +8,11 @@ timed three ways:
   phases      the CGX_PHASES device-clock medians on shard 0.
 On one GPU the shards' kernels share the device, so wall_us is the sum of all
 shards' work; the host side (enqueue_us) is what a distinct-device run pays
-too.  Exchange forms (CGX_LOCAL_XCHG, read at context creation): "kernel"
-(one pull kernel per consuming shard for the gather and each combine, the
-default) and "copy" (round 3's hipMemcpyPeerAsync per pair), interleaved.
+too.  Exchange forms (read at context creation), interleaved: "kernel" (the
+default: one pull kernel per consuming shard for p's gather, the two scalar
+combines folded into the update kernels), "nofuse" (CGX_LOCAL_FUSE=0: a
+combine kernel per shard and scalar) and "copy" (CGX_LOCAL_XCHG=copy: round
+3's hipMemcpyPeerAsync per pair).
 Usage:  python tools/r04_multishard_floor.py [rounds] [n,...] [S,...] [forms]
   > profiles/r04_multishard_floor.jsonl"""
 import json
@@ -38,7 +40,8 @@ def run(n, shards, steps=200, warm=30):
         t2 = time.perf_counter()
         ph = s.phase_times()
         rn, bn = s.residual_norm()
-    return {"n": n, "shards": shards, "steps": steps, "exchange": os.environ.get("CGX_LOCAL_XCHG", "default"),
+    return {"n": n, "shards": shards, "steps": steps, "exchange": ("copy" if os.environ.get("CGX_LOCAL_XCHG") == "copy" else
+                                             "nofuse" if os.environ.get("CGX_LOCAL_FUSE") == "0" else "kernel"),
             "flags": int(info.flags),
             "enqueue_us": round((t1 - t0) / steps * 1e6, 2), "wall_us": round((t2 - t0) / steps * 1e6, 2),
             "relres": rn / bn,
@@ -49,12 +52,13 @@ def main():
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 2
     sizes = tuple(int(v) for v in sys.argv[2].split(",")) if len(sys.argv) > 2 else (4096,)
     counts = tuple(int(v) for v in sys.argv[3].split(",")) if len(sys.argv) > 3 else (1, 2, 4, 8)
-    forms = tuple(sys.argv[4].split(",")) if len(sys.argv) > 4 else ("kernel", "copy")
+    forms = tuple(sys.argv[4].split(",")) if len(sys.argv) > 4 else ("kernel", "nofuse", "copy")
     for r in range(rounds):
         for n in sizes:
             for S in counts:
                 for form in forms if S > 1 else forms[:1]:
-                    os.environ["CGX_LOCAL_XCHG"] = form
+                    os.environ["CGX_LOCAL_XCHG"] = "copy" if form == "copy" else "kernel"
+                    os.environ["CGX_LOCAL_FUSE"] = "0" if form == "nofuse" else "1"
                     out = run(n, S)
                     out["round"] = r
                     print(json.dumps(out), flush=True)
