@@ -474,6 +474,162 @@ __global__ __launch_bounds__(kNT) void k_poisson_xflush_f64(const double *__rest
     }
 }
 
+// ---- k_poisson_p_f64, software-pipelined (CGX_P_PIPE) --------------------------
+// k_poisson_p_f64's arithmetic in its order (the same p_k, the same p.Ap
+// partials) with the next step's loads -- at an item's last step, the next
+// item's prefix rows and first step -- issued before this step's arithmetic
+// and stores, as k_poisson_xr_pipe_f64 does.  Full strips, 8-row items, NT +
+// HT.  The halo-row stores (top of the first run, bottom of the last) stay
+// conditional: they are wave-uniform and rare.
+template <int RBn, bool FIRST>
+struct PSet {
+    d2 rv[RBn], pv[RBn];
+    double rl[RBn], pl[RBn], rr[RBn], pr[RBn];
+};
+template <int RBn, bool FIRST>
+__device__ __forceinline__ void p_pipe_load(PSet<RBn, FIRST> &S, const double *__restrict__ rh,
+                                            const double *__restrict__ poh, int64_t m, int64_t i, const StripLane &L,
+                                            bool last) {
+    const int64_t cl = L.jw > 0 ? L.jw - 1 : 0, cr = L.jw + 128 < m ? L.jw + 128 : m - 1;
+#pragma unroll
+    for (int t = 0; t < RBn; ++t) {
+        const int64_t hc = (i + t + 1) * m;
+        const bool ht = last && t >= RBn - 2;  // the next item's first two rows: default policy (HT)
+        S.rv[t] = ht ? lds2<false>(rh + hc + m, L.off) : lds2<true>(rh + hc + m, L.off);
+        if constexpr (!FIRST) S.pv[t] = ht ? lds2<false>(poh + hc + m, L.off) : lds2<true>(poh + hc + m, L.off);
+        S.rl[t] = rh[hc + cl];
+        S.rr[t] = rh[hc + cr];
+        if constexpr (!FIRST) {
+            S.pl[t] = poh[hc + cl];
+            S.pr[t] = poh[hc + cr];
+        }
+    }
+}
+template <bool FIRST>
+__device__ __forceinline__ d2 p_form(d2 rv, d2 pv, double beta) {
+    if constexpr (FIRST) return rv;
+    d2 o;
+    o.x = __builtin_fma(beta, pv.x, rv.x);
+    o.y = __builtin_fma(beta, pv.y, rv.y);
+    return o;
+}
+template <int RBn, bool FIRST>
+__device__ __forceinline__ void p_pipe_step(const PSet<RBn, FIRST> &S, double *__restrict__ pnh, int64_t mloc,
+                                            int64_t m, int64_t i, const StripLane &L, double beta, d2 &pm, d2 &pc,
+                                            double &acc, double *eb) {
+    const int lane = threadIdx.x & 63;
+    d2 pr[RBn], ce[RBn];
+    double el[RBn], er[RBn];
+#pragma unroll
+    for (int t = 0; t < RBn; ++t) {
+        pr[t] = p_form<FIRST>(S.rv[t], S.pv[t], beta);
+        el[t] = FIRST ? S.rl[t] : __builtin_fma(beta, S.pl[t], S.rl[t]);
+        er[t] = FIRST ? S.rr[t] : __builtin_fma(beta, S.pr[t], S.rr[t]);
+    }
+#pragma unroll
+    for (int t = 0; t < RBn; ++t) ce[t] = t == 0 ? pc : pr[t - 1];
+    edges_put<RBn>(eb, L, ce);
+    __syncthreads();
+#pragma unroll
+    for (int t = 0; t < RBn; ++t) {
+        const d2 up = t == 0 ? pm : (t == 1 ? pc : pr[t - 2]);
+        const d2 dn = pr[t];
+        const double lw = edge_l(eb, L, t, L.has_l ? el[t] : 0.0), rw = edge_r(eb, L, t, L.has_r ? er[t] : 0.0);
+        double l = __shfl_up(ce[t].y, 1, 64);
+        double r = __shfl_down(ce[t].x, 1, 64);
+        l = lane == 0 ? lw : l;
+        r = lane == 63 ? rw : r;
+        d2 o;
+        o.x = 4.0 * ce[t].x - up.x - dn.x - l - ce[t].y;
+        o.y = 4.0 * ce[t].y - up.y - dn.y - ce[t].x - r;
+        acc += ce[t].x * o.x + ce[t].y * o.y;
+        sts2<true>(pnh + (i + t + 1) * m, L.off, ce[t]);
+    }
+    if (i + RBn == mloc) sts2<true>(pnh + (mloc + 1) * m, L.off, pr[RBn - 1]);  // bottom halo row of p_k
+    if constexpr (RBn >= 2) {
+        pm = pr[RBn - 2];
+        pc = pr[RBn - 1];
+    } else {
+        pm = pc;
+        pc = pr[0];
+    }
+}
+template <int RBn, int NS, bool FIRST>
+__device__ __forceinline__ double poisson_p_pipe_body(const double *__restrict__ rh, const double *__restrict__ poh,
+                                                      double *__restrict__ pnh, int64_t mloc, int64_t m,
+                                                      int64_t nstrips, ItemRanges ir, double beta, double *edge,
+                                                      int bands) {
+    constexpr int64_t kRpi = RBn * NS;
+    double acc = 0.0;
+    const Band bd = bands ? band_of(ir.w0, ir.cnt1, nstrips, bands) : Band{0, 0, 0, 0, 0};
+    const int64_t vstart = bands ? bd.start : blockIdx.x, vend = bands ? bd.count : ir.cnt1 + ir.cnt2;
+    const int64_t vstride = bands ? bd.stride : gridDim.x;
+    if (vstart >= vend) return acc;
+    auto item_of = [&](int64_t v) {
+        return bands ? band_item(bd, v) : v < ir.cnt1 ? ir.w0 + v : ir.w2 + (v - ir.cnt1);
+    };
+    int64_t v = vstart, w = item_of(v);
+    StripLane L = strip_lane(w, nstrips, m);
+    int64_t i0 = (w / nstrips) * kRpi;
+    d2 pm = p_form<FIRST>(lds2<false>(rh + i0 * m, L.off), FIRST ? (d2)(0.0) : lds2<false>(poh + i0 * m, L.off), beta);
+    d2 pc = p_form<FIRST>(lds2<false>(rh + (i0 + 1) * m, L.off),
+                          FIRST ? (d2)(0.0) : lds2<false>(poh + (i0 + 1) * m, L.off), beta);
+    PSet<RBn, FIRST> S[2];
+    p_pipe_load<RBn, FIRST>(S[0], rh, poh, m, i0, L, NS == 1);
+    for (;;) {
+        if (i0 == 0) sts2<true>(pnh, L.off, pm);  // top halo row of p_k
+        const int64_t vn = v + vstride < vend ? v + vstride : v;
+        const int64_t wn = item_of(vn);
+        const StripLane Ln = strip_lane(wn, nstrips, m);
+        const int64_t i0n = (wn / nstrips) * kRpi;
+        d2 rmn, pmn, rcn, pcn;
+#pragma unroll
+        for (int s = 0; s < NS; ++s) {
+            if (s + 1 < NS) {
+                p_pipe_load<RBn, FIRST>(S[(s + 1) & 1], rh, poh, m, i0 + (s + 1) * RBn, L, s + 2 == NS);
+            } else {
+                rmn = lds2<false>(rh + i0n * m, Ln.off);
+                rcn = lds2<false>(rh + (i0n + 1) * m, Ln.off);
+                if constexpr (!FIRST) {
+                    pmn = lds2<false>(poh + i0n * m, Ln.off);
+                    pcn = lds2<false>(poh + (i0n + 1) * m, Ln.off);
+                }
+                p_pipe_load<RBn, FIRST>(S[(s + 1) & 1], rh, poh, m, i0n, Ln, NS == 1);
+            }
+            p_pipe_step<RBn, FIRST>(S[s & 1], pnh, mloc, m, i0 + s * RBn, L, beta, pm, pc, acc,
+                                    edge + (s & 1) * (kWaves * 2 * kEdgeRB));
+        }
+        if (vn == v) break;
+        v = vn;
+        L = Ln;
+        i0 = i0n;
+        pm = p_form<FIRST>(rmn, FIRST ? (d2)(0.0) : pmn, beta);
+        pc = p_form<FIRST>(rcn, FIRST ? (d2)(0.0) : pcn, beta);
+    }
+    return acc;
+}
+template <int RBn, int NS, bool FIRST>
+__global__ __launch_bounds__(kNT) void k_poisson_p_pipe_f64(const double *__restrict__ rh,
+                                                            const double *__restrict__ poh, double *__restrict__ pnh,
+                                                            int64_t mloc, int64_t m, int64_t nstrips, ItemRanges ir,
+                                                            const double *rr, const double *rsold, int first,
+                                                            ConvArgs cv, double *dot_out, int add_to_out,
+                                                            double *partials, unsigned *ticket, int bands) {
+    static_assert(RBn <= kEdgeRB && NS % 2 == 0, "edge buffer / set parity");
+    __shared__ double edge[2 * kWaves * 2 * kEdgeRB];
+    if (cv.kdone) {
+        if (*cv.kdone != 0) return;
+        if (!first && cv.eps >= 0.0 && sqrt(*rr) < cv.eps) {
+            if (blockIdx.x == 0 && threadIdx.x == 0) record_convergence(cv, cv.k, *rr);
+            return;
+        }
+    }
+    // p_0 = r_0 (first) is its own instantiation: the other one's registers are what set the occupancy
+    const double acc = poisson_p_pipe_body<RBn, NS, FIRST>(rh, poh, pnh, mloc, m, nstrips, ir,
+                                                          FIRST ? 0.0 : cg_ratio(*rr, *rsold), edge, bands);
+    grid_sum_last_block(acc, partials, ticket, dot_out, add_to_out != 0);
+}
+
 // ---- k_poisson_xr_f64, software-pipelined (CGX_XR_PIPE) ----------------------
 // The same arithmetic, row by row and item by item in the same order as
 // k_poisson_xr_f64 (so r, x and every r.r partial are the same bits), with
@@ -732,6 +888,20 @@ static void launch_poisson_p(const PoissonPlan &pl, hipStream_t s, const double 
     int64_t grid = resident_grid(reinterpret_cast<const void *>(fn), ir.cnt1 + ir.cnt2);
     const int bands = pl.bands && ir.cnt2 == 0 && ir.cnt1 % pl.nstrips == 0 && grid >= 8 ? 1 + pl.band_rot : 0;
     if (bands) grid &= ~int64_t(7);
+    // the software-pipelined kernel (full strips, 8-row items, NT + HT): the same p_k; on its own
+    // occupancy's grid (3 waves per SIMD, not 4), so p.Ap adds its partials in another order
+    const int pipe_rb = env_int("CGX_P_PIPE", 0);
+    if ((pipe_rb == 2 || pipe_rb == 4) && m % (2 * kNT) == 0 && pl.rpi == 8 && mloc % 8 == 0 && pl.nt && pl.ht) {
+        auto fp = pipe_rb == 2 ? (first ? k_poisson_p_pipe_f64<2, 4, true> : k_poisson_p_pipe_f64<2, 4, false>)
+                               : (first ? k_poisson_p_pipe_f64<4, 2, true> : k_poisson_p_pipe_f64<4, 2, false>);
+        auto fg = pipe_rb == 2 ? k_poisson_p_pipe_f64<2, 4, false> : k_poisson_p_pipe_f64<4, 2, false>;
+        int64_t pg = resident_grid(reinterpret_cast<const void *>(fg), ir.cnt1 + ir.cnt2);
+        const int pbands = pl.bands && ir.cnt2 == 0 && ir.cnt1 % pl.nstrips == 0 && pg >= 8 ? 1 + pl.band_rot : 0;
+        if (pbands) pg &= ~int64_t(7);
+        hipLaunchKernelGGL(fp, dim3((unsigned)pg), dim3(kNT), 0, s, rh, poh, pnh, mloc, m, pl.nstrips, ir, rr, rsold,
+                           first, cv, pap_out, add_to_out, ws.partials, ws.tickets + T_MATVEC, pbands);
+        return;
+    }
     hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(kNT), 0, s, rh, poh, pnh, mloc, m, pl.nstrips, pl.rpi, ir, rr,
                        rsold, first, cv, pap_out, add_to_out, ws.partials, ws.tickets + T_MATVEC, bands);
 }

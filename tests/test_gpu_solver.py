@@ -891,6 +891,32 @@ def test_poisson_xr_pipelined_kernel_is_bitwise(monkeypatch, m, shards, period, 
         assert a[key][1:] == b[key][1:], key
 
 
+@pytest.mark.parametrize("rb", ["2", "4"])
+@pytest.mark.parametrize("m,shards", [(1024, None), (512, [0] * 4)])
+def test_poisson_p_pipelined_kernel(monkeypatch, m, shards, rb):
+    """The software-pipelined k_poisson_p_pipe_f64 (CGX_P_PIPE) forms the same
+    p_k; it runs on its own occupancy's grid, so p.Ap adds in another order:
+    the solve agrees with the plain kernel's to fp64 rounding in the same loop
+    count (gated, halo overlap on 4 slabs with its interior / edge parts), and
+    x every iteration / every third iteration stay bit for bit equal under it."""
+    monkeypatch.setenv("CGX_POISSON_FUSED", "1")
+    res = {}
+    for pipe in ("0", rb):
+        monkeypatch.setenv("CGX_P_PIPE", pipe)
+        with cg.Solver(None, poisson_m=m, devices=shards) as s:
+            s.fill(1.0, 0.0)
+            x, st = s.solve(None, eps=1e-8)
+            res[pipe] = (x, st.iterations, st.converged)
+    (x0, it0, c0), (x1, it1, c1) = res["0"], res[rb]
+    assert c0 and c1 and abs(it0 - it1) <= 1 and rel(x1, x0) <= 1e-9
+    monkeypatch.setenv("CGX_P_PIPE", rb)
+    a = _poisson_x_runs(m, shards, "3", monkeypatch)
+    b = _poisson_x_runs(m, shards, "0", monkeypatch)
+    for key in a:
+        assert np.array_equal(a[key][0], b[key][0]), key
+        assert a[key][1:] == b[key][1:], key
+
+
 def test_poisson_fused_in_pieces_and_iteration_cap():
     """Iterations issued in several cgx_iterate calls (fixed count, then
     convergence-tested) give the one-call solve; a cap that stops exactly at
