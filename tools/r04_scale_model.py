@@ -23,13 +23,14 @@ import statistics
 import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
-PROF = os.path.join(ROOT, "profiles")
+PROF = os.environ.get("R04_PROF_DIR", os.path.join(ROOT, "profiles"))
 N = 65536
 
 # RCCL small-message collectives over xGMI on one 8-GPU MI300-class node (LL
 # protocol): an 8-byte allreduce in the tens of microseconds at most; the
 # allgather of 8*N/G bytes per rank adds its transfer at ~100 GB/s effective
-# per peer link (MI355X: 7 xGMI links per GPU, ~153 GB/s each).  These are
+# per peer link (MI355X: 7 xGMI links per GPU, ~153 GB/s each, per the project
+# brief).  These are
 # assumptions, labelled as such in the output.
 ALLREDUCE_US = {"low": 6.0, "mid": 12.0, "high": 25.0}
 GATHER_LAT_US = {"low": 6.0, "mid": 12.0, "high": 25.0}
@@ -82,9 +83,9 @@ def main():
             "allgather_latency_us": GATHER_LAT_US,
             "allgather_GBps_per_peer_link": GATHER_GBPS_PER_LINK,
             "source": "not measurable on a one-GPU box (RCCL runs over loopback sockets there); RCCL's LL-protocol "
-                      "small-message latency on one xGMI-connected node is in the 5-25 us range; the MI355X has 7 "
-                      "xGMI links per GPU at ~153 GB/s (MI355X_MICROARCH.md / task brief), taken at 100 GB/s "
-                      "effective per peer",
+                      "small-message latency on one xGMI-connected node is assumed in the 5-25 us range (not from a "
+                      "document available here); the MI355X has 7 xGMI links per GPU at ~153 GB/s each (the "
+                      "project brief), taken at 100 GB/s effective per peer",
         },
         "per_G": {},
     }
@@ -114,7 +115,7 @@ def main():
                                                - k["update_xp"]), 2)},
                 "iteration_us": round(it_us, 1), "it_per_s": round(1e6 / it_us, 1),
                 "speedup_vs_1gpu": round(ms1 * 1e3 / it_us, 2),
-                "speedup_vs_1gpu_x_G": round(ms1 * 1e3 / it_us / G, 3)}
+                "efficiency": round(ms1 * 1e3 / it_us / G, 3)}
         entry["predicted"] = pred
         if G in floor:
             enq = statistics.median(floor[G])
