@@ -15,6 +15,10 @@ loopback sockets): the latency of RCCL's 8-byte allreduce and of the p
 allgather over xGMI, as a low / mid / high range.
 
   python tools/r04_scale_model.py > profiles/r04_scale_model.json
+  python tools/r04_scale_model.py --compare LINE.json [...]
+      (bench.py lines of an N>1 run, e.g. from the driver's SCALE record:
+      each phase's max over ranks against the model's mid prediction, and
+      the phase that is furthest above it)
 """
 import csv
 import json
@@ -130,5 +134,27 @@ def main():
     print()
 
 
+def compare(paths):
+    model = json.load(open(os.path.join(PROF, "r04_scale_model.json")))
+    for path in paths:
+        text = open(path).read()
+        line = json.loads([ln for ln in text.splitlines() if ln.strip().startswith("{")][-1])
+        G = str(line["n_gpus"])
+        pred = model["per_G"].get(G, {}).get("predicted", {}).get("mid")
+        meas = line.get("phases_us", {}).get("max_over_ranks")
+        if not pred or not meas:
+            print(json.dumps({"file": path, "n_gpus": G, "error": "no model entry or no phases_us"}))
+            continue
+        delta = {k: round(meas.get(k, 0.0) - v, 2) for k, v in pred["phases_us"].items()}
+        culprit = max(delta, key=delta.get)
+        print(json.dumps({"file": path, "n_gpus": G, "it_per_s": line["value"],
+                          "predicted_it_per_s": pred["it_per_s"], "measured_phases_us": meas,
+                          "predicted_phases_us": pred["phases_us"], "delta_us": delta,
+                          "furthest_above_model": culprit}))
+
+
 if __name__ == "__main__":
-    main()
+    if len(sys.argv) > 2 and sys.argv[1] == "--compare":
+        compare(sys.argv[2:])
+    else:
+        main()
