@@ -37,22 +37,34 @@ __device__ __forceinline__ T load_sys(const T *p) {
     return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_SYSTEM);
 }
 
-// PeerSum (cgx_kernels.h): the cnt partials in rank order, computed by thread
-// 0 of every block and shared through LDS; block 0 stores it for later use.
-// Every thread of the block must call it (it has a barrier).
-__device__ __forceinline__ double peer_sum_block(const PeerSum &c) {
+// The cnt (<= 64) per-shard partials src.p[q], one per lane, loaded together
+// (one round trip, not cnt): lanes past cnt hold 0.
+template <typename T>
+__device__ __forceinline__ T peer_lane_load(const PeerTable &src, int cnt) {
+    const int lane = threadIdx.x & 63;
+    return lane < cnt ? load_sys(reinterpret_cast<const T *>(src.p[lane])) : T(0);
+}
+__device__ __forceinline__ double readlane_f64(double v, int lane) {
+    const uint64_t b = __builtin_bit_cast(uint64_t, v);
+    const uint32_t lo = __builtin_amdgcn_readlane((uint32_t)b, lane), hi = __builtin_amdgcn_readlane((uint32_t)(b >> 32), lane);
+    return __builtin_bit_cast(double, ((uint64_t)hi << 32) | lo);
+}
+// The rank-order sum x_0 + x_1 + ... of the lanes' values (wave-uniform
+// result, the same adds in the same order as a sequential loop).
+__device__ __forceinline__ double lane_sum_ordered_f64(double x, int cnt) {
 #pragma clang fp contract(off)
-    __shared__ double sh;
-    if (threadIdx.x == 0) {
-        double in[kMaxPeers];
-        for (int q = 0; q < c.cnt; ++q) in[q] = load_sys(reinterpret_cast<const double *>(c.src.p[q]));
-        double v = in[0];
-        for (int q = 1; q < c.cnt; ++q) v = v + in[q];
-        sh = v;
-        if (blockIdx.x == 0) *c.out = v;
-    }
-    __syncthreads();
-    return sh;
+    double v = readlane_f64(x, 0);
+    for (int q = 1; q < cnt; ++q) v = v + readlane_f64(x, q);
+    return v;
+}
+
+// PeerSum (cgx_kernels.h): the cnt partials in rank order, computed by every
+// wave (the loads go out with the kernel's first vector loads; no barrier,
+// no LDS); block 0's thread 0 stores it for later kernels and the host.
+__device__ __forceinline__ double peer_sum_wave(const PeerSum &c) {
+    const double v = lane_sum_ordered_f64(peer_lane_load<double>(c.src, c.cnt), c.cnt);
+    if (blockIdx.x == 0 && threadIdx.x == 0) *c.out = v;
+    return v;
 }
 
 __device__ __forceinline__ double cg_ratio(double num, double den) {

@@ -300,7 +300,7 @@ __global__ __launch_bounds__(kNT) void k_update_r_f64(int64_t n, double *__restr
                                                       int64_t *ts, PeerSum pap_sum) {
     if (gate && *gate) return;
     ts_start(ts);
-    const double alpha = cg_ratio(*rsold, pap_sum.cnt ? peer_sum_block(pap_sum) : *pAp);
+    const double alpha = cg_ratio(*rsold, pap_sum.cnt ? peer_sum_wave(pap_sum) : *pAp);
     double acc = 0.0;
     if constexpr (VEC) {
         CGX_VEC_LOOP_BEGIN
@@ -346,7 +346,7 @@ __global__ __launch_bounds__(kNT) void k_update_xp_f64(int64_t n, double *__rest
     bool upd_p = rr != nullptr;
     if (cv.kdone && *cv.kdone != 0 && *cv.kdone <= cv.k) return;
     // the r.r combine folded in (multi-shard): every block sums the partials
-    const double rrv = rr_sum.cnt ? peer_sum_block(rr_sum) : rr ? *rr : 0.0;
+    const double rrv = rr_sum.cnt ? peer_sum_wave(rr_sum) : rr ? *rr : 0.0;
     if (cv.kdone) {
         const double rrn = rrv;
         if (cv.eps >= 0.0 && sqrt(rrn) < cv.eps) {
@@ -480,26 +480,33 @@ __global__ void k_sum_ordered(const T *in, int cnt, int stride, int mpich, T *ou
 // worth of traffic (512 KB of p per iteration at N = 65536).  (load_sys:
 // cgx_device.h.)
 
-// The same combines over a table of peer pointers (one partial per shard).
+// The same combines over a table of peer pointers (one partial per shard),
+// by one wave: lane q loads partial q (one round trip for all of them), then
+// the rank-order sum in lane order, or MPICH's recursive doubling with the
+// values kept in lanes (pairs (2q, 2q+1) for q < rem, then a pairwise tree:
+// the same adds in the same order as k_sum_ordered).
 template <typename T>
-__global__ void k_combine_peers(PeerTable src, int cnt, int mpich, T *out) {
+__global__ __launch_bounds__(64) void k_combine_peers(PeerTable src, int cnt, int mpich, T *out) {
 #pragma clang fp contract(off)
-    T in[kMaxPeers];
-    for (int q = 0; q < cnt; ++q) in[q] = load_sys(reinterpret_cast<const T *>(src.p[q]));
+    const int lane = threadIdx.x;
+    const T x = peer_lane_load<T>(src, cnt);
     if (!mpich) {
-        T s = in[0];
-        for (int q = 1; q < cnt; ++q) s = s + in[q];
-        *out = s;
+        T s = __shfl(x, 0, 64);
+        for (int q = 1; q < cnt; ++q) s = s + __shfl(x, q, 64);
+        if (lane == 0) *out = s;
         return;
     }
     int pof2 = 1;
     while (pof2 * 2 <= cnt) pof2 *= 2;
     const int rem = cnt - pof2;
-    T v[kMaxPeers];
-    for (int q = 0; q < pof2; ++q) v[q] = q < rem ? in[2 * q] + in[2 * q + 1] : in[q + rem];
-    for (int d = 1; d < pof2; d *= 2)
-        for (int q = 0; q < pof2; q += 2 * d) v[q] = v[q] + v[q + d];
-    *out = v[0];
+    const T a = __shfl(x, lane < rem ? 2 * lane : (lane + rem) & 63, 64);
+    const T b = __shfl(x, (2 * lane + 1) & 63, 64);
+    T v = lane < rem ? a + b : a;
+    for (int d = 1; d < pof2; d *= 2) {
+        const T w = __shfl(v, (lane + d) & 63, 64);
+        if (lane % (2 * d) == 0 && lane + d < pof2) v = v + w;
+    }
+    if (lane == 0) *out = v;
 }
 
 // blockIdx.y = the source slice; each thread moves kGU words of W (8 or 4)
@@ -542,13 +549,13 @@ hipError_t gather_slices(const PeerTable &src, int cnt, int skip, int64_t slice_
 
 hipError_t combine_peers_f64(const PeerTable &src, int cnt, double *out, hipStream_t s) {
     if (cnt < 1 || cnt > kMaxPeers) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_combine_peers<double>, dim3(1), dim3(1), 0, s, src, cnt, 0, out);
+    hipLaunchKernelGGL(k_combine_peers<double>, dim3(1), dim3(64), 0, s, src, cnt, 0, out);
     return hipGetLastError();
 }
 
 hipError_t combine_peers_f32(const PeerTable &src, int cnt, float *out, hipStream_t s, bool mpich) {
     if (cnt < 1 || cnt > kMaxPeers) return hipErrorInvalidValue;
-    hipLaunchKernelGGL(k_combine_peers<float>, dim3(1), dim3(1), 0, s, src, cnt, mpich ? 1 : 0, out);
+    hipLaunchKernelGGL(k_combine_peers<float>, dim3(1), dim3(64), 0, s, src, cnt, mpich ? 1 : 0, out);
     return hipGetLastError();
 }
 

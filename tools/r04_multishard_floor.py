@@ -1,10 +1,12 @@
 """Per-iteration cost of the single-process multi-shard path (cgx_create_multi,
 `cg_hip --gpus P`) at S = 1/2/4/8 row blocks, every shard on device 0
 (devices=[0]*S): fixed-count iterations (dense fp64, the overlapped exchange),
-timed three ways:
+timed four ways:
   enqueue_us  host time inside cgx_iterate per iteration (it returns without
               a sync for eps < 0, so this is the host's enqueue cost alone);
   wall_us     host time from the call to the end of cgx_synchronize;
+  enqueue_10_us  the same for 10 iterations right after a sync (empty queues:
+              the host's cost alone even when the device is the slower side);
   phases      the CGX_PHASES device-clock medians on shard 0.
 On one GPU the shards' kernels share the device, so wall_us is the sum of all
 shards' work; the host side (enqueue_us) is what a distinct-device run pays
@@ -39,11 +41,18 @@ def run(n, shards, steps=200, warm=30):
         s.synchronize()
         t2 = time.perf_counter()
         ph = s.phase_times()
+        # the enqueue alone, with the queues empty: 10 iterations (200 can fill
+        # the hardware queues on one GPU and then time the device instead)
+        t3 = time.perf_counter()
+        s.iterate(10, eps=-1.0)
+        t4 = time.perf_counter()
+        s.synchronize()
         rn, bn = s.residual_norm()
     return {"n": n, "shards": shards, "steps": steps, "exchange": ("copy" if os.environ.get("CGX_LOCAL_XCHG") == "copy" else
                                              "nofuse" if os.environ.get("CGX_LOCAL_FUSE") == "0" else "kernel"),
             "flags": int(info.flags),
             "enqueue_us": round((t1 - t0) / steps * 1e6, 2), "wall_us": round((t2 - t0) / steps * 1e6, 2),
+            "enqueue_10_us": round((t4 - t3) / 10 * 1e6, 2),
             "relres": rn / bn,
             "phases_median_us": {k: round(v["median_us"], 2) for k, v in ph.items() if v["samples"]}}
 
