@@ -76,7 +76,7 @@ def main():
         for line in open(fpath):
             d = json.loads(line)
             if d["n"] == 4096 and d["exchange"] == "kernel":
-                floor.setdefault(d["shards"], []).append(d["enqueue_us"])
+                floor.setdefault(d["shards"], []).append(d.get("enqueue_10_us", d["enqueue_us"]))
     out = {
         "what": "configs[2] (N=65536 dense fp64, row blocks) at G GPUs: one rank's measured kernels plus assumed "
                 "collective latencies -> predicted iteration, it/s and speed-up over the measured 1-GPU step; "
