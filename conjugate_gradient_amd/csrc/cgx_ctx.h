@@ -200,6 +200,7 @@ struct Shard {
     int64_t sym_stage_rows = 0;
     int sym_grid = 0;
     hipEvent_t ev_sync = nullptr;  // cross-shard ordering (LOCAL mode): local_barrier
+    hipEvent_t ev_sync2 = nullptr;  // ... the r.r record point of the threaded iteration (cgx_local_mt.hip)
     hipEvent_t ev_root = nullptr;  // CGX_COMM_P2P in LOCAL mode: shard 0's result is ready
     std::vector<hipEvent_t> ev_t;  // timing pairs (CGX_TIMING)
     int ev_used = 0;
@@ -237,6 +238,10 @@ struct Shard {
 };
 
 }  // namespace cgxh
+
+namespace cgxh {
+struct LocalPool;  // cgx_local_mt.hip
+}
 
 using namespace cgxh;
 
@@ -296,6 +301,9 @@ struct cgx_ctx {
     // partials, k_update_xp_f64 the r.r partials: PeerSum), so an iteration
     // launches no combine kernel (CGX_LOCAL_FUSE=0: separate combine kernels)
     bool fuse_combine = false;
+    // LOCAL mode: one host thread per row block enqueues its block's iteration
+    // (cgx_local_mt.hip); null when not used
+    cgxh::LocalPool *pool = nullptr;
     // CGX_PHASES: resolved per-iteration phase durations (us), cgx_phase_times' order;
     // the wall clock's rate, and the previous stamped iteration's first start /
     // last end (ticks; 0 = none) so the gap across a resolve is still measured
@@ -366,6 +374,12 @@ int dead_error(const cgx_ctx *c);
 int rank_wait_event(cgx_ctx *c, hipEvent_t ev, const char *what);
 int rank_wait_stream(cgx_ctx *c, hipStream_t st, const char *what);
 double rccl_timeout_from_env();
+// cgx_local_mt.hip
+bool local_mt_eligible(const cgx_ctx *c);
+int local_mt_start(cgx_ctx *c);
+void local_mt_stop(cgx_ctx *c);
+int local_mt_iteration(cgx_ctx *c, double eps, bool gated);
+PeerTable peer_table(const cgx_ctx *c, char *Shard::*buf, int64_t off);
 // cgx_iterate.hip
 int matvec_rows(cgx_ctx *c, Shard &s, const MatvecPlan &pl, const char *Arows, int64_t r0, int64_t rows,
                 const char *vec, bool fuse_dot, int dot_slot, bool gated = false, int64_t *ts = nullptr);

@@ -149,7 +149,7 @@ int local_barrier(cgx_ctx *c) {
 // The table of every shard's copy of a buffer at byte offset `off` (+ the
 // shard's own row offset when `own_rows`), in shard order, for the pull
 // kernels of the LOCAL exchange.
-static PeerTable peer_table(const cgx_ctx *c, char *Shard::*buf, int64_t off) {
+PeerTable peer_table(const cgx_ctx *c, char *Shard::*buf, int64_t off) {
     PeerTable t{};
     for (const auto &s : c->sh) t.p[s.index] = s.*buf + off;
     return t;

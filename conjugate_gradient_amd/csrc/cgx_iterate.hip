@@ -470,6 +470,13 @@ int do_iteration(cgx_ctx *c, double eps, int *stop, bool gated) {
     *stop = 0;
     const int pg = S_PAP + ring(k), pl = S_LPAP + ring(k);
     TRY(phase_iter_begin(c));
+    if (c->pool && (gated || eps < 0.0)) {  // each row block's thread enqueues its own work (cgx_local_mt.hip)
+        TRY(local_mt_iteration(c, eps, gated));
+        phase_iter_end(c);
+        c->k = k + 1;
+        c->total_iters += 1;
+        return CGX_OK;
+    }
     if (c->overlap) {
         TRY(overlapped_matvec(c, out_slot(c, pl, pg), gated));  // parallel_cg.c:290-293, overlapped
     } else {

@@ -29,7 +29,9 @@ int alloc_shard(cgx_ctx *c, Shard &s) {
     const size_t es = (size_t)c->es;
     HIPT(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
     HIPT(hipEventCreateWithFlags(&s.ev_sync, hipEventDisableTiming));
+    HIPT(hipEventCreateWithFlags(&s.ev_sync2, hipEventDisableTiming));
     HIPT(hipEventCreateWithFlags(&s.ev_root, hipEventDisableTiming));
+    if (!s.ev_pready) HIPT(hipEventCreateWithFlags(&s.ev_pready, hipEventDisableTiming));
     const size_t abytes = (size_t)s.nloc * (size_t)c->lda * es;
     auto dmalloc = [&](char **p, size_t bytes) -> int {
         if (bytes == 0) bytes = 16;
@@ -232,6 +234,7 @@ void free_shard(Shard &s) {
     for (auto e : s.ev_prog)
         if (e) (void)hipEventDestroy(e);
     if (s.ev_sync) (void)hipEventDestroy(s.ev_sync);
+    if (s.ev_sync2) (void)hipEventDestroy(s.ev_sync2);
     if (s.ev_root) (void)hipEventDestroy(s.ev_root);
     for (int q = 0; q < kMaxCopyStreams; ++q)
         if (s.copy[q]) {
@@ -299,7 +302,7 @@ int alloc_overlap(cgx_ctx *c) {
     for (auto &s : c->sh) {
         TRY(set_dev(s));
         HIPT(hipStreamCreateWithFlags(&s.cstream, hipStreamNonBlocking));
-        HIPT(hipEventCreateWithFlags(&s.ev_pready, hipEventDisableTiming));
+        if (!s.ev_pready) HIPT(hipEventCreateWithFlags(&s.ev_pready, hipEventDisableTiming));
         HIPT(hipEventCreateWithFlags(&s.ev_gathered, hipEventDisableTiming));
     }
     return CGX_OK;
@@ -394,6 +397,9 @@ int finish_create(cgx_ctx *c, cgx_ctx **out) {
             return rc;
         }
     }
+    // one enqueuing thread per row block (cgx_local_mt.hip); without it the
+    // iteration is enqueued by the calling thread, the same launches
+    if (local_mt_eligible(c) && local_mt_start(c) != CGX_OK) c->pool = nullptr;
     *out = c;
     return CGX_OK;
 }
@@ -656,6 +662,7 @@ int cgx_destroy(cgx_ctx *ctx) {
     // rank mode: drain with the deadline first, so a job whose peer died is
     // aborted here instead of hanging in the stream syncs below
     const int rc = (ctx->mode == M_RCCL && !ctx->dead) ? sync_all(ctx) : CGX_OK;
+    local_mt_stop(ctx);
     for (auto &s : ctx->sh) free_shard(s);
     delete ctx;
     return rc;

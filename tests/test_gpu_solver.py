@@ -115,9 +115,12 @@ def test_local_exchange_kernels_bitwise_equal_peer_copies(monkeypatch, kind, P):
     x0 = np.full(n, 0.125, dt)
     flags = cg.CGX_F32_REF if f32 else cg.CGX_F64 | (cg.CGX_NO_OVERLAP if kind == "f64_nooverlap" else 0)
     res = {}
-    for form in ("kernel", "nofuse", "copy"):  # nofuse: a combine kernel per scalar instead of the folded sums
+    # nofuse: a combine kernel per scalar instead of the folded sums; onethread: every block's work
+    # enqueued by the calling thread instead of one thread per block (cgx_local_mt.hip)
+    for form in ("kernel", "onethread", "nofuse", "copy"):
         monkeypatch.setenv("CGX_LOCAL_XCHG", "copy" if form == "copy" else "kernel")
         monkeypatch.setenv("CGX_LOCAL_FUSE", "0" if form == "nofuse" else "1")
+        monkeypatch.setenv("CGX_LOCAL_THREADS", "0" if form == "onethread" else "1")
         with cg.Solver(n, flags=flags, devices=[0] * P) as s:
             if kind == "f64" and P in (2, 8):
                 assert s.info.flags & cg.CGX_OVERLAP_ACTIVE
@@ -130,7 +133,7 @@ def test_local_exchange_kernels_bitwise_equal_peer_copies(monkeypatch, kind, P):
             monkeypatch.delenv("CGX_GATED")
         res[form] = (x, st.iterations, xf, rn, xh, sth.iterations)
     c = res["copy"]
-    for form in ("kernel", "nofuse"):
+    for form in ("kernel", "onethread", "nofuse"):
         r = res[form]
         assert r[1] == c[1] and r[5] == c[5] == c[1], form
         assert np.array_equal(r[0], c[0]) and np.array_equal(r[2], c[2]) and r[3] == c[3], form

@@ -12,7 +12,8 @@ On one GPU the shards' kernels share the device, so wall_us is the sum of all
 shards' work; the host side (enqueue_us) is what a distinct-device run pays
 too.  Exchange forms (read at context creation), interleaved: "kernel" (the
 default: one pull kernel per consuming shard for p's gather, the two scalar
-combines folded into the update kernels), "nofuse" (CGX_LOCAL_FUSE=0: a
+combines folded into the update kernels, one enqueuing thread per block),
+"onethread" (the same, all enqueued by the calling thread), "nofuse" (CGX_LOCAL_FUSE=0: a
 combine kernel per shard and scalar) and "copy" (CGX_LOCAL_XCHG=copy: round
 3's hipMemcpyPeerAsync per pair).
 Usage:  python tools/r04_multishard_floor.py [rounds] [n,...] [S,...] [forms]
@@ -49,7 +50,8 @@ def run(n, shards, steps=200, warm=30):
         s.synchronize()
         rn, bn = s.residual_norm()
     return {"n": n, "shards": shards, "steps": steps, "exchange": ("copy" if os.environ.get("CGX_LOCAL_XCHG") == "copy" else
-                                             "nofuse" if os.environ.get("CGX_LOCAL_FUSE") == "0" else "kernel"),
+                                             "nofuse" if os.environ.get("CGX_LOCAL_FUSE") == "0" else
+                                             "onethread" if os.environ.get("CGX_LOCAL_THREADS") == "0" else "kernel"),
             "flags": int(info.flags),
             "enqueue_us": round((t1 - t0) / steps * 1e6, 2), "wall_us": round((t2 - t0) / steps * 1e6, 2),
             "enqueue_10_us": round((t4 - t3) / 10 * 1e6, 2),
@@ -61,13 +63,14 @@ def main():
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 2
     sizes = tuple(int(v) for v in sys.argv[2].split(",")) if len(sys.argv) > 2 else (4096,)
     counts = tuple(int(v) for v in sys.argv[3].split(",")) if len(sys.argv) > 3 else (1, 2, 4, 8)
-    forms = tuple(sys.argv[4].split(",")) if len(sys.argv) > 4 else ("kernel", "nofuse", "copy")
+    forms = tuple(sys.argv[4].split(",")) if len(sys.argv) > 4 else ("kernel", "onethread", "nofuse", "copy")
     for r in range(rounds):
         for n in sizes:
             for S in counts:
                 for form in forms if S > 1 else forms[:1]:
                     os.environ["CGX_LOCAL_XCHG"] = "copy" if form == "copy" else "kernel"
                     os.environ["CGX_LOCAL_FUSE"] = "0" if form == "nofuse" else "1"
+                    os.environ["CGX_LOCAL_THREADS"] = "0" if form in ("onethread", "nofuse", "copy") else "1"
                     out = run(n, S)
                     out["round"] = r
                     print(json.dumps(out), flush=True)
