@@ -20,3 +20,8 @@ for f in ("gpurun_out/r04_floor_mt.jsonl", "gpurun_out/r04_floor_mt_65536.jsonl"
         d = json.loads(l)
         print(d["n"], d["shards"], d["exchange"], "enq", d["enqueue_us"], "enq10", d["enqueue_10_us"], "wall", d["wall_us"])
 PY
+timeout -k 10 400 python -u tools/ab_variants.py --rounds 2 --args "--workload poisson --steps 300" \
+    --variant default= --variant g1024=CGX_STENCIL_BLOCKS=1024 \
+    --variant g1024q=CGX_STENCIL_BLOCKS=1024,CGX_XR3_QUARTER=1 --variant q=CGX_XR3_QUARTER=1 \
+    > gpurun_out/r04_poisson_grid_ab.jsonl || exit 1
+cat gpurun_out/r04_poisson_grid_ab.jsonl
