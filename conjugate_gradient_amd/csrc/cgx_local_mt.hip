@@ -16,7 +16,8 @@
 //
 // Used for the dense fp64 iteration with the folded scalar combines, gated
 // or fixed-count (the host-checked form reads r.r between the kernels and
-// stays on the single-thread path).  CGX_LOCAL_THREADS=0 turns it off.
+// stays on the single-thread path), when the blocks span distinct devices
+// (local_mt_eligible).
 #include <atomic>
 #include <condition_variable>
 #include <thread>
@@ -173,11 +174,19 @@ static void worker(LocalPool *P, int index) {
     }
 }
 
+// On by default when the row blocks span distinct devices (peer access on):
+// each thread then launches onto its own device's queues.  With every block
+// on one GPU the runtime serialises the threads' launches on that device's
+// queues and the threaded enqueue measured no faster (275-345 vs 275-294 us
+// per iteration at 8 blocks, profiles/r04_multishard_floor_threads.jsonl), so
+// it stays off there unless CGX_LOCAL_THREADS=1 forces it (the tests do, for
+// the code path); CGX_LOCAL_THREADS=0 turns it off everywhere.
 bool local_mt_eligible(const cgx_ctx *c) {
     const char *e = std::getenv("CGX_LOCAL_THREADS");
     if (e && *e == '0') return false;
+    const bool force = e && *e == '1';
     return c->mode == M_LOCAL && c->fuse_combine && c->op == OP_DENSE && !f32ref(c) &&
-           !(c->flags & (CGX_HOST_STREAM | CGX_SYMMETRIC | CGX_COMM_P2P)) && c->sh.size() >= 2;
+           !(c->flags & (CGX_HOST_STREAM | CGX_SYMMETRIC | CGX_COMM_P2P)) && c->sh.size() >= 2 && (c->peer || force);
 }
 
 int local_mt_start(cgx_ctx *c) {
