@@ -942,9 +942,11 @@ static void launch_poisson_xr(const PoissonPlan &pl, hipStream_t s, const double
     if (bands) grid &= ~int64_t(7);
     const int reverse = env_int("CGX_STENCIL_REVERSE", 1);
     // the software-pipelined kernel: full strips, 8-row items, NT + HT (same bits, same grid)
-    // (CGX_XR_PIPE_CATCHUP: another rows-per-step for the x catch-up kernels, XM = 2 / 3)
-    const int pipe_rb = XM >= 2 && env_int("CGX_XR_PIPE_CATCHUP", 0) ? env_int("CGX_XR_PIPE_CATCHUP", 0)
-                                                                    : env_int("CGX_XR_PIPE", 0);
+    // CGX_XR_PIPE: rows per step of the pipelined kernel for XM = 0 / 1 (default 0: the plain
+    // kernel); CGX_XR_PIPE_CATCHUP: the same for the x catch-up kernels, XM = 2 / 3 (default 4:
+    // 1489-1496 vs 1471-1480 it/s at m = 8192, three interleaved rounds, the same bits;
+    // profiles/r04_poisson_catchup_ab.jsonl)
+    const int pipe_rb = XM >= 2 ? env_int("CGX_XR_PIPE_CATCHUP", 4) : env_int("CGX_XR_PIPE", 0);
     if ((pipe_rb == 2 || pipe_rb == 4) && m % (2 * kNT) == 0 && pl.rpi == 8 && mloc % 8 == 0 && pl.nt && pl.ht) {
         auto fp = pipe_rb == 2 ? k_poisson_xr_pipe_f64<2, 4, XM> : k_poisson_xr_pipe_f64<4, 2, XM>;
         hipLaunchKernelGGL(fp, dim3((unsigned)grid), dim3(kNT), 0, s, pnh, poh, pqh, x, r, m, pl.nstrips, pl.nitems,

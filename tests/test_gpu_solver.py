@@ -878,15 +878,18 @@ def test_poisson_x_every_other_iteration_is_bitwise(monkeypatch, m, shards, peri
 @pytest.mark.parametrize("period", ["0", "3"])
 @pytest.mark.parametrize("m,shards", [(1024, None), (1024, [0, 0]), (512, [0] * 4)])
 def test_poisson_xr_pipelined_kernel_is_bitwise(monkeypatch, m, shards, period, rb):
-    """The software-pipelined k_poisson_xr_pipe_f64 (CGX_XR_PIPE = rows per
-    step; full 512-column strips, 8-row items) does k_poisson_xr_f64's
-    arithmetic row by row and item by item in the same order on the same grid:
-    x and the loop counts are bit for bit the plain kernel's after every way a
-    solve can end, with x every iteration and every third iteration."""
+    """The software-pipelined k_poisson_xr_pipe_f64 (CGX_XR_PIPE /
+    CGX_XR_PIPE_CATCHUP = rows per step for the no-x / catch-up kernels, the
+    catch-up's the default at 4; full 512-column strips, 8-row items) does
+    k_poisson_xr_f64's arithmetic row by row and item by item in the same order
+    on the same grid: x and the loop counts are bit for bit the plain kernel's
+    after every way a solve can end, with x every iteration and every third."""
     monkeypatch.setenv("CGX_POISSON_FUSED", "1")
     monkeypatch.setenv("CGX_XR_PIPE", rb)
+    monkeypatch.setenv("CGX_XR_PIPE_CATCHUP", rb)
     a = _poisson_x_runs(m, shards, period, monkeypatch)
     monkeypatch.setenv("CGX_XR_PIPE", "0")
+    monkeypatch.setenv("CGX_XR_PIPE_CATCHUP", "0")
     b = _poisson_x_runs(m, shards, period, monkeypatch)
     assert a.keys() == b.keys()
     for key in a:
