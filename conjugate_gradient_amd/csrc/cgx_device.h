@@ -101,6 +101,12 @@ __device__ __forceinline__ double wave_sum(double v) {
 // the ticket.  An agent-scope release on the ticket would add a buffer_wbl2
 // (write-back of the whole L2's dirty lines) per block: measured 378 vs 283 us
 // on a 537 MB k_update_r (round 1), for no change in what the consumer reads.
+// The rule holds for gfx950 (the only target this library builds for); a
+// build for another part stops here instead of compiling a hand-off whose
+// correctness would rest on that part's cache policy.
+#if defined(__HIP_DEVICE_COMPILE__) && !defined(__gfx950__)
+#error "cgx: the write-through reduction hand-off (kHandoffNote) is validated on gfx950 only"
+#endif
 template <int NT = kNT>
 __device__ __forceinline__ void grid_sum_last_block(double v, double *partials, unsigned *ticket,
                                                     double *out, bool add_to_out = false) {
