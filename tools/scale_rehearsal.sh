@@ -8,10 +8,10 @@
 # checked is the flow: every rank generates its 65536/P-row block, the timed
 # region runs, one JSON line comes from rank 0, and the true residual after
 # the fixed-count run is the single-GPU run's.
-#   gpurun -- 'bash tools/scale_rehearsal.sh' (round 3: prints the per-phase maxima and the RCCL identity)
+#   gpurun -- 'bash tools/scale_rehearsal.sh' (prints the per-phase maxima and the RCCL identity)
 set -euo pipefail
 export TMPDIR=/tmp
-OUT=gpurun_out/r03_scale_rehearsal
+OUT=gpurun_out/scale_rehearsal
 mkdir -p $OUT
 port=29631
 for P in 2 4 8; do
