@@ -481,6 +481,22 @@ __global__ __launch_bounds__(kNT) void k_poisson_xflush_f64(const double *__rest
 // and stores, as k_poisson_xr_pipe_f64 does.  Full strips, 8-row items, NT +
 // HT.  The halo-row stores (top of the first run, bottom of the last) stay
 // conditional: they are wave-uniform and rare.
+// Side-point addresses of one row (row base `row`) for the pipelined kernels,
+// whose loads are unconditional.  Only the block's outer waves use them (the
+// inner waves take their neighbours' edges from LDS); with `hot` set, every
+// other wave loads that one L2-resident double instead, so the only side loads
+// that reach memory are the outer waves' (as in the plain kernels).  Without
+// it every wave loads its neighbours' edge columns: lines the neighbouring
+// wave streams with non-temporal loads.
+struct SidePts {
+    const double *l, *r;
+};
+__device__ __forceinline__ SidePts side_pts(const double *row, const StripLane &L, int64_t m, const double *__restrict__ hot) {
+    SidePts s;
+    s.l = (L.has_l || !hot) ? row + (L.jw > 0 ? L.jw - 1 : 0) : hot;
+    s.r = (L.has_r || !hot) ? row + (L.jw + 128 < m ? L.jw + 128 : m - 1) : hot;
+    return s;
+}
 template <int RBn, bool FIRST>
 struct PSet {
     d2 rv[RBn], pv[RBn];
@@ -489,19 +505,20 @@ struct PSet {
 template <int RBn, bool FIRST>
 __device__ __forceinline__ void p_pipe_load(PSet<RBn, FIRST> &S, const double *__restrict__ rh,
                                             const double *__restrict__ poh, int64_t m, int64_t i, const StripLane &L,
-                                            bool last) {
-    const int64_t cl = L.jw > 0 ? L.jw - 1 : 0, cr = L.jw + 128 < m ? L.jw + 128 : m - 1;
+                                            bool last, const double *__restrict__ hot) {
 #pragma unroll
     for (int t = 0; t < RBn; ++t) {
         const int64_t hc = (i + t + 1) * m;
         const bool ht = last && t >= RBn - 2;  // the next item's first two rows: default policy (HT)
         S.rv[t] = ht ? lds2<false>(rh + hc + m, L.off) : lds2<true>(rh + hc + m, L.off);
         if constexpr (!FIRST) S.pv[t] = ht ? lds2<false>(poh + hc + m, L.off) : lds2<true>(poh + hc + m, L.off);
-        S.rl[t] = rh[hc + cl];
-        S.rr[t] = rh[hc + cr];
+        const SidePts sr = side_pts(rh + hc, L, m, hot);
+        S.rl[t] = *sr.l;
+        S.rr[t] = *sr.r;
         if constexpr (!FIRST) {
-            S.pl[t] = poh[hc + cl];
-            S.pr[t] = poh[hc + cr];
+            const SidePts sp = side_pts(poh + hc, L, m, hot);
+            S.pl[t] = *sp.l;
+            S.pr[t] = *sp.r;
         }
     }
 }
@@ -558,7 +575,7 @@ template <int RBn, int NS, bool FIRST>
 __device__ __forceinline__ double poisson_p_pipe_body(const double *__restrict__ rh, const double *__restrict__ poh,
                                                       double *__restrict__ pnh, int64_t mloc, int64_t m,
                                                       int64_t nstrips, ItemRanges ir, double beta, double *edge,
-                                                      int bands) {
+                                                      int bands, const double *__restrict__ hot) {
     constexpr int64_t kRpi = RBn * NS;
     double acc = 0.0;
     const Band bd = bands ? band_of(ir.w0, ir.cnt1, nstrips, bands) : Band{0, 0, 0, 0, 0};
@@ -575,7 +592,7 @@ __device__ __forceinline__ double poisson_p_pipe_body(const double *__restrict__
     d2 pc = p_form<FIRST>(lds2<false>(rh + (i0 + 1) * m, L.off),
                           FIRST ? (d2)(0.0) : lds2<false>(poh + (i0 + 1) * m, L.off), beta);
     PSet<RBn, FIRST> S[2];
-    p_pipe_load<RBn, FIRST>(S[0], rh, poh, m, i0, L, NS == 1);
+    p_pipe_load<RBn, FIRST>(S[0], rh, poh, m, i0, L, NS == 1, hot);
     for (;;) {
         if (i0 == 0) sts2<true>(pnh, L.off, pm);  // top halo row of p_k
         const int64_t vn = v + vstride < vend ? v + vstride : v;
@@ -586,7 +603,7 @@ __device__ __forceinline__ double poisson_p_pipe_body(const double *__restrict__
 #pragma unroll
         for (int s = 0; s < NS; ++s) {
             if (s + 1 < NS) {
-                p_pipe_load<RBn, FIRST>(S[(s + 1) & 1], rh, poh, m, i0 + (s + 1) * RBn, L, s + 2 == NS);
+                p_pipe_load<RBn, FIRST>(S[(s + 1) & 1], rh, poh, m, i0 + (s + 1) * RBn, L, s + 2 == NS, hot);
             } else {
                 rmn = lds2<false>(rh + i0n * m, Ln.off);
                 rcn = lds2<false>(rh + (i0n + 1) * m, Ln.off);
@@ -594,7 +611,7 @@ __device__ __forceinline__ double poisson_p_pipe_body(const double *__restrict__
                     pmn = lds2<false>(poh + i0n * m, Ln.off);
                     pcn = lds2<false>(poh + (i0n + 1) * m, Ln.off);
                 }
-                p_pipe_load<RBn, FIRST>(S[(s + 1) & 1], rh, poh, m, i0n, Ln, NS == 1);
+                p_pipe_load<RBn, FIRST>(S[(s + 1) & 1], rh, poh, m, i0n, Ln, NS == 1, hot);
             }
             p_pipe_step<RBn, FIRST>(S[s & 1], pnh, mloc, m, i0 + s * RBn, L, beta, pm, pc, acc,
                                     edge + (s & 1) * (kWaves * 2 * kEdgeRB));
@@ -614,7 +631,8 @@ __global__ __launch_bounds__(kNT) void k_poisson_p_pipe_f64(const double *__rest
                                                             int64_t mloc, int64_t m, int64_t nstrips, ItemRanges ir,
                                                             const double *rr, const double *rsold, int first,
                                                             ConvArgs cv, double *dot_out, int add_to_out,
-                                                            double *partials, unsigned *ticket, int bands) {
+                                                            double *partials, unsigned *ticket, int bands,
+                                                            const double *__restrict__ hot) {
     static_assert(RBn <= kEdgeRB && NS % 2 == 0, "edge buffer / set parity");
     __shared__ double edge[2 * kWaves * 2 * kEdgeRB];
     if (cv.kdone) {
@@ -626,7 +644,7 @@ __global__ __launch_bounds__(kNT) void k_poisson_p_pipe_f64(const double *__rest
     }
     // p_0 = r_0 (first) is its own instantiation: the other one's registers are what set the occupancy
     const double acc = poisson_p_pipe_body<RBn, NS, FIRST>(rh, poh, pnh, mloc, m, nstrips, ir,
-                                                          FIRST ? 0.0 : cg_ratio(*rr, *rsold), edge, bands);
+                                                          FIRST ? 0.0 : cg_ratio(*rr, *rsold), edge, bands, hot);
     grid_sum_last_block(acc, partials, ticket, dot_out, add_to_out != 0);
 }
 
@@ -656,8 +674,7 @@ template <int RBn, int XM>
 __device__ __forceinline__ void xr_pipe_load(XrSet<RBn, XM> &S, const double *__restrict__ pnh,
                                              const double *__restrict__ poh, const double *__restrict__ pqh,
                                              const double *__restrict__ x, const double *__restrict__ r, int64_t m,
-                                             int64_t i, const StripLane &L, bool last) {
-    const int64_t cl = L.jw > 0 ? L.jw - 1 : 0, cr = L.jw + 128 < m ? L.jw + 128 : m - 1;
+                                             int64_t i, const StripLane &L, bool last, const double *__restrict__ hot) {
 #pragma unroll
     for (int t = 0; t < RBn; ++t) {
         const int64_t hc = (i + t + 1) * m, ic = (i + t) * m;
@@ -667,8 +684,9 @@ __device__ __forceinline__ void xr_pipe_load(XrSet<RBn, XM> &S, const double *__
         if constexpr (XM >= 2) S.po[t] = lds2<true>(poh + hc, L.off);
         if constexpr (XM == 3) S.pq[t] = lds2<true>(pqh + hc, L.off);
         S.rv[t] = lds2<true>(r + ic, L.off);
-        S.el[t] = pnh[hc + cl];
-        S.er[t] = pnh[hc + cr];
+        const SidePts sp = side_pts(pnh + hc, L, m, hot);
+        S.el[t] = *sp.l;
+        S.er[t] = *sp.r;
     }
 }
 template <int RBn, int XM>
@@ -733,7 +751,7 @@ __global__ __launch_bounds__(kNT) void k_poisson_xr_pipe_f64(const double *__res
                                                              int64_t nitems, int reverse, const double *rsold,
                                                              const double *pAp, double *rr_out, double *xalpha,
                                                              double *partials, unsigned *ticket, const int64_t *gate,
-                                                             int bands) {
+                                                             int bands, const double *__restrict__ hot) {
     static_assert(RBn <= kEdgeRB && NS % 2 == 0, "edge buffer / set parity");
     constexpr int64_t kRpi = RBn * NS;
     __shared__ double edge[2 * kWaves * 2 * kEdgeRB];
@@ -751,7 +769,7 @@ __global__ __launch_bounds__(kNT) void k_poisson_xr_pipe_f64(const double *__res
         int64_t i0 = (w / nstrips) * kRpi;
         d2 pm = lds2<false>(pnh + i0 * m, L.off), pc = lds2<false>(pnh + (i0 + 1) * m, L.off);
         XrSet<RBn, XM> S[2];
-        xr_pipe_load<RBn, XM>(S[0], pnh, poh, pqh, x, r, m, i0, L, NS == 1);
+        xr_pipe_load<RBn, XM>(S[0], pnh, poh, pqh, x, r, m, i0, L, NS == 1, hot);
         for (;;) {
             // the next item (the last one again when there is none: loaded, never used)
             const int64_t vn = v + bd.stride < bd.count ? v + bd.stride : v;
@@ -763,11 +781,11 @@ __global__ __launch_bounds__(kNT) void k_poisson_xr_pipe_f64(const double *__res
             for (int s = 0; s < NS; ++s) {
                 if (s + 1 < NS) {
                     xr_pipe_load<RBn, XM>(S[(s + 1) & 1], pnh, poh, pqh, x, r, m, i0 + (s + 1) * RBn, L,
-                                          s + 2 == NS);
+                                          s + 2 == NS, hot);
                 } else {
                     pmn = lds2<false>(pnh + i0n * m, Ln.off);
                     pcn = lds2<false>(pnh + (i0n + 1) * m, Ln.off);
-                    xr_pipe_load<RBn, XM>(S[(s + 1) & 1], pnh, poh, pqh, x, r, m, i0n, Ln, NS == 1);
+                    xr_pipe_load<RBn, XM>(S[(s + 1) & 1], pnh, poh, pqh, x, r, m, i0n, Ln, NS == 1, hot);
                 }
                 xr_pipe_step<RBn, XM>(S[s & 1], x, r, m, i0 + s * RBn, L, alpha, alpha_prev, alpha_prev2, pm, pc, acc,
                                       edge + (s & 1) * (kWaves * 2 * kEdgeRB));
@@ -836,7 +854,7 @@ hipError_t stencil5_f64(const double *ph, int64_t mloc, int64_t m, double *Ap, d
 // short items keep the rows in flight in a narrow band (64- and 128-row items
 // are 7-20 % slower).
 struct PoissonPlan {
-    int rb, nt, ht, bands, band_rot;
+    int rb, nt, ht, bands, band_rot, side_edge;
     int64_t nstrips, rpi, nitems, grid;
 };
 static PoissonPlan poisson_plan(int64_t mloc, int64_t m) {
@@ -848,6 +866,8 @@ static PoissonPlan poisson_plan(int64_t mloc, int64_t m) {
     // (profiles/r03_poisson_bands_ab.jsonl); CGX_POISSON_BANDS=0 turns them off
     p.bands = env_int("CGX_POISSON_BANDS", 1);
     p.band_rot = std::max(0, env_int("CGX_POISSON_BAND_ROT", 0));
+    // pipelined kernels: side points loaded by the outer waves only (side_pts)
+    p.side_edge = env_int("CGX_PIPE_SIDE_EDGE", 1);
     p.nstrips = (m + 2 * kNT - 1) / (2 * kNT);
     p.rpi = std::max(1, env_int("CGX_STENCIL_ROWS", 8));
     p.nitems = p.nstrips * ((mloc + p.rpi - 1) / p.rpi);
@@ -899,7 +919,8 @@ static void launch_poisson_p(const PoissonPlan &pl, hipStream_t s, const double 
         const int pbands = pl.bands && ir.cnt2 == 0 && ir.cnt1 % pl.nstrips == 0 && pg >= 8 ? 1 + pl.band_rot : 0;
         if (pbands) pg &= ~int64_t(7);
         hipLaunchKernelGGL(fp, dim3((unsigned)pg), dim3(kNT), 0, s, rh, poh, pnh, mloc, m, pl.nstrips, ir, rr, rsold,
-                           first, cv, pap_out, add_to_out, ws.partials, ws.tickets + T_MATVEC, pbands);
+                           first, cv, pap_out, add_to_out, ws.partials, ws.tickets + T_MATVEC, pbands,
+                           pl.side_edge ? (rr ? rr : rh) : nullptr);
         return;
     }
     hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(kNT), 0, s, rh, poh, pnh, mloc, m, pl.nstrips, pl.rpi, ir, rr,
@@ -950,7 +971,8 @@ static void launch_poisson_xr(const PoissonPlan &pl, hipStream_t s, const double
     if ((pipe_rb == 2 || pipe_rb == 4) && m % (2 * kNT) == 0 && pl.rpi == 8 && mloc % 8 == 0 && pl.nt && pl.ht) {
         auto fp = pipe_rb == 2 ? k_poisson_xr_pipe_f64<2, 4, XM> : k_poisson_xr_pipe_f64<4, 2, XM>;
         hipLaunchKernelGGL(fp, dim3((unsigned)grid), dim3(kNT), 0, s, pnh, poh, pqh, x, r, m, pl.nstrips, pl.nitems,
-                           reverse, rsold, pAp, rr_out, xalpha, ws.partials, ws.tickets + T_XR, gate, bands);
+                           reverse, rsold, pAp, rr_out, xalpha, ws.partials, ws.tickets + T_XR, gate, bands,
+                           pl.side_edge ? rsold : nullptr);
         return;
     }
     hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(kNT), 0, s, pnh, poh, pqh, x, r, mloc, m, pl.nstrips, pl.rpi,

@@ -874,17 +874,21 @@ def test_poisson_x_every_other_iteration_is_bitwise(monkeypatch, m, shards, peri
     assert rel(a["solve1"][0], xo) <= TOL
 
 
+@pytest.mark.parametrize("side_edge", ["1", "0"])
 @pytest.mark.parametrize("rb", ["2", "4"])
 @pytest.mark.parametrize("period", ["0", "3"])
 @pytest.mark.parametrize("m,shards", [(1024, None), (1024, [0, 0]), (512, [0] * 4)])
-def test_poisson_xr_pipelined_kernel_is_bitwise(monkeypatch, m, shards, period, rb):
+def test_poisson_xr_pipelined_kernel_is_bitwise(monkeypatch, m, shards, period, rb, side_edge):
     """The software-pipelined k_poisson_xr_pipe_f64 (CGX_XR_PIPE /
     CGX_XR_PIPE_CATCHUP = rows per step for the no-x / catch-up kernels, the
     catch-up's the default at 4; full 512-column strips, 8-row items) does
     k_poisson_xr_f64's arithmetic row by row and item by item in the same order
     on the same grid: x and the loop counts are bit for bit the plain kernel's
-    after every way a solve can end, with x every iteration and every third."""
+    after every way a solve can end, with x every iteration and every third.
+    Side points loaded by the outer waves only (CGX_PIPE_SIDE_EDGE=1, the
+    default) or by every wave: the same values either way."""
     monkeypatch.setenv("CGX_POISSON_FUSED", "1")
+    monkeypatch.setenv("CGX_PIPE_SIDE_EDGE", side_edge)
     monkeypatch.setenv("CGX_XR_PIPE", rb)
     monkeypatch.setenv("CGX_XR_PIPE_CATCHUP", rb)
     a = _poisson_x_runs(m, shards, period, monkeypatch)
@@ -897,15 +901,17 @@ def test_poisson_xr_pipelined_kernel_is_bitwise(monkeypatch, m, shards, period, 
         assert a[key][1:] == b[key][1:], key
 
 
+@pytest.mark.parametrize("side_edge", ["1", "0"])
 @pytest.mark.parametrize("rb", ["2", "4"])
 @pytest.mark.parametrize("m,shards", [(1024, None), (512, [0] * 4)])
-def test_poisson_p_pipelined_kernel(monkeypatch, m, shards, rb):
+def test_poisson_p_pipelined_kernel(monkeypatch, m, shards, rb, side_edge):
     """The software-pipelined k_poisson_p_pipe_f64 (CGX_P_PIPE) forms the same
     p_k; it runs on its own occupancy's grid, so p.Ap adds in another order:
     the solve agrees with the plain kernel's to fp64 rounding in the same loop
     count (gated, halo overlap on 4 slabs with its interior / edge parts), and
     x every iteration / every third iteration stay bit for bit equal under it."""
     monkeypatch.setenv("CGX_POISSON_FUSED", "1")
+    monkeypatch.setenv("CGX_PIPE_SIDE_EDGE", side_edge)
     res = {}
     for pipe in ("0", rb):
         monkeypatch.setenv("CGX_P_PIPE", pipe)
