@@ -929,6 +929,28 @@ def test_poisson_p_pipelined_kernel(monkeypatch, m, shards, rb, side_edge):
         assert a[key][1:] == b[key][1:], key
 
 
+@pytest.mark.parametrize("pipe", ["0", "4"])
+@pytest.mark.parametrize("m,shards", [(1024, None), (512, [0] * 4), (130, [0, 0])])
+def test_poisson_mall_tail_stores_are_bitwise(monkeypatch, m, shards, pipe):
+    """CGX_MALL_TAIL_MB only changes the cache policy of the last items'
+    output stores (default-policy instead of non-temporal): x and the loop
+    counts are bit for bit those without it, for the plain and the pipelined
+    kernels, one slab and several.  A tail larger than the grid keeps every
+    store cached."""
+    monkeypatch.setenv("CGX_POISSON_FUSED", "1")
+    monkeypatch.setenv("CGX_XR_PIPE", pipe)
+    monkeypatch.setenv("CGX_XR_PIPE_CATCHUP", pipe)
+    monkeypatch.setenv("CGX_P_PIPE", pipe)
+    runs = {}
+    for tail in ("0", "1", "4096"):
+        monkeypatch.setenv("CGX_MALL_TAIL_MB", tail)
+        runs[tail] = _poisson_x_runs(m, shards, "3", monkeypatch)
+    for tail in ("1", "4096"):
+        for key in runs["0"]:
+            assert np.array_equal(runs[tail][key][0], runs["0"][key][0]), (tail, key)
+            assert runs[tail][key][1:] == runs["0"][key][1:], (tail, key)
+
+
 def test_poisson_fused_in_pieces_and_iteration_cap():
     """Iterations issued in several cgx_iterate calls (fixed count, then
     convergence-tested) give the one-call solve; a cap that stops exactly at
