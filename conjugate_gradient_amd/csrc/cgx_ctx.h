@@ -235,6 +235,9 @@ struct Shard {
     // overlap of the p exchange with the own-column-block matVec
     hipStream_t cstream = nullptr;
     hipEvent_t ev_pready = nullptr, ev_gathered = nullptr;
+    // graph capture of LOCAL fixed-count iterations (cgx_iterate.hip local_graph_*):
+    // the fork from shard 0's stream, the joins back into it
+    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_cjoin = nullptr;
 };
 
 }  // namespace cgxh
@@ -304,6 +307,13 @@ struct cgx_ctx {
     // LOCAL mode: one host thread per row block enqueues its block's iteration
     // (cgx_local_mt.hip); null when not used
     cgxh::LocalPool *pool = nullptr;
+    // LOCAL mode, fixed-count iterations, every block on one device: graphs of
+    // lgraph_iters iterations, one per ring residue of the first iteration,
+    // captured once and replayed (cgx_iterate.hip); lgraph_off after a failed
+    // capture (the eager path then runs)
+    hipGraphExec_t lgraph[4] = {};
+    int lgraph_iters = 0;
+    bool lgraph_off = false;
     // CGX_PHASES: resolved per-iteration phase durations (us), cgx_phase_times' order;
     // the wall clock's rate, and the previous stamped iteration's first start /
     // last end (ticks; 0 = none) so the gap across a resolve is still measured
@@ -353,6 +363,7 @@ int finish_create(cgx_ctx *c, cgx_ctx **out);
 int timing_resolve(cgx_ctx *c);
 int phase_iter_begin(cgx_ctx *c);
 int64_t *ts_of(cgx_ctx *c, const Shard &s, int kern);
+void local_graph_reset(cgx_ctx *c);  // cgx_iterate.hip: drop the captured iteration graphs
 void phase_iter_end(cgx_ctx *c);
 int phase_resolve(cgx_ctx *c);
 int progress_mark(cgx_ctx *c);

@@ -582,6 +582,21 @@ int do_iteration(cgx_ctx *c, double eps, int *stop, bool gated) {
     return CGX_OK;
 }
 
+// Drop the captured LOCAL iteration graphs (local_graph_iterate below).
+void local_graph_reset(cgx_ctx *c) {
+    bool any = false;
+    for (auto &g : c->lgraph) any = any || g;
+    if (!any) return;
+    if (!c->sh.empty()) {
+        (void)set_dev(c->sh[0]);
+        (void)hipStreamSynchronize(c->sh[0].stream);  // no replay still running
+    }
+    for (auto &g : c->lgraph) {
+        if (g) (void)hipGraphExecDestroy(g);
+        g = nullptr;
+    }
+}
+
 }  // namespace cgxh
 
 extern "C" {
@@ -679,6 +694,181 @@ int cgx_iterate(cgx_ctx *c, int64_t count, double eps, int64_t *done, int *conve
     return rc;
 }
 
+// ---- graph replay of the one-process multi-shard iteration (LOCAL) ---------------
+// Fixed-count iterations (eps < 0: nothing is read back or decided on the
+// host) enqueue the same launches, waits and records every iteration, with
+// arguments that depend on k only through ring(k).  One thread enqueuing S
+// row blocks pays 5S launches, 4S event records and ~3S^2 stream waits per
+// iteration (about 270 us at S = 8, profiles/r04_multishard_floor.jsonl).
+// Here G iterations (CGX_LOCAL_GRAPH_ITERS, default 8) are captured once per
+// ring residue of their first iteration into a hipGraph -- do_iteration's
+// own enqueues, so the results are bit for bit the eager path's -- and
+// replayed with one hipGraphLaunch.  Every block on one device (a capture
+// across devices is not attempted), no CGX_TIMING / CGX_PHASES (their
+// host-side bookkeeping is per iteration); CGX_LOCAL_GRAPH=0 turns it off,
+// =2 makes a failed capture an error instead of a quiet return to the eager
+// path (the tests use it, so a replay that never happens cannot pass).
+static bool local_graph_eligible(const cgx_ctx *c, double eps) {
+    if (eps >= 0.0 || c->lgraph_off || c->mode != M_LOCAL || c->sh.size() < 2 || c->pool) return false;
+    if (c->op != OP_DENSE || f32ref(c) || c->fused || c->fold_p || c->fused_p || c->ref_fused) return false;
+    if (c->flags & (CGX_TIMING | CGX_PHASES | CGX_HOST_STREAM | CGX_SYMMETRIC | CGX_COMM_P2P)) return false;
+    for (const auto &s : c->sh)
+        if (s.dev != c->sh[0].dev) return false;
+    const char *e = std::getenv("CGX_LOCAL_GRAPH");
+    return !(e && *e == '0');
+}
+
+// Capture `iters` iterations from c->k into *out (nothing runs; c->k and the
+// counters are restored).  Every stream the iteration uses joins the capture
+// from shard 0's stream and is joined back into it.
+static bool graph_dbg() {
+    static const bool on = [] {
+        const char *e = std::getenv("CGX_GRAPH_DEBUG");
+        return e && *e == '1';
+    }();
+    return on;
+}
+#define GDBG(...)                                 \
+    do {                                          \
+        if (graph_dbg()) {                        \
+            std::fprintf(stderr, "[cgx graph] "); \
+            std::fprintf(stderr, __VA_ARGS__);    \
+            std::fprintf(stderr, "\n");           \
+        }                                         \
+    } while (0)
+
+static int local_graph_capture(cgx_ctx *c, int iters, hipGraphExec_t *out) {
+    Shard &s0 = c->sh[0];
+    // one stream (the default): every block's streams are shard 0's stream
+    // while the iterations are captured, so the graph is the host's enqueue
+    // order as a chain -- a valid order, since a stream waits only on events
+    // already recorded.  The blocks share one device, whose kernels would
+    // contend for the same CUs anyway.  CGX_LOCAL_GRAPH_STREAMS=multi
+    // captures the blocks' own streams instead (forked from and joined back
+    // into shard 0's); with this ROCm, hipStreamEndCapture faulted in the
+    // host runtime at 4 blocks and more (profiles/r04_local_graph.md).
+    const char *ms = std::getenv("CGX_LOCAL_GRAPH_STREAMS");
+    const bool multi = ms && std::strcmp(ms, "multi") == 0;
+    GDBG("capture %d iterations from k=%lld, %zu blocks, %s", iters, (long long)c->k, c->sh.size(),
+         multi ? "multi-stream" : "one stream");
+    TRY(set_dev(s0));
+    const int64_t k0 = c->k, t0 = c->total_iters;
+    std::vector<std::pair<hipStream_t, hipStream_t>> saved;
+    if (!multi)
+        for (auto &s : c->sh) {
+            saved.push_back({s.stream, s.cstream});
+            s.stream = s0.stream;
+            if (s.cstream) s.cstream = s0.stream;
+        }
+    HIPT(hipStreamBeginCapture(s0.stream, hipStreamCaptureModeRelaxed));
+    int rc = [&]() -> int {
+        if (multi) {
+            HIPT(hipEventRecord(s0.ev_fork, s0.stream));
+            for (auto &s : c->sh) {
+                if (&s != &s0) HIPT(hipStreamWaitEvent(s.stream, s0.ev_fork, 0));
+                if (s.cstream) HIPT(hipStreamWaitEvent(s.cstream, s0.ev_fork, 0));
+            }
+        }
+        for (int i = 0; i < iters; ++i) {
+            int stop = 0;
+            GDBG("  iteration %d", i);
+            TRY(do_iteration(c, -1.0, &stop));
+        }
+        GDBG("  joins");
+        TRY(set_dev(s0));
+        if (multi)
+            for (auto &s : c->sh) {
+                if (&s != &s0) {
+                    HIPT(hipEventRecord(s.ev_join, s.stream));
+                    HIPT(hipStreamWaitEvent(s0.stream, s.ev_join, 0));
+                }
+                if (s.cstream) {
+                    HIPT(hipEventRecord(s.ev_cjoin, s.cstream));
+                    HIPT(hipStreamWaitEvent(s0.stream, s.ev_cjoin, 0));
+                }
+            }
+        return CGX_OK;
+    }();
+    if (!multi)
+        for (size_t i = 0; i < c->sh.size(); ++i) {
+            c->sh[i].stream = saved[i].first;
+            c->sh[i].cstream = saved[i].second;
+        }
+    c->k = k0;
+    c->total_iters = t0;
+    hipGraph_t g = nullptr;
+    GDBG("  end capture (rc %d)", rc);
+    const hipError_t ec = hipStreamEndCapture(s0.stream, &g);
+    GDBG("  ended: %s", hipGetErrorString(ec));
+    if (rc == CGX_OK && ec != hipSuccess) rc = fail(CGX_ERR_HIP, "hipStreamEndCapture: %s", hipGetErrorString(ec));
+    if (rc == CGX_OK) {
+        const hipError_t ei = hipGraphInstantiate(out, g, nullptr, nullptr, 0);
+        GDBG("  instantiated: %s", hipGetErrorString(ei));
+        if (ei != hipSuccess) {
+            *out = nullptr;
+            rc = fail(CGX_ERR_HIP, "hipGraphInstantiate: %s", hipGetErrorString(ei));
+        }
+    }
+    if (g) (void)hipGraphDestroy(g);
+    (void)hipGetLastError();
+    return rc;
+}
+
+// One replay on shard 0's stream, ordered after the work already queued on
+// every stream and before whatever is queued on them next.
+static int local_graph_launch(cgx_ctx *c, hipGraphExec_t ex) {
+    Shard &s0 = c->sh[0];
+    TRY(set_dev(s0));
+    for (auto &s : c->sh) {
+        if (&s != &s0) {
+            HIPT(hipEventRecord(s.ev_join, s.stream));
+            HIPT(hipStreamWaitEvent(s0.stream, s.ev_join, 0));
+        }
+        if (s.cstream) {
+            HIPT(hipEventRecord(s.ev_cjoin, s.cstream));
+            HIPT(hipStreamWaitEvent(s0.stream, s.ev_cjoin, 0));
+        }
+    }
+    GDBG("launch");
+    HIPT(hipGraphLaunch(ex, s0.stream));
+    GDBG("  launched");
+    HIPT(hipEventRecord(s0.ev_fork, s0.stream));
+    for (auto &s : c->sh) {
+        if (&s != &s0) HIPT(hipStreamWaitEvent(s.stream, s0.ev_fork, 0));
+        if (s.cstream) HIPT(hipStreamWaitEvent(s.cstream, s0.ev_fork, 0));
+    }
+    return CGX_OK;
+}
+
+// As many whole graphs of fixed-count iterations as fit in `count`; returns
+// how many iterations ran that way (the caller runs the rest eagerly).
+static int local_graph_iterate(cgx_ctx *c, int64_t count, int64_t *did) {
+    *did = 0;
+    const char *ge = std::getenv("CGX_LOCAL_GRAPH_ITERS");
+    const int G = std::max(1, std::min(256, (ge && *ge) ? std::atoi(ge) : 8));
+    if (G != c->lgraph_iters) {
+        local_graph_reset(c);
+        c->lgraph_iters = G;
+    }
+    while (count - *did >= G && c->state == ST_BEGUN) {
+        hipGraphExec_t &ex = c->lgraph[ring(c->k)];
+        if (!ex) {
+            const int rc = local_graph_capture(c, G, &ex);
+            if (rc != CGX_OK) {
+                const char *e = std::getenv("CGX_LOCAL_GRAPH");
+                if (e && *e == '2') return rc;  // strict (the tests): a capture that fails is an error
+                c->lgraph_off = true;           // else the eager path runs from here on
+                return CGX_OK;
+            }
+        }
+        TRY(local_graph_launch(c, ex));
+        c->k += G;
+        c->total_iters += G;
+        *did += G;
+    }
+    return CGX_OK;
+}
+
 static int iterate_calls(cgx_ctx *c, int64_t count, double eps, int64_t *done, int *converged) {
     const char *gv = std::getenv("CGX_GATED");
     const bool gate_ok = !(gv && *gv == '0');
@@ -686,6 +876,7 @@ static int iterate_calls(cgx_ctx *c, int64_t count, double eps, int64_t *done, i
     if (c->state == ST_BEGUN && count > 0 && eps >= 0.0 && !(c->flags & CGX_HOST_STREAM) && gate_ok)
         return iterate_gated(c, count, eps, done, converged);
     int64_t did = 0;
+    if (c->state == ST_BEGUN && local_graph_eligible(c, eps)) TRY(local_graph_iterate(c, count, &did));
     while (did < count && c->state == ST_BEGUN) {
         int stop = 0;
         TRY(do_iteration(c, eps, &stop));
@@ -804,6 +995,7 @@ int cgx_set_matvec_plan(cgx_ctx *c, int rows_per_wave, int chunks_in_flight, int
         s.fold_plan = pl;  // the folded matVec follows the same rows per wave and grid (same p.Ap order)
     }
     if (R > 2) c->fold_p = false;  // the folded matVec has one or two rows per wave
+    local_graph_reset(c);          // the captured iterations launch the old plan's kernels
     return CGX_OK;
 }
 

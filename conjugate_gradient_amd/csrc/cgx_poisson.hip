@@ -112,19 +112,6 @@ __device__ __forceinline__ void sts2(double *row, uint32_t off, d2 v) {
     else *p = v;
 }
 
-// MALL tail: the last `tail` items a block's band (or the grid) walks store
-// the output the NEXT kernel reads first with default-policy stores instead
-// of non-temporal ones, so those lines can still sit in the 256 MB
-// memory-side cache when that kernel -- walking the other way -- starts on
-// them (k_poisson_p's p_k for k_poisson_xr; k_poisson_xr's r for the next
-// k_poisson_p).  Values are unchanged; CGX_MALL_TAIL_MB sets the bytes per
-// stream (0: every store non-temporal).
-template <bool NT>
-__device__ __forceinline__ void sts2_keep(double *row, uint32_t off, d2 v, bool keep) {
-    if (keep) sts2<false>(row, off, v);
-    else sts2<NT>(row, off, v);
-}
-
 // One lane's view of a work item: column pair j, j+1 (byte offset `off`,
 // 0 for lanes past the grid), its wave wv and the wave's first column jw.
 // Side points: lane 0 needs column j-1, lane 63 column j+2.  Inside a block
@@ -134,7 +121,6 @@ __device__ __forceinline__ void sts2_keep(double *row, uint32_t off, d2 v, bool 
 // costs a 64-128 B line per 8-B value: +25 % of the fetched bytes (PMC).
 struct StripLane {
     bool valid, has_l, has_r;
-    bool keep;  // this item's streamed output stays cached (MALL tail, see sts2_keep)
     int wv;
     uint32_t off;
     int64_t jw;
@@ -149,7 +135,6 @@ __device__ __forceinline__ StripLane strip_lane(int64_t w, int64_t nstrips, int6
     L.off = L.valid ? (uint32_t)(j * 8) : 0u;
     L.has_l = L.wv == 0 && L.jw > 0;
     L.has_r = L.wv == kWaves - 1 && L.jw + 128 < m;
-    L.keep = false;
     return L;
 }
 __device__ __forceinline__ d2 keep(bool valid, d2 v) {
@@ -233,7 +218,7 @@ __device__ __forceinline__ void poisson_p_step(const double *__restrict__ rh, co
         o.y = 4.0 * ce[t].y - up.y - dn.y - ce[t].x - r;
         acc += ce[t].x * o.x + ce[t].y * o.y;  // zero on lanes past the grid
         if (L.valid) {
-            sts2_keep<NT>(pnh + (i + t + 1) * m, L.off, ce[t], L.keep);
+            sts2<NT>(pnh + (i + t + 1) * m, L.off, ce[t]);
             if (i + t == mloc - 1) sts2<NT>(pnh + (mloc + 1) * m, L.off, dn);  // bottom halo row of p_k
         }
     }
@@ -285,16 +270,14 @@ struct ItemRanges {
 template <int RB, bool NT, bool FIRST, bool HT>
 __device__ __forceinline__ double poisson_p_body(const double *__restrict__ rh, const double *__restrict__ poh,
                                                  double *__restrict__ pnh, int64_t mloc, int64_t m, int64_t nstrips,
-                                                 int64_t rpi, ItemRanges ir, double beta, double *edge, int bands,
-                                                 int64_t tail) {
+                                                 int64_t rpi, ItemRanges ir, double beta, double *edge, int bands) {
     double acc = 0.0;
     int par = 0;
     const Band bd = bands ? band_of(ir.w0, ir.cnt1, nstrips, bands) : Band{0, 0, 0, 0, 0};
     const int64_t vend = bands ? bd.count : ir.cnt1 + ir.cnt2;
     for (int64_t v = bands ? bd.start : blockIdx.x; v < vend; v += bands ? bd.stride : gridDim.x) {
         const int64_t w = bands ? band_item(bd, v) : v < ir.cnt1 ? ir.w0 + v : ir.w2 + (v - ir.cnt1);
-        StripLane L = strip_lane(w, nstrips, m);
-        L.keep = v >= vend - tail;
+        const StripLane L = strip_lane(w, nstrips, m);
         const int64_t i0 = (w / nstrips) * rpi;
         const int64_t i1 = (i0 + rpi < mloc) ? i0 + rpi : mloc;
         d2 pm = pnv<NT && !HT, FIRST>(rh + i0 * m, poh + i0 * m, L, beta);
@@ -316,8 +299,7 @@ __global__ __launch_bounds__(kNT) void k_poisson_p_f64(const double *__restrict_
                                                        double *__restrict__ pnh, int64_t mloc, int64_t m,
                                                        int64_t nstrips, int64_t rpi, ItemRanges ir, const double *rr,
                                                        const double *rsold, int first, ConvArgs cv, double *dot_out,
-                                                       int add_to_out, double *partials, unsigned *ticket, int bands,
-                                                       int64_t tail) {
+                                                       int add_to_out, double *partials, unsigned *ticket, int bands) {
     static_assert(RB <= kEdgeRB, "edge buffer");
     __shared__ double edge[2 * kWaves * 2 * kEdgeRB];
     if (cv.kdone) {
@@ -329,9 +311,9 @@ __global__ __launch_bounds__(kNT) void k_poisson_p_f64(const double *__restrict_
     }
     // p_0 = r_0 (first) has its own instantiation: no p_{k-1} loads
     const double acc = first ? poisson_p_body<RB, NT, true, HT>(rh, poh, pnh, mloc, m, nstrips, rpi, ir, 0.0, edge,
-                                                                bands, tail)
+                                                                bands)
                              : poisson_p_body<RB, NT, false, HT>(rh, poh, pnh, mloc, m, nstrips, rpi, ir,
-                                                                 cg_ratio(*rr, *rsold), edge, bands, tail);
+                                                                 cg_ratio(*rr, *rsold), edge, bands);
     grid_sum_last_block(acc, partials, ticket, dot_out, add_to_out != 0);
 }
 
@@ -407,7 +389,7 @@ __device__ __forceinline__ void poisson_xr_step(const double *__restrict__ pnh, 
         acc += L.valid ? rn.x * rn.x + rn.y * rn.y : 0.0;
         if (L.valid) {
             if constexpr (XM != 0) sts2<NT>(x + (i + t) * m, L.off, xn);
-            sts2_keep<NT>(r + (i + t) * m, L.off, rn, L.keep);
+            sts2<NT>(r + (i + t) * m, L.off, rn);
         }
     }
     if constexpr (RBn >= 2) {
@@ -430,8 +412,7 @@ __global__ __launch_bounds__(kNT) void k_poisson_xr_f64(const double *__restrict
                                                         int64_t m, int64_t nstrips, int64_t rpi, int64_t nitems,
                                                         int reverse, const double *rsold, const double *pAp,
                                                         double *rr_out, double *xalpha, double *partials,
-                                                        unsigned *ticket, const int64_t *gate, int bands,
-                                                        int64_t tail) {
+                                                        unsigned *ticket, const int64_t *gate, int bands) {
     static_assert(RB <= kEdgeRB, "edge buffer");
     __shared__ double edge[2 * kWaves * 2 * kEdgeRB];
     if (gate && *gate) return;
@@ -448,8 +429,7 @@ __global__ __launch_bounds__(kNT) void k_poisson_xr_f64(const double *__restrict
         // kernel (k_poisson_p, forward) last wrote p_k, so the first bytes read
         // may still sit in the 256 MB MALL
         const int64_t w = band_item(bd, reverse ? bd.count - 1 - v : v);
-        StripLane L = strip_lane(w, nstrips, m);
-        L.keep = v >= bd.count - tail;
+        const StripLane L = strip_lane(w, nstrips, m);
         const int64_t i0 = (w / nstrips) * rpi;
         const int64_t i1 = (i0 + rpi < mloc) ? i0 + rpi : mloc;
         d2 pm = keep(L.valid, lds2<NT && !HT>(pnh + i0 * m, L.off));
@@ -580,7 +560,7 @@ __device__ __forceinline__ void p_pipe_step(const PSet<RBn, FIRST> &S, double *_
         o.x = 4.0 * ce[t].x - up.x - dn.x - l - ce[t].y;
         o.y = 4.0 * ce[t].y - up.y - dn.y - ce[t].x - r;
         acc += ce[t].x * o.x + ce[t].y * o.y;
-        sts2_keep<true>(pnh + (i + t + 1) * m, L.off, ce[t], L.keep);
+        sts2<true>(pnh + (i + t + 1) * m, L.off, ce[t]);
     }
     if (i + RBn == mloc) sts2<true>(pnh + (mloc + 1) * m, L.off, pr[RBn - 1]);  // bottom halo row of p_k
     if constexpr (RBn >= 2) {
@@ -595,7 +575,7 @@ template <int RBn, int NS, bool FIRST>
 __device__ __forceinline__ double poisson_p_pipe_body(const double *__restrict__ rh, const double *__restrict__ poh,
                                                       double *__restrict__ pnh, int64_t mloc, int64_t m,
                                                       int64_t nstrips, ItemRanges ir, double beta, double *edge,
-                                                      int bands, const double *__restrict__ hot, int64_t tail) {
+                                                      int bands, const double *__restrict__ hot) {
     constexpr int64_t kRpi = RBn * NS;
     double acc = 0.0;
     const Band bd = bands ? band_of(ir.w0, ir.cnt1, nstrips, bands) : Band{0, 0, 0, 0, 0};
@@ -607,7 +587,6 @@ __device__ __forceinline__ double poisson_p_pipe_body(const double *__restrict__
     };
     int64_t v = vstart, w = item_of(v);
     StripLane L = strip_lane(w, nstrips, m);
-    L.keep = v >= vend - tail;
     int64_t i0 = (w / nstrips) * kRpi;
     d2 pm = p_form<FIRST>(lds2<false>(rh + i0 * m, L.off), FIRST ? (d2)(0.0) : lds2<false>(poh + i0 * m, L.off), beta);
     d2 pc = p_form<FIRST>(lds2<false>(rh + (i0 + 1) * m, L.off),
@@ -618,8 +597,7 @@ __device__ __forceinline__ double poisson_p_pipe_body(const double *__restrict__
         if (i0 == 0) sts2<true>(pnh, L.off, pm);  // top halo row of p_k
         const int64_t vn = v + vstride < vend ? v + vstride : v;
         const int64_t wn = item_of(vn);
-        StripLane Ln = strip_lane(wn, nstrips, m);
-        Ln.keep = vn >= vend - tail;
+        const StripLane Ln = strip_lane(wn, nstrips, m);
         const int64_t i0n = (wn / nstrips) * kRpi;
         d2 rmn, pmn, rcn, pcn;
 #pragma unroll
@@ -654,7 +632,7 @@ __global__ __launch_bounds__(kNT) void k_poisson_p_pipe_f64(const double *__rest
                                                             const double *rr, const double *rsold, int first,
                                                             ConvArgs cv, double *dot_out, int add_to_out,
                                                             double *partials, unsigned *ticket, int bands,
-                                                            const double *__restrict__ hot, int64_t tail) {
+                                                            const double *__restrict__ hot) {
     static_assert(RBn <= kEdgeRB && NS % 2 == 0, "edge buffer / set parity");
     __shared__ double edge[2 * kWaves * 2 * kEdgeRB];
     if (cv.kdone) {
@@ -666,7 +644,7 @@ __global__ __launch_bounds__(kNT) void k_poisson_p_pipe_f64(const double *__rest
     }
     // p_0 = r_0 (first) is its own instantiation: the other one's registers are what set the occupancy
     const double acc = poisson_p_pipe_body<RBn, NS, FIRST>(rh, poh, pnh, mloc, m, nstrips, ir,
-                                                          FIRST ? 0.0 : cg_ratio(*rr, *rsold), edge, bands, hot, tail);
+                                                          FIRST ? 0.0 : cg_ratio(*rr, *rsold), edge, bands, hot);
     grid_sum_last_block(acc, partials, ticket, dot_out, add_to_out != 0);
 }
 
@@ -755,7 +733,7 @@ __device__ __forceinline__ void xr_pipe_step(const XrSet<RBn, XM> &S, double *__
         rn.y = __builtin_fma(-alpha, o.y, S.rv[t].y);
         acc += rn.x * rn.x + rn.y * rn.y;
         if constexpr (XM != 0) sts2<true>(x + (i + t) * m, L.off, xn);
-        sts2_keep<true>(r + (i + t) * m, L.off, rn, L.keep);
+        sts2<true>(r + (i + t) * m, L.off, rn);
     }
     if constexpr (RBn >= 2) {
         pm = S.pr[RBn - 2];
@@ -773,8 +751,7 @@ __global__ __launch_bounds__(kNT) void k_poisson_xr_pipe_f64(const double *__res
                                                              int64_t nitems, int reverse, const double *rsold,
                                                              const double *pAp, double *rr_out, double *xalpha,
                                                              double *partials, unsigned *ticket, const int64_t *gate,
-                                                             int bands, const double *__restrict__ hot,
-                                                             int64_t tail) {
+                                                             int bands, const double *__restrict__ hot) {
     static_assert(RBn <= kEdgeRB && NS % 2 == 0, "edge buffer / set parity");
     constexpr int64_t kRpi = RBn * NS;
     __shared__ double edge[2 * kWaves * 2 * kEdgeRB];
@@ -789,7 +766,6 @@ __global__ __launch_bounds__(kNT) void k_poisson_xr_pipe_f64(const double *__res
         auto item_of = [&](int64_t v) { return band_item(bd, reverse ? bd.count - 1 - v : v); };
         int64_t v = bd.start, w = item_of(v);
         StripLane L = strip_lane(w, nstrips, m);
-        L.keep = v >= bd.count - tail;
         int64_t i0 = (w / nstrips) * kRpi;
         d2 pm = lds2<false>(pnh + i0 * m, L.off), pc = lds2<false>(pnh + (i0 + 1) * m, L.off);
         XrSet<RBn, XM> S[2];
@@ -798,8 +774,7 @@ __global__ __launch_bounds__(kNT) void k_poisson_xr_pipe_f64(const double *__res
             // the next item (the last one again when there is none: loaded, never used)
             const int64_t vn = v + bd.stride < bd.count ? v + bd.stride : v;
             const int64_t wn = item_of(vn);
-            StripLane Ln = strip_lane(wn, nstrips, m);
-            Ln.keep = vn >= bd.count - tail;
+            const StripLane Ln = strip_lane(wn, nstrips, m);
             const int64_t i0n = (wn / nstrips) * kRpi;
             d2 pmn, pcn;
 #pragma unroll
@@ -880,7 +855,6 @@ hipError_t stencil5_f64(const double *ph, int64_t mloc, int64_t m, double *Ap, d
 // are 7-20 % slower).
 struct PoissonPlan {
     int rb, nt, ht, bands, band_rot, side_edge;
-    int64_t tail_mb;
     int64_t nstrips, rpi, nitems, grid;
 };
 static PoissonPlan poisson_plan(int64_t mloc, int64_t m) {
@@ -894,21 +868,11 @@ static PoissonPlan poisson_plan(int64_t mloc, int64_t m) {
     p.band_rot = std::max(0, env_int("CGX_POISSON_BAND_ROT", 0));
     // pipelined kernels: side points loaded by the outer waves only (side_pts)
     p.side_edge = env_int("CGX_PIPE_SIDE_EDGE", 1);
-    p.tail_mb = std::max(0, env_int("CGX_MALL_TAIL_MB", 0));
     p.nstrips = (m + 2 * kNT - 1) / (2 * kNT);
     p.rpi = std::max(1, env_int("CGX_STENCIL_ROWS", 8));
     p.nitems = p.nstrips * ((mloc + p.rpi - 1) / p.rpi);
     p.grid = 0;  // set per kernel from its occupancy (resident_grid)
     return p;
-}
-
-// Items per band (bands: the blocks of one XCD walk one eighth of the runs)
-// or per grid walk whose output stores stay cached (sts2_keep): tail_mb MiB
-// of one output stream in all.
-static int64_t mall_tail(const PoissonPlan &pl, int bands) {
-    const int64_t item_bytes = pl.rpi * 2 * kNT * (int64_t)sizeof(double);
-    const int64_t items = (pl.tail_mb << 20) / item_bytes;
-    return bands ? items / 8 : items;
 }
 
 // Every block resident at once (occupancy x CUs), capped by the work items
@@ -956,16 +920,15 @@ static void launch_poisson_p(const PoissonPlan &pl, hipStream_t s, const double 
         if (pbands) pg &= ~int64_t(7);
         hipLaunchKernelGGL(fp, dim3((unsigned)pg), dim3(kNT), 0, s, rh, poh, pnh, mloc, m, pl.nstrips, ir, rr, rsold,
                            first, cv, pap_out, add_to_out, ws.partials, ws.tickets + T_MATVEC, pbands,
-                           pl.side_edge ? (rr ? rr : rh) : nullptr, mall_tail(pl, pbands));
+                           pl.side_edge ? (rr ? rr : rh) : nullptr);
         return;
     }
     hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(kNT), 0, s, rh, poh, pnh, mloc, m, pl.nstrips, pl.rpi, ir, rr,
-                       rsold, first, cv, pap_out, add_to_out, ws.partials, ws.tickets + T_MATVEC, bands,
-                       mall_tail(pl, bands));
+                       rsold, first, cv, pap_out, add_to_out, ws.partials, ws.tickets + T_MATVEC, bands);
 }
 using XrFn = void (*)(const double *, const double *, const double *, double *, double *, int64_t, int64_t, int64_t,
                      int64_t, int64_t, int, const double *, const double *, double *, double *, double *, unsigned *,
-                     const int64_t *, int, int64_t);
+                     const int64_t *, int);
 template <int RB, int XM>
 static XrFn xr_fn(const PoissonPlan &pl) {
     return pl.nt ? (pl.ht ? k_poisson_xr_f64<RB, true, true, XM> : k_poisson_xr_f64<RB, true, false, XM>)
@@ -1009,12 +972,11 @@ static void launch_poisson_xr(const PoissonPlan &pl, hipStream_t s, const double
         auto fp = pipe_rb == 2 ? k_poisson_xr_pipe_f64<2, 4, XM> : k_poisson_xr_pipe_f64<4, 2, XM>;
         hipLaunchKernelGGL(fp, dim3((unsigned)grid), dim3(kNT), 0, s, pnh, poh, pqh, x, r, m, pl.nstrips, pl.nitems,
                            reverse, rsold, pAp, rr_out, xalpha, ws.partials, ws.tickets + T_XR, gate, bands,
-                           pl.side_edge ? rsold : nullptr, mall_tail(pl, bands));
+                           pl.side_edge ? rsold : nullptr);
         return;
     }
     hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(kNT), 0, s, pnh, poh, pqh, x, r, mloc, m, pl.nstrips, pl.rpi,
-                       pl.nitems, reverse, rsold, pAp, rr_out, xalpha, ws.partials, ws.tickets + T_XR, gate, bands,
-                       mall_tail(pl, bands));
+                       pl.nitems, reverse, rsold, pAp, rr_out, xalpha, ws.partials, ws.tickets + T_XR, gate, bands);
 }
 
 hipError_t poisson_p_f64(const double *rh, const double *poh, double *pnh, int64_t mloc, int64_t m, const double *rr,

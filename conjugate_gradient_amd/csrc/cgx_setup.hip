@@ -30,6 +30,9 @@ int alloc_shard(cgx_ctx *c, Shard &s) {
     HIPT(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
     HIPT(hipEventCreateWithFlags(&s.ev_sync, hipEventDisableTiming));
     HIPT(hipEventCreateWithFlags(&s.ev_sync2, hipEventDisableTiming));
+    HIPT(hipEventCreateWithFlags(&s.ev_fork, hipEventDisableTiming));
+    HIPT(hipEventCreateWithFlags(&s.ev_join, hipEventDisableTiming));
+    HIPT(hipEventCreateWithFlags(&s.ev_cjoin, hipEventDisableTiming));
     HIPT(hipEventCreateWithFlags(&s.ev_root, hipEventDisableTiming));
     if (!s.ev_pready) HIPT(hipEventCreateWithFlags(&s.ev_pready, hipEventDisableTiming));
     const size_t abytes = (size_t)s.nloc * (size_t)c->lda * es;
@@ -235,6 +238,8 @@ void free_shard(Shard &s) {
         if (e) (void)hipEventDestroy(e);
     if (s.ev_sync) (void)hipEventDestroy(s.ev_sync);
     if (s.ev_sync2) (void)hipEventDestroy(s.ev_sync2);
+    for (hipEvent_t e : {s.ev_fork, s.ev_join, s.ev_cjoin})
+        if (e) (void)hipEventDestroy(e);
     if (s.ev_root) (void)hipEventDestroy(s.ev_root);
     for (int q = 0; q < kMaxCopyStreams; ++q)
         if (s.copy[q]) {
@@ -663,6 +668,7 @@ int cgx_destroy(cgx_ctx *ctx) {
     // aborted here instead of hanging in the stream syncs below
     const int rc = (ctx->mode == M_RCCL && !ctx->dead) ? sync_all(ctx) : CGX_OK;
     local_mt_stop(ctx);
+    local_graph_reset(ctx);
     for (auto &s : ctx->sh) free_shard(s);
     delete ctx;
     return rc;

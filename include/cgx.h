@@ -239,7 +239,10 @@ int cgx_create(cgx_ctx **ctx, int64_t n, int device, int flags);
  * may repeat: several row blocks on one GPU).  Exchange by pull kernels on
  * each consuming block's stream: one gather of p (k_gather_slices), one
  * rank-order combine per scalar (k_combine_peers); CGX_LOCAL_XCHG=copy:
- * one hipMemcpyPeerAsync per block pair instead (the same bits). */
+ * one hipMemcpyPeerAsync per block pair instead (the same bits).  With every
+ * block on one device, fixed-count cgx_iterate calls replay G = 8 captured
+ * iterations per hipGraphLaunch (CGX_LOCAL_GRAPH=0 off, CGX_LOCAL_GRAPH_ITERS
+ * = G; the same bits; not with CGX_TIMING / CGX_PHASES). */
 int cgx_create_multi(cgx_ctx **ctx, int64_t n, int nshards, const int *devices, int flags);
 
 /* One process per GPU (parallel_cg.c's one MPI rank per process): this

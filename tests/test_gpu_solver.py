@@ -147,6 +147,53 @@ def test_local_exchange_kernels_bitwise_equal_peer_copies(monkeypatch, kind, P):
         assert itk == so.iterations and rel(xk, xo) <= TOL
 
 
+@pytest.mark.parametrize("P", [2, 3, 8])
+@pytest.mark.parametrize("overlap", [True, False])
+def test_local_graph_replay_bitwise(monkeypatch, P, overlap):
+    """Fixed-count iterations of the one-process multi-shard loop replayed
+    from captured hipGraphs (CGX_LOCAL_GRAPH; G iterations per graph, one
+    graph per ring residue of its first iteration) give x bit for bit the
+    eager path's: pieces that are and are not multiples of G and start at
+    every ring residue, eager iterations between replays, a matVec plan
+    change between calls (the graphs are captured again), G = 1, 3 and 8.
+    CGX_LOCAL_GRAPH=2: a capture that fails is an error, so the replay did
+    run."""
+    n = 2048 if P != 3 else 2049
+    A, b = oracle.spd_hash(n, seed=11, dtype=np.float64)
+    x0 = np.full(n, 0.125)
+    flags = cg.CGX_F64 | (0 if overlap else cg.CGX_NO_OVERLAP)
+    monkeypatch.setenv("CGX_LOCAL_THREADS", "0")
+
+    def run(graph, G):
+        monkeypatch.setenv("CGX_LOCAL_GRAPH", graph)
+        monkeypatch.setenv("CGX_LOCAL_GRAPH_ITERS", str(G))
+        out = []
+        with cg.Solver(n, flags=flags, devices=[0] * P) as s:
+            s.set_system(A, b, x0)
+            s.begin()
+            for cnt in (8, 1, 16, 3, 13):
+                assert s.iterate(cnt, eps=-1.0)[0] == cnt
+                out.append(s.get_x())
+            s.set_matvec_plan(1, 8)
+            for cnt in (9, 24):
+                s.iterate(cnt, eps=-1.0)
+                out.append(s.get_x())
+            rn, bn = s.residual_norm()
+            x, st = s.solve(x0, eps=1e-10)  # the convergence-tested solve after replays (eager)
+            out.append(x)
+        return out, rn / bn, st.iterations
+
+    eager, rel0, it0 = run("0", 8)
+    for G in (1, 3, 8):
+        got, rel1, it1 = run("2", G)
+        assert len(got) == len(eager)
+        for i, (g, e) in enumerate(zip(got, eager)):
+            assert np.array_equal(g, e), (G, i)
+        assert rel1 == rel0 and it1 == it0
+    xo, so = oracle.cg_f64(A, b, x0, eps=1e-10)
+    assert it0 == so.iterations and rel(eager[-1], xo) <= TOL
+
+
 @pytest.mark.parametrize("P", [2, 4, 8])
 @pytest.mark.parametrize("name", ["kat4", "spd1024", "spd4096"])
 def test_row_block_shards_f64(golden, name, P):
@@ -927,28 +974,6 @@ def test_poisson_p_pipelined_kernel(monkeypatch, m, shards, rb, side_edge):
     for key in a:
         assert np.array_equal(a[key][0], b[key][0]), key
         assert a[key][1:] == b[key][1:], key
-
-
-@pytest.mark.parametrize("pipe", ["0", "4"])
-@pytest.mark.parametrize("m,shards", [(1024, None), (512, [0] * 4), (130, [0, 0])])
-def test_poisson_mall_tail_stores_are_bitwise(monkeypatch, m, shards, pipe):
-    """CGX_MALL_TAIL_MB only changes the cache policy of the last items'
-    output stores (default-policy instead of non-temporal): x and the loop
-    counts are bit for bit those without it, for the plain and the pipelined
-    kernels, one slab and several.  A tail larger than the grid keeps every
-    store cached."""
-    monkeypatch.setenv("CGX_POISSON_FUSED", "1")
-    monkeypatch.setenv("CGX_XR_PIPE", pipe)
-    monkeypatch.setenv("CGX_XR_PIPE_CATCHUP", pipe)
-    monkeypatch.setenv("CGX_P_PIPE", pipe)
-    runs = {}
-    for tail in ("0", "1", "4096"):
-        monkeypatch.setenv("CGX_MALL_TAIL_MB", tail)
-        runs[tail] = _poisson_x_runs(m, shards, "3", monkeypatch)
-    for tail in ("1", "4096"):
-        for key in runs["0"]:
-            assert np.array_equal(runs[tail][key][0], runs["0"][key][0]), (tail, key)
-            assert runs[tail][key][1:] == runs["0"][key][1:], (tail, key)
 
 
 def test_poisson_fused_in_pieces_and_iteration_cap():

@@ -5,7 +5,7 @@ timed four ways:
   enqueue_us  host time inside cgx_iterate per iteration (it returns without
               a sync for eps < 0, so this is the host's enqueue cost alone);
   wall_us     host time from the call to the end of cgx_synchronize;
-  enqueue_10_us  the same for 10 iterations right after a sync (empty queues:
+  enqueue_10_us  the same for 10 (enqueue_16_us: 16) iterations right after a sync (empty queues:
               the host's cost alone even when the device is the slower side);
   phases      the CGX_PHASES device-clock medians on shard 0.
 On one GPU the shards' kernels share the device, so wall_us is the sum of all
@@ -14,8 +14,10 @@ too.  Exchange forms (read at context creation), interleaved: "kernel" (the
 default: one pull kernel per consuming shard for p's gather, the two scalar
 combines folded into the update kernels, one enqueuing thread per block),
 "onethread" (the same, all enqueued by the calling thread), "nofuse" (CGX_LOCAL_FUSE=0: a
-combine kernel per shard and scalar) and "copy" (CGX_LOCAL_XCHG=copy: round
-3's hipMemcpyPeerAsync per pair).
+combine kernel per shard and scalar), "copy" (CGX_LOCAL_XCHG=copy: round
+3's hipMemcpyPeerAsync per pair) and "graph" (onethread's iterations captured
+G = CGX_LOCAL_GRAPH_ITERS at a time into a hipGraph and replayed; without
+CGX_PHASES, which the replay does not take, so that form has no phases).
 Usage:  python tools/r04_multishard_floor.py [rounds] [n,...] [S,...] [forms]
   > profiles/r04_multishard_floor.jsonl"""
 import json
@@ -27,8 +29,8 @@ sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import conjugate_gradient_amd as cg  # noqa: E402
 
 
-def run(n, shards, steps=200, warm=30):
-    flags = cg.CGX_PHASES
+def run(n, shards, steps=200, warm=32, phases=True):
+    flags = cg.CGX_PHASES if phases else 0
     with cg.Solver(n, flags=flags, devices=[0] * shards) as s:
         s.generate_spd(42)
         info = s.info
@@ -41,20 +43,26 @@ def run(n, shards, steps=200, warm=30):
         t1 = time.perf_counter()
         s.synchronize()
         t2 = time.perf_counter()
-        ph = s.phase_times()
+        ph = s.phase_times() if phases else {}
         # the enqueue alone, with the queues empty: 10 iterations (200 can fill
         # the hardware queues on one GPU and then time the device instead)
         t3 = time.perf_counter()
         s.iterate(10, eps=-1.0)
         t4 = time.perf_counter()
         s.synchronize()
+        t5 = time.perf_counter()  # 16 (two whole graphs of 8 in the graph form)
+        s.iterate(16, eps=-1.0)
+        t6 = time.perf_counter()
+        s.synchronize()
         rn, bn = s.residual_norm()
     return {"n": n, "shards": shards, "steps": steps, "exchange": ("copy" if os.environ.get("CGX_LOCAL_XCHG") == "copy" else
                                              "nofuse" if os.environ.get("CGX_LOCAL_FUSE") == "0" else
+                                             "graph" if os.environ.get("CGX_LOCAL_GRAPH") != "0" and not phases else
                                              "onethread" if os.environ.get("CGX_LOCAL_THREADS") == "0" else "kernel"),
             "flags": int(info.flags),
             "enqueue_us": round((t1 - t0) / steps * 1e6, 2), "wall_us": round((t2 - t0) / steps * 1e6, 2),
             "enqueue_10_us": round((t4 - t3) / 10 * 1e6, 2),
+            "enqueue_16_us": round((t6 - t5) / 16 * 1e6, 2),
             "relres": rn / bn,
             "phases_median_us": {k: round(v["median_us"], 2) for k, v in ph.items() if v["samples"]}}
 
@@ -70,8 +78,11 @@ def main():
                 for form in forms if S > 1 else forms[:1]:
                     os.environ["CGX_LOCAL_XCHG"] = "copy" if form == "copy" else "kernel"
                     os.environ["CGX_LOCAL_FUSE"] = "0" if form == "nofuse" else "1"
-                    os.environ["CGX_LOCAL_THREADS"] = "0" if form in ("onethread", "nofuse", "copy") else "1"
-                    out = run(n, S)
+                    os.environ["CGX_LOCAL_THREADS"] = "0" if form in ("onethread", "nofuse", "copy", "graph") else "1"
+                    os.environ["CGX_LOCAL_GRAPH"] = "2" if form == "graph" else "0"
+                    out = run(n, S, phases=form != "graph")
+                    if form == "graph":
+                        out["graph_iters"] = int(os.environ.get("CGX_LOCAL_GRAPH_ITERS", "8"))
                     out["round"] = r
                     print(json.dumps(out), flush=True)
 

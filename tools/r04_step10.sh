@@ -20,4 +20,3 @@ for r in csv.DictReader(open('$f')):
     k=re.search(r'k_poisson\w*(<[^>]*>)?', r['Name'])
     if k: print(k.group(0), r['Calls'], round(float(r['AverageNs'])/1000,1))"; done
 cat gpurun_out/r04_step10_strip_mix.json gpurun_out/r04_step10_hbm_mix.json
-bash tools/r04_step11.sh || exit 1
