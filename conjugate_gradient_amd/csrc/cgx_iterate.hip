@@ -711,6 +711,7 @@ int cgx_iterate(cgx_ctx *c, int64_t count, double eps, int64_t *done, int *conve
 static bool local_graph_eligible(const cgx_ctx *c, double eps) {
     if (eps >= 0.0 || c->lgraph_off || c->mode != M_LOCAL || c->sh.size() < 2 || c->pool) return false;
     if (c->op != OP_DENSE || f32ref(c) || c->fused || c->fold_p || c->fused_p || c->ref_fused) return false;
+    if (!c->xchg_kernels || !c->fuse_combine) return false;  // the forms the bitwise tests replay
     if (c->flags & (CGX_TIMING | CGX_PHASES | CGX_HOST_STREAM | CGX_SYMMETRIC | CGX_COMM_P2P)) return false;
     for (const auto &s : c->sh)
         if (s.dev != c->sh[0].dev) return false;
@@ -753,6 +754,7 @@ static int local_graph_capture(cgx_ctx *c, int iters, hipGraphExec_t *out) {
          multi ? "multi-stream" : "one stream");
     TRY(set_dev(s0));
     const int64_t k0 = c->k, t0 = c->total_iters;
+    HIPT(hipStreamBeginCapture(s0.stream, hipStreamCaptureModeRelaxed));
     std::vector<std::pair<hipStream_t, hipStream_t>> saved;
     if (!multi)
         for (auto &s : c->sh) {
@@ -760,7 +762,6 @@ static int local_graph_capture(cgx_ctx *c, int iters, hipGraphExec_t *out) {
             s.stream = s0.stream;
             if (s.cstream) s.cstream = s0.stream;
         }
-    HIPT(hipStreamBeginCapture(s0.stream, hipStreamCaptureModeRelaxed));
     int rc = [&]() -> int {
         if (multi) {
             HIPT(hipEventRecord(s0.ev_fork, s0.stream));
