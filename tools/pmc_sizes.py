@@ -21,6 +21,9 @@ def short(name):
     if m.group(1) == "k_poisson_xr_f64" and m.group(2) and m.group(2).count(",") == 3:
         # x every other iteration: the variants move different bytes (XM = last argument)
         return f"k_poisson_xr_f64<XM={m.group(2).strip('<>').split(',')[-1].strip()}>"
+    if m.group(1) == "k_poisson_xr_pipe_f64" and m.group(2) and m.group(2).count(",") == 2:
+        # the software-pipelined form <RB, NS, XM>
+        return f"k_poisson_xr_pipe_f64<XM={m.group(2).strip('<>').split(',')[-1].strip()}>"
     return m.group(1)
 
 
@@ -31,14 +34,17 @@ def algorithmic(w, kernel, n, m):
     if w == "symmetric" and kernel == "k_symv_f64":
         t = n // 128
         return 8 * 128 * 128 * t * (t + 1) // 2 + 16 * n  # tiles + p + y (partials are overhead)
-    if w == "poisson" and kernel == "k_poisson_p_f64":
+    if w == "poisson" and kernel in ("k_poisson_p_f64", "k_poisson_p_pipe_f64"):
         return 24 * m * m
-    if w == "poisson" and kernel in ("k_poisson_xr_f64", "k_poisson_xr_f64<XM=1>"):
+    xr = kernel.replace("_pipe", "")
+    if w == "poisson" and xr in ("k_poisson_xr_f64", "k_poisson_xr_f64<XM=1>"):
         return 40 * m * m + 16 * m
-    if w == "poisson" and kernel == "k_poisson_xr_f64<XM=0>":  # p_k (+ halo rows), r -> r
+    if w == "poisson" and xr == "k_poisson_xr_f64<XM=0>":  # p_k (+ halo rows), r -> r
         return 24 * m * m + 16 * m
-    if w == "poisson" and kernel == "k_poisson_xr_f64<XM=2>":  # p_{k-1}, p_k (+ halo), x, r -> x, r
+    if w == "poisson" and xr == "k_poisson_xr_f64<XM=2>":  # p_{k-1}, p_k (+ halo), x, r -> x, r
         return 48 * m * m + 16 * m
+    if w == "poisson" and xr == "k_poisson_xr_f64<XM=3>":  # p_{k-2}, p_{k-1}, p_k (+ halo), x, r -> x, r
+        return 56 * m * m + 16 * m
     if w == "poisson" and kernel == "k_poisson_xflush_f64":
         return 24 * m * m
     return None
