@@ -21,14 +21,16 @@ def short(name):
     if m.group(1) == "k_poisson_xr_f64" and m.group(2) and m.group(2).count(",") == 3:
         # x every other iteration: the variants move different bytes (XM = last argument)
         return f"k_poisson_xr_f64<XM={m.group(2).strip('<>').split(',')[-1].strip()}>"
-    if m.group(1) == "k_poisson_xr_pipe_f64" and m.group(2) and m.group(2).count(",") == 2:
-        # the software-pipelined form <RB, NS, XM>
-        return f"k_poisson_xr_pipe_f64<XM={m.group(2).strip('<>').split(',')[-1].strip()}>"
+    if m.group(1) == "k_poisson_xr_pipe_f64" and m.group(2) and m.group(2).count(",") >= 2:
+        # the software-pipelined form <RB, NS, XM[, variant flags]>
+        return f"k_poisson_xr_pipe_f64<XM={m.group(2).strip('<>').split(',')[2].strip()}>"
     return m.group(1)
 
 
 def algorithmic(w, kernel, n, m):
-    """Bytes per launch (steady-state launch) of the kernels DESIGN prices."""
+    """Bytes per launch (steady-state launch) of the kernels DESIGN prices.
+    `w` may carry a variant suffix (poisson_et1): the part before '_' counts."""
+    w = w.split("_")[0]
     if w == "dense" and kernel == "k_matvec_f64":
         return 8 * n * n + 16 * n
     if w == "symmetric" and kernel == "k_symv_f64":
