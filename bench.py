@@ -341,8 +341,9 @@ def main(argv=None) -> int:
     # mistake for abbreviations of its options (--n, --m are ambiguous there)
     ap.add_argument("--m", "--grid", dest="m", type=int, default=8192, help="Poisson grid width (n = m*m)")
     ap.add_argument("--comm", choices=["collective", "p2p", "nooverlap", "deterministic"], default="collective",
-                    help="exchange: RCCL collectives with the p allgather overlapped (default), "
-                         "point-to-point_cg.c's gather-to-root + send-to-all (p2p), collectives "
+                    help="exchange: RCCL collectives, the p allgather overlapped with the own-block matVec "
+                         "when the context measured that faster at creation (default; the same bits either "
+                         "way), point-to-point_cg.c's gather-to-root + send-to-all (p2p), collectives "
                          "without overlap, or the scalars combined in rank order (deterministic)")
     ap.add_argument("--n", "--size", dest="n", type=int, default=None,
                     help="system size (default 65536 dense, 131072 stream)")
@@ -416,6 +417,7 @@ def main(argv=None) -> int:
         solver = cg.Solver(n, device=0, flags=flags, poisson_m=m)
     nloc = solver.info.nrows // len(devices or [0])
     overlap_on = bool(solver.info.flags & cg.CGX_OVERLAP_ACTIVE)
+    overlap = solver.overlap_info() if world > 1 and not (poisson or stream or symmetric) else None
     fused = bool(solver.info.flags & cg.CGX_FUSED_ACTIVE)
     # fused Poisson: x every other (or third) iteration
     xperiod = (3 if solver.info.flags & cg.CGX_XDEFER3_ACTIVE else 2) if solver.info.flags & cg.CGX_XDEFER_ACTIVE else 1
@@ -511,8 +513,9 @@ def main(argv=None) -> int:
     # The roofline takes the slowest rank's kernel spans (max over ranks);
     # matvec_ms stays the CGX_TIMING event figure of earlier rounds.
     mv_kernel_ms = None
-    if all_ph is not None and world > 1 and all_ph[0]["matvec_own"]["samples"] > 0:
-        mv_kernel_ms = max(ph["matvec_own"]["median_us"] + ph["matvec"]["median_us"] for ph in all_ph) / 1e3
+    if all_ph is not None and world > 1 and all_ph[0]["matvec"]["samples"] > 0:
+        mv_kernel_ms = max((ph["matvec_own"]["median_us"] if ph["matvec_own"]["samples"] else 0.0)
+                           + ph["matvec"]["median_us"] for ph in all_ph) / 1e3
     achieved = (link_bytes if link_bound else bytes_launch) / ((mv_kernel_ms or mv_ms) * 1e-3) / 1e9
     traffic, traffic_src = (None, None) if (stream or poisson) else pmc_traffic(n, world,
                                                                                "_symmetric" if symmetric else "")
@@ -560,7 +563,8 @@ def main(argv=None) -> int:
                          if devices else
                          "RCCL halo ncclSend/Recv + 2x allreduce" if poisson else
                          "point-to-point_cg.c pattern: ncclSend/Recv via rank 0" if args.comm == "p2p" else
-                         "RCCL allgather(p) overlapped + rank-ordered scalar combine (allgather of partials)"
+                         "RCCL allgather(p)" + (" overlapped" if overlap_on else "")
+                         + " + rank-ordered scalar combine (allgather of partials)"
                          if args.comm == "deterministic" else
                          "RCCL allgather(p) overlapped with own-block matVec + 2x allreduce"
                          if overlap_on else "RCCL allgather(p) + 2x allreduce"),
@@ -596,6 +600,8 @@ def main(argv=None) -> int:
         "iteration_gbps": (((24.0 + xr_bpp) if fused else 80.0) * n / (elapsed / args.steps) / 1e9)
         if poisson else None,
     }
+    if overlap is not None:
+        out["overlap"] = overlap
     if all_ph is not None:
         out["phases_us"] = phase_summary(all_ph, elapsed / args.steps * 1e3)
     if all_comm is not None:

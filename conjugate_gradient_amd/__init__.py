@@ -105,6 +105,15 @@ class CommInfo(ctypes.Structure):
                 ("device", ctypes.c_int), ("pci_bus_id", ctypes.c_char * 32)]
 
 
+class OverlapInfo(ctypes.Structure):
+    _fields_ = [("active", ctypes.c_int), ("decided_by", ctypes.c_int), ("allgather_us", ctypes.c_double),
+                ("split_us", ctypes.c_double), ("one_launch_us", ctypes.c_double), ("split_cost_us", ctypes.c_double)]
+
+
+# cgx_overlap_info.decided_by
+OVERLAP_DECIDED_BY = {0: "measured", 1: "forced_on", 2: "off", 3: "n/a"}
+
+
 class UniqueId(ctypes.Structure):
     _fields_ = [("bytes", ctypes.c_char * 128)]
 
@@ -134,6 +143,7 @@ def lib() -> ctypes.CDLL:
         "cgx_device_pci_bus_id": ([i32, ctypes.c_char_p, i32], i32),
         "cgx_device_link": ([i32, i32, ctypes.POINTER(i32), ctypes.POINTER(i32), ctypes.POINTER(i32)], i32),
         "cgx_get_comm_info": ([vp, ctypes.POINTER(CommInfo)], i32),
+        "cgx_get_overlap_info": ([vp, ctypes.POINTER(OverlapInfo)], i32),
         "cgx_get_phase_times": ([vp, ctypes.POINTER(PhaseTimes)], i32),
         "cgx_create": ([pctx, i64, i32, i32], i32),
         "cgx_create_multi": ([pctx, i64, i32, ctypes.POINTER(i32), i32], i32),
@@ -536,6 +546,17 @@ class Solver:
         _check(lib().cgx_get_comm_info(self._h, ctypes.byref(ci)), "cgx_get_comm_info")
         return {"rccl_nranks": ci.rccl_nranks, "rccl_device": ci.rccl_device, "rccl_rank": ci.rccl_rank,
                 "device": ci.device, "pci_bus_id": ci.pci_bus_id.decode()}
+
+    def overlap_info(self) -> dict:
+        """How the p exchange was chosen at creation (aligned row blocks): the
+        overlapped form when the measured allgather takes longer than the
+        matVec's split into two launches costs (cgx_get_overlap_info)."""
+        o = OverlapInfo()
+        _check(lib().cgx_get_overlap_info(self._h, ctypes.byref(o)), "cgx_get_overlap_info")
+        r = lambda v: None if v < 0 else round(v, 2)  # noqa: E731
+        return {"on": bool(o.active), "decided_by": OVERLAP_DECIDED_BY.get(o.decided_by, str(o.decided_by)),
+                "allgather_us": r(o.allgather_us), "split_cost_us": r(o.split_cost_us), "split_us": r(o.split_us),
+                "one_launch_us": r(o.one_launch_us)}
 
     def reset_timing(self) -> None:
         _check(lib().cgx_reset_timing(self._h), "cgx_reset_timing")

@@ -263,7 +263,18 @@ struct cgx_ctx {
     int converged = 0;
     double solve_ms = 0.0, matvec_ms = 0.0;
     int64_t matvec_count = 0, total_iters = 0;
+    // Row blocks aligned to the matVec's 128-column chunks (dense fp64,
+    // resident A, several blocks): every matVec of the context runs the
+    // rotated column order -- the block's own columns first, then the rest --
+    // with the own part and the rest summed separately, so the overlapped
+    // exchange (own launch beside the allgather, then the rest) and the plain
+    // one (allgather, then one launch) give the same bits, and the choice
+    // between them (choose_overlap, at creation) is a matter of speed only.
+    bool rot = false;
     bool overlap = false;  // own-column-block matVec while p is exchanged
+    // what choose_overlap measured (-1: not measured) and how it decided
+    double ov_ag_us = -1.0, ov_split_us = -1.0, ov_one_us = -1.0, ov_cost_us = -1.0;
+    int ov_how = CGX_OV_NA;
     bool fused = false;    // Poisson: two-kernel fused iteration (k_poisson_p + k_poisson_xr)
     bool fused_p = false;  // dense, one GPU, small n: two launches per iteration (matVec, k_update_xrp_f64)
     bool fold_p = false;   // ... with the p update folded into the matVec (k_matvec_fold_f64, k_update_xr_stop_f64)
@@ -271,6 +282,13 @@ struct cgx_ctx {
     bool ref_fused = false;   // ... and on one GPU: two launches per iteration (matVec + p.Ap, x/r/r.r/p)
     bool halo_overlap = false;  // fused Poisson, several slabs: r's halo exchange overlaps k_poisson_p
     bool halo_pending = false;  // an overlapped r halo exchange is in flight on the comm streams
+    // fused Poisson, one process, several slabs (pull kernels): k_poisson_p
+    // reads r's halo rows in place from the neighbouring slabs instead of
+    // copies into rh's halo rows
+    bool halo_pull = false;
+    // ... and the r.r of iteration c->k is still partials only (its combine
+    // folded into the next k_poisson_p): settle_rr forms it when needed
+    bool rr_unsummed = false;
     // fused Poisson: x updated every other iteration (k_poisson_xr_f64's XM;
     // CGX_POISSON_XDEFER=0: every iteration).  Within one cgx_iterate call the
     // iterations k0, k0+2, ... leave x out and k0+1, k0+3, ... catch up; a call
@@ -282,6 +300,12 @@ struct cgx_ctx {
     // alphas left out cannot be placed, so x is incomplete until the next
     // cgx_solve_begin; cgx_get_x / cgx_iterate / cgx_residual_norm refuse it
     bool x_incomplete = false;
+    bool xalpha_pending = false;  // fused Poisson: an xr kernel left alpha_k p_k out of x (xmode 0), not yet caught up
+    // a cgx_iterate call failed part-way through an iteration (a HIP error, an
+    // RCCL deadline, a row block's worker): some blocks may have applied part
+    // of iteration k, so repeating it would apply it twice -- cgx_iterate
+    // refuses until the next cgx_solve_begin
+    bool iter_failed = false;
     // rank mode fail-fast (cgx_exchange.hip, rank_wait_*): every host wait
     // polls with a deadline of rccl_timeout_s seconds (CGX_RCCL_TIMEOUT_S,
     // default 60, 0 = wait forever) and checks the communicator's asynchronous
@@ -356,7 +380,7 @@ bool small_matvec(const cgx_ctx *c);  // k_matvec_small_f64 applies (cgx_setup.h
 void free_shard(Shard &s);
 int check_n(int64_t n, int nranks);
 cgx_ctx *new_ctx(int64_t n, int nranks, int flags);
-bool can_overlap(const cgx_ctx *c);
+bool can_rotate(const cgx_ctx *c);
 int alloc_overlap(cgx_ctx *c);
 int finish_create(cgx_ctx *c, cgx_ctx **out);
 // cgx_exchange.hip
@@ -376,6 +400,7 @@ int exchange_allgather(cgx_ctx *c, bool from_x);
 int exchange_scalar(cgx_ctx *c, int lslot, int gslot);
 PeerSum peer_sum(const cgx_ctx *c, const Shard &d, int lslot, int gslot);
 int overlapped_matvec(cgx_ctx *c, int dot_slot, bool gated);
+int choose_overlap(cgx_ctx *c);
 int exchange_halo_async(cgx_ctx *c);
 int settle_halo(cgx_ctx *c);
 int sync_all(cgx_ctx *c);
@@ -402,6 +427,7 @@ int do_begin(cgx_ctx *c);
 int read_scalar(cgx_ctx *c, int gslot, double *out);
 int do_iteration_poisson(cgx_ctx *c, double eps, int *stop, bool gated);
 int poisson_x_finish(cgx_ctx *c);
+int settle_rr(cgx_ctx *c);
 int check_x_complete(const cgx_ctx *c);
 int do_iteration(cgx_ctx *c, double eps, int *stop, bool gated = false);
 // cgx_api.hip

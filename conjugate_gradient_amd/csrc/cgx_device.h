@@ -7,6 +7,7 @@
 
 #include <cstdint>
 #include <cstdlib>
+#include <cstring>
 #include <mutex>
 
 namespace cgx {
@@ -341,6 +342,22 @@ inline int cu_count(int device) {
 inline int env_int(const char *name, int dflt) {
     const char *s = std::getenv(name);
     return (s && *s) ? std::atoi(s) : dflt;
+}
+
+// One key of a plan override held in one environment variable as
+// "key=value,key=value" (CGX_MV_PLAN, CGX_SMALL_PLAN, CGX_POISSON_PLAN,
+// CGX_SYM_PLAN): the value of `key`, or dflt.
+inline int env_opt(const char *name, const char *key, int dflt) {
+    const char *s = std::getenv(name);
+    if (!s) return dflt;
+    const size_t kl = std::strlen(key);
+    for (const char *p = s; *p;) {
+        if (std::strncmp(p, key, kl) == 0 && p[kl] == '=') return std::atoi(p + kl + 1);
+        const char *q = std::strchr(p, ',');
+        if (!q) break;
+        p = q + 1;
+    }
+    return dflt;
 }
 
 inline unsigned grid_1d(int64_t n, int per_block, unsigned cap) {

@@ -486,6 +486,174 @@ int overlapped_matvec(cgx_ctx *c, int dot_slot, bool gated) {
     return CGX_OK;
 }
 
+// ---- overlapped or plain: the choice at creation ------------------------------
+// The two forms of an aligned multi-shard iteration (c->rot) give the same
+// bits, so the choice is speed only.  The overlap hides the allgather behind
+// the own-block launch but pays for splitting the matVec in two (a second
+// launch's fill and drain: about 32 us per iteration at 8 row blocks of
+// N = 65536, 8 us at 2, profiles/r04_rank_kernel_trace_g*.csv); the plain form
+// exposes the allgather.  So the context times both matVec forms on each of its
+// row blocks (zeros at this point: the same bytes move) and the allgather of p
+// itself, and overlaps only when the allgather takes longer than the split
+// costs.  Rank mode: every rank measures and the maxima over ranks decide, so
+// the ranks agree (they would pair their collectives either way).
+// CGX_NO_OVERLAP / CGX_OVERLAP=0 and CGX_OVERLAP=1 / force override the
+// decision (the numbers are still measured and reported).
+static int measure_split(cgx_ctx *c) {
+    constexpr int kReps = 3;
+    double split = 0.0, one = 0.0, cost = 0.0;
+    for (auto &s : c->sh) {  // one block at a time: blocks sharing a GPU would contend
+        TRY(set_dev(s));
+        hipEvent_t ev[3] = {};
+        for (auto &e : ev) HIPT(hipEventCreate(&e));
+        const double *A = reinterpret_cast<const double *>(s.A), *v = reinterpret_cast<const double *>(s.pfull);
+        double *Ap = reinterpret_cast<double *>(s.Ap), *dot = reinterpret_cast<double *>(slot(s, S_TR));
+        const double *pown = reinterpret_cast<const double *>(s.pown);
+        float best_split = 1e30f, best_one = 1e30f;
+        int rc = CGX_OK;
+        for (int rep = 0; rep <= kReps && rc == CGX_OK; ++rep) {  // rep 0 warms up
+            rc = [&]() -> int {
+                HIPT(hipEventRecord(ev[0], s.stream));
+                HIPT(matvec_f64_cols(s.plan, A, c->lda, s.nloc, c->lda, s.row0, s.nloc, false, v, Ap, nullptr,
+                                     nullptr, s.ws, s.stream));
+                HIPT(matvec_f64_cols(s.plan, A, c->lda, s.nloc, c->lda, (s.row0 + s.nloc) % c->lda, c->lda - s.nloc,
+                                     true, v, Ap, pown, dot, s.ws, s.stream));
+                HIPT(hipEventRecord(ev[1], s.stream));
+                HIPT(matvec_f64_cols(s.plan, A, c->lda, s.nloc, c->lda, s.row0, c->lda, false, v, Ap, pown, dot, s.ws,
+                                     s.stream, nullptr, nullptr, s.nloc));
+                HIPT(hipEventRecord(ev[2], s.stream));
+                TRY(rank_wait_stream(c, s.stream, "the overlap calibration"));
+                float t1 = 0.f, t2 = 0.f;
+                HIPT(hipEventElapsedTime(&t1, ev[0], ev[1]));
+                HIPT(hipEventElapsedTime(&t2, ev[1], ev[2]));
+                if (rep > 0) {
+                    best_split = std::min(best_split, t1);
+                    best_one = std::min(best_one, t2);
+                }
+                return CGX_OK;
+            }();
+        }
+        for (auto e : ev) (void)hipEventDestroy(e);
+        TRY(rc);
+        split = std::max(split, 1e3 * best_split);
+        one = std::max(one, 1e3 * best_one);
+        cost = std::max(cost, 1e3 * (best_split - best_one));
+    }
+    c->ov_split_us = split;
+    c->ov_one_us = one;
+    c->ov_cost_us = cost;
+    return CGX_OK;
+}
+
+static int measure_allgather(cgx_ctx *c) {
+    constexpr int kReps = 8;
+    if (c->mode == M_RCCL) {
+        Shard &s = c->sh[0];
+        TRY(set_dev(s));
+        hipEvent_t ev[2] = {};
+        for (auto &e : ev) HIPT(hipEventCreate(&e));
+        int rc = [&]() -> int {
+            for (int i = 0; i < 2; ++i)  // warm: the ranks meet, RCCL sets up its channels
+                NCCLC(c, ncclAllGather(s.pown, s.pfull, (size_t)s.nloc, ncclDouble, s.comm, s.stream),
+                      "ncclAllGather(p), overlap calibration");
+            TRY(rank_wait_stream(c, s.stream, "the overlap calibration"));
+            HIPT(hipEventRecord(ev[0], s.stream));
+            for (int i = 0; i < kReps; ++i)
+                NCCLC(c, ncclAllGather(s.pown, s.pfull, (size_t)s.nloc, ncclDouble, s.comm, s.stream),
+                      "ncclAllGather(p), overlap calibration");
+            HIPT(hipEventRecord(ev[1], s.stream));
+            TRY(rank_wait_stream(c, s.stream, "the overlap calibration"));
+            float ms = 0.f;
+            HIPT(hipEventElapsedTime(&ms, ev[0], ev[1]));
+            c->ov_ag_us = 1e3 * ms / kReps;
+            return CGX_OK;
+        }();
+        for (auto e : ev) (void)hipEventDestroy(e);
+        return rc;
+    }
+    // one process: the exchange as the plain iteration runs it (events, then
+    // the pull kernels), per block from its stream's start to its gather's end
+    const int S = (int)c->sh.size();
+    std::vector<hipEvent_t> ev(2 * S, nullptr);
+    int rc = [&]() -> int {
+        for (int q = 0; q < S; ++q) {
+            TRY(set_dev(c->sh[q]));
+            HIPT(hipEventCreate(&ev[2 * q]));
+            HIPT(hipEventCreate(&ev[2 * q + 1]));
+        }
+        double best = 1e30;
+        for (int rep = 0; rep <= 3; ++rep) {
+            TRY(sync_all(c));
+            for (int q = 0; q < S; ++q) {
+                TRY(set_dev(c->sh[q]));
+                HIPT(hipEventRecord(ev[2 * q], c->sh[q].stream));
+            }
+            TRY(exchange_allgather(c, false));
+            for (int q = 0; q < S; ++q) {
+                TRY(set_dev(c->sh[q]));
+                HIPT(hipEventRecord(ev[2 * q + 1], c->sh[q].stream));
+            }
+            TRY(sync_all(c));
+            double worst = 0.0;
+            for (int q = 0; q < S; ++q) {
+                float ms = 0.f;
+                HIPT(hipEventElapsedTime(&ms, ev[2 * q], ev[2 * q + 1]));
+                worst = std::max(worst, 1e3 * (double)ms);
+            }
+            if (rep > 0) best = std::min(best, worst);
+        }
+        c->ov_ag_us = best;
+        return CGX_OK;
+    }();
+    for (auto e : ev)
+        if (e) (void)hipEventDestroy(e);
+    return rc;
+}
+
+int choose_overlap(cgx_ctx *c) {
+    if (p2p(c)) {  // point-to-point_cg.c's exchange: through rank 0, never overlapped
+        c->overlap = false;
+        c->ov_how = CGX_OV_NA;
+        return CGX_OK;
+    }
+    const char *e = std::getenv("CGX_OVERLAP");
+    int forced = -1;  // -1: measure and decide
+    if ((c->flags & CGX_NO_OVERLAP) || (e && *e == '0')) forced = 0;
+    else if (e && (*e == '1' || std::strcmp(e, "force") == 0)) forced = 1;
+    if (c->mode == M_LOCAL || c->nranks > 1) {
+        TRY(measure_split(c));
+        TRY(measure_allgather(c));
+        if (c->mode == M_RCCL) {  // the maxima over ranks, on every rank
+            Shard &s = c->sh[0];
+            TRY(set_dev(s));
+            double *h = s.h_pin;
+            h[0] = c->ov_ag_us;
+            h[1] = c->ov_split_us;
+            h[2] = c->ov_one_us;
+            h[3] = c->ov_cost_us;
+            HIPT(hipMemcpyAsync(slot(s, S_GATHER), h, 32, hipMemcpyHostToDevice, s.stream));
+            NCCLC(c, ncclAllReduce(slot(s, S_GATHER), slot(s, S_GATHER), 4, ncclDouble, ncclMax, s.comm, s.stream),
+                  "ncclAllReduce(max), overlap calibration");
+            HIPT(hipMemcpyAsync(h, slot(s, S_GATHER), 32, hipMemcpyDeviceToHost, s.stream));
+            TRY(rank_wait_stream(c, s.stream, "the overlap calibration"));
+            c->ov_ag_us = h[0];
+            c->ov_split_us = h[1];
+            c->ov_one_us = h[2];
+            c->ov_cost_us = h[3];
+        }
+    }
+    if (forced >= 0) {
+        c->overlap = forced == 1;
+        c->ov_how = forced ? CGX_OV_FORCED : CGX_OV_OFF;
+    } else {
+        c->overlap = c->ov_ag_us > c->ov_cost_us;
+        c->ov_how = CGX_OV_MEASURED;
+    }
+    debug_log("overlap %s (allgather %.1f us, split %.1f us, one launch %.1f us, cost %.1f us, how %d)",
+              c->overlap ? "on" : "off", c->ov_ag_us, c->ov_split_us, c->ov_one_us, c->ov_cost_us, c->ov_how);
+    return CGX_OK;
+}
+
 // Overlapped r halo exchange (several slabs): on the comm streams, after
 // everything already on the compute streams (the r update and the r.r
 // allreduce, so two RCCL operations never run at once).  The next

@@ -16,6 +16,14 @@ int matvec_rows(cgx_ctx *c, Shard &s, const MatvecPlan &pl, const char *Arows, i
         HIPT(matvec_ref_f32(reinterpret_cast<const float *>(Arows), c->lda, rows, c->n,
                             reinterpret_cast<const float *>(vec), reinterpret_cast<float *>(s.Ap) + r0, s.stream,
                             gate_of(s, gated)));
+    } else if (c->rot && Arows == s.A && r0 == 0 && rows == s.nloc) {
+        // the block's own columns, then the rest, summed apart and added: the
+        // overlapped form's bits in one launch (cgx_ctx::rot)
+        HIPT(matvec_f64_cols(pl, reinterpret_cast<const double *>(Arows), c->lda, rows, c->lda, s.row0, c->lda, false,
+                             reinterpret_cast<const double *>(vec), reinterpret_cast<double *>(s.Ap),
+                             fuse_dot ? reinterpret_cast<const double *>(s.pown) : nullptr,
+                             fuse_dot ? reinterpret_cast<double *>(slot(s, dot_slot)) : nullptr, s.ws, s.stream,
+                             gated ? reinterpret_cast<const int64_t *>(slot(s, S_KDONE)) : nullptr, ts, s.nloc));
     } else {
         HIPT(matvec_f64(pl, reinterpret_cast<const double *>(Arows), c->lda, rows, c->lda,
                         reinterpret_cast<const double *>(vec), reinterpret_cast<double *>(s.Ap) + r0,
@@ -208,7 +216,9 @@ int do_begin(cgx_ctx *c) {
         }
     }
     TRY(exchange_scalar(c, ls, gs));
-    if (c->fused) TRY(exchange_halo_of(c, &Shard::rh));  // r0's halo rows for k_poisson_p
+    c->rr_unsummed = false;
+    // r0's halo rows for k_poisson_p (which reads them in place itself with halo_pull)
+    if (c->fused && !c->halo_pull) TRY(exchange_halo_of(c, &Shard::rh));
     // The device-side convergence record {kdone, r.r} was reset by the residual
     // kernel above (k_residual_f64 / k_dot_ref_f32_blk<kDotResid>); the host copy here.
     for (auto &s : c->sh) s.h_rec[0] = s.h_rec[1] = 0;  // no kernel of this solve has run yet (do_begin follows a sync)
@@ -216,6 +226,8 @@ int do_begin(cgx_ctx *c) {
     c->converged = 0;
     c->state = ST_BEGUN;
     c->x_incomplete = false;
+    c->xalpha_pending = false;
+    c->iter_failed = false;
     return CGX_OK;
 }
 
@@ -267,19 +279,36 @@ int do_iteration_poisson(cgx_ctx *c, double eps, int *stop, bool gated) {
     const int64_t jx = (k - c->xd_k0) % c->xd;
     const int xmode = c->xd == 1 ? 1 : jx == c->xd - 1 ? c->xd : 0;
     const int xslot = S_XALPHA + (xmode == 0 ? (int)jx : 0);
-    for (auto &s : c->sh) {
+    // One process, several slabs (c->fuse_combine): the scalar combines are
+    // folded into the kernels that consume them -- p.Ap into k_poisson_xr,
+    // r.r into the next k_poisson_p (not when the host reads r.r after the
+    // iteration: then a combine kernel forms it) -- and r's halo rows are read
+    // in place from the neighbouring slabs by k_poisson_p (c->halo_pull).
+    // Both wait on the same cross-stream events the combines waited on.
+    const bool fold_rr = c->fuse_combine && (gated || eps < 0.0);
+    const int S = (int)c->sh.size();
+    const int64_t mloc = c->sh[0].nloc / m;
+    for (int q = 0; q < S; ++q) {
+        Shard &s = c->sh[q];
         TRY(set_dev(s));
         char *pold = poisson_slab(c, s, k - 1), *pnew = poisson_slab(c, s, k);
+        // the previous slab's last interior row of r, the next slab's first
+        const double *r_up = c->halo_pull && q > 0 ? D(c->sh[q - 1].rh) + mloc * m : nullptr;
+        const double *r_dn = c->halo_pull && q < S - 1 ? D(c->sh[q + 1].r) : nullptr;
+        const PeerSum rs = c->rr_unsummed ? peer_sum(c, s, S_LRR + ring(k), rk) : PeerSum{};
         for (int part : split ? std::initializer_list<int>{1, 2} : std::initializer_list<int>{0}) {
             if (part == 2) HIPT(hipStreamWaitEvent(s.stream, s.ev_gathered, 0));
-            HIPT(poisson_p_f64(D(s.rh), D(pold), D(pnew), s.nloc / m, m, D(slot(s, rk)), D(slot(s, rkm1)), k == 0,
+            HIPT(poisson_p_f64(D(s.rh), D(pold), D(pnew), mloc, m, D(slot(s, rk)), D(slot(s, rkm1)), k == 0,
                                D(slot(s, out_slot(c, pl, pg))), s.ws, s.stream, gated ? eps : -1.0, k,
                                gated ? reinterpret_cast<int64_t *>(slot(s, S_KDONE)) : nullptr,
-                               gated ? D(slot(s, S_RRFINAL)) : nullptr, part, rec_of(c, s, gated)));
+                               gated ? D(slot(s, S_RRFINAL)) : nullptr, part, rec_of(c, s, gated), r_up, r_dn,
+                               c->rr_unsummed ? &rs : nullptr));
         }
     }
+    c->rr_unsummed = false;
     c->halo_pending = false;
-    TRY(exchange_scalar(c, pl, pg));
+    if (c->fuse_combine) TRY(local_barrier(c));  // MPI_Allreduce(p.Ap): summed by k_poisson_xr itself
+    else TRY(exchange_scalar(c, pl, pg));
     const int rg = S_RR + ring(k + 1), rl = S_LRR + ring(k + 1);
     const int ro = out_slot(c, rl, rg);
     for (auto &s : c->sh) {
@@ -289,14 +318,22 @@ int do_iteration_poisson(cgx_ctx *c, double eps, int *stop, bool gated) {
         if (timing) HIPT(hipEventRecord(s.ev_t[2 * s.ev_used], s.stream));
         char *pnew = poisson_slab(c, s, k), *pold = poisson_slab(c, s, k - 1),
              *pq = c->xd == 3 ? poisson_slab(c, s, k - 2) : nullptr;
-        HIPT(poisson_xr_f64(D(pnew), D(pold), D(pq), D(s.x), D(s.r), s.nloc / m, m, D(slot(s, rk)), D(slot(s, pg)),
-                            D(slot(s, ro)), xmode, D(slot(s, xslot)), s.ws, s.stream, gate_of(s, gated)));
+        const PeerSum ps = c->fuse_combine ? peer_sum(c, s, pl, pg) : PeerSum{};
+        HIPT(poisson_xr_f64(D(pnew), D(pold), D(pq), D(s.x), D(s.r), mloc, m, D(slot(s, rk)), D(slot(s, pg)),
+                            D(slot(s, ro)), xmode, D(slot(s, xslot)), s.ws, s.stream, gate_of(s, gated),
+                            c->fuse_combine ? &ps : nullptr));
         if (timing) {
             HIPT(hipEventRecord(s.ev_t[2 * s.ev_used + 1], s.stream));
             s.ev_used++;
         }
     }
-    TRY(exchange_scalar(c, rl, rg));
+    c->xalpha_pending = xmode == 0;  // the catch-up (xmode xd) and every-iteration x (1) leave nothing out
+    if (fold_rr) {  // MPI_Allreduce(r.r): summed by the next k_poisson_p (or settle_rr)
+        TRY(local_barrier(c));
+        c->rr_unsummed = true;
+    } else {
+        TRY(exchange_scalar(c, rl, rg));
+    }
     c->k = k + 1;
     c->total_iters += 1;
     if (!gated && eps >= 0.0) {
@@ -310,7 +347,19 @@ int do_iteration_poisson(cgx_ctx *c, double eps, int *stop, bool gated) {
             return CGX_OK;
         }
     }
+    if (c->halo_pull) return CGX_OK;  // the next k_poisson_p reads the neighbours' rows itself
     return c->halo_overlap ? exchange_halo_async(c) : exchange_halo_of(c, &Shard::rh);
+}
+
+// The r.r of the last iteration enqueued, when its combine was left to the
+// next k_poisson_p (rr_unsummed): formed now by the combine kernels, for the
+// host to read (or a later call's first k_poisson_p, which sums the same
+// partials again).
+int settle_rr(cgx_ctx *c) {
+    if (!c->rr_unsummed) return CGX_OK;
+    TRY(exchange_scalar(c, S_LRR + ring(c->k), S_RR + ring(c->k)));
+    c->rr_unsummed = false;
+    return CGX_OK;
 }
 
 // The end of a cgx_iterate call (the device's loop count known: c->k): when
@@ -331,6 +380,7 @@ int poisson_x_finish(cgx_ctx *c) {
         }
     }
     c->xd_k0 = c->k;
+    c->xalpha_pending = false;
     return CGX_OK;
 }
 
@@ -616,8 +666,6 @@ static int iterate_gated(cgx_ctx *c, int64_t count, double eps, int64_t *done, i
     Shard &s0 = c->sh[0];
     const char *la = std::getenv("CGX_LOOKAHEAD");
     const int look = std::max(1, std::min(kLookRing - 1, (la && *la) ? std::atoi(la) : 2));
-    const char *le = std::getenv("CGX_LOOK_EVERY");  // an event after every E-th iteration
-    const int64_t every = std::max(1, (le && *le) ? std::atoi(le) : 1);
     const int64_t k0 = c->k;
     int64_t issued = 0, kd = 0;
     volatile int64_t *rec = s0.h_rec;  // {kdone, r.r bits}, stored by the deciding kernel
@@ -632,12 +680,11 @@ static int iterate_gated(cgx_ctx *c, int64_t count, double eps, int64_t *done, i
         int stop = 0;
         TRY(do_iteration(c, eps, &stop, /*gated=*/true));
         TRY(set_dev(s0));
-        if ((issued + 1) % every) continue;
-        const int64_t ev = (issued + 1) / every - 1;  // this event's index
+        const int64_t ev = issued;  // an event after every iteration
         HIPT(hipEventRecord(s0.ev_look[ev % kLookRing], s0.stream));
         if (ev >= look) {
             TRY(rank_wait_event(c, s0.ev_look[(ev - look) % kLookRing], "an earlier iteration"));
-            const int64_t synced = (ev - look + 1) * every - 1;  // the last iteration that event covers
+            const int64_t synced = ev - look;  // the last iteration that event covers
             // Only a record left by an iteration the event covers counts: the
             // host-mapped word may already show a later iteration's decision,
             // and acting on that would make the number of enqueued iterations
@@ -663,6 +710,7 @@ static int iterate_gated(cgx_ctx *c, int64_t count, double eps, int64_t *done, i
         c->state = ST_CONVERGED;
     } else {
         double rr = 0.0;
+        TRY(settle_rr(c));
         TRY(read_scalar(c, S_RR + ring(c->k), &rr));
         c->last_rr = rr;
         // The fused Poisson iteration decides a stop one iteration later (at
@@ -686,11 +734,18 @@ int cgx_iterate(cgx_ctx *c, int64_t count, double eps, int64_t *done, int *conve
     if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
     if (c->state == ST_IDLE) return fail(CGX_ERR_STATE, "cgx_iterate before cgx_solve_begin");
     TRY(check_x_complete(c));
+    if (c->iter_failed)
+        return fail(CGX_ERR_STATE, "an earlier cgx_iterate failed part-way through iteration %lld: the solve "
+                                   "cannot continue (cgx_solve_begin starts a new one)", (long long)c->k);
     const int rc = iterate_calls(c, count, eps, done, converged);
-    // A failure inside the call (a HIP error, an RCCL deadline) may leave x
-    // updates deferred (poisson_x_finish not reached): say so at the next use
-    // of x instead of handing out an x with terms silently missing.
-    if (rc != CGX_OK && c->fused && c->xd > 1) c->x_incomplete = true;
+    if (rc != CGX_OK) {
+        // Part of an iteration may have run on some row blocks (or all of
+        // r's update without x's): repeating it would apply it twice.  And
+        // when x updates were left out (poisson_x_finish not reached), say so
+        // at the next use of x instead of handing out an x with terms missing.
+        c->iter_failed = true;
+        if (c->fused && c->xd > 1 && (c->k > c->xd_k0 || c->xalpha_pending)) c->x_incomplete = true;
+    }
     return rc;
 }
 
@@ -720,91 +775,47 @@ static bool local_graph_eligible(const cgx_ctx *c, double eps) {
 }
 
 // Capture `iters` iterations from c->k into *out (nothing runs; c->k and the
-// counters are restored).  Every stream the iteration uses joins the capture
-// from shard 0's stream and is joined back into it.
-static bool graph_dbg() {
-    static const bool on = [] {
-        const char *e = std::getenv("CGX_GRAPH_DEBUG");
-        return e && *e == '1';
-    }();
-    return on;
-}
-#define GDBG(...)                                 \
-    do {                                          \
-        if (graph_dbg()) {                        \
-            std::fprintf(stderr, "[cgx graph] "); \
-            std::fprintf(stderr, __VA_ARGS__);    \
-            std::fprintf(stderr, "\n");           \
-        }                                         \
-    } while (0)
-
+// counters are restored).
 static int local_graph_capture(cgx_ctx *c, int iters, hipGraphExec_t *out) {
     Shard &s0 = c->sh[0];
-    // one stream (the default): every block's streams are shard 0's stream
-    // while the iterations are captured, so the graph is the host's enqueue
-    // order as a chain -- a valid order, since a stream waits only on events
-    // already recorded.  The blocks share one device, whose kernels would
-    // contend for the same CUs anyway.  CGX_LOCAL_GRAPH_STREAMS=multi
-    // captures the blocks' own streams instead (forked from and joined back
-    // into shard 0's); with this ROCm, hipStreamEndCapture faulted in the
-    // host runtime at 4 blocks and more (profiles/r04_local_graph.md).
-    const char *ms = std::getenv("CGX_LOCAL_GRAPH_STREAMS");
-    const bool multi = ms && std::strcmp(ms, "multi") == 0;
-    GDBG("capture %d iterations from k=%lld, %zu blocks, %s", iters, (long long)c->k, c->sh.size(),
-         multi ? "multi-stream" : "one stream");
+    // One stream: every block's streams are shard 0's stream while the
+    // iterations are captured, so the graph is the host's enqueue order as a
+    // chain -- a valid order, since a stream waits only on events already
+    // recorded.  The blocks share one device, whose kernels would contend for
+    // the same CUs anyway.  (Round 4 also captured the blocks' own streams,
+    // forked from and joined back into shard 0's; that capture re-records the
+    // same per-block events two or three times per iteration with
+    // O(blocks^2) cross-stream waits on them, and hipStreamEndCapture faulted
+    // in the host runtime at 4 blocks and more -- profiles/r04_local_graph.md.
+    // The form was removed in round 5: no setting reaches it.)
     TRY(set_dev(s0));
     const int64_t k0 = c->k, t0 = c->total_iters;
     HIPT(hipStreamBeginCapture(s0.stream, hipStreamCaptureModeRelaxed));
     std::vector<std::pair<hipStream_t, hipStream_t>> saved;
-    if (!multi)
-        for (auto &s : c->sh) {
-            saved.push_back({s.stream, s.cstream});
-            s.stream = s0.stream;
-            if (s.cstream) s.cstream = s0.stream;
-        }
+    for (auto &s : c->sh) {
+        saved.push_back({s.stream, s.cstream});
+        s.stream = s0.stream;
+        if (s.cstream) s.cstream = s0.stream;
+    }
     int rc = [&]() -> int {
-        if (multi) {
-            HIPT(hipEventRecord(s0.ev_fork, s0.stream));
-            for (auto &s : c->sh) {
-                if (&s != &s0) HIPT(hipStreamWaitEvent(s.stream, s0.ev_fork, 0));
-                if (s.cstream) HIPT(hipStreamWaitEvent(s.cstream, s0.ev_fork, 0));
-            }
-        }
         for (int i = 0; i < iters; ++i) {
             int stop = 0;
-            GDBG("  iteration %d", i);
             TRY(do_iteration(c, -1.0, &stop));
         }
-        GDBG("  joins");
-        TRY(set_dev(s0));
-        if (multi)
-            for (auto &s : c->sh) {
-                if (&s != &s0) {
-                    HIPT(hipEventRecord(s.ev_join, s.stream));
-                    HIPT(hipStreamWaitEvent(s0.stream, s.ev_join, 0));
-                }
-                if (s.cstream) {
-                    HIPT(hipEventRecord(s.ev_cjoin, s.cstream));
-                    HIPT(hipStreamWaitEvent(s0.stream, s.ev_cjoin, 0));
-                }
-            }
         return CGX_OK;
     }();
-    if (!multi)
-        for (size_t i = 0; i < c->sh.size(); ++i) {
-            c->sh[i].stream = saved[i].first;
-            c->sh[i].cstream = saved[i].second;
-        }
+    for (size_t i = 0; i < c->sh.size(); ++i) {
+        c->sh[i].stream = saved[i].first;
+        c->sh[i].cstream = saved[i].second;
+    }
     c->k = k0;
     c->total_iters = t0;
     hipGraph_t g = nullptr;
-    GDBG("  end capture (rc %d)", rc);
+    (void)set_dev(s0);
     const hipError_t ec = hipStreamEndCapture(s0.stream, &g);
-    GDBG("  ended: %s", hipGetErrorString(ec));
     if (rc == CGX_OK && ec != hipSuccess) rc = fail(CGX_ERR_HIP, "hipStreamEndCapture: %s", hipGetErrorString(ec));
     if (rc == CGX_OK) {
         const hipError_t ei = hipGraphInstantiate(out, g, nullptr, nullptr, 0);
-        GDBG("  instantiated: %s", hipGetErrorString(ei));
         if (ei != hipSuccess) {
             *out = nullptr;
             rc = fail(CGX_ERR_HIP, "hipGraphInstantiate: %s", hipGetErrorString(ei));
@@ -830,9 +841,7 @@ static int local_graph_launch(cgx_ctx *c, hipGraphExec_t ex) {
             HIPT(hipStreamWaitEvent(s0.stream, s.ev_cjoin, 0));
         }
     }
-    GDBG("launch");
     HIPT(hipGraphLaunch(ex, s0.stream));
-    GDBG("  launched");
     HIPT(hipEventRecord(s0.ev_fork, s0.stream));
     for (auto &s : c->sh) {
         if (&s != &s0) HIPT(hipStreamWaitEvent(s.stream, s0.ev_fork, 0));
@@ -885,6 +894,7 @@ static int iterate_calls(cgx_ctx *c, int64_t count, double eps, int64_t *done, i
         ++did;
         if (stop) break;
     }
+    TRY(settle_rr(c));
     TRY(poisson_x_finish(c));
     if (done) *done = did;
     if (converged) *converged = c->converged;

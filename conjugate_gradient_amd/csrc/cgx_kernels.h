@@ -65,15 +65,16 @@ struct MatvecPlan {
     int blocks = 0;   // grid (256-thread blocks), grid-stride over row groups
     int small = 0;    // > 0: k_matvec_small_f64 with this many threads per block (vector in LDS)
 };
-// R/U/nt/blocks_per_cu <= 0 pick the defaults (env CGX_MV_* may override).
+// R/U/nt/blocks_per_cu <= 0 pick the defaults (env CGX_MV_PLAN="R=..,U=..,nt=..,bpc=.."
+// may override).
 // cols > 0 (the row length): fewer than 8 whole 128-column chunks per row
 // take U = 4 or 2, so all of a row's loads are issued at once.
 MatvecPlan plan_matvec_f64(int device, int64_t rows, int R = 0, int U = 0, int nt = -1,
                            int blocks_per_cu = 0, int64_t cols = 0);
 // The LDS-staged matVec of small systems (cgx_matvec.hip k_matvec_small_f64):
 // rows of lda columns, 2048 <= lda <= 8192; small = 0 (not applicable)
-// otherwise.  CGX_MV_SMALL=0 turns it off; CGX_SMALL_NT / CGX_SMALL_U pick
-// the block size (512, 1024) and chunks per step (4, 8).
+// otherwise.  CGX_MV_SMALL=0 turns it off; CGX_SMALL_PLAN="threads=..,U=..,nt=.."
+// picks the block size (512, 1024), chunks per step (4, 8) and A's load policy.
 MatvecPlan plan_matvec_small_f64(int device, int64_t rows, int64_t lda);
 
 // ---- fp64 -------------------------------------------------------------------
@@ -88,11 +89,15 @@ hipError_t matvec_f64(const MatvecPlan &pl, const double *A, int64_t lda, int64_
 // Columns [col_first, col_first+col_count) mod cols (all multiples of 128,
 // cols = the padded width): out[i] = (accumulate ? out[i] : 0) + partial row
 // sum; optional fused dot as above.  Used to overlap the p exchange with the
-// shard's own column block.
+// shard's own column block.  col_seg > 0 (not with accumulate): the first
+// col_seg columns of the range and the rest are summed separately and added
+// (own + rest) -- the bits of a col_seg launch followed by an accumulating
+// launch of the rest, in one launch (the unoverlapped iteration of an
+// aligned row block, so both forms give the same x).
 hipError_t matvec_f64_cols(const MatvecPlan &pl, const double *A, int64_t lda, int64_t rows, int64_t cols,
                            int64_t col_first, int64_t col_count, bool accumulate, const double *v, double *out,
                            const double *pown, double *dot_out, const RedWs &ws, hipStream_t s,
-                           const int64_t *gate = nullptr, int64_t *ts = nullptr);
+                           const int64_t *gate = nullptr, int64_t *ts = nullptr, int64_t col_seg = 0);
 // r = b - Ax; p = r (if p); *rr_out = r.r (if rr_out).  Ax == nullptr: Ax = 0
 // (r = b - 0.0).  clear2: two int64 the kernel zeroes (the convergence record).
 hipError_t residual_f64(int64_t n, const double *b, const double *Ax, double *r, double *p,
@@ -152,17 +157,25 @@ hipError_t stencil5_f64(const double *ph, int64_t mloc, int64_t m, double *Ap, d
 // Fused Poisson CG iteration (even m, 16-B-aligned buffers; see the kernels).
 // rh, poh, pnh: r, p_{k-1}, p_k slabs with one halo row above and below.
 bool poisson_fusable(int64_t mloc, int64_t m);
+// part: 0 all rows; 1 interior runs; 2 the two edge runs (+= part 1's p.Ap).
+// r_up / r_dn (one process, several slabs): r's top / bottom halo row is read
+// in place from the neighbouring slab's boundary row (system-scope loads)
+// instead of from rh's halo rows.  rr_sum: *rr is the rank-order sum of the
+// slabs' r.r partials, formed by the kernel (block 0 stores it to rr_sum->out).
 hipError_t poisson_p_f64(const double *rh, const double *poh, double *pnh, int64_t mloc, int64_t m, const double *rr,
                          const double *rsold, bool first, double *pap_out, const RedWs &ws, hipStream_t s,
                          double eps = -1.0, int64_t k = 0, int64_t *kdone = nullptr, double *rrfinal = nullptr,
-                         int part = 0, int64_t *hrec = nullptr);  // part: 0 all rows; 1 interior runs; 2 the two edge runs (+= part 1's p.Ap)
+                         int part = 0, int64_t *hrec = nullptr, const double *r_up = nullptr,
+                         const double *r_dn = nullptr, const PeerSum *rr_sum = nullptr);
 // xmode: 1 x += alpha p_k; 0 x untouched, alpha_k to *xalpha; 2 x += alpha_{k-1}
 // p_{k-1} (poh, xalpha[0]) then += alpha_k p_k (x every other iteration);
 // 3 x += alpha_{k-2} p_{k-2} (pqh, xalpha[0]), alpha_{k-1} p_{k-1} (poh,
-// xalpha[1]), alpha_k p_k (x every third iteration).
+// xalpha[1]), alpha_k p_k (x every third iteration).  pap_sum: p.Ap from the
+// slabs' partials, as poisson_p_f64's rr_sum.
 hipError_t poisson_xr_f64(const double *pnh, const double *poh, const double *pqh, double *x, double *r,
                           int64_t mloc, int64_t m, const double *rsold, const double *pAp, double *rr_out, int xmode,
-                          double *xalpha, const RedWs &ws, hipStream_t s, const int64_t *gate = nullptr);
+                          double *xalpha, const RedWs &ws, hipStream_t s, const int64_t *gate = nullptr,
+                          const PeerSum *pap_sum = nullptr);
 // x += xalpha[0] p (pnh) [then += xalpha[1] p (pbh) when pbh != nullptr] over the
 // slab interior: the x updates the last iterations left out.
 hipError_t poisson_xflush_f64(const double *pnh, const double *pbh, double *x, int64_t mloc, int64_t m,

@@ -109,8 +109,7 @@ static int shard_iteration(LocalPool &P, Shard &d) {
         for (auto &s : c->sh)
             if (&s != &d) HIPT(hipStreamWaitEvent(d.stream, s.ev_pready, 0));
         HIPT(gather_slices(pown, S, d.index, d.nloc * (int64_t)es, d.pfull, d.stream));
-        HIPT(matvec_f64(d.plan, CD(d.A), c->lda, d.nloc, c->lda, CD(d.pfull), D(d.Ap), CD(d.pown), D(slot(d, pl)),
-                        d.ws, d.stream, gate_of(d, gated), ts_of(c, d, TK_MV)));
+        TRY(matvec_rows(c, d, d.plan, d.A, 0, d.nloc, d.pfull, true, pl, gated, ts_of(c, d, TK_MV)));
     }
     if (timing) {
         HIPT(hipEventRecord(d.ev_t[2 * d.ev_used + 1], d.stream));
@@ -174,19 +173,18 @@ static void worker(LocalPool *P, int index) {
     }
 }
 
-// On by default when the row blocks span distinct devices (peer access on):
-// each thread then launches onto its own device's queues.  With every block
-// on one GPU the runtime serialises the threads' launches on that device's
-// queues and the threaded enqueue measured no faster (275-345 vs 275-294 us
-// per iteration at 8 blocks, profiles/r04_multishard_floor_threads.jsonl), so
-// it stays off there unless CGX_LOCAL_THREADS=1 forces it (the tests do, for
-// the code path); CGX_LOCAL_THREADS=0 turns it off everywhere.
+// Opt-in (CGX_LOCAL_THREADS=1).  With every block on one GPU the runtime
+// serialises the threads' launches on that device's queues and the threaded
+// enqueue measured no faster (275-345 vs 275-294 us per iteration at 8
+// blocks, profiles/r04_multishard_floor_threads.jsonl).  Across distinct
+// devices, where each thread would launch onto its own device's queues, it
+// has not run on hardware yet (the suite's distinct-device tests run it when
+// a box has two GPUs or more), so it is not the default there either.
 bool local_mt_eligible(const cgx_ctx *c) {
     const char *e = std::getenv("CGX_LOCAL_THREADS");
-    if (e && *e == '0') return false;
-    const bool force = e && *e == '1';
+    if (!(e && *e == '1')) return false;
     return c->mode == M_LOCAL && c->fuse_combine && c->op == OP_DENSE && !f32ref(c) &&
-           !(c->flags & (CGX_HOST_STREAM | CGX_SYMMETRIC | CGX_COMM_P2P)) && c->sh.size() >= 2 && (c->peer || force);
+           !(c->flags & (CGX_HOST_STREAM | CGX_SYMMETRIC | CGX_COMM_P2P)) && c->sh.size() >= 2;
 }
 
 int local_mt_start(cgx_ctx *c) {

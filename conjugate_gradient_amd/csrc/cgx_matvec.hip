@@ -133,14 +133,80 @@ __device__ __forceinline__ void mv_chunks_pipe(const d2 *const (&arow)[R], int l
     }
 }
 
+// The virtual chunks [v0, v1) of the rotated order that starts at physical
+// chunk cfirst (virtual v = physical (cfirst + v) mod nchunk), as at most two
+// physical pieces in order.
+template <int R, int U, int NT, bool PIPE>
+__device__ __forceinline__ void mv_range(const d2 *const (&arow)[R], int lane, const d2 *v2, int64_t nchunk,
+                                         int64_t cfirst, int64_t v0, int64_t v1, d2 (&acc)[R]) {
+    if (v1 <= v0) return;
+    const int64_t a = cfirst + v0 < nchunk ? cfirst + v0 : cfirst + v0 - nchunk;
+    const int64_t b = a + (v1 - v0) < nchunk ? a + (v1 - v0) : nchunk;
+    const int64_t wrap = (v1 - v0) - (b - a);
+    if constexpr (PIPE) {
+        mv_chunks_pipe<R, U, NT>(arow, lane, v2, a, b, acc);
+        if (wrap > 0) mv_chunks_pipe<R, U, NT>(arow, lane, v2, 0, wrap, acc);
+    } else {
+        mv_chunks<R, U, NT>(arow, lane, v2, a, b, acc);
+        if (wrap > 0) mv_chunks<R, U, NT>(arow, lane, v2, 0, wrap, acc);
+    }
+}
+
+// The one-launch form of the overlapped matVec (rotated column order, two
+// accumulators): one software pipeline runs through the whole rotated row --
+// the own column block (virtual chunks [0, cseg)) into acc1, then the rest,
+// across the wrap, into acc -- with the next step's loads issued before the
+// current step's FMAs, the segment end and the wrap included.  Each
+// accumulator sees the FMA chain the own / rest launches apply, in the same
+// order, so the row sums are theirs bit for bit.  Needs U | cseg, U | ccount
+// and U | (nchunk - cfirst) (no step straddles the segment end or the wrap).
+template <int R, int U, int NT>
+__device__ __forceinline__ void mv_rot_pipe(const d2 *const (&arow)[R], int lane, const d2 *v2, int64_t nchunk,
+                                            int64_t cfirst, int64_t cseg, int64_t ccount, d2 (&acc1)[R],
+                                            d2 (&acc)[R]) {
+    d2 pa[U], aa[R][U], pb[U], ab[R][U];
+    const int64_t wrapv = nchunk - cfirst;  // the first virtual chunk past the wrap
+    auto phys = [&](int64_t vc) { return vc < wrapv ? cfirst + vc : vc - wrapv; };
+    auto seg_end = [&](int64_t vc) {
+        if (vc == cseg) {
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                acc1[r] = acc[r];
+                acc[r] = (d2)(0.0);
+            }
+        }
+    };
+    int64_t vc = 0;
+    mv_load_step<R, U, NT>(arow, lane, v2, phys(0), pa, aa);
+    for (;;) {
+        const bool more = vc + U < ccount;
+        if (more) mv_load_step<R, U, NT>(arow, lane, v2, phys(vc + U), pb, ab);
+        mv_fma_step<R, U>(pa, aa, acc);
+        vc += U;
+        seg_end(vc);
+        if (!more) break;
+        const bool more2 = vc + U < ccount;
+        if (more2) mv_load_step<R, U, NT>(arow, lane, v2, phys(vc + U), pa, aa);
+        mv_fma_step<R, U>(pb, ab, acc);
+        vc += U;
+        seg_end(vc);
+        if (!more2) break;
+    }
+}
+
 // Column range: the `ccount` 128-column chunks starting at chunk `cfirst`,
 // wrapping modulo the vec_cols/128 aligned chunks; `tail` adds the scalar
 // columns [vec_cols, cols).  `accumulate` adds the existing out[i] (the
 // overlap path computes the shard's own column block first, then the rest).
-template <int R, int U, int NT, bool PIPE = false>
+// ROT (0 < cseg < ccount): the own block and the rest in one launch -- the
+// first cseg chunks of the range and the others summed separately and added,
+// out[i] = own + rest, which is what the own launch followed by the
+// accumulating rest launch stores (the overlapped exchange's two launches and
+// the one launch after the exchange give the same bits).
+template <int R, int U, int NT, bool PIPE = false, bool ROT = false>
 __global__ __launch_bounds__(kNT) void k_matvec_f64(
     const double *__restrict__ A, int64_t lda, int64_t rows, int64_t cols, int64_t vec_cols, int64_t cfirst,
-    int64_t ccount, int tail, int accumulate, const double *__restrict__ v, double *__restrict__ out,
+    int64_t ccount, int64_t cseg, int tail, int accumulate, const double *__restrict__ v, double *__restrict__ out,
     const double *__restrict__ pown, double *dot_out, double *partials, unsigned *ticket, const int64_t *gate,
     int64_t *ts) {
     if (gate && *gate) return;  // the solve converged in an earlier iteration (device-side gating)
@@ -167,24 +233,42 @@ __global__ __launch_bounds__(kNT) void k_matvec_f64(
             arow[r] = reinterpret_cast<const d2 *>(A + ridx[r] * lda) + lane;
             acc[r] = (d2)(0.0);
         }
-        if constexpr (PIPE) {
-            mv_chunks_pipe<R, U, NT>(arow, lane, v2, ca, cb, acc);
-            if (wrap > 0) mv_chunks_pipe<R, U, NT>(arow, lane, v2, 0, wrap, acc);
-        } else {
-            mv_chunks<R, U, NT>(arow, lane, v2, ca, cb, acc);
-            if (wrap > 0) mv_chunks<R, U, NT>(arow, lane, v2, 0, wrap, acc);
-        }
-        if (tail)
-            for (int64_t j = ctail + lane; j < cols; j += 64) {
-                const double vj = v[j];
-#pragma unroll
-                for (int r = 0; r < R; ++r) acc[r].x = __builtin_fma(A[ridx[r] * lda + j], vj, acc[r].x);
-            }
         double mine = 0.0;
+        if constexpr (ROT) {
+            d2 acc1[R];
 #pragma unroll
-        for (int r = 0; r < R; ++r) {
-            const double s = wave_sum(acc[r].x + acc[r].y);
-            if (lane == r) mine = s;
+            for (int r = 0; r < R; ++r) acc1[r] = (d2)(0.0);
+            if (PIPE && cseg % U == 0 && ccount % U == 0 && (nchunk - cfirst) % U == 0)
+                mv_rot_pipe<R, U, NT>(arow, lane, v2, nchunk, cfirst, cseg, ccount, acc1, acc);
+            else {
+                mv_range<R, U, NT, PIPE>(arow, lane, v2, nchunk, cfirst, 0, cseg, acc1);
+                mv_range<R, U, NT, PIPE>(arow, lane, v2, nchunk, cfirst, cseg, ccount, acc);
+            }
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const double s1 = wave_sum(acc1[r].x + acc1[r].y);
+                const double s2 = wave_sum(acc[r].x + acc[r].y);
+                if (lane == r) mine = s1 + s2;  // the rest launch's out[i] (= s1) + its own sum
+            }
+        } else {
+            if constexpr (PIPE) {
+                mv_chunks_pipe<R, U, NT>(arow, lane, v2, ca, cb, acc);
+                if (wrap > 0) mv_chunks_pipe<R, U, NT>(arow, lane, v2, 0, wrap, acc);
+            } else {
+                mv_chunks<R, U, NT>(arow, lane, v2, ca, cb, acc);
+                if (wrap > 0) mv_chunks<R, U, NT>(arow, lane, v2, 0, wrap, acc);
+            }
+            if (tail)
+                for (int64_t j = ctail + lane; j < cols; j += 64) {
+                    const double vj = v[j];
+#pragma unroll
+                    for (int r = 0; r < R; ++r) acc[r].x = __builtin_fma(A[ridx[r] * lda + j], vj, acc[r].x);
+                }
+#pragma unroll
+            for (int r = 0; r < R; ++r) {
+                const double s = wave_sum(acc[r].x + acc[r].y);
+                if (lane == r) mine = s;
+            }
         }
         if (lane < R && r0 + lane < rows) {
             if (accumulate) mine = out[r0 + lane] + mine;
@@ -460,34 +544,38 @@ FoldFn pick_fold(int R, int U, int nt) {
     return (nt == 0 || nt == 2) ? pick_fold_u<0>(R, U) : pick_fold_u<1>(R, U);
 }
 
-using MvFn = void (*)(const double *, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, int, int,
+using MvFn = void (*)(const double *, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, int64_t, int, int,
                       const double *, double *, const double *, double *, double *, unsigned *, const int64_t *,
                       int64_t *);
 
-template <int R, int U>
+template <int R, int U, bool ROT>
 MvFn pick_nt(int nt) {
     switch (nt) {
-        case 0: return k_matvec_f64<R, U, 0>;
-        case 2: return k_matvec_f64<R, U, 0, true>;  // pipelined, default-policy loads
-        case 8: return k_matvec_f64<R, U, 1, true>;  // pipelined, global nt (the default)
-        default: return k_matvec_f64<R, U, 1>;
+        case 0: return k_matvec_f64<R, U, 0, false, ROT>;
+        case 2: return k_matvec_f64<R, U, 0, true, ROT>;  // pipelined, default-policy loads
+        case 8: return k_matvec_f64<R, U, 1, true, ROT>;  // pipelined, global nt (the default)
+        default: return k_matvec_f64<R, U, 1, false, ROT>;
     }
 }
-template <int R>
+template <int R, bool ROT>
 MvFn pick_u(int U, int nt) {
     switch (U) {
-        case 2: return pick_nt<R, 2>(nt);
-        case 8: return pick_nt<R, 8>(nt);
-        default: return pick_nt<R, 4>(nt);
+        case 2: return pick_nt<R, 2, ROT>(nt);
+        case 8: return pick_nt<R, 8, ROT>(nt);
+        default: return pick_nt<R, 4, ROT>(nt);
     }
 }
-MvFn pick_mv(int R, int U, int nt) {
+template <bool ROT>
+MvFn pick_r(int R, int U, int nt) {
     switch (R) {
-        case 1: return pick_u<1>(U, nt);
-        case 2: return pick_u<2>(U, nt);
-        case 8: return pick_u<8>(U, nt);
-        default: return pick_u<4>(U, nt);
+        case 1: return pick_u<1, ROT>(U, nt);
+        case 2: return pick_u<2, ROT>(U, nt);
+        case 8: return pick_u<8, ROT>(U, nt);
+        default: return pick_u<4, ROT>(U, nt);
     }
+}
+MvFn pick_mv(int R, int U, int nt, bool rot = false) {
+    return rot ? pick_r<true>(R, U, nt) : pick_r<false>(R, U, nt);
 }
 
 }  // namespace
@@ -517,9 +605,9 @@ MatvecPlan plan_matvec_f64(int device, int64_t rows, int R, int U, int nt, int b
     // an A of up to 64 MiB with default-policy loads (2), so it stays in the
     // 256 MB MALL between iterations (profiles/r03_iteration_floor_mall_l2.jsonl)
     pl.nt = (cols > 0 && rows * cols * 8 <= (int64_t(64) << 20)) ? 2 : 8;
-    pl.R = env_int("CGX_MV_R", pl.R);
-    pl.U = env_int("CGX_MV_U", pl.U);
-    pl.nt = env_int("CGX_MV_NT", pl.nt);
+    pl.R = env_opt("CGX_MV_PLAN", "R", pl.R);
+    pl.U = env_opt("CGX_MV_PLAN", "U", pl.U);
+    pl.nt = env_opt("CGX_MV_PLAN", "nt", pl.nt);
     if (R > 0) pl.R = R;
     if (U > 0) pl.U = U;
     if (nt >= 0) pl.nt = nt;
@@ -530,7 +618,7 @@ MatvecPlan plan_matvec_f64(int device, int64_t rows, int R, int U, int nt, int b
     const void *fn = reinterpret_cast<const void *>(pick_mv(pl.R, pl.U, pl.nt));
     if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&per_cu, fn, kNT, 0) != hipSuccess || per_cu <= 0)
         per_cu = 2;
-    per_cu = env_int("CGX_MV_BLOCKS_PER_CU", per_cu);
+    per_cu = env_opt("CGX_MV_PLAN", "bpc", per_cu);
     if (blocks_per_cu > 0) per_cu = blocks_per_cu;
     const int64_t groups = (rows + pl.R - 1) / pl.R;
     const int64_t need = (groups + (kNT / 64) - 1) / (kNT / 64);
@@ -552,8 +640,8 @@ MatvecPlan plan_matvec_small_f64(int device, int64_t rows, int64_t lda) {
     // 91.0 us against 14.3 / 30.8 / 92.1 for round 2's two-launch form on
     // the same box; 1024 threads x 4 chunks: 14.6-14.8 / 30.9-33.3 / 92.2-92.4,
     // x 8: 15.2 / 31.0 / 91.1-91.4 (profiles/r03_iteration_floor_small*.jsonl).
-    pl.small = env_int("CGX_SMALL_NT", 512);
-    pl.U = env_int("CGX_SMALL_U", chunks % 8 ? 4 : 8);
+    pl.small = env_opt("CGX_SMALL_PLAN", "threads", 512);
+    pl.U = env_opt("CGX_SMALL_PLAN", "U", chunks % 8 ? 4 : 8);
     if ((pl.small != 512 && pl.small != 1024) || (pl.U != 4 && pl.U != 8) || chunks % pl.U) {
         pl.small = 0;
         return pl;
@@ -563,7 +651,7 @@ MatvecPlan plan_matvec_small_f64(int device, int64_t rows, int64_t lda) {
     // MALL between iterations: 13.4 vs 13.9 us per iteration at n = 2048 (33.5
     // MB); at 4096 (134 MB) 30.6 vs 30.2, at 8192 (537 MB) 103 vs 90
     // (profiles/r03_iteration_floor_small_mall.jsonl)
-    pl.nt = env_int("CGX_SMALL_ANT", rows * lda * 8 <= (int64_t(64) << 20) ? 0 : 1) ? 8 : 0;
+    pl.nt = env_opt("CGX_SMALL_PLAN", "nt", rows * lda * 8 <= (int64_t(64) << 20) ? 0 : 1) ? 8 : 0;
     const int64_t need = (rows + pl.small / 64 - 1) / (pl.small / 64);
     pl.blocks = (int)std::max<int64_t>(1, std::min<int64_t>(need, std::min<int64_t>(cus, kMaxRedBlocks)));
     return pl;
@@ -589,22 +677,25 @@ hipError_t matvec_f64(const MatvecPlan &pl, const double *A, int64_t lda, int64_
     const int64_t vec_cols = aligned ? (cols & ~int64_t(127)) : 0;
     MvFn fn = pick_mv(pl.R, pl.U, pl.nt);
     hipLaunchKernelGGL(fn, dim3(pl.blocks), dim3(kNT), 0, s, A, lda, rows, cols, vec_cols, int64_t(0),
-                       vec_cols >> 7, 1, 0, v, out, pown, dot_out, ws.partials, ws.tickets + T_MATVEC, gate, ts);
+                       vec_cols >> 7, int64_t(0), 1, 0, v, out, pown, dot_out, ws.partials, ws.tickets + T_MATVEC,
+                       gate, ts);
     return hipGetLastError();
 }
 
 hipError_t matvec_f64_cols(const MatvecPlan &pl, const double *A, int64_t lda, int64_t rows, int64_t cols,
                            int64_t col_first, int64_t col_count, bool accumulate, const double *v, double *out,
                            const double *pown, double *dot_out, const RedWs &ws, hipStream_t s,
-                           const int64_t *gate, int64_t *ts) {
+                           const int64_t *gate, int64_t *ts, int64_t col_seg) {
     if (rows <= 0) return hipSuccess;
-    if ((cols & 127) || (col_first & 127) || (col_count & 127) || (lda & 1) ||
+    if ((cols & 127) || (col_first & 127) || (col_count & 127) || (col_seg & 127) || (lda & 1) ||
+        col_first >= cols || col_count > cols || col_seg < 0 || col_seg > col_count || (col_seg && accumulate) ||
         ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(v)) & 15))
         return hipErrorInvalidValue;
-    MvFn fn = pick_mv(pl.R, pl.U, pl.nt);
+    const bool rot = col_seg > 0 && col_seg < col_count;
+    MvFn fn = pick_mv(pl.R, pl.U, pl.nt, rot);
     hipLaunchKernelGGL(fn, dim3(pl.blocks), dim3(kNT), 0, s, A, lda, rows, cols, cols, col_first >> 7,
-                       col_count >> 7, 0, accumulate ? 1 : 0, v, out, pown, dot_out, ws.partials,
-                       ws.tickets + T_MATVEC, gate, ts);
+                       col_count >> 7, rot ? col_seg >> 7 : int64_t(0), 0, accumulate ? 1 : 0, v, out, pown,
+                       dot_out, ws.partials, ws.tickets + T_MATVEC, gate, ts);
     return hipGetLastError();
 }
 

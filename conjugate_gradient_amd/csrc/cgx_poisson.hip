@@ -164,10 +164,27 @@ __device__ __forceinline__ double edge_r(const double *eb, const StripLane &L, i
     return L.wv < kWaves - 1 ? eb[((L.wv + 1) * 2 + 0) * kEdgeRB + t] : outer;
 }
 
-// p_k rows (FIRST: p_0 = r_0)
-template <bool NT, bool FIRST>
-__device__ __forceinline__ d2 pnv(const double *rrow, const double *prow, const StripLane &L, double beta) {
-    const d2 rv = lds2<NT>(rrow, L.off);
+// The fused kernels stream with non-temporal loads and stores, except an
+// item's last two rows: those are the next item's first two (its halo) and
+// are loaded with default policy so the block that reads them next finds them
+// in L2 (profiles/r01_sweep_poisson*.jsonl).
+constexpr bool NT = true, HT = true;
+
+// p_k rows (FIRST: p_0 = r_0).  sys: r's row is a neighbouring row block's
+// boundary row, read where it lies (the one-process halo pull): system-scope
+// 8-B loads, so no line this device's L2 kept from an earlier iteration is
+// used (the same loads as the other pull kernels, cgx_device.h load_sys).
+template <bool NTL, bool FIRST>
+__device__ __forceinline__ d2 pnv(const double *rrow, const double *prow, const StripLane &L, double beta,
+                                  bool sys = false) {
+    d2 rv;
+    if (sys) {
+        const double *q = rrow + (L.off >> 3);
+        rv.x = load_sys(q);
+        rv.y = load_sys(q + 1);
+    } else {
+        rv = lds2<NTL>(rrow, L.off);
+    }
     if constexpr (FIRST) return keep(L.valid, rv);
     const d2 pv = lds2<NT>(prow, L.off);
     d2 o;
@@ -182,21 +199,25 @@ __device__ __forceinline__ double pns(const double *rrow, const double *prow, in
 }
 
 // RBn output rows starting at interior row i: pm, pc carry p_k rows h = i, i+1.
-template <int RBn, bool NT, bool FIRST, bool HT>
+// rdn (one process, several row blocks): r's bottom halo row is the next
+// block's first row, read in place instead of from rh's halo row.
+template <int RBn, bool FIRST>
 __device__ __forceinline__ void poisson_p_step(const double *__restrict__ rh, const double *__restrict__ poh,
                                                double *__restrict__ pnh, int64_t mloc, int64_t m, int64_t i,
                                                const StripLane &L, double beta, d2 &pm, d2 &pc, double &acc,
-                                               double *eb) {
+                                               double *eb, const double *rdn) {
     const int lane = threadIdx.x & 63;
     d2 pr[RBn], ce[RBn];
     double el[RBn], er[RBn];
 #pragma unroll
     for (int t = 0; t < RBn; ++t) {
         const int64_t hc = (i + t + 1) * m;  // centre row (halo coordinates) of output row i+t
+        const bool pull = rdn && i + t + 1 == mloc;  // the row below is the bottom halo row
+        const double *rrow = pull ? rdn : rh + hc + m;
         // HT: the last two rows are the next item's first two (its halo):
         // default-policy loads keep them in L2 for the block that reads them next
-        pr[t] = (HT && t >= RBn - 2) ? pnv<false, FIRST>(rh + hc + m, poh + hc + m, L, beta)
-                                     : pnv<NT, FIRST>(rh + hc + m, poh + hc + m, L, beta);
+        pr[t] = (HT && t >= RBn - 2) ? pnv<false, FIRST>(rrow, poh + hc + m, L, beta, pull)
+                                     : pnv<NT, FIRST>(rrow, poh + hc + m, L, beta, pull);
         el[t] = L.has_l ? pns<FIRST>(rh + hc, poh + hc, L.jw - 1, beta) : 0.0;
         er[t] = L.has_r ? pns<FIRST>(rh + hc, poh + hc, L.jw + 128, beta) : 0.0;
     }
@@ -267,10 +288,21 @@ struct ItemRanges {
     int64_t w0, cnt1, w2, cnt2;
 };
 
-template <int RB, bool NT, bool FIRST, bool HT>
+// The halo pull (one process, several row blocks; rank mode and one block:
+// both null): r's top halo row is the previous block's last row (rup), its
+// bottom halo row the next block's first (rdn), read where they lie.  The
+// producers' r updates are ordered before this kernel by the r.r combine's
+// cross-stream events; the copies into rh's halo rows that did this before
+// round 5 moved the same bytes, so p_k is the same bits.
+struct HaloPull {
+    const double *up, *dn;
+};
+
+template <int RB, bool FIRST>
 __device__ __forceinline__ double poisson_p_body(const double *__restrict__ rh, const double *__restrict__ poh,
                                                  double *__restrict__ pnh, int64_t mloc, int64_t m, int64_t nstrips,
-                                                 int64_t rpi, ItemRanges ir, double beta, double *edge, int bands) {
+                                                 int64_t rpi, ItemRanges ir, double beta, double *edge, int bands,
+                                                 HaloPull hp) {
     double acc = 0.0;
     int par = 0;
     const Band bd = bands ? band_of(ir.w0, ir.cnt1, nstrips, bands) : Band{0, 0, 0, 0, 0};
@@ -280,40 +312,43 @@ __device__ __forceinline__ double poisson_p_body(const double *__restrict__ rh, 
         const StripLane L = strip_lane(w, nstrips, m);
         const int64_t i0 = (w / nstrips) * rpi;
         const int64_t i1 = (i0 + rpi < mloc) ? i0 + rpi : mloc;
-        d2 pm = pnv<NT && !HT, FIRST>(rh + i0 * m, poh + i0 * m, L, beta);
+        const bool pull = hp.up && i0 == 0;  // the top halo row
+        d2 pm = pnv<NT && !HT, FIRST>(pull ? hp.up : rh + i0 * m, poh + i0 * m, L, beta, pull);
         d2 pc = pnv<NT && !HT, FIRST>(rh + (i0 + 1) * m, poh + (i0 + 1) * m, L, beta);
         if (L.valid && i0 == 0) sts2<NT>(pnh, L.off, pm);  // top halo row of p_k
         int64_t i = i0;
         for (; i + RB <= i1; i += RB, par ^= 1)
-            poisson_p_step<RB, NT, FIRST, HT>(rh, poh, pnh, mloc, m, i, L, beta, pm, pc, acc,
-                                          edge + par * (kWaves * 2 * kEdgeRB));
+            poisson_p_step<RB, FIRST>(rh, poh, pnh, mloc, m, i, L, beta, pm, pc, acc,
+                                      edge + par * (kWaves * 2 * kEdgeRB), hp.dn);
         for (; i < i1; ++i, par ^= 1)
-            poisson_p_step<1, NT, FIRST, HT>(rh, poh, pnh, mloc, m, i, L, beta, pm, pc, acc,
-                                         edge + par * (kWaves * 2 * kEdgeRB));
+            poisson_p_step<1, FIRST>(rh, poh, pnh, mloc, m, i, L, beta, pm, pc, acc,
+                                     edge + par * (kWaves * 2 * kEdgeRB), hp.dn);
     }
     return acc;
 }
 
-template <int RB, bool NT, bool HT>
+// rr_sum.cnt > 0 (one process, several row blocks): r.r_k is the rank-order
+// sum of the blocks' partials, formed here (k_combine_peers' sum, the same
+// bits) instead of by a combine kernel of its own; block 0 stores it.
+template <int RB>
 __global__ __launch_bounds__(kNT) void k_poisson_p_f64(const double *__restrict__ rh, const double *__restrict__ poh,
                                                        double *__restrict__ pnh, int64_t mloc, int64_t m,
                                                        int64_t nstrips, int64_t rpi, ItemRanges ir, const double *rr,
                                                        const double *rsold, int first, ConvArgs cv, double *dot_out,
-                                                       int add_to_out, double *partials, unsigned *ticket, int bands) {
+                                                       int add_to_out, double *partials, unsigned *ticket, int bands,
+                                                       HaloPull hp, PeerSum rr_sum) {
     static_assert(RB <= kEdgeRB, "edge buffer");
     __shared__ double edge[2 * kWaves * 2 * kEdgeRB];
-    if (cv.kdone) {
-        if (*cv.kdone != 0) return;
-        if (!first && cv.eps >= 0.0 && sqrt(*rr) < cv.eps) {  // the same decision in every block
-            if (blockIdx.x == 0 && threadIdx.x == 0) record_convergence(cv, cv.k, *rr);
-            return;
-        }
+    if (cv.kdone && *cv.kdone != 0) return;
+    const double rrk = first ? 0.0 : rr_sum.cnt ? peer_sum_wave(rr_sum) : *rr;
+    if (cv.kdone && !first && cv.eps >= 0.0 && sqrt(rrk) < cv.eps) {  // the same decision in every block
+        if (blockIdx.x == 0 && threadIdx.x == 0) record_convergence(cv, cv.k, rrk);
+        return;
     }
     // p_0 = r_0 (first) has its own instantiation: no p_{k-1} loads
-    const double acc = first ? poisson_p_body<RB, NT, true, HT>(rh, poh, pnh, mloc, m, nstrips, rpi, ir, 0.0, edge,
-                                                                bands)
-                             : poisson_p_body<RB, NT, false, HT>(rh, poh, pnh, mloc, m, nstrips, rpi, ir,
-                                                                 cg_ratio(*rr, *rsold), edge, bands);
+    const double acc = first ? poisson_p_body<RB, true>(rh, poh, pnh, mloc, m, nstrips, rpi, ir, 0.0, edge, bands, hp)
+                             : poisson_p_body<RB, false>(rh, poh, pnh, mloc, m, nstrips, rpi, ir,
+                                                         cg_ratio(rrk, *rsold), edge, bands, hp);
     grid_sum_last_block(acc, partials, ticket, dot_out, add_to_out != 0);
 }
 
@@ -331,7 +366,7 @@ __global__ __launch_bounds__(kNT) void k_poisson_p_f64(const double *__restrict_
 // bit for bit the every-iteration update's; a solve that ends after an XM = 0
 // iteration finishes x with k_poisson_xflush_f64.  60 instead of 64 B per
 // point per iteration over a pair of iterations.
-template <int RBn, bool NT, bool HT, int XM>
+template <int RBn, int XM>
 __device__ __forceinline__ void poisson_xr_step(const double *__restrict__ pnh, const double *__restrict__ poh,
                                                 const double *__restrict__ pqh, double *__restrict__ x,
                                                 double *__restrict__ r, int64_t m, int64_t i, const StripLane &L,
@@ -405,18 +440,20 @@ __device__ __forceinline__ void poisson_xr_step(const double *__restrict__ pnh, 
 // partials add in the same order whichever variant runs (a thread adds its
 // rows in row order whatever RB is): x is the same bits with and without the
 // deferral.
-template <int RB, bool NT, bool HT, int XM>
+template <int RB, int XM>
 __global__ __launch_bounds__(kNT) void k_poisson_xr_f64(const double *__restrict__ pnh, const double *__restrict__ poh,
                                                         const double *__restrict__ pqh, double *__restrict__ x,
                                                         double *__restrict__ r, int64_t mloc,
                                                         int64_t m, int64_t nstrips, int64_t rpi, int64_t nitems,
                                                         int reverse, const double *rsold, const double *pAp,
                                                         double *rr_out, double *xalpha, double *partials,
-                                                        unsigned *ticket, const int64_t *gate, int bands) {
+                                                        unsigned *ticket, const int64_t *gate, int bands,
+                                                        PeerSum pap_sum) {
     static_assert(RB <= kEdgeRB, "edge buffer");
     __shared__ double edge[2 * kWaves * 2 * kEdgeRB];
     if (gate && *gate) return;
-    const double alpha = cg_ratio(*rsold, *pAp);
+    // pap_sum.cnt > 0: p.Ap summed here from the row blocks' partials (as k_poisson_p_f64's r.r)
+    const double alpha = cg_ratio(*rsold, pap_sum.cnt ? peer_sum_wave(pap_sum) : *pAp);
     // XM = 2: alpha_{k-1} = xalpha[0]; XM = 3: alpha_{k-2} = xalpha[0], alpha_{k-1} = xalpha[1]
     const double alpha_prev = XM == 2 ? xalpha[0] : XM == 3 ? xalpha[1] : 0.0;
     const double alpha_prev2 = XM == 3 ? xalpha[0] : 0.0;
@@ -436,10 +473,10 @@ __global__ __launch_bounds__(kNT) void k_poisson_xr_f64(const double *__restrict
         d2 pc = keep(L.valid, lds2<NT && !HT>(pnh + (i0 + 1) * m, L.off));
         int64_t i = i0;
         for (; i + RB <= i1; i += RB, par ^= 1)
-            poisson_xr_step<RB, NT, HT, XM>(pnh, poh, pqh, x, r, m, i, L, alpha, alpha_prev, alpha_prev2, pm, pc, acc,
+            poisson_xr_step<RB, XM>(pnh, poh, pqh, x, r, m, i, L, alpha, alpha_prev, alpha_prev2, pm, pc, acc,
                                             edge + par * (kWaves * 2 * kEdgeRB));
         for (; i < i1; ++i, par ^= 1)
-            poisson_xr_step<1, NT, HT, XM>(pnh, poh, pqh, x, r, m, i, L, alpha, alpha_prev, alpha_prev2, pm, pc, acc,
+            poisson_xr_step<1, XM>(pnh, poh, pqh, x, r, m, i, L, alpha, alpha_prev, alpha_prev2, pm, pc, acc,
                                            edge + par * (kWaves * 2 * kEdgeRB));
     }
     // XM = 0: alpha_k for the next iteration's (or the flush's) x update.  Read
@@ -474,14 +511,8 @@ __global__ __launch_bounds__(kNT) void k_poisson_xflush_f64(const double *__rest
     }
 }
 
-// ---- k_poisson_p_f64, software-pipelined (CGX_P_PIPE) --------------------------
-// k_poisson_p_f64's arithmetic in its order (the same p_k, the same p.Ap
-// partials) with the next step's loads -- at an item's last step, the next
-// item's prefix rows and first step -- issued before this step's arithmetic
-// and stores, as k_poisson_xr_pipe_f64 does.  Full strips, 8-row items, NT +
-// HT.  The halo-row stores (top of the first run, bottom of the last) stay
-// conditional: they are wave-uniform and rare.
-// Side-point addresses of one row (row base `row`) for the pipelined kernels,
+// ---- the software-pipelined x catch-up kernel -------------------------------
+// Side-point addresses of one row (row base `row`) for the pipelined kernel,
 // whose loads are unconditional.  Only the block's outer waves use them (the
 // inner waves take their neighbours' edges from LDS); with `hot` set, every
 // other wave loads that one L2-resident double instead, so the only side loads
@@ -497,158 +528,8 @@ __device__ __forceinline__ SidePts side_pts(const double *row, const StripLane &
     s.r = (L.has_r || !hot) ? row + (L.jw + 128 < m ? L.jw + 128 : m - 1) : hot;
     return s;
 }
-template <int RBn, bool FIRST>
-struct PSet {
-    d2 rv[RBn], pv[RBn];
-    double rl[RBn], pl[RBn], rr[RBn], pr[RBn];
-};
-template <int RBn, bool FIRST>
-__device__ __forceinline__ void p_pipe_load(PSet<RBn, FIRST> &S, const double *__restrict__ rh,
-                                            const double *__restrict__ poh, int64_t m, int64_t i, const StripLane &L,
-                                            bool last, const double *__restrict__ hot) {
-#pragma unroll
-    for (int t = 0; t < RBn; ++t) {
-        const int64_t hc = (i + t + 1) * m;
-        const bool ht = last && t >= RBn - 2;  // the next item's first two rows: default policy (HT)
-        S.rv[t] = ht ? lds2<false>(rh + hc + m, L.off) : lds2<true>(rh + hc + m, L.off);
-        if constexpr (!FIRST) S.pv[t] = ht ? lds2<false>(poh + hc + m, L.off) : lds2<true>(poh + hc + m, L.off);
-        const SidePts sr = side_pts(rh + hc, L, m, hot);
-        S.rl[t] = *sr.l;
-        S.rr[t] = *sr.r;
-        if constexpr (!FIRST) {
-            const SidePts sp = side_pts(poh + hc, L, m, hot);
-            S.pl[t] = *sp.l;
-            S.pr[t] = *sp.r;
-        }
-    }
-}
-template <bool FIRST>
-__device__ __forceinline__ d2 p_form(d2 rv, d2 pv, double beta) {
-    if constexpr (FIRST) return rv;
-    d2 o;
-    o.x = __builtin_fma(beta, pv.x, rv.x);
-    o.y = __builtin_fma(beta, pv.y, rv.y);
-    return o;
-}
-template <int RBn, bool FIRST>
-__device__ __forceinline__ void p_pipe_step(const PSet<RBn, FIRST> &S, double *__restrict__ pnh, int64_t mloc,
-                                            int64_t m, int64_t i, const StripLane &L, double beta, d2 &pm, d2 &pc,
-                                            double &acc, double *eb) {
-    const int lane = threadIdx.x & 63;
-    d2 pr[RBn], ce[RBn];
-    double el[RBn], er[RBn];
-#pragma unroll
-    for (int t = 0; t < RBn; ++t) {
-        pr[t] = p_form<FIRST>(S.rv[t], S.pv[t], beta);
-        el[t] = FIRST ? S.rl[t] : __builtin_fma(beta, S.pl[t], S.rl[t]);
-        er[t] = FIRST ? S.rr[t] : __builtin_fma(beta, S.pr[t], S.rr[t]);
-    }
-#pragma unroll
-    for (int t = 0; t < RBn; ++t) ce[t] = t == 0 ? pc : pr[t - 1];
-    edges_put<RBn>(eb, L, ce);
-    __syncthreads();
-#pragma unroll
-    for (int t = 0; t < RBn; ++t) {
-        const d2 up = t == 0 ? pm : (t == 1 ? pc : pr[t - 2]);
-        const d2 dn = pr[t];
-        const double lw = edge_l(eb, L, t, L.has_l ? el[t] : 0.0), rw = edge_r(eb, L, t, L.has_r ? er[t] : 0.0);
-        double l = __shfl_up(ce[t].y, 1, 64);
-        double r = __shfl_down(ce[t].x, 1, 64);
-        l = lane == 0 ? lw : l;
-        r = lane == 63 ? rw : r;
-        d2 o;
-        o.x = 4.0 * ce[t].x - up.x - dn.x - l - ce[t].y;
-        o.y = 4.0 * ce[t].y - up.y - dn.y - ce[t].x - r;
-        acc += ce[t].x * o.x + ce[t].y * o.y;
-        sts2<true>(pnh + (i + t + 1) * m, L.off, ce[t]);
-    }
-    if (i + RBn == mloc) sts2<true>(pnh + (mloc + 1) * m, L.off, pr[RBn - 1]);  // bottom halo row of p_k
-    if constexpr (RBn >= 2) {
-        pm = pr[RBn - 2];
-        pc = pr[RBn - 1];
-    } else {
-        pm = pc;
-        pc = pr[0];
-    }
-}
-template <int RBn, int NS, bool FIRST>
-__device__ __forceinline__ double poisson_p_pipe_body(const double *__restrict__ rh, const double *__restrict__ poh,
-                                                      double *__restrict__ pnh, int64_t mloc, int64_t m,
-                                                      int64_t nstrips, ItemRanges ir, double beta, double *edge,
-                                                      int bands, const double *__restrict__ hot) {
-    constexpr int64_t kRpi = RBn * NS;
-    double acc = 0.0;
-    const Band bd = bands ? band_of(ir.w0, ir.cnt1, nstrips, bands) : Band{0, 0, 0, 0, 0};
-    const int64_t vstart = bands ? bd.start : blockIdx.x, vend = bands ? bd.count : ir.cnt1 + ir.cnt2;
-    const int64_t vstride = bands ? bd.stride : gridDim.x;
-    if (vstart >= vend) return acc;
-    auto item_of = [&](int64_t v) {
-        return bands ? band_item(bd, v) : v < ir.cnt1 ? ir.w0 + v : ir.w2 + (v - ir.cnt1);
-    };
-    int64_t v = vstart, w = item_of(v);
-    StripLane L = strip_lane(w, nstrips, m);
-    int64_t i0 = (w / nstrips) * kRpi;
-    d2 pm = p_form<FIRST>(lds2<false>(rh + i0 * m, L.off), FIRST ? (d2)(0.0) : lds2<false>(poh + i0 * m, L.off), beta);
-    d2 pc = p_form<FIRST>(lds2<false>(rh + (i0 + 1) * m, L.off),
-                          FIRST ? (d2)(0.0) : lds2<false>(poh + (i0 + 1) * m, L.off), beta);
-    PSet<RBn, FIRST> S[2];
-    p_pipe_load<RBn, FIRST>(S[0], rh, poh, m, i0, L, NS == 1, hot);
-    for (;;) {
-        if (i0 == 0) sts2<true>(pnh, L.off, pm);  // top halo row of p_k
-        const int64_t vn = v + vstride < vend ? v + vstride : v;
-        const int64_t wn = item_of(vn);
-        const StripLane Ln = strip_lane(wn, nstrips, m);
-        const int64_t i0n = (wn / nstrips) * kRpi;
-        d2 rmn, pmn, rcn, pcn;
-#pragma unroll
-        for (int s = 0; s < NS; ++s) {
-            if (s + 1 < NS) {
-                p_pipe_load<RBn, FIRST>(S[(s + 1) & 1], rh, poh, m, i0 + (s + 1) * RBn, L, s + 2 == NS, hot);
-            } else {
-                rmn = lds2<false>(rh + i0n * m, Ln.off);
-                rcn = lds2<false>(rh + (i0n + 1) * m, Ln.off);
-                if constexpr (!FIRST) {
-                    pmn = lds2<false>(poh + i0n * m, Ln.off);
-                    pcn = lds2<false>(poh + (i0n + 1) * m, Ln.off);
-                }
-                p_pipe_load<RBn, FIRST>(S[(s + 1) & 1], rh, poh, m, i0n, Ln, NS == 1, hot);
-            }
-            p_pipe_step<RBn, FIRST>(S[s & 1], pnh, mloc, m, i0 + s * RBn, L, beta, pm, pc, acc,
-                                    edge + (s & 1) * (kWaves * 2 * kEdgeRB));
-        }
-        if (vn == v) break;
-        v = vn;
-        L = Ln;
-        i0 = i0n;
-        pm = p_form<FIRST>(rmn, FIRST ? (d2)(0.0) : pmn, beta);
-        pc = p_form<FIRST>(rcn, FIRST ? (d2)(0.0) : pcn, beta);
-    }
-    return acc;
-}
-template <int RBn, int NS, bool FIRST>
-__global__ __launch_bounds__(kNT) void k_poisson_p_pipe_f64(const double *__restrict__ rh,
-                                                            const double *__restrict__ poh, double *__restrict__ pnh,
-                                                            int64_t mloc, int64_t m, int64_t nstrips, ItemRanges ir,
-                                                            const double *rr, const double *rsold, int first,
-                                                            ConvArgs cv, double *dot_out, int add_to_out,
-                                                            double *partials, unsigned *ticket, int bands,
-                                                            const double *__restrict__ hot) {
-    static_assert(RBn <= kEdgeRB && NS % 2 == 0, "edge buffer / set parity");
-    __shared__ double edge[2 * kWaves * 2 * kEdgeRB];
-    if (cv.kdone) {
-        if (*cv.kdone != 0) return;
-        if (!first && cv.eps >= 0.0 && sqrt(*rr) < cv.eps) {
-            if (blockIdx.x == 0 && threadIdx.x == 0) record_convergence(cv, cv.k, *rr);
-            return;
-        }
-    }
-    // p_0 = r_0 (first) is its own instantiation: the other one's registers are what set the occupancy
-    const double acc = poisson_p_pipe_body<RBn, NS, FIRST>(rh, poh, pnh, mloc, m, nstrips, ir,
-                                                          FIRST ? 0.0 : cg_ratio(*rr, *rsold), edge, bands, hot);
-    grid_sum_last_block(acc, partials, ticket, dot_out, add_to_out != 0);
-}
 
-// ---- k_poisson_xr_f64, software-pipelined (CGX_XR_PIPE) ----------------------
+// ---- k_poisson_xr_f64, software-pipelined (the x catch-up, XM = 2 / 3) --------
 // The same arithmetic, row by row and item by item in the same order as
 // k_poisson_xr_f64 (so r, x and every r.r partial are the same bits), with
 // the loads of the next step -- or, at an item's last step, of the next
@@ -751,12 +632,13 @@ __global__ __launch_bounds__(kNT) void k_poisson_xr_pipe_f64(const double *__res
                                                              int64_t nitems, int reverse, const double *rsold,
                                                              const double *pAp, double *rr_out, double *xalpha,
                                                              double *partials, unsigned *ticket, const int64_t *gate,
-                                                             int bands, const double *__restrict__ hot) {
+                                                             int bands, const double *__restrict__ hot,
+                                                             PeerSum pap_sum) {
     static_assert(RBn <= kEdgeRB && NS % 2 == 0, "edge buffer / set parity");
     constexpr int64_t kRpi = RBn * NS;
     __shared__ double edge[2 * kWaves * 2 * kEdgeRB];
     if (gate && *gate) return;
-    const double alpha = cg_ratio(*rsold, *pAp);
+    const double alpha = cg_ratio(*rsold, pap_sum.cnt ? peer_sum_wave(pap_sum) : *pAp);
     const double alpha_prev = XM == 2 ? xalpha[0] : XM == 3 ? xalpha[1] : 0.0;
     const double alpha_prev2 = XM == 3 ? xalpha[0] : 0.0;
     double acc = 0.0;
@@ -846,38 +728,37 @@ hipError_t stencil5_f64(const double *ph, int64_t mloc, int64_t m, double *Ap, d
     return hipGetLastError();
 }
 
-// Fused Poisson kernels: rows per step RB (CGX_STENCIL_RB: 1, 2, 4, 8), rows
-// per work item (CGX_STENCIL_ROWS), resident blocks (CGX_STENCIL_BLOCKS), NT
-// streams (CGX_STENCIL_NT=0: default-policy loads/stores).  Defaults RB=8,
-// 8-row items, occupancy-sized grid: measured at m=8192 over RB 2..8, items
-// of 8..128 rows and 1024..4096 blocks (profiles/r01_sweep_poisson*.jsonl);
-// short items keep the rows in flight in a narrow band (64- and 128-row items
-// are 7-20 % slower).
+// Fused Poisson kernels: the plan.  Rows per step RB (1, 2, 4, 8), rows per
+// work item, XCD bands, the xr kernels' walk direction and the grid, from
+// CGX_POISSON_PLAN="rb=..,rows=..,bands=..,reverse=..,blocks=.." (keys
+// optional).  Defaults RB=8, 8-row items, XCD bands on, the xr kernels walking
+// backwards, an occupancy-sized grid: measured at m=8192 over RB 2..8, items
+// of 8..128 rows and 1024..4096 blocks (profiles/r01_sweep_poisson*.jsonl;
+// short items keep the rows in flight in a narrow band, 64- and 128-row items
+// are 7-20 % slower), re-checked on round 4's final tree
+// (profiles/r04_poisson_knobs_ab.jsonl, profiles/r04_poisson_rows_ab.jsonl).
 struct PoissonPlan {
-    int rb, nt, ht, bands, band_rot, side_edge;
-    int64_t nstrips, rpi, nitems, grid;
+    int rb, bands, reverse, blocks, pipe;
+    int64_t nstrips, rpi, nitems;
 };
 static PoissonPlan poisson_plan(int64_t mloc, int64_t m) {
     PoissonPlan p;
-    p.rb = env_int("CGX_STENCIL_RB", 8);
-    p.nt = env_int("CGX_STENCIL_NT", 1);
-    p.ht = env_int("CGX_STENCIL_HALO_T", 1);
+    p.rb = env_opt("CGX_POISSON_PLAN", "rb", 8);
     // XCD bands: 1341 vs 1288 it/s at m = 8192, two interleaved rounds
-    // (profiles/r03_poisson_bands_ab.jsonl); CGX_POISSON_BANDS=0 turns them off
-    p.bands = env_int("CGX_POISSON_BANDS", 1);
-    p.band_rot = std::max(0, env_int("CGX_POISSON_BAND_ROT", 0));
-    // pipelined kernels: side points loaded by the outer waves only (side_pts)
-    p.side_edge = env_int("CGX_PIPE_SIDE_EDGE", 1);
+    // (profiles/r03_poisson_bands_ab.jsonl)
+    p.bands = env_opt("CGX_POISSON_PLAN", "bands", 1);
+    p.reverse = env_opt("CGX_POISSON_PLAN", "reverse", 1);
+    p.blocks = env_opt("CGX_POISSON_PLAN", "blocks", 0);
+    p.pipe = env_opt("CGX_POISSON_PLAN", "pipe", 1);  // 0: the x catch-up on the plain kernel (the same bits)
     p.nstrips = (m + 2 * kNT - 1) / (2 * kNT);
-    p.rpi = std::max(1, env_int("CGX_STENCIL_ROWS", 8));
+    p.rpi = std::max(1, env_opt("CGX_POISSON_PLAN", "rows", 8));
     p.nitems = p.nstrips * ((mloc + p.rpi - 1) / p.rpi);
-    p.grid = 0;  // set per kernel from its occupancy (resident_grid)
     return p;
 }
 
 // Every block resident at once (occupancy x CUs), capped by the work items
-// and the reduction slots; CGX_STENCIL_BLOCKS overrides.
-static int64_t resident_grid(const void *fn, int64_t nitems) {
+// and the reduction slots; the plan's `blocks` overrides.
+static int64_t resident_grid(const PoissonPlan &pl, const void *fn, int64_t nitems) {
     int dev = 0, per_cu = 0;
     (void)hipGetDevice(&dev);
     static std::mutex mu;
@@ -892,97 +773,80 @@ static int64_t resident_grid(const void *fn, int64_t nitems) {
             cache.push_back({{fn, dev}, per_cu});
         }
     }
-    int64_t g = (int64_t)per_cu * cu_count(dev);
-    g = env_int("CGX_STENCIL_BLOCKS", (int)g);
+    const int64_t g = pl.blocks > 0 ? pl.blocks : (int64_t)per_cu * cu_count(dev);
     return std::max<int64_t>(1, std::min<int64_t>({g, nitems, kMaxRedBlocks}));
 }
 
 bool poisson_fusable(int64_t mloc, int64_t m) { return mloc > 0 && m > 0 && (m & 1) == 0; }
 
+static PeerSum no_sum() {
+    PeerSum z{};
+    z.cnt = 0;
+    return z;
+}
+
 template <int RB>
 static void launch_poisson_p(const PoissonPlan &pl, hipStream_t s, const double *rh, const double *poh, double *pnh,
                              int64_t mloc, int64_t m, const double *rr, const double *rsold, int first, ConvArgs cv,
-                             double *pap_out, const RedWs &ws, ItemRanges ir, int add_to_out) {
-    auto fn = pl.nt ? (pl.ht ? k_poisson_p_f64<RB, true, true> : k_poisson_p_f64<RB, true, false>)
-                    : k_poisson_p_f64<RB, false, false>;
-    int64_t grid = resident_grid(reinterpret_cast<const void *>(fn), ir.cnt1 + ir.cnt2);
-    const int bands = pl.bands && ir.cnt2 == 0 && ir.cnt1 % pl.nstrips == 0 && grid >= 8 ? 1 + pl.band_rot : 0;
+                             double *pap_out, const RedWs &ws, ItemRanges ir, int add_to_out, HaloPull hp,
+                             const PeerSum &rr_sum) {
+    auto fn = k_poisson_p_f64<RB>;
+    int64_t grid = resident_grid(pl, reinterpret_cast<const void *>(fn), ir.cnt1 + ir.cnt2);
+    const int bands = pl.bands && ir.cnt2 == 0 && ir.cnt1 % pl.nstrips == 0 && grid >= 8 ? 1 : 0;
     if (bands) grid &= ~int64_t(7);
-    // the software-pipelined kernel (full strips, 8-row items, NT + HT): the same p_k; on its own
-    // occupancy's grid (3 waves per SIMD, not 4), so p.Ap adds its partials in another order
-    const int pipe_rb = env_int("CGX_P_PIPE", 0);
-    if ((pipe_rb == 2 || pipe_rb == 4) && m % (2 * kNT) == 0 && pl.rpi == 8 && mloc % 8 == 0 && pl.nt && pl.ht) {
-        auto fp = pipe_rb == 2 ? (first ? k_poisson_p_pipe_f64<2, 4, true> : k_poisson_p_pipe_f64<2, 4, false>)
-                               : (first ? k_poisson_p_pipe_f64<4, 2, true> : k_poisson_p_pipe_f64<4, 2, false>);
-        auto fg = pipe_rb == 2 ? k_poisson_p_pipe_f64<2, 4, false> : k_poisson_p_pipe_f64<4, 2, false>;
-        int64_t pg = resident_grid(reinterpret_cast<const void *>(fg), ir.cnt1 + ir.cnt2);
-        const int pbands = pl.bands && ir.cnt2 == 0 && ir.cnt1 % pl.nstrips == 0 && pg >= 8 ? 1 + pl.band_rot : 0;
-        if (pbands) pg &= ~int64_t(7);
-        hipLaunchKernelGGL(fp, dim3((unsigned)pg), dim3(kNT), 0, s, rh, poh, pnh, mloc, m, pl.nstrips, ir, rr, rsold,
-                           first, cv, pap_out, add_to_out, ws.partials, ws.tickets + T_MATVEC, pbands,
-                           pl.side_edge ? (rr ? rr : rh) : nullptr);
-        return;
-    }
     hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(kNT), 0, s, rh, poh, pnh, mloc, m, pl.nstrips, pl.rpi, ir, rr,
-                       rsold, first, cv, pap_out, add_to_out, ws.partials, ws.tickets + T_MATVEC, bands);
+                       rsold, first, cv, pap_out, add_to_out, ws.partials, ws.tickets + T_MATVEC, bands, hp, rr_sum);
 }
 using XrFn = void (*)(const double *, const double *, const double *, double *, double *, int64_t, int64_t, int64_t,
                      int64_t, int64_t, int, const double *, const double *, double *, double *, double *, unsigned *,
-                     const int64_t *, int);
-template <int RB, int XM>
-static XrFn xr_fn(const PoissonPlan &pl) {
-    return pl.nt ? (pl.ht ? k_poisson_xr_f64<RB, true, true, XM> : k_poisson_xr_f64<RB, true, false, XM>)
-                 : k_poisson_xr_f64<RB, false, false, XM>;
-}
+                     const int64_t *, int, PeerSum);
 template <int XM>
-static XrFn xr_fn_rb(const PoissonPlan &pl, int rb) {
+static XrFn xr_fn_rb(int rb) {
     switch (rb) {
-        case 1: return xr_fn<1, XM>(pl);
-        case 2: return xr_fn<2, XM>(pl);
-        case 8: return xr_fn<8, XM>(pl);
-        default: return xr_fn<4, XM>(pl);
+        case 1: return k_poisson_xr_f64<1, XM>;
+        case 2: return k_poisson_xr_f64<2, XM>;
+        case 8: return k_poisson_xr_f64<8, XM>;
+        default: return k_poisson_xr_f64<4, XM>;
     }
 }
 // Every x mode runs on the grid of the every-iteration kernel at the plan's
 // RB (its occupancy), so the r.r partials add in the same order whichever
-// variant runs.  XM = 2 steps RB / 2 rows at a time (RB = 8: 193 VGPRs, 2
-// waves per SIMD, fewer than that grid; held to 3 waves it spilled).
+// variant runs.  XM = 2 / 3 carry p_{k-1} (and p_{k-2}): RB / 2 rows per step
+// (XM = 3 at RB = 8: 130 VGPRs).  The x catch-up (XM = 2 / 3) runs the
+// software-pipelined kernel where it applies (full strips, 8-row items):
+// 1489-1496 vs 1471-1480 it/s at m = 8192, three interleaved rounds, the same
+// bits (profiles/r04_poisson_catchup_ab.jsonl).  The pipelined form of the
+// other kernels measured no better (XM = 0: 283 vs 276 us in the kernel trace;
+// k_poisson_p: 1346-1464 vs 1475 it/s) and was removed in round 5.
 template <int XM>
 static void launch_poisson_xr(const PoissonPlan &pl, hipStream_t s, const double *pnh, const double *poh,
                               const double *pqh, double *x, double *r, int64_t mloc, int64_t m, const double *rsold,
                               const double *pAp, double *rr_out, double *xalpha, const RedWs &ws,
-                              const int64_t *gate) {
-    // XM = 2 / 3 carry p_{k-1} (and p_{k-2}): RB / 2 rows per step (XM = 3 at RB = 8:
-    // 130 VGPRs; CGX_XR3_QUARTER=1: RB / 4, 82)
-    const int rb = XM == 3 && env_int("CGX_XR3_QUARTER", 0) ? std::max(1, pl.rb / 4)
-                   : XM >= 2 && pl.rb > 1 && !env_int("CGX_XR2_FULL_RB", 0) ? pl.rb / 2 : pl.rb;
-    const XrFn fn = xr_fn_rb<XM>(pl, rb);
-    const XrFn fg = env_int("CGX_XR_OWN_GRID", 0) ? fn : xr_fn_rb<1>(pl, pl.rb);
-    int64_t grid = resident_grid(reinterpret_cast<const void *>(fg), pl.nitems);
-    const int bands = pl.bands && grid >= 8 ? 1 + pl.band_rot : 0;
+                              const int64_t *gate, const PeerSum &pap_sum) {
+    const int rb = XM >= 2 && pl.rb > 1 ? pl.rb / 2 : pl.rb;
+    const XrFn fn = xr_fn_rb<XM>(rb);
+    int64_t grid = resident_grid(pl, reinterpret_cast<const void *>(xr_fn_rb<1>(pl.rb)), pl.nitems);
+    const int bands = pl.bands && grid >= 8 ? 1 : 0;
     if (bands) grid &= ~int64_t(7);
-    const int reverse = env_int("CGX_STENCIL_REVERSE", 1);
-    // the software-pipelined kernel: full strips, 8-row items, NT + HT (same bits, same grid)
-    // CGX_XR_PIPE: rows per step of the pipelined kernel for XM = 0 / 1 (default 0: the plain
-    // kernel); CGX_XR_PIPE_CATCHUP: the same for the x catch-up kernels, XM = 2 / 3 (default 4:
-    // 1489-1496 vs 1471-1480 it/s at m = 8192, three interleaved rounds, the same bits;
-    // profiles/r04_poisson_catchup_ab.jsonl)
-    const int pipe_rb = XM >= 2 ? env_int("CGX_XR_PIPE_CATCHUP", 4) : env_int("CGX_XR_PIPE", 0);
-    if ((pipe_rb == 2 || pipe_rb == 4) && m % (2 * kNT) == 0 && pl.rpi == 8 && mloc % 8 == 0 && pl.nt && pl.ht) {
-        auto fp = pipe_rb == 2 ? k_poisson_xr_pipe_f64<2, 4, XM> : k_poisson_xr_pipe_f64<4, 2, XM>;
-        hipLaunchKernelGGL(fp, dim3((unsigned)grid), dim3(kNT), 0, s, pnh, poh, pqh, x, r, m, pl.nstrips, pl.nitems,
-                           reverse, rsold, pAp, rr_out, xalpha, ws.partials, ws.tickets + T_XR, gate, bands,
-                           pl.side_edge ? rsold : nullptr);
+    if (XM >= 2 && pl.pipe && m % (2 * kNT) == 0 && pl.rpi == 8 && mloc % 8 == 0) {
+        auto fp = k_poisson_xr_pipe_f64<4, 2, XM>;
+        hipLaunchKernelGGL(fp, dim3((unsigned)grid), dim3(kNT), 0, s, pnh, poh, pqh, x, r,
+                           m, pl.nstrips, pl.nitems, pl.reverse, rsold, pAp, rr_out, xalpha, ws.partials,
+                           ws.tickets + T_XR, gate, bands, rsold, pap_sum);
         return;
     }
     hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(kNT), 0, s, pnh, poh, pqh, x, r, mloc, m, pl.nstrips, pl.rpi,
-                       pl.nitems, reverse, rsold, pAp, rr_out, xalpha, ws.partials, ws.tickets + T_XR, gate, bands);
+                       pl.nitems, pl.reverse, rsold, pAp, rr_out, xalpha, ws.partials, ws.tickets + T_XR, gate, bands,
+                       pap_sum);
 }
 
 hipError_t poisson_p_f64(const double *rh, const double *poh, double *pnh, int64_t mloc, int64_t m, const double *rr,
                          const double *rsold, bool first, double *pap_out, const RedWs &ws, hipStream_t s, double eps,
-                         int64_t k, int64_t *kdone, double *rrfinal, int part, int64_t *hrec) {
+                         int64_t k, int64_t *kdone, double *rrfinal, int part, int64_t *hrec, const double *r_up,
+                         const double *r_dn, const PeerSum *rr_sum) {
     if (!poisson_fusable(mloc, m) || !al16(rh) || !al16(pnh) || (!first && !al16(poh))) return hipErrorInvalidValue;
+    if ((r_up && !al16(r_up)) || (r_dn && !al16(r_dn)) || (rr_sum && (rr_sum->cnt < 0 || rr_sum->cnt > kMaxPeers)))
+        return hipErrorInvalidValue;
     ConvArgs cv;
     cv.eps = eps;
     cv.k = k;
@@ -1002,28 +866,32 @@ hipError_t poisson_p_f64(const double *rh, const double *poh, double *pnh, int64
         ir = ItemRanges{0, ns, (nruns - 1) * ns, nruns > 1 ? ns : 0};
         add = nruns > 2;
     }
+    const HaloPull hp{r_up, r_dn};
+    const PeerSum rs = rr_sum ? *rr_sum : no_sum();
     switch (pl.rb) {
-        case 1: launch_poisson_p<1>(pl, s, rh, poh, pnh, mloc, m, rr, rsold, first, cv, pap_out, ws, ir, add); break;
-        case 2: launch_poisson_p<2>(pl, s, rh, poh, pnh, mloc, m, rr, rsold, first, cv, pap_out, ws, ir, add); break;
-        case 8: launch_poisson_p<8>(pl, s, rh, poh, pnh, mloc, m, rr, rsold, first, cv, pap_out, ws, ir, add); break;
-        default: launch_poisson_p<4>(pl, s, rh, poh, pnh, mloc, m, rr, rsold, first, cv, pap_out, ws, ir, add); break;
+        case 1: launch_poisson_p<1>(pl, s, rh, poh, pnh, mloc, m, rr, rsold, first, cv, pap_out, ws, ir, add, hp, rs); break;
+        case 2: launch_poisson_p<2>(pl, s, rh, poh, pnh, mloc, m, rr, rsold, first, cv, pap_out, ws, ir, add, hp, rs); break;
+        case 8: launch_poisson_p<8>(pl, s, rh, poh, pnh, mloc, m, rr, rsold, first, cv, pap_out, ws, ir, add, hp, rs); break;
+        default: launch_poisson_p<4>(pl, s, rh, poh, pnh, mloc, m, rr, rsold, first, cv, pap_out, ws, ir, add, hp, rs); break;
     }
     return hipGetLastError();
 }
 
 hipError_t poisson_xr_f64(const double *pnh, const double *poh, const double *pqh, double *x, double *r,
                           int64_t mloc, int64_t m, const double *rsold, const double *pAp, double *rr_out, int xmode,
-                          double *xalpha, const RedWs &ws, hipStream_t s, const int64_t *gate) {
+                          double *xalpha, const RedWs &ws, hipStream_t s, const int64_t *gate,
+                          const PeerSum *pap_sum) {
     if (!poisson_fusable(mloc, m) || !al16(pnh) || !al16(x) || !al16(r)) return hipErrorInvalidValue;
     if (xmode < 0 || xmode > 3 || (xmode != 1 && !xalpha) || (xmode >= 2 && !al16(poh)) ||
-        (xmode == 3 && !al16(pqh)))
+        (xmode == 3 && !al16(pqh)) || (pap_sum && (pap_sum->cnt < 0 || pap_sum->cnt > kMaxPeers)))
         return hipErrorInvalidValue;
     const PoissonPlan pl = poisson_plan(mloc, m);
+    const PeerSum ps = pap_sum ? *pap_sum : no_sum();
     switch (xmode) {
-        case 0: launch_poisson_xr<0>(pl, s, pnh, poh, pqh, x, r, mloc, m, rsold, pAp, rr_out, xalpha, ws, gate); break;
-        case 2: launch_poisson_xr<2>(pl, s, pnh, poh, pqh, x, r, mloc, m, rsold, pAp, rr_out, xalpha, ws, gate); break;
-        case 3: launch_poisson_xr<3>(pl, s, pnh, poh, pqh, x, r, mloc, m, rsold, pAp, rr_out, xalpha, ws, gate); break;
-        default: launch_poisson_xr<1>(pl, s, pnh, poh, pqh, x, r, mloc, m, rsold, pAp, rr_out, xalpha, ws, gate); break;
+        case 0: launch_poisson_xr<0>(pl, s, pnh, poh, pqh, x, r, mloc, m, rsold, pAp, rr_out, xalpha, ws, gate, ps); break;
+        case 2: launch_poisson_xr<2>(pl, s, pnh, poh, pqh, x, r, mloc, m, rsold, pAp, rr_out, xalpha, ws, gate, ps); break;
+        case 3: launch_poisson_xr<3>(pl, s, pnh, poh, pqh, x, r, mloc, m, rsold, pAp, rr_out, xalpha, ws, gate, ps); break;
+        default: launch_poisson_xr<1>(pl, s, pnh, poh, pqh, x, r, mloc, m, rsold, pAp, rr_out, xalpha, ws, gate, ps); break;
     }
     return hipGetLastError();
 }

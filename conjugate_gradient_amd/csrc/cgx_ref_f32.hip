@@ -8,115 +8,20 @@ namespace {
 // ---------------------------------------------------------------------------
 // fp32 kernels in serialConjugate.c's exact operation order (CGX_F32_REF)
 // ---------------------------------------------------------------------------
-// matVec: one lane per row, columns in ascending order, out = ((0 + a0 v0) + a1 v1) + ...
-// A 64x64 tile is staged through LDS so the global reads stay coalesced.
-// One lane per row keeps the reference's order: out[i] = ((0 + a_i0 v_0) +
-// a_i1 v_1) + ..., every product and sum rounded to float.  A wave owns 64
-// rows and walks 64 x 128 tiles: the next tile is loaded into registers
-// (32 float4 loads per lane, coalesced 512-B row pieces, all issued at once)
-// while the current one is consumed from LDS, then written to the other LDS
-// buffer (row stride 129 floats: conflict-free when lane t walks row t).
-constexpr int kRefTC = 128;  // tile columns
-__global__ __launch_bounds__(64) void k_matvec_ref_f32(const float *__restrict__ A, int64_t lda,
-                                                       int64_t rows, int64_t cols,
-                                                       const float *__restrict__ v,
-                                                       float *__restrict__ out,
-                                                       const int64_t *gate) {
-#pragma clang fp contract(off)
-    if (gate && *gate) return;  // converged in an earlier iteration (device-side gating)
-    __shared__ float tile[2][64][kRefTC + 1];
-    __shared__ float pv[2][kRefTC];
-    typedef float f4 __attribute__((ext_vector_type(4)));
-    const int t = threadIdx.x;
-    const int64_t row0 = (int64_t)blockIdx.x * 64;
-    const int q = t & 31;          // column quad of this lane within a tile row
-    const int rsub = t >> 5;       // 0/1: which of two rows this lane loads per step
-    const bool vec_ok = (lda & 3) == 0 && ((reinterpret_cast<uintptr_t>(A) & 15) == 0);
-    const int64_t ntiles = (cols + kRefTC - 1) / kRefTC;
-    f4 nx[32];
-    float pn[2];
-    auto load_tile = [&](int64_t c0) {
-        const int w = (cols - c0 < kRefTC) ? (int)(cols - c0) : kRefTC;
-        if (vec_ok && row0 + 64 <= rows && w == kRefTC) {  // whole tile: 32 unconditional 16-B loads
-            const float *base = A + (row0 + rsub) * lda + c0 + 4 * q;
-#pragma unroll
-            for (int k = 0; k < 32; ++k) nx[k] = *reinterpret_cast<const f4 *>(base + (int64_t)(2 * k) * lda);
-            pn[0] = v[c0 + t];
-            pn[1] = v[c0 + t + 64];
-            return;
-        }
-#pragma unroll
-        for (int k = 0; k < 32; ++k) {
-            const int64_t rr = row0 + 2 * k + rsub;
-            const int c = 4 * q;
-            f4 val = (f4)(0.0f);
-            if (rr < rows) {
-                if (vec_ok && c + 4 <= w) {
-                    val = *reinterpret_cast<const f4 *>(A + rr * lda + c0 + c);
-                } else {
-                    for (int e = 0; e < 4; ++e)
-                        if (c + e < w) val[e] = A[rr * lda + c0 + c + e];
-                }
-            }
-            nx[k] = val;
-        }
-        pn[0] = (t < w) ? v[c0 + t] : 0.0f;
-        pn[1] = (t + 64 < w) ? v[c0 + t + 64] : 0.0f;
-    };
-    auto store_tile = [&](int b) {
-#pragma unroll
-        for (int k = 0; k < 32; ++k) {
-            float *dst = &tile[b][2 * k + rsub][4 * q];
-            dst[0] = nx[k][0];
-            dst[1] = nx[k][1];
-            dst[2] = nx[k][2];
-            dst[3] = nx[k][3];
-        }
-        pv[b][t] = pn[0];
-        pv[b][t + 64] = pn[1];
-    };
-    float acc = 0.0f;
-    if (ntiles > 0) {
-        load_tile(0);
-        store_tile(0);
-        __syncthreads();
-    }
-    for (int64_t tt = 0; tt < ntiles; ++tt) {
-        const int b = (int)(tt & 1);
-        const int64_t c0 = tt * kRefTC;
-        const int w = (cols - c0 < kRefTC) ? (int)(cols - c0) : kRefTC;
-        if (tt + 1 < ntiles) load_tile(c0 + kRefTC);  // in flight during the chain below
-        if (w == kRefTC) {
-#pragma unroll 16
-            for (int j = 0; j < kRefTC; ++j) {
-                const float prod = tile[b][t][j] * pv[b][j];
-                acc = acc + prod;
-            }
-        } else {
-            for (int j = 0; j < w; ++j) {
-                const float prod = tile[b][t][j] * pv[b][j];
-                acc = acc + prod;
-            }
-        }
-        if (tt + 1 < ntiles) store_tile(b ^ 1);
-        __syncthreads();
-    }
-    if (row0 + t < rows) out[row0 + t] = acc;
-}
-
-// The same float arithmetic with more of the chip in flight.  k_matvec_ref_f32
-// above has every row of the system progressing through the columns at the
-// same pace, so the bytes in flight chip-wide are rows x 128 columns x 4 B
-// (4 MiB at N=8192, about 2 TB/s at HBM latency) on 128 waves.  Here a wave
-// owns 16 rows and walks 16 x 512 tiles: all 64 lanes load the next tile
-// (32 coalesced 16-B loads each, 32 KiB per wave, 16 MiB chip-wide at
+// matVec: one lane per row keeps the reference's order, out[i] = ((0 +
+// a_i0 v_0) + a_i1 v_1) + ..., every product and sum rounded to float.  Round
+// 1's kernel had a wave own 64 rows and walk 64 x 128 tiles through LDS, so
+// the bytes in flight chip-wide were rows x 128 columns x 4 B (4 MiB at
+// N=8192, about 2 TB/s at HBM latency) on 128 waves.  Here a wave owns 16
+// rows and walks 16 x 512 tiles: all 64 lanes load the next tile (32
+// coalesced 16-B loads each, 32 KiB per wave, 16 MiB chip-wide at
 // N=8192) while lanes 0-15 run their rows' sequential sums over the current
 // one.  The products A[i][j] * x[j] (each rounded to float, as
 // serialConjugate.c:117 forms them) are made by all 64 lanes when a tile is
 // stored, so a row's chain is one LDS read per 4 columns and 4 dependent
 // adds.  Rows are padded to 516 floats: 16-B aligned, and lanes 0-15 reading
 // columns 4j..4j+3 hit banks 4*lane + 4j .. +3, all distinct.
-// Measured at N=8192: 62 us per matVec (the 64-row kernel: 166 us); an
+// Measured at N=8192: 62 us per matVec (the 64-row kernel, removed: 166 us); an
 // 8-row x 1024-column variant (32 MiB in flight) measured 64 us.
 constexpr int kRef2Rows = 16, kRef2TC = 512, kRef2Ld = kRef2TC + 4;
 __global__ __launch_bounds__(64) void k_matvec_ref_f32_r16(const float *__restrict__ A, int64_t lda,
@@ -372,115 +277,13 @@ __device__ __forceinline__ float dot_ref_body(int64_t n, const DotArgs &d, f4v (
 constexpr int kRef3Rows = 32, kRef3TC = 512, kRef3Q = kRef3TC / 4, kRef3Ld4 = kRef3Q + 1;
 constexpr int kRef3K = kRef3Rows * kRef3Q / 256;
 static_assert(kRef3K == 16, "lane t: column quad t % 128 of rows t / 128 + 2k");
-template <bool FULL>
-__global__ __launch_bounds__(256) void k_matvec_ref_f32_w4(const float *__restrict__ A, int64_t lda,
-                                                           int64_t rows, int64_t cols,
-                                                           const float *__restrict__ v,
-                                                           float *__restrict__ out,
-                                                           const int64_t *gate) {
-#pragma clang fp contract(off)
-    if (gate && *gate) return;  // converged in an earlier iteration (device-side gating)
-    typedef float f4 __attribute__((ext_vector_type(4)));
-    __shared__ f4 prod[2][kRef3Rows * kRef3Ld4];
-    const int t = threadIdx.x;
-    const int64_t row0 = (int64_t)blockIdx.x * kRef3Rows;
-    const int64_t ntiles = (cols + kRef3TC - 1) / kRef3TC;
-    const int quad = t % kRef3Q, rsub = t / kRef3Q;
-    const int64_t brows = rows - row0 < kRef3Rows ? rows - row0 : kRef3Rows;
-    const __amdgpu_buffer_rsrc_t ars =
-        __builtin_amdgcn_make_buffer_rsrc((void *)(A + row0 * lda), 0, (int)(brows * lda * 4), 0x00020000);
-    const __amdgpu_buffer_rsrc_t vrs = __builtin_amdgcn_make_buffer_rsrc((void *)v, 0, (int)(cols * 4), 0x00020000);
-    const int voff = (int)((rsub * lda + 4 * quad) * 4);
-    const int end_off = (int)(brows * lda * 4);  // a tile past the end: every load out of range
-    f4 a0[kRef3K], a1[kRef3K];
-    f4 p0, p1;
-    auto issue = [&](f4 (&a)[kRef3K], f4 &pv, int64_t tile) {
-        const bool real = tile < ntiles;
-        const int c4 = (int)(tile * kRef3TC * 4);
-#pragma unroll
-        for (int k = 0; k < kRef3K; ++k)
-            a[k] = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(
-                                              ars, voff, real ? (int)(2 * k * lda * 4) + c4 : end_off, 2));
-        pv = __builtin_bit_cast(f4, __builtin_amdgcn_raw_buffer_load_b128(vrs, quad * 16, real ? c4 : (int)(cols * 4), 0));
-    };
-    auto store = [&](f4 (&a)[kRef3K], f4 &pv, int slot, int64_t tile) {
-        if (!FULL) {  // columns past `cols`: +0 products whatever A's padding holds
-            const int64_t cq = tile * kRef3TC + 4 * quad;
-            for (int e = 0; e < 4; ++e)
-                if (cq + e >= cols) {
-                    pv[e] = 0.0f;
-#pragma unroll
-                    for (int k = 0; k < kRef3K; ++k) a[k][e] = 0.0f;
-                }
-        }
-#pragma unroll
-        for (int k = 0; k < kRef3K; ++k) prod[slot][(rsub + 2 * k) * kRef3Ld4 + quad] = a[k] * pv;
-    };
-    float acc = 0.0f;  // matvec[i] = 0.0  (serialConjugate.c:114)
-    auto chain = [&](int slot) {  // matvec[i] += A[i][j] * x[j], j ascending (:117)
-        const f4 *trow = &prod[slot][t * kRef3Ld4];
-        constexpr int G = 8;  // two register sets of G quads: one read from LDS while the other is added
-        f4 q[G], qn[G];
-        auto add = [&](const f4 (&w)[G]) {
-#pragma unroll
-            for (int u = 0; u < G; ++u) {
-                acc = acc + w[u].x;
-                acc = acc + w[u].y;
-                acc = acc + w[u].z;
-                acc = acc + w[u].w;
-            }
-        };
-#pragma unroll
-        for (int u = 0; u < G; ++u) q[u] = trow[u];
-#pragma unroll 1
-        for (int j4 = 0; j4 < kRef3Q; j4 += 2 * G) {
-#pragma unroll
-            for (int u = 0; u < G; ++u) qn[u] = trow[j4 + G + u];
-            add(q);
-            if (j4 + 2 * G < kRef3Q) {
-#pragma unroll
-                for (int u = 0; u < G; ++u) q[u] = trow[j4 + 2 * G + u];
-            }
-            add(qn);
-        }
-    };
-    issue(a0, p0, 0);
-    __builtin_amdgcn_sched_barrier(0);
-    issue(a1, p1, 1);
-    __builtin_amdgcn_sched_barrier(0);
-    store(a0, p0, 0, 0);
-    __builtin_amdgcn_sched_barrier(0);
-    issue(a0, p0, 2);
-    __builtin_amdgcn_sched_barrier(0);
-    __syncthreads();
-    // step for tile tt (slot tt & 1): wave 0 adds it up; every lane stores
-    // tile tt + 1 (register set (tt + 1) & 1) into the other slot and reuses
-    // that set for tile tt + 3.  Unrolled by two so the sets are static.
-    for (int64_t tt = 0; tt < ntiles; tt += 2) {
-        if (t < kRef3Rows) chain(0);
-        __builtin_amdgcn_sched_barrier(0);
-        store(a1, p1, 1, tt + 1);
-        __builtin_amdgcn_sched_barrier(0);
-        issue(a1, p1, tt + 3);
-        __builtin_amdgcn_sched_barrier(0);
-        __syncthreads();
-        if (t < kRef3Rows && tt + 1 < ntiles) chain(1);
-        __builtin_amdgcn_sched_barrier(0);
-        store(a0, p0, 0, tt + 2);
-        __builtin_amdgcn_sched_barrier(0);
-        issue(a0, p0, tt + 4);
-        __builtin_amdgcn_sched_barrier(0);
-        __syncthreads();
-    }
-    if (t < kRef3Rows && row0 + t < rows) out[row0 + t] = acc;
-}
-
-// The same with a dedicated adding wave: 5 waves, wave 0 only runs the
-// chains and waves 1-4 only load and form products, so a step costs
-// max(chain, loads) rather than chain + wave 0's own share of the loads.
-// Measured at N=8192 (rocprofv3, profiles/r02_kernel_stats_ref_f32_n8192.csv):
-// 49.6 us against 53.9 for k_matvec_ref_f32_w4 and 62.3 for the 16-row
-// kernel; a third register set (192 KiB in flight per CU) measured 51.9.
+// With a dedicated adding wave: 5 waves, wave 0 only runs the chains and
+// waves 1-4 only load and form products, so a step costs max(chain, loads)
+// rather than chain + wave 0's own share of the loads.  Measured at N=8192
+// (rocprofv3, profiles/r02_kernel_stats_ref_f32_n8192.csv): 49.6 us against
+// 53.9 for the 4-wave form in which wave 0 also loads (removed in round 5) and
+// 62.3 for the 16-row kernel; a third register set (192 KiB in flight per CU)
+// measured 51.9.
 //
 // DOT (the single-GPU two-launch iteration): the rows go out write-through
 // (sc1) and the last block to arrive (ticket) runs vecVec(p, Ap) over all
@@ -626,51 +429,6 @@ __global__ __launch_bounds__(320) void k_matvec_ref_f32_w5(const float *__restri
     if (DOT) dot_epilogue(rows, out, pown, dot_out, ticket, t);
 }
 
-// vecVec: one wave; products in parallel, the sum strictly sequential in
-// index order (s = s + a_i b_i), broadcast lane by lane with v_readlane.
-__global__ __launch_bounds__(64) void k_dot_ref_f32(int64_t n, const float *__restrict__ a,
-                                                    const float *__restrict__ b, float *out,
-                                                    const int64_t *gate) {
-#pragma clang fp contract(off)
-    if (gate && *gate) return;  // converged in an earlier iteration (device-side gating)
-    // One wave.  The products of 8 chunks of 64 (each rounded to float, as
-    // serialConjugate.c:150 forms them) go to LDS; then every lane walks them
-    // in index order with 16-B broadcast reads and adds them one by one, the
-    // reference's single sequential sum (all lanes hold the same s).
-    constexpr int B = 8;
-    typedef float f4 __attribute__((ext_vector_type(4)));
-    __shared__ f4 sp[B * 64 / 4];
-    float *spf = reinterpret_cast<float *>(sp);
-    const int lane = threadIdx.x;
-    float s = 0.0f;
-    for (int64_t c0 = 0; c0 < n; c0 += 64 * B) {
-        float pr[B];
-#pragma unroll
-        for (int u = 0; u < B; ++u) {
-            const int64_t i = c0 + u * 64 + lane;
-            pr[u] = i < n ? a[i] * b[i] : 0.0f;
-        }
-#pragma unroll
-        for (int u = 0; u < B; ++u) spf[u * 64 + lane] = pr[u];
-        __syncthreads();
-        const int64_t left = n - c0;
-        if (left >= 64 * B) {
-#pragma unroll 8
-            for (int q = 0; q < B * 16; ++q) {
-                const f4 v = sp[q];
-                s = s + v.x;
-                s = s + v.y;
-                s = s + v.z;
-                s = s + v.w;
-            }
-        } else {
-            for (int i = 0; i < (int)left; ++i) s = s + spf[i];
-        }
-        __syncthreads();
-    }
-    if (lane == 0) *out = s;
-}
-
 template <int MODE>
 __global__ __launch_bounds__(256) void k_dot_ref_f32_blk(int64_t n, DotArgs d, float *out, const int64_t *gate,
                                                          ConvArgs cv) {
@@ -780,45 +538,31 @@ __global__ __launch_bounds__(kNT) void k_update_p_ref_f32(int64_t n, float *__re
 hipError_t matvec_ref_f32(const float *A, int64_t lda, int64_t rows, int64_t cols, const float *v,
                           float *out, hipStream_t s, const int64_t *gate) {
     if (rows <= 0) return hipSuccess;
-    const int variant = env_int("CGX_REF_MV", 3);
     // 16-B aligned rows and x; the buffer offsets (32 rows of lda floats) fit in 31 bits
     const bool vec_ok = (lda & 3) == 0 && lda < (int64_t(1) << 23) &&
                         ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(v)) & 15) == 0;
-    if (variant == 1)  // the 64-row, 128-column-tile kernel (kept for A/B)
-        hipLaunchKernelGGL(k_matvec_ref_f32, dim3((unsigned)((rows + 63) / 64)), dim3(64), 0, s, A, lda, rows,
-                           cols, v, out, gate);
-    else if ((variant == 3 || variant == 4) && vec_ok) {
+    if (vec_ok) {
         const bool full = rows % kRef3Rows == 0 && cols % kRef3TC == 0;
         const dim3 grid((unsigned)((rows + kRef3Rows - 1) / kRef3Rows));
-        if (variant == 3)  // a dedicated adding wave (default)
-            hipLaunchKernelGGL((full ? k_matvec_ref_f32_w5<true, false> : k_matvec_ref_f32_w5<false, false>), grid,
-                               dim3(320), 0, s, A, lda, rows, cols, v, out, gate, nullptr, nullptr, nullptr);
-        else  // wave 0 adds and loads
-            hipLaunchKernelGGL(full ? k_matvec_ref_f32_w4<true> : k_matvec_ref_f32_w4<false>, grid, dim3(256), 0, s,
-                               A, lda, rows, cols, v, out, gate);
-    }
-    else
+        hipLaunchKernelGGL((full ? k_matvec_ref_f32_w5<true, false> : k_matvec_ref_f32_w5<false, false>), grid,
+                           dim3(320), 0, s, A, lda, rows, cols, v, out, gate, nullptr, nullptr, nullptr);
+    } else {  // unaligned rows: the 16-row kernel (scalar loads)
         hipLaunchKernelGGL(k_matvec_ref_f32_r16, dim3((unsigned)((rows + kRef2Rows - 1) / kRef2Rows)), dim3(64), 0,
                            s, A, lda, rows, cols, v, out, gate);
+    }
     return hipGetLastError();
 }
 
 hipError_t dot_ref_f32(int64_t n, const float *a, const float *b, float *out, hipStream_t s, const int64_t *gate) {
-    if (env_int("CGX_REF_DOT", 2) == 1)  // the one-wave kernel (kept for A/B)
-        hipLaunchKernelGGL(k_dot_ref_f32, dim3(1), dim3(64), 0, s, n, a, b, out, gate);
-    else
-    {
-        DotArgs d;
-        d.a = a;
-        d.b = b;
-        hipLaunchKernelGGL(k_dot_ref_f32_blk<kDotPlain>, dim3(1), dim3(256), 0, s, n, d, out, gate, ConvArgs{});
-    }
+    DotArgs d;
+    d.a = a;
+    d.b = b;
+    hipLaunchKernelGGL(k_dot_ref_f32_blk<kDotPlain>, dim3(1), dim3(256), 0, s, n, d, out, gate, ConvArgs{});
     return hipGetLastError();
 }
 
 bool matvec_dot_ref_f32_fusable(const float *A, int64_t lda, const float *v) {
-    return env_int("CGX_REF_MV", 3) == 3 && env_int("CGX_REF_DOT", 2) == 2 && (lda & 3) == 0 &&
-           lda < (int64_t(1) << 23) && ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(v)) & 15) == 0;
+    return (lda & 3) == 0 && lda < (int64_t(1) << 23) && ((reinterpret_cast<uintptr_t>(A) | reinterpret_cast<uintptr_t>(v)) & 15) == 0;
 }
 
 hipError_t matvec_dot_ref_f32(const float *A, int64_t lda, int64_t rows, int64_t cols, const float *v, float *out,
@@ -912,8 +656,6 @@ hipError_t preload_ref_f32() {
     hipFuncAttributes a;
     hipError_t e = hipFuncGetAttributes(&a, reinterpret_cast<const void *>(k_matvec_ref_f32_r16));
     if (e == hipSuccess) e = hipFuncGetAttributes(&a, reinterpret_cast<const void *>(k_dot_ref_f32_blk<kDotXR>));
-    if (e == hipSuccess) e = hipFuncGetAttributes(&a, reinterpret_cast<const void *>(k_matvec_ref_f32_w4<true>));
-    if (e == hipSuccess) e = hipFuncGetAttributes(&a, reinterpret_cast<const void *>(k_matvec_ref_f32_w4<false>));
     if (e == hipSuccess) e = hipFuncGetAttributes(&a, reinterpret_cast<const void *>(k_matvec_ref_f32_w5<true, false>));
     if (e == hipSuccess) e = hipFuncGetAttributes(&a, reinterpret_cast<const void *>(k_matvec_ref_f32_w5<true, true>));
     if (e == hipSuccess) e = hipFuncGetAttributes(&a, reinterpret_cast<const void *>(k_dot_ref_f32_blk<kDotXRP>));

@@ -176,19 +176,16 @@ int alloc_shard(cgx_ctx *c, Shard &s) {
         // record, which the deciding kernel stores with system-scope atomics
         // itself, so the events need no system-scope release of their own: a
         // convergence-tested solve 2-10 % faster at N = 512-8192
-        // (profiles/r03_look_ab.jsonl; CGX_LOOK_FENCE=1 puts it back).
-        const char *f = std::getenv("CGX_LOOK_FENCE");
-        const unsigned lflags = hipEventDisableTiming | ((f && *f == '1') ? 0u : (unsigned)hipEventDisableSystemFence);
+        // (profiles/r03_look_ab.jsonl).
+        const unsigned lflags = hipEventDisableTiming | (unsigned)hipEventDisableSystemFence;
         for (int q = 0; q < kLookRing; ++q) HIPT(hipEventCreateWithFlags(&s.ev_look[q], lflags));
     }
     // Timing-only events (the matVec brackets) skip the system-scope release
     // an event does by default when it completes: that fence writes back and
     // invalidates the caches; an event costs 3.3 us on the stream without it,
     // 4.4 us with it (profiles/r03_event_fence_ab.jsonl).  Nothing reads memory
-    // through these events; they only time.  CGX_EVENT_FENCE=1 restores the
-    // default events.
-    const char *ef = std::getenv("CGX_EVENT_FENCE");
-    const unsigned tflags = (ef && *ef == '1') ? hipEventDefault : hipEventDisableSystemFence;
+    // through these events; they only time.
+    const unsigned tflags = hipEventDisableSystemFence;
     if (c->flags & CGX_TIMING) {
         s.ev_t.resize(2 * kEvPairs);
         for (auto &e : s.ev_t) HIPT(hipEventCreateWithFlags(&e, tflags));
@@ -285,17 +282,17 @@ cgx_ctx *new_ctx(int64_t n, int nranks, int flags) {
     return c;
 }
 
-// Overlap p's exchange with the own-column-block part of the matVec: dense
-// fp64 resident A, more than one row block, every block aligned to the
-// matVec's 128-column chunks.  CGX_OVERLAP=0 disables it.
-bool can_overlap(const cgx_ctx *c) {
-    if (c->op != OP_DENSE || f32ref(c) || (c->flags & CGX_HOST_STREAM)) return false;
-    if (c->flags & (CGX_NO_OVERLAP | CGX_COMM_P2P)) return false;
+// The rotated column order (cgx_ctx::rot), which makes the overlapped
+// exchange possible and bit-neutral: dense fp64 resident row-major A, more
+// than one row block, every block aligned to the matVec's 128-column chunks
+// (also with CGX_COMM_P2P, which never overlaps: the same bits as the
+// collective exchange).  CGX_OVERLAP=force also takes it at world size 1
+// in rank mode (the in-place allgather on the comm stream and the event
+// hand-offs run with nothing to exchange), so one GPU can execute the
+// rank-mode overlap path.
+bool can_rotate(const cgx_ctx *c) {
+    if (c->op != OP_DENSE || f32ref(c) || (c->flags & (CGX_HOST_STREAM | CGX_SYMMETRIC))) return false;
     const char *e = std::getenv("CGX_OVERLAP");
-    if (e && *e == '0') return false;
-    // CGX_OVERLAP=force: also at world size 1 in rank mode (the in-place
-    // allgather on the comm stream and the event hand-offs run with nothing to
-    // exchange), so one GPU can execute the rank-mode overlap path.
     const bool force = e && std::strcmp(e, "force") == 0;
     if (c->mode == M_SINGLE || (c->mode == M_RCCL && c->nranks == 1 && !force)) return false;
     for (const auto &s : c->sh)
@@ -367,9 +364,10 @@ int finish_create(cgx_ctx *c, cgx_ctx **out) {
         c->xchg_kernels = !(e && !std::strcmp(e, "copy"));
         const char *f = std::getenv("CGX_LOCAL_FUSE");
         c->fuse_combine = c->mode == M_LOCAL && c->xchg_kernels && !(f && *f == '0') && !(c->flags & CGX_F32_REF) &&
-                          !(c->flags & CGX_COMM_P2P) && c->op == OP_DENSE && (int)c->sh.size() <= kMaxPeers;
+                          !(c->flags & CGX_COMM_P2P) && (int)c->sh.size() <= kMaxPeers;
     }
-    c->overlap = can_overlap(c);
+    c->rot = can_rotate(c);
+    c->overlap = false;  // choose_overlap below, once the row blocks exist
     c->fused_p = can_fuse_p(c);
     {  // the folded form of the two-launch iteration (CGX_FOLD_P=0 / 1: never / at any fused n)
         const char *e = std::getenv("CGX_FOLD_P");
@@ -380,9 +378,16 @@ int finish_create(cgx_ctx *c, cgx_ctx **out) {
     if (c->op == OP_POISSON) {  // CGX_POISSON_FUSED=0: the three-kernel split (stencil, r, x/p)
         const char *e = std::getenv("CGX_POISSON_FUSED");
         c->fused = !(e && *e == '0') && poisson_fusable(c->sh[0].nloc / c->m, c->m);
+        // one process, several slabs: the next k_poisson_p reads r's halo rows
+        // in place (no copies, nothing to overlap); CGX_LOCAL_XCHG=copy keeps
+        // round 3's peer copies and combine kernels (the same bits)
+        c->halo_pull = c->fused && c->mode == M_LOCAL && c->xchg_kernels;
+        if (!c->fused || c->mode != M_LOCAL) c->fuse_combine = false;  // dense: decided above; Poisson: fused only
+        // rank mode: r's halo rows travel by ncclSend/Recv on the comm stream
+        // while k_poisson_p runs the slab's interior (CGX_HALO_OVERLAP=0: before it)
         const char *h = std::getenv("CGX_HALO_OVERLAP");
         const bool force = h && std::strcmp(h, "force") == 0;  // also at world size 1 in rank mode
-        c->halo_overlap = c->fused && !(h && *h == '0') && c->mode != M_SINGLE &&
+        c->halo_overlap = c->fused && !(h && *h == '0') && !c->halo_pull && c->mode != M_SINGLE &&
                           !(c->mode == M_RCCL && c->nranks == 1 && !force);
         const char *xd = std::getenv("CGX_POISSON_XDEFER");
         c->xdefer = c->fused && !(xd && *xd == '0');
@@ -391,16 +396,21 @@ int finish_create(cgx_ctx *c, cgx_ctx **out) {
         // profiles/r03_poisson_xdefer3_ab.jsonl); CGX_POISSON_XDEFER=2: every other
         c->xd = !c->xdefer ? 1 : (xd && *xd == '2') ? 2 : 3;
     }
+    auto undo = [c](int rc) {
+        std::string keep = g_err;
+        for (auto &t : c->sh) free_shard(t);
+        delete c;
+        snprintf(g_err, sizeof g_err, "%s", keep.c_str());
+        return rc;
+    };
     for (auto &s : c->sh) {
         int rc = alloc_shard(c, s);
-        if (rc == CGX_OK && (c->overlap || c->halo_overlap) && &s == &c->sh.back()) rc = alloc_overlap(c);
-        if (rc != CGX_OK) {
-            std::string keep = g_err;
-            for (auto &t : c->sh) free_shard(t);
-            delete c;
-            snprintf(g_err, sizeof g_err, "%s", keep.c_str());
-            return rc;
-        }
+        if (rc == CGX_OK && (c->rot || c->halo_overlap) && &s == &c->sh.back()) rc = alloc_overlap(c);
+        if (rc != CGX_OK) return undo(rc);
+    }
+    if (c->rot) {  // overlapped or plain exchange, by measurement (rank mode: a collective decision)
+        const int rc = choose_overlap(c);
+        if (rc != CGX_OK) return undo(rc);
     }
     // one enqueuing thread per row block (cgx_local_mt.hip); without it the
     // iteration is enqueued by the calling thread, the same launches
@@ -693,6 +703,17 @@ int cgx_get_info(const cgx_ctx *c, cgx_info *info) {
     return CGX_OK;
 }
 
+int cgx_get_overlap_info(const cgx_ctx *c, cgx_overlap_info *info) {
+    if (!c || !info) return fail(CGX_ERR_ARG, "NULL argument");
+    info->active = c->overlap ? 1 : 0;
+    info->decided_by = c->ov_how;
+    info->allgather_us = c->ov_ag_us;
+    info->split_us = c->ov_split_us;
+    info->one_launch_us = c->ov_one_us;
+    info->split_cost_us = c->ov_cost_us;
+    return CGX_OK;
+}
+
 int cgx_get_comm_info(cgx_ctx *c, cgx_comm_info *info) {
     if (!c || !info) return fail(CGX_ERR_ARG, "NULL argument");
     std::memset(info, 0, sizeof *info);
@@ -790,6 +811,7 @@ int cgx_set_rows(cgx_ctx *c, int64_t row0, int64_t nrows, const void *A_rows, in
         }
         TRY(rank_wait_stream(c, s.stream, "the copies of cgx_set_rows"));
     }
+    if (x_rows && row0 == 0 && nrows == c->n) c->x_incomplete = false;  // x fully defined again
     c->state = ST_IDLE;
     return CGX_OK;
 }

@@ -358,7 +358,7 @@ int sym_grid(int device) {
     // for a free CU would run its whole range after the others.  (The
     // occupancy query can over-report by a block for 256-thread kernels:
     // cdna_hip_programming.md.)
-    per_cu = std::min(per_cu, env_int("CGX_SYM_BLOCKS_PER_CU", 1));
+    per_cu = std::min(per_cu, env_opt("CGX_SYM_PLAN", "bpc", 1));
     return cus * per_cu;
 }
 
@@ -368,10 +368,10 @@ int sym_grid(int device) {
 // units per block), so the streams spread over the HBM channels however the
 // pages land.  N=65536: 399.5-399.7 it/s (6.91 TB/s on the stored bytes)
 // against 387.6-388.6 with 1026, four processes each, alternating
-// (profiles/r03_symmetric_per_odd_ab.jsonl).  CGX_SYM_PER_ODD=0: the plain count.
+// (profiles/r03_symmetric_per_odd_ab.jsonl).  CGX_SYM_PLAN=odd=0: the plain count.
 static int64_t sym_units_per_block(int64_t units, int grid) {
     int64_t per = (units + grid - 1) / grid;
-    if (env_int("CGX_SYM_PER_ODD", 1) && per > 1) per |= 1;
+    if (env_opt("CGX_SYM_PLAN", "odd", 1) && per > 1) per |= 1;
     return per;
 }
 
@@ -392,7 +392,7 @@ hipError_t symv_tiles_f64(const double *At, int64_t q_base, int64_t count, int64
         ((reinterpret_cast<uintptr_t>(At) | reinterpret_cast<uintptr_t>(p)) & 15))
         return hipErrorInvalidValue;
     const int64_t per = sym_units_per_block(2 * count, grid);
-    auto fn = env_int("CGX_SYM_NT", 1) ? k_symv_f64<1> : k_symv_f64<0>;
+    auto fn = env_opt("CGX_SYM_PLAN", "nt", 1) ? k_symv_f64<1> : k_symv_f64<0>;
     hipLaunchKernelGGL(fn, dim3(grid), dim3(kSymNT), 0, s, At, lda / kSymT, q_base, count, per, tile_runs ? 1 : 0, p,
                        prow, pcol, gate);
     return hipGetLastError();

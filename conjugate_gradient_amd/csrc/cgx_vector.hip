@@ -571,9 +571,7 @@ hipError_t update_xr_f64(int64_t n, double *x, double *r, const double *p, const
                          const double *rsold, const double *pAp, double *rr_out, const RedWs &ws,
                          hipStream_t s) {
     const bool vec = al16(x) && al16(r) && al16(p) && al16(Ap);
-    const int vp = env_int("CGX_VEC_POLICY", 2);
-    auto fn = !vec ? k_update_xr_f64<false> : vp == 1 ? k_update_xr_f64<true, 1>
-                                            : vp == 2 ? k_update_xr_f64<true, 2> : k_update_xr_f64<true, 0>;
+    auto fn = !vec ? k_update_xr_f64<false> : k_update_xr_f64<true, 2>;  // the solver kernels' policy (ldv)
     hipLaunchKernelGGL(fn, dim3(grid_vec(n)), dim3(kNT), 0, s, n, x, r, p, Ap, rsold, pAp, rr_out, ws.partials,
                        ws.tickets + T_XR);
     return hipGetLastError();
@@ -582,9 +580,7 @@ hipError_t update_xr_f64(int64_t n, double *x, double *r, const double *p, const
 hipError_t update_p_f64(int64_t n, double *p, const double *r, const double *rr, const double *rsold,
                         hipStream_t s) {
     const bool vec = al16(p) && al16(r);
-    const int vp = env_int("CGX_VEC_POLICY", 2);
-    auto fn = !vec ? k_update_p_f64<false> : vp == 1 ? k_update_p_f64<true, 1>
-                                           : vp == 2 ? k_update_p_f64<true, 2> : k_update_p_f64<true, 0>;
+    auto fn = !vec ? k_update_p_f64<false> : k_update_p_f64<true, 2>;
     hipLaunchKernelGGL(fn, dim3(grid_vec(n)), dim3(kNT), 0, s, n, p, r, rr, rsold);
     return hipGetLastError();
 }

@@ -75,8 +75,14 @@ extern "C" {
 #define CGX_TIMING       0x100 /* time every matVec launch with HIP events      */
 #define CGX_NO_OVERLAP   0x400 /* multi-shard dense fp64: do not overlap the p
                                   exchange with the own-column-block matVec
-                                  (on by default when every row block is a
-                                  multiple of 128 rows; env CGX_OVERLAP=0) */
+                                  (the allgather, then one matVec launch).
+                                  Without it the form is chosen at creation
+                                  when every row block is a multiple of 128
+                                  rows: the overlap runs only if the measured
+                                  allgather takes longer than splitting the
+                                  matVec in two costs (cgx_get_overlap_info;
+                                  env CGX_OVERLAP=0 / 1: never / always).  Both
+                                  forms give the same bits. */
 #define CGX_OVERLAP_ACTIVE 0x800 /* reported in cgx_info.flags when it is on */
 #define CGX_FUSED_ACTIVE 0x2000 /* reported in cgx_info.flags: a fused
                                    iteration is on -- the Poisson operator's
@@ -214,6 +220,28 @@ typedef struct {
     char pci_bus_id[32];
 } cgx_comm_info;
 
+/* How the p exchange of an aligned multi-shard dense fp64 context was chosen
+ * (parallel_cg.c:290-293: allgather p, then the matVec).  At creation the
+ * context times, on its own row blocks, the matVec split in two launches
+ * (own column block, then the rest) against the one launch, and the
+ * allgather of p (RCCL in rank mode, the pull kernels in one process); in
+ * rank mode the maxima over ranks, so every rank decides alike.  The
+ * overlapped form runs when the allgather takes longer than the split costs.
+ * Times in microseconds, -1 when not measured. */
+#define CGX_OV_MEASURED 0 /* chosen from the measurement                     */
+#define CGX_OV_FORCED   1 /* CGX_OVERLAP=1 / force: on                       */
+#define CGX_OV_OFF      2 /* CGX_NO_OVERLAP or CGX_OVERLAP=0: off            */
+#define CGX_OV_NA       3 /* no choice: one shard, unaligned blocks, fp32,
+                             streamed A, p2p exchange                        */
+typedef struct {
+    int    active;         /* the overlapped form runs (CGX_OVERLAP_ACTIVE) */
+    int    decided_by;     /* CGX_OV_*                                      */
+    double allgather_us;   /* one allgather of p                            */
+    double split_us;       /* own-block launch + rest launch                */
+    double one_launch_us;  /* the one launch over the whole row block       */
+    double split_cost_us;  /* split_us - one_launch_us (max over blocks)    */
+} cgx_overlap_info;
+
 /* ---- errors / info ------------------------------------------------------- */
 const char *cgx_strerror(int code);
 /* Detail message of the last failure on this thread ("" if none). */
@@ -279,6 +307,7 @@ int cgx_create_poisson_rank(cgx_ctx **ctx, int64_t m, int rank, int nranks,
 int cgx_destroy(cgx_ctx *ctx);
 int cgx_get_info(const cgx_ctx *ctx, cgx_info *info);
 int cgx_get_comm_info(cgx_ctx *ctx, cgx_comm_info *info);
+int cgx_get_overlap_info(const cgx_ctx *ctx, cgx_overlap_info *info);
 
 /* ---- data in / out (host arrays; element type per flags) ----------------- */
 /* Rows [row0, row0+nrows) of A (row-major, host leading dimension lda_host),

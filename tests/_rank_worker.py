@@ -56,6 +56,7 @@ def main():
     else:
         flags = {"f32ref": cg.CGX_F32_REF, "p2p": cg.CGX_COMM_P2P, "nooverlap": cg.CGX_NO_OVERLAP,
                  "deterministic": cg.CGX_DETERMINISTIC, "headline_det": cg.CGX_DETERMINISTIC,
+                 "det_overlap": cg.CGX_DETERMINISTIC,
                  "p2p_f32ref": cg.CGX_F32_REF | cg.CGX_COMM_P2P}.get(mode, cg.CGX_F64)
         if not flags & cg.CGX_F32_REF:
             flags |= cg.CGX_F64
@@ -67,8 +68,14 @@ def main():
             x0 = np.zeros(n)
         else:
             A, b, x0 = case(f"spd{n}", np.float32 if f32 else np.float64)
-        with cg.Solver(n, rank=rank, nranks=P, unique_id=uid, device=0, flags=flags) as s:
+        if mode in ("overlap_on", "det_overlap"):  # the overlapped form whatever the measurement says
+            os.environ["CGX_OVERLAP"] = "1"
+        # one GPU per rank where the box has them (tests/test_gpu_multidevice.py), else all on device 0
+        dev = rank if os.environ.get("CGX_TEST_RANK_DEVICE") == "rank" else 0
+        with cg.Solver(n, rank=rank, nranks=P, unique_id=uid, device=dev, flags=flags) as s:
+            res["comm"] = s.comm_info()
             res["overlap"] = bool(s.info.flags & cg.CGX_OVERLAP_ACTIVE)
+            res["overlap_info"] = s.overlap_info()
             res["nrows"] = s.info.nrows
             if A is None:
                 s.generate_spd(42)

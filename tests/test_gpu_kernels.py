@@ -39,16 +39,13 @@ def test_matvec_ref_f32_nonfinite_bitwise(rows, cols):
     assert np.array_equal(out.to_host().view(np.uint32), ref.view(np.uint32))
 
 
-# CGX_REF_MV: 64-row x 128 tiles / 16-row x 512 tiles / 32-row blocks with two tiles in flight and a
-# dedicated adding wave (default) / the same with wave 0 also loading.  3 and 4 run their FULL form when
-# rows % 32 == 0 and cols % 512 == 0, a bounds-checked form for other multiples of 4, the 16-row kernel when
-# cols % 4 != 0.
-@pytest.mark.parametrize("variant", ["1", "2", "3", "4"])
+# The 32-row blocks with two 512-column tiles in flight and a dedicated adding wave: their FULL form when
+# rows % 32 == 0 and cols % 512 == 0, a bounds-checked form for other multiples of 4; the 16-row kernel
+# when cols % 4 != 0 (rows not 16-B aligned).
 @pytest.mark.parametrize("rows,cols", [(1, 1), (2, 2), (5, 3), (64, 64), (300, 257), (1000, 1000), (8192, 96),
                                        (16, 512), (17, 513), (33, 1536), (48, 1025), (100, 4100), (32, 512),
                                        (64, 1024), (96, 2560), (31, 4), (33, 516), (1024, 8192), (8192, 8192)])
-def test_matvec_ref_f32_bitwise(monkeypatch, variant, rows, cols):
-    monkeypatch.setenv("CGX_REF_MV", variant)
+def test_matvec_ref_f32_bitwise(rows, cols):
     rng = np.random.default_rng(rows * 7 + cols)
     A = rng.random((rows, cols), dtype=np.float32) - 0.5
     v = rng.random(cols, dtype=np.float32)
@@ -58,10 +55,8 @@ def test_matvec_ref_f32_bitwise(monkeypatch, variant, rows, cols):
     assert np.array_equal(out.to_host().view(np.uint32), ref.view(np.uint32))
 
 
-@pytest.mark.parametrize("variant", ["1", "2"])  # CGX_REF_DOT: one wave / 4 waves, loads off the chain (default)
 @pytest.mark.parametrize("n", [1, 63, 64, 65, 1000, 4096, 4097, 8192, 8193, 20000])
-def test_dot_ref_f32_bitwise(monkeypatch, variant, n):
-    monkeypatch.setenv("CGX_REF_DOT", variant)
+def test_dot_ref_f32_bitwise(n):
     rng = np.random.default_rng(n)
     a = rng.random(n, dtype=np.float32) - 0.5
     b = rng.random(n, dtype=np.float32)
@@ -159,8 +154,7 @@ def test_matvec_small_lds_bitwise_equals_l2_kernel(monkeypatch, rows, cols):
     assert np.all(np.abs(base - oracle.matvec_f64(A, v)) <= F64_TOL * (np.abs(A) @ np.abs(v)))
     monkeypatch.setenv("CGX_MV_SMALL", "2")
     for nt, u in (("512", "8"), ("512", "4"), ("1024", "4"), ("1024", "8")):
-        monkeypatch.setenv("CGX_SMALL_NT", nt)
-        monkeypatch.setenv("CGX_SMALL_U", u)
+        monkeypatch.setenv("CGX_SMALL_PLAN", f"threads={nt},U={u}")
         out = cg.DeviceArray(rows)
         cg.matVec(A_d, v_d, out, rows, cols)
         assert np.array_equal(out.to_host(), base), (nt, u)
@@ -185,9 +179,7 @@ def test_matvec_f64_every_plan_bitwise_equal(monkeypatch, rows, cols):
     bound = F64_TOL * (np.abs(A) @ np.abs(v))
     assert np.all(np.abs(base - ref) <= bound)
     for R, U, nt in MV_PLANS:
-        monkeypatch.setenv("CGX_MV_R", str(R))
-        monkeypatch.setenv("CGX_MV_U", str(U))
-        monkeypatch.setenv("CGX_MV_NT", str(nt))
+        monkeypatch.setenv("CGX_MV_PLAN", f"R={R},U={U},nt={nt}")
         out = cg.DeviceArray(rows)
         cg.matVec(A_d, v_d, out, rows, cols)
         assert np.array_equal(out.to_host(), base), (R, U, nt)

@@ -75,17 +75,33 @@ def run_ranks(tmp_path, mode, n, P, timeout=150):
 
 @pytest.mark.timeout(200)
 @pytest.mark.parametrize("P", [2, 4])
-@pytest.mark.parametrize("mode", ["collective", "nooverlap", "p2p", "deterministic"])
+@pytest.mark.parametrize("mode", ["collective", "overlap_on", "nooverlap", "p2p", "deterministic", "det_overlap"])
 def test_rank_mode_f64(tmp_path, mode, P):
+    """Row blocks of 1024/P rows (multiples of 128): the exchange form is
+    chosen at creation from the measured allgather and split cost (the same
+    on every rank), or forced (CGX_OVERLAP=1, CGX_NO_OVERLAP); p2p has no
+    choice.  Both forms give the same bits: the rank-ordered combine equals
+    the multi-shard solve, overlapped or not."""
     n = 1024
     x, res = run_ranks(tmp_path, mode, n, P)
     assert res[0]["nrows"] == n // P
-    assert res[0]["overlap"] == (mode in ("collective", "deterministic"))  # row blocks are multiples of 128
+    info = res[0]["overlap_info"]
+    for r in res:  # every rank decided alike, from the same (max over ranks) numbers
+        assert r["overlap_info"] == info and r["overlap"] == res[0]["overlap"]
+    if mode in ("collective", "deterministic"):
+        assert info["decided_by"] == "measured" and info["allgather_us"] > 0 and info["one_launch_us"] > 0
+        assert res[0]["overlap"] == (info["allgather_us"] > info["split_cost_us"])
+    elif mode in ("overlap_on", "det_overlap"):
+        assert res[0]["overlap"] and info["decided_by"] == "forced_on"
+    elif mode == "nooverlap":
+        assert not res[0]["overlap"] and info["decided_by"] == "off"
+    else:
+        assert not res[0]["overlap"] and info["decided_by"] == "n/a"
     A, b, x0 = case(f"spd{n}", np.float64)
     xo, so = oracle.cg_f64(A, b, x0, eps=1e-10)
     assert res[0]["iterations"] == so.iterations
     assert rel(x, xo) <= TOL and res[0]["relres"] <= TOL
-    if mode == "deterministic":  # rank-ordered scalar combine == the multi-shard bits
+    if mode in ("deterministic", "det_overlap"):  # rank-ordered scalar combine == the multi-shard bits
         xs = x0.copy()
         cg.conjugrad(A, b, xs, eps=1e-10, shards=[0] * P)
         assert np.array_equal(x, xs)
@@ -100,7 +116,9 @@ def test_rank_mode_f64_sizes(tmp_path, n, P):
     chunks) and a larger system, collective exchange."""
     x, res = run_ranks(tmp_path, "sized", n, P)
     assert res[0]["nrows"] == n // P
-    assert res[0]["overlap"] == ((n // P) % 128 == 0)
+    aligned = (n // P) % 128 == 0  # the form is chosen (measured) only for aligned row blocks
+    assert res[0]["overlap_info"]["decided_by"] == ("measured" if aligned else "n/a")
+    assert aligned or not res[0]["overlap"]
     A, b = oracle.spd_matlab(n, np.float64)
     xo, so = oracle.cg_f64(A, b, np.zeros(n), eps=1e-10)
     assert res[0]["iterations"] == so.iterations
@@ -178,12 +196,12 @@ def hash_oracle(n):
 @pytest.mark.timeout(600)
 def test_rank_mode_headline_n65536_world2(tmp_path):
     """BASELINE configs[2] through the rank path at full size: N=65536 on 2
-    RCCL ranks (17.2 GB of A each, the overlapped allgather, the scalar
+    RCCL ranks (17.2 GB of A each, the allgather in the measured form, the scalar
     allreduces), generated on the device; x within 1e-10 of the fp64 oracle
     with conjgrad.m's loop count, true residual <= 1e-10 ||b||."""
     n, P = 65536, 2
     x, res = run_ranks(tmp_path, "headline", n, P, timeout=500)
-    assert res[0]["nrows"] == n // P and res[0]["overlap"]
+    assert res[0]["nrows"] == n // P and res[0]["overlap_info"]["decided_by"] == "measured"
     xo, so = hash_oracle(n)
     assert res[0]["converged"] and res[0]["iterations"] == so.iterations
     assert rel(x, xo) <= TOL and res[0]["relres"] <= TOL
@@ -194,7 +212,7 @@ def test_rank_mode_headline_n65536_world2(tmp_path):
 def test_rank_mode_headline_n65536_world8(tmp_path, mode):
     """configs[2] in the driver's placement: N=65536 over 8 RCCL rank
     processes (parallel_cg.c:83's row blocks: 8192 rows x 65536 = 4.3 GB of A
-    each; the loop :283-323 with the overlapped allgather and the two scalar
+    each; the loop :283-323 with the allgather in the measured form and the two scalar
     exchanges), generated on the device, converged at eps 1e-10.  Every rank
     ends with the same x; the loop count is conjgrad.m's; x within 1e-10 of
     the fp64 oracle; true residual <= 1e-10 ||b||.  CGX_DETERMINISTIC
@@ -202,7 +220,7 @@ def test_rank_mode_headline_n65536_world8(tmp_path, mode):
     solve of the same system in one process."""
     n, P = 65536, 8
     x, res = run_ranks(tmp_path, mode, n, P, timeout=780)
-    assert res[0]["nrows"] == n // P and res[0]["overlap"]
+    assert res[0]["nrows"] == n // P and res[0]["overlap_info"]["decided_by"] == "measured"
     xo, so = hash_oracle(n)
     assert res[0]["converged"] and res[0]["iterations"] == so.iterations
     assert rel(x, xo) <= TOL and res[0]["relres"] <= TOL

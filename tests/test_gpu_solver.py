@@ -117,6 +117,8 @@ def test_local_exchange_kernels_bitwise_equal_peer_copies(monkeypatch, kind, P):
     res = {}
     # nofuse: a combine kernel per scalar instead of the folded sums; onethread: every block's work
     # enqueued by the calling thread instead of one thread per block (cgx_local_mt.hip)
+    if kind == "f64":  # the overlapped gather (f64_nooverlap: the one-launch form of the same bits)
+        monkeypatch.setenv("CGX_OVERLAP", "1")
     for form in ("kernel", "onethread", "nofuse", "copy"):
         monkeypatch.setenv("CGX_LOCAL_XCHG", "copy" if form == "copy" else "kernel")
         monkeypatch.setenv("CGX_LOCAL_FUSE", "0" if form == "nofuse" else "1")
@@ -162,6 +164,8 @@ def test_local_graph_replay_bitwise(monkeypatch, P, overlap):
     A, b = oracle.spd_hash(n, seed=11, dtype=np.float64)
     x0 = np.full(n, 0.125)
     flags = cg.CGX_F64 | (0 if overlap else cg.CGX_NO_OVERLAP)
+    if overlap:
+        monkeypatch.setenv("CGX_OVERLAP", "1")  # whatever the measurement at creation would pick
     monkeypatch.setenv("CGX_LOCAL_THREADS", "0")
 
     def run(graph, G):
@@ -467,8 +471,8 @@ def test_create_multi_leaves_no_hip_error():
     assert cg.device_link(0, 0)["link"] == "unknown" and len(cg.device_pci_bus_id(0)) >= 12
 
 
-@pytest.mark.parametrize("kind", ["single", "small_fused", "shards_overlap", "shards_plain", "gated"])
-def test_phase_times_tile_the_iteration(kind):
+@pytest.mark.parametrize("kind", ["single", "small_fused", "shards_overlap", "shards_one", "shards_plain", "gated"])
+def test_phase_times_tile_the_iteration(monkeypatch, kind):
     """CGX_PHASES: the iteration's kernels stamp their start and end on the
     device clock; the phases are resolved after the fact.  Every kernel phase
     gets one sample per iteration (the gap and the iteration one fewer), more
@@ -477,9 +481,11 @@ def test_phase_times_tile_the_iteration(kind):
     mean iteration.  A converged, device-gated solve stops sampling where the
     kernels stop running."""
     n, steps = {"small_fused": 2048, "single": 16384}.get(kind, 4096), 1100  # > the 1024-iteration stamp ring
-    devices = {"shards_overlap": [0, 0], "shards_plain": [0, 0, 0]}.get(kind)  # 4095/3 rows: no overlap
-    if kind == "shards_plain":
+    devices = {"shards_overlap": [0, 0], "shards_one": [0, 0], "shards_plain": [0, 0, 0]}.get(kind)
+    if kind == "shards_plain":  # 4095/3 rows: not 128-aligned, one launch in column order
         n = 4095
+    if kind in ("shards_overlap", "shards_one"):  # aligned: the overlapped form, or the one-launch form
+        monkeypatch.setenv("CGX_OVERLAP", "1" if kind == "shards_overlap" else "0")
     with cg.Solver(n, flags=cg.CGX_PHASES | cg.CGX_TIMING, devices=devices) as s:
         s.generate_spd(5)
         if kind == "gated":
@@ -502,7 +508,9 @@ def test_phase_times_tile_the_iteration(kind):
             "shards_overlap": {"matvec_own": S, "gather_exposed": S, "matvec": S, "combine_pap": S, "update_r": S,
                                "combine_rr": S, "update_xp": S, "gap": F},
             "shards_plain": {"gather_exposed": F, "matvec": S, "combine_pap": S, "update_r": S, "combine_rr": S,
-                             "update_xp": S}}[kind]
+                             "update_xp": S}}
+    want["shards_one"] = want["shards_plain"]
+    want = want[kind]
     for name in cg.PHASE_NAMES[:8]:
         assert ph[name]["samples"] == want.get(name, 0), (name, ph[name])
         if name in want:
@@ -852,8 +860,11 @@ def test_poisson_halo_overlap_matches(monkeypatch, m, P, eps):
     k_poisson_p does the slab's interior runs; its two edge runs follow the
     exchange and add their p.Ap share.  Same loop count and x (to 1e-12) as the
     exchange-then-kernel order (CGX_HALO_OVERLAP=0), gated and host-checked.
+    In one process the overlap exists with the peer-copy exchange
+    (CGX_LOCAL_XCHG=copy; the default pull has nothing to overlap).
     (eps above the attainable-residual floor: see test_poisson_matches_oracle.)"""
     n = m * m
+    monkeypatch.setenv("CGX_LOCAL_XCHG", "copy")
     xo, so = oracle.cg_poisson_f64(m, np.ones(n), np.zeros(n), eps=eps)
     for gated in ("1", "0"):
         monkeypatch.setenv("CGX_GATED", gated)
@@ -921,26 +932,19 @@ def test_poisson_x_every_other_iteration_is_bitwise(monkeypatch, m, shards, peri
     assert rel(a["solve1"][0], xo) <= TOL
 
 
-@pytest.mark.parametrize("side_edge", ["1", "0"])
-@pytest.mark.parametrize("rb", ["2", "4"])
-@pytest.mark.parametrize("period", ["0", "3"])
+@pytest.mark.parametrize("period", ["2", "3"])
 @pytest.mark.parametrize("m,shards", [(1024, None), (1024, [0, 0]), (512, [0] * 4)])
-def test_poisson_xr_pipelined_kernel_is_bitwise(monkeypatch, m, shards, period, rb, side_edge):
-    """The software-pipelined k_poisson_xr_pipe_f64 (CGX_XR_PIPE /
-    CGX_XR_PIPE_CATCHUP = rows per step for the no-x / catch-up kernels, the
-    catch-up's the default at 4; full 512-column strips, 8-row items) does
-    k_poisson_xr_f64's arithmetic row by row and item by item in the same order
-    on the same grid: x and the loop counts are bit for bit the plain kernel's
-    after every way a solve can end, with x every iteration and every third.
-    Side points loaded by the outer waves only (CGX_PIPE_SIDE_EDGE=1, the
-    default) or by every wave: the same values either way."""
+def test_poisson_xr_pipelined_kernel_is_bitwise(monkeypatch, m, shards, period):
+    """The software-pipelined x catch-up (k_poisson_xr_pipe_f64, the default
+    for full 512-column strips and 8-row items) does k_poisson_xr_f64's
+    arithmetic row by row and item by item in the same order on the same
+    grid: x and the loop counts are bit for bit the plain kernel's
+    (CGX_POISSON_PLAN=pipe=0) after every way a solve can end, with x every
+    other and every third iteration."""
     monkeypatch.setenv("CGX_POISSON_FUSED", "1")
-    monkeypatch.setenv("CGX_PIPE_SIDE_EDGE", side_edge)
-    monkeypatch.setenv("CGX_XR_PIPE", rb)
-    monkeypatch.setenv("CGX_XR_PIPE_CATCHUP", rb)
+    monkeypatch.delenv("CGX_POISSON_PLAN", raising=False)
     a = _poisson_x_runs(m, shards, period, monkeypatch)
-    monkeypatch.setenv("CGX_XR_PIPE", "0")
-    monkeypatch.setenv("CGX_XR_PIPE_CATCHUP", "0")
+    monkeypatch.setenv("CGX_POISSON_PLAN", "pipe=0")
     b = _poisson_x_runs(m, shards, period, monkeypatch)
     assert a.keys() == b.keys()
     for key in a:
@@ -948,32 +952,30 @@ def test_poisson_xr_pipelined_kernel_is_bitwise(monkeypatch, m, shards, period, 
         assert a[key][1:] == b[key][1:], key
 
 
-@pytest.mark.parametrize("side_edge", ["1", "0"])
-@pytest.mark.parametrize("rb", ["2", "4"])
-@pytest.mark.parametrize("m,shards", [(1024, None), (512, [0] * 4)])
-def test_poisson_p_pipelined_kernel(monkeypatch, m, shards, rb, side_edge):
-    """The software-pipelined k_poisson_p_pipe_f64 (CGX_P_PIPE) forms the same
-    p_k; it runs on its own occupancy's grid, so p.Ap adds in another order:
-    the solve agrees with the plain kernel's to fp64 rounding in the same loop
-    count (gated, halo overlap on 4 slabs with its interior / edge parts), and
-    x every iteration / every third iteration stay bit for bit equal under it."""
+@pytest.mark.parametrize("m,shards", [(96, [0] * 4), (130, [0, 0]), (1024, [0] * 8), (512, [0] * 2)])
+def test_poisson_local_pull_bitwise_equal_copies(monkeypatch, m, shards):
+    """One process, several slabs: k_poisson_p reads r's halo rows in place
+    from the neighbouring slabs (system-scope loads after the r.r combine's
+    events), and the two scalar combines are summed by the kernels that use
+    them (p.Ap by k_poisson_xr, r.r by the next k_poisson_p; a combine kernel
+    only when the host reads r.r).  Against round 3's per-neighbour peer
+    copies with combine kernels (CGX_LOCAL_XCHG=copy) and the pull with
+    combine kernels (CGX_LOCAL_FUSE=0): x and the loop counts bit for bit,
+    gated, host-checked, fixed counts and pieces, x every third iteration."""
     monkeypatch.setenv("CGX_POISSON_FUSED", "1")
-    monkeypatch.setenv("CGX_PIPE_SIDE_EDGE", side_edge)
     res = {}
-    for pipe in ("0", rb):
-        monkeypatch.setenv("CGX_P_PIPE", pipe)
-        with cg.Solver(None, poisson_m=m, devices=shards) as s:
-            s.fill(1.0, 0.0)
-            x, st = s.solve(None, eps=1e-8)
-            res[pipe] = (x, st.iterations, st.converged)
-    (x0, it0, c0), (x1, it1, c1) = res["0"], res[rb]
-    assert c0 and c1 and abs(it0 - it1) <= 1 and rel(x1, x0) <= 1e-9
-    monkeypatch.setenv("CGX_P_PIPE", rb)
-    a = _poisson_x_runs(m, shards, "3", monkeypatch)
-    b = _poisson_x_runs(m, shards, "0", monkeypatch)
-    for key in a:
-        assert np.array_equal(a[key][0], b[key][0]), key
-        assert a[key][1:] == b[key][1:], key
+    for form in ("pull", "nofuse", "copy"):
+        monkeypatch.setenv("CGX_LOCAL_XCHG", "copy" if form == "copy" else "kernel")
+        monkeypatch.setenv("CGX_LOCAL_FUSE", "0" if form == "nofuse" else "1")
+        res[form] = _poisson_x_runs(m, shards, "3", monkeypatch)
+    for form in ("pull", "nofuse"):
+        assert res[form].keys() == res["copy"].keys()
+        for key in res["copy"]:
+            assert np.array_equal(res[form][key][0], res["copy"][key][0]), (form, key)
+            assert res[form][key][1:] == res["copy"][key][1:], (form, key)
+    n = m * m
+    xo, so = oracle.cg_poisson_f64(m, np.ones(n), np.zeros(n), eps=1e-10)
+    assert res["pull"]["solve1"][1] == so.iterations and rel(res["pull"]["solve1"][0], xo) <= 1e-9
 
 
 def test_poisson_fused_in_pieces_and_iteration_cap():
@@ -1043,22 +1045,40 @@ def test_poisson_rejects_bad_use():
 
 
 @pytest.mark.parametrize("P", [2, 4, 8])
-def test_overlapped_exchange_matches(P):
-    """Own-column-block matVec overlapped with the p exchange (default when
-    blocks are 128-aligned) == the sequential exchange, to fp64 rounding of
-    the two-piece row sums; both == oracle."""
+def test_overlap_choice_is_bitwise_neutral(monkeypatch, P):
+    """Aligned row blocks: the context measures the allgather and the cost of
+    splitting the matVec at creation and picks the overlapped form (own
+    column block beside the exchange, then the rest) or the plain one (the
+    exchange, then one launch).  The one launch sums the own block and the
+    rest apart and adds them, as the two launches do: x is the same bits in
+    every form (forced on, forced off by env or flag, measured), gated and
+    fixed-count, from x0 = 0 and from a nonzero x0; all == oracle."""
     n = 2048
     A, b = oracle.spd_hash(n, seed=11)
+    x0 = np.full(n, 0.125)
     res = {}
-    for flags in (cg.CGX_F64, cg.CGX_F64 | cg.CGX_NO_OVERLAP):
-        with cg.Solver(n, flags=flags, devices=[0] * P) as s:
-            assert bool(s.info.flags & cg.CGX_OVERLAP_ACTIVE) == (not flags & cg.CGX_NO_OVERLAP)
+    for form, env, flags in (("on", "1", 0), ("off", "0", 0), ("flag", None, cg.CGX_NO_OVERLAP),
+                             ("measured", None, 0)):
+        if env is None:
+            monkeypatch.delenv("CGX_OVERLAP", raising=False)
+        else:
+            monkeypatch.setenv("CGX_OVERLAP", env)
+        with cg.Solver(n, flags=cg.CGX_F64 | flags, devices=[0] * P) as s:
+            info = s.overlap_info()
+            on = bool(s.info.flags & cg.CGX_OVERLAP_ACTIVE)
+            assert info["on"] == on and info["one_launch_us"] > 0 and info["allgather_us"] > 0
+            assert info["decided_by"] == {"on": "forced_on", "off": "off", "flag": "off"}.get(form, "measured")
+            assert on == {"on": True, "off": False, "flag": False}.get(form, info["allgather_us"] >
+                                                                        info["split_cost_us"])
             s.set_system(A, b)
-            res[flags] = s.solve(None, eps=1e-10)
+            xg, st = s.solve(None, eps=1e-10)
+            xf, _ = s.solve(x0, eps=-1.0, max_iter=9)
+        res[form] = (xg, st.iterations, xf)
     xo, so = oracle.cg_f64(A, b, np.zeros(n), eps=1e-10)
-    for x, st in res.values():
-        assert st.iterations == so.iterations
-        assert rel(x, xo) <= TOL
+    ref = res["on"]
+    assert ref[1] == so.iterations and rel(ref[0], xo) <= TOL
+    for form, r in res.items():
+        assert r[1] == ref[1] and np.array_equal(r[0], ref[0]) and np.array_equal(r[2], ref[2]), form
 
 
 @pytest.mark.parametrize("P", [2, 4])
