@@ -1,6 +1,6 @@
 #!/bin/bash
 # Interleaved A/B of one environment knob on a bench workload (GPU box, repo root):
-#   VAR=CGX_STENCIL_REVERSE VALUES="0 1" ROUNDS=3 ARGS="--workload poisson" bash tools/ab_env.sh
+#   VAR=CGX_POISSON_PLAN VALUES="reverse=0 reverse=1" ROUNDS=3 ARGS="--workload poisson" bash tools/ab_env.sh
 set -euo pipefail
 for round in $(seq 1 ${ROUNDS:-3}); do
   for v in ${VALUES:-0 1}; do

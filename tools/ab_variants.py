@@ -3,8 +3,7 @@ repo root): every round runs each variant once, in a separate bench.py
 process, so a slow box or process-to-process drift hits every variant alike.
 
   python tools/ab_variants.py --rounds 2 --args "--workload poisson --steps 300" \
-      --variant default= --variant grid1024=CGX_STENCIL_BLOCKS=1024 \
-      --variant grid1024_q=CGX_STENCIL_BLOCKS=1024,CGX_XR3_QUARTER=1 > out.jsonl
+      --variant default= --variant grid1024=CGX_POISSON_PLAN=blocks=1024 > out.jsonl
 
 A variant is NAME=VAR=VALUE[,VAR=VALUE...] (NAME= alone: the defaults).
 Each line: the variant, the round, it/s, the roofline figure, relres."""

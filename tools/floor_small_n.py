@@ -13,27 +13,17 @@ import time
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import conjugate_gradient_amd as cg  # noqa: E402
 
-KNOBS = ("CGX_FUSE_P", "CGX_FOLD_P", "CGX_MV_R", "CGX_MV_U", "CGX_MV_SMALL", "CGX_SMALL_NT", "CGX_SMALL_U",
-         "CGX_SMALL_ANT", "CGX_MV_NT")
+KNOBS = ("CGX_FUSE_P", "CGX_FOLD_P", "CGX_MV_PLAN", "CGX_MV_SMALL", "CGX_SMALL_PLAN")
 # form -> the knobs it sets (the rest: the library's default)
 FORMS = {"three": {"CGX_FUSE_P": "0", "CGX_FOLD_P": "0"}, "two": {"CGX_FUSE_P": "1", "CGX_FOLD_P": "0"},
          "fold": {"CGX_FUSE_P": "1", "CGX_FOLD_P": "1"}, "default": {},
          # round 2's kernels: k_matvec_f64 reading p through L2 (no LDS staging)
          "two_l2p": {"CGX_FUSE_P": "1", "CGX_FOLD_P": "0", "CGX_MV_SMALL": "0"},
          "fold_l2p": {"CGX_FUSE_P": "1", "CGX_FOLD_P": "1", "CGX_MV_SMALL": "0"}}
-if os.environ.get("R03_FOLD_VARIANTS"):  # the plans tried for the fold (CGX_MV_* also sets the k = 0 matVec's)
-    FORMS.update({"fold_r2u4": {"CGX_FUSE_P": "1", "CGX_FOLD_P": "1", "CGX_MV_R": "2", "CGX_MV_U": "4",
-                                "CGX_MV_SMALL": "0"},
-                  "fold_r2u8": {"CGX_FUSE_P": "1", "CGX_FOLD_P": "1", "CGX_MV_R": "2", "CGX_MV_U": "8",
-                                "CGX_MV_SMALL": "0"}})
-if os.environ.get("R03_SMALL_VARIANTS"):  # k_matvec_small_f64's block size and chunks per step
+if os.environ.get("SMALL_VARIANTS"):  # k_matvec_small_f64's block size and chunks per step
     for nt in ("512", "1024"):
         for u in ("4", "8"):
-            FORMS[f"fold_nt{nt}u{u}"] = {"CGX_FUSE_P": "1", "CGX_FOLD_P": "1", "CGX_SMALL_NT": nt, "CGX_SMALL_U": u}
-if os.environ.get("R03_SMALL_MALL"):  # default-policy A loads: A (<= 537 MB) may stay in the 256 MB MALL
-    FORMS["fold_mall"] = {"CGX_FUSE_P": "1", "CGX_FOLD_P": "1", "CGX_SMALL_ANT": "0"}
-    FORMS["fold_nt"] = {"CGX_FUSE_P": "1", "CGX_FOLD_P": "1", "CGX_SMALL_ANT": "1", "CGX_MV_NT": "8"}
-    FORMS["two_nt"] = {"CGX_FUSE_P": "1", "CGX_FOLD_P": "0", "CGX_SMALL_ANT": "1", "CGX_MV_NT": "8"}
+            FORMS[f"fold_nt{nt}u{u}"] = {"CGX_FUSE_P": "1", "CGX_FOLD_P": "1", "CGX_SMALL_PLAN": f"threads={nt},U={u}"}
 
 
 def run(n, form, steps=400, warm=50):

@@ -16,9 +16,9 @@ import conjugate_gradient_amd as cg  # noqa: E402
 
 
 def main():
-    for env in ({"CGX_POISSON_FUSED": "1", "CGX_STENCIL_REVERSE": "1"},
-                {"CGX_POISSON_FUSED": "1", "CGX_STENCIL_REVERSE": "0"},
-                {"CGX_POISSON_FUSED": "0", "CGX_STENCIL_REVERSE": "1"}):
+    for env in ({"CGX_POISSON_FUSED": "1", "CGX_POISSON_PLAN": "reverse=1"},
+                {"CGX_POISSON_FUSED": "1", "CGX_POISSON_PLAN": "reverse=0"},
+                {"CGX_POISSON_FUSED": "0", "CGX_POISSON_PLAN": "reverse=1"}):
         os.environ.update(env)
         for m in (256, 1024):
             with cg.Solver(None, poisson_m=m) as s:

@@ -1,0 +1,178 @@
+"""The 1 -> 2/4/8 GPU prediction for configs[2] (N=65536, row blocks), made
+from what one GPU can measure, so that a SCALE line's per-phase breakdown
+(bench.py `phases_us`) can be read against it phase by phase.
+
+Measured inputs (committed under profiles/):
+  - the 1-GPU iteration: the driver's N=1 bench line (BENCH_r04.json at the
+    repo root: ms_per_step), or profiles/r05_scale_inputs.json;
+  - one rank's kernels at G ranks without the collectives, in both forms the
+    context chooses between at creation (cgx_exchange.hip choose_overlap):
+    split (own-column-block launch beside the allgather, then the rest) and
+    one (the allgather, then one launch of the same bits) -- the wall time per
+    iteration from tools/microbench/rank_iteration (profiles/r05_rank_iteration.jsonl)
+    and, where present, a rocprofv3 kernel trace of it
+    (profiles/r05_rank_kernel_trace_g{G}.csv) for the per-kernel medians.
+Stated assumptions (not measurable on a one-GPU box, where RCCL runs over
+loopback sockets): the latency of RCCL's 8-byte allreduce and of the p
+allgather over xGMI, as a low / mid / high range.
+
+Per G and case the model predicts both forms and the one the library would
+pick (overlap only when the allgather takes longer than the split costs),
+which is the form a SCALE line reports in its "overlap" key.
+
+  python tools/scale_model.py > profiles/r05_scale_model.json
+  python tools/scale_model.py --compare LINE.json [...]
+      (bench.py lines of an N>1 run, e.g. from the driver's SCALE record:
+      the form that ran, each phase's max over ranks against the model's mid
+      prediction for that form, and the phase furthest above it)
+"""
+import csv
+import json
+import os
+import statistics
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PROF = os.environ.get("SCALE_PROF_DIR", os.path.join(ROOT, "profiles"))
+TAG = os.environ.get("SCALE_TAG", "r05")
+N = 65536
+
+# RCCL small-message collectives over xGMI on one 8-GPU MI300-class node (LL
+# protocol): an 8-byte allreduce in the tens of microseconds at most; the
+# allgather of 8*N/G bytes per rank adds its transfer at ~100 GB/s effective
+# per peer link (MI355X: 7 xGMI links per GPU, ~153 GB/s each, per the project
+# brief).  These are assumptions, labelled as such in the output.
+ALLREDUCE_US = {"low": 6.0, "mid": 12.0, "high": 25.0}
+GATHER_LAT_US = {"low": 6.0, "mid": 12.0, "high": 25.0}
+GATHER_GBPS_PER_LINK = 100.0
+
+
+def one_gpu_anchor():
+    rec = os.path.join(ROOT, "BENCH_r04.json")
+    if os.path.exists(rec):
+        d = json.load(open(rec))["parsed"]
+        return d["ms_per_step"], f"BENCH_r04.json: the driver's round-4 N=1 bench line ({d['value']:.2f} it/s)"
+    d = json.load(open(os.path.join(PROF, f"{TAG}_scale_inputs.json")))
+    return d["one_gpu_ms_per_step"], d["source"]
+
+
+def kernel_spans(trace_csv):
+    """Per-kernel medians (us) of rank_iteration's traced iterations, by form:
+    split = [matVec own, matVec rest, update_r, update_xp], one = [matVec
+    (rotated, ROT), update_r, update_xp], natural = [matVec, update_r, update_xp]."""
+    rows = list(csv.DictReader(open(trace_csv)))
+    ks = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows)
+    ks = [k for k in ks if "k_matvec_f64" in k[2] or "k_update_r_f64" in k[2] or "k_update_xp_f64" in k[2]]
+    dur = lambda k: (k[1] - k[0]) / 1e3  # noqa: E731
+    rot = lambda k: "k_matvec_f64" in k[2] and k[2].split("(")[0].replace(" ", "").endswith("true,true>")  # noqa: E731
+    mv = lambda k: "k_matvec_f64" in k[2]  # noqa: E731
+    out = {"split": {"matvec_own": [], "matvec": [], "update_r": [], "update_xp": []},
+           "one": {"matvec": [], "update_r": [], "update_xp": []},
+           "natural": {"matvec": [], "update_r": [], "update_xp": []}}
+    i = 0
+    while i < len(ks) - 2:
+        a, b, c = ks[i], ks[i + 1], ks[i + 2]
+        if mv(a) and not rot(a) and mv(b) and i + 3 < len(ks) and "update_r" in c[2]:
+            for key, k in zip(("matvec_own", "matvec", "update_r", "update_xp"), ks[i:i + 4]):
+                out["split"][key].append(dur(k))
+            i += 4
+        elif mv(a) and "update_r" in b[2] and "update_xp" in c[2]:
+            form = "one" if rot(a) else "natural"
+            for key, k in zip(("matvec", "update_r", "update_xp"), (a, b, c)):
+                out[form][key].append(dur(k))
+            i += 3
+        else:
+            i += 1
+    return {f: {k: round(statistics.median(v), 2) for k, v in d.items() if v} for f, d in out.items()}
+
+
+def main():
+    ms1, src1 = one_gpu_anchor()
+    walls = {}
+    for line in open(os.path.join(PROF, f"{TAG}_rank_iteration.jsonl")):
+        d = json.loads(line)
+        w = d["us_per_iteration_without_collectives"]
+        if d.get("rank", d["ranks"] // 2) == d["ranks"] // 2:  # a middle rank: its rest wraps (the slowest)
+            walls.setdefault(d["ranks"], []).append(w)
+    out = {
+        "what": "configs[2] (N=65536 dense fp64, row blocks) at G GPUs: one rank's measured kernels in both "
+                "exchange forms plus assumed collective latencies -> predicted iteration, it/s and speed-up over "
+                "the measured 1-GPU step, and the form the library picks (overlap only when the allgather is "
+                "longer than the split costs); the phase keys are bench.py phases_us's",
+        "one_gpu": {"ms_per_step": ms1, "it_per_s": 1e3 / ms1, "source": src1},
+        "assumptions": {
+            "allreduce_8B_us": ALLREDUCE_US,
+            "allgather_latency_us": GATHER_LAT_US,
+            "allgather_GBps_per_peer_link": GATHER_GBPS_PER_LINK,
+            "source": "not measurable on a one-GPU box (RCCL runs over loopback sockets there); RCCL's LL-protocol "
+                      "small-message latency on one xGMI-connected node is assumed in the 5-25 us range (not from a "
+                      "document available here); the MI355X has 7 xGMI links per GPU at ~153 GB/s each (the "
+                      "project brief), taken at 100 GB/s effective per peer",
+        },
+        "per_G": {},
+    }
+    for G in (2, 4, 8):
+        if G not in walls:
+            continue
+        split = statistics.median(w["split"] for w in walls[G])
+        one = statistics.median(w["one"] for w in walls[G])
+        tr = os.path.join(PROF, f"{TAG}_rank_kernel_trace_g{G}.csv")
+        k = kernel_spans(tr) if os.path.exists(tr) else None
+        own = (k["split"]["matvec_own"] if k else split * 0.13)
+        slice_bytes = 8 * N // G
+        entry = {"rows_per_rank": N // G, "measured": {
+            "us_per_iteration_without_collectives": {"split": round(split, 2), "one": round(one, 2),
+                                                     "rounds": len(walls[G])},
+            "split_cost_us": round(split - one, 2),
+            "kernel_medians_us": k,
+            "matvec_TBps_one_launch": round((8 * (N // G) * N + 8 * N + 8 * (N // G))
+                                            / (k["one"]["matvec"] * 1e-6) / 1e12, 3) if k else None}}
+        pred = {}
+        for case in ("low", "mid", "high"):
+            gather = GATHER_LAT_US[case] + slice_bytes / (GATHER_GBPS_PER_LINK * 1e3)  # per peer, peers in parallel
+            ar = ALLREDUCE_US[case]
+            forms = {"overlap": split + max(0.0, gather - own) + 2 * ar, "plain": one + gather + 2 * ar}
+            chosen = "overlap" if gather > split - one else "plain"
+            it_us = forms[chosen]
+            pred[case] = {
+                "allgather_us": round(gather, 2),
+                "iteration_us": {f: round(v, 1) for f, v in forms.items()},
+                "chosen": chosen,
+                "phases_us": ({"matvec_own": round(own, 2), "gather_exposed": round(max(0.0, gather - own), 2)}
+                              if chosen == "overlap" else {"matvec_own": 0.0, "gather_exposed": round(gather, 2)})
+                | {"combine_pap": ar, "combine_rr": ar},
+                "it_per_s": round(1e6 / it_us, 1),
+                "speedup_vs_1gpu": round(ms1 * 1e3 / it_us, 2),
+                "efficiency": round(ms1 * 1e3 / it_us / G, 3)}
+        entry["predicted"] = pred
+        out["per_G"][str(G)] = entry
+    json.dump(out, sys.stdout, indent=1)
+    print()
+
+
+def compare(paths):
+    model = json.load(open(os.path.join(PROF, f"{TAG}_scale_model.json")))
+    for path in paths:
+        text = open(path).read()
+        line = json.loads([ln for ln in text.splitlines() if ln.strip().startswith("{")][-1])
+        G = str(line["n_gpus"])
+        pred = model["per_G"].get(G, {}).get("predicted", {}).get("mid")
+        meas = line.get("phases_us", {}).get("max_over_ranks")
+        if not pred or not meas:
+            print(json.dumps({"file": path, "n_gpus": G, "error": "no model entry or no phases_us"}))
+            continue
+        ran = "overlap" if line.get("overlap", {}).get("on") else "plain"
+        delta = {ph: round(meas.get(ph, 0.0) - v, 2) for ph, v in pred["phases_us"].items()}
+        print(json.dumps({"file": path, "n_gpus": G, "it_per_s": line["value"], "form_ran": ran,
+                          "form_model_picks": pred["chosen"], "overlap_measured": line.get("overlap"),
+                          "predicted_iteration_us": pred["iteration_us"][ran],
+                          "measured_iteration_us": meas.get("iteration"), "measured_phases_us": meas,
+                          "predicted_phases_us": pred["phases_us"], "delta_us": delta,
+                          "furthest_above_model": max(delta, key=delta.get)}))
+
+
+if __name__ == "__main__":
+    if len(sys.argv) > 2 and sys.argv[1] == "--compare":
+        compare(sys.argv[2:])
+    else:
+        main()

@@ -1,7 +1,7 @@
 #!/usr/bin/env python3
 """matVec plan sweep for a row block of given height (e.g. the 8192 x 65536
 block one GPU owns at N=65536 over 8 GPUs), through the kernel-level entry
-point cgx_matvec with the plan taken from CGX_MV_* environment variables.
+point cgx_matvec with the plan taken from CGX_MV_PLAN.
 Wall-clock timing over `--reps` back-to-back launches (launch overhead is
 included: a few us against ~0.6 ms), interleaved rounds in one process.
 
@@ -41,11 +41,7 @@ def main():
     L = cg.lib()
     for _ in range(args.rounds):
         for c in configs:
-            os.environ["CGX_MV_R"], os.environ["CGX_MV_U"], os.environ["CGX_MV_NT"] = map(str, c[:3])
-            if c[3] > 0:
-                os.environ["CGX_MV_BLOCKS_PER_CU"] = str(c[3])
-            else:
-                os.environ.pop("CGX_MV_BLOCKS_PER_CU", None)
+            os.environ["CGX_MV_PLAN"] = f"R={c[0]},U={c[1]},nt={c[2]}" + (f",bpc={c[3]}" if c[3] > 0 else "")
             cg.matVec(A, v, out, rows, cols)
             L.cgx_dev_synchronize()
             t0 = time.perf_counter()

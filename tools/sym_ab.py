@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""In-process A/B of the CGX_SYMMETRIC matVec (load policy CGX_SYM_NT, read
+"""In-process A/B of the CGX_SYMMETRIC matVec (load policy CGX_SYM_PLAN nt=, read
 per launch) against the row-major kernel on the same
 system: interleaved rounds of fixed-count iterations, matVec time from HIP
 events (CGX_TIMING), medians per variant.
@@ -14,7 +14,7 @@ import sys
 sys.path.insert(0, os.path.dirname(os.path.dirname(os.path.abspath(__file__))))
 import conjugate_gradient_amd as cg  # noqa: E402
 
-VARIANTS = {"sym_nt": {"CGX_SYM_NT": "1"}, "sym_default_policy": {"CGX_SYM_NT": "0"}}
+VARIANTS = {"sym_nt": {"CGX_SYM_PLAN": "nt=1"}, "sym_default_policy": {"CGX_SYM_PLAN": "nt=0"}}
 
 
 def main():
