@@ -58,7 +58,7 @@ CGX_XDEFER3_ACTIVE = 0x200000
 
 # cgx_phase_times indices (include/cgx.h), in the order the phases tile an iteration
 PHASE_NAMES = ("matvec_own", "gather_exposed", "matvec", "combine_pap", "update_r", "combine_rr", "update_xp",
-               "gap", "iteration")
+               "gap", "iteration", "matvec_busy")
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
 LIB_PATH = os.path.join(_HERE, "lib", "libcgx.so")
@@ -96,8 +96,8 @@ class Info(ctypes.Structure):
 
 
 class PhaseTimes(ctypes.Structure):
-    _fields_ = [("samples", ctypes.c_int64 * 9), ("median_us", ctypes.c_double * 9),
-                ("mean_us", ctypes.c_double * 9)]
+    _fields_ = [("samples", ctypes.c_int64 * 10), ("median_us", ctypes.c_double * 10),
+                ("mean_us", ctypes.c_double * 10)]
 
 
 class CommInfo(ctypes.Structure):

@@ -400,6 +400,7 @@ int exchange_allgather(cgx_ctx *c, bool from_x);
 int exchange_scalar(cgx_ctx *c, int lslot, int gslot);
 PeerSum peer_sum(const cgx_ctx *c, const Shard &d, int lslot, int gslot);
 int overlapped_matvec(cgx_ctx *c, int dot_slot, bool gated);
+int overlap_matvecs(cgx_ctx *c, Shard &d, int dot_slot, bool gated, bool timed = true);
 int choose_overlap(cgx_ctx *c);
 int exchange_halo_async(cgx_ctx *c);
 int settle_halo(cgx_ctx *c);

@@ -107,6 +107,25 @@ int phase_resolve(cgx_ctx *c) {
             c->ts_prev_start = c->ts_prev_end = 0;
             continue;
         }
+        {  // the matVec kernels' busy time: the union of their spans (the overlap's own block and rest)
+            std::pair<int64_t, int64_t> iv[2];
+            int niv = 0;
+            for (int k : {TK_OWN, TK_MV})
+                if (st[k] != 0 && en[k] != 0) iv[niv++] = {st[k], en[k]};
+            std::sort(iv, iv + niv);
+            int64_t busy = 0, cs = 0, ce = 0;
+            for (int j = 0; j < niv; ++j) {
+                if (j == 0 || iv[j].first > ce) {
+                    busy += ce - cs;
+                    cs = iv[j].first;
+                    ce = iv[j].second;
+                } else {
+                    ce = std::max(ce, iv[j].second);
+                }
+            }
+            busy += ce - cs;
+            if (niv) add(CGX_PH_MATVEC_BUSY, 0, busy);
+        }
         if (c->ts_prev_end) {
             // before the first kernel: p's allgather when it is not overlapped
             // (a non-overlapped exchange between iterations), else the launch gap
@@ -433,10 +452,39 @@ int exchange_scalar(cgx_ctx *c, int lslot, int gslot) {
 // Where a kernel writes its (partial) scalar: the global slot directly when
 // there is nothing to combine, else the shard-local slot.
 
-// Overlapped exchange + matVec: p is allgathered on each shard's comm
-// stream while the compute stream multiplies the shard's own column block
-// (its own p is already local); the rest of the columns follow once the
-// gather has landed, accumulating into Ap with the fused p.Ap partial.
+// The overlapped matVec of row block d once p's exchange is enqueued on
+// d.cstream (the RCCL allgather, or the pull kernel): the own column block on
+// the compute stream (its p is local) while the exchange runs, then, once p
+// has landed, the rest of the columns, accumulating, with the fused p.Ap.
+// (Round 5 also ran the rest launch on the exchange stream beside the own
+// block, with an add kernel after both: 644.9 against 638.7 us per iteration
+// at 8 row blocks of N = 65536 -- the matVec's one wave per SIMD leaves no room
+// for a second kernel's waves, so the two did not overlap, and the add cost
+// its launch; profiles/r05_rank_iteration.jsonl.  Removed.)
+int overlap_matvecs(cgx_ctx *c, Shard &d, int dot_slot, bool gated, bool timed) {
+    const double *A = reinterpret_cast<const double *>(d.A);
+    const double *v = reinterpret_cast<const double *>(d.pfull);
+    double *Ap = reinterpret_cast<double *>(d.Ap);
+    HIPT(hipEventRecord(d.ev_gathered, d.cstream));
+    const bool timing = timed && (c->flags & CGX_TIMING) && (&d == &c->sh[0]);
+    if (timing && d.ev_used >= kEvPairs) TRY(timing_resolve(c));
+    if (timing) HIPT(hipEventRecord(d.ev_t[2 * d.ev_used], d.stream));
+    HIPT(matvec_f64_cols(d.plan, A, c->lda, d.nloc, c->lda, d.row0, d.nloc, false, v, Ap, nullptr, nullptr, d.ws,
+                         d.stream, gate_of(d, gated), ts_of(c, d, TK_OWN)));
+    HIPT(hipStreamWaitEvent(d.stream, d.ev_gathered, 0));
+    HIPT(matvec_f64_cols(d.plan, A, c->lda, d.nloc, c->lda, (d.row0 + d.nloc) % c->lda, c->lda - d.nloc, true, v, Ap,
+                         reinterpret_cast<const double *>(d.pown), reinterpret_cast<double *>(slot(d, dot_slot)),
+                         d.ws, d.stream, gate_of(d, gated), ts_of(c, d, TK_MV)));
+    if (timing) {
+        HIPT(hipEventRecord(d.ev_t[2 * d.ev_used + 1], d.stream));
+        d.ev_used++;
+    }
+    return CGX_OK;
+}
+
+// Overlapped exchange + matVec (parallel_cg.c:290-293): p is allgathered on
+// each shard's exchange stream while the compute stream multiplies the
+// shard's own column block; overlap_matvecs does the rest.
 int overlapped_matvec(cgx_ctx *c, int dot_slot, bool gated) {
     const size_t es = (size_t)c->es;
     for (auto &s : c->sh) {
@@ -448,7 +496,6 @@ int overlapped_matvec(cgx_ctx *c, int dot_slot, bool gated) {
         HIPT(hipStreamWaitEvent(s.cstream, s.ev_pready, 0));
         NCCLC(c, ncclAllGather(s.pown, s.pfull, (size_t)s.nloc, ncclDouble, s.comm, s.cstream),
               "ncclAllGather(p), overlapped");
-        HIPT(hipEventRecord(s.ev_gathered, s.cstream));
     } else {
         const PeerTable src = peer_table(c, &Shard::pown, 0);
         for (auto &d : c->sh) {
@@ -460,28 +507,11 @@ int overlapped_matvec(cgx_ctx *c, int dot_slot, bool gated) {
                 for (auto &s : c->sh)
                     if (&s != &d)
                         HIPT(hipMemcpyPeerAsync(d.pfull + s.row0 * es, d.dev, s.pown, s.dev, s.nloc * es, d.cstream));
-            HIPT(hipEventRecord(d.ev_gathered, d.cstream));
         }
     }
     for (auto &s : c->sh) {
         TRY(set_dev(s));
-        const bool timing = (c->flags & CGX_TIMING) && (&s == &c->sh[0]);
-        if (timing && s.ev_used >= kEvPairs) TRY(timing_resolve(c));
-        if (timing) HIPT(hipEventRecord(s.ev_t[2 * s.ev_used], s.stream));
-        const double *A = reinterpret_cast<const double *>(s.A);
-        const double *v = reinterpret_cast<const double *>(s.pfull);
-        double *Ap = reinterpret_cast<double *>(s.Ap);
-        HIPT(matvec_f64_cols(s.plan, A, c->lda, s.nloc, c->lda, s.row0, s.nloc, false, v, Ap, nullptr, nullptr,
-                             s.ws, s.stream, gate_of(s, gated), ts_of(c, s, TK_OWN)));
-        HIPT(hipStreamWaitEvent(s.stream, s.ev_gathered, 0));
-        HIPT(matvec_f64_cols(s.plan, A, c->lda, s.nloc, c->lda, (s.row0 + s.nloc) % c->lda, c->lda - s.nloc, true,
-                             v, Ap, reinterpret_cast<const double *>(s.pown),
-                             reinterpret_cast<double *>(slot(s, dot_slot)), s.ws, s.stream, gate_of(s, gated),
-                             ts_of(c, s, TK_MV)));
-        if (timing) {
-            HIPT(hipEventRecord(s.ev_t[2 * s.ev_used + 1], s.stream));
-            s.ev_used++;
-        }
+        TRY(overlap_matvecs(c, s, dot_slot, gated));
     }
     return CGX_OK;
 }
@@ -489,13 +519,12 @@ int overlapped_matvec(cgx_ctx *c, int dot_slot, bool gated) {
 // ---- overlapped or plain: the choice at creation ------------------------------
 // The two forms of an aligned multi-shard iteration (c->rot) give the same
 // bits, so the choice is speed only.  The overlap hides the allgather behind
-// the own-block launch but pays for splitting the matVec in two (a second
-// launch's fill and drain: about 32 us per iteration at 8 row blocks of
-// N = 65536, 8 us at 2, profiles/r04_rank_kernel_trace_g*.csv); the plain form
-// exposes the allgather.  So the context times both matVec forms on each of its
-// row blocks (zeros at this point: the same bytes move) and the allgather of p
-// itself, and overlaps only when the allgather takes longer than the split
-// costs.  Rank mode: every rank measures and the maxima over ranks decide, so
+// the own-block launch but pays for splitting the matVec in two launches (a
+// second fill and drain: 15 / 20 / 23 us per iteration at 8 / 4 / 2 row blocks
+// of N = 65536, profiles/r05_rank_iteration.jsonl); the plain form exposes
+// the allgather.  So the context times both matVec forms on each of its row blocks
+// (zeros at this point: the same bytes move) and the allgather of p itself,
+// and overlaps only when the allgather takes longer than the split costs.  Rank mode: every rank measures and the maxima over ranks decide, so
 // the ranks agree (they would pair their collectives either way).
 // CGX_NO_OVERLAP / CGX_OVERLAP=0 and CGX_OVERLAP=1 / force override the
 // decision (the numbers are still measured and reported).
@@ -514,10 +543,8 @@ static int measure_split(cgx_ctx *c) {
         for (int rep = 0; rep <= kReps && rc == CGX_OK; ++rep) {  // rep 0 warms up
             rc = [&]() -> int {
                 HIPT(hipEventRecord(ev[0], s.stream));
-                HIPT(matvec_f64_cols(s.plan, A, c->lda, s.nloc, c->lda, s.row0, s.nloc, false, v, Ap, nullptr,
-                                     nullptr, s.ws, s.stream));
-                HIPT(matvec_f64_cols(s.plan, A, c->lda, s.nloc, c->lda, (s.row0 + s.nloc) % c->lda, c->lda - s.nloc,
-                                     true, v, Ap, pown, dot, s.ws, s.stream));
+                HIPT(hipStreamWaitEvent(s.cstream, ev[0], 0));  // the overlapped form with nothing to exchange
+                TRY(overlap_matvecs(c, s, S_TR, false, false));
                 HIPT(hipEventRecord(ev[1], s.stream));
                 HIPT(matvec_f64_cols(s.plan, A, c->lda, s.nloc, c->lda, s.row0, c->lda, false, v, Ap, pown, dot, s.ws,
                                      s.stream, nullptr, nullptr, s.nloc));

@@ -98,13 +98,6 @@ hipError_t matvec_f64_cols(const MatvecPlan &pl, const double *A, int64_t lda, i
                            int64_t col_first, int64_t col_count, bool accumulate, const double *v, double *out,
                            const double *pown, double *dot_out, const RedWs &ws, hipStream_t s,
                            const int64_t *gate = nullptr, int64_t *ts = nullptr, int64_t col_seg = 0);
-// out[i] = own[i] + rest[i] (+ *dot_out = pown . out, in the order the plan's
-// matVec fuses it): the own-block and the rest launches' row sums (both with
-// accumulate = false) added as the accumulating rest launch adds them, so the
-// two may run on two streams at once with the bits of the sequential form.
-hipError_t matvec_add_f64(const MatvecPlan &pl, int64_t rows, const double *own, const double *rest, double *out,
-                          const double *pown, double *dot_out, const RedWs &ws, hipStream_t s,
-                          const int64_t *gate = nullptr, int64_t *ts = nullptr);
 // r = b - Ax; p = r (if p); *rr_out = r.r (if rr_out).  Ax == nullptr: Ax = 0
 // (r = b - 0.0).  clear2: two int64 the kernel zeroes (the convergence record).
 hipError_t residual_f64(int64_t n, const double *b, const double *Ax, double *r, double *p,

@@ -93,27 +93,21 @@ static int shard_iteration(LocalPool &P, Shard &d) {
     BAR();
     const PeerTable pown = peer_table(c, &Shard::pown, 0);
     const bool timing = (c->flags & CGX_TIMING) && d.index == 0;
-    if (timing && d.ev_used >= kEvPairs) TRY(timing_resolve(c));
-    if (timing) HIPT(hipEventRecord(d.ev_t[2 * d.ev_used], d.stream));
     if (c->overlap) {  // parallel_cg.c:290-293, overlapped (overlapped_matvec)
         for (auto &s : c->sh) HIPT(hipStreamWaitEvent(d.cstream, s.ev_pready, 0));
         HIPT(gather_slices(pown, S, d.index, d.nloc * (int64_t)es, d.pfull, d.cstream));
-        HIPT(hipEventRecord(d.ev_gathered, d.cstream));
-        HIPT(matvec_f64_cols(d.plan, CD(d.A), c->lda, d.nloc, c->lda, d.row0, d.nloc, false, CD(d.pfull), D(d.Ap),
-                             nullptr, nullptr, d.ws, d.stream, gate_of(d, gated), ts_of(c, d, TK_OWN)));
-        HIPT(hipStreamWaitEvent(d.stream, d.ev_gathered, 0));
-        HIPT(matvec_f64_cols(d.plan, CD(d.A), c->lda, d.nloc, c->lda, (d.row0 + d.nloc) % c->lda, c->lda - d.nloc,
-                             true, CD(d.pfull), D(d.Ap), CD(d.pown), D(slot(d, pl)), d.ws, d.stream,
-                             gate_of(d, gated), ts_of(c, d, TK_MV)));
+        TRY(overlap_matvecs(c, d, pl, gated));
     } else {  // MPI_Allgather(local_p -> p), then the matVec (parallel_cg.c:290-293)
+        if (timing && d.ev_used >= kEvPairs) TRY(timing_resolve(c));
+        if (timing) HIPT(hipEventRecord(d.ev_t[2 * d.ev_used], d.stream));
         for (auto &s : c->sh)
             if (&s != &d) HIPT(hipStreamWaitEvent(d.stream, s.ev_pready, 0));
         HIPT(gather_slices(pown, S, d.index, d.nloc * (int64_t)es, d.pfull, d.stream));
         TRY(matvec_rows(c, d, d.plan, d.A, 0, d.nloc, d.pfull, true, pl, gated, ts_of(c, d, TK_MV)));
-    }
-    if (timing) {
-        HIPT(hipEventRecord(d.ev_t[2 * d.ev_used + 1], d.stream));
-        d.ev_used++;
+        if (timing) {
+            HIPT(hipEventRecord(d.ev_t[2 * d.ev_used + 1], d.stream));
+            d.ev_used++;
+        }
     }
     // 2. MPI_Allreduce(p.Ap) (parallel_cg.c:294): summed by k_update_r_f64 itself
     HIPT(hipEventRecord(d.ev_sync, d.stream));

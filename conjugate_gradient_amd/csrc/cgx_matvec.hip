@@ -280,38 +280,6 @@ __global__ __launch_bounds__(kNT) void k_matvec_f64(
     ts_end(ts);
 }
 
-// The overlapped exchange's two partial row sums added, out[i] = own[i] +
-// rest[i] (the accumulating rest launch's `out[i] + mine`, so the same bits),
-// with the fused p.Ap: rows are visited by the same (block, wave, lane) as in
-// k_matvec_f64<R> on the plan's grid, so every thread's partial and the
-// last-block reduction add in the same order as the matVec's own fused dot.
-// Lets the own-block and the rest launches run on two streams at once (the
-// rest after p's gather), each filling the other's ramp and tail.
-template <int R>
-__global__ __launch_bounds__(kNT) void k_matvec_add_f64(int64_t rows, const double *__restrict__ own,
-                                                        const double *__restrict__ rest, double *__restrict__ out,
-                                                        const double *__restrict__ pown, double *dot_out,
-                                                        double *partials, unsigned *ticket, const int64_t *gate,
-                                                        int64_t *ts) {
-    if (gate && *gate) return;
-    ts_start(ts);
-    const int lane = threadIdx.x & 63;
-    const int wid = threadIdx.x >> 6;
-    const int64_t ngroups = (rows + R - 1) / R;
-    const int64_t wstride = (int64_t)gridDim.x * (kNT / 64);
-    double dacc = 0.0;
-    for (int64_t g = (int64_t)blockIdx.x * (kNT / 64) + wid; g < ngroups; g += wstride) {
-        const int64_t i = g * R + lane;
-        if (lane < R && i < rows) {
-            const double mine = own[i] + rest[i];
-            out[i] = mine;
-            if (pown) dacc += pown[i] * mine;
-        }
-    }
-    if (pown) grid_sum_last_block(dacc, partials, ticket, dot_out);
-    ts_end(ts);
-}
-
 // ---------------------------------------------------------------------------
 // The matVec of a small system's two-launch iteration with the previous
 // iteration's p update folded in (one GPU, n <= kFusePMax): p_k is never
@@ -728,17 +696,6 @@ hipError_t matvec_f64_cols(const MatvecPlan &pl, const double *A, int64_t lda, i
     hipLaunchKernelGGL(fn, dim3(pl.blocks), dim3(kNT), 0, s, A, lda, rows, cols, cols, col_first >> 7,
                        col_count >> 7, rot ? col_seg >> 7 : int64_t(0), 0, accumulate ? 1 : 0, v, out, pown,
                        dot_out, ws.partials, ws.tickets + T_MATVEC, gate, ts);
-    return hipGetLastError();
-}
-
-hipError_t matvec_add_f64(const MatvecPlan &pl, int64_t rows, const double *own, const double *rest, double *out,
-                          const double *pown, double *dot_out, const RedWs &ws, hipStream_t s, const int64_t *gate,
-                          int64_t *ts) {
-    if (rows <= 0) return hipSuccess;
-    auto fn = pl.R == 1 ? k_matvec_add_f64<1> : pl.R == 2 ? k_matvec_add_f64<2> : pl.R == 8 ? k_matvec_add_f64<8>
-                                                                                              : k_matvec_add_f64<4>;
-    hipLaunchKernelGGL(fn, dim3(pl.blocks), dim3(kNT), 0, s, rows, own, rest, out, pown, dot_out, ws.partials,
-                       ws.tickets + T_MATVEC, gate, ts);
     return hipGetLastError();
 }
 

@@ -190,10 +190,14 @@ typedef struct {
  * + COMBINE_PAP + UPDATE_R + COMBINE_RR + UPDATE_XP + GAP = ITERATION. */
 #define CGX_PH_MATVEC_OWN     0 /* overlap: own-column-block matVec (p local)   */
 #define CGX_PH_GATHER_EXPOSED 1 /* the compute stream waiting for p's allgather
-                                   (overlap: after its own block; otherwise the
-                                   whole allgather, launch gap included)
+                                   (overlap: after its own block, until the rest
+                                   launch on the exchange stream -- which runs
+                                   right after the allgather, beside the own
+                                   block -- has finished; otherwise the whole
+                                   allgather, launch gap included)
                                    parallel_cg.c:290-291                        */
-#define CGX_PH_MATVEC         2 /* the (rest of the) matVec with p.Ap   :292-293 */
+#define CGX_PH_MATVEC         2 /* the matVec with p.Ap (overlap: the kernel
+                                   adding the two row sums, with p.Ap) :292-293 */
 #define CGX_PH_COMBINE_PAP    3 /* MPI_Allreduce(p.Ap) counterpart        :294   */
 #define CGX_PH_UPDATE_R       4 /* r -= alpha Ap, r.r                     :304-309 */
 #define CGX_PH_COMBINE_RR     5 /* MPI_Allreduce(r.r) counterpart         :313   */
@@ -201,7 +205,12 @@ typedef struct {
 #define CGX_PH_GAP            7 /* end of an iteration to the start of the next
                                    (host launch rate, lookahead waits)          */
 #define CGX_PH_ITERATION      8 /* start of an iteration to the start of the next */
-#define CGX_PH_COUNT          9
+#define CGX_PH_MATVEC_BUSY    9 /* not a tile: the time the iteration's matVec
+                                   kernels ran, the union of their spans (with
+                                   the overlap: the own-block launch, the rest
+                                   launch on the exchange stream, the add) --
+                                   the matVec's duration without the wait for p */
+#define CGX_PH_COUNT         10
 typedef struct {
     int64_t samples[CGX_PH_COUNT];
     double  median_us[CGX_PH_COUNT];

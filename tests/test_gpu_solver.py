@@ -513,6 +513,16 @@ def test_phase_times_tile_the_iteration(monkeypatch, kind):
     want = want[kind]
     for name in cg.PHASE_NAMES[:8]:
         assert ph[name]["samples"] == want.get(name, 0), (name, ph[name])
+    # matvec_busy (not a tile): the union of the matVec kernels' spans, one per iteration -- the matVec
+    # itself without the overlap; with it at least the own block, and within own + rest-wait + add
+    busy = ph["matvec_busy"]
+    assert busy["samples"] == S, busy
+    if kind == "shards_overlap":
+        assert ph["matvec_own"]["mean_us"] <= busy["mean_us"]
+        assert busy["mean_us"] <= 1.01 * (ph["matvec_own"]["mean_us"] + ph["gather_exposed"]["mean_us"]
+                                          + ph["matvec"]["mean_us"])
+    else:
+        assert abs(busy["mean_us"] - ph["matvec"]["mean_us"]) <= 0.01 * ph["matvec"]["mean_us"] + 0.05
         if name in want:
             assert ph[name]["mean_us"] > 0, (name, ph[name])
     tiles = sum(ph[k]["mean_us"] * ph[k]["samples"] for k in cg.PHASE_NAMES[:8]) / (steps - 1)

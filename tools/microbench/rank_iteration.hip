@@ -6,7 +6,7 @@
 //     rank's own column block (p is local; the allgather runs beside it on the
 //     comm stream), then, after the gather, the other columns, accumulating,
 //     with the fused p.Ap
-//   conc (round 5's overlap): the own-block launch on the compute stream and
+//   conc (measured, not adopted): the own-block launch on the compute stream and
 //     the rest launch on the comm stream right after the gather, at the same
 //     time; then k_matvec_add_f64 adds the two row sums with the fused p.Ap
 //   one (plain exchange): the gather, then one matVec over the whole row block
@@ -35,7 +35,7 @@
 #include <string>
 #include <vector>
 
-#include "cgx_kernels.h"
+#include "cgx_device.h"
 
 #define CK(x)                                                                       \
     do {                                                                            \
@@ -50,6 +50,31 @@
 __global__ void k_wait(int64_t ticks) {
     const int64_t t0 = (int64_t)__builtin_amdgcn_s_memrealtime();
     while ((int64_t)__builtin_amdgcn_s_memrealtime() - t0 < ticks) __builtin_amdgcn_s_sleep(2);
+}
+
+// conc's add (measured and not adopted, round 5): out[i] = own[i] + rest[i]
+// (the accumulating rest launch's `out[i] + mine`, the same bits) with the
+// fused p.Ap, rows visited by the same (block, wave, lane) as in
+// k_matvec_f64<R> on the plan's grid, so p.Ap adds in the matVec's order.
+template <int R>
+__global__ __launch_bounds__(cgx::kNT) void k_matvec_add_f64(int64_t rows, const double *__restrict__ own,
+                                                             const double *__restrict__ rest, double *__restrict__ out,
+                                                             const double *__restrict__ pown, double *dot_out,
+                                                             double *partials, unsigned *ticket) {
+    const int lane = threadIdx.x & 63;
+    const int wid = threadIdx.x >> 6;
+    const int64_t ngroups = (rows + R - 1) / R;
+    const int64_t wstride = (int64_t)gridDim.x * (cgx::kNT / 64);
+    double dacc = 0.0;
+    for (int64_t g = (int64_t)blockIdx.x * (cgx::kNT / 64) + wid; g < ngroups; g += wstride) {
+        const int64_t i = g * R + lane;
+        if (lane < R && i < rows) {
+            const double mine = own[i] + rest[i];
+            out[i] = mine;
+            dacc += pown[i] * mine;
+        }
+    }
+    cgx::grid_sum_last_block(dacc, partials, ticket, dot_out);
 }
 
 int main(int argc, char **argv) {
@@ -110,7 +135,9 @@ int main(int argc, char **argv) {
             CK(hipEventRecord(ev_rest, cs));
             CK(cgx::matvec_f64_cols(pl, A, n, rows, n, own0, rows, false, p, out, nullptr, nullptr, ws, s));
             CK(hipStreamWaitEvent(s, ev_rest, 0));
-            CK(cgx::matvec_add_f64(pl, rows, out, Aprest, out, pown, dot, ws, s));
+            hipLaunchKernelGGL(pl.R == 1 ? k_matvec_add_f64<1> : k_matvec_add_f64<2>, dim3(pl.blocks), dim3(cgx::kNT),
+                               0, s, rows, out, Aprest, out, pown, dot, ws.partials, ws.tickets + cgx::T_MATVEC);
+            CK(hipGetLastError());
         } else if (form == 2) {  // one
             gather(s);
             CK(cgx::matvec_f64_cols(pl, A, n, rows, n, own0, n, false, p, out, pown, dot, ws, s, nullptr, nullptr, rows));

@@ -29,6 +29,7 @@ which is the form a SCALE line reports in its "overlap" key.
 import csv
 import json
 import os
+import re
 import statistics
 import sys
 
@@ -62,17 +63,25 @@ def kernel_spans(trace_csv):
     (rotated, ROT), update_r, update_xp], natural = [matVec, update_r, update_xp]."""
     rows = list(csv.DictReader(open(trace_csv)))
     ks = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Kernel_Name"]) for r in rows)
-    ks = [k for k in ks if "k_matvec_f64" in k[2] or "k_update_r_f64" in k[2] or "k_update_xp_f64" in k[2]]
+    ks = [k for k in ks if any(x in k[2] for x in ("k_matvec_f64<", "k_matvec_add_f64<", "k_update_r_f64", "k_update_xp_f64"))]
     dur = lambda k: (k[1] - k[0]) / 1e3  # noqa: E731
-    rot = lambda k: "k_matvec_f64" in k[2] and k[2].split("(")[0].replace(" ", "").endswith("true,true>")  # noqa: E731
-    mv = lambda k: "k_matvec_f64" in k[2]  # noqa: E731
+    rot = lambda k: "k_matvec_f64<" in k[2] and re.search(r"k_matvec_f64<[^>]*true, true>", k[2]) is not None  # noqa: E731
+    mv = lambda k: "k_matvec_f64<" in k[2]  # noqa: E731
     out = {"split": {"matvec_own": [], "matvec": [], "update_r": [], "update_xp": []},
+           "conc": {"matvec_own": [], "matvec_rest": [], "add": [], "update_r": [], "update_xp": []},
            "one": {"matvec": [], "update_r": [], "update_xp": []},
            "natural": {"matvec": [], "update_r": [], "update_xp": []}}
     i = 0
     while i < len(ks) - 2:
         a, b, c = ks[i], ks[i + 1], ks[i + 2]
-        if mv(a) and not rot(a) and mv(b) and i + 3 < len(ks) and "update_r" in c[2]:
+        if mv(a) and not rot(a) and mv(b) and i + 4 < len(ks) and "k_matvec_add_f64" in c[2]:
+            # the conc form (measured, not adopted): own and rest on two streams (whichever started first), the add
+            own, rest = (a, b) if a[1] - a[0] < b[1] - b[0] else (b, a)
+            for key, k in zip(("matvec_own", "matvec_rest", "add", "update_r", "update_xp"),
+                              (own, rest, c, ks[i + 3], ks[i + 4])):
+                out["conc"][key].append(dur(k))
+            i += 5
+        elif mv(a) and not rot(a) and mv(b) and i + 3 < len(ks) and "update_r" in c[2]:
             for key, k in zip(("matvec_own", "matvec", "update_r", "update_xp"), ks[i:i + 4]):
                 out["split"][key].append(dur(k))
             i += 4
@@ -92,7 +101,8 @@ def main():
     for line in open(os.path.join(PROF, f"{TAG}_rank_iteration.jsonl")):
         d = json.loads(line)
         w = d["us_per_iteration_without_collectives"]
-        if d.get("rank", d["ranks"] // 2) == d["ranks"] // 2:  # a middle rank: its rest wraps (the slowest)
+        # a middle rank (its rest wraps), no emulated gather (the model adds the exchange itself)
+        if d.get("rank", d["ranks"] // 2) == d["ranks"] // 2 and not d.get("gather_us"):
             walls.setdefault(d["ranks"], []).append(w)
     out = {
         "what": "configs[2] (N=65536 dense fp64, row blocks) at G GPUs: one rank's measured kernels in both "
