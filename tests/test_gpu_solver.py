@@ -971,8 +971,11 @@ def test_poisson_local_pull_bitwise_equal_copies(monkeypatch, m, shards):
     only when the host reads r.r).  Against round 3's per-neighbour peer
     copies with combine kernels (CGX_LOCAL_XCHG=copy) and the pull with
     combine kernels (CGX_LOCAL_FUSE=0): x and the loop counts bit for bit,
-    gated, host-checked, fixed counts and pieces, x every third iteration."""
+    gated, host-checked, fixed counts and pieces, x every third iteration.
+    (The copies run before k_poisson_p, CGX_HALO_OVERLAP=0: behind its interior
+    runs p.Ap would add the edge runs' share separately, other bits.)"""
     monkeypatch.setenv("CGX_POISSON_FUSED", "1")
+    monkeypatch.setenv("CGX_HALO_OVERLAP", "0")
     res = {}
     for form in ("pull", "nofuse", "copy"):
         monkeypatch.setenv("CGX_LOCAL_XCHG", "copy" if form == "copy" else "kernel")
@@ -983,9 +986,10 @@ def test_poisson_local_pull_bitwise_equal_copies(monkeypatch, m, shards):
         for key in res["copy"]:
             assert np.array_equal(res[form][key][0], res["copy"][key][0]), (form, key)
             assert res[form][key][1:] == res["copy"][key][1:], (form, key)
-    n = m * m
-    xo, so = oracle.cg_poisson_f64(m, np.ones(n), np.zeros(n), eps=1e-10)
-    assert res["pull"]["solve1"][1] == so.iterations and rel(res["pull"]["solve1"][0], xo) <= 1e-9
+    if m <= 130:  # eps 1e-10 is above the attainable-residual floor only on small grids (test_poisson_matches_oracle)
+        n = m * m
+        xo, so = oracle.cg_poisson_f64(m, np.ones(n), np.zeros(n), eps=1e-10)
+        assert res["pull"]["solve1"][1] == so.iterations and rel(res["pull"]["solve1"][0], xo) <= 1e-9
 
 
 def test_poisson_fused_in_pieces_and_iteration_cap():
