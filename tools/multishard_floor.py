@@ -18,8 +18,14 @@ combine kernel per shard and scalar), "copy" (CGX_LOCAL_XCHG=copy: round
 3's hipMemcpyPeerAsync per pair) and "graph" (onethread's iterations captured
 G = CGX_LOCAL_GRAPH_ITERS at a time into a hipGraph and replayed; without
 CGX_PHASES, which the replay does not take, so that form has no phases).
-Usage:  python tools/r04_multishard_floor.py [rounds] [n,...] [S,...] [forms]
-  > profiles/r04_multishard_floor.jsonl"""
+With --poisson the sizes are grid widths m and the operator is the fused
+Poisson iteration (no CGX_PHASES): forms "pull" (round 5's default: r's halo
+rows read in place by k_poisson_p, both scalar combines folded into the
+kernels), "nofuse" (the pull with a combine kernel per slab and scalar) and
+"copy" (round 4's default: per-neighbour hipMemcpyPeerAsync of the halo rows
+behind k_poisson_p's interior runs, combine kernels).
+Usage:  python tools/multishard_floor.py [--poisson] [rounds] [n or m,...] [S,...] [forms]
+  > profiles/rNN_multishard_floor.jsonl"""
 import json
 import os
 import sys
@@ -67,7 +73,47 @@ def run(n, shards, steps=200, warm=32, phases=True):
             "phases_median_us": {k: round(v["median_us"], 2) for k, v in ph.items() if v["samples"]}}
 
 
+def run_poisson(m, shards, steps=200, warm=30):
+    with cg.Solver(None, poisson_m=m, devices=[0] * shards) as s:
+        s.fill(1.0, 0.0)
+        info = s.info
+        s.begin()
+        s.iterate(warm, eps=-1.0)
+        s.synchronize()
+        t0 = time.perf_counter()
+        s.iterate(steps, eps=-1.0)
+        t1 = time.perf_counter()
+        s.synchronize()
+        t2 = time.perf_counter()
+        s.iterate(9, eps=-1.0)  # the enqueue alone, queues empty (a multiple of the x period 3)
+        t3 = time.perf_counter()
+        s.synchronize()
+    return {"m": m, "shards": shards, "steps": steps,
+            "exchange": ("copy" if os.environ.get("CGX_LOCAL_XCHG") == "copy" else
+                         "nofuse" if os.environ.get("CGX_LOCAL_FUSE") == "0" else "pull"),
+            "flags": int(info.flags), "enqueue_us": round((t1 - t0) / steps * 1e6, 2),
+            "wall_us": round((t2 - t0) / steps * 1e6, 2), "enqueue_9_us": round((t3 - t2) / 9 * 1e6, 2)}
+
+
+def main_poisson(argv):
+    rounds = int(argv[0]) if len(argv) > 0 else 2
+    sizes = tuple(int(v) for v in argv[1].split(",")) if len(argv) > 1 else (1024, 2048, 4096, 8192)
+    counts = tuple(int(v) for v in argv[2].split(",")) if len(argv) > 2 else (8,)
+    forms = tuple(argv[3].split(",")) if len(argv) > 3 else ("pull", "nofuse", "copy")
+    for r in range(rounds):
+        for m in sizes:
+            for S in counts:
+                for form in forms:
+                    os.environ["CGX_LOCAL_XCHG"] = "copy" if form == "copy" else "kernel"
+                    os.environ["CGX_LOCAL_FUSE"] = "0" if form == "nofuse" else "1"
+                    out = run_poisson(m, S)
+                    out["round"] = r
+                    print(json.dumps(out), flush=True)
+
+
 def main():
+    if len(sys.argv) > 1 and sys.argv[1] == "--poisson":
+        return main_poisson(sys.argv[2:])
     rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 2
     sizes = tuple(int(v) for v in sys.argv[2].split(",")) if len(sys.argv) > 2 else (4096,)
     counts = tuple(int(v) for v in sys.argv[3].split(",")) if len(sys.argv) > 3 else (1, 2, 4, 8)
