@@ -504,19 +504,19 @@ def main(argv=None) -> int:
     link_bytes = bytes_launch - res_bytes if stream else bytes_launch
     # ... unless so much of A is resident that HBM, not the link, bounds the matVec
     link_bound = stream and link_bytes / H2D_PEAK_GBS >= bytes_launch / HBM_PEAK_GBS
-    # Several row blocks with the overlap: the matVec is the own-column-block
-    # launch on the compute stream, the rest launch on the exchange stream
-    # after p's allgather, and an add; the CGX_TIMING events bracket all of
-    # it, the wait for the allgather included.  The kernels' own spans come
-    # from the CGX_PHASES stamps (device clock, first block's start to last
-    # block's end): the union of their spans (matvec_busy) is the matVec's
-    # duration on rank 0's GPU.
+    # Several row blocks: the matVec is one rotated launch after p's
+    # allgather, or (overlap chosen) the own-column-block launch beside the
+    # allgather and the rest launch after it, both on the compute stream; the
+    # CGX_TIMING events bracket all of it, the wait for the allgather
+    # included.  The kernels' own spans come from the CGX_PHASES stamps
+    # (device clock, first block's start to last block's end): the union of
+    # their spans (matvec_busy) is the matVec's duration on rank 0's GPU.
     # The roofline takes the slowest rank's kernel spans (max over ranks);
     # matvec_ms stays the CGX_TIMING event figure of earlier rounds.
     mv_kernel_ms = None
     if all_ph is not None and world > 1 and all_ph[0]["matvec_busy"]["samples"] > 0:
-        # the union of the matVec kernels' spans (the overlap runs its own-block and rest launches on two
-        # streams at once, then an add): the matVec's duration without the wait for p
+        # the union of the matVec kernels' spans (one launch, or the overlap's own-block and rest
+        # launches): the matVec's duration without the wait for p
         mv_kernel_ms = max(ph["matvec_busy"]["median_us"] for ph in all_ph) / 1e3
     achieved = (link_bytes if link_bound else bytes_launch) / ((mv_kernel_ms or mv_ms) * 1e-3) / 1e9
     traffic, traffic_src = (None, None) if (stream or poisson) else pmc_traffic(n, world,

@@ -3,6 +3,7 @@
 #include "cgx_device.h"
 
 #include <algorithm>
+#include <type_traits>
 
 namespace cgx {
 namespace {
@@ -97,15 +98,19 @@ __global__ __launch_bounds__(kNT) void k_stencil5_strip_f64(const double *__rest
 // empty asm on the VGPR), so loop strength reduction cannot fold it into a
 // per-lane 64-bit pointer induction variable: every access keeps the
 // `global_load ... vOff, s[base]` form, with the row stepping in SGPRs.
-template <bool NT>
-__device__ __forceinline__ d2 lds2(const double *row, uint32_t off) {
+// k_poisson_p_f64 passes the array base and the row's byte offset plus the
+// lane's in one 32-bit VGPR (OT = uint32_t; slabs of 4 GiB or more: a 64-bit
+// VGPR pair), so its rows step with one VALU add per row shared by the three
+// arrays, not a 64-bit scalar add per row and array.
+template <bool NT, typename OT = uint32_t>
+__device__ __forceinline__ d2 lds2(const double *row, OT off) {
     asm volatile("" : "+v"(off));
     const d2 *p = reinterpret_cast<const d2 *>(reinterpret_cast<const char *>(row) + off);
     if constexpr (NT) return __builtin_nontemporal_load(p);
     else return *p;
 }
-template <bool NT>
-__device__ __forceinline__ void sts2(double *row, uint32_t off, d2 v) {
+template <bool NT, typename OT = uint32_t>
+__device__ __forceinline__ void sts2(double *row, OT off, d2 v) {
     asm volatile("" : "+v"(off));
     d2 *p = reinterpret_cast<d2 *>(reinterpret_cast<char *>(row) + off);
     if constexpr (NT) __builtin_nontemporal_store(v, p);
@@ -174,52 +179,57 @@ constexpr bool NT = true, HT = true;
 // boundary row, read where it lies (the one-process halo pull): system-scope
 // 8-B loads, so no line this device's L2 kept from an earlier iteration is
 // used (the same loads as the other pull kernels, cgx_device.h load_sys).
-template <bool NTL, bool FIRST>
-__device__ __forceinline__ d2 pnv(const double *rrow, const double *prow, const StripLane &L, double beta,
-                                  bool sys = false) {
+// rbase + roff: r's row (byte offset, the lane's included), pbase + poff p_{k-1}'s.
+template <bool NTL, bool FIRST, typename OT>
+__device__ __forceinline__ d2 pnv(const double *rbase, OT roff, const double *pbase, OT poff, const StripLane &L,
+                                  double beta, bool sys = false) {
     d2 rv;
     if (sys) {
-        const double *q = rrow + (L.off >> 3);
+        const double *q = reinterpret_cast<const double *>(reinterpret_cast<const char *>(rbase) + roff);
         rv.x = load_sys(q);
         rv.y = load_sys(q + 1);
     } else {
-        rv = lds2<NTL>(rrow, L.off);
+        rv = lds2<NTL>(rbase, roff);
     }
     if constexpr (FIRST) return keep(L.valid, rv);
-    const d2 pv = lds2<NT>(prow, L.off);
+    // NTL for both rows: an item's last two rows (default policy) are the next item's first two,
+    // p_{k-1}'s as well as r's (round 5 briefly streamed p's past L2: 8 % more DRAM reads, 268 -> 283 us)
+    const d2 pv = lds2<NTL>(pbase, poff);
     d2 o;
     o.x = __builtin_fma(beta, pv.x, rv.x);
     o.y = __builtin_fma(beta, pv.y, rv.y);
     return keep(L.valid, o);
 }
-template <bool FIRST>
-__device__ __forceinline__ double pns(const double *rrow, const double *prow, int64_t col, double beta) {
-    if constexpr (FIRST) return rrow[col];
-    else return __builtin_fma(beta, prow[col], rrow[col]);
+// One side point: byte offset `off` into r and p_{k-1} (wave-uniform: a scalar load).
+template <bool FIRST, typename OT>
+__device__ __forceinline__ double pns(const double *rbase, const double *pbase, OT off, double beta) {
+    const double rv = *reinterpret_cast<const double *>(reinterpret_cast<const char *>(rbase) + off);
+    if constexpr (FIRST) return rv;
+    else return __builtin_fma(beta, *reinterpret_cast<const double *>(reinterpret_cast<const char *>(pbase) + off), rv);
 }
 
 // RBn output rows starting at interior row i: pm, pc carry p_k rows h = i, i+1.
 // rdn (one process, several row blocks): r's bottom halo row is the next
 // block's first row, read in place instead of from rh's halo row.
-template <int RBn, bool FIRST>
+template <int RBn, bool FIRST, typename OT>
 __device__ __forceinline__ void poisson_p_step(const double *__restrict__ rh, const double *__restrict__ poh,
                                                double *__restrict__ pnh, int64_t mloc, int64_t m, int64_t i,
                                                const StripLane &L, double beta, d2 &pm, d2 &pc, double &acc,
                                                double *eb, const double *rdn) {
     const int lane = threadIdx.x & 63;
+    const OT mb = (OT)m * 8, oc0 = (OT)((i + 1) * m) * 8, lo = (OT)L.off;
     d2 pr[RBn], ce[RBn];
     double el[RBn], er[RBn];
 #pragma unroll
     for (int t = 0; t < RBn; ++t) {
-        const int64_t hc = (i + t + 1) * m;  // centre row (halo coordinates) of output row i+t
+        const OT oc = oc0 + (OT)t * mb, od = oc + mb;  // centre row (halo coordinates) of output row i+t, the row below
         const bool pull = rdn && i + t + 1 == mloc;  // the row below is the bottom halo row
-        const double *rrow = pull ? rdn : rh + hc + m;
         // HT: the last two rows are the next item's first two (its halo):
         // default-policy loads keep them in L2 for the block that reads them next
-        pr[t] = (HT && t >= RBn - 2) ? pnv<false, FIRST>(rrow, poh + hc + m, L, beta, pull)
-                                     : pnv<NT, FIRST>(rrow, poh + hc + m, L, beta, pull);
-        el[t] = L.has_l ? pns<FIRST>(rh + hc, poh + hc, L.jw - 1, beta) : 0.0;
-        er[t] = L.has_r ? pns<FIRST>(rh + hc, poh + hc, L.jw + 128, beta) : 0.0;
+        pr[t] = (HT && t >= RBn - 2) ? pnv<false, FIRST>(pull ? rdn : rh, pull ? lo : od + lo, poh, od + lo, L, beta, pull)
+                                     : pnv<NT, FIRST>(pull ? rdn : rh, pull ? lo : od + lo, poh, od + lo, L, beta, pull);
+        el[t] = L.has_l ? pns<FIRST>(rh, poh, oc + (OT)(L.jw - 1) * 8, beta) : 0.0;
+        er[t] = L.has_r ? pns<FIRST>(rh, poh, oc + (OT)(L.jw + 128) * 8, beta) : 0.0;
     }
 #pragma unroll
     for (int t = 0; t < RBn; ++t) ce[t] = t == 0 ? pc : pr[t - 1];
@@ -239,8 +249,8 @@ __device__ __forceinline__ void poisson_p_step(const double *__restrict__ rh, co
         o.y = 4.0 * ce[t].y - up.y - dn.y - ce[t].x - r;
         acc += ce[t].x * o.x + ce[t].y * o.y;  // zero on lanes past the grid
         if (L.valid) {
-            sts2<NT>(pnh + (i + t + 1) * m, L.off, ce[t]);
-            if (i + t == mloc - 1) sts2<NT>(pnh + (mloc + 1) * m, L.off, dn);  // bottom halo row of p_k
+            sts2<NT>(pnh, oc0 + (OT)t * mb + lo, ce[t]);
+            if (i + t == mloc - 1) sts2<NT>(pnh, (OT)((mloc + 1) * m) * 8 + lo, dn);  // bottom halo row of p_k
         }
     }
     if constexpr (RBn >= 2) {
@@ -298,7 +308,7 @@ struct HaloPull {
     const double *up, *dn;
 };
 
-template <int RB, bool FIRST>
+template <int RB, bool FIRST, typename OT>
 __device__ __forceinline__ double poisson_p_body(const double *__restrict__ rh, const double *__restrict__ poh,
                                                  double *__restrict__ pnh, int64_t mloc, int64_t m, int64_t nstrips,
                                                  int64_t rpi, ItemRanges ir, double beta, double *edge, int bands,
@@ -313,42 +323,67 @@ __device__ __forceinline__ double poisson_p_body(const double *__restrict__ rh, 
         const int64_t i0 = (w / nstrips) * rpi;
         const int64_t i1 = (i0 + rpi < mloc) ? i0 + rpi : mloc;
         const bool pull = hp.up && i0 == 0;  // the top halo row
-        d2 pm = pnv<NT && !HT, FIRST>(pull ? hp.up : rh + i0 * m, poh + i0 * m, L, beta, pull);
-        d2 pc = pnv<NT && !HT, FIRST>(rh + (i0 + 1) * m, poh + (i0 + 1) * m, L, beta);
-        if (L.valid && i0 == 0) sts2<NT>(pnh, L.off, pm);  // top halo row of p_k
+        const OT lo = (OT)L.off, o0 = (OT)(i0 * m) * 8 + lo, o1 = (OT)((i0 + 1) * m) * 8 + lo;
+        d2 pm = pnv<NT && !HT, FIRST>(pull ? hp.up : rh, pull ? lo : o0, poh, o0, L, beta, pull);
+        d2 pc = pnv<NT && !HT, FIRST>(rh, o1, poh, o1, L, beta);
+        if (L.valid && i0 == 0) sts2<NT>(pnh, lo, pm);  // top halo row of p_k
         int64_t i = i0;
         for (; i + RB <= i1; i += RB, par ^= 1)
-            poisson_p_step<RB, FIRST>(rh, poh, pnh, mloc, m, i, L, beta, pm, pc, acc,
-                                      edge + par * (kWaves * 2 * kEdgeRB), hp.dn);
+            poisson_p_step<RB, FIRST, OT>(rh, poh, pnh, mloc, m, i, L, beta, pm, pc, acc,
+                                          edge + par * (kWaves * 2 * kEdgeRB), hp.dn);
         for (; i < i1; ++i, par ^= 1)
-            poisson_p_step<1, FIRST>(rh, poh, pnh, mloc, m, i, L, beta, pm, pc, acc,
-                                     edge + par * (kWaves * 2 * kEdgeRB), hp.dn);
+            poisson_p_step<1, FIRST, OT>(rh, poh, pnh, mloc, m, i, L, beta, pm, pc, acc,
+                                         edge + par * (kWaves * 2 * kEdgeRB), hp.dn);
     }
     return acc;
 }
 
-// rr_sum.cnt > 0 (one process, several row blocks): r.r_k is the rank-order
-// sum of the blocks' partials, formed here (k_combine_peers' sum, the same
-// bits) instead of by a combine kernel of its own; block 0 stores it.
-template <int RB>
+// The one-process pull's arguments (several row blocks): the halo pull above,
+// and rr_sum.cnt > 0: r.r_k is the rank-order sum of the blocks' partials,
+// formed here (k_combine_peers' sum, the same bits) instead of by a combine
+// kernel of its own; block 0 stores it.  One block and rank mode launch the
+// NoPull instantiation, which has neither the arguments nor the tests: with
+// them in its signature and its inner loop (round 5's first form) the
+// kernel ran at 284-294 instead of 268-269 us per launch at m = 8192 on one
+// box (profiles/r05_poisson_p_pull_ab.jsonl).
+struct NoPull {};
+struct PullArgs {
+    HaloPull hp;
+    PeerSum rr_sum;
+};
+// p.Ap for the xr kernels: the slot, or the blocks' partials summed in rank order
+__device__ __forceinline__ double pap_of(const NoPull &, const double *pAp) { return *pAp; }
+__device__ __forceinline__ double pap_of(const PeerSum &ps, const double *pAp) {
+    return ps.cnt ? peer_sum_wave(ps) : *pAp;
+}
+template <int RB, class PA, typename OT>
 __global__ __launch_bounds__(kNT) void k_poisson_p_f64(const double *__restrict__ rh, const double *__restrict__ poh,
                                                        double *__restrict__ pnh, int64_t mloc, int64_t m,
                                                        int64_t nstrips, int64_t rpi, ItemRanges ir, const double *rr,
                                                        const double *rsold, int first, ConvArgs cv, double *dot_out,
                                                        int add_to_out, double *partials, unsigned *ticket, int bands,
-                                                       HaloPull hp, PeerSum rr_sum) {
+                                                       PA pa) {
     static_assert(RB <= kEdgeRB, "edge buffer");
+    constexpr bool PULL = std::is_same<PA, PullArgs>::value;
     __shared__ double edge[2 * kWaves * 2 * kEdgeRB];
-    if (cv.kdone && *cv.kdone != 0) return;
-    const double rrk = first ? 0.0 : rr_sum.cnt ? peer_sum_wave(rr_sum) : *rr;
-    if (cv.kdone && !first && cv.eps >= 0.0 && sqrt(rrk) < cv.eps) {  // the same decision in every block
-        if (blockIdx.x == 0 && threadIdx.x == 0) record_convergence(cv, cv.k, rrk);
-        return;
+    double rrk = 0.0;  // r.r_k (not read when first)
+    if (!first) {
+        if constexpr (PULL) rrk = pa.rr_sum.cnt ? peer_sum_wave(pa.rr_sum) : *rr;
+        else rrk = *rr;
     }
+    if (cv.kdone) {
+        if (*cv.kdone != 0) return;
+        if (!first && cv.eps >= 0.0 && sqrt(rrk) < cv.eps) {  // the same decision in every block
+            if (blockIdx.x == 0 && threadIdx.x == 0) record_convergence(cv, cv.k, rrk);
+            return;
+        }
+    }
+    HaloPull h{nullptr, nullptr};
+    if constexpr (PULL) h = pa.hp;
     // p_0 = r_0 (first) has its own instantiation: no p_{k-1} loads
-    const double acc = first ? poisson_p_body<RB, true>(rh, poh, pnh, mloc, m, nstrips, rpi, ir, 0.0, edge, bands, hp)
-                             : poisson_p_body<RB, false>(rh, poh, pnh, mloc, m, nstrips, rpi, ir,
-                                                         cg_ratio(rrk, *rsold), edge, bands, hp);
+    const double acc = first ? poisson_p_body<RB, true, OT>(rh, poh, pnh, mloc, m, nstrips, rpi, ir, 0.0, edge, bands, h)
+                             : poisson_p_body<RB, false, OT>(rh, poh, pnh, mloc, m, nstrips, rpi, ir,
+                                                             cg_ratio(rrk, *rsold), edge, bands, h);
     grid_sum_last_block(acc, partials, ticket, dot_out, add_to_out != 0);
 }
 
@@ -440,7 +475,9 @@ __device__ __forceinline__ void poisson_xr_step(const double *__restrict__ pnh, 
 // partials add in the same order whichever variant runs (a thread adds its
 // rows in row order whatever RB is): x is the same bits with and without the
 // deferral.
-template <int RB, int XM>
+// PS: PeerSum (one process, several row blocks: p.Ap summed here from the
+// blocks' partials, as k_poisson_p_f64's r.r) or NoPull (read *pAp).
+template <int RB, int XM, class PS>
 __global__ __launch_bounds__(kNT) void k_poisson_xr_f64(const double *__restrict__ pnh, const double *__restrict__ poh,
                                                         const double *__restrict__ pqh, double *__restrict__ x,
                                                         double *__restrict__ r, int64_t mloc,
@@ -448,12 +485,11 @@ __global__ __launch_bounds__(kNT) void k_poisson_xr_f64(const double *__restrict
                                                         int reverse, const double *rsold, const double *pAp,
                                                         double *rr_out, double *xalpha, double *partials,
                                                         unsigned *ticket, const int64_t *gate, int bands,
-                                                        PeerSum pap_sum) {
+                                                        PS pap_sum) {
     static_assert(RB <= kEdgeRB, "edge buffer");
     __shared__ double edge[2 * kWaves * 2 * kEdgeRB];
     if (gate && *gate) return;
-    // pap_sum.cnt > 0: p.Ap summed here from the row blocks' partials (as k_poisson_p_f64's r.r)
-    const double alpha = cg_ratio(*rsold, pap_sum.cnt ? peer_sum_wave(pap_sum) : *pAp);
+    const double alpha = cg_ratio(*rsold, pap_of(pap_sum, pAp));
     // XM = 2: alpha_{k-1} = xalpha[0]; XM = 3: alpha_{k-2} = xalpha[0], alpha_{k-1} = xalpha[1]
     const double alpha_prev = XM == 2 ? xalpha[0] : XM == 3 ? xalpha[1] : 0.0;
     const double alpha_prev2 = XM == 3 ? xalpha[0] : 0.0;
@@ -624,7 +660,7 @@ __device__ __forceinline__ void xr_pipe_step(const XrSet<RBn, XM> &S, double *__
         pc = S.pr[0];
     }
 }
-template <int RBn, int NS, int XM>
+template <int RBn, int NS, int XM, class PS>
 __global__ __launch_bounds__(kNT) void k_poisson_xr_pipe_f64(const double *__restrict__ pnh,
                                                              const double *__restrict__ poh,
                                                              const double *__restrict__ pqh, double *__restrict__ x,
@@ -633,12 +669,12 @@ __global__ __launch_bounds__(kNT) void k_poisson_xr_pipe_f64(const double *__res
                                                              const double *pAp, double *rr_out, double *xalpha,
                                                              double *partials, unsigned *ticket, const int64_t *gate,
                                                              int bands, const double *__restrict__ hot,
-                                                             PeerSum pap_sum) {
+                                                             PS pap_sum) {
     static_assert(RBn <= kEdgeRB && NS % 2 == 0, "edge buffer / set parity");
     constexpr int64_t kRpi = RBn * NS;
     __shared__ double edge[2 * kWaves * 2 * kEdgeRB];
     if (gate && *gate) return;
-    const double alpha = cg_ratio(*rsold, pap_sum.cnt ? peer_sum_wave(pap_sum) : *pAp);
+    const double alpha = cg_ratio(*rsold, pap_of(pap_sum, pAp));
     const double alpha_prev = XM == 2 ? xalpha[0] : XM == 3 ? xalpha[1] : 0.0;
     const double alpha_prev2 = XM == 3 ? xalpha[0] : 0.0;
     double acc = 0.0;
@@ -785,28 +821,49 @@ static PeerSum no_sum() {
     return z;
 }
 
+template <int RB, class PA, typename OT>
+static void launch_p(const PoissonPlan &pl, hipStream_t s, const double *rh, const double *poh, double *pnh,
+                     int64_t mloc, int64_t m, const double *rr, const double *rsold, int first, ConvArgs cv,
+                     double *pap_out, const RedWs &ws, ItemRanges ir, int add_to_out, const PA &pa) {
+    auto fn = k_poisson_p_f64<RB, PA, OT>;
+    int64_t grid = resident_grid(pl, reinterpret_cast<const void *>(fn), ir.cnt1 + ir.cnt2);
+    const int bands = pl.bands && ir.cnt2 == 0 && ir.cnt1 % pl.nstrips == 0 && grid >= 8 ? 1 : 0;
+    if (bands) grid &= ~int64_t(7);
+    hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(kNT), 0, s, rh, poh, pnh, mloc, m, pl.nstrips, pl.rpi, ir, rr,
+                       rsold, first, cv, pap_out, add_to_out, ws.partials, ws.tickets + T_MATVEC, bands, pa);
+}
 template <int RB>
 static void launch_poisson_p(const PoissonPlan &pl, hipStream_t s, const double *rh, const double *poh, double *pnh,
                              int64_t mloc, int64_t m, const double *rr, const double *rsold, int first, ConvArgs cv,
                              double *pap_out, const RedWs &ws, ItemRanges ir, int add_to_out, HaloPull hp,
                              const PeerSum &rr_sum) {
-    auto fn = k_poisson_p_f64<RB>;
-    int64_t grid = resident_grid(pl, reinterpret_cast<const void *>(fn), ir.cnt1 + ir.cnt2);
-    const int bands = pl.bands && ir.cnt2 == 0 && ir.cnt1 % pl.nstrips == 0 && grid >= 8 ? 1 : 0;
-    if (bands) grid &= ~int64_t(7);
-    hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(kNT), 0, s, rh, poh, pnh, mloc, m, pl.nstrips, pl.rpi, ir, rr,
-                       rsold, first, cv, pap_out, add_to_out, ws.partials, ws.tickets + T_MATVEC, bands, hp, rr_sum);
+    // every byte offset into a slab (halo rows included) fits 32 bits: the one-VGPR offsets
+    const bool o32 = (mloc + 2) * m * 8 <= (int64_t)UINT32_MAX;
+    if (hp.up || hp.dn || rr_sum.cnt) {
+        const PullArgs pa{hp, rr_sum};
+        if (o32) launch_p<RB, PullArgs, uint32_t>(pl, s, rh, poh, pnh, mloc, m, rr, rsold, first, cv, pap_out, ws, ir,
+                                                  add_to_out, pa);
+        else launch_p<RB, PullArgs, uint64_t>(pl, s, rh, poh, pnh, mloc, m, rr, rsold, first, cv, pap_out, ws, ir,
+                                              add_to_out, pa);
+    } else if (o32) {
+        launch_p<RB, NoPull, uint32_t>(pl, s, rh, poh, pnh, mloc, m, rr, rsold, first, cv, pap_out, ws, ir, add_to_out,
+                                       NoPull{});
+    } else {
+        launch_p<RB, NoPull, uint64_t>(pl, s, rh, poh, pnh, mloc, m, rr, rsold, first, cv, pap_out, ws, ir, add_to_out,
+                                       NoPull{});
+    }
 }
+template <int XM, class PS>
 using XrFn = void (*)(const double *, const double *, const double *, double *, double *, int64_t, int64_t, int64_t,
-                     int64_t, int64_t, int, const double *, const double *, double *, double *, double *, unsigned *,
-                     const int64_t *, int, PeerSum);
-template <int XM>
-static XrFn xr_fn_rb(int rb) {
+                      int64_t, int64_t, int, const double *, const double *, double *, double *, double *, unsigned *,
+                      const int64_t *, int, PS);
+template <int XM, class PS>
+static XrFn<XM, PS> xr_fn_rb(int rb) {
     switch (rb) {
-        case 1: return k_poisson_xr_f64<1, XM>;
-        case 2: return k_poisson_xr_f64<2, XM>;
-        case 8: return k_poisson_xr_f64<8, XM>;
-        default: return k_poisson_xr_f64<4, XM>;
+        case 1: return k_poisson_xr_f64<1, XM, PS>;
+        case 2: return k_poisson_xr_f64<2, XM, PS>;
+        case 8: return k_poisson_xr_f64<8, XM, PS>;
+        default: return k_poisson_xr_f64<4, XM, PS>;
     }
 }
 // Every x mode runs on the grid of the every-iteration kernel at the plan's
@@ -818,18 +875,18 @@ static XrFn xr_fn_rb(int rb) {
 // bits (profiles/r04_poisson_catchup_ab.jsonl).  The pipelined form of the
 // other kernels measured no better (XM = 0: 283 vs 276 us in the kernel trace;
 // k_poisson_p: 1346-1464 vs 1475 it/s) and was removed in round 5.
-template <int XM>
+template <int XM, class PS>
 static void launch_poisson_xr(const PoissonPlan &pl, hipStream_t s, const double *pnh, const double *poh,
                               const double *pqh, double *x, double *r, int64_t mloc, int64_t m, const double *rsold,
                               const double *pAp, double *rr_out, double *xalpha, const RedWs &ws,
-                              const int64_t *gate, const PeerSum &pap_sum) {
+                              const int64_t *gate, const PS &pap_sum) {
     const int rb = XM >= 2 && pl.rb > 1 ? pl.rb / 2 : pl.rb;
-    const XrFn fn = xr_fn_rb<XM>(rb);
-    int64_t grid = resident_grid(pl, reinterpret_cast<const void *>(xr_fn_rb<1>(pl.rb)), pl.nitems);
+    const XrFn<XM, PS> fn = xr_fn_rb<XM, PS>(rb);
+    int64_t grid = resident_grid(pl, reinterpret_cast<const void *>(xr_fn_rb<1, PS>(pl.rb)), pl.nitems);
     const int bands = pl.bands && grid >= 8 ? 1 : 0;
     if (bands) grid &= ~int64_t(7);
     if (XM >= 2 && pl.pipe && m % (2 * kNT) == 0 && pl.rpi == 8 && mloc % 8 == 0) {
-        auto fp = k_poisson_xr_pipe_f64<4, 2, XM>;
+        auto fp = k_poisson_xr_pipe_f64<4, 2, XM, PS>;
         hipLaunchKernelGGL(fp, dim3((unsigned)grid), dim3(kNT), 0, s, pnh, poh, pqh, x, r,
                            m, pl.nstrips, pl.nitems, pl.reverse, rsold, pAp, rr_out, xalpha, ws.partials,
                            ws.tickets + T_XR, gate, bands, rsold, pap_sum);
@@ -838,6 +895,18 @@ static void launch_poisson_xr(const PoissonPlan &pl, hipStream_t s, const double
     hipLaunchKernelGGL(fn, dim3((unsigned)grid), dim3(kNT), 0, s, pnh, poh, pqh, x, r, mloc, m, pl.nstrips, pl.rpi,
                        pl.nitems, pl.reverse, rsold, pAp, rr_out, xalpha, ws.partials, ws.tickets + T_XR, gate, bands,
                        pap_sum);
+}
+template <int XM>
+static void launch_poisson_xr_any(const PoissonPlan &pl, hipStream_t s, const double *pnh, const double *poh,
+                                  const double *pqh, double *x, double *r, int64_t mloc, int64_t m,
+                                  const double *rsold, const double *pAp, double *rr_out, double *xalpha,
+                                  const RedWs &ws, const int64_t *gate, const PeerSum *pap_sum) {
+    if (pap_sum && pap_sum->cnt > 0)
+        launch_poisson_xr<XM, PeerSum>(pl, s, pnh, poh, pqh, x, r, mloc, m, rsold, pAp, rr_out, xalpha, ws, gate,
+                                       *pap_sum);
+    else
+        launch_poisson_xr<XM, NoPull>(pl, s, pnh, poh, pqh, x, r, mloc, m, rsold, pAp, rr_out, xalpha, ws, gate,
+                                      NoPull{});
 }
 
 hipError_t poisson_p_f64(const double *rh, const double *poh, double *pnh, int64_t mloc, int64_t m, const double *rr,
@@ -886,12 +955,11 @@ hipError_t poisson_xr_f64(const double *pnh, const double *poh, const double *pq
         (xmode == 3 && !al16(pqh)) || (pap_sum && (pap_sum->cnt < 0 || pap_sum->cnt > kMaxPeers)))
         return hipErrorInvalidValue;
     const PoissonPlan pl = poisson_plan(mloc, m);
-    const PeerSum ps = pap_sum ? *pap_sum : no_sum();
     switch (xmode) {
-        case 0: launch_poisson_xr<0>(pl, s, pnh, poh, pqh, x, r, mloc, m, rsold, pAp, rr_out, xalpha, ws, gate, ps); break;
-        case 2: launch_poisson_xr<2>(pl, s, pnh, poh, pqh, x, r, mloc, m, rsold, pAp, rr_out, xalpha, ws, gate, ps); break;
-        case 3: launch_poisson_xr<3>(pl, s, pnh, poh, pqh, x, r, mloc, m, rsold, pAp, rr_out, xalpha, ws, gate, ps); break;
-        default: launch_poisson_xr<1>(pl, s, pnh, poh, pqh, x, r, mloc, m, rsold, pAp, rr_out, xalpha, ws, gate, ps); break;
+        case 0: launch_poisson_xr_any<0>(pl, s, pnh, poh, pqh, x, r, mloc, m, rsold, pAp, rr_out, xalpha, ws, gate, pap_sum); break;
+        case 2: launch_poisson_xr_any<2>(pl, s, pnh, poh, pqh, x, r, mloc, m, rsold, pAp, rr_out, xalpha, ws, gate, pap_sum); break;
+        case 3: launch_poisson_xr_any<3>(pl, s, pnh, poh, pqh, x, r, mloc, m, rsold, pAp, rr_out, xalpha, ws, gate, pap_sum); break;
+        default: launch_poisson_xr_any<1>(pl, s, pnh, poh, pqh, x, r, mloc, m, rsold, pAp, rr_out, xalpha, ws, gate, pap_sum); break;
     }
     return hipGetLastError();
 }
