@@ -342,10 +342,8 @@ __device__ __forceinline__ double poisson_p_body(const double *__restrict__ rh, 
 // and rr_sum.cnt > 0: r.r_k is the rank-order sum of the blocks' partials,
 // formed here (k_combine_peers' sum, the same bits) instead of by a combine
 // kernel of its own; block 0 stores it.  One block and rank mode launch the
-// NoPull instantiation, which has neither the arguments nor the tests: with
-// them in its signature and its inner loop (round 5's first form) the
-// kernel ran at 284-294 instead of 268-269 us per launch at m = 8192 on one
-// box (profiles/r05_poisson_p_pull_ab.jsonl).
+// NoPull instantiation, which has neither the arguments nor the pull tests
+// (its code is the pre-pull kernel's; profiles/r05_poisson_regression.json).
 struct NoPull {};
 struct PullArgs {
     HaloPull hp;
