@@ -296,15 +296,16 @@ struct cgx_ctx {
     bool xdefer = false;
     int xd = 1;  // the period: 2 (default) or 3 (CGX_POISSON_XDEFER=3, a third p slab)
     int64_t xd_k0 = 0;
-    // a cgx_iterate call failed with x updates still deferred (xd > 1): the
-    // alphas left out cannot be placed, so x is incomplete until the next
-    // cgx_solve_begin; cgx_get_x / cgx_iterate / cgx_residual_norm refuse it
-    bool x_incomplete = false;
+    // a cgx_iterate call failed: x may hold part of an iteration, or (x_deferred,
+    // xd > 1) lack the alphas left out, which cannot be placed -- x is
+    // incomplete until cgx_set_x defines it or the next cgx_solve_begin;
+    // cgx_get_x / cgx_iterate / cgx_residual_norm refuse it
+    bool x_incomplete = false, x_deferred = false;
     bool xalpha_pending = false;  // fused Poisson: an xr kernel left alpha_k p_k out of x (xmode 0), not yet caught up
     // a cgx_iterate call failed part-way through an iteration (a HIP error, an
     // RCCL deadline, a row block's worker): some blocks may have applied part
     // of iteration k, so repeating it would apply it twice -- cgx_iterate
-    // refuses until the next cgx_solve_begin
+    // refuses until the next cgx_solve_begin (x: x_incomplete)
     bool iter_failed = false;
     // rank mode fail-fast (cgx_exchange.hip, rank_wait_*): every host wait
     // polls with a deadline of rccl_timeout_s seconds (CGX_RCCL_TIMEOUT_S,

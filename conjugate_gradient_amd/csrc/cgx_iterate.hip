@@ -225,7 +225,7 @@ int do_begin(cgx_ctx *c) {
     c->k = 0;
     c->converged = 0;
     c->state = ST_BEGUN;
-    c->x_incomplete = false;
+    c->x_incomplete = c->x_deferred = false;
     c->xalpha_pending = false;
     c->iter_failed = false;
     return CGX_OK;
@@ -386,8 +386,11 @@ int poisson_x_finish(cgx_ctx *c) {
 
 int check_x_complete(const cgx_ctx *c) {
     if (!c->x_incomplete) return CGX_OK;
-    return fail(CGX_ERR_STATE, "an earlier cgx_iterate failed with x updates still deferred (Poisson, x every "
-                               "%d-th iteration): x is incomplete until the next cgx_solve_begin", c->xd);
+    if (c->x_deferred)
+        return fail(CGX_ERR_STATE, "an earlier cgx_iterate failed with x updates still deferred (Poisson, x every "
+                                   "%d-th iteration): x is incomplete until the next cgx_solve_begin", c->xd);
+    return fail(CGX_ERR_STATE, "an earlier cgx_iterate failed part-way through iteration %lld: x may hold part of it "
+                               "and is incomplete until cgx_set_x or the next cgx_solve_begin", (long long)c->k);
 }
 
 // One loop iteration k (serialConjugate.c:215-244 / parallel_cg.c:290-323).
@@ -733,10 +736,10 @@ int cgx_iterate(cgx_ctx *c, int64_t count, double eps, int64_t *done, int *conve
     const Range range_("cgx_iterate");
     if (!c) return fail(CGX_ERR_ARG, "ctx is NULL");
     if (c->state == ST_IDLE) return fail(CGX_ERR_STATE, "cgx_iterate before cgx_solve_begin");
-    TRY(check_x_complete(c));
     if (c->iter_failed)
         return fail(CGX_ERR_STATE, "an earlier cgx_iterate failed part-way through iteration %lld: the solve "
                                    "cannot continue (cgx_solve_begin starts a new one)", (long long)c->k);
+    TRY(check_x_complete(c));
     const int rc = iterate_calls(c, count, eps, done, converged);
     if (rc != CGX_OK) {
         // Part of an iteration may have run on some row blocks (or all of
@@ -744,7 +747,8 @@ int cgx_iterate(cgx_ctx *c, int64_t count, double eps, int64_t *done, int *conve
         // when x updates were left out (poisson_x_finish not reached), say so
         // at the next use of x instead of handing out an x with terms missing.
         c->iter_failed = true;
-        if (c->fused && c->xd > 1 && (c->k > c->xd_k0 || c->xalpha_pending)) c->x_incomplete = true;
+        c->x_incomplete = true;
+        c->x_deferred = c->fused && c->xd > 1 && (c->k > c->xd_k0 || c->xalpha_pending);
     }
     return rc;
 }

@@ -811,7 +811,7 @@ int cgx_set_rows(cgx_ctx *c, int64_t row0, int64_t nrows, const void *A_rows, in
         }
         TRY(rank_wait_stream(c, s.stream, "the copies of cgx_set_rows"));
     }
-    if (x_rows && row0 == 0 && nrows == c->n) c->x_incomplete = false;  // x fully defined again
+    if (x_rows && row0 == 0 && nrows == c->n) c->x_incomplete = c->x_deferred = false;  // x fully defined again
     c->state = ST_IDLE;
     return CGX_OK;
 }

@@ -333,7 +333,11 @@ int cgx_set_system(cgx_ctx *ctx, const void *A, const void *b, const void *x0);
 int cgx_generate_spd(cgx_ctx *ctx, uint64_t seed);
 /* b = b_value and x0 = x_value everywhere (e.g. the Poisson config: b = 1, x0 = 0). */
 int cgx_fill(cgx_ctx *ctx, double b_value, double x_value);
-/* x (n entries, replicated result like parallel_cg.c's local_vectorX). */
+/* x (n entries, replicated result like parallel_cg.c's local_vectorX).
+ * After a cgx_iterate that failed part-way (a HIP error, an RCCL deadline),
+ * x may hold part of an iteration: cgx_get_x and cgx_residual_norm return
+ * CGX_ERR_STATE until cgx_set_x defines x again or cgx_solve_begin starts a
+ * new solve, and cgx_iterate refuses until cgx_solve_begin. */
 int cgx_get_x(cgx_ctx *ctx, void *x);
 int cgx_set_x(cgx_ctx *ctx, const void *x);
 

@@ -130,10 +130,20 @@ def fail_fast(mode, n, P, rank, uid, out):
         res["created_s"] = time.time() - t0
         say("set_system + solve")
         s.set_system(A, b, x0)
-        s.solve(None, eps=1e-10)
+        res["failed_in"] = "cgx_solve_begin"
+        s.begin()
+        res["failed_in"] = "cgx_iterate"
+        s.iterate(n, eps=1e-10)
+        res["failed_in"] = None
     except cg.CgxError as e:
         res.update(error=str(e), code=e.code)
         say(f"error: {e}")
+        if s is not None:  # after a failed iterate x may hold part of an iteration: refused
+            try:
+                s.get_x()
+                res["get_x"] = "ok"
+            except cg.CgxError as e2:
+                res.update(get_x=str(e2), get_x_code=e2.code)
     res["elapsed_s"] = time.time() - t0
     with open(out + f"_r{rank}.json", "w") as f:
         json.dump(res, f)
