@@ -311,9 +311,13 @@ def test_bench_under_torchrun_world2(workload):
         # the per-phase breakdown: every rank, every phase, and the phases tile the iteration
         ph = out["phases_us"]
         assert ph["iterations_sampled"] == steps - 1 and len(ph["per_rank"]) == 2
+        # the exchange form the context measured and chose at creation, named in the line
+        ov = out["overlap"]
+        assert ov["decided_by"] == "measured" and ov["on"] == (ov["allgather_us"] > ov["split_cost_us"]), ov
         for r in ph["per_rank"]:
             assert set(r) == set(cg.PHASE_NAMES)
-            assert r["matvec_own"] > 0 and r["matvec"] > 0 and r["combine_pap"] > 0 and r["iteration"] > 0
+            assert (r["matvec_own"] > 0) == ov["on"] and r["matvec"] > 0 and r["combine_pap"] > 0
+            assert r["iteration"] > 0 and r["matvec_busy"] >= r["matvec"]
         assert abs(ph["tiling_mean_sum_over_ms_per_step"] - 1) <= 0.05, ph
         # the matVec roofline uses the two kernels' own spans (slowest rank), not the event bracket around
         # the allgather wait, which matvec_ms keeps
