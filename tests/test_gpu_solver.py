@@ -375,6 +375,30 @@ def test_configs4_poisson_m8192_full_size():
     assert abs(rn - ro) <= 1e-9 * ro and abs(bn - m) <= 1e-12 * m
 
 
+@pytest.mark.timeout(600)
+def test_poisson_slab_over_4gib_byte_offsets():
+    """k_poisson_p addresses a slab's rows by 32-bit byte offsets while every
+    offset fits (halo rows included: (m + 2) m 8 B <= 2^32 - 1), else by 64-bit
+    ones.  m = 23172 is the first even grid past that bound on one slab: 5
+    fixed iterations against the fp64 oracle (x and the true residual to 1e-9)."""
+    m, iters = 23172, 5
+    assert (m + 2) * m * 8 > 2**32 - 1 >= (m // 2 + 2) * m * 8
+    n = m * m
+    with cg.Solver(None, poisson_m=m) as s:
+        assert s.info.flags & cg.CGX_FUSED_ACTIVE
+        s.fill(1.0, 0.0)
+        x, st = s.solve(None, eps=-1.0, max_iter=iters)
+        rn, bn = s.residual_norm()
+    assert st.iterations == iters
+    oracle.set_threads(16)
+    xo, so = oracle.cg_poisson_f64(m, np.ones(n), np.zeros(n), eps=-1.0, max_iter=iters)
+    assert so.iterations == iters
+    assert rel(x, xo) <= 1e-9
+    del x
+    ro = np.linalg.norm(1.0 - oracle.poisson_apply(m, xo))
+    assert abs(rn - ro) <= 1e-9 * ro and abs(bn - m) <= 1e-12 * m
+
+
 def test_solve_in_pieces_and_fixed_count():
     """cgx_solve_begin + cgx_iterate == cgx_solve; eps < 0 runs exactly max_iter."""
     A, b, x0 = case("spd1024", np.float64)
