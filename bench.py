@@ -115,22 +115,68 @@ def matvec_bytes(n: int, nloc: int) -> int:
     return 8 * nloc * n + 8 * n + 8 * nloc
 
 
-def pmc_traffic(n: int, nranks: int, suffix: str = "") -> tuple[float | None, str | None]:
-    """HBM bytes per matVec launch from the committed PMC passes (rocprofv3
-    cannot run inside this process), and where that figure came from."""
+def pmc_traffic(key: str) -> tuple[float | None, str | None]:
+    """HBM bytes per launch of the roofline's kernel from the committed PMC
+    passes (rocprofv3 cannot run inside this process), and where that figure
+    came from.  Keys: "n<N>_g<G>[_symmetric]" (the dense matVec),
+    "poisson_m<M>_g<G>" (the Poisson xr kernels, averaged over their x-update
+    cycle)."""
     path = os.path.join(ROOT, "profiles", "pmc_summary.json")
     try:
         with open(path) as f:
             s = json.load(f)
-        key = f"n{n}_g{nranks}{suffix}"
         if key not in s:
             return None, None
         e = s[key]
         src = (f"profiles/pmc_summary.json[{key}]: 2*FETCH_SIZE + WRITE_SIZE from separate rocprofv3 --pmc passes "
                f"of this workload (tag {e.get('tag', '?')}), not counted in this run")
-        return float(e["hbm_bytes_per_matvec"]), src
-    except (OSError, ValueError, KeyError):
+        return float(e.get("hbm_bytes_per_launch", e.get("hbm_bytes_per_matvec"))), src
+    except (OSError, ValueError, KeyError, TypeError):
         return None, None
+
+
+def exchange_text(world: int, flags: int, *, devices=None, poisson: bool = False, comm: str = "collective") -> str:
+    """What the per-iteration exchange ran as, from the context's reported
+    flags (cgx_info.flags: CGX_OVERLAP_ACTIVE, CGX_PULL_ACTIVE,
+    CGX_FOLDED_ACTIVE, CGX_HALO_PULL_ACTIVE, CGX_THREADS_ACTIVE,
+    CGX_HALO_OVERLAP_ACTIVE), not from what the defaults are meant to be."""
+    import conjugate_gradient_amd as cg
+    if world == 1:
+        return "none (single GPU)"
+    overlap = bool(flags & cg.CGX_OVERLAP_ACTIVE)
+    pull, folded = bool(flags & cg.CGX_PULL_ACTIVE), bool(flags & cg.CGX_FOLDED_ACTIVE)
+    if devices:
+        where = "one process, row blocks on devices " + ",".join(map(str, devices))
+        if poisson:
+            halo = ("r's halo rows read in place from the neighbouring slabs by k_poisson_p (halo pull)"
+                    if flags & cg.CGX_HALO_PULL_ACTIVE else
+                    "halo rows by peer copies" + (" beside k_poisson_p's interior"
+                                                  if flags & cg.CGX_HALO_OVERLAP_ACTIVE else ""))
+            scal = ("r.r and p.Ap summed in rank order inside k_poisson_p / k_poisson_xr (folded combines)" if folded
+                    else "scalars combined in rank order by a pull kernel per slab" if pull else
+                    "scalars by peer copies + a combine kernel per slab")
+            text = f"{where}: {halo} + {scal}"
+        elif comm == "p2p":
+            text = f"{where}: point-to-point_cg.c pattern, device copies through block 0"
+        else:
+            gather = ("p gathered by a pull kernel per block over peer access" if pull else
+                      "p gathered by a peer copy per block pair")
+            gather += " (overlapped with the own-block matVec)" if overlap else ""
+            scal = ("p.Ap and r.r summed in rank order inside k_update_r / k_update_xp (folded combines)" if folded
+                    else "scalars combined in rank order by a pull kernel per block" if pull else
+                    "scalars by peer copies + a combine kernel per block")
+            text = f"{where}: {gather} + {scal}"
+        return text + ("; one enqueuing host thread per block" if flags & cg.CGX_THREADS_ACTIVE else "")
+    if poisson:
+        return ("RCCL halo ncclSend/Recv" + (" beside k_poisson_p's interior" if flags & cg.CGX_HALO_OVERLAP_ACTIVE
+                                               else "") + " + 2x allreduce")
+    if comm == "p2p":
+        return "point-to-point_cg.c pattern: ncclSend/Recv via rank 0"
+    if comm == "deterministic":
+        return ("RCCL allgather(p)" + (" overlapped" if overlap else "")
+                + " + rank-ordered scalar combine (allgather of partials)")
+    return ("RCCL allgather(p) overlapped with own-block matVec + 2x allreduce" if overlap else
+            "RCCL allgather(p) + 2x allreduce")
 
 
 def cpu_baseline(n: int, iters: int = 5, threads_gen: int = 16) -> dict:
@@ -248,6 +294,36 @@ def cpu_baseline_poisson(m: int, iters: int = 3) -> dict:
     }
 
 
+def check_summary(rnorm: float, bnorm: float, rr_rec: float) -> dict:
+    """The true residual ||b - A x|| / ||b|| after the run, next to the CG
+    recurrence's sqrt(r.r) / ||b||: while the residual is well above
+    rounding the two agree (x and r updated consistently, at full size);
+    near convergence the recurrence goes on falling and they part."""
+    import math
+    rel_true = rnorm / bnorm
+    rel_rec = math.sqrt(max(rr_rec, 0.0)) / bnorm
+    out = {"relres": rel_true, "recurrence_relres": rel_rec}
+    if rel_true > 1e-8:
+        gap = abs(rel_true - rel_rec) / rel_true
+        out.update(recurrence_gap=gap, recurrence_agrees=gap <= 1e-6)
+    return out
+
+
+def poisson_oracle_check(m: int, iters: int, x_gpu) -> dict:
+    """configs[4] at full size against the oracle: the same fixed iteration
+    count of the fp64 matrix-free CG (oracle_cg_poisson_f64, the restatement
+    the tests pin) from x0 = 0, b = 1, on the host's cores (not timed, not a
+    baseline); x within 1e-9 (the Poisson tests' tolerance)."""
+    import numpy as np
+
+    import oracle
+    oracle.set_threads(16)
+    n = m * m
+    xo, _ = oracle.cg_poisson_f64(m, np.ones(n), np.zeros(n), max_iter=iters, eps=-1.0)
+    rel = float(np.linalg.norm(x_gpu - xo) / np.linalg.norm(xo))
+    return {"oracle_iterations": iters, "x_vs_oracle": rel, "x_vs_oracle_tol": 1e-9, "oracle_agrees": rel <= 1e-9}
+
+
 # The phases that tile an iteration on the compute stream (cgx.h CGX_PH_*):
 # their medians add up to about the iteration time.
 TILING_PHASES = ("matvec_own", "gather_exposed", "matvec", "combine_pap", "update_r", "combine_rr", "update_xp", "gap")
@@ -305,10 +381,11 @@ def rccl_summary(all_comm: list, solver_device: int) -> dict:
     }
 
 
-def local_summary(devices: list, peer_active: bool) -> dict:
+def local_summary(devices: list, peer_active: bool, flags: int = 0) -> dict:
     """The single-process multi-GPU run (cgx_create_multi): which devices hold
-    the row blocks, their PCI bus ids, and the link / peer access from the
-    first block's device to each other device."""
+    the row blocks, their PCI bus ids, the link / peer access from the first
+    block's device to each other device, and the context's reported flags
+    (cgx_info.flags: what the exchange ran as)."""
     import conjugate_gradient_amd as cg
     d0 = devices[0]
     return {
@@ -317,6 +394,7 @@ def local_summary(devices: list, peer_active: bool) -> dict:
         "distinct_devices": len(set(devices)),
         "pci_bus_ids": [cg.device_pci_bus_id(d) for d in devices],
         "peer_active": peer_active,
+        "flags": flags,
         "links_from_block0": [{"to_block": q, "link": "same device"} if d == d0 else
                               {"to_block": q, **cg.device_link(d0, d)} for q, d in enumerate(devices) if q],
     }
@@ -416,7 +494,7 @@ def main(argv=None) -> int:
     else:
         solver = cg.Solver(n, device=0, flags=flags, poisson_m=m)
     nloc = solver.info.nrows // len(devices or [0])
-    overlap_on = bool(solver.info.flags & cg.CGX_OVERLAP_ACTIVE)
+    ctx_flags = solver.info.flags
     overlap = solver.overlap_info() if world > 1 and not (poisson or stream or symmetric) else None
     fused = bool(solver.info.flags & cg.CGX_FUSED_ACTIVE)
     # fused Poisson: x every other (or third) iteration
@@ -446,6 +524,7 @@ def main(argv=None) -> int:
         dist.barrier()
     t0 = time.perf_counter()
     done, _ = solver.iterate(args.steps, eps=-1.0)
+    t_enq = time.perf_counter()  # fixed-count cgx_iterate returns once everything is enqueued
     solver.synchronize()
     cg.lib().cgx_dev_synchronize()
     t1 = time.perf_counter()
@@ -453,10 +532,12 @@ def main(argv=None) -> int:
         dist.barrier()
     assert done == args.steps
     elapsed = t1 - t0
+    enqueue_s = t_enq - t0
     st = solver.stats()
     mv_ms = st.matvec_ms / max(1, st.matvec_count)
     if dist:
         elapsed = max_over_ranks(dist, elapsed)
+        enqueue_s = max_over_ranks(dist, enqueue_s)
         mv_ms_max = max_over_ranks(dist, mv_ms)
     else:
         mv_ms_max = mv_ms
@@ -469,8 +550,12 @@ def main(argv=None) -> int:
     all_ph = gather_objects(dist, ph) if (dist and phases) else ([ph] if phases else None)
     all_comm = gather_objects(dist, comm) if comm is not None else None
 
-    # correctness after the timed region (not timed): true residual of x
+    # correctness after the timed region (not timed): the true residual of x,
+    # and the CG recurrence's r.r, which must agree with it while the
+    # residual is above rounding (x and r updated consistently at full size)
+    rr_rec = st.rr
     rnorm, bnorm = solver.residual_norm()
+    x_gpu = solver.get_x() if (poisson and world == 1 and not args.no_cpu and rank == 0) else None
     solver.close()
 
     if rank != 0:
@@ -519,8 +604,8 @@ def main(argv=None) -> int:
         # launches): the matVec's duration without the wait for p
         mv_kernel_ms = max(ph["matvec_busy"]["median_us"] for ph in all_ph) / 1e3
     achieved = (link_bytes if link_bound else bytes_launch) / ((mv_kernel_ms or mv_ms) * 1e-3) / 1e9
-    traffic, traffic_src = (None, None) if (stream or poisson) else pmc_traffic(n, world,
-                                                                               "_symmetric" if symmetric else "")
+    traffic, traffic_src = (None, None) if stream else pmc_traffic(
+        f"poisson_m{m}_g{world}" if poisson else f"n{n}_g{world}" + ("_symmetric" if symmetric else ""))
     peak = H2D_PEAK_GBS if link_bound else HBM_PEAK_GBS
     iters_per_s = args.steps / elapsed
     out = {
@@ -554,23 +639,12 @@ def main(argv=None) -> int:
             "n": n,
             "rows_per_gpu": nloc,
             "parallelism": f"rowblock{world}",
-            "exchange": ("none (single GPU)" if world == 1 else
-                         ("one process, row blocks on devices " + ",".join(map(str, devices)) +
-                          ": halo rows by peer copies + scalars combined by a pull kernel per block"
-                          if poisson else
-                          "one process, row blocks on devices " + ",".join(map(str, devices)) +
-                          ": p gathered by a pull kernel per block over peer access"
-                          + (" (overlapped with the own-block matVec)" if overlap_on else "")
-                          + " + scalars combined in rank order by a pull kernel per block")
-                         if devices else
-                         "RCCL halo ncclSend/Recv + 2x allreduce" if poisson else
-                         "point-to-point_cg.c pattern: ncclSend/Recv via rank 0" if args.comm == "p2p" else
-                         "RCCL allgather(p)" + (" overlapped" if overlap_on else "")
-                         + " + rank-ordered scalar combine (allgather of partials)"
-                         if args.comm == "deterministic" else
-                         "RCCL allgather(p) overlapped with own-block matVec + 2x allreduce"
-                         if overlap_on else "RCCL allgather(p) + 2x allreduce"),
+            "exchange": exchange_text(world, ctx_flags, devices=devices, poisson=poisson, comm=args.comm),
         },
+        # the host's side: time inside the fixed-count cgx_iterate call (it returns once the K
+        # iterations are enqueued; a full hardware queue makes it wait, so a value near ms_per_step
+        # means the device ran behind, one above it means the host bounds the loop); max over ranks
+        "host_enqueue_us_per_iteration": enqueue_s / args.steps * 1e6,
         "matvec_gbps": bytes_launch / (mv_ms * 1e-3) / 1e9,
         "matvec_ms": mv_ms,
         "matvec_ms_source": ("HIP events around the matVec launch(es) on rank 0's / block 0's stream (CGX_TIMING); "
@@ -596,7 +670,7 @@ def main(argv=None) -> int:
             "algorithmic_bytes_per_launch": bytes_launch,
             "link_bytes_per_launch": link_bytes if stream else None,
         },
-        "check": {"relres": rnorm / bnorm},
+        "check": check_summary(rnorm, bnorm, rr_rec),
         # algorithmic bytes of a whole iteration: 64 B/point fused (r, p_{k-1} -> p_k;
         # p_k, x, r -> x, r), 60 with x updated every other iteration (58.67 every
         # third), 80 B/point for the stencil / r / x,p split
@@ -611,9 +685,11 @@ def main(argv=None) -> int:
         out["rccl"] = rccl_summary(all_comm, solver_device=local_rank % max(1, cg.device_count()))
     if devices:
         out["config"]["row_blocks"] = len(devices)
-        out["multi_device"] = local_summary(devices, peer_flag)
+        out["multi_device"] = local_summary(devices, peer_flag, ctx_flags)
     if world == 1 and not args.no_cpu and poisson:
         out["cpu_baseline"] = cpu_baseline_poisson(m)
+        out["check"].update(poisson_oracle_check(m, args.warmup + args.steps, x_gpu))
+        del x_gpu
     elif world == 1 and not args.no_cpu and not stream and not symmetric:
         out["cpu_baseline"] = cpu_baseline(args.cpu_n or n)
         out["cpu_baseline_mt"] = cpu_baseline_mt(args.cpu_n or n)

@@ -32,7 +32,9 @@ import numpy as np
 
 __all__ = [
     "CGX_F64", "CGX_F32_REF", "CGX_TIMING", "CGX_HOST_STREAM", "CGX_NO_OVERLAP", "CGX_COMM_P2P", "CGX_SYMMETRIC",
-    "CGX_PHASES", "CGX_PEER_ACTIVE", "CGX_SMALL_ACTIVE", "CGX_FOLD_ACTIVE", "CGX_XDEFER_ACTIVE", "CGX_XDEFER3_ACTIVE", "PHASE_NAMES", "CgxError", "Stats",
+    "CGX_PHASES", "CGX_PEER_ACTIVE", "CGX_SMALL_ACTIVE", "CGX_FOLD_ACTIVE", "CGX_XDEFER_ACTIVE", "CGX_XDEFER3_ACTIVE",
+    "CGX_PULL_ACTIVE", "CGX_FOLDED_ACTIVE", "CGX_HALO_PULL_ACTIVE", "CGX_THREADS_ACTIVE", "CGX_HALO_OVERLAP_ACTIVE",
+    "PHASE_NAMES", "overlap_rule", "CgxError", "Stats",
     "Solver", "lib", "build",
     "device_pci_bus_id", "device_link",
     "conjugrad", "matVec", "vecVec", "residual", "update_xr", "update_p", "read_text",
@@ -55,6 +57,11 @@ CGX_SMALL_ACTIVE = 0x40000
 CGX_FOLD_ACTIVE = 0x80000
 CGX_XDEFER_ACTIVE = 0x100000
 CGX_XDEFER3_ACTIVE = 0x200000
+CGX_PULL_ACTIVE = 0x400000
+CGX_FOLDED_ACTIVE = 0x800000
+CGX_HALO_PULL_ACTIVE = 0x1000000
+CGX_THREADS_ACTIVE = 0x2000000
+CGX_HALO_OVERLAP_ACTIVE = 0x4000000
 
 # cgx_phase_times indices (include/cgx.h), in the order the phases tile an iteration
 PHASE_NAMES = ("matvec_own", "gather_exposed", "matvec", "combine_pap", "update_r", "combine_rr", "update_xp",
@@ -107,11 +114,18 @@ class CommInfo(ctypes.Structure):
 
 class OverlapInfo(ctypes.Structure):
     _fields_ = [("active", ctypes.c_int), ("decided_by", ctypes.c_int), ("allgather_us", ctypes.c_double),
-                ("split_us", ctypes.c_double), ("one_launch_us", ctypes.c_double), ("split_cost_us", ctypes.c_double)]
+                ("split_us", ctypes.c_double), ("one_launch_us", ctypes.c_double), ("split_cost_us", ctypes.c_double),
+                ("overlap_form_us", ctypes.c_double), ("plain_form_us", ctypes.c_double), ("margin", ctypes.c_double)]
 
 
 # cgx_overlap_info.decided_by
 OVERLAP_DECIDED_BY = {0: "measured", 1: "forced_on", 2: "off", 3: "n/a"}
+
+
+def overlap_rule(info: dict) -> bool:
+    """The library's decision rule on an overlap_info() dict (measured case):
+    the overlapped form when it beat the plain form by more than the margin."""
+    return info["overlap_form_us"] < (1.0 - info["margin"]) * info["plain_form_us"]
 
 
 class UniqueId(ctypes.Structure):
@@ -548,13 +562,17 @@ class Solver:
                 "device": ci.device, "pci_bus_id": ci.pci_bus_id.decode()}
 
     def overlap_info(self) -> dict:
-        """How the p exchange was chosen at creation (aligned row blocks): the
-        overlapped form when the measured allgather takes longer than the
-        matVec's split into two launches costs (cgx_get_overlap_info)."""
+        """How the p exchange was chosen at creation (aligned row blocks,
+        cgx_get_overlap_info): both whole forms, exchange + matVec, timed end
+        to end; the overlapped one runs when overlap_form_us < (1 - margin) *
+        plain_form_us.  The parts (allgather alone, the split, the one
+        launch) are reported too.  Values as the library decided on them (not
+        rounded); None where not measured."""
         o = OverlapInfo()
         _check(lib().cgx_get_overlap_info(self._h, ctypes.byref(o)), "cgx_get_overlap_info")
-        r = lambda v: None if v < 0 else round(v, 2)  # noqa: E731
+        r = lambda v: None if v < 0 else float(v)  # noqa: E731
         return {"on": bool(o.active), "decided_by": OVERLAP_DECIDED_BY.get(o.decided_by, str(o.decided_by)),
+                "overlap_form_us": r(o.overlap_form_us), "plain_form_us": r(o.plain_form_us), "margin": o.margin,
                 "allgather_us": r(o.allgather_us), "split_cost_us": r(o.split_cost_us), "split_us": r(o.split_us),
                 "one_launch_us": r(o.one_launch_us)}
 

@@ -145,6 +145,9 @@ namespace cgxh {
 
 constexpr int kScalSlots = 138;  // 16 ring slots, up to 112 gathered partials, 10 aux
 constexpr int kMaxShards = 32;
+// choose_overlap: the overlapped form runs when its measured time is below
+// (1 - kOverlapMargin) x the plain form's (cgx_overlap_info.margin)
+constexpr double kOverlapMargin = 0.01;
 constexpr int S_RR = 0, S_PAP = 4, S_LRR = 8, S_LPAP = 12, S_GATHER = 16;
 constexpr int S_TR = 128, S_TB = 129, S_LTR = 130, S_LTB = 131;  // true-residual check
 constexpr int S_XNZ = 134;  // rank mode: count of ranks whose x0 is not all zeros
@@ -235,9 +238,6 @@ struct Shard {
     // overlap of the p exchange with the own-column-block matVec
     hipStream_t cstream = nullptr;
     hipEvent_t ev_pready = nullptr, ev_gathered = nullptr;
-    // graph capture of LOCAL fixed-count iterations (cgx_iterate.hip local_graph_*):
-    // the fork from shard 0's stream, the joins back into it
-    hipEvent_t ev_fork = nullptr, ev_join = nullptr, ev_cjoin = nullptr;
 };
 
 }  // namespace cgxh
@@ -274,6 +274,8 @@ struct cgx_ctx {
     bool overlap = false;  // own-column-block matVec while p is exchanged
     // what choose_overlap measured (-1: not measured) and how it decided
     double ov_ag_us = -1.0, ov_split_us = -1.0, ov_one_us = -1.0, ov_cost_us = -1.0;
+    // ... and the two whole forms, exchange + matVec end to end (the decision)
+    double ov_form_us = -1.0, ov_plain_form_us = -1.0;
     int ov_how = CGX_OV_NA;
     bool fused = false;    // Poisson: two-kernel fused iteration (k_poisson_p + k_poisson_xr)
     bool fused_p = false;  // dense, one GPU, small n: two launches per iteration (matVec, k_update_xrp_f64)
@@ -332,13 +334,6 @@ struct cgx_ctx {
     // LOCAL mode: one host thread per row block enqueues its block's iteration
     // (cgx_local_mt.hip); null when not used
     cgxh::LocalPool *pool = nullptr;
-    // LOCAL mode, fixed-count iterations, every block on one device: graphs of
-    // lgraph_iters iterations, one per ring residue of the first iteration,
-    // captured once and replayed (cgx_iterate.hip); lgraph_off after a failed
-    // capture (the eager path then runs)
-    hipGraphExec_t lgraph[4] = {};
-    int lgraph_iters = 0;
-    bool lgraph_off = false;
     // CGX_PHASES: resolved per-iteration phase durations (us), cgx_phase_times' order;
     // the wall clock's rate, and the previous stamped iteration's first start /
     // last end (ticks; 0 = none) so the gap across a resolve is still measured
@@ -388,7 +383,6 @@ int finish_create(cgx_ctx *c, cgx_ctx **out);
 int timing_resolve(cgx_ctx *c);
 int phase_iter_begin(cgx_ctx *c);
 int64_t *ts_of(cgx_ctx *c, const Shard &s, int kern);
-void local_graph_reset(cgx_ctx *c);  // cgx_iterate.hip: drop the captured iteration graphs
 void phase_iter_end(cgx_ctx *c);
 int phase_resolve(cgx_ctx *c);
 int progress_mark(cgx_ctx *c);
@@ -400,7 +394,7 @@ int p2p_scalar(cgx_ctx *c, int lslot, int gslot);
 int exchange_allgather(cgx_ctx *c, bool from_x);
 int exchange_scalar(cgx_ctx *c, int lslot, int gslot);
 PeerSum peer_sum(const cgx_ctx *c, const Shard &d, int lslot, int gslot);
-int overlapped_matvec(cgx_ctx *c, int dot_slot, bool gated);
+int overlapped_matvec(cgx_ctx *c, int dot_slot, bool gated, bool timed = true);
 int overlap_matvecs(cgx_ctx *c, Shard &d, int dot_slot, bool gated, bool timed = true);
 int choose_overlap(cgx_ctx *c);
 int exchange_halo_async(cgx_ctx *c);

@@ -485,7 +485,7 @@ int overlap_matvecs(cgx_ctx *c, Shard &d, int dot_slot, bool gated, bool timed) 
 // Overlapped exchange + matVec (parallel_cg.c:290-293): p is allgathered on
 // each shard's exchange stream while the compute stream multiplies the
 // shard's own column block; overlap_matvecs does the rest.
-int overlapped_matvec(cgx_ctx *c, int dot_slot, bool gated) {
+int overlapped_matvec(cgx_ctx *c, int dot_slot, bool gated, bool timed) {
     const size_t es = (size_t)c->es;
     for (auto &s : c->sh) {
         TRY(set_dev(s));
@@ -511,7 +511,7 @@ int overlapped_matvec(cgx_ctx *c, int dot_slot, bool gated) {
     }
     for (auto &s : c->sh) {
         TRY(set_dev(s));
-        TRY(overlap_matvecs(c, s, dot_slot, gated));
+        TRY(overlap_matvecs(c, s, dot_slot, gated, timed));
     }
     return CGX_OK;
 }
@@ -522,12 +522,21 @@ int overlapped_matvec(cgx_ctx *c, int dot_slot, bool gated) {
 // the own-block launch but pays for splitting the matVec in two launches (a
 // second fill and drain: 15 / 20 / 23 us per iteration at 8 / 4 / 2 row blocks
 // of N = 65536, profiles/r05_rank_iteration.jsonl); the plain form exposes
-// the allgather.  So the context times both matVec forms on each of its row blocks
-// (zeros at this point: the same bytes move) and the allgather of p itself,
-// and overlaps only when the allgather takes longer than the split costs.  Rank mode: every rank measures and the maxima over ranks decide, so
-// the ranks agree (they would pair their collectives either way).
+// the allgather.  The exchange and the matVec also compete when they run
+// together (the allgather's kernel beside a matVec that holds every CU and
+// saturates HBM), which the parts timed alone cannot show.  So the context
+// times both WHOLE forms end to end on its own row blocks (zeros at this
+// point: the same bytes move) -- the real allgather (RCCL or the pull
+// kernels) with the matVec(s) after or beside it -- and overlaps only when
+// that form is faster by more than kOverlapMargin (a hysteresis: runs of the
+// same configuration do not flip between forms on noise).  The parts (the
+// split, the one launch, the allgather alone) are still timed and reported.
+// Rank mode: every rank measures and the maxima over ranks decide, so the
+// ranks agree (they would pair their collectives either way).
 // CGX_NO_OVERLAP / CGX_OVERLAP=0 and CGX_OVERLAP=1 / force override the
-// decision (the numbers are still measured and reported).
+// decision (the numbers are still measured and reported).  kOverlapMargin:
+// cgx_ctx.h.
+
 static int measure_split(cgx_ctx *c) {
     constexpr int kReps = 3;
     double split = 0.0, one = 0.0, cost = 0.0;
@@ -637,6 +646,85 @@ static int measure_allgather(cgx_ctx *c) {
     return rc;
 }
 
+// Both exchange + matVec forms end to end, as the iteration runs them:
+// plain = exchange_allgather then one rotated launch per block; overlap =
+// overlapped_matvec.  Each timed region holds kBack forms back to back (the
+// host runs ahead after the first, as in the iteration, and each form's
+// gather waits for every block's previous matVec, as the next iteration's
+// does); per pass the slowest block's average, best of kPasses, after one
+// warm-up of each.  Rank mode: a one-double allreduce right before each timed
+// region lines the ranks up on the device, so host skew between the ranks is
+// not timed.
+static int measure_forms(cgx_ctx *c) {
+    constexpr int kBack = 2, kPasses = 2;
+    const int S = (int)c->sh.size();
+    std::vector<hipEvent_t> ev(2 * S, nullptr);
+    auto one_form = [&](bool overlap) -> int {
+        if (overlap) return overlapped_matvec(c, S_TR, false, false);
+        TRY(exchange_allgather(c, false));
+        for (auto &s : c->sh) {
+            TRY(set_dev(s));
+            HIPT(matvec_f64_cols(s.plan, reinterpret_cast<const double *>(s.A), c->lda, s.nloc, c->lda, s.row0,
+                                 c->lda, false, reinterpret_cast<const double *>(s.pfull),
+                                 reinterpret_cast<double *>(s.Ap), reinterpret_cast<const double *>(s.pown),
+                                 reinterpret_cast<double *>(slot(s, S_TR)), s.ws, s.stream, nullptr, nullptr,
+                                 s.nloc));
+        }
+        return CGX_OK;
+    };
+    auto timed = [&](bool overlap, int reps, double *us) -> int {
+        TRY(sync_all(c));
+        if (c->mode == M_RCCL) {  // line the ranks up
+            Shard &s = c->sh[0];
+            TRY(set_dev(s));
+            NCCLC(c, ncclAllReduce(slot(s, S_GATHER), slot(s, S_GATHER), 1, ncclDouble, ncclMax, s.comm, s.stream),
+                  "ncclAllReduce(max), overlap calibration");
+        }
+        for (int q = 0; q < S; ++q) {
+            TRY(set_dev(c->sh[q]));
+            HIPT(hipEventRecord(ev[2 * q], c->sh[q].stream));
+        }
+        for (int r = 0; r < reps; ++r) TRY(one_form(overlap));
+        for (int q = 0; q < S; ++q) {
+            TRY(set_dev(c->sh[q]));
+            HIPT(hipEventRecord(ev[2 * q + 1], c->sh[q].stream));
+        }
+        TRY(sync_all(c));
+        double worst = 0.0;
+        for (int q = 0; q < S; ++q) {
+            float ms = 0.f;
+            HIPT(hipEventElapsedTime(&ms, ev[2 * q], ev[2 * q + 1]));
+            worst = std::max(worst, 1e3 * (double)ms / reps);
+        }
+        *us = worst;
+        return CGX_OK;
+    };
+    int rc = [&]() -> int {
+        for (int q = 0; q < S; ++q) {
+            TRY(set_dev(c->sh[q]));
+            HIPT(hipEventCreate(&ev[2 * q]));
+            HIPT(hipEventCreate(&ev[2 * q + 1]));
+        }
+        double t = 0.0, best_plain = 1e300, best_ov = 1e300;
+        TRY(timed(false, 1, &t));  // warm-up of each form
+        TRY(timed(true, 1, &t));
+        for (int pass = 0; pass < kPasses; ++pass) {
+            TRY(timed(false, kBack, &t));
+            best_plain = std::min(best_plain, t);
+            TRY(timed(true, kBack, &t));
+            best_ov = std::min(best_ov, t);
+        }
+        c->ov_plain_form_us = best_plain;
+        c->ov_form_us = best_ov;
+        return CGX_OK;
+    }();
+    for (auto e : ev)
+        if (e) (void)hipEventDestroy(e);
+    return rc;
+}
+
+constexpr int kOvNums = 6;  // the numbers choose_overlap takes the max over ranks of
+
 int choose_overlap(cgx_ctx *c) {
     if (p2p(c)) {  // point-to-point_cg.c's exchange: through rank 0, never overlapped
         c->overlap = false;
@@ -650,34 +738,34 @@ int choose_overlap(cgx_ctx *c) {
     if (c->mode == M_LOCAL || c->nranks > 1) {
         TRY(measure_split(c));
         TRY(measure_allgather(c));
+        TRY(measure_forms(c));
         if (c->mode == M_RCCL) {  // the maxima over ranks, on every rank
             Shard &s = c->sh[0];
             TRY(set_dev(s));
             double *h = s.h_pin;
-            h[0] = c->ov_ag_us;
-            h[1] = c->ov_split_us;
-            h[2] = c->ov_one_us;
-            h[3] = c->ov_cost_us;
-            HIPT(hipMemcpyAsync(slot(s, S_GATHER), h, 32, hipMemcpyHostToDevice, s.stream));
-            NCCLC(c, ncclAllReduce(slot(s, S_GATHER), slot(s, S_GATHER), 4, ncclDouble, ncclMax, s.comm, s.stream),
+            double *const v[kOvNums] = {&c->ov_ag_us, &c->ov_split_us, &c->ov_one_us, &c->ov_cost_us,
+                                        &c->ov_form_us, &c->ov_plain_form_us};
+            for (int i = 0; i < kOvNums; ++i) h[i] = *v[i];
+            HIPT(hipMemcpyAsync(slot(s, S_GATHER), h, 8 * kOvNums, hipMemcpyHostToDevice, s.stream));
+            NCCLC(c, ncclAllReduce(slot(s, S_GATHER), slot(s, S_GATHER), kOvNums, ncclDouble, ncclMax, s.comm,
+                                   s.stream),
                   "ncclAllReduce(max), overlap calibration");
-            HIPT(hipMemcpyAsync(h, slot(s, S_GATHER), 32, hipMemcpyDeviceToHost, s.stream));
+            HIPT(hipMemcpyAsync(h, slot(s, S_GATHER), 8 * kOvNums, hipMemcpyDeviceToHost, s.stream));
             TRY(rank_wait_stream(c, s.stream, "the overlap calibration"));
-            c->ov_ag_us = h[0];
-            c->ov_split_us = h[1];
-            c->ov_one_us = h[2];
-            c->ov_cost_us = h[3];
+            for (int i = 0; i < kOvNums; ++i) *v[i] = h[i];
         }
     }
     if (forced >= 0) {
         c->overlap = forced == 1;
         c->ov_how = forced ? CGX_OV_FORCED : CGX_OV_OFF;
     } else {
-        c->overlap = c->ov_ag_us > c->ov_cost_us;
+        c->overlap = c->ov_form_us < (1.0 - kOverlapMargin) * c->ov_plain_form_us;
         c->ov_how = CGX_OV_MEASURED;
     }
-    debug_log("overlap %s (allgather %.1f us, split %.1f us, one launch %.1f us, cost %.1f us, how %d)",
-              c->overlap ? "on" : "off", c->ov_ag_us, c->ov_split_us, c->ov_one_us, c->ov_cost_us, c->ov_how);
+    debug_log("overlap %s (overlap form %.1f us, plain form %.1f us; allgather %.1f us, split %.1f us, one launch "
+              "%.1f us, cost %.1f us; how %d)",
+              c->overlap ? "on" : "off", c->ov_form_us, c->ov_plain_form_us, c->ov_ag_us, c->ov_split_us,
+              c->ov_one_us, c->ov_cost_us, c->ov_how);
     return CGX_OK;
 }
 

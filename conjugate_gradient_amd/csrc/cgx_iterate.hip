@@ -388,7 +388,8 @@ int check_x_complete(const cgx_ctx *c) {
     if (!c->x_incomplete) return CGX_OK;
     if (c->x_deferred)
         return fail(CGX_ERR_STATE, "an earlier cgx_iterate failed with x updates still deferred (Poisson, x every "
-                                   "%d-th iteration): x is incomplete until the next cgx_solve_begin", c->xd);
+                                   "%d-th iteration): x is incomplete until cgx_set_x or the next cgx_solve_begin",
+                    c->xd);
     return fail(CGX_ERR_STATE, "an earlier cgx_iterate failed part-way through iteration %lld: x may hold part of it "
                                "and is incomplete until cgx_set_x or the next cgx_solve_begin", (long long)c->k);
 }
@@ -635,21 +636,6 @@ int do_iteration(cgx_ctx *c, double eps, int *stop, bool gated) {
     return CGX_OK;
 }
 
-// Drop the captured LOCAL iteration graphs (local_graph_iterate below).
-void local_graph_reset(cgx_ctx *c) {
-    bool any = false;
-    for (auto &g : c->lgraph) any = any || g;
-    if (!any) return;
-    if (!c->sh.empty()) {
-        (void)set_dev(c->sh[0]);
-        (void)hipStreamSynchronize(c->sh[0].stream);  // no replay still running
-    }
-    for (auto &g : c->lgraph) {
-        if (g) (void)hipGraphExecDestroy(g);
-        g = nullptr;
-    }
-}
-
 }  // namespace cgxh
 
 extern "C" {
@@ -711,6 +697,10 @@ static int iterate_gated(cgx_ctx *c, int64_t count, double eps, int64_t *done, i
         c->k = kdev;
         c->converged = 1;
         c->state = ST_CONVERGED;
+        // fused Poisson: the deciding k_poisson_p (iteration kdev) formed
+        // r.r_kdev from the slabs' partials into its slot before it decided,
+        // and the launches after it skip themselves: nothing is left unsummed
+        c->rr_unsummed = false;
     } else {
         double rr = 0.0;
         TRY(settle_rr(c));
@@ -753,136 +743,6 @@ int cgx_iterate(cgx_ctx *c, int64_t count, double eps, int64_t *done, int *conve
     return rc;
 }
 
-// ---- graph replay of the one-process multi-shard iteration (LOCAL) ---------------
-// Fixed-count iterations (eps < 0: nothing is read back or decided on the
-// host) enqueue the same launches, waits and records every iteration, with
-// arguments that depend on k only through ring(k).  One thread enqueuing S
-// row blocks pays 5S launches, 4S event records and ~3S^2 stream waits per
-// iteration (about 270 us at S = 8, profiles/r04_multishard_floor.jsonl).
-// Here G iterations (CGX_LOCAL_GRAPH_ITERS, default 8) are captured once per
-// ring residue of their first iteration into a hipGraph -- do_iteration's
-// own enqueues, so the results are bit for bit the eager path's -- and
-// replayed with one hipGraphLaunch.  Every block on one device (a capture
-// across devices is not attempted), no CGX_TIMING / CGX_PHASES (their
-// host-side bookkeeping is per iteration); CGX_LOCAL_GRAPH=0 turns it off,
-// =2 makes a failed capture an error instead of a quiet return to the eager
-// path (the tests use it, so a replay that never happens cannot pass).
-static bool local_graph_eligible(const cgx_ctx *c, double eps) {
-    if (eps >= 0.0 || c->lgraph_off || c->mode != M_LOCAL || c->sh.size() < 2 || c->pool) return false;
-    if (c->op != OP_DENSE || f32ref(c) || c->fused || c->fold_p || c->fused_p || c->ref_fused) return false;
-    if (!c->xchg_kernels || !c->fuse_combine) return false;  // the forms the bitwise tests replay
-    if (c->flags & (CGX_TIMING | CGX_PHASES | CGX_HOST_STREAM | CGX_SYMMETRIC | CGX_COMM_P2P)) return false;
-    for (const auto &s : c->sh)
-        if (s.dev != c->sh[0].dev) return false;
-    const char *e = std::getenv("CGX_LOCAL_GRAPH");
-    return !(e && *e == '0');
-}
-
-// Capture `iters` iterations from c->k into *out (nothing runs; c->k and the
-// counters are restored).
-static int local_graph_capture(cgx_ctx *c, int iters, hipGraphExec_t *out) {
-    Shard &s0 = c->sh[0];
-    // One stream: every block's streams are shard 0's stream while the
-    // iterations are captured, so the graph is the host's enqueue order as a
-    // chain -- a valid order, since a stream waits only on events already
-    // recorded.  The blocks share one device, whose kernels would contend for
-    // the same CUs anyway.  (Round 4 also captured the blocks' own streams,
-    // forked from and joined back into shard 0's; that capture re-records the
-    // same per-block events two or three times per iteration with
-    // O(blocks^2) cross-stream waits on them, and hipStreamEndCapture faulted
-    // in the host runtime at 4 blocks and more -- profiles/r04_local_graph.md.
-    // The form was removed in round 5: no setting reaches it.)
-    TRY(set_dev(s0));
-    const int64_t k0 = c->k, t0 = c->total_iters;
-    HIPT(hipStreamBeginCapture(s0.stream, hipStreamCaptureModeRelaxed));
-    std::vector<std::pair<hipStream_t, hipStream_t>> saved;
-    for (auto &s : c->sh) {
-        saved.push_back({s.stream, s.cstream});
-        s.stream = s0.stream;
-        if (s.cstream) s.cstream = s0.stream;
-    }
-    int rc = [&]() -> int {
-        for (int i = 0; i < iters; ++i) {
-            int stop = 0;
-            TRY(do_iteration(c, -1.0, &stop));
-        }
-        return CGX_OK;
-    }();
-    for (size_t i = 0; i < c->sh.size(); ++i) {
-        c->sh[i].stream = saved[i].first;
-        c->sh[i].cstream = saved[i].second;
-    }
-    c->k = k0;
-    c->total_iters = t0;
-    hipGraph_t g = nullptr;
-    (void)set_dev(s0);
-    const hipError_t ec = hipStreamEndCapture(s0.stream, &g);
-    if (rc == CGX_OK && ec != hipSuccess) rc = fail(CGX_ERR_HIP, "hipStreamEndCapture: %s", hipGetErrorString(ec));
-    if (rc == CGX_OK) {
-        const hipError_t ei = hipGraphInstantiate(out, g, nullptr, nullptr, 0);
-        if (ei != hipSuccess) {
-            *out = nullptr;
-            rc = fail(CGX_ERR_HIP, "hipGraphInstantiate: %s", hipGetErrorString(ei));
-        }
-    }
-    if (g) (void)hipGraphDestroy(g);
-    (void)hipGetLastError();
-    return rc;
-}
-
-// One replay on shard 0's stream, ordered after the work already queued on
-// every stream and before whatever is queued on them next.
-static int local_graph_launch(cgx_ctx *c, hipGraphExec_t ex) {
-    Shard &s0 = c->sh[0];
-    TRY(set_dev(s0));
-    for (auto &s : c->sh) {
-        if (&s != &s0) {
-            HIPT(hipEventRecord(s.ev_join, s.stream));
-            HIPT(hipStreamWaitEvent(s0.stream, s.ev_join, 0));
-        }
-        if (s.cstream) {
-            HIPT(hipEventRecord(s.ev_cjoin, s.cstream));
-            HIPT(hipStreamWaitEvent(s0.stream, s.ev_cjoin, 0));
-        }
-    }
-    HIPT(hipGraphLaunch(ex, s0.stream));
-    HIPT(hipEventRecord(s0.ev_fork, s0.stream));
-    for (auto &s : c->sh) {
-        if (&s != &s0) HIPT(hipStreamWaitEvent(s.stream, s0.ev_fork, 0));
-        if (s.cstream) HIPT(hipStreamWaitEvent(s.cstream, s0.ev_fork, 0));
-    }
-    return CGX_OK;
-}
-
-// As many whole graphs of fixed-count iterations as fit in `count`; returns
-// how many iterations ran that way (the caller runs the rest eagerly).
-static int local_graph_iterate(cgx_ctx *c, int64_t count, int64_t *did) {
-    *did = 0;
-    const char *ge = std::getenv("CGX_LOCAL_GRAPH_ITERS");
-    const int G = std::max(1, std::min(256, (ge && *ge) ? std::atoi(ge) : 8));
-    if (G != c->lgraph_iters) {
-        local_graph_reset(c);
-        c->lgraph_iters = G;
-    }
-    while (count - *did >= G && c->state == ST_BEGUN) {
-        hipGraphExec_t &ex = c->lgraph[ring(c->k)];
-        if (!ex) {
-            const int rc = local_graph_capture(c, G, &ex);
-            if (rc != CGX_OK) {
-                const char *e = std::getenv("CGX_LOCAL_GRAPH");
-                if (e && *e == '2') return rc;  // strict (the tests): a capture that fails is an error
-                c->lgraph_off = true;           // else the eager path runs from here on
-                return CGX_OK;
-            }
-        }
-        TRY(local_graph_launch(c, ex));
-        c->k += G;
-        c->total_iters += G;
-        *did += G;
-    }
-    return CGX_OK;
-}
-
 static int iterate_calls(cgx_ctx *c, int64_t count, double eps, int64_t *done, int *converged) {
     const char *gv = std::getenv("CGX_GATED");
     const bool gate_ok = !(gv && *gv == '0');
@@ -890,7 +750,6 @@ static int iterate_calls(cgx_ctx *c, int64_t count, double eps, int64_t *done, i
     if (c->state == ST_BEGUN && count > 0 && eps >= 0.0 && !(c->flags & CGX_HOST_STREAM) && gate_ok)
         return iterate_gated(c, count, eps, done, converged);
     int64_t did = 0;
-    if (c->state == ST_BEGUN && local_graph_eligible(c, eps)) TRY(local_graph_iterate(c, count, &did));
     while (did < count && c->state == ST_BEGUN) {
         int stop = 0;
         TRY(do_iteration(c, eps, &stop));
@@ -935,6 +794,9 @@ int cgx_get_stats(cgx_ctx *c, cgx_stats *st) {
     TRY(timing_resolve(c));
     st->iterations = c->k;
     st->converged = c->converged;
+    // fixed-count iterations read nothing back: the current r.r from its slot
+    // (iterate_calls settled a folded Poisson r.r already)
+    if (c->state == ST_BEGUN && c->k > 0 && !c->rr_unsummed) TRY(read_scalar(c, S_RR + ring(c->k), &c->last_rr));
     st->rr = c->last_rr;
     st->solve_ms = c->solve_ms;
     st->matvec_ms = c->matvec_ms;
@@ -1010,7 +872,6 @@ int cgx_set_matvec_plan(cgx_ctx *c, int rows_per_wave, int chunks_in_flight, int
         s.fold_plan = pl;  // the folded matVec follows the same rows per wave and grid (same p.Ap order)
     }
     if (R > 2) c->fold_p = false;  // the folded matVec has one or two rows per wave
-    local_graph_reset(c);          // the captured iterations launch the old plan's kernels
     return CGX_OK;
 }
 

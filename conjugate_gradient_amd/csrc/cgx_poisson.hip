@@ -364,13 +364,16 @@ __global__ __launch_bounds__(kNT) void k_poisson_p_f64(const double *__restrict_
     static_assert(RB <= kEdgeRB, "edge buffer");
     constexpr bool PULL = std::is_same<PA, PullArgs>::value;
     __shared__ double edge[2 * kWaves * 2 * kEdgeRB];
+    // a launch after the stop returns before it reads anything (the slabs'
+    // r.r partials included, which the folded combine would read over xGMI and
+    // store again)
+    if (cv.kdone && *cv.kdone != 0) return;
     double rrk = 0.0;  // r.r_k (not read when first)
     if (!first) {
         if constexpr (PULL) rrk = pa.rr_sum.cnt ? peer_sum_wave(pa.rr_sum) : *rr;
         else rrk = *rr;
     }
     if (cv.kdone) {
-        if (*cv.kdone != 0) return;
         if (!first && cv.eps >= 0.0 && sqrt(rrk) < cv.eps) {  // the same decision in every block
             if (blockIdx.x == 0 && threadIdx.x == 0) record_convergence(cv, cv.k, rrk);
             return;

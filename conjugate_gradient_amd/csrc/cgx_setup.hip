@@ -30,9 +30,6 @@ int alloc_shard(cgx_ctx *c, Shard &s) {
     HIPT(hipStreamCreateWithFlags(&s.stream, hipStreamNonBlocking));
     HIPT(hipEventCreateWithFlags(&s.ev_sync, hipEventDisableTiming));
     HIPT(hipEventCreateWithFlags(&s.ev_sync2, hipEventDisableTiming));
-    HIPT(hipEventCreateWithFlags(&s.ev_fork, hipEventDisableTiming));
-    HIPT(hipEventCreateWithFlags(&s.ev_join, hipEventDisableTiming));
-    HIPT(hipEventCreateWithFlags(&s.ev_cjoin, hipEventDisableTiming));
     HIPT(hipEventCreateWithFlags(&s.ev_root, hipEventDisableTiming));
     if (!s.ev_pready) HIPT(hipEventCreateWithFlags(&s.ev_pready, hipEventDisableTiming));
     const size_t abytes = (size_t)s.nloc * (size_t)c->lda * es;
@@ -235,8 +232,6 @@ void free_shard(Shard &s) {
         if (e) (void)hipEventDestroy(e);
     if (s.ev_sync) (void)hipEventDestroy(s.ev_sync);
     if (s.ev_sync2) (void)hipEventDestroy(s.ev_sync2);
-    for (hipEvent_t e : {s.ev_fork, s.ev_join, s.ev_cjoin})
-        if (e) (void)hipEventDestroy(e);
     if (s.ev_root) (void)hipEventDestroy(s.ev_root);
     for (int q = 0; q < kMaxCopyStreams; ++q)
         if (s.copy[q]) {
@@ -678,7 +673,6 @@ int cgx_destroy(cgx_ctx *ctx) {
     // aborted here instead of hanging in the stream syncs below
     const int rc = (ctx->mode == M_RCCL && !ctx->dead) ? sync_all(ctx) : CGX_OK;
     local_mt_stop(ctx);
-    local_graph_reset(ctx);
     for (auto &s : ctx->sh) free_shard(s);
     delete ctx;
     return rc;
@@ -698,7 +692,10 @@ int cgx_get_info(const cgx_ctx *c, cgx_info *info) {
                   ((c->fused || c->fused_p || c->ref_fused) ? CGX_FUSED_ACTIVE : 0) | (c->peer ? CGX_PEER_ACTIVE : 0) |
                   (c->sh[0].plan.small ? CGX_SMALL_ACTIVE : 0) | (c->fold_p ? CGX_FOLD_ACTIVE : 0) |
                   (c->xdefer ? CGX_XDEFER_ACTIVE : 0) |
-                  (c->xd == 3 ? CGX_XDEFER3_ACTIVE : 0);
+                  (c->xd == 3 ? CGX_XDEFER3_ACTIVE : 0) |
+                  ((c->mode == M_LOCAL && c->xchg_kernels) ? CGX_PULL_ACTIVE : 0) |
+                  (c->fuse_combine ? CGX_FOLDED_ACTIVE : 0) | (c->halo_pull ? CGX_HALO_PULL_ACTIVE : 0) |
+                  (c->pool ? CGX_THREADS_ACTIVE : 0) | (c->halo_overlap ? CGX_HALO_OVERLAP_ACTIVE : 0);
     info->elem_bytes = c->es;
     return CGX_OK;
 }
@@ -711,6 +708,9 @@ int cgx_get_overlap_info(const cgx_ctx *c, cgx_overlap_info *info) {
     info->split_us = c->ov_split_us;
     info->one_launch_us = c->ov_one_us;
     info->split_cost_us = c->ov_cost_us;
+    info->overlap_form_us = c->ov_form_us;
+    info->plain_form_us = c->ov_plain_form_us;
+    info->margin = kOverlapMargin;
     return CGX_OK;
 }
 

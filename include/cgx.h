@@ -57,7 +57,7 @@
 extern "C" {
 #endif
 
-#define CGX_VERSION 100 /* 0.1.0 */
+#define CGX_VERSION 101 /* 0.1.1: cgx_overlap_info gained the end-to-end form times */
 
 /* ---- status codes (0 = OK, negative = error) --------------------------- */
 #define CGX_OK            0
@@ -152,6 +152,25 @@ extern "C" {
                                     CGX_XDEFER_ACTIVE: every third iteration
                                     (the default, a third p slab;
                                     CGX_POISSON_XDEFER=2: every other) */
+/* Reported in cgx_info.flags: how a context with several row blocks
+ * exchanges, so a caller (bench.py) can say what ran. */
+#define CGX_PULL_ACTIVE   0x400000 /* one process: the exchange runs as pull
+                                    kernels on each consuming block's stream
+                                    (else one hipMemcpyPeerAsync per block pair,
+                                    CGX_LOCAL_XCHG=copy) */
+#define CGX_FOLDED_ACTIVE 0x800000 /* one process, fp64: both scalar combines
+                                    summed in rank order by the kernels that
+                                    consume them (else a combine kernel per
+                                    block and scalar, CGX_LOCAL_FUSE=0) */
+#define CGX_HALO_PULL_ACTIVE 0x1000000 /* one process, fused Poisson: r's halo
+                                    rows read in place from the neighbouring
+                                    slabs by k_poisson_p (no halo copies) */
+#define CGX_THREADS_ACTIVE 0x2000000 /* one process: one host thread per row
+                                    block enqueues its work (CGX_LOCAL_THREADS=1) */
+#define CGX_HALO_OVERLAP_ACTIVE 0x4000000 /* fused Poisson over slabs in rank
+                                    mode (or copies): r's halo exchange runs on
+                                    the comm stream beside k_poisson_p's
+                                    interior (CGX_HALO_OVERLAP=0: before it) */
 
 typedef struct cgx_ctx cgx_ctx;
 
@@ -190,14 +209,14 @@ typedef struct {
  * + COMBINE_PAP + UPDATE_R + COMBINE_RR + UPDATE_XP + GAP = ITERATION. */
 #define CGX_PH_MATVEC_OWN     0 /* overlap: own-column-block matVec (p local)   */
 #define CGX_PH_GATHER_EXPOSED 1 /* the compute stream waiting for p's allgather
-                                   (overlap: after its own block, until the rest
-                                   launch on the exchange stream -- which runs
-                                   right after the allgather, beside the own
-                                   block -- has finished; otherwise the whole
-                                   allgather, launch gap included)
-                                   parallel_cg.c:290-291                        */
-#define CGX_PH_MATVEC         2 /* the matVec with p.Ap (overlap: the kernel
-                                   adding the two row sums, with p.Ap) :292-293 */
+                                   (overlap: from the end of the own-block
+                                   launch to the start of the rest launch,
+                                   which waits for the allgather on the same
+                                   stream; otherwise the whole allgather,
+                                   launch gap included) parallel_cg.c:290-291 */
+#define CGX_PH_MATVEC         2 /* the matVec with p.Ap (overlap: the rest
+                                   launch, accumulating onto the own block's
+                                   row sums, with p.Ap)               :292-293 */
 #define CGX_PH_COMBINE_PAP    3 /* MPI_Allreduce(p.Ap) counterpart        :294   */
 #define CGX_PH_UPDATE_R       4 /* r -= alpha Ap, r.r                     :304-309 */
 #define CGX_PH_COMBINE_RR     5 /* MPI_Allreduce(r.r) counterpart         :313   */
@@ -207,9 +226,9 @@ typedef struct {
 #define CGX_PH_ITERATION      8 /* start of an iteration to the start of the next */
 #define CGX_PH_MATVEC_BUSY    9 /* not a tile: the time the iteration's matVec
                                    kernels ran, the union of their spans (with
-                                   the overlap: the own-block launch, the rest
-                                   launch on the exchange stream, the add) --
-                                   the matVec's duration without the wait for p */
+                                   the overlap: the own-block launch and the
+                                   rest launch) -- the matVec's duration
+                                   without the wait for p */
 #define CGX_PH_COUNT         10
 typedef struct {
     int64_t samples[CGX_PH_COUNT];
@@ -231,12 +250,15 @@ typedef struct {
 
 /* How the p exchange of an aligned multi-shard dense fp64 context was chosen
  * (parallel_cg.c:290-293: allgather p, then the matVec).  At creation the
- * context times, on its own row blocks, the matVec split in two launches
- * (own column block, then the rest) against the one launch, and the
- * allgather of p (RCCL in rank mode, the pull kernels in one process); in
- * rank mode the maxima over ranks, so every rank decides alike.  The
- * overlapped form runs when the allgather takes longer than the split costs.
- * Times in microseconds, -1 when not measured. */
+ * context times both whole forms end to end on its own row blocks: overlap =
+ * the real allgather (RCCL in rank mode, the pull kernels in one process) in
+ * flight beside the own-column-block launch, then the rest launch; plain =
+ * the allgather, then one launch over the whole row block.  The overlapped
+ * form runs when overlap_form_us < (1 - margin) * plain_form_us.  In rank
+ * mode every number is the max over ranks, so every rank decides alike.  The
+ * parts are timed too and reported: the matVec split in two launches against
+ * the one launch, and the allgather alone.  Times in microseconds, -1 when
+ * not measured. */
 #define CGX_OV_MEASURED 0 /* chosen from the measurement                     */
 #define CGX_OV_FORCED   1 /* CGX_OVERLAP=1 / force: on                       */
 #define CGX_OV_OFF      2 /* CGX_NO_OVERLAP or CGX_OVERLAP=0: off            */
@@ -249,6 +271,11 @@ typedef struct {
     double split_us;       /* own-block launch + rest launch                */
     double one_launch_us;  /* the one launch over the whole row block       */
     double split_cost_us;  /* split_us - one_launch_us (max over blocks)    */
+    double overlap_form_us; /* the overlapped form, allgather included (the
+                               slowest block, best of 2 passes of 2 forms
+                               back to back)                                 */
+    double plain_form_us;  /* the plain form: allgather, then one launch     */
+    double margin;         /* the hysteresis of the decision (0.01)          */
 } cgx_overlap_info;
 
 /* ---- errors / info ------------------------------------------------------- */
@@ -276,10 +303,7 @@ int cgx_create(cgx_ctx **ctx, int64_t n, int device, int flags);
  * may repeat: several row blocks on one GPU).  Exchange by pull kernels on
  * each consuming block's stream: one gather of p (k_gather_slices), one
  * rank-order combine per scalar (k_combine_peers); CGX_LOCAL_XCHG=copy:
- * one hipMemcpyPeerAsync per block pair instead (the same bits).  With every
- * block on one device, fixed-count cgx_iterate calls replay G = 8 captured
- * iterations per hipGraphLaunch (CGX_LOCAL_GRAPH=0 off, CGX_LOCAL_GRAPH_ITERS
- * = G; the same bits; not with CGX_TIMING / CGX_PHASES). */
+ * one hipMemcpyPeerAsync per block pair instead (the same bits). */
 int cgx_create_multi(cgx_ctx **ctx, int64_t n, int nshards, const int *devices, int flags);
 
 /* One process per GPU (parallel_cg.c's one MPI rank per process): this

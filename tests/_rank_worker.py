@@ -46,9 +46,12 @@ def main():
     res = {"rank": rank}
     if mode in ("peer_dies", "peer_absent", "poisson_peer_dies"):
         return fail_fast(mode, n, P, rank, uid, out)
+    # one GPU per rank where the box has them (tests/test_gpu_multidevice.py), else all on device 0
+    dev = rank if os.environ.get("CGX_TEST_RANK_DEVICE") == "rank" else 0
     if mode.startswith("poisson"):
         m = n
-        with cg.Solver(None, poisson_m=m, rank=rank, nranks=P, unique_id=uid, device=0) as s:
+        with cg.Solver(None, poisson_m=m, rank=rank, nranks=P, unique_id=uid, device=dev) as s:
+            res["comm"] = s.comm_info()
             s.fill(1.0, 0.0)
             eps = 1e-8 if mode == "poisson_eps" else -1.0
             x, st = s.solve(None, eps=eps, max_iter=-1 if eps > 0 else 120)
@@ -70,8 +73,6 @@ def main():
             A, b, x0 = case(f"spd{n}", np.float32 if f32 else np.float64)
         if mode in ("overlap_on", "det_overlap"):  # the overlapped form whatever the measurement says
             os.environ["CGX_OVERLAP"] = "1"
-        # one GPU per rank where the box has them (tests/test_gpu_multidevice.py), else all on device 0
-        dev = rank if os.environ.get("CGX_TEST_RANK_DEVICE") == "rank" else 0
         with cg.Solver(n, rank=rank, nranks=P, unique_id=uid, device=dev, flags=flags) as s:
             res["comm"] = s.comm_info()
             res["overlap"] = bool(s.info.flags & cg.CGX_OVERLAP_ACTIVE)

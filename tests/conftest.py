@@ -14,8 +14,21 @@ if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
 
+# Collected after every other test: the paths only a node with several GPUs
+# executes (distinct devices, xGMI).  A failure there under `pytest -x` must
+# not keep the full-size configuration tests of the other files from running.
+LAST_MODULES = ("test_gpu_multidevice.py",)
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X GPU (libcgx kernels run)")
+
+
+def pytest_collection_modifyitems(config, items):
+    last = [it for it in items if os.path.basename(str(it.fspath)) in LAST_MODULES]
+    if last:
+        keep = [it for it in items if os.path.basename(str(it.fspath)) not in LAST_MODULES]
+        items[:] = keep + last
 
 
 @pytest.fixture(scope="session")

@@ -102,7 +102,7 @@ def test_gfx950_code_object(built):
 
 def test_errors_and_version(built):
     L = cg.lib()
-    assert L.cgx_version() == 100
+    assert L.cgx_version() == 101
     assert L.cgx_strerror(0) == b"ok"
     for code in (-1, -2, -3, -4, -5, -6, -7):
         assert L.cgx_strerror(code) not in (b"ok", b"unknown error")

@@ -70,13 +70,13 @@ def test_traffic_lookup_names_its_source():
     """roofline.traffic is the committed PMC figure for the same workload
     (rocprofv3 cannot run inside the bench process): the bench reports where
     it came from, and null where no pass exists (e.g. N=4096)."""
-    t, src = bench.pmc_traffic(65536, 1)
+    t, src = bench.pmc_traffic("n65536_g1")
     assert t is not None and 1.0 <= t / bench.matvec_bytes(65536, 65536) < 1.01
     assert "pmc_summary.json[n65536_g1]" in src and "FETCH_SIZE" in src
     for g in (2, 4, 8):
-        t, src = bench.pmc_traffic(65536, g)
+        t, src = bench.pmc_traffic(f"n65536_g{g}")
         assert t is not None and 1.0 <= t / bench.matvec_bytes(65536, 65536 // g) < 1.01, g
-    assert bench.pmc_traffic(4096, 1) == (None, None)
+    assert bench.pmc_traffic("n4096_g1") == (None, None)
 
 
 def _phases(scale):

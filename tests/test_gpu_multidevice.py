@@ -2,7 +2,10 @@
 
 Everything else in the suite puts every row block (or rank) on device 0.
 These tests run where two or more GPUs are visible -- the driver's 8-GPU
-node -- and are skipped with the reason otherwise:
+node -- and are skipped with the reason otherwise.  tests/conftest.py
+collects this file last, so under `pytest -x` a failure on a topology no
+earlier round has run cannot keep the full-size configuration tests of the
+other files from running.
 
   * cgx_create_multi over devices 0..G-1 (G = min(8, visible)): the pull
     kernels read the other devices' p slices and scalar partials over xGMI
@@ -11,9 +14,19 @@ node -- and are skipped with the reason otherwise:
     and separate scalar combines; the per-pair peer copies.  Each must give
     x bit for bit equal to the same partition on one device ([0] * G),
     overlapped and plain, gated and fixed-count.
+  * configs[2] at its stated size (N = 65536) over G distinct GPUs, in one
+    process and with one process per GPU: within 1e-10 of the fp64 oracle
+    with conjgrad.m's loop count.
+  * CGX_F32_REF over distinct devices, collective and p2p: bit for bit the
+    unmodified parallel_cg.c / point-to-point_cg.c under mpiexec -np G
+    (tests/golden/mpi/; parallel_cg.c:288-324, point-to-point_cg.c:444-473).
+  * Poisson slabs over distinct devices (the halo pull and the folded
+    PeerSum combines over xGMI): bitwise against [0] * G and against the
+    oracle; and a Poisson rank run with one process per GPU.
   * the rank path with one process per GPU (parallel_cg.c's one MPI rank per
-    process, :109-117 and :288-324): RCCL over xGMI between distinct devices,
-    x within 1e-10 of the fp64 oracle with conjgrad.m's loop count.
+    process, :109-117 and :288-324): RCCL over xGMI between distinct devices.
+  * bench.py --gpus G without a launcher, the one-process line a SCALE run
+    would print.
 """
 import json
 import os
@@ -25,6 +38,7 @@ import pytest
 
 import conjugate_gradient_amd as cg
 import oracle
+from _cases import case, golden_mpi, hash_oracle, mpi_golden_x
 
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
@@ -35,15 +49,22 @@ def rel(a, b):
     return float(np.linalg.norm(a - b) / np.linalg.norm(b))
 
 
-def gpus() -> int:
-    return min(8, cg.device_count())
-
-
 def visible() -> int:
     try:
         return cg.device_count()
     except cg.CgxError:
         return 0
+
+
+def gpus() -> int:
+    return min(8, visible())
+
+
+def gpus_pow2() -> int:
+    """The largest of 2 / 4 / 8 that the visible GPUs allow: the MPI goldens
+    exist for np = 2, 4, 8, and N = 65536 splits evenly over them."""
+    g = gpus()
+    return 8 if g >= 8 else 4 if g >= 4 else 2
 
 
 needs_two = pytest.mark.skipif("visible() < 2",
@@ -71,52 +92,22 @@ def solve_multi(monkeypatch, n, devices, form, overlap):
     return flags, xg, st.iterations, xf, rn / bn
 
 
-@needs_two
-@pytest.mark.parametrize("overlap", [True, False])
-@pytest.mark.parametrize("form", ["kernel", "threads", "nofuse", "copy"])
-def test_distinct_devices_bitwise_equal_one_device(monkeypatch, form, overlap):
-    G = gpus()
-    n = 1024 * G  # 1024-row blocks: aligned, so both exchange forms apply
-    ref = solve_multi(monkeypatch, n, [0] * G, "kernel", overlap)
-    got = solve_multi(monkeypatch, n, list(range(G)), form, overlap)
-    assert got[0] & cg.CGX_PEER_ACTIVE and bool(got[0] & cg.CGX_OVERLAP_ACTIVE) == overlap
-    assert got[2] == ref[2], (got[2], ref[2])
-    assert np.array_equal(got[1], ref[1]) and np.array_equal(got[3], ref[3])
-    assert got[4] == ref[4] and got[4] <= TOL
-
-
-@needs_two
-def test_distinct_devices_measured_choice_matches_oracle():
-    """The default (measured) exchange form across distinct devices, against
-    the fp64 oracle on a MATLAB-generated system."""
-    G = gpus()
-    n = 1024 * G
-    A, b = oracle.spd_matlab(n, np.float64)
-    x = np.zeros(n)
-    st = cg.conjugrad(A, b, x, eps=1e-10, shards=list(range(G)))
-    xo, so = oracle.cg_f64(A, b, np.zeros(n), eps=1e-10)
-    assert st.iterations == so.iterations and rel(x, xo) <= TOL
-
-
-@needs_two
-@pytest.mark.timeout(300)
-def test_rank_path_one_process_per_gpu(tmp_path):
-    """torchrun's placement: world = min(8, visible) rank processes, rank r on
-    device r, RCCL over xGMI (no NCCL_HOSTID: RCCL sees one host)."""
-    G = gpus()
-    n = 1024 * G
-    uidfile, out = str(tmp_path / "uid.bin"), str(tmp_path / "sized")
+def run_ranks_per_gpu(tmp_path, mode, n, G, timeout=240):
+    """torchrun's placement: G rank processes, rank r on device r, RCCL over
+    xGMI (no NCCL_HOSTID: RCCL sees one host).  Returns (x of rank 0, every
+    rank's result dict); every rank must end with the same x."""
+    uidfile, out = str(tmp_path / "uid.bin"), str(tmp_path / mode)
     procs = []
     for r in range(G):
         env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", CGX_TEST_RANK_DEVICE="rank")
         env.pop("NCCL_HOSTID", None)
-        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "_rank_worker.py"), "sized", str(n), str(G),
+        procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "_rank_worker.py"), mode, str(n), str(G),
                                        str(r), uidfile, out], env=env, stdout=subprocess.PIPE,
                                       stderr=subprocess.STDOUT, text=True))
     logs = []
     try:
         for p in procs:
-            logs.append(p.communicate(timeout=240)[0])
+            logs.append(p.communicate(timeout=timeout)[0])
     finally:
         for p in procs:
             if p.poll() is None:
@@ -126,11 +117,221 @@ def test_rank_path_one_process_per_gpu(tmp_path):
         assert p.returncode == 0, f"rank {r} exited {p.returncode}:\n{logs[r][-3000:]}"
     res = [json.load(open(out + f"_r{r}.json")) for r in range(G)]
     xs = [np.load(out + f"_x{r}.npy") for r in range(G)]
-    assert sorted(r["comm"]["rccl_device"] for r in res) == list(range(G))
+    assert sorted(r["comm"]["device"] for r in res) == list(range(G))
     for r in range(1, G):
         assert np.array_equal(xs[r], xs[0]) and res[r]["iterations"] == res[0]["iterations"]
-    assert res[0]["overlap_info"]["decided_by"] == "measured"
+    return xs[0], res
+
+
+# ---- one process, dense ----------------------------------------------------------
+@needs_two
+@pytest.mark.parametrize("overlap", [True, False])
+@pytest.mark.parametrize("form", ["kernel", "threads", "nofuse", "copy"])
+def test_distinct_devices_bitwise_equal_one_device(monkeypatch, form, overlap):
+    G = gpus()
+    n = 1024 * G  # 1024-row blocks: aligned, so both exchange forms apply
+    ref = solve_multi(monkeypatch, n, [0] * G, "kernel", overlap)
+    got = solve_multi(monkeypatch, n, list(range(G)), form, overlap)
+    assert got[0] & cg.CGX_PEER_ACTIVE and bool(got[0] & cg.CGX_OVERLAP_ACTIVE) == overlap
+    assert bool(got[0] & cg.CGX_THREADS_ACTIVE) == (form == "threads")
+    assert bool(got[0] & cg.CGX_PULL_ACTIVE) == (form != "copy")
+    assert got[2] == ref[2], (got[2], ref[2])
+    assert np.array_equal(got[1], ref[1]) and np.array_equal(got[3], ref[3])
+    assert got[4] == ref[4] and got[4] <= TOL
+
+
+@needs_two
+def test_create_multi_distinct_devices_peer_access():
+    """cgx_create_multi over devices 0 and 1 enables peer access after
+    hipDeviceCanAccessPeer and leaves no HIP error pending; without peer
+    access it is refused by name, never a silent host-staged copy."""
+    L = cg.lib()
+    link = cg.device_link(0, 1)
+    if link["peer_access"]:
+        with cg.Solver(1024, devices=[0, 1]) as s:
+            assert L.cgx_hip_last_error() == 0 and s.info.flags & cg.CGX_PEER_ACTIVE
+    else:
+        with pytest.raises(cg.CgxError, match="cannot access"):
+            cg.Solver(1024, devices=[0, 1])
+
+
+@needs_two
+def test_distinct_devices_measured_choice_matches_oracle():
+    """The default (measured) exchange form across distinct devices, against
+    the fp64 oracle on a MATLAB-generated system; the decision follows the
+    rule on the two forms timed end to end."""
+    G = gpus()
+    n = 1024 * G
+    A, b = oracle.spd_matlab(n, np.float64)
+    with cg.Solver(n, devices=list(range(G))) as s:
+        info = s.overlap_info()
+        assert info["decided_by"] == "measured" and info["on"] == cg.overlap_rule(info)
+        s.set_system(A, b)
+        x, st = s.solve(None, eps=1e-10)
+    xo, so = oracle.cg_f64(A, b, np.zeros(n), eps=1e-10)
+    assert st.iterations == so.iterations and rel(x, xo) <= TOL
+
+
+@needs_two
+@pytest.mark.timeout(900)
+def test_headline_n65536_distinct_devices_one_process():
+    """configs[2] at its stated size over G distinct GPUs from one process
+    (cgx_create_multi: 65536/G rows x 65536 of A per GPU, p gathered by pull
+    kernels over xGMI in the measured form), generated on the devices,
+    converged at eps 1e-10: loop count == conjgrad.m's, x within 1e-10 of the
+    fp64 oracle, true residual <= 1e-10 ||b||."""
+    n, G = 65536, gpus_pow2()
+    with cg.Solver(n, devices=list(range(G))) as s:
+        assert s.info.flags & cg.CGX_PEER_ACTIVE and s.overlap_info()["decided_by"] == "measured"
+        s.generate_spd(42)
+        x, st = s.solve(None, eps=1e-10)
+        rn, bn = s.residual_norm()
+    xo, so = hash_oracle(n)
+    assert st.converged and st.iterations == so.iterations
+    assert rel(x, xo) <= TOL and rn <= TOL * bn
+
+
+@needs_two
+@pytest.mark.parametrize("program", ["parallel", "p2p"])
+def test_f32ref_distinct_devices_bitwise_vs_mpi_reference(program):
+    """CGX_F32_REF over G distinct GPUs in one process == the unmodified
+    parallel_cg.c (MPICH's MPI_Allreduce order) / point-to-point_cg.c (allSum,
+    rank order) under mpiexec -np G on spd8192, bit for bit, same loop count."""
+    G = gpus_pow2()
+    key = f"{program}_spd8192_np{G}"
+    r = golden_mpi()["runs"][key]
+    A, b, x0 = case(r["case"])
+    flags = cg.CGX_F32_REF | (cg.CGX_COMM_P2P if program == "p2p" else 0)
+    with cg.Solver(b.size, flags=flags, devices=list(range(G))) as s:
+        assert s.info.flags & cg.CGX_PEER_ACTIVE
+        s.set_system(A, b, x0)
+        x, st = s.solve(None, eps=1e-6)
+    assert st.iterations == r["ref_iterations"] and st.converged == 1
+    assert np.array_equal(x.view(np.uint32), mpi_golden_x(key).view(np.uint32))
+
+
+# ---- one process, Poisson slabs ----------------------------------------------------
+@needs_two
+@pytest.mark.parametrize("form", ["pull", "nofuse", "copy"])
+def test_poisson_distinct_devices_bitwise_equal_one_device(monkeypatch, form):
+    """Poisson slabs on G distinct GPUs: k_poisson_p reads the neighbours'
+    halo rows of r in place over xGMI (halo pull), the r.r and p.Ap partials
+    are summed in rank order by the consuming kernels (PeerSum) -- or, nofuse,
+    by combine kernels, or, copy, round 4's peer copies.  x bit for bit the
+    same partition's on one device, gated and fixed-count; against the oracle
+    at m = 128 (1e-10 converged, 1e-9 after 40 fixed iterations)."""
+    G = gpus_pow2()
+    m = 128
+    monkeypatch.setenv("CGX_LOCAL_XCHG", "copy" if form == "copy" else "kernel")
+    monkeypatch.setenv("CGX_LOCAL_FUSE", "0" if form == "nofuse" else "1")
+
+    def run(devices):
+        with cg.Solver(None, poisson_m=m, devices=devices) as s:
+            flags = s.info.flags
+            s.fill(1.0, 0.0)
+            xg, st = s.solve(None, eps=1e-8)
+            s.fill(1.0, 0.0)
+            xf, _ = s.solve(None, eps=-1.0, max_iter=40)
+        return flags, xg, st.iterations, xf
+
+    ref = run([0] * G)
+    got = run(list(range(G)))
+    assert got[0] & cg.CGX_PEER_ACTIVE
+    assert bool(got[0] & cg.CGX_HALO_PULL_ACTIVE) == (form != "copy")
+    assert bool(got[0] & cg.CGX_FOLDED_ACTIVE) == (form == "pull")
+    assert got[2] == ref[2] and np.array_equal(got[1], ref[1]) and np.array_equal(got[3], ref[3])
+    n = m * m
+    xo, so = oracle.cg_poisson_f64(m, np.ones(n), np.zeros(n), eps=1e-8)
+    assert got[2] == so.iterations and rel(got[1], xo) <= TOL
+    xo, _ = oracle.cg_poisson_f64(m, np.ones(n), np.zeros(n), eps=-1.0, max_iter=40)
+    assert rel(got[3], xo) <= 1e-9
+
+
+# ---- one process per GPU (RCCL over xGMI) ------------------------------------------
+@needs_two
+@pytest.mark.timeout(300)
+def test_rank_path_one_process_per_gpu(tmp_path):
+    G = gpus()
+    n = 1024 * G
+    x, res = run_ranks_per_gpu(tmp_path, "sized", n, G)
+    assert sorted(r["comm"]["rccl_device"] for r in res) == list(range(G))
+    info = res[0]["overlap_info"]
+    assert info["decided_by"] == "measured" and info["on"] == cg.overlap_rule(info)
     A, b = oracle.spd_matlab(n, np.float64)
     xo, so = oracle.cg_f64(A, b, np.zeros(n), eps=1e-10)
     assert res[0]["iterations"] == so.iterations
-    assert rel(xs[0], xo) <= TOL and res[0]["relres"] <= TOL
+    assert rel(x, xo) <= TOL and res[0]["relres"] <= TOL
+
+
+@needs_two
+@pytest.mark.timeout(900)
+def test_headline_n65536_one_process_per_gpu(tmp_path):
+    """configs[2] in the driver's placement on real GPUs: N = 65536 over G
+    rank processes, rank r on device r, RCCL allgather / allreduce over xGMI,
+    generated on the devices, converged at eps 1e-10 -- conjgrad.m's loop
+    count, x within 1e-10 of the fp64 oracle."""
+    n, G = 65536, gpus_pow2()
+    x, res = run_ranks_per_gpu(tmp_path, "headline", n, G, timeout=780)
+    assert res[0]["nrows"] == n // G and res[0]["overlap_info"]["decided_by"] == "measured"
+    xo, so = hash_oracle(n)
+    assert res[0]["converged"] and res[0]["iterations"] == so.iterations
+    assert rel(x, xo) <= TOL and res[0]["relres"] <= TOL
+
+
+@needs_two
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("mode", ["f32ref", "p2p_f32ref"])
+def test_rank_f32ref_one_process_per_gpu_bitwise_vs_mpi_reference(tmp_path, mode):
+    """G RCCL ranks on G GPUs == parallel_cg.c / point-to-point_cg.c on G MPI
+    ranks (spd8192), bit for bit, same loop count."""
+    n, G = 8192, gpus_pow2()
+    x, res = run_ranks_per_gpu(tmp_path, mode, n, G)
+    key = ("p2p" if mode.startswith("p2p") else "parallel") + f"_spd{n}_np{G}"
+    assert res[0]["iterations"] == golden_mpi()["runs"][key]["ref_iterations"]
+    assert np.array_equal(x.view(np.uint32), mpi_golden_x(key).view(np.uint32))
+
+
+@needs_two
+@pytest.mark.timeout(300)
+def test_poisson_rank_one_process_per_gpu(tmp_path):
+    """Poisson slabs, one rank process per GPU: r's halo rows by
+    ncclSend/Recv over xGMI, both scalars by allreduce; against the oracle."""
+    m, G = 128, gpus_pow2()
+    x, res = run_ranks_per_gpu(tmp_path, "poisson_eps", m, G)
+    xo, so = oracle.cg_poisson_f64(m, np.ones(m * m), np.zeros(m * m), eps=1e-8, max_iter=-1)
+    assert res[0]["iterations"] == so.iterations and rel(x, xo) <= TOL
+
+
+# ---- the bench line without a launcher ---------------------------------------------
+@needs_two
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("workload", ["dense", "poisson"])
+def test_bench_without_launcher_distinct_devices(workload):
+    """`bench.py --gpus G` without torchrun (cgx_create_multi over devices
+    0..G-1): one JSON line whose multi_device lists G distinct devices with
+    peer access, whose exchange text follows the context's flags, which
+    carries the measured overlap choice (dense) and the host's enqueue time
+    per iteration."""
+    import bench
+    G = gpus()
+    args = ["--gpus", str(G), "--steps", "5", "--warmup", "1", "--settle", "0", "--no-cpu"]
+    args += ["--size", str(8192 * G)] if workload == "dense" else ["--workload", "poisson", "--grid", str(512 * G)]
+    p = subprocess.run([sys.executable, os.path.join(os.path.dirname(HERE), "bench.py")] + args,
+                       capture_output=True, text=True, timeout=240)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-3000:]
+    lines = [ln for ln in p.stdout.splitlines() if ln.startswith("{")]
+    assert len(lines) == 1
+    out = json.loads(lines[0])
+    md = out["multi_device"]
+    assert out["n_gpus"] == G and md["devices"] == list(range(G)) and md["distinct_devices"] == G
+    assert md["peer_active"] and len(set(md["pci_bus_ids"])) == G
+    assert all(lk["link"] != "same device" for lk in md["links_from_block0"])
+    assert out["host_enqueue_us_per_iteration"] > 0
+    assert out["config"]["exchange"] == bench.exchange_text(G, md["flags"], devices=md["devices"],
+                                                            poisson=workload == "poisson")
+    if workload == "dense":
+        ov = out["overlap"]
+        assert ov["decided_by"] == "measured" and ov["on"] == cg.overlap_rule(ov)
+        assert out["check"]["relres"] < 1e-6
+    else:
+        assert "halo pull" in out["config"]["exchange"]

@@ -18,7 +18,8 @@ import pytest
 
 import conjugate_gradient_amd as cg
 import oracle
-from _cases import COMBINE_OF, KATS, SPD_ALL, SPD_SMALL, case, golden_mpi, golden_x, mpi_golden_x, mpi_runs
+from _cases import (COMBINE_OF, KATS, SPD_ALL, SPD_SMALL, case, golden_mpi, golden_x, hash_oracle, mpi_golden_x,
+                    mpi_runs)
 
 pytestmark = pytest.mark.gpu
 TOL = 1e-10
@@ -149,55 +150,6 @@ def test_local_exchange_kernels_bitwise_equal_peer_copies(monkeypatch, kind, P):
         assert itk == so.iterations and rel(xk, xo) <= TOL
 
 
-@pytest.mark.parametrize("P", [2, 3, 8])
-@pytest.mark.parametrize("overlap", [True, False])
-def test_local_graph_replay_bitwise(monkeypatch, P, overlap):
-    """Fixed-count iterations of the one-process multi-shard loop replayed
-    from captured hipGraphs (CGX_LOCAL_GRAPH; G iterations per graph, one
-    graph per ring residue of its first iteration) give x bit for bit the
-    eager path's: pieces that are and are not multiples of G and start at
-    every ring residue, eager iterations between replays, a matVec plan
-    change between calls (the graphs are captured again), G = 1, 3 and 8.
-    CGX_LOCAL_GRAPH=2: a capture that fails is an error, so the replay did
-    run."""
-    n = 2048 if P != 3 else 2049
-    A, b = oracle.spd_hash(n, seed=11, dtype=np.float64)
-    x0 = np.full(n, 0.125)
-    flags = cg.CGX_F64 | (0 if overlap else cg.CGX_NO_OVERLAP)
-    if overlap:
-        monkeypatch.setenv("CGX_OVERLAP", "1")  # whatever the measurement at creation would pick
-    monkeypatch.setenv("CGX_LOCAL_THREADS", "0")
-
-    def run(graph, G):
-        monkeypatch.setenv("CGX_LOCAL_GRAPH", graph)
-        monkeypatch.setenv("CGX_LOCAL_GRAPH_ITERS", str(G))
-        out = []
-        with cg.Solver(n, flags=flags, devices=[0] * P) as s:
-            s.set_system(A, b, x0)
-            s.begin()
-            for cnt in (8, 1, 16, 3, 13):
-                assert s.iterate(cnt, eps=-1.0)[0] == cnt
-                out.append(s.get_x())
-            s.set_matvec_plan(1, 8)
-            for cnt in (9, 24):
-                s.iterate(cnt, eps=-1.0)
-                out.append(s.get_x())
-            rn, bn = s.residual_norm()
-            x, st = s.solve(x0, eps=1e-10)  # the convergence-tested solve after replays (eager)
-            out.append(x)
-        return out, rn / bn, st.iterations
-
-    eager, rel0, it0 = run("0", 8)
-    for G in (1, 3, 8):
-        got, rel1, it1 = run("2", G)
-        assert len(got) == len(eager)
-        for i, (g, e) in enumerate(zip(got, eager)):
-            assert np.array_equal(g, e), (G, i)
-        assert rel1 == rel0 and it1 == it0
-    xo, so = oracle.cg_f64(A, b, x0, eps=1e-10)
-    assert it0 == so.iterations and rel(eager[-1], xo) <= TOL
-
-
 @pytest.mark.parametrize("P", [2, 4, 8])
 @pytest.mark.parametrize("name", ["kat4", "spd1024", "spd4096"])
 def test_row_block_shards_f64(golden, name, P):
@@ -316,20 +268,12 @@ def test_n65536_full_size_against_cpu_oracle(P):
     assert rn <= TOL * bn
 
 
-_ORACLE_CACHE = {}
-
-
 def _oracle_n65536():
-    return _oracle_hash(65536)
+    return hash_oracle(65536)
 
 
 def _oracle_hash(n, seed=42):
-    """conjgrad.m on the bench's counter-hash system, A regenerated per matVec
-    on 16 host threads (no n*n memory; bit-identical to the stored form)."""
-    if n not in _ORACLE_CACHE:
-        oracle.set_threads(16)
-        _ORACLE_CACHE[n] = oracle.cg_f64_hash(n, seed, eps=1e-10)
-    return _ORACLE_CACHE[n]
+    return hash_oracle(n, seed)
 
 
 @pytest.mark.timeout(900)
@@ -484,14 +428,7 @@ def test_create_multi_leaves_no_hip_error():
         s.generate_spd(1)
         _, st = s.solve(None, eps=1e-10)
         assert st.converged
-    if cg.device_count() >= 2:
-        link = cg.device_link(0, 1)
-        if link["peer_access"]:
-            with cg.Solver(1024, devices=[0, 1]) as s:
-                assert L.cgx_hip_last_error() == 0 and s.info.flags & cg.CGX_PEER_ACTIVE
-        else:  # named in the error, not a silent host-staged copy
-            with pytest.raises(cg.CgxError, match="cannot access"):
-                cg.Solver(1024, devices=[0, 1])
+    # (distinct devices: tests/test_gpu_multidevice.py::test_create_multi_distinct_devices_peer_access)
     assert cg.device_link(0, 0)["link"] == "unknown" and len(cg.device_pci_bus_id(0)) >= 12
 
 
@@ -538,7 +475,8 @@ def test_phase_times_tile_the_iteration(monkeypatch, kind):
     for name in cg.PHASE_NAMES[:8]:
         assert ph[name]["samples"] == want.get(name, 0), (name, ph[name])
     # matvec_busy (not a tile): the union of the matVec kernels' spans, one per iteration -- the matVec
-    # itself without the overlap; with it at least the own block, and within own + rest-wait + add
+    # itself without the overlap; with it at least the own block, and within own block + the wait for p
+    # (gather_exposed) + the rest launch, all three on the compute stream
     busy = ph["matvec_busy"]
     assert busy["samples"] == S, busy
     if kind == "shards_overlap":
@@ -1084,10 +1022,9 @@ def test_poisson_rejects_bad_use():
 
 @pytest.mark.parametrize("P", [2, 4, 8])
 def test_overlap_choice_is_bitwise_neutral(monkeypatch, P):
-    """Aligned row blocks: the context measures the allgather and the cost of
-    splitting the matVec at creation and picks the overlapped form (own
-    column block beside the exchange, then the rest) or the plain one (the
-    exchange, then one launch).  The one launch sums the own block and the
+    """Aligned row blocks: the context times both whole forms at creation and
+    picks the overlapped form (own column block beside the exchange, then the
+    rest) or the plain one (the exchange, then one launch).  The one launch sums the own block and the
     rest apart and adds them, as the two launches do: x is the same bits in
     every form (forced on, forced off by env or flag, measured), gated and
     fixed-count, from x0 = 0 and from a nonzero x0; all == oracle."""
@@ -1105,9 +1042,9 @@ def test_overlap_choice_is_bitwise_neutral(monkeypatch, P):
             info = s.overlap_info()
             on = bool(s.info.flags & cg.CGX_OVERLAP_ACTIVE)
             assert info["on"] == on and info["one_launch_us"] > 0 and info["allgather_us"] > 0
+            assert info["overlap_form_us"] > 0 and info["plain_form_us"] > 0 and info["margin"] == 0.01
             assert info["decided_by"] == {"on": "forced_on", "off": "off", "flag": "off"}.get(form, "measured")
-            assert on == {"on": True, "off": False, "flag": False}.get(form, info["allgather_us"] >
-                                                                        info["split_cost_us"])
+            assert on == {"on": True, "off": False, "flag": False}.get(form, cg.overlap_rule(info))
             s.set_system(A, b)
             xg, st = s.solve(None, eps=1e-10)
             xf, _ = s.solve(x0, eps=-1.0, max_iter=9)

@@ -14,10 +14,10 @@ too.  Exchange forms (read at context creation), interleaved: "kernel" (the
 default: one pull kernel per consuming shard for p's gather, the two scalar
 combines folded into the update kernels, one enqueuing thread per block),
 "onethread" (the same, all enqueued by the calling thread), "nofuse" (CGX_LOCAL_FUSE=0: a
-combine kernel per shard and scalar), "copy" (CGX_LOCAL_XCHG=copy: round
-3's hipMemcpyPeerAsync per pair) and "graph" (onethread's iterations captured
-G = CGX_LOCAL_GRAPH_ITERS at a time into a hipGraph and replayed; without
-CGX_PHASES, which the replay does not take, so that form has no phases).
+combine kernel per shard and scalar) and "copy" (CGX_LOCAL_XCHG=copy: round
+3's hipMemcpyPeerAsync per pair).  (Round 4's "graph" form, a hipGraph replay
+with every block on one device, was removed in round 6: no deployment puts
+every row block on one GPU.)
 With --poisson the sizes are grid widths m and the operator is the fused
 Poisson iteration (no CGX_PHASES): forms "pull" (round 5's default: r's halo
 rows read in place by k_poisson_p, both scalar combines folded into the
@@ -56,14 +56,13 @@ def run(n, shards, steps=200, warm=32, phases=True):
         s.iterate(10, eps=-1.0)
         t4 = time.perf_counter()
         s.synchronize()
-        t5 = time.perf_counter()  # 16 (two whole graphs of 8 in the graph form)
+        t5 = time.perf_counter()
         s.iterate(16, eps=-1.0)
         t6 = time.perf_counter()
         s.synchronize()
         rn, bn = s.residual_norm()
     return {"n": n, "shards": shards, "steps": steps, "exchange": ("copy" if os.environ.get("CGX_LOCAL_XCHG") == "copy" else
                                              "nofuse" if os.environ.get("CGX_LOCAL_FUSE") == "0" else
-                                             "graph" if os.environ.get("CGX_LOCAL_GRAPH") != "0" and not phases else
                                              "onethread" if os.environ.get("CGX_LOCAL_THREADS") == "0" else "kernel"),
             "flags": int(info.flags),
             "enqueue_us": round((t1 - t0) / steps * 1e6, 2), "wall_us": round((t2 - t0) / steps * 1e6, 2),
@@ -124,11 +123,8 @@ def main():
                 for form in forms if S > 1 else forms[:1]:
                     os.environ["CGX_LOCAL_XCHG"] = "copy" if form == "copy" else "kernel"
                     os.environ["CGX_LOCAL_FUSE"] = "0" if form == "nofuse" else "1"
-                    os.environ["CGX_LOCAL_THREADS"] = "0" if form in ("onethread", "nofuse", "copy", "graph") else "1"
-                    os.environ["CGX_LOCAL_GRAPH"] = "2" if form == "graph" else "0"
-                    out = run(n, S, phases=form != "graph")
-                    if form == "graph":
-                        out["graph_iters"] = int(os.environ.get("CGX_LOCAL_GRAPH_ITERS", "8"))
+                    os.environ["CGX_LOCAL_THREADS"] = "0" if form in ("onethread", "nofuse", "copy") else "1"
+                    out = run(n, S)
                     out["round"] = r
                     print(json.dumps(out), flush=True)
 
