@@ -3,8 +3,9 @@ from what one GPU can measure, so that a SCALE line's per-phase breakdown
 (bench.py `phases_us`) can be read against it phase by phase.
 
 Measured inputs (committed under profiles/):
-  - the 1-GPU iteration: the driver's N=1 bench line (BENCH_r04.json at the
-    repo root: ms_per_step), or profiles/r05_scale_inputs.json;
+  - the 1-GPU iteration: the driver's latest N=1 bench line (the highest
+    BENCH_rNN.json at the repo root: ms_per_step), or
+    profiles/<tag>_scale_inputs.json;
   - one rank's kernels at G ranks without the collectives, in both forms the
     context chooses between at creation (cgx_exchange.hip choose_overlap):
     split (own-column-block launch beside the allgather, then the rest) and
@@ -17,15 +18,32 @@ loopback sockets): the latency of RCCL's 8-byte allreduce and of the p
 allgather over xGMI, as a low / mid / high range.
 
 Per G and case the model predicts both forms and the one the library would
-pick (overlap only when the allgather takes longer than the split costs),
-which is the form a SCALE line reports in its "overlap" key.
+pick (overlap only when that form is the faster one end to end), which is
+the form a SCALE line reports in its "overlap" key.
 
-  python tools/scale_model.py > profiles/r05_scale_model.json
+Two deployments, two predictions per G:
+  "rccl"  -- one process per GPU (torchrun, the driver's N>1 launch): the
+             RCCL allgather and two 8-byte allreduces per iteration;
+  "local" -- `bench.py --gpus G` without a launcher (cgx_create_multi over
+             devices 0..G-1): p gathered by a pull kernel per device over
+             xGMI, both scalars summed by the update kernels themselves
+             (folded combines, no collective), every launch enqueued by one
+             host thread.  Measured inputs (profiles/r06_local_inputs.jsonl,
+             tools/local_inputs.py: the configs[2] blocks all on one GPU):
+             the host's enqueue per iteration at S blocks, and the pull
+             gather as the context times it at creation (S gathers at once
+             on one device: per device, its S-th share).  Assumed: the xGMI
+             latency of a peer read.  The iteration is the slower of the
+             device's work and the host's enqueue, and the model says which.
+
+  python tools/scale_model.py > profiles/r06_scale_model.json
   python tools/scale_model.py --compare LINE.json [...]
       (bench.py lines of an N>1 run, e.g. from the driver's SCALE record:
-      the form that ran, each phase's max over ranks against the model's mid
+      the deployment (the line's `rccl` or `multi_device` key), the form that
+      ran, each phase's max over ranks against that deployment's mid
       prediction for that form, and the phase furthest above it)
 """
+import collections
 import csv
 import json
 import os
@@ -35,7 +53,9 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PROF = os.environ.get("SCALE_PROF_DIR", os.path.join(ROOT, "profiles"))
-TAG = os.environ.get("SCALE_TAG", "r05")
+TAG = os.environ.get("SCALE_TAG", "r05")          # the rank-iteration inputs
+LOCAL_TAG = os.environ.get("SCALE_LOCAL_TAG", "r06")  # the one-process inputs
+MODEL_TAG = os.environ.get("SCALE_MODEL_TAG", "r06")  # the committed model --compare reads
 N = 65536
 
 # RCCL small-message collectives over xGMI on one 8-GPU MI300-class node (LL
@@ -46,15 +66,38 @@ N = 65536
 ALLREDUCE_US = {"low": 6.0, "mid": 12.0, "high": 25.0}
 GATHER_LAT_US = {"low": 6.0, "mid": 12.0, "high": 25.0}
 GATHER_GBPS_PER_LINK = 100.0
+# one process: a system-scope load of a peer device's memory over xGMI (the
+# pull gather's first bytes, each folded combine's partials)
+PEER_LOAD_US = {"low": 2.0, "mid": 4.0, "high": 8.0}
 
 
 def one_gpu_anchor():
-    rec = os.path.join(ROOT, "BENCH_r04.json")
-    if os.path.exists(rec):
-        d = json.load(open(rec))["parsed"]
-        return d["ms_per_step"], f"BENCH_r04.json: the driver's round-4 N=1 bench line ({d['value']:.2f} it/s)"
+    recs = sorted((int(m.group(1)), f) for f in os.listdir(ROOT) if (m := re.fullmatch(r"BENCH_r(\d+)\.json", f)))
+    for num, f in reversed(recs):
+        d = json.load(open(os.path.join(ROOT, f))).get("parsed") or {}
+        if d.get("ms_per_step"):
+            return d["ms_per_step"], f"{f}: the driver's round-{num} N=1 bench line ({d['value']:.2f} it/s)"
     d = json.load(open(os.path.join(PROF, f"{TAG}_scale_inputs.json")))
     return d["one_gpu_ms_per_step"], d["source"]
+
+
+def local_inputs():
+    """Per block count S: the medians over rounds of the default enqueue form
+    (one host thread) and of the creation-time pull-gather figure."""
+    path = os.path.join(PROF, f"{LOCAL_TAG}_local_inputs.jsonl")
+    if not os.path.exists(path):
+        return None
+    rows = collections.defaultdict(lambda: {"enqueue_us": [], "gather_us": []})
+    for line in open(path):
+        d = json.loads(line)
+        if d["form"] != "onethread":
+            continue
+        rows[d["blocks"]]["enqueue_us"].append(d["enqueue_us"])
+        rows[d["blocks"]]["gather_us"].append(d["overlap_info"]["allgather_us"])
+    return {S: {"host_enqueue_us": statistics.median(v["enqueue_us"]),
+                "host_enqueue_range_us": [min(v["enqueue_us"]), max(v["enqueue_us"])],
+                "gather_one_gpu_us": statistics.median(v["gather_us"]), "rounds": len(v["enqueue_us"])}
+            for S, v in rows.items()}
 
 
 def kernel_spans(trace_csv):
@@ -95,8 +138,40 @@ def kernel_spans(trace_csv):
     return {f: {k: round(statistics.median(v), 2) for k, v in d.items() if v} for f, d in out.items()}
 
 
+def local_prediction(G, split, one, own, ms1, li):
+    """bench.py --gpus G without a launcher: the pull gather on each device
+    (its share of the one-GPU figure + the peer-read latency + the slice
+    transfer), the two folded combines (a peer read each, inside the update
+    kernels), against the host enqueueing every block's launches."""
+    slice_bytes = 8 * N // G
+    pred = {}
+    for case in ("low", "mid", "high"):
+        lat = PEER_LOAD_US[case]
+        gather = li["gather_one_gpu_us"] / G + lat + slice_bytes / (GATHER_GBPS_PER_LINK * 1e3)
+        forms = {"overlap": split + max(0.0, gather - own) + 2 * lat, "plain": one + gather + 2 * lat}
+        chosen = min(forms, key=forms.get)
+        device_us = forms[chosen]
+        host_us = li["host_enqueue_us"]
+        it_us = max(device_us, host_us)
+        pred[case] = {
+            "allgather_us": round(gather, 2),
+            "device_iteration_us": {f: round(v, 1) for f, v in forms.items()},
+            "chosen": chosen,
+            "host_enqueue_us": host_us,
+            "bound": "host" if host_us > device_us else "device",
+            "iteration_us": round(it_us, 1),
+            "phases_us": ({"matvec_own": round(own, 2), "gather_exposed": round(max(0.0, gather - own), 2)}
+                          if chosen == "overlap" else {"matvec_own": 0.0, "gather_exposed": round(gather, 2)}),
+            "it_per_s": round(1e6 / it_us, 1),
+            "speedup_vs_1gpu": round(ms1 * 1e3 / it_us, 2),
+            "efficiency": round(ms1 * 1e3 / it_us / G, 3)}
+    return {"inputs": li | {"source": f"profiles/{LOCAL_TAG}_local_inputs.jsonl (tools/local_inputs.py)"},
+            "predicted": pred}
+
+
 def main():
     ms1, src1 = one_gpu_anchor()
+    loc = local_inputs()
     walls = {}
     for line in open(os.path.join(PROF, f"{TAG}_rank_iteration.jsonl")):
         d = json.loads(line)
@@ -114,10 +189,12 @@ def main():
             "allreduce_8B_us": ALLREDUCE_US,
             "allgather_latency_us": GATHER_LAT_US,
             "allgather_GBps_per_peer_link": GATHER_GBPS_PER_LINK,
+            "peer_load_latency_us": PEER_LOAD_US,
             "source": "not measurable on a one-GPU box (RCCL runs over loopback sockets there); RCCL's LL-protocol "
                       "small-message latency on one xGMI-connected node is assumed in the 5-25 us range (not from a "
                       "document available here); the MI355X has 7 xGMI links per GPU at ~153 GB/s each (the "
-                      "project brief), taken at 100 GB/s effective per peer",
+                      "project brief), taken at 100 GB/s effective per peer; a peer read's latency over xGMI "
+                      "(one process) assumed 2-8 us",
         },
         "per_G": {},
     }
@@ -142,7 +219,7 @@ def main():
             gather = GATHER_LAT_US[case] + slice_bytes / (GATHER_GBPS_PER_LINK * 1e3)  # per peer, peers in parallel
             ar = ALLREDUCE_US[case]
             forms = {"overlap": split + max(0.0, gather - own) + 2 * ar, "plain": one + gather + 2 * ar}
-            chosen = "overlap" if gather > split - one else "plain"
+            chosen = min(forms, key=forms.get)  # the library times both forms end to end and runs the faster
             it_us = forms[chosen]
             pred[case] = {
                 "allgather_us": round(gather, 2),
@@ -155,30 +232,45 @@ def main():
                 "speedup_vs_1gpu": round(ms1 * 1e3 / it_us, 2),
                 "efficiency": round(ms1 * 1e3 / it_us / G, 3)}
         entry["predicted"] = pred
+        li = (loc or {}).get(G)
+        if li:
+            entry["local"] = local_prediction(G, split, one, own, ms1, li)
         out["per_G"][str(G)] = entry
     json.dump(out, sys.stdout, indent=1)
     print()
 
 
 def compare(paths):
-    model = json.load(open(os.path.join(PROF, f"{TAG}_scale_model.json")))
+    model = json.load(open(os.path.join(PROF, f"{MODEL_TAG}_scale_model.json")))
     for path in paths:
         text = open(path).read()
         line = json.loads([ln for ln in text.splitlines() if ln.strip().startswith("{")][-1])
         G = str(line["n_gpus"])
-        pred = model["per_G"].get(G, {}).get("predicted", {}).get("mid")
+        local = "multi_device" in line and "rccl" not in line
+        entry = model["per_G"].get(G, {})
+        pred = (entry.get("local") or {}).get("predicted", {}).get("mid") if local else \
+            entry.get("predicted", {}).get("mid")
         meas = line.get("phases_us", {}).get("max_over_ranks")
         if not pred or not meas:
-            print(json.dumps({"file": path, "n_gpus": G, "error": "no model entry or no phases_us"}))
+            print(json.dumps({"file": path, "n_gpus": G, "deployment": "local" if local else "rccl",
+                              "error": "no model entry or no phases_us"}))
             continue
         ran = "overlap" if line.get("overlap", {}).get("on") else "plain"
         delta = {ph: round(meas.get(ph, 0.0) - v, 2) for ph, v in pred["phases_us"].items()}
-        print(json.dumps({"file": path, "n_gpus": G, "it_per_s": line["value"], "form_ran": ran,
-                          "form_model_picks": pred["chosen"], "overlap_measured": line.get("overlap"),
-                          "predicted_iteration_us": pred["iteration_us"][ran],
-                          "measured_iteration_us": meas.get("iteration"), "measured_phases_us": meas,
-                          "predicted_phases_us": pred["phases_us"], "delta_us": delta,
-                          "furthest_above_model": max(delta, key=delta.get)}))
+        out = {"file": path, "n_gpus": G, "deployment": "local" if local else "rccl", "it_per_s": line["value"],
+               "form_ran": ran, "form_model_picks": pred["chosen"], "overlap_measured": line.get("overlap"),
+               "measured_iteration_us": meas.get("iteration"), "measured_phases_us": meas,
+               "predicted_phases_us": pred["phases_us"], "delta_us": delta,
+               "furthest_above_model": max(delta, key=delta.get)}
+        if local:  # the slower of the device's work and the host's enqueue
+            host = line.get("host_enqueue_us_per_iteration")
+            out.update(predicted_iteration_us=pred["iteration_us"], predicted_bound=pred["bound"],
+                       predicted_host_enqueue_us=pred["host_enqueue_us"], measured_host_enqueue_us=host,
+                       measured_bound=None if host is None or meas.get("iteration") is None else
+                       "host" if host >= 0.95 * meas["iteration"] else "device")
+        else:
+            out["predicted_iteration_us"] = pred["iteration_us"][ran]
+        print(json.dumps(out))
 
 
 if __name__ == "__main__":

@@ -1,6 +1,7 @@
 # symmetric storage: the iteration rate after each fresh allocation of A within one process
+# (round 5's probe behind profiles/r05_symmetric_realloc.jsonl)
 import json, sys, time
-sys.path.insert(0, '/root/repo')
+sys.path.insert(0, __import__('os').path.dirname(__import__('os').path.dirname(__import__('os').path.abspath(__file__))))
 import conjugate_gradient_amd as cg
 n = 65536
 pad = []

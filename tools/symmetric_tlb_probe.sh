@@ -1,3 +1,4 @@
+# round 5: UTCL1 translation counters of k_symv_f64 over six processes (profiles/r05_symprobe_tlb/)
 export TMPDIR=/tmp; D=gpurun_out/r05_tlb; mkdir -p $D
 C="TCP_UTCL1_TRANSLATION_MISS_sum TCP_UTCL1_TRANSLATION_HIT_sum TCP_UTCL1_STALL_MULTI_MISS_sum TCP_UTCL1_PERMISSION_MISS_sum"
 for i in 1 2 3 4 5 6; do
