@@ -27,6 +27,13 @@ other files from running.
     process, :109-117 and :288-324): RCCL over xGMI between distinct devices.
   * bench.py --gpus G without a launcher, the one-process line a SCALE run
     would print.
+
+Rehearsal (CGX_TEST_MULTIDEVICE_REHEARSAL=1, one GPU): the same tests with
+8 "devices" that are all device 0 -- row blocks [0] * G, rank processes
+with their own NCCL_HOSTID (RCCL's socket transport), bench.py --devices
+0,...,0 -- and the assertions about distinct devices and peer access
+skipped.  It runs the tests' own code paths before the first node with
+several GPUs does (tools/multidevice_rehearsal.sh).
 """
 import json
 import os
@@ -43,6 +50,7 @@ from _cases import case, golden_mpi, hash_oracle, mpi_golden_x
 pytestmark = pytest.mark.gpu
 HERE = os.path.dirname(os.path.abspath(__file__))
 TOL = 1e-10
+REHEARSAL = os.environ.get("CGX_TEST_MULTIDEVICE_REHEARSAL") == "1"
 
 
 def rel(a, b):
@@ -50,10 +58,23 @@ def rel(a, b):
 
 
 def visible() -> int:
+    if REHEARSAL:
+        return 8
     try:
         return cg.device_count()
     except cg.CgxError:
         return 0
+
+
+def devs(G: int) -> list:
+    """Devices 0..G-1 (the rehearsal: device 0, G times)."""
+    return [0] * G if REHEARSAL else list(range(G))
+
+
+def distinct(flags: int) -> bool:
+    """The context spans distinct devices with peer access (trivially true
+    in the rehearsal, where there is one device)."""
+    return REHEARSAL or bool(flags & cg.CGX_PEER_ACTIVE)
 
 
 def gpus() -> int:
@@ -99,8 +120,13 @@ def run_ranks_per_gpu(tmp_path, mode, n, G, timeout=240):
     uidfile, out = str(tmp_path / "uid.bin"), str(tmp_path / mode)
     procs = []
     for r in range(G):
-        env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", CGX_TEST_RANK_DEVICE="rank")
-        env.pop("NCCL_HOSTID", None)
+        if REHEARSAL:  # every rank on device 0: RCCL needs a host id per rank (socket transport)
+            env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", NCCL_HOSTID=f"cgx-rehearsal-{r}",
+                       NCCL_SOCKET_IFNAME="lo", NCCL_IB_DISABLE="1")
+            env.pop("CGX_TEST_RANK_DEVICE", None)
+        else:
+            env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0", CGX_TEST_RANK_DEVICE="rank")
+            env.pop("NCCL_HOSTID", None)
         procs.append(subprocess.Popen([sys.executable, os.path.join(HERE, "_rank_worker.py"), mode, str(n), str(G),
                                        str(r), uidfile, out], env=env, stdout=subprocess.PIPE,
                                       stderr=subprocess.STDOUT, text=True))
@@ -117,7 +143,7 @@ def run_ranks_per_gpu(tmp_path, mode, n, G, timeout=240):
         assert p.returncode == 0, f"rank {r} exited {p.returncode}:\n{logs[r][-3000:]}"
     res = [json.load(open(out + f"_r{r}.json")) for r in range(G)]
     xs = [np.load(out + f"_x{r}.npy") for r in range(G)]
-    assert sorted(r["comm"]["device"] for r in res) == list(range(G))
+    assert sorted(r["comm"]["device"] for r in res) == devs(G)
     for r in range(1, G):
         assert np.array_equal(xs[r], xs[0]) and res[r]["iterations"] == res[0]["iterations"]
     return xs[0], res
@@ -131,8 +157,8 @@ def test_distinct_devices_bitwise_equal_one_device(monkeypatch, form, overlap):
     G = gpus()
     n = 1024 * G  # 1024-row blocks: aligned, so both exchange forms apply
     ref = solve_multi(monkeypatch, n, [0] * G, "kernel", overlap)
-    got = solve_multi(monkeypatch, n, list(range(G)), form, overlap)
-    assert got[0] & cg.CGX_PEER_ACTIVE and bool(got[0] & cg.CGX_OVERLAP_ACTIVE) == overlap
+    got = solve_multi(monkeypatch, n, devs(G), form, overlap)
+    assert distinct(got[0]) and bool(got[0] & cg.CGX_OVERLAP_ACTIVE) == overlap
     assert bool(got[0] & cg.CGX_THREADS_ACTIVE) == (form == "threads")
     assert bool(got[0] & cg.CGX_PULL_ACTIVE) == (form != "copy")
     assert got[2] == ref[2], (got[2], ref[2])
@@ -145,6 +171,8 @@ def test_create_multi_distinct_devices_peer_access():
     """cgx_create_multi over devices 0 and 1 enables peer access after
     hipDeviceCanAccessPeer and leaves no HIP error pending; without peer
     access it is refused by name, never a silent host-staged copy."""
+    if REHEARSAL:
+        pytest.skip("rehearsal: one device, nothing to enable")
     L = cg.lib()
     link = cg.device_link(0, 1)
     if link["peer_access"]:
@@ -163,7 +191,7 @@ def test_distinct_devices_measured_choice_matches_oracle():
     G = gpus()
     n = 1024 * G
     A, b = oracle.spd_matlab(n, np.float64)
-    with cg.Solver(n, devices=list(range(G))) as s:
+    with cg.Solver(n, devices=devs(G)) as s:
         info = s.overlap_info()
         assert info["decided_by"] == "measured" and info["on"] == cg.overlap_rule(info)
         s.set_system(A, b)
@@ -181,8 +209,8 @@ def test_headline_n65536_distinct_devices_one_process():
     converged at eps 1e-10: loop count == conjgrad.m's, x within 1e-10 of the
     fp64 oracle, true residual <= 1e-10 ||b||."""
     n, G = 65536, gpus_pow2()
-    with cg.Solver(n, devices=list(range(G))) as s:
-        assert s.info.flags & cg.CGX_PEER_ACTIVE and s.overlap_info()["decided_by"] == "measured"
+    with cg.Solver(n, devices=devs(G)) as s:
+        assert distinct(s.info.flags) and s.overlap_info()["decided_by"] == "measured"
         s.generate_spd(42)
         x, st = s.solve(None, eps=1e-10)
         rn, bn = s.residual_norm()
@@ -202,8 +230,8 @@ def test_f32ref_distinct_devices_bitwise_vs_mpi_reference(program):
     r = golden_mpi()["runs"][key]
     A, b, x0 = case(r["case"])
     flags = cg.CGX_F32_REF | (cg.CGX_COMM_P2P if program == "p2p" else 0)
-    with cg.Solver(b.size, flags=flags, devices=list(range(G))) as s:
-        assert s.info.flags & cg.CGX_PEER_ACTIVE
+    with cg.Solver(b.size, flags=flags, devices=devs(G)) as s:
+        assert distinct(s.info.flags)
         s.set_system(A, b, x0)
         x, st = s.solve(None, eps=1e-6)
     assert st.iterations == r["ref_iterations"] and st.converged == 1
@@ -235,8 +263,8 @@ def test_poisson_distinct_devices_bitwise_equal_one_device(monkeypatch, form):
         return flags, xg, st.iterations, xf
 
     ref = run([0] * G)
-    got = run(list(range(G)))
-    assert got[0] & cg.CGX_PEER_ACTIVE
+    got = run(devs(G))
+    assert distinct(got[0])
     assert bool(got[0] & cg.CGX_HALO_PULL_ACTIVE) == (form != "copy")
     assert bool(got[0] & cg.CGX_FOLDED_ACTIVE) == (form == "pull")
     assert got[2] == ref[2] and np.array_equal(got[1], ref[1]) and np.array_equal(got[3], ref[3])
@@ -254,7 +282,7 @@ def test_rank_path_one_process_per_gpu(tmp_path):
     G = gpus()
     n = 1024 * G
     x, res = run_ranks_per_gpu(tmp_path, "sized", n, G)
-    assert sorted(r["comm"]["rccl_device"] for r in res) == list(range(G))
+    assert sorted(r["comm"]["rccl_device"] for r in res) == devs(G)
     info = res[0]["overlap_info"]
     assert info["decided_by"] == "measured" and info["on"] == cg.overlap_rule(info)
     A, b = oracle.spd_matlab(n, np.float64)
@@ -314,7 +342,8 @@ def test_bench_without_launcher_distinct_devices(workload):
     per iteration."""
     import bench
     G = gpus()
-    args = ["--gpus", str(G), "--steps", "5", "--warmup", "1", "--settle", "0", "--no-cpu"]
+    args = (["--devices", ",".join(map(str, devs(G)))] if REHEARSAL else ["--gpus", str(G)])
+    args += ["--steps", "5", "--warmup", "1", "--settle", "0", "--no-cpu"]
     args += ["--size", str(8192 * G)] if workload == "dense" else ["--workload", "poisson", "--grid", str(512 * G)]
     p = subprocess.run([sys.executable, os.path.join(os.path.dirname(HERE), "bench.py")] + args,
                        capture_output=True, text=True, timeout=240)
@@ -323,9 +352,11 @@ def test_bench_without_launcher_distinct_devices(workload):
     assert len(lines) == 1
     out = json.loads(lines[0])
     md = out["multi_device"]
-    assert out["n_gpus"] == G and md["devices"] == list(range(G)) and md["distinct_devices"] == G
-    assert md["peer_active"] and len(set(md["pci_bus_ids"])) == G
-    assert all(lk["link"] != "same device" for lk in md["links_from_block0"])
+    assert md["devices"] == devs(G) and out["config"]["row_blocks"] == G
+    if not REHEARSAL:
+        assert out["n_gpus"] == G and md["distinct_devices"] == G
+        assert md["peer_active"] and len(set(md["pci_bus_ids"])) == G
+        assert all(lk["link"] != "same device" for lk in md["links_from_block0"])
     assert out["host_enqueue_us_per_iteration"] > 0
     assert out["config"]["exchange"] == bench.exchange_text(G, md["flags"], devices=md["devices"],
                                                             poisson=workload == "poisson")
