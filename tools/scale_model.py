@@ -245,8 +245,9 @@ def compare(paths):
     for path in paths:
         text = open(path).read()
         line = json.loads([ln for ln in text.splitlines() if ln.strip().startswith("{")][-1])
-        G = str(line["n_gpus"])
         local = "multi_device" in line and "rccl" not in line
+        # one process: the row blocks (a rehearsal puts several on one GPU; n_gpus counts devices)
+        G = str(line.get("config", {}).get("row_blocks") or line["n_gpus"]) if local else str(line["n_gpus"])
         entry = model["per_G"].get(G, {})
         pred = (entry.get("local") or {}).get("predicted", {}).get("mid") if local else \
             entry.get("predicted", {}).get("mid")
