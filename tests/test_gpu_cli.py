@@ -19,8 +19,14 @@ def _gpu(built):
     assert cg.device_count() >= 1
 
 
+# One device for every cg_hip run here (`--gpus P` puts its row blocks on
+# devices g % visible): on a node with several GPUs the distinct-device CLI
+# run is tests/test_gpu_multidevice.py's, collected last.
+ONE_GPU = dict(os.environ, HIP_VISIBLE_DEVICES="0")
+
+
 def run(*args, timeout=300):
-    r = subprocess.run([cg.CLI_PATH, *args], capture_output=True, text=True, timeout=timeout)
+    r = subprocess.run([cg.CLI_PATH, *args], capture_output=True, text=True, timeout=timeout, env=ONE_GPU)
     assert r.returncode == 0, r.stdout + r.stderr
     return r.stdout
 
@@ -59,7 +65,7 @@ def test_cli_full_teardown_same_output(golden, tmp_path):
         with open(dst, "w") as f:
             r = subprocess.run([cg.CLI_PATH, "--fp32-ref", "--print-x", "--stats", *paths], stdout=f,
                                stderr=subprocess.PIPE, text=True, timeout=300,
-                               env=dict(os.environ, CGX_CLI_FAST_EXIT=mode, CGX_CLI_HUGEPAGES=mode, CGX_CLI_TIMES="1"))
+                               env=dict(ONE_GPU, CGX_CLI_FAST_EXIT=mode, CGX_CLI_HUGEPAGES=mode, CGX_CLI_TIMES="1"))
         assert r.returncode == 0, r.stderr
         assert f'"fast_exit": {mode}' in r.stderr
         outs[mode] = dst.read_text().splitlines()
@@ -98,7 +104,7 @@ def test_cli_generated_text_files_multi_gpu(golden, tmp_path):
     out3 = run("--symmetric", "--stats", "--eps", "1e-10", "--print-x", *paths)
     x3 = printed_x(out3, n, np.float64)
     assert np.linalg.norm(x3 - xo) <= 1e-10 * np.linalg.norm(xo)
-    r = subprocess.run([cg.CLI_PATH, "--symmetric", "--fp32-ref", *paths], capture_output=True, text=True)
+    r = subprocess.run([cg.CLI_PATH, "--symmetric", "--fp32-ref", *paths], capture_output=True, text=True, env=ONE_GPU)
     assert r.returncode == 2
 
 
@@ -133,7 +139,7 @@ def test_cli_streamed_a_equals_materialized(golden, tmp_path, args):
     for mode, extra in (("stream", {"CGX_CLI_BLOCK_MB": repr(block_mb), "CGX_CLI_RING_MB": repr(3 * block_mb)}),
                         ("whole", {"CGX_CLI_STREAM": "0"})):
         r = subprocess.run([cg.CLI_PATH, *args, "--print-x", "--stats", *paths], capture_output=True, text=True,
-                           timeout=300, env=dict(os.environ, CGX_CLI_TIMES="1", **extra))
+                           timeout=300, env=dict(ONE_GPU, CGX_CLI_TIMES="1", **extra))
         assert r.returncode == 0, r.stdout + r.stderr
         assert f'"streamed": {int(mode == "stream")}' in r.stderr
         outs[mode] = r.stdout
@@ -156,6 +162,6 @@ def test_cli_streamed_a_bad_file_fails(tmp_path, cut):
     with open(paths[0], "w") as f:
         f.write("\n".join(lines) + "\n")
     r = subprocess.run([cg.CLI_PATH, "--fp32-ref", *paths], capture_output=True, text=True, timeout=300,
-                       env=dict(os.environ, CGX_CLI_BLOCK_MB=repr(25 * n * 4 / 1048576)))
+                       env=dict(ONE_GPU, CGX_CLI_BLOCK_MB=repr(25 * n * 4 / 1048576)))
     assert r.returncode == 1
     assert ("fewer than" if cut == "short" else "malformed number") in r.stderr

@@ -34,8 +34,11 @@ def run_mpi(nranks, *args, timeout=240):
     for r in range(nranks):
         if r:
             cmd.append(":")
+        # every rank on device 0 (CGX_DEVICE), also on a node with several GPUs: the one-rank-per-GPU
+        # cg_mpi run is tests/test_gpu_multidevice.py's, collected last
         cmd += ["-np", "1", "-env", "NCCL_HOSTID", f"cgx-mpi-host-{r}", "-env", "NCCL_SOCKET_IFNAME", "lo",
-                "-env", "NCCL_IB_DISABLE", "1", "-env", "CGX_RCCL_TIMEOUT_S", "120", CG_MPI, *args]
+                "-env", "NCCL_IB_DISABLE", "1", "-env", "CGX_RCCL_TIMEOUT_S", "120", "-env", "CGX_DEVICE", "0",
+                CG_MPI, *args]
     r = subprocess.run(cmd, capture_output=True, text=True, timeout=timeout)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-4000:]
     return r.stdout

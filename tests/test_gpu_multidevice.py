@@ -27,6 +27,9 @@ other files from running.
     process, :109-117 and :288-324): RCCL over xGMI between distinct devices.
   * bench.py --gpus G without a launcher, the one-process line a SCALE run
     would print.
+  * the drop-in programs: `cg_hip --gpus G` over devices 0..G-1 and
+    `mpiexec -np G cg_mpi` with one rank per GPU, x bit for bit the
+    unmodified MPI programs' (the other files pin their CLI runs to device 0).
 
 Rehearsal (CGX_TEST_MULTIDEVICE_REHEARSAL=1, one GPU): the same tests with
 8 "devices" that are all device 0 -- row blocks [0] * G, rank processes
@@ -366,3 +369,67 @@ def test_bench_without_launcher_distinct_devices(workload):
         assert out["check"]["relres"] < 1e-6
     else:
         assert "halo pull" in out["config"]["exchange"]
+
+
+# ---- the two drop-in programs over distinct devices --------------------------------
+@pytest.fixture(scope="module")
+def spd512_files(tmp_path_factory):
+    """generateSPDmatrix(512) written as the MATLAB script writes it."""
+    d = tmp_path_factory.mktemp("spd512")
+    A, b = oracle.spd_matlab(512, np.float64)
+    for name, arr, dec in (("A.txt", A, 4), ("b.txt", b, 4), ("x0.txt", np.zeros(512), 1)):
+        oracle.write_text(str(d / name), arr, dec)
+    return [str(d / f) for f in ("A.txt", "b.txt", "x0.txt")]
+
+
+def printed_x(out, n, dtype):
+    return np.array([float(v) for v in out.strip().splitlines()[-n:]], dtype=dtype)
+
+
+@needs_two
+@pytest.mark.timeout(300)
+def test_cg_hip_gpus_distinct_devices_bitwise_vs_mpi_reference(spd512_files):
+    """`cg_hip --gpus G` (one process, row blocks on devices 0..G-1) on the
+    text files == `mpiexec -np G` of the unmodified parallel_cg.c, bit for
+    bit, with the loop count."""
+    G = gpus_pow2()
+    key = f"parallel_spd512_np{G}"
+    env = dict(os.environ, HIP_VISIBLE_DEVICES="0") if REHEARSAL else dict(os.environ)
+    args = ["--gpus", str(G), "--fp32-ref", "--print-x", "--stats"]
+    r = subprocess.run([cg.CLI_PATH, *args, *spd512_files], capture_output=True, text=True, timeout=240, env=env)
+    assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
+    assert f"iterations: {golden_mpi()['runs'][key]['ref_iterations']} converged: 1" in r.stdout
+    x = printed_x(r.stdout, 512, np.float32)
+    assert np.array_equal(x.view(np.uint32), mpi_golden_x(key).view(np.uint32))
+
+
+@needs_two
+@pytest.mark.timeout(300)
+@pytest.mark.parametrize("program", ["parallel", "p2p"])
+def test_cg_mpi_one_rank_per_gpu_bitwise_vs_mpi_reference(spd512_files, program):
+    """`mpiexec -np G cg_mpi` as parallel_cg.c is launched: one rank per
+    GPU (the node-local rank picks the device), RCCL over xGMI (no per-rank
+    host id), x bit for bit the unmodified program's under mpiexec -np G."""
+    mpiexec = "/opt/conda/bin/mpiexec"
+    cg_mpi = os.path.join(os.path.dirname(cg.CLI_PATH), "cg_mpi")
+    if not (os.path.exists(mpiexec) and os.path.exists(cg_mpi)):
+        pytest.skip("MPICH mpiexec or bin/cg_mpi absent")
+    G = gpus_pow2()
+    key = f"{program}_spd512_np{G}"
+    args = ["--fp32-ref", "--print-x", "--stats"] + (["--p2p"] if program == "p2p" else []) + spd512_files
+    cmd = [mpiexec]
+    for r in range(G):
+        if r:
+            cmd.append(":")
+        cmd += ["-np", "1", "-env", "CGX_RCCL_TIMEOUT_S", "120"]
+        if REHEARSAL:  # every rank on device 0: a host id per rank (RCCL's socket transport)
+            cmd += ["-env", "NCCL_HOSTID", f"cgx-rehearsal-{r}", "-env", "NCCL_SOCKET_IFNAME", "lo",
+                    "-env", "NCCL_IB_DISABLE", "1", "-env", "CGX_DEVICE", "0"]
+        cmd += [cg_mpi, *args]
+    env = dict(os.environ, HSA_ENABLE_IPC_MODE_LEGACY="0")
+    env.pop("NCCL_HOSTID", None)
+    p = subprocess.run(cmd, capture_output=True, text=True, timeout=240, env=env)
+    assert p.returncode == 0, p.stdout[-2000:] + p.stderr[-4000:]
+    assert f"iterations: {golden_mpi()['runs'][key]['ref_iterations']} converged: 1" in p.stdout
+    x = printed_x(p.stdout, 512, np.float32)
+    assert np.array_equal(x.view(np.uint32), mpi_golden_x(key).view(np.uint32))
