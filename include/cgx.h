@@ -78,9 +78,10 @@ extern "C" {
                                   (the allgather, then one matVec launch).
                                   Without it the form is chosen at creation
                                   when every row block is a multiple of 128
-                                  rows: the overlap runs only if the measured
-                                  allgather takes longer than splitting the
-                                  matVec in two costs (cgx_get_overlap_info;
+                                  rows: the overlap runs only if that whole
+                                  form (allgather beside the split matVec),
+                                  timed end to end at creation, beats the
+                                  plain one by 1 % (cgx_get_overlap_info;
                                   env CGX_OVERLAP=0 / 1: never / always).  Both
                                   forms give the same bits. */
 #define CGX_OVERLAP_ACTIVE 0x800 /* reported in cgx_info.flags when it is on */

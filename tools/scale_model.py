@@ -182,8 +182,9 @@ def main():
     out = {
         "what": "configs[2] (N=65536 dense fp64, row blocks) at G GPUs: one rank's measured kernels in both "
                 "exchange forms plus assumed collective latencies -> predicted iteration, it/s and speed-up over "
-                "the measured 1-GPU step, and the form the library picks (overlap only when the allgather is "
-                "longer than the split costs); the phase keys are bench.py phases_us's",
+                "the measured 1-GPU step, and the form the library picks (the faster one end to end, as the "
+                "library times both at creation); the phase keys are bench.py phases_us's; 'local' = the "
+                "one-process deployment (host enqueue against device work)",
         "one_gpu": {"ms_per_step": ms1, "it_per_s": 1e3 / ms1, "source": src1},
         "assumptions": {
             "allreduce_8B_us": ALLREDUCE_US,
