@@ -77,6 +77,10 @@ def test_traffic_lookup_names_its_source():
         t, src = bench.pmc_traffic(f"n65536_g{g}")
         assert t is not None and 1.0 <= t / bench.matvec_bytes(65536, 65536 // g) < 1.01, g
     assert bench.pmc_traffic("n4096_g1") == (None, None)
+    # configs[4]: the xr kernels' bytes per launch over the x cycle, against the line's algorithmic figure
+    t, src = bench.pmc_traffic("poisson_m8192_g1")
+    m = 8192
+    assert t is not None and 1.0 <= t / (104.0 / 3 * m * m + 16 * m) < 1.06 and "poisson_m8192_g1" in src
 
 
 def _phases(scale):
