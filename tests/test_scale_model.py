@@ -79,3 +79,19 @@ def test_compare_reads_a_local_line(tmp_path):
     assert out["deployment"] == "local" and out["form_ran"] == pred["chosen"]
     assert out["predicted_iteration_us"] == pred["iteration_us"] and out["predicted_bound"] == pred["bound"]
     assert out["measured_host_enqueue_us"] == 690.0 and out["measured_bound"] == "host"
+
+
+def test_compare_reads_a_driver_record(tmp_path):
+    """A driver record (the bench lines inside a JSON document, e.g. under
+    "parsed", one per N) is read line by line."""
+    model = json.loads(run())
+    (tmp_path / "r06_scale_model.json").write_text(json.dumps(model))
+    pred = model["per_G"]["4"]["predicted"]["mid"]
+    line4 = {"n_gpus": 4, "value": 800.0, "overlap": {"on": pred["chosen"] == "overlap"},
+             "rccl": {"nranks": 4}, "phases_us": {"max_over_ranks": dict(pred["phases_us"], iteration=1250.0)}}
+    rec = {"runs": [{"n": 1, "parsed": {"n_gpus": 1, "value": 210.0}}, {"n": 4, "parsed": line4}]}
+    path = tmp_path / "SCALE_rXX.json"
+    path.write_text(json.dumps(rec, indent=1))
+    outs = [json.loads(ln) for ln in run("--compare", str(path), env={"SCALE_PROF_DIR": str(tmp_path)}).splitlines()]
+    assert [o["n_gpus"] for o in outs] == ["1", "4"]
+    assert "error" in outs[0] and outs[1]["deployment"] == "rccl" and outs[1]["measured_iteration_us"] == 1250.0

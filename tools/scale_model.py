@@ -241,11 +241,34 @@ def main():
     print()
 
 
+def bench_lines(path):
+    """The bench.py lines in a file: a driver record (BENCH_/SCALE_rNN.json: the
+    lines sit inside it, e.g. under "parsed", one per N), or a captured
+    stdout (the last JSON line)."""
+    text = open(path).read()
+    try:
+        doc = json.loads(text)
+    except ValueError:
+        return [json.loads([ln for ln in text.splitlines() if ln.strip().startswith("{")][-1])]
+    found = []
+
+    def walk(o):
+        if isinstance(o, dict):
+            if "n_gpus" in o and "value" in o:
+                found.append(o)
+                return
+            for v in o.values():
+                walk(v)
+        elif isinstance(o, list):
+            for v in o:
+                walk(v)
+    walk(doc)
+    return found
+
+
 def compare(paths):
     model = json.load(open(os.path.join(PROF, f"{MODEL_TAG}_scale_model.json")))
-    for path in paths:
-        text = open(path).read()
-        line = json.loads([ln for ln in text.splitlines() if ln.strip().startswith("{")][-1])
+    for path, line in ((p, ln) for p in paths for ln in bench_lines(p)):
         local = "multi_device" in line and "rccl" not in line
         # one process: the row blocks (a rehearsal puts several on one GPU; n_gpus counts devices)
         G = str(line.get("config", {}).get("row_blocks") or line["n_gpus"]) if local else str(line["n_gpus"])
