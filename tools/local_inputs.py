@@ -16,7 +16,8 @@ Forms: "onethread" (the default: the calling thread enqueues every block's
 work) and "threads" (CGX_LOCAL_THREADS=1: one host thread per block; on one
 GPU the runtime serialises their launches).
 
-  python tools/local_inputs.py [rounds] > profiles/rNN_local_inputs.jsonl
+  python tools/local_inputs.py [rounds] [--blocks 2,4,8] [--forms onethread,threads] [--iters 10]
+      > profiles/rNN_local_inputs.jsonl
 """
 import json
 import os
@@ -29,9 +30,9 @@ import conjugate_gradient_amd as cg  # noqa: E402
 N = 65536
 
 
-def run(S, form, iters=10):
+def run(S, form, iters=10, n=N):
     os.environ["CGX_LOCAL_THREADS"] = "1" if form == "threads" else "0"
-    with cg.Solver(N, devices=[0] * S) as s:
+    with cg.Solver(n, devices=[0] * S) as s:
         info = s.overlap_info()
         flags = s.info.flags
         s.generate_spd(42)
@@ -43,17 +44,26 @@ def run(S, form, iters=10):
         t1 = time.perf_counter()
         s.synchronize()
         t2 = time.perf_counter()
-    return {"n": N, "blocks": S, "form": form, "flags": int(flags),
+    return {"n": n, "blocks": S, "form": form, "flags": int(flags),
             "threads_active": bool(flags & cg.CGX_THREADS_ACTIVE), "overlap_info": info,
             "enqueue_us": round((t1 - t0) / iters * 1e6, 2), "wall_us": round((t2 - t0) / iters * 1e6, 2)}
 
 
 def main():
-    rounds = int(sys.argv[1]) if len(sys.argv) > 1 else 2
-    for r in range(rounds):
-        for S in (2, 4, 8):
-            for form in ("onethread", "threads"):
-                out = run(S, form)
+    import argparse
+    ap = argparse.ArgumentParser()
+    ap.add_argument("rounds", type=int, nargs="?", default=2)
+    ap.add_argument("--blocks", default="2,4,8")
+    ap.add_argument("--forms", default="onethread,threads")
+    ap.add_argument("--iters", type=int, default=10)
+    ap.add_argument("--n", type=int, default=N,
+                    help="system size; at N = 65536 the shared GPU runs behind the host, whose launches then "
+                         "wait for queue space, so the host's own cost is read at a small N (4096)")
+    a = ap.parse_args()
+    for r in range(a.rounds):
+        for S in (int(v) for v in a.blocks.split(",")):
+            for form in a.forms.split(","):
+                out = run(S, form, a.iters, a.n)
                 out["round"] = r
                 print(json.dumps(out), flush=True)
 
