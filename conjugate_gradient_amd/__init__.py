@@ -115,7 +115,8 @@ class CommInfo(ctypes.Structure):
 class OverlapInfo(ctypes.Structure):
     _fields_ = [("active", ctypes.c_int), ("decided_by", ctypes.c_int), ("allgather_us", ctypes.c_double),
                 ("split_us", ctypes.c_double), ("one_launch_us", ctypes.c_double), ("split_cost_us", ctypes.c_double),
-                ("overlap_form_us", ctypes.c_double), ("plain_form_us", ctypes.c_double), ("margin", ctypes.c_double)]
+                ("overlap_form_us", ctypes.c_double), ("plain_form_us", ctypes.c_double), ("margin", ctypes.c_double),
+                ("forms_ms", ctypes.c_double)]
 
 
 # cgx_overlap_info.decided_by
@@ -573,6 +574,7 @@ class Solver:
         r = lambda v: None if v < 0 else float(v)  # noqa: E731
         return {"on": bool(o.active), "decided_by": OVERLAP_DECIDED_BY.get(o.decided_by, str(o.decided_by)),
                 "overlap_form_us": r(o.overlap_form_us), "plain_form_us": r(o.plain_form_us), "margin": o.margin,
+                "forms_ms": r(o.forms_ms),
                 "allgather_us": r(o.allgather_us), "split_cost_us": r(o.split_cost_us), "split_us": r(o.split_us),
                 "one_launch_us": r(o.one_launch_us)}
 

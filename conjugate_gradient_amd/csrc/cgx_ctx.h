@@ -276,6 +276,7 @@ struct cgx_ctx {
     double ov_ag_us = -1.0, ov_split_us = -1.0, ov_one_us = -1.0, ov_cost_us = -1.0;
     // ... and the two whole forms, exchange + matVec end to end (the decision)
     double ov_form_us = -1.0, ov_plain_form_us = -1.0;
+    double ov_forms_ms = -1.0;  // host wall time of that timing (this rank)
     int ov_how = CGX_OV_NA;
     bool fused = false;    // Poisson: two-kernel fused iteration (k_poisson_p + k_poisson_xr)
     bool fused_p = false;  // dense, one GPU, small n: two launches per iteration (matVec, k_update_xrp_f64)

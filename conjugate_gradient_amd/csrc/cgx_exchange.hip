@@ -4,6 +4,7 @@
 //   point-to-point_cg.c:239-256,339-394 (CGX_COMM_P2P) -> p2p_allgather / p2p_scalar
 // in RCCL rank mode, by device copies in multi-shard mode; the overlap of
 // p's exchange with the own-column-block matVec; the Poisson halo rows.
+#include <chrono>
 #include <thread>
 
 #include "cgx_ctx.h"
@@ -738,7 +739,9 @@ int choose_overlap(cgx_ctx *c) {
     if (c->mode == M_LOCAL || c->nranks > 1) {
         TRY(measure_split(c));
         TRY(measure_allgather(c));
+        const auto t0 = std::chrono::steady_clock::now();
         TRY(measure_forms(c));
+        c->ov_forms_ms = std::chrono::duration<double, std::milli>(std::chrono::steady_clock::now() - t0).count();
         if (c->mode == M_RCCL) {  // the maxima over ranks, on every rank
             Shard &s = c->sh[0];
             TRY(set_dev(s));

@@ -711,6 +711,7 @@ int cgx_get_overlap_info(const cgx_ctx *c, cgx_overlap_info *info) {
     info->overlap_form_us = c->ov_form_us;
     info->plain_form_us = c->ov_plain_form_us;
     info->margin = kOverlapMargin;
+    info->forms_ms = c->ov_forms_ms;
     return CGX_OK;
 }
 

@@ -277,6 +277,8 @@ typedef struct {
                                back to back)                                 */
     double plain_form_us;  /* the plain form: allgather, then one launch     */
     double margin;         /* the hysteresis of the decision (0.01)          */
+    double forms_ms;       /* host wall time the end-to-end timing added to
+                              the context's creation (this process)         */
 } cgx_overlap_info;
 
 /* ---- errors / info ------------------------------------------------------- */

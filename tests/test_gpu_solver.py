@@ -1043,6 +1043,7 @@ def test_overlap_choice_is_bitwise_neutral(monkeypatch, P):
             on = bool(s.info.flags & cg.CGX_OVERLAP_ACTIVE)
             assert info["on"] == on and info["one_launch_us"] > 0 and info["allgather_us"] > 0
             assert info["overlap_form_us"] > 0 and info["plain_form_us"] > 0 and info["margin"] == 0.01
+            assert 0 < info["forms_ms"] < 60_000
             assert info["decided_by"] == {"on": "forced_on", "off": "off", "flag": "off"}.get(form, "measured")
             assert on == {"on": True, "off": False, "flag": False}.get(form, cg.overlap_rule(info))
             s.set_system(A, b)
