@@ -4,13 +4,17 @@
  *
  *   serialConjugate.c  : cg_hip matrixA.txt vectorb.txt initialguess.txt
  *   parallel_cg.c      : cg_hip --gpus P matrixA.txt vectorb.txt initialguess.txt
+ *   point-to-point_cg.c: cg_hip --gpus P --p2p matrixA.txt vectorb.txt initialguess.txt
+ *                        (its exchange: every slice to block 0, then from block 0
+ *                        to every block; the scalars summed in rank order)
  *
  * Same positional arguments (serialConjugate.c:48-52, 65-67), same text
  * formats, same stdout lines:
  *   "Computing cg of matrix size : <N*N>"             serialConjugate.c:58
  *   "average clock execution time in seconds: %f"     serialConjugate.c:250
  *   with --gpus > 1 additionally, as parallel_cg.c:123-126 / :334-335:
- *   "collective data distribution time in seconds: %f"
+ *   "collective data distribution time in seconds: %f"  (--p2p: "p2p data
+ *    distribution time in seconds: %f", point-to-point_cg.c:133)
  *   "cg method execution time in seconds: %f"
  *   "clock execution time in seconds: %f"
  * Same stopping rule: stop when sqrt(r.r) < EPSILON (1.0e-6,
@@ -103,7 +107,7 @@ static double now_s(void) {
 
 static void usage(const char *prog) {
     fprintf(stderr,
-            "usage: %s [--gpus P] [--fp32-ref | --symmetric] [--eps E] [--max-iter M] [--dims FILE] [--n N]\n"
+            "usage: %s [--gpus P [--p2p]] [--fp32-ref | --symmetric] [--eps E] [--max-iter M] [--dims FILE] [--n N]\n"
             "          [--threads T] [--print-x] [--stats] matrixA vectorb initialguess\n"
             "       %s --spd N [--seed S] [--gpus P] [--eps E] [--max-iter M] [--stats]\n",
             prog, prog);
@@ -257,7 +261,7 @@ static int opt_double(const char *name, const char *v, double *out) {
 
 int main(int argc, char **argv) {
     const double t_prog0 = now_s();
-    int gpus = 1, fp32ref = 0, symmetric = 0, print_x = 0, stats = 0;
+    int gpus = 1, fp32ref = 0, symmetric = 0, print_x = 0, stats = 0, p2p = 0;
     long ncpu = sysconf(_SC_NPROCESSORS_ONLN);
     int threads = (int)(ncpu < 1 ? 1 : (ncpu > 16 ? 16 : ncpu)); /* text parsing threads */
     double eps = EPSILON_DEFAULT;
@@ -276,6 +280,7 @@ int main(int argc, char **argv) {
             gpus = (v < 0 || v > 1000) ? -1 : (int)v;
         } else if (!strcmp(a, "--fp32-ref")) fp32ref = 1;
         else if (!strcmp(a, "--symmetric")) symmetric = 1;
+        else if (!strcmp(a, "--p2p")) p2p = 1;
         else if (!strcmp(a, "--eps") && has_val) {
             if (!opt_double(a, argv[++i], &eps)) return 2;
         } else if (!strcmp(a, "--max-iter") && has_val) {
@@ -305,6 +310,10 @@ int main(int argc, char **argv) {
     }
     if (gpus < 1) { fprintf(stderr, "--gpus must be >= 1\n"); return 2; }
     if (gpus > 32) { fprintf(stderr, "--gpus must be <= 32\n"); return 2; }
+    if (p2p && symmetric) {
+        fprintf(stderr, "--p2p is an exchange of several row blocks (--symmetric is one GPU)\n");
+        return 2;
+    }
     if (symmetric && (fp32ref || gpus != 1)) {
         fprintf(stderr, "--symmetric is fp64 on one GPU (no --fp32-ref, --gpus 1)\n");
         return 2;
@@ -330,7 +339,7 @@ int main(int argc, char **argv) {
     printf("Computing cg of matrix size : %lld\n", (long long)n * (long long)n); /* serialConjugate.c:58 */
     fflush(stdout);
 
-    const int flags = fp32ref ? CGX_F32_REF : (CGX_F64 | (symmetric ? CGX_SYMMETRIC : 0));
+    const int flags = (fp32ref ? CGX_F32_REF : (CGX_F64 | (symmetric ? CGX_SYMMETRIC : 0))) | (p2p ? CGX_COMM_P2P : 0);
     const size_t es = fp32ref ? 4 : 8;
     void *x = malloc((size_t)n * es);
     void *A = NULL, *b = NULL;
@@ -484,7 +493,7 @@ int main(int argc, char **argv) {
 
     if (gpus > 1) {
         printf("cg method execution time in seconds: %f\n", st.solve_ms / 1e3);
-        printf("collective data distribution time in seconds: %f\n", t_dist1 - t_dist0);
+        printf("%s data distribution time in seconds: %f\n", p2p ? "p2p" : "collective", t_dist1 - t_dist0);
         printf("clock execution time in seconds: %f\n", now_s() - t_prog0);
     } else {
         printf("average clock execution time in seconds: %f\n", st.solve_ms / 1e3);

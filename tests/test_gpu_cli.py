@@ -9,7 +9,7 @@ import pytest
 
 import conjugate_gradient_amd as cg
 import oracle
-from _cases import FIX, case, golden_x, mpi_golden_x
+from _cases import FIX, case, golden_mpi, golden_x, mpi_golden_x
 
 pytestmark = pytest.mark.gpu
 
@@ -165,3 +165,22 @@ def test_cli_streamed_a_bad_file_fails(tmp_path, cut):
                        env=dict(ONE_GPU, CGX_CLI_BLOCK_MB=repr(25 * n * 4 / 1048576)))
     assert r.returncode == 1
     assert ("fewer than" if cut == "short" else "malformed number") in r.stderr
+
+
+@pytest.mark.parametrize("P", [2, 4, 8])
+@pytest.mark.parametrize("program", ["parallel", "p2p"])
+def test_cli_gpus_equals_mpi_programs(tmp_path, program, P):
+    """`cg_hip --gpus P [--p2p] --fp32-ref` in one process == `mpiexec -np P`
+    of the unmodified parallel_cg.c / point-to-point_cg.c on the same files:
+    x bit for bit, the loop count, and each program's lines in its order (cg
+    time, then its distribution time, then the clock time)."""
+    n, paths = _spd512_files(tmp_path)
+    key = f"{program}_spd512_np{P}"
+    out = run("--gpus", str(P), *(["--p2p"] if program == "p2p" else []), "--fp32-ref", "--print-x", "--stats", *paths)
+    dist = "p2p" if program == "p2p" else "collective"  # point-to-point_cg.c:133 / parallel_cg.c:123
+    lines = [ln.split(":")[0] for ln in out.splitlines() if "time in seconds:" in ln]
+    assert lines == ["cg method execution time in seconds", f"{dist} data distribution time in seconds",
+                     "clock execution time in seconds"], lines
+    assert f"iterations: {golden_mpi()['runs'][key]['ref_iterations']} converged: 1" in out
+    x = printed_x(out, n, np.float32)
+    assert np.array_equal(x.view(np.uint32), mpi_golden_x(key).view(np.uint32))

@@ -388,14 +388,15 @@ def printed_x(out, n, dtype):
 
 @needs_two
 @pytest.mark.timeout(300)
-def test_cg_hip_gpus_distinct_devices_bitwise_vs_mpi_reference(spd512_files):
-    """`cg_hip --gpus G` (one process, row blocks on devices 0..G-1) on the
-    text files == `mpiexec -np G` of the unmodified parallel_cg.c, bit for
-    bit, with the loop count."""
+@pytest.mark.parametrize("program", ["parallel", "p2p"])
+def test_cg_hip_gpus_distinct_devices_bitwise_vs_mpi_reference(spd512_files, program):
+    """`cg_hip --gpus G [--p2p]` (one process, row blocks on devices 0..G-1)
+    on the text files == `mpiexec -np G` of the unmodified parallel_cg.c /
+    point-to-point_cg.c, bit for bit, with the loop count."""
     G = gpus_pow2()
-    key = f"parallel_spd512_np{G}"
+    key = f"{program}_spd512_np{G}"
     env = dict(os.environ, HIP_VISIBLE_DEVICES="0") if REHEARSAL else dict(os.environ)
-    args = ["--gpus", str(G), "--fp32-ref", "--print-x", "--stats"]
+    args = ["--gpus", str(G), "--fp32-ref", "--print-x", "--stats"] + (["--p2p"] if program == "p2p" else [])
     r = subprocess.run([cg.CLI_PATH, *args, *spd512_files], capture_output=True, text=True, timeout=240, env=env)
     assert r.returncode == 0, r.stdout[-2000:] + r.stderr[-3000:]
     assert f"iterations: {golden_mpi()['runs'][key]['ref_iterations']} converged: 1" in r.stdout
