@@ -349,6 +349,14 @@ int main(int argc, char **argv) {
     big_buf Abuf = {NULL, NULL, 0};
     pthread_t freer;
     int freeing = 0;
+    /* Several row blocks: the solve is host-bound (one thread enqueues every
+     * block's launches, records and waits), and two munmaps of a GiB or more
+     * on the helper thread hold the process's mm lock against it -- `cg_hip
+     * --gpus P --fp32-ref` at N = 4096 / 8192 measured 1-24 ms per solve
+     * against 0.7-3.9 ms in a process with nothing to release
+     * (profiles/r06_published_mpi_sizes.json, r06_multi_solve_latency.jsonl).
+     * So with P > 1 the release starts after the solve. */
+    const int defer_release = gpus > 1;
     const char *se = getenv("CGX_CLI_STREAM");
     const int stream_a = spd_n <= 0 && !(se && !strcmp(se, "0"));
     if (!x) { fprintf(stderr, "can't allocate memory for vector\n"); return 1; }
@@ -438,8 +446,10 @@ int main(int argc, char **argv) {
         }
         if (!read_rc) read_rc = read_file(pos[1], n, fp32ref, b, threads) || read_file(pos[2], n, fp32ref, x, 1);
         rel.text = st.text;
-        if (pthread_create(&freer, NULL, release_buf, &rel) == 0) freeing = 1;
-        else release_buf(&rel);
+        if (!defer_release) {
+            if (pthread_create(&freer, NULL, release_buf, &rel) == 0) freeing = 1;
+            else release_buf(&rel);
+        }
     } else {
         read_rc = spd_n > 0 ? 0
                             : (read_file(pos[0], n * n, fp32ref, A, threads) ||
@@ -475,8 +485,10 @@ int main(int argc, char **argv) {
         /* A is no longer needed: release it on a helper thread while the
          * solve runs (unmapping 268 MB took 16-30 ms on the critical path) */
         rel.buf = Abuf;
-        if (pthread_create(&freer, NULL, release_buf, &rel) == 0) freeing = 1;
-        else release_buf(&rel);
+        if (!defer_release) {
+            if (pthread_create(&freer, NULL, release_buf, &rel) == 0) freeing = 1;
+            else release_buf(&rel);
+        }
         free(b);
         if (rc != CGX_OK) return die_cgx(rc, "cgx_set_system");
     }
@@ -490,6 +502,10 @@ int main(int argc, char **argv) {
     rc = cgx_get_x(ctx, x);
     if (rc != CGX_OK) return die_cgx(rc, "cgx_get_x");
     const double t_x = now_s();
+    if (defer_release) {
+        if (pthread_create(&freer, NULL, release_buf, &rel) == 0) freeing = 1;
+        else release_buf(&rel);
+    }
 
     if (gpus > 1) {
         printf("cg method execution time in seconds: %f\n", st.solve_ms / 1e3);
