@@ -349,14 +349,20 @@ int main(int argc, char **argv) {
     big_buf Abuf = {NULL, NULL, 0};
     pthread_t freer;
     int freeing = 0;
-    /* Several row blocks: the solve is host-bound (one thread enqueues every
-     * block's launches, records and waits), and two munmaps of a GiB or more
-     * on the helper thread hold the process's mm lock against it -- `cg_hip
+    /* A's buffers are released on a helper thread AFTER the solve.  Two
+     * munmaps of a GiB or more hold the process's mm lock, and a solve that
+     * enqueues while they run waits on it: with several row blocks (host-bound:
+     * one thread enqueues every block's launches, records and waits) `cg_hip
      * --gpus P --fp32-ref` at N = 4096 / 8192 measured 1-24 ms per solve
      * against 0.7-3.9 ms in a process with nothing to release
-     * (profiles/r06_published_mpi_sizes.json, r06_multi_solve_latency.jsonl).
-     * So with P > 1 the release starts after the solve. */
-    const int defer_release = gpus > 1;
+     * (profiles/r06_published_mpi_sizes_before.json, r06_multi_solve_latency.jsonl);
+     * on one GPU 0.23-0.25 against 0.19-0.20 ms at N = 1024 and 0.33-0.36
+     * against 0.30-0.31 at 2048, the same at 4096 / 8192
+     * (profiles/r06_cli_release_ab.jsonl).  CGX_CLI_RELEASE=during keeps the
+     * release beside the solve (it then overlaps the solve instead of the
+     * process's exit). */
+    const char *re = getenv("CGX_CLI_RELEASE");
+    const int defer_release = !(re && !strcmp(re, "during"));
     const char *se = getenv("CGX_CLI_STREAM");
     const int stream_a = spd_n <= 0 && !(se && !strcmp(se, "0"));
     if (!x) { fprintf(stderr, "can't allocate memory for vector\n"); return 1; }

@@ -107,7 +107,7 @@ def main():
             times = []
             for _ in range(a.runs):
                 out = subprocess.run([cg.CLI_PATH, "--fp32-ref", "--stats", "--print-x", *paths], check=True,
-                                     capture_output=True, text=True).stdout
+                                     capture_output=True, text=True, env=dict(os.environ, HIP_VISIBLE_DEVICES="0")).stdout
                 times.append(float(out.split("average clock execution time in seconds:")[1].split()[0]))
                 x = np.array([float(v) for v in out.strip().splitlines()[-n:]], dtype=np.float32)
                 assert np.array_equal(x.view(np.uint32), xr.view(np.uint32)), n
