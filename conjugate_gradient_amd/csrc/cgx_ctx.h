@@ -332,6 +332,10 @@ struct cgx_ctx {
     // partials, k_update_xp_f64 the r.r partials: PeerSum), so an iteration
     // launches no combine kernel (CGX_LOCAL_FUSE=0: separate combine kernels)
     bool fuse_combine = false;
+    // ... and for CGX_F32_REF: both scalars summed in MPICH order by the
+    // kernels that consume them (k_dot_ref_f32_blk<kDotXR>: p.Ap,
+    // k_update_p_ref_f32: r.r; PeerSumF32), the same bits as the combine kernels
+    bool fuse_f32 = false;
     // LOCAL mode: one host thread per row block enqueues its block's iteration
     // (cgx_local_mt.hip); null when not used
     cgxh::LocalPool *pool = nullptr;
@@ -395,6 +399,7 @@ int p2p_scalar(cgx_ctx *c, int lslot, int gslot);
 int exchange_allgather(cgx_ctx *c, bool from_x);
 int exchange_scalar(cgx_ctx *c, int lslot, int gslot);
 PeerSum peer_sum(const cgx_ctx *c, const Shard &d, int lslot, int gslot);
+PeerSumF32 peer_sum_f32(const cgx_ctx *c, const Shard &d, int lslot, int gslot);
 int overlapped_matvec(cgx_ctx *c, int dot_slot, bool gated, bool timed = true);
 int overlap_matvecs(cgx_ctx *c, Shard &d, int dot_slot, bool gated, bool timed = true);
 int choose_overlap(cgx_ctx *c);

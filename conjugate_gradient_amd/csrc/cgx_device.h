@@ -68,6 +68,30 @@ __device__ __forceinline__ double peer_sum_wave(const PeerSum &c) {
     return v;
 }
 
+// PeerSumF32: parallel_cg.c's MPI_Allreduce (MPICH 3.3's recursive doubling)
+// of the cnt float partials, by every wave (all 64 lanes active): lane q
+// loads partial q, pairs (2q, 2q+1) for q < rem combine first, then the
+// pairwise tree over pof2 values -- k_combine_peers<float>'s adds in its
+// order; wave-uniform result; block 0's thread 0 stores it.
+__device__ __forceinline__ float peer_sum_mpich_f32(const PeerSumF32 &c) {
+#pragma clang fp contract(off)
+    const int lane = threadIdx.x & 63;
+    const float x = peer_lane_load<float>(c.src, c.cnt);
+    int pof2 = 1;
+    while (pof2 * 2 <= c.cnt) pof2 *= 2;
+    const int rem = c.cnt - pof2;
+    const float a = __shfl(x, lane < rem ? 2 * lane : (lane + rem) & 63, 64);
+    const float b = __shfl(x, (2 * lane + 1) & 63, 64);
+    float v = lane < rem ? a + b : a;
+    for (int d = 1; d < pof2; d *= 2) {
+        const float w = __shfl(v, (lane + d) & 63, 64);
+        if (lane % (2 * d) == 0 && lane + d < pof2) v = v + w;
+    }
+    const float r = __shfl(v, 0, 64);
+    if (blockIdx.x == 0 && threadIdx.x == 0) *c.out = r;
+    return r;
+}
+
 __device__ __forceinline__ double cg_ratio(double num, double den) {
     return (den != 0.0 || !(__builtin_fabs(num) < 0x1p-1022)) ? num / den : 0.0;
 }

@@ -398,6 +398,14 @@ PeerSum peer_sum(const cgx_ctx *c, const Shard &d, int lslot, int gslot) {
     return ps;
 }
 
+PeerSumF32 peer_sum_f32(const cgx_ctx *c, const Shard &d, int lslot, int gslot) {
+    PeerSumF32 ps{};
+    ps.src = peer_table(c, &Shard::scal, 8 * (int64_t)lslot);
+    ps.cnt = (int)c->sh.size();
+    ps.out = reinterpret_cast<float *>(slot(d, gslot));
+    return ps;
+}
+
 // Combine the per-shard partials in slot `lslot` into the global slot `gslot`.
 int exchange_scalar(cgx_ctx *c, int lslot, int gslot) {
     if (c->mode == M_SINGLE) return CGX_OK;  // kernels wrote the global slot directly

@@ -542,22 +542,26 @@ int do_iteration(cgx_ctx *c, double eps, int *stop, bool gated) {
     }
     // MPI_Allreduce(p.Ap)  parallel_cg.c:294 -- multi-shard fp64: summed by
     // k_update_r_f64 itself after the barrier (fuse_combine)
-    if (c->fuse_combine) TRY(local_barrier(c));
+    // (F32_REF, fuse_f32: summed in MPICH order by k_dot_ref_f32_blk<kDotXR>)
+    const bool fold = c->fuse_combine || c->fuse_f32;
+    if (fold) TRY(local_barrier(c));
     else TRY(exchange_scalar(c, pl, pg));
     const int rg = S_RR + ring(k + 1), rl = S_LRR + ring(k + 1);
     const int ro = out_slot(c, rl, rg);
-    // the r.r combine folds into k_update_xp_f64 unless the host reads r.r
-    // first (host-checked convergence)
-    const bool fuse_rr = c->fuse_combine && (gated || eps < 0.0);
+    // the r.r combine folds into k_update_xp_f64 (F32_REF: k_update_p_ref_f32)
+    // unless the host reads r.r first (host-checked convergence)
+    const bool fuse_rr = fold && (gated || eps < 0.0);
     for (auto &s : c->sh) {
         TRY(set_dev(s));
         if (f32ref(c)) {
             // x += alpha p; r -= alpha Ap; r.r in one launch  (serialConjugate.c:219-234)
+            const PeerSumF32 ps = c->fuse_f32 ? peer_sum_f32(c, s, pl, pg) : PeerSumF32{};
             HIPT(update_xr_dot_ref_f32(s.nloc, reinterpret_cast<float *>(s.x), reinterpret_cast<float *>(s.r),
                                        reinterpret_cast<const float *>(s.pown), reinterpret_cast<const float *>(s.Ap),
                                        reinterpret_cast<const float *>(slot(s, S_RR + ring(k))),
                                        reinterpret_cast<const float *>(slot(s, pg)),
-                                       reinterpret_cast<float *>(slot(s, ro)), s.stream, gate_of(s, gated)));
+                                       reinterpret_cast<float *>(slot(s, ro)), s.stream, gate_of(s, gated),
+                                       c->fuse_f32 ? &ps : nullptr));
         } else {
             // r -= alpha Ap, r.r; x's update is deferred into the p update
             const PeerSum ps = c->fuse_combine ? peer_sum(c, s, pl, pg) : PeerSum{};
@@ -575,11 +579,13 @@ int do_iteration(cgx_ctx *c, double eps, int *stop, bool gated) {
         for (auto &s : c->sh) {
             TRY(set_dev(s));
             if (f32ref(c)) {  // x is current; the p update decides the stop first
+                const PeerSumF32 ps = fuse_rr ? peer_sum_f32(c, s, rl, rg) : PeerSumF32{};
                 HIPT(update_p_ref_f32(s.nloc, reinterpret_cast<float *>(s.pown), reinterpret_cast<const float *>(s.r),
                                       reinterpret_cast<const float *>(slot(s, rg)),
                                       reinterpret_cast<const float *>(slot(s, S_RR + ring(k))), s.stream, eps, k,
                                       reinterpret_cast<int64_t *>(slot(s, S_KDONE)),
-                                      reinterpret_cast<double *>(slot(s, S_RRFINAL)), rec_of(c, s, gated)));
+                                      reinterpret_cast<double *>(slot(s, S_RRFINAL)), rec_of(c, s, gated),
+                                      fuse_rr ? &ps : nullptr));
                 continue;
             }
             const PeerSum ps = fuse_rr ? peer_sum(c, s, rl, rg) : PeerSum{};
@@ -618,11 +624,13 @@ int do_iteration(cgx_ctx *c, double eps, int *stop, bool gated) {
     }
     for (auto &s : c->sh) {  // p = r + (beta/rsold) p    serialConjugate.c:239-243
         TRY(set_dev(s));
-        if (f32ref(c))
+        if (f32ref(c)) {
+            const PeerSumF32 ps = fuse_rr ? peer_sum_f32(c, s, rl, rg) : PeerSumF32{};
             HIPT(update_p_ref_f32(s.nloc, reinterpret_cast<float *>(s.pown),
                                   reinterpret_cast<const float *>(s.r), reinterpret_cast<const float *>(slot(s, rg)),
-                                  reinterpret_cast<const float *>(slot(s, S_RR + ring(k))), s.stream));
-        else {  // x += alpha p (deferred from the r update), then p = r + beta p
+                                  reinterpret_cast<const float *>(slot(s, S_RR + ring(k))), s.stream, -1.0, 0,
+                                  nullptr, nullptr, nullptr, fuse_rr ? &ps : nullptr));
+        } else {  // x += alpha p (deferred from the r update), then p = r + beta p
             const PeerSum ps = fuse_rr ? peer_sum(c, s, rl, rg) : PeerSum{};
             HIPT(update_xp_f64(s.nloc, reinterpret_cast<double *>(s.x), reinterpret_cast<double *>(s.pown),
                                reinterpret_cast<const double *>(s.r),

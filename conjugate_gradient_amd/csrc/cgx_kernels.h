@@ -48,6 +48,14 @@ struct PeerSum {
     int cnt;
     double *out;
 };
+// The F32_REF counterpart: the cnt float partials combined in MPICH's
+// MPI_Allreduce order (k_combine_peers<float>'s mpich form, the same adds),
+// folded into k_dot_ref_f32_blk<kDotXR> (p.Ap) and k_update_p_ref_f32 (r.r).
+struct PeerSumF32 {
+    PeerTable src;
+    int cnt;
+    float *out;
+};
 
 // CGX_PHASES in-kernel timestamps: a kernel given `ts` stores block 0's entry
 // time in ts[0] and block b's exit time in ts[1 + b] (b < kTsMaxBlocks), on
@@ -231,8 +239,11 @@ hipError_t update_xr_ref_f32(int64_t n, float *x, float *r, const float *p, cons
                              const float *rsold, const float *pAp, hipStream_t s, const int64_t *gate = nullptr);
 // one launch each: x += p alpha, r -= Ap alpha, *rr = r.r (serialConjugate.c:219-234) /
 // r = p = b - Ax, *rr = r.r (:209-212); the same float operations as the separate kernels
+// pap_sum (several row blocks in one process): p.Ap summed from the blocks'
+// partials in MPICH order instead of read from *pAp, which block 0 stores.
 hipError_t update_xr_dot_ref_f32(int64_t n, float *x, float *r, const float *p, const float *Ap, const float *rsold,
-                                 const float *pAp, float *rr, hipStream_t s, const int64_t *gate = nullptr);
+                                 const float *pAp, float *rr, hipStream_t s, const int64_t *gate = nullptr,
+                                 const PeerSumF32 *pap_sum = nullptr);
 hipError_t residual_dot_ref_f32(int64_t n, const float *b, const float *Ax, float *r, float *p, float *rr,
                                 hipStream_t s, int64_t *clear2 = nullptr);  // clear2: as residual_f64
 // The single-GPU two-launch F32_REF iteration (the same float operations as
@@ -247,9 +258,11 @@ hipError_t matvec_dot_ref_f32(const float *A, int64_t lda, int64_t rows, int64_t
 hipError_t update_xrp_dot_ref_f32(int64_t n, float *x, float *r, float *p, const float *Ap, const float *rsold,
                                   const float *pAp, float *rr, hipStream_t s, const int64_t *gate, double eps,
                                   int64_t k, int64_t *kdone, double *rrfinal, int64_t *hrec);
+// rr_sum: likewise for r.r (stored to *rr by block 0)
 hipError_t update_p_ref_f32(int64_t n, float *p, const float *r, const float *rr,
                             const float *rsold, hipStream_t s, double eps = -1.0, int64_t k = 0,
-                            int64_t *kdone = nullptr, double *rrfinal = nullptr, int64_t *hrec = nullptr);
+                            int64_t *kdone = nullptr, double *rrfinal = nullptr, int64_t *hrec = nullptr,
+                            const PeerSumF32 *rr_sum = nullptr);
 hipError_t gen_spd_f32(int64_t n, int64_t lda, int64_t row0, int64_t nrows, uint64_t seed,
                        float *A, float *b, hipStream_t s);
 // F32_REF combine: rank order (allSum) or, with mpich, MPICH's MPI_Allreduce order.

@@ -145,6 +145,9 @@ struct DotArgs {
     const float *a = nullptr, *b = nullptr;  // plain: the two vectors; resid: b, Ax
     float *x = nullptr, *r = nullptr, *p = nullptr;
     const float *Ap = nullptr, *rsold = nullptr, *pAp = nullptr;
+    // kDotXR, several row blocks in one process: p.Ap from the blocks'
+    // partials (MPICH order) instead of *pAp; cnt = 0: *pAp
+    PeerSumF32 pap_sum{};
 };
 template <int MODE, bool SC1B>
 __device__ __forceinline__ float dot_ref_body(int64_t n, const DotArgs &d, f4v (*sp)[kDotChunk / 4], int t) {
@@ -153,7 +156,11 @@ __device__ __forceinline__ float dot_ref_body(int64_t n, const DotArgs &d, f4v (
     constexpr int U = kDotChunk / 256;
     const bool act = t < 256;
     float av[U], bv[U], cv[U], dv[U];
-    const float alpha = MODE == kDotXR ? *d.rsold / *d.pAp : 0.0f;  // alpha = rsold / pAp  (:220)
+    float alpha = 0.0f;
+    if constexpr (MODE == kDotXR) {  // alpha = rsold / pAp  (:220)
+        const float pap = d.pap_sum.cnt ? peer_sum_mpich_f32(d.pap_sum) : *d.pAp;
+        alpha = *d.rsold / pap;
+    }
     auto load = [&](int64_t c0) {
         if (!act) return;
 #pragma unroll
@@ -513,20 +520,26 @@ __global__ __launch_bounds__(kNT) void k_update_xr_ref_f32(int64_t n, float *__r
 // `if (sqrt(rsnew) < EPSILON) break;` (:235-238: the float r.r widened to
 // double, as C's sqrt takes it): on convergence it records k+1 and r.r and
 // leaves p alone (the loop has ended); in a later iteration it does nothing.
+// rr_sum.cnt > 0 (several row blocks in one process): r.r from the blocks'
+// partials in MPICH order (PeerSumF32) instead of *rr, block 0 storing it.
 __global__ __launch_bounds__(kNT) void k_update_p_ref_f32(int64_t n, float *__restrict__ p,
                                                           const float *__restrict__ r,
-                                                          const float *rr, const float *rsold, ConvArgs cv) {
+                                                          const float *rr, const float *rsold, ConvArgs cv,
+                                                          PeerSumF32 rr_sum) {
 #pragma clang fp contract(off)
     if (cv.kdone) {
         const int64_t kd = *cv.kdone;
         if (kd != 0 && kd <= cv.k) return;
-        const double rrn = (double)*rr;
+    }
+    const float rrv = rr_sum.cnt ? peer_sum_mpich_f32(rr_sum) : *rr;
+    if (cv.kdone) {
+        const double rrn = (double)rrv;
         if (cv.eps >= 0.0 && sqrt(rrn) < cv.eps) {
             if (blockIdx.x == 0 && threadIdx.x == 0) record_convergence(cv, cv.k + 1, rrn);
             return;
         }
     }
-    const float ratio = *rr / *rsold;
+    const float ratio = rrv / *rsold;
     for (int64_t i = (int64_t)blockIdx.x * kNT + threadIdx.x; i < n; i += (int64_t)gridDim.x * kNT) {
         const float t = p[i] * ratio;
         p[i] = r[i] + t;
@@ -601,7 +614,8 @@ hipError_t update_xrp_dot_ref_f32(int64_t n, float *x, float *r, float *p, const
 }
 
 hipError_t update_xr_dot_ref_f32(int64_t n, float *x, float *r, const float *p, const float *Ap, const float *rsold,
-                                 const float *pAp, float *rr, hipStream_t s, const int64_t *gate) {
+                                 const float *pAp, float *rr, hipStream_t s, const int64_t *gate,
+                                 const PeerSumF32 *pap_sum) {
     DotArgs d;
     d.x = x;
     d.r = r;
@@ -609,6 +623,10 @@ hipError_t update_xr_dot_ref_f32(int64_t n, float *x, float *r, const float *p, 
     d.Ap = Ap;
     d.rsold = rsold;
     d.pAp = pAp;
+    if (pap_sum) {
+        if (pap_sum->cnt < 0 || pap_sum->cnt > kMaxPeers) return hipErrorInvalidValue;
+        d.pap_sum = *pap_sum;
+    }
     hipLaunchKernelGGL(k_dot_ref_f32_blk<kDotXR>, dim3(1), dim3(256), 0, s, n, d, rr, gate, ConvArgs{});
     return hipGetLastError();
 }
@@ -640,14 +658,20 @@ hipError_t update_xr_ref_f32(int64_t n, float *x, float *r, const float *p, cons
 }
 
 hipError_t update_p_ref_f32(int64_t n, float *p, const float *r, const float *rr, const float *rsold,
-                            hipStream_t s, double eps, int64_t k, int64_t *kdone, double *rrfinal, int64_t *hrec) {
+                            hipStream_t s, double eps, int64_t k, int64_t *kdone, double *rrfinal, int64_t *hrec,
+                            const PeerSumF32 *rr_sum) {
+    PeerSumF32 rs{};
+    if (rr_sum) {
+        if (rr_sum->cnt < 0 || rr_sum->cnt > kMaxPeers) return hipErrorInvalidValue;
+        rs = *rr_sum;
+    }
     ConvArgs cv;
     cv.eps = eps;
     cv.k = k;
     cv.kdone = kdone;
     cv.rrfinal = rrfinal;
     cv.hrec = hrec;
-    hipLaunchKernelGGL(k_update_p_ref_f32, dim3(grid_vec(n)), dim3(kNT), 0, s, n, p, r, rr, rsold, cv);
+    hipLaunchKernelGGL(k_update_p_ref_f32, dim3(grid_vec(n)), dim3(kNT), 0, s, n, p, r, rr, rsold, cv, rs);
     return hipGetLastError();
 }
 

@@ -360,6 +360,8 @@ int finish_create(cgx_ctx *c, cgx_ctx **out) {
         const char *f = std::getenv("CGX_LOCAL_FUSE");
         c->fuse_combine = c->mode == M_LOCAL && c->xchg_kernels && !(f && *f == '0') && !(c->flags & CGX_F32_REF) &&
                           !(c->flags & CGX_COMM_P2P) && (int)c->sh.size() <= kMaxPeers;
+        c->fuse_f32 = c->mode == M_LOCAL && c->xchg_kernels && !(f && *f == '0') && (c->flags & CGX_F32_REF) &&
+                      !(c->flags & CGX_COMM_P2P) && (int)c->sh.size() <= kMaxPeers && c->op == OP_DENSE;
     }
     c->rot = can_rotate(c);
     c->overlap = false;  // choose_overlap below, once the row blocks exist
@@ -694,7 +696,7 @@ int cgx_get_info(const cgx_ctx *c, cgx_info *info) {
                   (c->xdefer ? CGX_XDEFER_ACTIVE : 0) |
                   (c->xd == 3 ? CGX_XDEFER3_ACTIVE : 0) |
                   ((c->mode == M_LOCAL && c->xchg_kernels) ? CGX_PULL_ACTIVE : 0) |
-                  (c->fuse_combine ? CGX_FOLDED_ACTIVE : 0) | (c->halo_pull ? CGX_HALO_PULL_ACTIVE : 0) |
+                  ((c->fuse_combine || c->fuse_f32) ? CGX_FOLDED_ACTIVE : 0) | (c->halo_pull ? CGX_HALO_PULL_ACTIVE : 0) |
                   (c->pool ? CGX_THREADS_ACTIVE : 0) | (c->halo_overlap ? CGX_HALO_OVERLAP_ACTIVE : 0);
     info->elem_bytes = c->es;
     return CGX_OK;
