@@ -264,17 +264,32 @@ int p2p_allgather(cgx_ctx *c, bool from_x) {
     }
     TRY(local_barrier(c));
     Shard &r0 = c->sh[0];
+    const int S = (int)c->sh.size();
+    const int64_t slice = r0.nloc * (int64_t)es;
     TRY(set_dev(r0));
-    for (auto &s : c->sh) {
-        if (&s == &r0 && !from_x) continue;
-        HIPT(hipMemcpyPeerAsync(r0.pfull + s.row0 * es, r0.dev, from_x ? s.x : s.pown, s.dev, s.nloc * es, r0.stream));
+    // every slice to block 0 (gatherRow), then the whole vector from block 0 to
+    // every block (BcastVector): pull kernels on the receiving streams (one
+    // launch each instead of one peer copy per slice), or, with
+    // CGX_LOCAL_XCHG=copy, the peer copies; the same bytes either way
+    if (c->xchg_kernels) {
+        HIPT(gather_slices(peer_table(c, from_x ? &Shard::x : &Shard::pown, 0), S, from_x ? -1 : 0, slice, r0.pfull,
+                           r0.stream));
+    } else {
+        for (auto &s : c->sh) {
+            if (&s == &r0 && !from_x) continue;
+            HIPT(hipMemcpyPeerAsync(r0.pfull + s.row0 * es, r0.dev, from_x ? s.x : s.pown, s.dev, s.nloc * es,
+                                    r0.stream));
+        }
     }
     HIPT(hipEventRecord(r0.ev_root, r0.stream));
+    PeerTable whole{};  // block 0's full vector, slice by slice
+    for (int q = 0; q < S; ++q) whole.p[q] = r0.pfull + (int64_t)q * slice;
     for (auto &d : c->sh) {
         if (&d == &r0) continue;
         TRY(set_dev(d));
         HIPT(hipStreamWaitEvent(d.stream, r0.ev_root, 0));
-        HIPT(hipMemcpyPeerAsync(d.pfull, d.dev, r0.pfull, r0.dev, (size_t)c->n * es, d.stream));
+        if (c->xchg_kernels) HIPT(gather_slices(whole, S, -1, slice, d.pfull, d.stream));
+        else HIPT(hipMemcpyPeerAsync(d.pfull, d.dev, r0.pfull, r0.dev, (size_t)c->n * es, d.stream));
     }
     // Shard 0 must not touch its pfull again until every shard has copied it:
     // with from_x its very next kernels (matVec, then the residual writing p
@@ -321,20 +336,36 @@ int p2p_scalar(cgx_ctx *c, int lslot, int gslot) {
     Shard &r0 = c->sh[0];
     const int S = (int)c->sh.size();
     TRY(set_dev(r0));
-    for (auto &s : c->sh)
-        HIPT(hipMemcpyPeerAsync(slot(r0, S_GATHER + s.index), r0.dev, slot(s, lslot), s.dev, 8, r0.stream));
-    if (f32ref(c))
-        HIPT(sum_ordered_f32(reinterpret_cast<const float *>(slot(r0, S_GATHER)), S,
-                             reinterpret_cast<float *>(slot(r0, gslot)), r0.stream, false));
-    else
-        HIPT(sum_ordered_f64(reinterpret_cast<const double *>(slot(r0, S_GATHER)), S,
-                             reinterpret_cast<double *>(slot(r0, gslot)), r0.stream));
+    // block 0 pulls the partials and sums them in rank order (one kernel, the
+    // adds of sum_ordered's rank order), then every block pulls the sum (a
+    // "sum" of one value: the value); CGX_LOCAL_XCHG=copy: peer copies
+    if (c->xchg_kernels) {
+        const PeerTable src = peer_table(c, &Shard::scal, 8 * (int64_t)lslot);
+        if (f32ref(c)) HIPT(combine_peers_f32(src, S, reinterpret_cast<float *>(slot(r0, gslot)), r0.stream, false));
+        else HIPT(combine_peers_f64(src, S, reinterpret_cast<double *>(slot(r0, gslot)), r0.stream));
+    } else {
+        for (auto &s : c->sh)
+            HIPT(hipMemcpyPeerAsync(slot(r0, S_GATHER + s.index), r0.dev, slot(s, lslot), s.dev, 8, r0.stream));
+        if (f32ref(c))
+            HIPT(sum_ordered_f32(reinterpret_cast<const float *>(slot(r0, S_GATHER)), S,
+                                 reinterpret_cast<float *>(slot(r0, gslot)), r0.stream, false));
+        else
+            HIPT(sum_ordered_f64(reinterpret_cast<const double *>(slot(r0, S_GATHER)), S,
+                                 reinterpret_cast<double *>(slot(r0, gslot)), r0.stream));
+    }
     HIPT(hipEventRecord(r0.ev_root, r0.stream));
+    PeerTable root{};
+    root.p[0] = static_cast<const char *>(slot(r0, gslot));
     for (auto &d : c->sh) {
         if (&d == &r0) continue;
         TRY(set_dev(d));
         HIPT(hipStreamWaitEvent(d.stream, r0.ev_root, 0));
-        HIPT(hipMemcpyPeerAsync(slot(d, gslot), d.dev, slot(r0, gslot), r0.dev, 8, d.stream));
+        if (!c->xchg_kernels)
+            HIPT(hipMemcpyPeerAsync(slot(d, gslot), d.dev, slot(r0, gslot), r0.dev, 8, d.stream));
+        else if (f32ref(c))
+            HIPT(combine_peers_f32(root, 1, reinterpret_cast<float *>(slot(d, gslot)), d.stream, false));
+        else
+            HIPT(combine_peers_f64(root, 1, reinterpret_cast<double *>(slot(d, gslot)), d.stream));
     }
     return local_barrier(c);  // as in p2p_allgather: shard 0's slots stay put until copied
 }

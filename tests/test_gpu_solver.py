@@ -99,7 +99,7 @@ def test_f32ref_shards_bit_exact_vs_mpi_reference(key):
 
 
 @pytest.mark.parametrize("P", [2, 3, 8])
-@pytest.mark.parametrize("kind", ["f64", "f64_nooverlap", "f32ref"])
+@pytest.mark.parametrize("kind", ["f64", "f64_nooverlap", "f32ref", "p2p_f64", "p2p_f32ref"])
 def test_local_exchange_kernels_bitwise_equal_peer_copies(monkeypatch, kind, P):
     """The multi-shard exchange in one process: the pull kernels (one gather
     kernel per consuming shard; the scalar combines folded into the update
@@ -108,13 +108,16 @@ def test_local_exchange_kernels_bitwise_equal_peer_copies(monkeypatch, kind, P):
     per-pair peer copies (CGX_LOCAL_XCHG=copy): x bit for bit, the same loop
     count -- gated and fixed-count, with the overlapped gather, the plain one
     (3 shards: 2049/3 rows; CGX_NO_OVERLAP), the x0 allgather of a nonzero x0,
-    and F32_REF's MPICH-order combine (never folded)."""
+    F32_REF's MPICH-order combine (folded since round 6), and the p2p
+    pattern (CGX_COMM_P2P: through block 0, rank order) by pull kernels or
+    by copies."""
     n = 2048 if P != 3 else 2049
-    f32 = kind == "f32ref"
+    f32 = kind.endswith("f32ref")
     dt = np.float32 if f32 else np.float64
     A, b = oracle.spd_hash(n, seed=11, dtype=dt)
     x0 = np.full(n, 0.125, dt)
     flags = cg.CGX_F32_REF if f32 else cg.CGX_F64 | (cg.CGX_NO_OVERLAP if kind == "f64_nooverlap" else 0)
+    flags |= cg.CGX_COMM_P2P if kind.startswith("p2p") else 0
     res = {}
     # nofuse: a combine kernel per scalar instead of the folded sums; onethread: every block's work
     # enqueued by the calling thread instead of one thread per block (cgx_local_mt.hip)
@@ -143,7 +146,7 @@ def test_local_exchange_kernels_bitwise_equal_peer_copies(monkeypatch, kind, P):
         assert np.array_equal(r[4], c[0]), form
     xk, itk = res["kernel"][0], res["kernel"][1]
     if f32:
-        xo, so = oracle.cg_f32ref(A, b, x0, eps=1e-6, nparts=P, combine="mpich")
+        xo, so = oracle.cg_f32ref(A, b, x0, eps=1e-6, nparts=P, combine="rank" if kind.startswith("p2p") else "mpich")
         assert itk == so.iterations and np.array_equal(xk.view(np.uint32), xo.view(np.uint32))
     else:
         xo, so = oracle.cg_f64(A, b, x0, eps=1e-10)
