@@ -178,6 +178,7 @@ def lib() -> ctypes.CDLL:
         "cgx_set_x": ([vp, vp], i32),
         "cgx_solve": ([vp, vp, f64, i64, ctypes.POINTER(Stats)], i32),
         "cgx_solve_begin": ([vp], i32),
+        "cgx_conjugrad": ([vp, vp, vp, i64, i32, f64, i64, ctypes.POINTER(Stats)], i32),
         "cgx_iterate": ([vp, i64, f64, ctypes.POINTER(i64), ctypes.POINTER(i32)], i32),
         "cgx_get_stats": ([vp, ctypes.POINTER(Stats)], i32),
         "cgx_reset_timing": ([vp], i32),

@@ -235,4 +235,21 @@ int cgx_update_p(int dtype, int64_t n, void *p, const void *r, const void *rr_de
     return CGX_OK;
 }
 
+int cgx_conjugrad(const void *A, const void *b, void *x, int64_t n, int flags, double eps, int64_t max_iter,
+                  cgx_stats *st) {
+    if (!A || !b || !x) return fail(CGX_ERR_ARG, "cgx_conjugrad: A, b and x are required");
+    cgx_ctx *ctx = nullptr;
+    int rc = cgx_create(&ctx, n, 0, flags);
+    if (rc != CGX_OK) return rc;
+    rc = cgx_set_system(ctx, A, b, x);
+    if (rc == CGX_OK) rc = cgx_solve(ctx, x, eps, max_iter, st);
+    if (rc != CGX_OK) {  // keep the first failure's detail over the teardown's
+        std::string keep = g_err;
+        (void)cgx_destroy(ctx);
+        snprintf(g_err, sizeof g_err, "%s", keep.c_str());
+        return rc;
+    }
+    return cgx_destroy(ctx);
+}
+
 }  // extern "C"

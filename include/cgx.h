@@ -375,6 +375,15 @@ int cgx_set_x(cgx_ctx *ctx, const void *x);
  * in a long fixed-count run) take alpha = beta = 0 in fp64, so x stays at the
  * solution; CGX_F32_REF divides as serialConjugate.c does (0/0 = NaN). */
 int cgx_solve(cgx_ctx *ctx, void *x_inout, double eps, int64_t max_iter, cgx_stats *st);
+/* serialConjugate.c's `conjugrad(A, b, x)` (:180-259) in one call, for a
+ * literal function-level drop-in: `conjugrad(A, b, x);` becomes
+ * `cgx_conjugrad(A, b, x, ROWS, CGX_F32_REF, 1.0e-6, -1, NULL);`.  Host
+ * arrays as the reference passes them (A row-major n x n, b, x in / out;
+ * float with CGX_F32_REF -- the reference's x bit for bit -- else double),
+ * one context on device 0 created, used and destroyed inside the call; st
+ * may be NULL.  Repeated solves on one system: the context functions above. */
+int cgx_conjugrad(const void *A, const void *b, void *x, int64_t n, int flags, double eps, int64_t max_iter,
+                  cgx_stats *st);
 /* The same solve in pieces: r0 = p0 = b - A x, then `count` iterations. */
 int cgx_solve_begin(cgx_ctx *ctx);
 int cgx_iterate(cgx_ctx *ctx, int64_t count, double eps, int64_t *done, int *converged);

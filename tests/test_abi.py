@@ -374,3 +374,21 @@ def test_device_queries_without_a_gpu_fail_cleanly(built):
         cg.device_link(0, 1)
     with pytest.raises(cg.CgxError):
         cg.device_pci_bus_id(0)
+
+
+def test_conjugrad_dropin_builds_and_checks_arguments(built, tmp_path):
+    """The one-call drop-in compiles and links as a maintainer would write it;
+    without a GPU (or with a NULL array) it returns an error code instead of
+    aborting."""
+    from _native import build_conjugrad_dropin
+    exe = build_conjugrad_dropin(tmp_path)
+    assert os.path.exists(exe)
+    L = cg.lib()
+    assert L.cgx_conjugrad(None, None, None, 4, cg.CGX_F32_REF, 1e-6, -1, None) == -1  # CGX_ERR_ARG
+    if cg.device_count() == 0:
+        import numpy as np
+        A = np.eye(4, dtype=np.float32)
+        b = np.ones(4, np.float32)
+        x = np.zeros(4, np.float32)
+        assert L.cgx_conjugrad(A.ctypes.data, b.ctypes.data, x.ctypes.data, 4, cg.CGX_F32_REF, 1e-6, -1,
+                               None) == -7  # CGX_ERR_NODEV

@@ -184,3 +184,34 @@ def test_cli_gpus_equals_mpi_programs(tmp_path, program, P):
     assert f"iterations: {golden_mpi()['runs'][key]['ref_iterations']} converged: 1" in out
     x = printed_x(out, n, np.float32)
     assert np.array_equal(x.view(np.uint32), mpi_golden_x(key).view(np.uint32))
+
+
+@pytest.mark.parametrize("name,files", [
+    ("kat2", ("matrixA.txt", "vectorb.txt", "initialguess.txt")),
+    ("kat4", ("matrixA1.txt", "vectorb1.txt", "X0.txt")),
+])
+def test_conjugrad_dropin_program(golden, tmp_path, name, files):
+    """The function-level drop-in: the reference's serial
+    main with `conjugrad(A, b, x)` replaced by one cgx_conjugrad call gives
+    serialConjugate.c's x bit for bit and its loop count."""
+    from _native import build_conjugrad_dropin
+    exe = build_conjugrad_dropin(tmp_path)
+    n = golden["cases"][name]["n"]
+    r = subprocess.run([exe, str(n), *[os.path.join(FIX, f) for f in files]], capture_output=True, text=True,
+                       timeout=120, env=ONE_GPU)
+    assert r.returncode == 0, r.stdout + r.stderr
+    assert f"iterations: {golden['cases'][name]['ref_iterations']} converged: 1" in r.stdout
+    x = printed_x(r.stdout, n, np.float32)
+    assert np.array_equal(x.view(np.uint32), golden_x(golden, name).view(np.uint32))
+
+
+def test_conjugrad_dropin_generated_spd512(golden, tmp_path):
+    """The same program on generateSPDmatrix(512) written as the MATLAB script
+    writes it."""
+    from _native import build_conjugrad_dropin
+    exe = build_conjugrad_dropin(tmp_path)
+    n, paths = _spd512_files(tmp_path)
+    r = subprocess.run([exe, str(n), *paths], capture_output=True, text=True, timeout=120, env=ONE_GPU)
+    assert r.returncode == 0, r.stdout + r.stderr
+    x = printed_x(r.stdout, n, np.float32)
+    assert np.array_equal(x.view(np.uint32), golden_x(golden, "spd512").view(np.uint32))
