@@ -57,6 +57,31 @@ def test_f64_parity(golden, name):
     assert rel(golden_x(golden, name), x) <= 1e-5
 
 
+@pytest.mark.parametrize("name", ["kat4", "spd512"])
+def test_cgx_conjugrad_one_call_f64(golden, name):
+    """cgx_conjugrad (the one-call drop-in, include/cgx.h) with CGX_F64 double
+    arrays: x in place, bitwise equal to the context path's x, its stats filled;
+    a size that does not fit a context fails with the create's error and leaves x."""
+    import ctypes
+    A, b, x0 = case(name, np.float64)
+    x_ctx = x0.copy()
+    st_ctx = cg.conjugrad(A, b, x_ctx, eps=1e-10)
+    x = x0.copy()
+    st = cg.Stats()
+    L = cg.lib()
+    A_c, b_c = np.ascontiguousarray(A), np.ascontiguousarray(b)
+    rc = L.cgx_conjugrad(A_c.ctypes.data, b_c.ctypes.data, x.ctypes.data, A.shape[0], cg.CGX_F64, 1e-10, -1,
+                         ctypes.byref(st))
+    assert rc == 0, L.cgx_last_error().decode()
+    assert np.array_equal(x.view(np.uint64), x_ctx.view(np.uint64))
+    assert st.iterations == st_ctx.iterations == golden["cases"][name]["conjgrad_m_f64_iterations"]
+    assert st.converged == 1
+    x_bad = x0.copy()
+    assert L.cgx_conjugrad(A_c.ctypes.data, b_c.ctypes.data, x_bad.ctypes.data, 0, cg.CGX_F64, 1e-10, -1,
+                           None) != 0
+    assert np.array_equal(x_bad, x0)
+
+
 def test_known_answers():
     A, b, x0 = case("kat2", np.float64)
     x = x0.copy()
