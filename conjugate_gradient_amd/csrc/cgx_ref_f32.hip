@@ -219,38 +219,38 @@ __device__ __forceinline__ float dot_ref_body(int64_t n, const DotArgs &d, f4v (
         const int buf = (int)(ch & 1);
         if (ch + 1 < nch) load((ch + 1) * kDotChunk);
         if (t < 64) {  // wave 0: sum += v1[i] * v2[i], i ascending (:152)
+            // two register sets of G quads: one read from LDS while the other
+            // is added (G = 16: 2.9-3.3 ns per dependent add against 3.2-3.6
+            // at G = 8, tools/microbench/add_chain.hip).  A short last chunk
+            // runs the same loop up to the next 2G quads: store() wrote +0.0f
+            // past n, and s + 0.0f == s exactly (s starts at +0 and a
+            // round-to-nearest sum never makes -0 from it), so at most 127
+            // no-op adds replace a one-element-per-step LDS loop.
+            constexpr int G = 16;
             const int64_t left = n - ch * kDotChunk;
-            if (left >= kDotChunk) {
-                // two register sets of G quads: one read from LDS while the
-                // other is added (G = 16: 2.9-3.3 ns per dependent add
-                // against 3.2-3.6 at G = 8, tools/microbench/add_chain.hip)
-                constexpr int G = 16;
-                f4 q[G], qn[G];
-                auto add = [&](const f4 (&w)[G]) {
+            const int nq = left >= kDotChunk ? kDotChunk / 4 : (int)((left + 8 * G - 1) / (8 * G)) * (2 * G);
+            f4 q[G], qn[G];
+            auto add = [&](const f4 (&w)[G]) {
 #pragma unroll
-                    for (int u = 0; u < G; ++u) {
-                        s = s + w[u].x;
-                        s = s + w[u].y;
-                        s = s + w[u].z;
-                        s = s + w[u].w;
-                    }
-                };
-#pragma unroll
-                for (int u = 0; u < G; ++u) q[u] = sp[buf][u];
-#pragma unroll 1
-                for (int j = 0; j < kDotChunk / 4; j += 2 * G) {
-#pragma unroll
-                    for (int u = 0; u < G; ++u) qn[u] = sp[buf][j + G + u];
-                    add(q);
-                    if (j + 2 * G < kDotChunk / 4) {
-#pragma unroll
-                        for (int u = 0; u < G; ++u) q[u] = sp[buf][j + 2 * G + u];
-                    }
-                    add(qn);
+                for (int u = 0; u < G; ++u) {
+                    s = s + w[u].x;
+                    s = s + w[u].y;
+                    s = s + w[u].z;
+                    s = s + w[u].w;
                 }
-            } else {
-                const float *spf = reinterpret_cast<const float *>(sp[buf]);
-                for (int i = 0; i < (int)left; ++i) s = s + spf[i];
+            };
+#pragma unroll
+            for (int u = 0; u < G; ++u) q[u] = sp[buf][u];
+#pragma unroll 1
+            for (int j = 0; j < nq; j += 2 * G) {
+#pragma unroll
+                for (int u = 0; u < G; ++u) qn[u] = sp[buf][j + G + u];
+                add(q);
+                if (j + 2 * G < nq) {
+#pragma unroll
+                    for (int u = 0; u < G; ++u) q[u] = sp[buf][j + 2 * G + u];
+                }
+                add(qn);
             }
         }
         if (ch + 1 < nch) store(buf ^ 1, (ch + 1) * kDotChunk);
