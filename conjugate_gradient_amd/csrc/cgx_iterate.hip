@@ -192,13 +192,17 @@ int do_begin(cgx_ctx *c) {
     TRY(settle_halo(c));
     bool zero = false;  // CGX_F32_REF always does the matVec: no need to ask (in rank mode: a collective)
     if (!f32ref(c)) TRY(x0_is_zero(c, &zero));
-    if (!zero) TRY(exchange_allgather(c, /*from_x=*/true));  // full x0 into pfull
+    // One GPU, CGX_F32_REF in HBM: the matVec reads x0 where it lies (its
+    // vector loads stop at n, where pfull would be zero-padded), so x0 is not
+    // copied into pfull first -- one copy fewer per solve.
+    const bool x_direct = f32ref(c) && c->mode == M_SINGLE && !(c->flags & CGX_HOST_STREAM);
+    if (!zero && !x_direct) TRY(exchange_allgather(c, /*from_x=*/true));  // full x0 into pfull
     const int gs = S_RR + ring(0), ls = S_LRR + ring(0);
     const int os = out_slot(c, ls, gs);
     for (auto &s : c->sh) {
         TRY(set_dev(s));
         if (!zero)
-            TRY(launch_matvec(c, s, s.pfull, false, 0));
+            TRY(launch_matvec(c, s, x_direct ? s.x : s.pfull, false, 0));
         s.x_zero = false;  // the iterations update x
         if (f32ref(c)) {
             HIPT(residual_dot_ref_f32(s.nloc, reinterpret_cast<const float *>(s.b),

@@ -149,8 +149,12 @@ struct DotArgs {
     // partials (MPICH order) instead of *pAp; cnt = 0: *pAp
     PeerSumF32 pap_sum{};
 };
-template <int MODE, bool SC1B>
-__device__ __forceinline__ float dot_ref_body(int64_t n, const DotArgs &d, f4v (*sp)[kDotChunk / 4], int t) {
+// ONE: n <= kDotChunk (one chunk, no next-chunk registers live during the
+// chain); then keep_p / keep_r (kDotXR) hold this thread's p and new r values
+// for the caller's p update (element u*256 + t in [u]).
+template <int MODE, bool SC1B, bool ONE = false>
+__device__ __forceinline__ float dot_ref_body(int64_t n, const DotArgs &d, f4v (*sp)[kDotChunk / 4], int t,
+                                              float *keep_p = nullptr, float *keep_r = nullptr) {
 #pragma clang fp contract(off)
     typedef f4v f4;
     constexpr int U = kDotChunk / 256;
@@ -197,6 +201,10 @@ __device__ __forceinline__ float dot_ref_body(int64_t n, const DotArgs &d, f4v (
                     d.x[i] = xn;
                     d.r[i] = rn;
                 }
+                if (ONE && keep_p) {
+                    keep_p[u] = bv[u];
+                    keep_r[u] = rn;
+                }
                 spf[u * 256 + t] = i < n ? rn * rn : 0.0f;
             } else {
                 const float rn = av[u] - bv[u];  // r = b - Ax; p = b - Ax  (:210-211)
@@ -208,7 +216,7 @@ __device__ __forceinline__ float dot_ref_body(int64_t n, const DotArgs &d, f4v (
             }
         }
     };
-    const int64_t nch = (n + kDotChunk - 1) / kDotChunk;
+    const int64_t nch = ONE ? (n > 0 ? 1 : 0) : (n + kDotChunk - 1) / kDotChunk;
     float s = 0.0f;  // sum = 0.0  (:149)
     if (nch > 0) {
         load(0);
@@ -217,7 +225,7 @@ __device__ __forceinline__ float dot_ref_body(int64_t n, const DotArgs &d, f4v (
     }
     for (int64_t ch = 0; ch < nch; ++ch) {
         const int buf = (int)(ch & 1);
-        if (ch + 1 < nch) load((ch + 1) * kDotChunk);
+        if (!ONE && ch + 1 < nch) load((ch + 1) * kDotChunk);
         if (t < 64) {  // wave 0: sum += v1[i] * v2[i], i ascending (:152)
             // two register sets of G quads: one read from LDS while the other
             // is added (G = 16: 2.9-3.3 ns per dependent add against 3.2-3.6
@@ -253,7 +261,7 @@ __device__ __forceinline__ float dot_ref_body(int64_t n, const DotArgs &d, f4v (
                 add(qn);
             }
         }
-        if (ch + 1 < nch) store(buf ^ 1, (ch + 1) * kDotChunk);
+        if (!ONE && ch + 1 < nch) store(buf ^ 1, (ch + 1) * kDotChunk);
         __syncthreads();
     }
     return s;
@@ -450,7 +458,12 @@ __global__ __launch_bounds__(256) void k_dot_ref_f32_blk(int64_t n, DotArgs d, f
             *cv.rrfinal = 0.0;
         }
     }
-    const float s = dot_ref_body<MODE == kDotXRP ? (int)kDotXR : MODE, false>(n, d, sp, t);
+    constexpr int U = 16;  // every load of a step issued before its stores: one round trip per 4096
+    static_assert(U * 256 == kDotChunk, "one chunk of the body is one step of the p update");
+    float kp[U], kr[U];  // n <= kDotChunk: p and the new r of this thread's elements, kept from the body
+    constexpr int BODY = MODE == kDotXRP ? (int)kDotXR : MODE;
+    const bool keep = MODE == kDotXRP && n <= kDotChunk;
+    const float s = keep ? dot_ref_body<BODY, false, true>(n, d, sp, t, kp, kr) : dot_ref_body<BODY, false>(n, d, sp, t);
     if (t == 0) *out = s;
     if constexpr (MODE == kDotXRP) {
         // The single-GPU two-launch iteration's update: this block also makes
@@ -467,7 +480,15 @@ __global__ __launch_bounds__(256) void k_dot_ref_f32_blk(int64_t n, DotArgs d, f
             return;
         }
         const float ratio = rr / *d.rsold;
-        constexpr int U = 16;  // every load of a step issued before its stores: one round trip per 4096
+        if (keep) {  // one chunk: no reload of p and r
+#pragma unroll
+            for (int u = 0; u < U; ++u) {
+                const int64_t i = u * 256 + t;
+                const float tp = kp[u] * ratio;
+                if (i < n) d.p[i] = kr[u] + tp;
+            }
+            return;
+        }
         for (int64_t c0 = 0; c0 < n; c0 += 256 * U) {
             float pv[U], rv[U];
 #pragma unroll
