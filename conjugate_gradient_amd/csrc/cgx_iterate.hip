@@ -665,8 +665,13 @@ int cgx_solve_begin(cgx_ctx *c) {
 // event-ordered), so at most `look` no-op iterations are ever enqueued.
 static int iterate_gated(cgx_ctx *c, int64_t count, double eps, int64_t *done, int *converged) {
     Shard &s0 = c->sh[0];
+    // One GPU: one iteration ahead keeps the device fed (its iteration takes
+    // longer than the host's enqueue) and enqueues one no-op iteration fewer
+    // after the stop; several row blocks: two (the host's enqueue is the
+    // longer one at 8 blocks).  profiles/r06_lookahead_ab.jsonl
     const char *la = std::getenv("CGX_LOOKAHEAD");
-    const int look = std::max(1, std::min(kLookRing - 1, (la && *la) ? std::atoi(la) : 2));
+    const int look_def = c->mode == M_SINGLE ? 1 : 2;
+    const int look = std::max(1, std::min(kLookRing - 1, (la && *la) ? std::atoi(la) : look_def));
     const int64_t k0 = c->k;
     int64_t issued = 0, kd = 0;
     volatile int64_t *rec = s0.h_rec;  // {kdone, r.r bits}, stored by the deciding kernel
