@@ -432,6 +432,8 @@ int poisson_x_finish(cgx_ctx *c);
 int settle_rr(cgx_ctx *c);
 int check_x_complete(const cgx_ctx *c);
 int do_iteration(cgx_ctx *c, double eps, int *stop, bool gated = false);
+bool warm_eligible(const cgx_ctx *c);
+int warm_solve_kernels(cgx_ctx *c);
 // cgx_api.hip
 int dev_ws(RedWs *out);
 int check_dtype(int dtype);

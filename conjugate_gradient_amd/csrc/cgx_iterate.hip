@@ -648,6 +648,52 @@ int do_iteration(cgx_ctx *c, double eps, int *stop, bool gated) {
     return CGX_OK;
 }
 
+// The first launch of each kernel in a process costs the HIP runtime several
+// microseconds more than later launches (rocprofv3 --hip-trace of a fresh
+// process's first solve: 9-14 us against 6-7 us per hipLaunchKernel), about
+// 20 us over a small system's first solve -- the only solve `cg_hip` runs.
+// One GPU, small n: the context pays it at creation.  The solve's start runs
+// for real on alloc_shard's zeroed x and b (A x with x = 0, whatever A holds:
+// only r, p, Ap and the scalar slots are written), then two gated iterations
+// whose kernels all return at once (the record holds -1: converged before
+// any iteration, under both gate tests) and one record of each lookahead
+// event; the written buffers and the host
+// state then go back to what alloc_shard left.  CGX_WARM=0: no warm-up.
+constexpr int64_t kWarmMaxN = 16384;
+bool warm_eligible(const cgx_ctx *c) {
+    if (c->mode != M_SINGLE || c->op != OP_DENSE || c->n > kWarmMaxN) return false;
+    if (c->flags & (CGX_TIMING | CGX_PHASES | CGX_HOST_STREAM | CGX_SYMMETRIC)) return false;
+    const char *e = std::getenv("CGX_WARM");
+    return !(e && *e == '0');
+}
+
+int warm_solve_kernels(cgx_ctx *c) {
+    Shard &s = c->sh[0];
+    TRY(set_dev(s));
+    TRY(do_begin(c));
+    int64_t *pin = reinterpret_cast<int64_t *>(s.h_pin);
+    pin[0] = -1;
+    HIPT(hipMemcpyAsync(slot(s, S_KDONE), pin, 8, hipMemcpyHostToDevice, s.stream));
+    int stop = 0;
+    for (int i = 0; i < 2; ++i) TRY(do_iteration(c, 0.0, &stop, /*gated=*/true));
+    for (auto &e : s.ev_look) HIPT(hipEventRecord(e, s.stream));  // the gated loop's events: first records too
+    const size_t es = (size_t)c->es;
+    HIPT(hipMemsetAsync(s.r, 0, (c->fold_p ? c->lda : s.nloc) * es, s.stream));
+    HIPT(hipMemsetAsync(s.Ap, 0, s.nloc * es, s.stream));
+    HIPT(hipMemsetAsync(s.pfull, 0, c->lda * es, s.stream));
+    if (s.p_alt) HIPT(hipMemsetAsync(s.p_alt, 0, c->lda * es, s.stream));
+    HIPT(hipMemsetAsync(s.scal, 0, kScalSlots * 8, s.stream));
+    HIPT(hipStreamSynchronize(s.stream));
+    s.x_zero = true;
+    s.h_rec[0] = s.h_rec[1] = 0;
+    c->state = ST_IDLE;
+    c->k = c->xd_k0 = c->total_iters = 0;
+    c->converged = 0;
+    c->last_rr = 0.0;
+    c->rr_unsummed = c->x_incomplete = c->x_deferred = c->xalpha_pending = c->iter_failed = false;
+    return CGX_OK;
+}
+
 }  // namespace cgxh
 
 extern "C" {

@@ -412,6 +412,10 @@ int finish_create(cgx_ctx *c, cgx_ctx **out) {
     // one enqueuing thread per row block (cgx_local_mt.hip); without it the
     // iteration is enqueued by the calling thread, the same launches
     if (local_mt_eligible(c) && local_mt_start(c) != CGX_OK) c->pool = nullptr;
+    if (warm_eligible(c)) {
+        const int rc = warm_solve_kernels(c);
+        if (rc != CGX_OK) return undo(rc);
+    }
     *out = c;
     return CGX_OK;
 }
