@@ -1148,6 +1148,25 @@ def test_ragged_sizes_and_blocks(n, P):
     assert st32.iterations == sr.iterations and np.array_equal(x32, ref)
 
 
+@pytest.mark.parametrize("n,P", [(129, 1), (4095, 1), (4097, 1), (5000, 1), (8191, 1), (9000, 2)])
+def test_f32ref_partial_dot_chunks(n, P):
+    """The sequential dots walk 4096-element chunks; a short chunk (n below
+    4096, or the last one) runs the pipelined chain over +0 padding.  Sizes
+    around and past one chunk, on one GPU and as two row blocks of 4500:
+    x and the loop count bit for bit the P-part oracle's."""
+    A, b = oracle.spd_hash(n, seed=n)
+    A32, b32 = A.astype(np.float32), b.astype(np.float32)
+    del A
+    x0 = np.zeros(n, np.float32)
+    with cg.Solver(n, flags=cg.CGX_F32_REF, devices=[0] * P if P > 1 else None) as s:
+        s.set_system(A32, b32, x0)
+        x, st = s.solve(None, eps=1e-6)
+    ref, sr = oracle.cg_f32ref(A32, b32, x0, nparts=P, combine="mpich")
+    assert st.iterations == sr.iterations and st.converged == 1
+    assert np.array_equal(x.view(np.uint32), ref.view(np.uint32))
+    assert np.float32(st.rr) == np.float32(sr.rr)
+
+
 @pytest.mark.parametrize("n,P,seed", [(777, 3, 1), (1000, 4, 2), (2304, 2, 3)])
 def test_f32ref_bit_exact_many_iterations(n, P, seed):
     """A harder system than generateSPDmatrix (eigenvalues spread over two
