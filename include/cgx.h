@@ -299,7 +299,11 @@ int cgx_device_pci_bus_id(int device, char *buf, int len);
 int cgx_device_link(int device_a, int device_b, int *link_type, int *hops, int *peer);
 
 /* ---- context lifetime ------------------------------------------------------ */
-/* One GPU (device `device`).  Replaces serialConjugate.c's single process. */
+/* One GPU (device `device`).  Replaces serialConjugate.c's single process.
+ * Dense n <= 16384 (no CGX_TIMING / CGX_PHASES / CGX_HOST_STREAM /
+ * CGX_SYMMETRIC): the solve's kernels are launched once here, as no-ops, so
+ * the first solve does not carry the runtime's first-launch cost
+ * (CGX_WARM=0: not). */
 int cgx_create(cgx_ctx **ctx, int64_t n, int device, int flags);
 
 /* One process driving `nshards` row blocks on devices[0..nshards-1] (a device
